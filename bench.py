@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X-native Accord deps path (BASELINE.json metric).
+
+One "step" = one pass of the hot path over one batch: batched PreAccept deps for every txn of
+the stream (validate/pack -> (key, txn) radix bucketing into CommandsForKey histories ->
+segments -> per-txn conflict scan + KeyDeps linearisation, count and fill), with the batch
+already resident in HBM.  Workload (BASELINE.json configs[1]): 1,048,576 key txns, 8 keys
+each, Zipf(0.99) over 100,000 keys, 50% writes, window W=256, seed 2.
+
+Multi-GPU (`torchrun --nproc-per-node N`): the keyspace is split into 8*N CommandStores by
+EvenSplit (local/ShardDistributor.java:46-157); rank r owns a contiguous block of stores and
+computes the per-store KeyDeps of every txn restricted to its keys (weak scaling: each rank gets
+a stream of the config-2 size).  KeyDeps of key-disjoint stores need no data exchange to be
+complete per store; the coordinator-side union is a later row.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+
+import numpy as np  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_bytes(n, P, kc, U, D):
+    """B = 20N + 4(N+1) + 4P + 8D + 4*sum(k_i) + 4U + 12N (keys only)."""
+    return 20 * n + 4 * (n + 1) + 4 * P + 8 * D + 4 * kc + 4 * U + 12 * n
+
+
+def fill_kernel_bytes(n, P, kc, U, D):
+    """Algorithmic bytes of ONE launch of the fill kernel (keydeps_kernel<*, true>): reads lsb
+    (8N), key_off (4(N+1)), key_ord (4P), seg_start/seg_end (8P), each raw candidate once (4D),
+    the three offset arrays (12(N+1)); writes keys (4kc), txnIds (4U), keysToTxnIds (4(kc+D))."""
+    return 8 * n + 4 * (n + 1) + 4 * P + 8 * P + 4 * D + 12 * (n + 1) + 4 * kc + 4 * U + 4 * (kc + D)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--keys-per-txn", type=int, default=8)
+    ap.add_argument("--keyspace", type=int, default=100_000)
+    ap.add_argument("--zipf", type=float, default=0.99)
+    ap.add_argument("--window", type=int, default=256)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=24_000, help="txns of the CPU-baseline prefix sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+
+    from accord_amd import CommandStore, generate_stream
+
+    # ---- workload: every rank generates the config-2 stream with its own seed (weak scaling)
+    s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, 0.5, seed=args.seed + rank)
+    stores_total = 8 * world
+    # EvenSplit over [0, keyspace): store b owns [b*ks/S, (b+1)*ks/S); rank owns stores
+    # [8*rank, 8*rank+8) -> one contiguous key block per rank.
+    key_lo = (8 * rank) * args.keyspace // stores_total
+    key_hi = (8 * rank + 8) * args.keyspace // stores_total
+    if world > 1:
+        s = restrict_to_keys(s, key_lo, key_hi)
+
+    store = CommandStore(device=0 if world == 1 else local_rank, key_lo=key_lo, key_hi=key_hi,
+                         window=args.window, profile=True)
+    store.upload(s)
+
+    def step():
+        store.compute()
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    barrier()
+    hip.hipDeviceSynchronize()
+    t0 = time.perf_counter()
+    stage = {"validate": 0.0, "sort": 0.0, "segment": 0.0, "count": 0.0, "scan": 0.0, "fill": 0.0, "total": 0.0}
+    for _ in range(args.steps):
+        step()
+        t = store.timing()
+        stage["validate"] += t.validate_ms
+        stage["sort"] += t.sort_ms
+        stage["segment"] += t.segment_ms
+        stage["count"] += t.count_ms
+        stage["scan"] += t.scan_ms
+        stage["fill"] += t.fill_ms
+        stage["total"] += t.total_ms
+    hip.hipDeviceSynchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    for k in stage:
+        stage[k] /= max(1, args.steps)
+
+    # sizes for the byte model (from the device view totals of the last step)
+    view = store.device_view()
+    n = s.n
+    P = s.pairs
+    kc = int(view["kd_keys_total"])
+    U = int(view["kd_vals_total"])
+    D = int(view["kd_k2v_total"]) - kc
+
+    if rank != 0:
+        store.close()
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    txns_total = args.n * world * args.steps
+    value = txns_total / elapsed
+    B = algorithmic_bytes(n, P, kc, U, D)
+    Bf = fill_kernel_bytes(n, P, kc, U, D)
+    fill_gbs = Bf / (stage["fill"] * 1e-3) / 1e9 if stage["fill"] > 0 else None
+    pipe_gbs = B / (stage["total"] * 1e-3) / 1e9 if stage["total"] > 0 else None
+
+    cpu = None
+    if not args.no_cpu:
+        cpu = cpu_baseline(s if world == 1 else None, args)
+
+    line = {
+        "metric": "PreAccept deps/sec (batched txns)",
+        "value": value,
+        "unit": "txns/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32/u64 integer",
+        "data": "synthetic (SURVEY.md §8d stream, splitmix64 + Zipf rejection-inversion)",
+        "config": {"workload": "config2: 1M key txns x 8 keys, Zipf(0.99) over 100k keys, 50% writes, W=256",
+                   "n_txns_per_gpu": args.n, "keys_per_txn": args.keys_per_txn, "keyspace": args.keyspace,
+                   "zipf": args.zipf, "window": args.window, "seed": args.seed,
+                   "stores": stores_total, "parallelism": f"keyspace-sharded x{world}"},
+        "deps_per_s": D * world * args.steps / elapsed,
+        "sizes": {"N": n, "P": P, "keys_out": kc, "U": U, "D": D},
+        "stage_ms": stage,
+        "roofline": {"kernel": "keydeps_kernel<1,true> (fill)", "bound": "hbm",
+                     "achieved": fill_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None, "traffic": None,
+                     "algorithmic_bytes_per_launch": Bf},
+        "pipeline_roofline": {"bytes": B, "achieved": pipe_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                              "frac": (pipe_gbs / PEAK_HBM_GBS) if pipe_gbs else None,
+                              "formula": "SURVEY.md §8d B / device time of the whole pipeline"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+    store.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def restrict_to_keys(s, lo, hi):
+    """Slice every txn's keys to the store block [lo, hi) (CommandStores.mapReduce fan-out,
+    local/CommandStores.java:575-592); txns with no key in the block keep an empty key set."""
+    from accord_amd import Stream
+    keep = (s.key_ord >= lo) & (s.key_ord < hi)
+    counts = np.add.reduceat(keep.astype(np.uint32), s.key_off[:-1].astype(np.int64)) if s.pairs else np.zeros(s.n, np.uint32)
+    empty = s.key_off[1:] == s.key_off[:-1]
+    counts = np.where(empty, 0, counts).astype(np.uint32)
+    key_off = np.zeros(s.n + 1, np.uint32)
+    np.cumsum(counts, out=key_off[1:])
+    return Stream(s.msb, s.lsb, s.node, key_off, s.key_ord[keep].copy(), s.rng_off, s.rng_start, s.rng_end)
+
+
+def cpu_baseline(s, args):
+    """The oracle's literal restatement of the reference algorithm (sorted-array CommandsForKey
+    copied/re-sorted on every status change, linear mapReduceActive scan, RelationMultiMap
+    builder) on the first --cpu-sample txns of the same stream, 1 thread."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        from accord_amd import generate_stream
+        if s is None:
+            s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, 0.5, seed=args.seed)
+        m = min(args.cpu_sample, s.n)
+        t0 = time.perf_counter()
+        oracle_lib.deps_literal(s, args.window, limit=m)
+        dt = time.perf_counter() - t0
+        return {"value": m / dt, "unit": "txns/s", "cores": 1, "kind": "port",
+                "sample": f"first {m} txns of the config-2 stream (literal reference algorithm, "
+                          f"{dt:.1f} s; CFK history grows with the prefix so the full 1M run would be slower)"}
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "unit": "txns/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
+
+
+if __name__ == "__main__":
+    main()

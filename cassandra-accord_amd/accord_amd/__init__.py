@@ -1,0 +1,440 @@
+"""Host-side mirror of the Accord deps path over the C ABI of libaccord_deps.so.
+
+This package mirrors the reference's operator surface for the dependency-calculation path
+(accord-core, see include/accord_deps.h for file:line citations):
+
+  * :class:`CommandStore` ~ ``accord.local.CommandStore`` / ``SafeCommandStore`` with the new
+    batched entry ``calculate_deps_batch`` (PreAccept.calculatePartialDeps for a whole stream).
+  * :class:`PartialDeps` ~ per-txn ``KeyDeps``/``RangeDeps`` in their exact serialised layout
+    (``KeyDeps.SerializerSupport.create(keys, txnIds, keysToTxnIds)``).
+  * :func:`txn_id_str`, :func:`keydeps_str` ~ ``TxnId.toString`` / ``KeyDeps.toString``.
+
+Errors map to :class:`IllegalStateException` / :class:`IllegalArgumentException` like the
+reference's ``Invariants`` (utils/Invariants.java:43-60).  There is no CPU fallback: compute
+calls fail loudly when the HIP library or a device is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+__all__ = [
+    "AccordError", "IllegalStateException", "IllegalArgumentException", "lib", "lib_path",
+    "Stream", "generate_stream", "CommandStore", "PartialDeps", "Timing",
+    "txn_id_str", "keydeps_str", "rangedeps_str", "EXPORTED_SYMBOLS",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG_ROOT = os.path.dirname(_HERE)
+lib_path = os.path.join(_PKG_ROOT, "libaccord_deps.so")
+
+ACCORD_OK = 0
+ERR = {
+    -1: "ARG", -2: "UNSORTED", -3: "KIND", -4: "KEYS", -5: "DOMAIN", -6: "RANGES",
+    -7: "CAPACITY", -8: "HIP", -9: "OOM", -10: "STATE",
+}
+STORE_PROFILE = 1
+
+EXPORTED_SYMBOLS = [
+    "accord_store_create", "accord_store_destroy", "accord_last_error", "accord_store_stream",
+    "accord_deps_batch", "accord_deps_release", "accord_batch_upload", "accord_deps_compute",
+    "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
+    "accord_workload_generate", "accord_workload_free",
+]
+
+
+class AccordError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{ERR.get(code, code)}] {msg}")
+        self.code = code
+
+
+class IllegalStateException(AccordError):
+    pass
+
+
+class IllegalArgumentException(AccordError):
+    pass
+
+
+def _raise(code: int, msg: str):
+    if code in (-1, -2, -3, -4, -5, -6):
+        raise IllegalArgumentException(code, msg)
+    raise IllegalStateException(code, msg)
+
+
+# ---------------------------------------------------------------- ctypes structures
+_u32p = C.POINTER(C.c_uint32)
+_i32p = C.POINTER(C.c_int32)
+_u64p = C.POINTER(C.c_uint64)
+
+
+class _StoreCfg(C.Structure):
+    _fields_ = [("device", C.c_int32), ("key_lo", C.c_uint32), ("key_hi", C.c_uint32),
+                ("window", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class _Batch(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("msb", _u64p), ("lsb", _u64p), ("node", _i32p),
+                ("key_off", _u32p), ("key_ord", _u32p), ("rng_off", _u32p),
+                ("rng_start", _u32p), ("rng_end", _u32p)]
+
+
+class _Deps(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32),
+                ("kd_keys_total", C.c_uint64), ("kd_vals_total", C.c_uint64), ("kd_k2v_total", C.c_uint64),
+                ("rd_rngs_total", C.c_uint64), ("rd_vals_total", C.c_uint64), ("rd_r2v_total", C.c_uint64),
+                ("kd_key_off", _u32p), ("kd_keys", _u32p), ("kd_val_off", _u32p), ("kd_vals", _u32p),
+                ("kd_k2v_off", _u32p), ("kd_k2v", _i32p),
+                ("rd_rng_off", _u32p), ("rd_rng_start", _u32p), ("rd_rng_end", _u32p),
+                ("rd_val_off", _u32p), ("rd_vals", _u32p), ("rd_r2v_off", _u32p), ("rd_r2v", _i32p),
+                ("owner", C.c_void_p)]
+
+
+class _Timing(C.Structure):
+    _fields_ = [("validate_ms", C.c_float), ("sort_ms", C.c_float), ("segment_ms", C.c_float),
+                ("count_ms", C.c_float), ("scan_ms", C.c_float), ("fill_ms", C.c_float),
+                ("range_ms", C.c_float), ("total_ms", C.c_float),
+                ("pairs", C.c_uint64), ("hist_entries", C.c_uint64)]
+
+
+class _WorkloadCfg(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("keys_per_txn", C.c_uint32), ("keyspace", C.c_uint32),
+                ("ranges_max", C.c_uint32), ("zipf_s", C.c_double), ("write_frac", C.c_double),
+                ("range_frac", C.c_double), ("range_len_max", C.c_uint32), ("node_mod", C.c_uint32),
+                ("seed", C.c_uint64)]
+
+
+_LIB: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree HIP library; raise loudly if it is missing (no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(lib_path):
+            raise ImportError(f"libaccord_deps.so not built at {lib_path}: run __graft_entry__.build()")
+        L = C.CDLL(lib_path)
+        L.accord_store_create.argtypes = [C.POINTER(_StoreCfg), C.POINTER(C.c_void_p)]
+        L.accord_store_destroy.argtypes = [C.c_void_p]
+        L.accord_last_error.argtypes = [C.c_void_p]
+        L.accord_last_error.restype = C.c_char_p
+        L.accord_store_stream.argtypes = [C.c_void_p]
+        L.accord_store_stream.restype = C.c_void_p
+        L.accord_deps_batch.argtypes = [C.c_void_p, C.POINTER(_Batch), C.POINTER(_Deps)]
+        L.accord_deps_release.argtypes = [C.POINTER(_Deps)]
+        L.accord_deps_release.restype = None
+        L.accord_batch_upload.argtypes = [C.c_void_p, C.POINTER(_Batch)]
+        L.accord_deps_compute.argtypes = [C.c_void_p]
+        L.accord_deps_device_view.argtypes = [C.c_void_p, C.POINTER(_Deps)]
+        L.accord_deps_download.argtypes = [C.c_void_p, C.POINTER(_Deps)]
+        L.accord_store_timing.argtypes = [C.c_void_p, C.POINTER(_Timing)]
+        L.accord_workload_generate.argtypes = [C.POINTER(_WorkloadCfg), C.POINTER(_Batch)]
+        L.accord_workload_free.argtypes = [C.POINTER(_Batch)]
+        L.accord_workload_free.restype = None
+        for name in EXPORTED_SYMBOLS:
+            f = getattr(L, name)
+            if f.restype is C.c_int:  # default
+                f.restype = C.c_int32
+        _LIB = L
+    return _LIB
+
+
+# ---------------------------------------------------------------- streams
+@dataclass
+class Stream:
+    """A batch of transactions in TxnId order (SoA), plus the model window."""
+    msb: np.ndarray
+    lsb: np.ndarray
+    node: np.ndarray
+    key_off: np.ndarray
+    key_ord: np.ndarray
+    rng_off: np.ndarray
+    rng_start: np.ndarray
+    rng_end: np.ndarray
+
+    @property
+    def n(self) -> int:
+        return int(self.msb.shape[0])
+
+    @property
+    def pairs(self) -> int:
+        return int(self.key_off[-1])
+
+    def kinds(self) -> np.ndarray:
+        return ((self.lsb >> np.uint64(1)) & np.uint64(7)).astype(np.uint8)
+
+    def domains(self) -> np.ndarray:
+        return (self.lsb & np.uint64(1)).astype(np.uint8)
+
+    def prefix(self, m: int) -> "Stream":
+        m = min(m, self.n)
+        k1 = int(self.key_off[m])
+        r1 = int(self.rng_off[m])
+        return Stream(self.msb[:m].copy(), self.lsb[:m].copy(), self.node[:m].copy(),
+                      self.key_off[:m + 1].copy(), self.key_ord[:k1].copy(), self.rng_off[:m + 1].copy(),
+                      self.rng_start[:r1].copy(), self.rng_end[:r1].copy())
+
+    def c_batch(self) -> _Batch:
+        self._keep = [np.ascontiguousarray(a) for a in (self.msb, self.lsb, self.node, self.key_off, self.key_ord,
+                                                        self.rng_off, self.rng_start, self.rng_end)]
+        msb, lsb, node, ko, kord, ro, rs, re = self._keep
+        b = _Batch()
+        b.n = self.n
+        b.msb = msb.ctypes.data_as(_u64p)
+        b.lsb = lsb.ctypes.data_as(_u64p)
+        b.node = node.ctypes.data_as(_i32p)
+        b.key_off = ko.ctypes.data_as(_u32p)
+        b.key_ord = kord.ctypes.data_as(_u32p)
+        has_ranges = ro.shape[0] > 0 and int(ro[-1]) > 0
+        b.rng_off = ro.ctypes.data_as(_u32p) if has_ranges else None
+        b.rng_start = rs.ctypes.data_as(_u32p) if has_ranges else None
+        b.rng_end = re.ctypes.data_as(_u32p) if has_ranges else None
+        return b
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+
+def generate_stream(n: int, keys_per_txn: int = 4, keyspace: int = 100_000, zipf_s: float = 0.0,
+                    write_frac: float = 0.5, range_frac: float = 0.0, ranges_max: int = 2,
+                    range_len_max: int = 1000, node_mod: int = 7, seed: int = 1) -> Stream:
+    """SURVEY.md §8d synthetic stream (generated by the library's host code)."""
+    cfg = _WorkloadCfg(n, keys_per_txn, keyspace, ranges_max, zipf_s, write_frac, range_frac,
+                       range_len_max, node_mod, seed)
+    b = _Batch()
+    rc = lib().accord_workload_generate(C.byref(cfg), C.byref(b))
+    if rc != ACCORD_OK:
+        _raise(rc, lib().accord_last_error(None).decode())
+    try:
+        P = b.key_off[n] if n else 0
+        R = b.rng_off[n] if n else 0
+        s = Stream(_arr(b.msb, n, np.uint64), _arr(b.lsb, n, np.uint64), _arr(b.node, n, np.int32),
+                   _arr(b.key_off, n + 1, np.uint32), _arr(b.key_ord, P, np.uint32),
+                   _arr(b.rng_off, n + 1, np.uint32), _arr(b.rng_start, R, np.uint32), _arr(b.rng_end, R, np.uint32))
+    finally:
+        lib().accord_workload_free(C.byref(b))
+    return s
+
+
+# ---------------------------------------------------------------- deps
+@dataclass
+class PartialDeps:
+    """Per-txn KeyDeps/RangeDeps of a batch in the exact reference layout (CSR over txns)."""
+    kd_key_off: np.ndarray
+    kd_keys: np.ndarray
+    kd_val_off: np.ndarray
+    kd_vals: np.ndarray
+    kd_k2v_off: np.ndarray
+    kd_k2v: np.ndarray
+    rd_rng_off: np.ndarray
+    rd_rng_start: np.ndarray
+    rd_rng_end: np.ndarray
+    rd_val_off: np.ndarray
+    rd_vals: np.ndarray
+    rd_r2v_off: np.ndarray
+    rd_r2v: np.ndarray
+
+    FIELDS = ("kd_key_off", "kd_keys", "kd_val_off", "kd_vals", "kd_k2v_off", "kd_k2v",
+              "rd_rng_off", "rd_rng_start", "rd_rng_end", "rd_val_off", "rd_vals", "rd_r2v_off", "rd_r2v")
+
+    @property
+    def n(self) -> int:
+        return int(self.kd_key_off.shape[0]) - 1
+
+    def key_deps(self, i: int):
+        """(keys, txnIds as stream indices, keysToTxnIds) of txn i -- KeyDeps.SerializerSupport."""
+        return (self.kd_keys[self.kd_key_off[i]:self.kd_key_off[i + 1]],
+                self.kd_vals[self.kd_val_off[i]:self.kd_val_off[i + 1]],
+                self.kd_k2v[self.kd_k2v_off[i]:self.kd_k2v_off[i + 1]])
+
+    def range_deps(self, i: int):
+        a, b = self.rd_rng_off[i], self.rd_rng_off[i + 1]
+        return (self.rd_rng_start[a:b], self.rd_rng_end[a:b],
+                self.rd_vals[self.rd_val_off[i]:self.rd_val_off[i + 1]],
+                self.rd_r2v[self.rd_r2v_off[i]:self.rd_r2v_off[i + 1]])
+
+    def totals(self):
+        return dict(keys=int(self.kd_key_off[-1]), vals=int(self.kd_val_off[-1]), k2v=int(self.kd_k2v_off[-1]),
+                    body=int(self.kd_k2v_off[-1] - self.kd_key_off[-1]), rd_vals=int(self.rd_val_off[-1]))
+
+    @staticmethod
+    def from_c(d: _Deps) -> "PartialDeps":
+        n = d.n
+        kw = {}
+        kw["kd_key_off"] = _arr(d.kd_key_off, n + 1, np.uint32)
+        kw["kd_val_off"] = _arr(d.kd_val_off, n + 1, np.uint32)
+        kw["kd_k2v_off"] = _arr(d.kd_k2v_off, n + 1, np.uint32)
+        kw["kd_keys"] = _arr(d.kd_keys, int(kw["kd_key_off"][-1]), np.uint32)
+        kw["kd_vals"] = _arr(d.kd_vals, int(kw["kd_val_off"][-1]), np.uint32)
+        kw["kd_k2v"] = _arr(d.kd_k2v, int(kw["kd_k2v_off"][-1]), np.int32)
+        kw["rd_rng_off"] = _arr(d.rd_rng_off, n + 1, np.uint32)
+        kw["rd_val_off"] = _arr(d.rd_val_off, n + 1, np.uint32)
+        kw["rd_r2v_off"] = _arr(d.rd_r2v_off, n + 1, np.uint32)
+        R = int(kw["rd_rng_off"][-1])
+        kw["rd_rng_start"] = _arr(d.rd_rng_start, R, np.uint32)
+        kw["rd_rng_end"] = _arr(d.rd_rng_end, R, np.uint32)
+        kw["rd_vals"] = _arr(d.rd_vals, int(kw["rd_val_off"][-1]), np.uint32)
+        kw["rd_r2v"] = _arr(d.rd_r2v, int(kw["rd_r2v_off"][-1]), np.int32)
+        return PartialDeps(**kw)
+
+    def equals(self, other: "PartialDeps") -> bool:
+        return all(np.array_equal(getattr(self, f), getattr(other, f)) for f in self.FIELDS)
+
+    def first_difference(self, other: "PartialDeps"):
+        for f in self.FIELDS:
+            a, b = getattr(self, f), getattr(other, f)
+            if a.shape != b.shape:
+                return f, "shape", a.shape, b.shape
+            bad = np.nonzero(a != b)[0]
+            if bad.size:
+                j = int(bad[0])
+                return f, j, a[j], b[j]
+        return None
+
+
+@dataclass
+class Timing:
+    validate_ms: float
+    sort_ms: float
+    segment_ms: float
+    count_ms: float
+    scan_ms: float
+    fill_ms: float
+    range_ms: float
+    total_ms: float
+    pairs: int
+    hist_entries: int
+
+
+class CommandStore:
+    """One CommandStore == one HIP stream on one device (impl/InMemoryCommandStore.java:89)."""
+
+    def __init__(self, device: int = 0, key_lo: int = 0, key_hi: int = 100_000, window: int = 256,
+                 profile: bool = False):
+        cfg = _StoreCfg(device, key_lo, key_hi, window, STORE_PROFILE if profile else 0, 0)
+        h = C.c_void_p()
+        rc = lib().accord_store_create(C.byref(cfg), C.byref(h))
+        if rc != ACCORD_OK:
+            _raise(rc, lib().accord_last_error(None).decode())
+        self._h = h
+        self.window = window
+        self.key_lo, self.key_hi = key_lo, key_hi
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().accord_store_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != ACCORD_OK:
+            _raise(rc, lib().accord_last_error(self._h).decode())
+
+    @property
+    def stream_handle(self) -> int:
+        return int(lib().accord_store_stream(self._h) or 0)
+
+    def calculate_deps_batch(self, s: Stream) -> PartialDeps:
+        """PreAccept.calculatePartialDeps for every txn of the batch, in TxnId order."""
+        b = s.c_batch()
+        d = _Deps()
+        self._check(lib().accord_deps_batch(self._h, C.byref(b), C.byref(d)))
+        try:
+            return PartialDeps.from_c(d)
+        finally:
+            lib().accord_deps_release(C.byref(d))
+
+    # device-resident pipeline
+    def upload(self, s: Stream):
+        b = s.c_batch()
+        self._check(lib().accord_batch_upload(self._h, C.byref(b)))
+
+    def compute(self):
+        self._check(lib().accord_deps_compute(self._h))
+
+    def download(self) -> PartialDeps:
+        d = _Deps()
+        self._check(lib().accord_deps_download(self._h, C.byref(d)))
+        try:
+            return PartialDeps.from_c(d)
+        finally:
+            lib().accord_deps_release(C.byref(d))
+
+    def device_view(self) -> dict:
+        d = _Deps()
+        self._check(lib().accord_deps_device_view(self._h, C.byref(d)))
+        out = {"n": d.n, "kd_keys_total": d.kd_keys_total, "kd_vals_total": d.kd_vals_total,
+               "kd_k2v_total": d.kd_k2v_total}
+        for f in PartialDeps.FIELDS:
+            out[f] = C.cast(getattr(d, f), C.c_void_p).value or 0
+        return out
+
+    def timing(self) -> Timing:
+        t = _Timing()
+        self._check(lib().accord_store_timing(self._h, C.byref(t)))
+        return Timing(t.validate_ms, t.sort_ms, t.segment_ms, t.count_ms, t.scan_ms, t.fill_ms, t.range_ms,
+                      t.total_ms, t.pairs, t.hist_entries)
+
+
+# ---------------------------------------------------------------- string forms
+_DOMAIN = "KR"
+_KIND = "RWESXL"
+
+
+def txn_id_str(msb: int, lsb: int, node: int) -> str:
+    """TxnId.toString (primitives/TxnId.java:118-122): [epoch,hlc,flags(DK),node]."""
+    msb, lsb = int(msb), int(lsb)
+    epoch = msb >> 15
+    hlc = ((msb & 0x7FFF) << 48) | (lsb >> 16)
+    flags = lsb & 0xFFFF
+    return f"[{epoch},{hlc},{flags}({_DOMAIN[flags & 1]}{_KIND[(flags >> 1) & 7]}),{int(node)}]"
+
+
+def keydeps_str(keys, vals, k2v, s: Stream) -> str:
+    """KeyDeps.toString -> RelationMultiMap.toSimpleString (utils/RelationMultiMap.java:963-987)."""
+    keys = list(keys)
+    if len(keys) == len(k2v):
+        return "{}"
+    out, t = [], len(keys)
+    for k, key in enumerate(keys):
+        ids = []
+        while t < k2v[k]:
+            j = int(vals[k2v[t]])
+            ids.append(txn_id_str(s.msb[j], s.lsb[j], s.node[j]))
+            t += 1
+        out.append(f"{int(key)}:[{', '.join(ids)}]")
+    return "{" + ", ".join(out) + "}"
+
+
+def rangedeps_str(starts, ends, vals, r2v, s: Stream) -> str:
+    """RangeDeps.toString with IntKey ranges printed as (s,e] (Range.java:433-440)."""
+    if len(starts) == len(r2v):
+        return "{}"
+    out, t = [], len(starts)
+    for k in range(len(starts)):
+        ids = []
+        while t < r2v[k]:
+            j = int(vals[r2v[t]])
+            ids.append(txn_id_str(s.msb[j], s.lsb[j], s.node[j]))
+            t += 1
+        out.append(f"({int(starts[k])},{int(ends[k])}]:[{', '.join(ids)}]")
+    return "{" + ", ".join(out) + "}"

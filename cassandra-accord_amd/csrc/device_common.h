@@ -1,0 +1,77 @@
+// Device helpers shared by the deps kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ACC_WAVE 64
+
+__device__ __forceinline__ uint32_t lane_id()
+{
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// Order LDS traffic between lanes of ONE wave (waves of a workgroup run different txns, so a
+// block barrier is not usable inside the per-txn loops).  LDS ops of a wave are processed in
+// order; the waitcnt + memory clobber keeps the compiler from reordering across it.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (l >= (uint32_t)d) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t t = __shfl_up(v, d, 64);
+        if (l >= (uint32_t)d) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// ---- TxnId semantics (primitives/Timestamp.java:208-217, TxnId.java:124-157, Txn.java) ----
+// Kind ordinals: Read 0, Write 1, EphemeralRead 2, SyncPoint 3, ExclusiveSyncPoint 4, LocalOnly 5
+// witnesses(): Read/EphemeralRead -> Ws, Write -> RsOrWs, SyncPoints -> AnyGloballyVisible.
+// Encoded as a bitmask over entry kinds: Ws = {W}, RsOrWs = {R,W}, AnyGV = {R,W,SP,ESP}.
+__host__ __device__ __forceinline__ uint32_t witness_mask(uint32_t kind)
+{
+    switch (kind) {
+    case 0: case 2: return 0x2u;
+    case 1: return 0x3u;
+    case 3: case 4: return 0x1Bu;
+    default: return 0u;      // LocalOnly / invalid: rejected by validation
+    }
+}
+
+__device__ __forceinline__ int ts_cmp(uint64_t am, uint64_t al, int32_t an, uint64_t bm, uint64_t bl, int32_t bn)
+{
+    if (am != bm) return am < bm ? -1 : 1;
+    uint64_t ah = al >> 16, bh = bl >> 16;
+    if (ah != bh) return ah < bh ? -1 : 1;
+    uint64_t af = al & 0x1Eull, bf = bl & 0x1Eull;
+    if (af != bf) return af < bf ? -1 : 1;
+    if (an != bn) return an < bn ? -1 : 1;
+    return 0;
+}
+
+// History entry: txn index in the low 29 bits, entry kind in the top 3 bits.
+#define ENT_TXN_MASK 0x1FFFFFFFu
+#define ENT_KIND_SHIFT 29

@@ -1,0 +1,57 @@
+// Host-side launch wrappers of the deps kernels (implemented in *.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace accord {
+
+// device error word codes (first error wins; see include/accord_deps.h)
+struct DevStatus {
+    unsigned long long first;   // (txn << 32) | -code of the lowest-index failure; ~0 = none
+    uint32_t overflow;          // txns that exceeded the per-wave capacity
+    uint32_t overflow_first;    // lowest such txn (~0 = none)
+};
+
+// ---- radix sort (radix_sort.hip) ----
+size_t radix_sort_temp_bytes(uint32_t n);
+// Stable LSD sort of (key, val) by key over `bits` low bits.  Result ends in keys_out/vals_out.
+// keys_tmp/vals_tmp are ping-pong buffers of n entries.
+void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys_out, uint32_t *vals_out,
+                      uint32_t *keys_tmp, uint32_t *vals_tmp, uint32_t n, int bits, void *temp, hipStream_t s);
+
+// ---- scan (scan.hip) ----
+size_t scan_temp_bytes(uint32_t n);
+// out[i] = sum(in[0..i)), i in [0, n]; out has n+1 entries; total also written to *total_dev (u64).
+void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, unsigned long long *total_dev, void *temp,
+                        hipStream_t s);
+
+// ---- key deps pipeline (keydeps.hip) ----
+struct KeyDepsParams {
+    uint32_t n;
+    const uint64_t *msb, *lsb;
+    const int32_t *node;
+    const uint32_t *key_off, *key_ord;
+    uint32_t key_lo, key_hi;
+    uint32_t window;
+    // history
+    const uint32_t *hist;        // sorted entries (kind<<29 | txn)
+    const uint32_t *seg_start;   // [nkeys]
+    const uint32_t *seg_end;     // [nkeys]
+    // count outputs
+    uint32_t *cnt_keys, *cnt_vals, *cnt_k2v;
+    // fill inputs/outputs
+    const uint32_t *kd_key_off, *kd_val_off, *kd_k2v_off;
+    uint32_t *kd_keys, *kd_vals;
+    int32_t *kd_k2v;
+    DevStatus *status;
+};
+
+void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
+                          const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
+                          const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
+                          uint32_t *pair_key, uint32_t *pair_val, DevStatus *status, hipStream_t s);
+void launch_segments(uint32_t P, const uint32_t *sorted_keys, uint32_t *seg_start, uint32_t *seg_end, hipStream_t s);
+void launch_keydeps_count(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
+void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
+
+} // namespace accord

@@ -1,0 +1,403 @@
+// C ABI implementation (include/accord_deps.h): one accord_store == one CommandStore == one
+// HIP stream, with a grow-only HBM arena for the batch, the per-key histories and the outputs.
+#include "../../include/accord_deps.h"
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes)
+    {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <typename T> T *as() const { return (T *)p; }
+};
+
+enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_COUNT_ALL };
+
+struct HostTotals {
+    accord::DevStatus status;
+    unsigned long long totals[3];
+};
+
+} // namespace
+
+struct accord_store {
+    accord_store_cfg cfg{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    // batch (device)
+    uint32_t n = 0, P = 0, R = 0;
+    bool has_batch = false, computed = false;
+    DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
+    // work
+    DevBuf pair_key, pair_val, sort_key, sort_val, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
+    DevBuf cnt_keys, cnt_vals, cnt_k2v, kd_key_off, kd_val_off, kd_k2v_off, scan_tmp, status_totals;
+    // outputs
+    DevBuf kd_keys, kd_vals, kd_k2v, rd_zero_off;
+    uint64_t tot_keys = 0, tot_vals = 0, tot_k2v = 0;
+    HostTotals *pinned = nullptr;
+    hipEvent_t ev[EV_COUNT_ALL] = {};
+    bool events = false;
+    accord_timing timing{};
+    int wpl = 1;
+};
+
+namespace {
+
+int32_t fail(accord_store *s, int32_t code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (s) s->err = buf;
+    g_last_error = buf;
+    return code;
+}
+
+#define HIPCHECK(s, expr)                                                                             \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) return fail((s), ACCORD_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+int bits_for(uint32_t maxval)
+{
+    int b = 0;
+    while (b < 32 && (maxval >> b) != 0) ++b;
+    return b < 1 ? 1 : b;
+}
+
+void record(accord_store *s, int stage)
+{
+    if (s->events) (void)hipEventRecord(s->ev[stage], s->stream);
+}
+
+const char *code_name(int32_t c)
+{
+    switch (c) {
+    case ACCORD_ERR_UNSORTED: return "batch TxnIds are not strictly ascending (Timestamp.compareTo)";
+    case ACCORD_ERR_KIND: return "txn kind has no witnesses() (LocalOnly or invalid ordinal)";
+    case ACCORD_ERR_KEYS: return "keys not sorted unique or outside the store's key range";
+    case ACCORD_ERR_DOMAIN: return "TxnId domain bit inconsistent with its keys/ranges";
+    case ACCORD_ERR_RANGES: return "ranges not sorted, de-overlapped and non-empty";
+    case ACCORD_ERR_ARG: return "malformed CSR offsets";
+    default: return "error";
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+int32_t accord_store_create(const accord_store_cfg *cfg, accord_store **out)
+{
+    if (!cfg || !out) return fail(nullptr, ACCORD_ERR_ARG, "accord_store_create: null argument");
+    *out = nullptr;
+    if (cfg->key_hi <= cfg->key_lo) return fail(nullptr, ACCORD_ERR_ARG, "empty key range [%u,%u)", cfg->key_lo, cfg->key_hi);
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0)
+        return fail(nullptr, ACCORD_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, ACCORD_ERR_ARG, "bad device %d", cfg->device);
+    accord_store *s = new (std::nothrow) accord_store();
+    if (!s) return fail(nullptr, ACCORD_ERR_OOM, "out of host memory");
+    s->cfg = *cfg;
+    if ((e = hipSetDevice(cfg->device)) != hipSuccess || (e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) {
+        delete s;
+        return fail(nullptr, ACCORD_ERR_HIP, "stream create: %s", hipGetErrorString(e));
+    }
+    if ((e = hipHostMalloc((void **)&s->pinned, sizeof(HostTotals), hipHostMallocDefault)) != hipSuccess) {
+        (void)hipStreamDestroy(s->stream);
+        delete s;
+        return fail(nullptr, ACCORD_ERR_HIP, "pinned alloc: %s", hipGetErrorString(e));
+    }
+    s->events = (cfg->flags & ACCORD_STORE_PROFILE) != 0;
+    if (s->events)
+        for (auto &ev : s->ev) (void)hipEventCreate(&ev);
+    uint32_t span_need = cfg->window + 2048;
+    s->wpl = span_need <= 4096 ? 1 : span_need <= 8192 ? 2 : 4;
+    *out = s;
+    return ACCORD_OK;
+}
+
+int32_t accord_store_destroy(accord_store *s)
+{
+    if (!s) return ACCORD_OK;
+    (void)hipSetDevice(s->cfg.device);
+    (void)hipStreamSynchronize(s->stream);
+    DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
+                      &s->pair_key, &s->pair_val, &s->sort_key, &s->sort_val, &s->tmp_key, &s->tmp_val,
+                      &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
+                      &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
+                      &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off};
+    for (DevBuf *b : bufs) b->release();
+    if (s->events)
+        for (auto &ev : s->ev) (void)hipEventDestroy(ev);
+    if (s->pinned) (void)hipHostFree(s->pinned);
+    (void)hipStreamDestroy(s->stream);
+    delete s;
+    return ACCORD_OK;
+}
+
+const char *accord_last_error(const accord_store *s)
+{
+    return s ? s->err.c_str() : g_last_error.c_str();
+}
+
+void *accord_store_stream(accord_store *s) { return s ? (void *)s->stream : nullptr; }
+
+int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
+{
+    if (!s || !b || !b->msb || !b->lsb || !b->node || !b->key_off || (!b->key_ord && b->n))
+        return fail(s, ACCORD_ERR_ARG, "accord_batch_upload: null argument");
+    if (b->n >= (1u << 29)) return fail(s, ACCORD_ERR_CAPACITY, "batch of %u txns exceeds 2^29", b->n);
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    const uint32_t n = b->n;
+    for (uint32_t i = 0; i < n; ++i)   // CSR sanity before anything indexes with it
+        if (b->key_off[i + 1] < b->key_off[i] || (b->rng_off && b->rng_off[i + 1] < b->rng_off[i]))
+            return fail(s, ACCORD_ERR_ARG, "CSR offsets decrease at txn %u", i);
+    if (b->key_off[0] != 0 || (b->rng_off && b->rng_off[0] != 0))
+        return fail(s, ACCORD_ERR_ARG, "CSR offsets must start at 0");
+    const uint32_t P = b->key_off[n];
+    const uint32_t R = b->rng_off ? b->rng_off[n] : 0;
+    if (R != 0)
+        return fail(s, ACCORD_ERR_STATE, "range-domain txns are not supported by this build yet (RangeDeps path)");
+    s->n = n; s->P = P; s->R = R;
+    s->has_batch = false; s->computed = false;
+    HIPCHECK(s, s->msb.ensure((size_t)n * 8));
+    HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
+    HIPCHECK(s, s->node.ensure((size_t)n * 4));
+    HIPCHECK(s, s->key_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->key_ord.ensure((size_t)P * 4));
+    HIPCHECK(s, s->rng_off.ensure(((size_t)n + 1) * 4));
+    if (n) {
+        HIPCHECK(s, hipMemcpyAsync(s->msb.p, b->msb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->lsb.p, b->lsb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->node.p, b->node, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
+    }
+    HIPCHECK(s, hipMemcpyAsync(s->key_off.p, b->key_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
+    if (P) HIPCHECK(s, hipMemcpyAsync(s->key_ord.p, b->key_ord, (size_t)P * 4, hipMemcpyHostToDevice, s->stream));
+    HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
+    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    s->has_batch = true;
+    return ACCORD_OK;
+}
+
+int32_t accord_deps_compute(accord_store *s)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (!s->has_batch) return fail(s, ACCORD_ERR_STATE, "accord_deps_compute before accord_batch_upload");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    const uint32_t n = s->n, P = s->P;
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    hipStream_t st = s->stream;
+    s->computed = false;
+
+    HIPCHECK(s, s->pair_key.ensure((size_t)P * 4));
+    HIPCHECK(s, s->pair_val.ensure((size_t)P * 4));
+    HIPCHECK(s, s->sort_key.ensure((size_t)P * 4));
+    HIPCHECK(s, s->sort_val.ensure((size_t)P * 4));
+    HIPCHECK(s, s->tmp_key.ensure((size_t)P * 4));
+    HIPCHECK(s, s->tmp_val.ensure((size_t)P * 4));
+    HIPCHECK(s, s->seg_start.ensure((size_t)nkeys * 4));
+    HIPCHECK(s, s->seg_end.ensure((size_t)nkeys * 4));
+    HIPCHECK(s, s->radix_tmp.ensure(accord::radix_sort_temp_bytes(P)));
+    HIPCHECK(s, s->cnt_keys.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->cnt_vals.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->cnt_k2v.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->kd_key_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->kd_val_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->kd_k2v_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n)));
+    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
+    HIPCHECK(s, s->rd_zero_off.ensure(((size_t)n + 1) * 4));
+
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    record(s, EV_START);
+    HIPCHECK(s, hipMemsetAsync(dev, 0xFF, sizeof(HostTotals), st));
+    HIPCHECK(s, hipMemsetAsync(&dev->status.overflow, 0, sizeof(uint32_t), st));
+    HIPCHECK(s, hipMemsetAsync(s->rd_zero_off.p, 0, ((size_t)n + 1) * 4, st));
+    accord::launch_validate_pack(n, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->node.as<int32_t>(),
+                                 s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->rng_off.as<uint32_t>(),
+                                 nullptr, nullptr, s->cfg.key_lo, s->cfg.key_hi, s->pair_key.as<uint32_t>(),
+                                 s->pair_val.as<uint32_t>(), &dev->status, st);
+    record(s, EV_VALIDATE);
+    accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), s->pair_val.as<uint32_t>(), s->sort_key.as<uint32_t>(),
+                             s->sort_val.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(), P,
+                             bits_for(nkeys - 1), s->radix_tmp.p, st);
+    record(s, EV_SORT);
+    HIPCHECK(s, hipMemsetAsync(s->seg_start.p, 0, (size_t)nkeys * 4, st));
+    HIPCHECK(s, hipMemsetAsync(s->seg_end.p, 0, (size_t)nkeys * 4, st));
+    accord::launch_segments(P, s->sort_key.as<uint32_t>(), s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(), st);
+    record(s, EV_SEGMENT);
+
+    accord::KeyDepsParams kp{};
+    kp.n = n;
+    kp.msb = s->msb.as<uint64_t>(); kp.lsb = s->lsb.as<uint64_t>(); kp.node = s->node.as<int32_t>();
+    kp.key_off = s->key_off.as<uint32_t>(); kp.key_ord = s->key_ord.as<uint32_t>();
+    kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
+    kp.hist = s->sort_val.as<uint32_t>();
+    kp.seg_start = s->seg_start.as<uint32_t>(); kp.seg_end = s->seg_end.as<uint32_t>();
+    kp.cnt_keys = s->cnt_keys.as<uint32_t>(); kp.cnt_vals = s->cnt_vals.as<uint32_t>(); kp.cnt_k2v = s->cnt_k2v.as<uint32_t>();
+    kp.status = &dev->status;
+    accord::launch_keydeps_count(kp, s->wpl, st);
+    record(s, EV_COUNT);
+    accord::exclusive_scan_u32(kp.cnt_keys, s->kd_key_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
+    accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[1], s->scan_tmp.p, st);
+    accord::exclusive_scan_u32(kp.cnt_k2v, s->kd_k2v_off.as<uint32_t>(), n, &dev->totals[2], s->scan_tmp.p, st);
+    record(s, EV_SCAN);
+    HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+
+    const HostTotals &h = *s->pinned;
+    if (h.status.first != ~0ull) {
+        const uint32_t where = (uint32_t)(h.status.first >> 32);
+        const int32_t code = -(int32_t)(uint32_t)(h.status.first & 0xFFFFFFFFu);
+        return fail(s, code, "%s (txn %u)", code_name(code), where);
+    }
+    if (h.status.overflow)
+        return fail(s, ACCORD_ERR_CAPACITY, "%u txns exceed the per-wave capacity (first: txn %u)", h.status.overflow,
+                    h.status.overflow_first);
+    for (int t = 0; t < 3; ++t)
+        if (h.totals[t] >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "deps output exceeds 2^32 entries");
+    s->tot_keys = h.totals[0]; s->tot_vals = h.totals[1]; s->tot_k2v = h.totals[2];
+    HIPCHECK(s, s->kd_keys.ensure(s->tot_keys * 4));
+    HIPCHECK(s, s->kd_vals.ensure(s->tot_vals * 4));
+    HIPCHECK(s, s->kd_k2v.ensure(s->tot_k2v * 4));
+    kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.kd_val_off = s->kd_val_off.as<uint32_t>();
+    kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
+    kp.kd_keys = s->kd_keys.as<uint32_t>(); kp.kd_vals = s->kd_vals.as<uint32_t>(); kp.kd_k2v = s->kd_k2v.as<int32_t>();
+    accord::launch_keydeps_fill(kp, s->wpl, st);
+    record(s, EV_FILL);
+    HIPCHECK(s, hipStreamSynchronize(st));
+    HIPCHECK(s, hipGetLastError());
+
+    if (s->events) {
+        auto el = [&](int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, s->ev[a], s->ev[b]); return ms; };
+        s->timing.validate_ms = el(EV_START, EV_VALIDATE);
+        s->timing.sort_ms = el(EV_VALIDATE, EV_SORT);
+        s->timing.segment_ms = el(EV_SORT, EV_SEGMENT);
+        s->timing.count_ms = el(EV_SEGMENT, EV_COUNT);
+        s->timing.scan_ms = el(EV_COUNT, EV_SCAN);
+        s->timing.fill_ms = el(EV_SCAN, EV_FILL);
+        s->timing.range_ms = 0;
+        s->timing.total_ms = el(EV_START, EV_FILL);
+    }
+    s->timing.pairs = P;
+    s->timing.hist_entries = P;
+    s->computed = true;
+    return ACCORD_OK;
+}
+
+int32_t accord_store_timing(accord_store *s, accord_timing *t)
+{
+    if (!s || !t) return fail(s, ACCORD_ERR_ARG, "null argument");
+    *t = s->timing;
+    return ACCORD_OK;
+}
+
+int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
+{
+    if (!s || !d) return fail(s, ACCORD_ERR_ARG, "null argument");
+    if (!s->computed) return fail(s, ACCORD_ERR_STATE, "no computed deps");
+    std::memset(d, 0, sizeof(*d));
+    d->n = s->n;
+    d->kd_keys_total = s->tot_keys; d->kd_vals_total = s->tot_vals; d->kd_k2v_total = s->tot_k2v;
+    d->kd_key_off = s->kd_key_off.as<uint32_t>(); d->kd_keys = s->kd_keys.as<uint32_t>();
+    d->kd_val_off = s->kd_val_off.as<uint32_t>(); d->kd_vals = s->kd_vals.as<uint32_t>();
+    d->kd_k2v_off = s->kd_k2v_off.as<uint32_t>(); d->kd_k2v = s->kd_k2v.as<int32_t>();
+    d->rd_rng_off = d->rd_val_off = d->rd_r2v_off = s->rd_zero_off.as<uint32_t>();
+    return ACCORD_OK;
+}
+
+struct HostDepsOwner {
+    std::vector<uint32_t> kd_key_off, kd_keys, kd_val_off, kd_vals, kd_k2v_off;
+    std::vector<int32_t> kd_k2v;
+    std::vector<uint32_t> rd_rng_off, rd_rng_start, rd_rng_end, rd_val_off, rd_vals, rd_r2v_off;
+    std::vector<int32_t> rd_r2v;
+};
+
+int32_t accord_deps_download(accord_store *s, accord_deps *out)
+{
+    if (!s || !out) return fail(s, ACCORD_ERR_ARG, "null argument");
+    if (!s->computed) return fail(s, ACCORD_ERR_STATE, "no computed deps");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    HostDepsOwner *o = new (std::nothrow) HostDepsOwner();
+    if (!o) return fail(s, ACCORD_ERR_OOM, "out of host memory");
+    const size_t n1 = (size_t)s->n + 1;
+    try {
+        o->kd_key_off.resize(n1); o->kd_val_off.resize(n1); o->kd_k2v_off.resize(n1);
+        o->kd_keys.resize(s->tot_keys + 1); o->kd_vals.resize(s->tot_vals + 1); o->kd_k2v.resize(s->tot_k2v + 1);
+        o->rd_rng_off.assign(n1, 0); o->rd_val_off.assign(n1, 0); o->rd_r2v_off.assign(n1, 0);
+        o->rd_rng_start.resize(1); o->rd_rng_end.resize(1); o->rd_vals.resize(1); o->rd_r2v.resize(1);
+    } catch (...) {
+        delete o;
+        return fail(s, ACCORD_ERR_OOM, "out of host memory");
+    }
+    auto cp = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream) : hipSuccess;
+    };
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = cp(o->kd_key_off.data(), s->kd_key_off.p, n1 * 4);
+    if (e == hipSuccess) e = cp(o->kd_val_off.data(), s->kd_val_off.p, n1 * 4);
+    if (e == hipSuccess) e = cp(o->kd_k2v_off.data(), s->kd_k2v_off.p, n1 * 4);
+    if (e == hipSuccess) e = cp(o->kd_keys.data(), s->kd_keys.p, s->tot_keys * 4);
+    if (e == hipSuccess) e = cp(o->kd_vals.data(), s->kd_vals.p, s->tot_vals * 4);
+    if (e == hipSuccess) e = cp(o->kd_k2v.data(), s->kd_k2v.p, s->tot_k2v * 4);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e != hipSuccess) {
+        delete o;
+        return fail(s, ACCORD_ERR_HIP, "download: %s", hipGetErrorString(e));
+    }
+    std::memset(out, 0, sizeof(*out));
+    out->n = s->n;
+    out->kd_keys_total = s->tot_keys; out->kd_vals_total = s->tot_vals; out->kd_k2v_total = s->tot_k2v;
+    out->kd_key_off = o->kd_key_off.data(); out->kd_keys = o->kd_keys.data();
+    out->kd_val_off = o->kd_val_off.data(); out->kd_vals = o->kd_vals.data();
+    out->kd_k2v_off = o->kd_k2v_off.data(); out->kd_k2v = o->kd_k2v.data();
+    out->rd_rng_off = o->rd_rng_off.data(); out->rd_rng_start = o->rd_rng_start.data();
+    out->rd_rng_end = o->rd_rng_end.data(); out->rd_val_off = o->rd_val_off.data();
+    out->rd_vals = o->rd_vals.data(); out->rd_r2v_off = o->rd_r2v_off.data(); out->rd_r2v = o->rd_r2v.data();
+    out->owner = o;
+    return ACCORD_OK;
+}
+
+void accord_deps_release(accord_deps *d)
+{
+    if (!d) return;
+    delete (HostDepsOwner *)d->owner;
+    std::memset(d, 0, sizeof(*d));
+}
+
+int32_t accord_deps_batch(accord_store *s, const accord_batch *b, accord_deps *out)
+{
+    int32_t rc = accord_batch_upload(s, b);
+    if (rc) return rc;
+    rc = accord_deps_compute(s);
+    if (rc) return rc;
+    return accord_deps_download(s, out);
+}
+
+} // extern "C"

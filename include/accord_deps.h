@@ -1,0 +1,145 @@
+/*
+ * accord_deps.h -- C ABI of the MI355X-native Accord dependency-calculation path.
+ *
+ * This is the drop-in boundary for ONE hot path of ifesdjeen/cassandra-accord (accord-core):
+ * the replica-side deps calculation behind SafeCommandStore.mapReduceActive
+ * (local/SafeCommandStore.java:274) as driven by PreAccept.calculatePartialDeps
+ * (messages/PreAccept.java:245-265), producing KeyDeps/RangeDeps in their exact serialised
+ * layout (KeyDeps.SerializerSupport.create, primitives/KeyDeps.java:69-72;
+ * RangeDeps.SerializerSupport.create, primitives/RangeDeps.java:69-72).
+ *
+ * Conventions (mirroring the reference, see INTEGRATION.md for the Panama FFM binding):
+ *  - one accord_store handle == one CommandStore == one HIP stream.  Handles are not
+ *    thread-safe; different handles may be used concurrently (the reference's one thread per
+ *    store: impl/InMemoryCommandStore.java:1131-1158).
+ *  - every call returns an int32 status; nonzero maps to IllegalStateException /
+ *    IllegalArgumentException on the Java side (utils/Invariants.java:43-60), with the message
+ *    from accord_last_error().
+ *  - TxnIds are exchanged as SoA (msb, lsb, node) exactly as the Java fields
+ *    (primitives/Timestamp.java:77-79); Java re-materialises them with TxnId.fromBits
+ *    (primitives/TxnId.java:37-40).  Deps values are u32 indices into the batch's TxnId table.
+ *  - keys are u32 ordinals of the store's sorted key dictionary (ordinal order ==
+ *    Key.compareTo order); ranges are (start, end] ordinal pairs (Range.EndInclusive,
+ *    primitives/Range.java:40-88).
+ *  - input buffers are borrowed for the duration of a call; outputs are owned by the
+ *    library until accord_deps_release().
+ *  - there is no CPU fallback: without a usable HIP device every compute call fails with
+ *    ACCORD_ERR_HIP.
+ */
+#ifndef ACCORD_DEPS_H
+#define ACCORD_DEPS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACCORD_OK               0
+#define ACCORD_ERR_ARG         -1   /* bad argument */
+#define ACCORD_ERR_UNSORTED    -2   /* batch TxnIds not strictly ascending (Timestamp.compareTo) */
+#define ACCORD_ERR_KIND        -3   /* a txn kind whose witnesses() throws (LocalOnly, bad ordinal) */
+#define ACCORD_ERR_KEYS        -4   /* keys not sorted-unique, or outside the store's key range */
+#define ACCORD_ERR_DOMAIN      -5   /* domain bit inconsistent with keys/ranges payload */
+#define ACCORD_ERR_RANGES      -6   /* ranges not sorted / de-overlapped / empty */
+#define ACCORD_ERR_CAPACITY    -7   /* a size limit of this build was exceeded */
+#define ACCORD_ERR_HIP         -8   /* HIP runtime error / no device */
+#define ACCORD_ERR_OOM         -9   /* host or device allocation failed */
+#define ACCORD_ERR_STATE      -10   /* call out of sequence */
+
+#define ACCORD_STORE_PROFILE   1u   /* record HIP events around every kernel */
+
+typedef struct accord_store accord_store;
+
+typedef struct {
+    int32_t  device;        /* HIP device ordinal */
+    uint32_t key_lo;        /* store owns key ordinals [key_lo, key_hi) (CommandStores slice) */
+    uint32_t key_hi;
+    uint32_t window;        /* W of the status-at-time model */
+    uint32_t flags;         /* ACCORD_STORE_PROFILE */
+    uint32_t reserved;
+} accord_store_cfg;
+
+/* A batch of transactions in TxnId order (the PreAccept stream of SURVEY.md §8d).  Key txns
+ * (TxnId domain bit 0) carry sorted unique key ordinals; range txns (domain bit 1) carry sorted,
+ * de-overlapped (start, end] ranges (AbstractRanges.sortAndDeoverlap, MERGE_OVERLAPPING).
+ * Pointers are host pointers unless a call says otherwise. */
+typedef struct {
+    uint32_t        n;
+    const uint64_t *msb;        /* [n] Timestamp.msb */
+    const uint64_t *lsb;        /* [n] Timestamp.lsb (hlc low bits << 16 | flags) */
+    const int32_t  *node;       /* [n] Node.Id.id */
+    const uint32_t *key_off;    /* [n+1] CSR into key_ord */
+    const uint32_t *key_ord;    /* [key_off[n]] */
+    const uint32_t *rng_off;    /* [n+1] CSR into rng_start/rng_end, or NULL (no range txns) */
+    const uint32_t *rng_start;
+    const uint32_t *rng_end;
+} accord_batch;
+
+/* Per-txn PartialDeps, exact reference layout (KeyDeps.java:150-187, RangeDeps.java:81-99):
+ * for txn i
+ *   KeyDeps.keys         = kd_keys[kd_key_off[i] .. kd_key_off[i+1])
+ *   KeyDeps.txnIds       = batch txns kd_vals[kd_val_off[i] .. kd_val_off[i+1])  (TxnId order)
+ *   KeyDeps.keysToTxnIds = kd_k2v[kd_k2v_off[i] .. kd_k2v_off[i+1])   (the int[] verbatim)
+ * and the same for RangeDeps (ranges as (rd_rng_start, rd_rng_end] pairs). */
+typedef struct {
+    uint32_t  n;
+    uint32_t  reserved;
+    uint64_t  kd_keys_total, kd_vals_total, kd_k2v_total;
+    uint64_t  rd_rngs_total, rd_vals_total, rd_r2v_total;
+    uint32_t *kd_key_off, *kd_keys, *kd_val_off, *kd_vals, *kd_k2v_off;
+    int32_t  *kd_k2v;
+    uint32_t *rd_rng_off, *rd_rng_start, *rd_rng_end, *rd_val_off, *rd_vals, *rd_r2v_off;
+    int32_t  *rd_r2v;
+    void     *owner;            /* library-private */
+} accord_deps;
+
+/* Per-stage device time of the last accord_deps_compute (ms, HIP events on the store's
+ * stream; zero unless the store was created with ACCORD_STORE_PROFILE). */
+typedef struct {
+    float validate_ms, sort_ms, segment_ms, count_ms, scan_ms, fill_ms, range_ms, total_ms;
+    uint64_t pairs, hist_entries;
+} accord_timing;
+
+/* ---- store lifecycle (CommandStore; impl/InMemoryCommandStore.java:89) ---- */
+int32_t     accord_store_create(const accord_store_cfg *cfg, accord_store **out);
+int32_t     accord_store_destroy(accord_store *store);
+const char *accord_last_error(const accord_store *store);   /* NULL store: last global error */
+void       *accord_store_stream(accord_store *store);        /* the store's hipStream_t */
+
+/* ---- synchronous batch entry: host in, host out ----
+ * CommandStore.calculateDepsBatch(TxnId[], Seekables[], ...) -> PartialDeps[]: identical to
+ * calling PreAccept.calculatePartialDeps (messages/PreAccept.java:245-265) for every txn in
+ * TxnId order under the status-at-time model with window cfg.window. */
+int32_t accord_deps_batch(accord_store *store, const accord_batch *batch, accord_deps *out);
+void    accord_deps_release(accord_deps *deps);
+
+/* ---- device-resident pipeline (inputs already in HBM; used by the bench) ---- */
+int32_t accord_batch_upload(accord_store *store, const accord_batch *host_batch);  /* H2D, sync */
+int32_t accord_deps_compute(accord_store *store);          /* enqueue + run the whole pipeline */
+int32_t accord_deps_device_view(accord_store *store, accord_deps *dev);  /* device pointers */
+int32_t accord_deps_download(accord_store *store, accord_deps *out);     /* D2H copy, host-owned */
+int32_t accord_store_timing(accord_store *store, accord_timing *t);
+
+/* ---- synthetic workload (SURVEY.md §8d stream; splitmix64 + Zipf rejection-inversion) ---- */
+typedef struct {
+    uint32_t n;               /* txns */
+    uint32_t keys_per_txn;    /* k distinct keys per key txn */
+    uint32_t keyspace;        /* key ordinals [0, keyspace) */
+    uint32_t ranges_max;      /* range txns carry 1..ranges_max ranges */
+    double   zipf_s;          /* 0 = uniform */
+    double   write_frac;      /* P(Write) */
+    double   range_frac;      /* fraction of range-domain txns */
+    uint32_t range_len_max;   /* (s, s+len], len ~ U[1, range_len_max] */
+    uint32_t node_mod;        /* node = 1 + (i mod node_mod) */
+    uint64_t seed;
+} accord_workload_cfg;
+
+/* arrays are malloc'd; free with accord_workload_free */
+int32_t accord_workload_generate(const accord_workload_cfg *cfg, accord_batch *out);
+void    accord_workload_free(accord_batch *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

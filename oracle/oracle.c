@@ -1,0 +1,965 @@
+/*
+ * oracle.c -- CPU restatement of the reference dependency-calculation path.
+ * TEST INFRASTRUCTURE ONLY (see oracle.h header).  All file:line citations are relative to
+ * /root/reference/accord-core/src/main/java/accord/.
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------
+ * Timestamp / TxnId  (primitives/Timestamp.java, primitives/TxnId.java, local/Node.java)
+ * ------------------------------------------------------------------------------------------ */
+
+#define IDENTITY_FLAGS 0x1EULL                   /* Timestamp.java:42 */
+#define IDENTITY_LSB   0xFFFFFFFFFFFF001EULL     /* Timestamp.java:41 */
+
+int or_ts_compare(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode)
+{
+    /* Timestamp.compareTo: Long.compareUnsigned(msb), then Long.compare(lowHlc(lsb)) where
+     * lowHlc = lsb >>> 16 (always non-negative), then flags & IDENTITY_FLAGS, then
+     * Node.Id.compareTo = Integer.compare (Node.java:134-137). */
+    if (amsb != bmsb) return amsb < bmsb ? -1 : 1;
+    uint64_t ah = alsb >> 16, bh = blsb >> 16;
+    if (ah != bh) return ah < bh ? -1 : 1;
+    uint64_t af = alsb & IDENTITY_FLAGS, bf = blsb & IDENTITY_FLAGS;
+    if (af != bf) return af < bf ? -1 : 1;
+    if (anode != bnode) return anode < bnode ? -1 : 1;
+    return 0;
+}
+
+int or_ts_equals(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode)
+{
+    return amsb == bmsb && ((alsb ^ blsb) & IDENTITY_LSB) == 0 && anode == bnode;
+}
+
+typedef struct { uint64_t msb, lsb; int32_t node; } ts_t;
+
+static inline int ts_cmp(const ts_t *a, const ts_t *b)
+{
+    return or_ts_compare(a->msb, a->lsb, a->node, b->msb, b->lsb, b->node);
+}
+
+/* Txn.Kind ordinals (primitives/Txn.java:53-118) and TxnId flag decoding (TxnId.java:129-157) */
+enum { K_READ = 0, K_WRITE = 1, K_EPHEMERAL_READ = 2, K_SYNC_POINT = 3, K_EXCL_SYNC_POINT = 4, K_LOCAL_ONLY = 5 };
+static inline int kind_of(uint64_t lsb)   { return (int)((lsb >> 1) & 7); }
+static inline int domain_of(uint64_t lsb) { return (int)(lsb & 1); }      /* 0 Key, 1 Range */
+
+/* Kind.isGloballyVisible (Txn.java:187-201); -1 = AssertionError */
+static int is_globally_visible(int k)
+{
+    switch (k) {
+    case K_EPHEMERAL_READ: case K_LOCAL_ONLY: return 0;
+    case K_WRITE: case K_READ: case K_EXCL_SYNC_POINT: case K_SYNC_POINT: return 1;
+    default: return -1;
+    }
+}
+
+/* Kind.witnesses() (Txn.java:221-235) as a Kinds code, and Kinds.test (Txn.java:140-152) */
+enum { WS = 0, RS_OR_WS = 1, ANY_GLOBALLY_VISIBLE = 2 };
+static int witnesses_of(int k)
+{
+    switch (k) {
+    case K_EPHEMERAL_READ: case K_READ: return WS;
+    case K_WRITE: return RS_OR_WS;
+    case K_SYNC_POINT: case K_EXCL_SYNC_POINT: return ANY_GLOBALLY_VISIBLE;
+    default: return -1;            /* LocalOnly: AssertionError */
+    }
+}
+static int kinds_test(int kinds, int k)
+{
+    switch (kinds) {
+    case WS: return k == K_WRITE;
+    case RS_OR_WS: return k == K_READ || k == K_WRITE;
+    case ANY_GLOBALLY_VISIBLE: return is_globally_visible(k) == 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Small growable arrays
+ * ------------------------------------------------------------------------------------------ */
+typedef struct { uint32_t *p; size_t n, cap; } u32v;
+typedef struct { int32_t *p; size_t n, cap; } i32v;
+
+static int u32v_push(u32v *v, uint32_t x)
+{
+    if (v->n == v->cap) {
+        size_t nc = v->cap ? v->cap * 2 : 64;
+        uint32_t *np = (uint32_t *)realloc(v->p, nc * sizeof(uint32_t));
+        if (!np) return -1;
+        v->p = np; v->cap = nc;
+    }
+    v->p[v->n++] = x;
+    return 0;
+}
+static int i32v_push(i32v *v, int32_t x)
+{
+    if (v->n == v->cap) {
+        size_t nc = v->cap ? v->cap * 2 : 64;
+        int32_t *np = (int32_t *)realloc(v->p, nc * sizeof(int32_t));
+        if (!np) return -1;
+        v->p = np; v->cap = nc;
+    }
+    v->p[v->n++] = x;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * RelationMultiMap.AbstractBuilder  (utils/RelationMultiMap.java:88-271)
+ *
+ * Keys are 64-bit comparable codes: a key ordinal (IntKey, Integer.compare: IntKey.java:161-165)
+ * or a range packed as start<<32|end, which orders exactly like Range.compare (start, then end:
+ * Range.java:310-317).  Values are indices into a TxnId table compared with Timestamp.compareTo
+ * and de-duplicated with Timestamp.equals.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    const ts_t *tbl;          /* value table */
+    uint64_t *keys;  uint32_t *key_limits; size_t kcap;
+    uint32_t *k2v;   size_t vcap;        /* keysToValues buffer: values in add order */
+    uint32_t key_count, key_offset, total_count;
+    int has_ordered_keys, has_ordered_values;
+} mm_builder;
+
+static void mmb_init(mm_builder *b, const ts_t *tbl)
+{
+    memset(b, 0, sizeof(*b));
+    b->tbl = tbl;
+    b->has_ordered_keys = 1;
+    b->has_ordered_values = 1;
+}
+static void mmb_reset(mm_builder *b)
+{
+    b->key_count = b->key_offset = b->total_count = 0;
+    b->has_ordered_keys = b->has_ordered_values = 1;
+}
+static void mmb_free(mm_builder *b)
+{
+    free(b->keys); free(b->key_limits); free(b->k2v);
+    memset(b, 0, sizeof(*b));
+}
+
+static inline int vcmp(const ts_t *tbl, uint32_t a, uint32_t b) { return ts_cmp(&tbl[a], &tbl[b]); }
+
+/* stable insertion/merge sort of value indices by TxnId (Arrays.sort on objects is a stable
+ * TimSort; equal-identity duplicates keep add order, and de-dup keeps the first) */
+static void stable_sort_vals(const ts_t *tbl, uint32_t *a, uint32_t n, uint32_t *tmp)
+{
+    if (n < 2) return;
+    if (n <= 16) {
+        for (uint32_t i = 1; i < n; ++i) {
+            uint32_t x = a[i]; uint32_t j = i;
+            while (j > 0 && vcmp(tbl, a[j - 1], x) > 0) { a[j] = a[j - 1]; --j; }
+            a[j] = x;
+        }
+        return;
+    }
+    uint32_t h = n / 2;
+    stable_sort_vals(tbl, a, h, tmp);
+    stable_sort_vals(tbl, a + h, n - h, tmp);
+    uint32_t i = 0, j = h, o = 0;
+    while (i < h && j < n) tmp[o++] = (vcmp(tbl, a[j], a[i]) < 0) ? a[j++] : a[i++];
+    while (i < h) tmp[o++] = a[i++];
+    while (j < n) tmp[o++] = a[j++];
+    memcpy(a, tmp, n * sizeof(uint32_t));
+}
+
+static int mmb_finish_key(mm_builder *b)       /* finishKey(): RelationMultiMap.java:147-173 */
+{
+    if (b->total_count == b->key_offset && b->key_count > 0) { --b->key_count; return 0; }
+    if (b->key_count == 0) return 0;
+    if (!b->has_ordered_values) {
+        uint32_t n = b->total_count - b->key_offset;
+        uint32_t *tmp = (uint32_t *)malloc((size_t)n * sizeof(uint32_t) + 4);
+        if (!tmp) return -1;
+        stable_sort_vals(b->tbl, b->k2v + b->key_offset, n, tmp);
+        free(tmp);
+        uint32_t removed = 0;
+        for (uint32_t i = b->key_offset + 1; i < b->total_count; ++i) {
+            const ts_t *p = &b->tbl[b->k2v[i - 1]], *q = &b->tbl[b->k2v[i]];
+            if (or_ts_equals(p->msb, p->lsb, p->node, q->msb, q->lsb, q->node)) ++removed;
+            else if (removed > 0) b->k2v[i - removed] = b->k2v[i];
+        }
+        b->total_count -= removed;
+    }
+    b->key_limits[b->key_count - 1] = b->total_count;
+    b->key_offset = b->total_count;
+    return 0;
+}
+
+static int mmb_next_key(mm_builder *b, uint64_t key)   /* nextKey(): :125-145 */
+{
+    if (b->key_count > 0 && b->keys[b->key_count - 1] >= key) b->has_ordered_keys = 0;
+    if (mmb_finish_key(b)) return -1;
+    if (b->key_count == b->kcap) {
+        size_t nc = b->kcap ? b->kcap * 2 : 16;
+        uint64_t *nk = (uint64_t *)realloc(b->keys, nc * sizeof(uint64_t));
+        uint32_t *nl = nk ? (uint32_t *)realloc(b->key_limits, nc * sizeof(uint32_t)) : NULL;
+        if (!nk || !nl) { if (nk) b->keys = nk; return -1; }
+        b->keys = nk; b->key_limits = nl; b->kcap = nc;
+    }
+    b->keys[b->key_count++] = key;
+    b->has_ordered_values = 1;
+    return 0;
+}
+
+static int mmb_add_value(mm_builder *b, uint32_t v)   /* add(V): :185-199 */
+{
+    if (b->has_ordered_values && b->total_count > b->key_offset
+        && vcmp(b->tbl, b->k2v[b->total_count - 1], v) >= 0)
+        b->has_ordered_values = 0;
+    if (b->total_count >= b->vcap) {
+        size_t nc = b->vcap ? b->vcap * 2 : 64;
+        uint32_t *nv = (uint32_t *)realloc(b->k2v, nc * sizeof(uint32_t));
+        if (!nv) return -1;
+        b->k2v = nv; b->vcap = nc;
+    }
+    b->k2v[b->total_count++] = v;
+    return 0;
+}
+
+static int mmb_add(mm_builder *b, uint64_t key, uint32_t v)   /* add(K, V): :175-180 */
+{
+    if (b->key_count == 0 || b->keys[b->key_count - 1] != key)
+        if (mmb_next_key(b, key)) return -1;
+    return mmb_add_value(b, v);
+}
+
+/* Output accumulator for a sequence of per-txn multimaps */
+typedef struct {
+    u32v key_off, keys_lo, keys_hi, val_off, vals, k2v_off;
+    i32v k2v;
+} mm_out;
+
+static int mmo_init(mm_out *o)
+{
+    memset(o, 0, sizeof(*o));
+    if (u32v_push(&o->key_off, 0) || u32v_push(&o->val_off, 0) || u32v_push(&o->k2v_off, 0)) return -1;
+    return 0;
+}
+static void mmo_free(mm_out *o)
+{
+    free(o->key_off.p); free(o->keys_lo.p); free(o->keys_hi.p); free(o->val_off.p);
+    free(o->vals.p); free(o->k2v_off.p); free(o->k2v.p);
+    memset(o, 0, sizeof(*o));
+}
+static int mmo_close_txn(mm_out *o)
+{
+    if (u32v_push(&o->key_off, (uint32_t)o->keys_lo.n)) return -1;
+    if (u32v_push(&o->val_off, (uint32_t)o->vals.n)) return -1;
+    if (u32v_push(&o->k2v_off, (uint32_t)o->k2v.n)) return -1;
+    return 0;
+}
+
+static int cmp_u64(const void *a, const void *b)
+{
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* build(): :201-260.  Appends one multimap to `o` (possibly empty = none()).  is_range selects
+ * how a key code is split into the output key arrays.  Returns -1 on a builder exception. */
+static int mmb_build(mm_builder *b, mm_out *o, int is_range)
+{
+    if (b->total_count == 0) return mmo_close_txn(o);                 /* none() */
+    if (mmb_finish_key(b)) return -1;
+
+    uint32_t total = b->total_count;
+    uint32_t *uniq = (uint32_t *)malloc((size_t)total * sizeof(uint32_t) + 4);
+    uint32_t *tmp = (uint32_t *)malloc((size_t)total * sizeof(uint32_t) + 4);
+    if (!uniq || !tmp) { free(uniq); free(tmp); return -1; }
+    memcpy(uniq, b->k2v, total * sizeof(uint32_t));
+    stable_sort_vals(b->tbl, uniq, total, tmp);
+    uint32_t value_count = 1;
+    for (uint32_t i = 1; i < total; ++i) {
+        const ts_t *p = &b->tbl[uniq[value_count - 1]], *q = &b->tbl[uniq[i]];
+        if (!or_ts_equals(p->msb, p->lsb, p->node, q->msb, q->lsb, q->node)) uniq[value_count++] = uniq[i];
+    }
+    free(tmp);
+
+    uint32_t kc = b->key_count;
+    uint64_t *sorted_keys = (uint64_t *)malloc((size_t)kc * sizeof(uint64_t) + 8);
+    uint32_t *sorted_idx = NULL;
+    if (!sorted_keys) { free(uniq); return -1; }
+    memcpy(sorted_keys, b->keys, kc * sizeof(uint64_t));
+    if (!b->has_ordered_keys) {
+        sorted_idx = (uint32_t *)malloc((size_t)kc * sizeof(uint32_t) + 4);
+        if (!sorted_idx) { free(uniq); free(sorted_keys); return -1; }
+        qsort(sorted_keys, kc, sizeof(uint64_t), cmp_u64);
+        for (uint32_t i = 1; i < kc; ++i)
+            if (sorted_keys[i - 1] == sorted_keys[i]) {   /* "Key ... has been visited more than once" */
+                free(uniq); free(sorted_keys); free(sorted_idx); return -1;
+            }
+        for (uint32_t i = 0; i < kc; ++i) {
+            uint32_t lo = 0, hi = kc;
+            while (lo < hi) { uint32_t m = (lo + hi) / 2; if (sorted_keys[m] < b->keys[i]) lo = m + 1; else hi = m; }
+            sorted_idx[lo] = i;
+        }
+    }
+
+    /* emit keys, values, then result[keyCount + totalCount] */
+    for (uint32_t ki = 0; ki < kc; ++ki) {
+        uint64_t k = sorted_keys[ki];
+        if (u32v_push(&o->keys_lo, is_range ? (uint32_t)(k >> 32) : (uint32_t)k)) goto fail;
+        if (u32v_push(&o->keys_hi, is_range ? (uint32_t)k : 0)) goto fail;
+    }
+    for (uint32_t v = 0; v < value_count; ++v)
+        if (u32v_push(&o->vals, uniq[v])) goto fail;
+
+    size_t base = o->k2v.n;
+    for (uint32_t i = 0; i < kc; ++i) if (i32v_push(&o->k2v, 0)) goto fail;
+    int32_t offset = (int32_t)kc;
+    for (uint32_t ki = 0; ki < kc; ++ki) {
+        uint32_t k = sorted_idx ? sorted_idx[ki] : ki;
+        uint32_t from = k == 0 ? 0 : b->key_limits[k - 1];
+        uint32_t to = b->key_limits[k];
+        /* SortedArrays.foldlIntersection(values, keysToValues[from,to)) -> result[offset++] = li */
+        uint32_t li = 0;
+        for (uint32_t r = from; r < to; ++r) {
+            uint32_t lo = li, hi = value_count;
+            while (lo < hi) { uint32_t m = (lo + hi) / 2; if (vcmp(b->tbl, uniq[m], b->k2v[r]) < 0) lo = m + 1; else hi = m; }
+            if (lo < value_count && vcmp(b->tbl, uniq[lo], b->k2v[r]) == 0) {
+                if (i32v_push(&o->k2v, (int32_t)lo)) goto fail;
+                ++offset;
+                li = lo + 1;
+            }
+        }
+        o->k2v.p[base + ki] = offset;
+    }
+    free(uniq); free(sorted_keys); free(sorted_idx);
+    return mmo_close_txn(o);
+fail:
+    free(uniq); free(sorted_keys); free(sorted_idx);
+    return -1;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * CommandsForKey (local/CommandsForKey.java) -- literal restatement of the state and of
+ * mapReduceActive.  InternalStatus ordinals: :194-203.
+ * ------------------------------------------------------------------------------------------ */
+enum { S_TRANSITIVELY_KNOWN = 0, S_HISTORICAL, S_PREACCEPTED, S_ACCEPTED, S_COMMITTED, S_STABLE,
+       S_APPLIED, S_INVALID_OR_TRUNCATED };
+
+typedef struct {
+    uint32_t txn;            /* index into the stream table (TxnId) */
+    uint8_t  status;
+    ts_t     execute_at;
+} txninfo_t;
+
+typedef struct {
+    txninfo_t *txns;   uint32_t n;     /* sorted by TxnId, :415 */
+    uint32_t *committed; uint32_t nc;  /* indices into txns, sorted by executeAt, :419 */
+} cfk_t;
+
+static const ts_t *g_sort_tbl;         /* qsort context (single-threaded oracle) */
+static const txninfo_t *g_sort_txns;
+static int cmp_committed(const void *a, const void *b)
+{
+    const txninfo_t *x = &g_sort_txns[*(const uint32_t *)a], *y = &g_sort_txns[*(const uint32_t *)b];
+    int c = ts_cmp(&x->execute_at, &y->execute_at);
+    if (c) return c;
+    /* Arrays.sort(Object[], Comparator) is stable: keep TxnId order among equal executeAt */
+    return (*(const uint32_t *)a < *(const uint32_t *)b) ? -1 : 1;
+}
+
+/* CommandsForKey(...) constructor: rebuild committed[] by a full pass + sort (:422-470).
+ * The reference allocates a brand new TxnInfo[] on every update (insert :880-944,
+ * update :652-706); the copy is restated so the CPU baseline pays the same O(n) per change. */
+static int cfk_rebuild(cfk_t *c, txninfo_t *new_txns, uint32_t new_n)
+{
+    free(c->txns);
+    c->txns = new_txns; c->n = new_n;
+    uint32_t count = 0;
+    for (uint32_t i = 0; i < new_n; ++i)
+        if (new_txns[i].status >= S_COMMITTED && new_txns[i].status != S_INVALID_OR_TRUNCATED) ++count;
+    free(c->committed);
+    c->committed = (uint32_t *)malloc((size_t)count * sizeof(uint32_t) + 4);
+    if (!c->committed) return -1;
+    c->nc = 0;
+    for (uint32_t i = 0; i < new_n; ++i)
+        if (new_txns[i].status >= S_COMMITTED && new_txns[i].status != S_INVALID_OR_TRUNCATED) c->committed[c->nc++] = i;
+    g_sort_txns = new_txns;
+    qsort(c->committed, c->nc, sizeof(uint32_t), cmp_committed);
+    return 0;
+}
+
+/* Arrays.binarySearch(txns, ts): returns index of an equal element, else -(ins)-1 */
+static long cfk_search(const cfk_t *c, const ts_t *tbl, const ts_t *ts)
+{
+    long lo = 0, hi = (long)c->n - 1;
+    while (lo <= hi) {
+        long m = (lo + hi) >> 1;
+        int r = ts_cmp(&tbl[c->txns[m].txn], ts);
+        if (r < 0) lo = m + 1; else if (r > 0) hi = m - 1; else return m;
+    }
+    return -(lo + 1);
+}
+
+static int cfk_insert(cfk_t *c, const ts_t *tbl, uint32_t txn, uint8_t status)
+{
+    long pos = cfk_search(c, tbl, &tbl[txn]);
+    if (pos >= 0) return -1;                 /* already present: not expected in the model */
+    pos = -1 - pos;
+    txninfo_t *nt = (txninfo_t *)malloc(((size_t)c->n + 1) * sizeof(txninfo_t));
+    if (!nt) return -1;
+    memcpy(nt, c->txns, (size_t)pos * sizeof(txninfo_t));
+    nt[pos].txn = txn; nt[pos].status = status; nt[pos].execute_at = tbl[txn];
+    memcpy(nt + pos + 1, c->txns + pos, ((size_t)c->n - pos) * sizeof(txninfo_t));
+    return cfk_rebuild(c, nt, c->n + 1);
+}
+
+static int cfk_update_status(cfk_t *c, const ts_t *tbl, uint32_t txn, uint8_t status, const ts_t *execute_at)
+{
+    long pos = cfk_search(c, tbl, &tbl[txn]);
+    if (pos < 0) return -1;
+    txninfo_t *nt = (txninfo_t *)malloc((size_t)c->n * sizeof(txninfo_t) + sizeof(txninfo_t));
+    if (!nt) return -1;
+    memcpy(nt, c->txns, (size_t)c->n * sizeof(txninfo_t));
+    nt[pos].status = status; nt[pos].execute_at = *execute_at;
+    return cfk_rebuild(c, nt, c->n);
+}
+
+/* CommandsForKey.mapReduceActive (:614-650), emitting (key, txn) into the builder */
+static int cfk_map_reduce_active(const cfk_t *c, const ts_t *tbl, const ts_t *started_before, int test_kinds,
+                                 uint64_t key, mm_builder *b, long exclude_txn)
+{
+    const ts_t *max_committed_before = NULL;
+    {
+        /* SortedArrays.binarySearch(committed, ..., (f, v) -> f.compareTo(v.executeAt), FAST) */
+        long lo = 0, hi = (long)c->nc - 1, found = -1;
+        while (lo <= hi) {
+            long m = (lo + hi) >> 1;
+            int r = ts_cmp(started_before, &c->txns[c->committed[m]].execute_at);
+            if (r > 0) lo = m + 1; else if (r < 0) hi = m - 1; else { found = m; break; }
+        }
+        long i = found >= 0 ? found - 1 : lo - 1;            /* i<0 ? -2-i : --i */
+        while (i >= 0 && kind_of(tbl[c->txns[c->committed[i]].txn].lsb) != K_WRITE) --i;
+        max_committed_before = i < 0 ? NULL : &c->txns[c->committed[i]].execute_at;
+    }
+    long end = cfk_search(c, tbl, started_before);           /* insertPos(0, startedBefore) */
+    if (end < 0) end = -1 - end;
+
+    for (long i = 0; i < end; ++i) {
+        const txninfo_t *t = &c->txns[i];
+        if (!kinds_test(test_kinds, kind_of(tbl[t->txn].lsb))) continue;
+        switch (t->status) {
+        case S_COMMITTED: case S_STABLE: case S_APPLIED:
+            if (max_committed_before == NULL || ts_cmp(&t->execute_at, max_committed_before) >= 0) break;
+            continue;
+        case S_TRANSITIVELY_KNOWN: case S_INVALID_OR_TRUNCATED:
+            continue;
+        default: break;
+        }
+        /* PreAccept.calculatePartialDeps lambda (messages/PreAccept.java:255-258): p1 filter */
+        if (exclude_txn >= 0 && (uint32_t)exclude_txn == t->txn) continue;
+        if (mmb_add(b, key, t->txn)) return -1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Range commands (impl/InMemoryCommandStore.java:100 TreeMap<TxnId,RangeCommand>, registered
+ * at :739-762, scanned at :883-1016).  SaveStatus is collapsed to {live, Erased}.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    uint32_t txn;
+    int erased;
+    uint32_t r0, r1;                 /* its ranges: stream rng_* [r0, r1) */
+} rangecmd_t;
+
+typedef struct { uint64_t range; uint32_t *txns; uint32_t n, cap; } collect_t;
+
+static int range_intersects_key(uint32_t s, uint32_t e, uint32_t key) { return s < key && key <= e; }
+static int range_intersects_range(uint32_t s, uint32_t e, uint32_t s2, uint32_t e2) { return s < e2 && s2 < e; }
+
+/* ------------------------------------------------------------------------------------------
+ * Stream driver (status-at-time model)
+ * ------------------------------------------------------------------------------------------ */
+
+static int alloc_out(or_deps *out, mm_out *kd, mm_out *rd, uint32_t n)
+{
+    memset(out, 0, sizeof(*out));
+    out->n = n;
+#define TAKE(dst, v) do { out->dst = (v).p ? (v).p : (__typeof__(out->dst))malloc(4); (v).p = NULL; if (!out->dst) return -1; } while (0)
+    TAKE(kd_key_off, kd->key_off); TAKE(kd_keys, kd->keys_lo); TAKE(kd_val_off, kd->val_off);
+    TAKE(kd_vals, kd->vals); TAKE(kd_k2v_off, kd->k2v_off); TAKE(kd_k2v, kd->k2v);
+    TAKE(rd_rng_off, rd->key_off); TAKE(rd_rng_start, rd->keys_lo); TAKE(rd_rng_end, rd->keys_hi);
+    TAKE(rd_val_off, rd->val_off); TAKE(rd_vals, rd->vals); TAKE(rd_r2v_off, rd->k2v_off); TAKE(rd_r2v, rd->k2v);
+#undef TAKE
+    return 0;
+}
+
+void or_deps_free(or_deps *d)
+{
+    if (!d) return;
+    free(d->kd_key_off); free(d->kd_keys); free(d->kd_val_off); free(d->kd_vals); free(d->kd_k2v_off); free(d->kd_k2v);
+    free(d->rd_rng_off); free(d->rd_rng_start); free(d->rd_rng_end); free(d->rd_val_off); free(d->rd_vals);
+    free(d->rd_r2v_off); free(d->rd_r2v);
+    memset(d, 0, sizeof(*d));
+}
+
+static uint32_t max_key(const or_stream *s, uint32_t n)
+{
+    uint32_t m = 0;
+    for (uint32_t p = 0; p < s->key_off[n]; ++p) if (s->key_ord[p] > m) m = s->key_ord[p];
+    if (s->rng_off)
+        for (uint32_t r = 0; r < s->rng_off[n]; ++r) if (s->rng_end[r] > m) m = s->rng_end[r];
+    return m;
+}
+
+/* validation shared by both restatements: TxnId strictly ascending, keys sorted unique,
+ * ranges sorted and de-overlapped (AbstractRanges.sortAndDeoverlap MERGE_OVERLAPPING:
+ * AbstractRanges.java:696-782), domain consistent with the payload, no LocalOnly query. */
+static int validate(const or_stream *s, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        if (i > 0 && or_ts_compare(s->msb[i - 1], s->lsb[i - 1], s->node[i - 1], s->msb[i], s->lsb[i], s->node[i]) >= 0) return -2;
+        if (witnesses_of(kind_of(s->lsb[i])) < 0) return -3;
+        for (uint32_t p = s->key_off[i] + 1; p < s->key_off[i + 1]; ++p) if (s->key_ord[p - 1] >= s->key_ord[p]) return -4;
+        if (s->key_ord && s->key_off[i + 1] > s->key_off[i] && s->key_ord[s->key_off[i + 1] - 1] >= 0x80000000u) return -4;
+        uint32_t nr = s->rng_off ? s->rng_off[i + 1] - s->rng_off[i] : 0;
+        if (domain_of(s->lsb[i]) == 0 && nr) return -5;
+        if (domain_of(s->lsb[i]) == 1 && s->key_off[i + 1] != s->key_off[i]) return -5;
+        for (uint32_t r = 0; r < nr; ++r) {
+            uint32_t a = s->rng_off[i] + r;
+            if (s->rng_start[a] >= s->rng_end[a]) return -6;
+            if (r > 0 && s->rng_end[a - 1] > s->rng_start[a]) return -6;
+        }
+    }
+    return 0;
+}
+
+static int stream_literal(const or_stream *s, uint32_t n, or_deps *out)
+{
+    int rc = validate(s, n);
+    if (rc) return rc;
+    ts_t *tbl = (ts_t *)malloc((size_t)(n ? n : 1) * sizeof(ts_t));
+    if (!tbl) return -1;
+    for (uint32_t i = 0; i < n; ++i) { tbl[i].msb = s->msb[i]; tbl[i].lsb = s->lsb[i]; tbl[i].node = s->node[i]; }
+    g_sort_tbl = tbl;
+    uint32_t nkeys = max_key(s, n) + 1;
+    cfk_t *cfks = (cfk_t *)calloc(nkeys, sizeof(cfk_t));
+    rangecmd_t *rcs = (rangecmd_t *)calloc(n ? n : 1, sizeof(rangecmd_t));
+    uint32_t nrc = 0, rc_erase_cursor = 0;
+    mm_builder kb, rb;
+    mm_out kd, rd;
+    collect_t *coll = NULL; uint32_t ncoll = 0, capcoll = 0;
+    mmb_init(&kb, tbl); mmb_init(&rb, tbl);
+    rc = -1;
+    if (!cfks || !rcs || mmo_init(&kd) || mmo_init(&rd)) goto done;
+
+    for (uint32_t i = 0; i < n; ++i) {
+        /* 1. status at time i: txn j = i-W-1 leaves the window -> APPLIED (executeAt=txnId) if a
+         *    key txn, Erased if a range txn. */
+        if (i >= s->window + 1) {
+            uint32_t j = i - s->window - 1;
+            if (domain_of(s->lsb[j]) == 0) {
+                if (is_globally_visible(kind_of(s->lsb[j])) == 1)
+                    for (uint32_t p = s->key_off[j]; p < s->key_off[j + 1]; ++p)
+                        if (cfk_update_status(&cfks[s->key_ord[p]], tbl, j, S_APPLIED, &tbl[j])) goto done;
+            } else {
+                while (rc_erase_cursor < nrc && rcs[rc_erase_cursor].txn <= j) {
+                    if (rcs[rc_erase_cursor].txn == j) rcs[rc_erase_cursor].erased = 1;
+                    ++rc_erase_cursor;
+                }
+            }
+        }
+        /* 2. register txn i as PREACCEPTED (SafeCommandStore.updateCommandsForKey :212-239 ->
+         *    CommandsForKey.insert; range txns -> InMemoryCommandStore rangeCommands :739-762) */
+        int kind_i = kind_of(s->lsb[i]);
+        if (domain_of(s->lsb[i]) == 0) {
+            if (is_globally_visible(kind_i) == 1)
+                for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p)
+                    if (cfk_insert(&cfks[s->key_ord[p]], tbl, i, S_PREACCEPTED)) goto done;
+        } else {
+            rcs[nrc].txn = i; rcs[nrc].erased = 0; rcs[nrc].r0 = s->rng_off[i]; rcs[nrc].r1 = s->rng_off[i + 1];
+            ++nrc;
+        }
+
+        /* 3. calculatePartialDeps (messages/PreAccept.java:245-265): startedBefore = executeAt =
+         *    txnId, p1 = null, keys first then ranges (SafeCommandStore.java:269-274). */
+        int test_kinds = witnesses_of(kind_i);
+        mmb_reset(&kb); mmb_reset(&rb);
+        const ts_t *sb = &tbl[i];
+        if (domain_of(s->lsb[i]) == 0) {
+            for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) {
+                uint32_t key = s->key_ord[p];
+                if (cfk_map_reduce_active(&cfks[key], tbl, sb, test_kinds, key, &kb, -1)) goto done;
+            }
+        } else {
+            /* mapReduceForKey Range case (InMemoryCommandStore.java:274-289): every CFK key in
+             * each (start,end] in ascending order */
+            for (uint32_t r = s->rng_off[i]; r < s->rng_off[i + 1]; ++r)
+                for (uint32_t key = s->rng_start[r] + 1; key <= s->rng_end[r] && key < nkeys; ++key)
+                    if (cfks[key].n && cfk_map_reduce_active(&cfks[key], tbl, sb, test_kinds, key, &kb, -1)) goto done;
+        }
+        /* mapReduceRangesInternal: TreeMap<Range, List<TxnInfo>> collect by Range.compare */
+        ncoll = 0;
+        for (uint32_t c = 0; c < nrc; ++c) {
+            const rangecmd_t *cmd = &rcs[c];
+            if (cmd->erased) continue;                                         /* :891 */
+            if (ts_cmp(&tbl[cmd->txn], sb) >= 0) continue;                     /* :901-902 */
+            if (!kinds_test(test_kinds, kind_of(s->lsb[cmd->txn]))) continue;  /* :927 */
+            for (uint32_t a = cmd->r0; a < cmd->r1; ++a) {                     /* foldl :953-959 */
+                uint32_t rs = s->rng_start[a], re = s->rng_end[a];
+                int hit = 0;
+                if (domain_of(s->lsb[i]) == 0) {
+                    for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1] && !hit; ++p)
+                        hit = range_intersects_key(rs, re, s->key_ord[p]);
+                } else {
+                    for (uint32_t r = s->rng_off[i]; r < s->rng_off[i + 1] && !hit; ++r)
+                        hit = range_intersects_range(rs, re, s->rng_start[r], s->rng_end[r]);
+                }
+                if (!hit) continue;
+                uint64_t code = ((uint64_t)rs << 32) | re;
+                uint32_t ci = 0;
+                while (ci < ncoll && coll[ci].range != code) ++ci;
+                if (ci == ncoll) {
+                    if (ncoll == capcoll) {
+                        uint32_t nc = capcoll ? capcoll * 2 : 16;
+                        collect_t *np = (collect_t *)realloc(coll, nc * sizeof(collect_t));
+                        if (!np) goto done;
+                        memset(np + capcoll, 0, (nc - capcoll) * sizeof(collect_t));
+                        coll = np; capcoll = nc;
+                    }
+                    coll[ncoll].range = code; coll[ncoll].n = 0;
+                    ++ncoll;
+                }
+                collect_t *cl = &coll[ci];
+                if (cl->n == 0 || cl->txns[cl->n - 1] != cmd->txn) {
+                    if (cl->n == cl->cap) {
+                        uint32_t nc = cl->cap ? cl->cap * 2 : 8;
+                        uint32_t *np = (uint32_t *)realloc(cl->txns, nc * sizeof(uint32_t));
+                        if (!np) goto done;
+                        cl->txns = np; cl->cap = nc;
+                    }
+                    cl->txns[cl->n++] = cmd->txn;
+                }
+            }
+        }
+        /* replay in Range.compare order */
+        for (uint32_t a = 1; a < ncoll; ++a) {
+            collect_t x = coll[a]; uint32_t b2 = a;
+            while (b2 > 0 && coll[b2 - 1].range > x.range) { coll[b2] = coll[b2 - 1]; --b2; }
+            coll[b2] = x;
+        }
+        for (uint32_t a = 0; a < ncoll; ++a)
+            for (uint32_t t = 0; t < coll[a].n; ++t)
+                if (mmb_add(&rb, coll[a].range, coll[a].txns[t])) goto done;
+
+        if (mmb_build(&kb, &kd, 0)) goto done;
+        if (mmb_build(&rb, &rd, 1)) goto done;
+    }
+    if (alloc_out(out, &kd, &rd, n)) goto done;
+    rc = 0;
+done:
+    if (cfks) { for (uint32_t k = 0; k < nkeys; ++k) { free(cfks[k].txns); free(cfks[k].committed); } }
+    free(cfks); free(rcs);
+    if (coll) { for (uint32_t a = 0; a < capcoll; ++a) free(coll[a].txns); }
+    free(coll);
+    mmb_free(&kb); mmb_free(&rb);
+    mmo_free(&kd); mmo_free(&rd);
+    free(tbl);
+    return rc;
+}
+
+int or_stream_deps_literal(const or_stream *s, or_deps *out) { return stream_literal(s, s->n, out); }
+int or_stream_deps_literal_prefix(const or_stream *s, uint32_t limit, or_deps *out)
+{
+    return stream_literal(s, limit < s->n ? limit : s->n, out);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Fast restatement.  Under the status-at-time model the a3 filter for (txn i, key) reduces to
+ * the witnessed entries of the key's history in [lcw, i) where lcw is the last Write entry
+ * j < i-W (else the start of the history): CommandsForKey.java:620-645 with every j < i-W
+ * APPLIED at executeAt=txnId (so committed[] is the history prefix before i-W) and every
+ * i-W <= j < i PREACCEPTED.  Range commands: live iff j >= i-W, no pruning (InMemoryCommandStore
+ * .java:883-1016).
+ * ------------------------------------------------------------------------------------------ */
+static int cmp_u32(const void *a, const void *b)
+{
+    uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+int or_stream_deps_fast(const or_stream *s, or_deps *out)
+{
+    uint32_t n = s->n;
+    int rc = validate(s, n);
+    if (rc) return rc;
+    uint32_t nkeys = max_key(s, n) + 1;
+    uint32_t P = s->key_off[n];
+    uint32_t *hoff = (uint32_t *)calloc((size_t)nkeys + 1, sizeof(uint32_t));
+    uint32_t *hist = (uint32_t *)malloc((size_t)(P ? P : 1) * sizeof(uint32_t));
+    uint32_t *cur = (uint32_t *)malloc((size_t)(nkeys + 1) * sizeof(uint32_t));
+    mm_out kd, rd;
+    u32v lists = {0}, lens = {0}, heads = {0}, uni = {0}, rcmd = {0};
+    rc = -1;
+    if (!hoff || !hist || !cur || mmo_init(&kd) || mmo_init(&rd)) goto done;
+
+    /* histories: stable counting sort of registered (key, txn) pairs */
+    for (uint32_t i = 0; i < n; ++i)
+        if (domain_of(s->lsb[i]) == 0 && is_globally_visible(kind_of(s->lsb[i])) == 1)
+            for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) hoff[s->key_ord[p] + 1]++;
+    for (uint32_t k = 0; k < nkeys; ++k) hoff[k + 1] += hoff[k];
+    memcpy(cur, hoff, (size_t)(nkeys + 1) * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n; ++i)
+        if (domain_of(s->lsb[i]) == 0 && is_globally_visible(kind_of(s->lsb[i])) == 1)
+            for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) hist[cur[s->key_ord[p]]++] = i;
+
+    /* range commands in TxnId order */
+    for (uint32_t i = 0; i < n; ++i) if (domain_of(s->lsb[i]) == 1) if (u32v_push(&rcmd, i)) goto done;
+
+    for (uint32_t i = 0; i < n; ++i) {
+        int tk = witnesses_of(kind_of(s->lsb[i]));
+        int64_t applied_before = (int64_t)i - (int64_t)s->window;    /* j < i-W are applied */
+        lists.n = 0; lens.n = 0; heads.n = 0;
+        u32v qkeys = {0};
+        /* keys queried: own keys, or every key inside own ranges (CFKs that exist) */
+        if (domain_of(s->lsb[i]) == 0) {
+            for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) if (u32v_push(&qkeys, s->key_ord[p])) goto done;
+        } else {
+            for (uint32_t r = s->rng_off[i]; r < s->rng_off[i + 1]; ++r)
+                for (uint32_t key = s->rng_start[r] + 1; key <= s->rng_end[r] && key < nkeys; ++key)
+                    if (hoff[key + 1] > hoff[key]) if (u32v_push(&qkeys, key)) goto done;
+        }
+        uint32_t kc = 0;
+        for (uint32_t q = 0; q < qkeys.n; ++q) {
+            uint32_t key = qkeys.p[q];
+            uint32_t a = hoff[key], b = hoff[key + 1];
+            uint32_t lo = a, hi = b;                      /* p = lower_bound(i) */
+            while (lo < hi) { uint32_t m = (lo + hi) / 2; if (hist[m] < i) lo = m + 1; else hi = m; }
+            uint32_t p = lo;
+            uint32_t start = a;
+            if (applied_before > 0) {
+                uint32_t l2 = a, h2 = p;                  /* last entry < i-W */
+                while (l2 < h2) { uint32_t m = (l2 + h2) / 2; if ((int64_t)hist[m] < applied_before) l2 = m + 1; else h2 = m; }
+                long w = (long)l2 - 1;
+                while (w >= (long)a && kind_of(s->lsb[hist[w]]) != K_WRITE) --w;
+                if (w >= (long)a) start = (uint32_t)w;
+            }
+            uint32_t before = (uint32_t)lists.n;
+            for (uint32_t e = start; e < p; ++e)
+                if (kinds_test(tk, kind_of(s->lsb[hist[e]]))) if (u32v_push(&lists, hist[e])) goto done;
+            uint32_t c = (uint32_t)lists.n - before;
+            if (c) { if (u32v_push(&lens, c) || u32v_push(&heads, key)) goto done; ++kc; }
+        }
+        free(qkeys.p);
+        /* KeyDeps: keys = heads, values = sorted union, k2v = header + remapped body */
+        uni.n = 0;
+        for (size_t e = 0; e < lists.n; ++e) if (u32v_push(&uni, lists.p[e])) goto done;
+        qsort(uni.p, uni.n, sizeof(uint32_t), cmp_u32);
+        size_t un = 0;
+        for (size_t e = 0; e < uni.n; ++e) if (un == 0 || uni.p[un - 1] != uni.p[e]) uni.p[un++] = uni.p[e];
+        for (uint32_t q = 0; q < kc; ++q) if (u32v_push(&kd.keys_lo, heads.p[q])) goto done;
+        for (size_t e = 0; e < un; ++e) if (u32v_push(&kd.vals, uni.p[e])) goto done;
+        int32_t off = (int32_t)kc;
+        for (uint32_t q = 0; q < kc; ++q) { off += (int32_t)lens.p[q]; if (i32v_push(&kd.k2v, off)) goto done; }
+        for (size_t e = 0; e < lists.n; ++e) {
+            uint32_t *f = (uint32_t *)bsearch(&lists.p[e], uni.p, un, sizeof(uint32_t), cmp_u32);
+            if (i32v_push(&kd.k2v, (int32_t)(f - uni.p))) goto done;
+        }
+        if (mmo_close_txn(&kd)) goto done;
+
+        /* RangeDeps: live witnessed range commands j in [i-W, i) whose ranges intersect */
+        {
+            mm_builder rb; mmb_init(&rb, NULL);
+            /* collect (range code, txn) pairs then build canonical multimap directly */
+            u32v rlo = {0}, rhi = {0}, rtx = {0};
+            for (size_t c = 0; c < rcmd.n; ++c) {
+                uint32_t j = rcmd.p[c];
+                if (j >= i) break;
+                if ((int64_t)j < applied_before) continue;
+                if (!kinds_test(tk, kind_of(s->lsb[j]))) continue;
+                for (uint32_t a = s->rng_off[j]; a < s->rng_off[j + 1]; ++a) {
+                    uint32_t rs = s->rng_start[a], re = s->rng_end[a];
+                    int hit = 0;
+                    if (domain_of(s->lsb[i]) == 0) {
+                        uint32_t lo = s->key_off[i], hi = s->key_off[i + 1];   /* first key > rs */
+                        while (lo < hi) { uint32_t m = (lo + hi) / 2; if (s->key_ord[m] <= rs) lo = m + 1; else hi = m; }
+                        hit = lo < s->key_off[i + 1] && s->key_ord[lo] <= re;
+                    } else {
+                        for (uint32_t r = s->rng_off[i]; r < s->rng_off[i + 1] && !hit; ++r)
+                            hit = range_intersects_range(rs, re, s->rng_start[r], s->rng_end[r]);
+                    }
+                    if (hit) { if (u32v_push(&rlo, rs) || u32v_push(&rhi, re) || u32v_push(&rtx, j)) goto done; }
+                }
+            }
+            /* ranges sorted by (start,end); values per range are ascending txn (j ascending) */
+            size_t m = rtx.n;
+            uint32_t *ord = (uint32_t *)malloc((m ? m : 1) * sizeof(uint32_t));
+            uint64_t *codes = (uint64_t *)malloc((m ? m : 1) * sizeof(uint64_t));
+            if (!ord || !codes) { free(ord); free(codes); goto done; }
+            for (size_t e = 0; e < m; ++e) codes[e] = ((uint64_t)rlo.p[e] << 32) | rhi.p[e];
+            for (size_t e = 0; e < m; ++e) ord[e] = (uint32_t)e;
+            /* stable insertion by code (m is small) */
+            for (size_t e = 1; e < m; ++e) {
+                uint32_t x = ord[e]; size_t f = e;
+                while (f > 0 && codes[ord[f - 1]] > codes[x]) { ord[f] = ord[f - 1]; --f; }
+                ord[f] = x;
+            }
+            u32v rv = {0};
+            for (size_t e = 0; e < m; ++e) if (u32v_push(&rv, rtx.p[e])) goto done;
+            qsort(rv.p, rv.n, sizeof(uint32_t), cmp_u32);
+            size_t rvn = 0;
+            for (size_t e = 0; e < rv.n; ++e) if (rvn == 0 || rv.p[rvn - 1] != rv.p[e]) rv.p[rvn++] = rv.p[e];
+            size_t nk = 0;
+            for (size_t e = 0; e < m; ++e) if (e == 0 || codes[ord[e]] != codes[ord[e - 1]]) ++nk;
+            size_t hdr = rd.k2v.n;
+            for (size_t e = 0; e < nk; ++e) if (i32v_push(&rd.k2v, 0)) goto done;
+            size_t ki = 0;
+            for (size_t e = 0; e < m; ++e) {
+                if (e == 0 || codes[ord[e]] != codes[ord[e - 1]]) {
+                    if (u32v_push(&rd.keys_lo, rlo.p[ord[e]]) || u32v_push(&rd.keys_hi, rhi.p[ord[e]])) goto done;
+                    if (e > 0) { rd.k2v.p[hdr + ki] = (int32_t)(rd.k2v.n - hdr); ++ki; }
+                }
+                uint32_t *f = (uint32_t *)bsearch(&rtx.p[ord[e]], rv.p, rvn, sizeof(uint32_t), cmp_u32);
+                if (i32v_push(&rd.k2v, (int32_t)(f - rv.p))) goto done;
+            }
+            if (nk) rd.k2v.p[hdr + ki] = (int32_t)(rd.k2v.n - hdr);
+            for (size_t e = 0; e < rvn; ++e) if (u32v_push(&rd.vals, rv.p[e])) goto done;
+            if (mmo_close_txn(&rd)) goto done;
+            free(ord); free(codes); free(rv.p); free(rlo.p); free(rhi.p); free(rtx.p);
+            mmb_free(&rb);
+        }
+    }
+    if (alloc_out(out, &kd, &rd, n)) goto done;
+    rc = 0;
+done:
+    free(hoff); free(hist); free(cur);
+    free(lists.p); free(lens.p); free(heads.p); free(uni.p); free(rcmd.p);
+    mmo_free(&kd); mmo_free(&rd);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Primitive entry points for the restated reference property tests
+ * ------------------------------------------------------------------------------------------ */
+int or_keydeps_build(uint32_t nadds, const uint32_t *keys, const uint32_t *vals,
+                     uint32_t ntbl, const uint64_t *tbl_msb, const uint64_t *tbl_lsb, const int32_t *tbl_node,
+                     or_deps *out)
+{
+    ts_t *tbl = (ts_t *)malloc((size_t)(ntbl ? ntbl : 1) * sizeof(ts_t));
+    if (!tbl) return -1;
+    for (uint32_t i = 0; i < ntbl; ++i) { tbl[i].msb = tbl_msb[i]; tbl[i].lsb = tbl_lsb[i]; tbl[i].node = tbl_node[i]; }
+    mm_builder b; mm_out kd, rd;
+    int rc = -1;
+    mmb_init(&b, tbl);
+    if (mmo_init(&kd) || mmo_init(&rd)) goto done;
+    for (uint32_t a = 0; a < nadds; ++a) if (mmb_add(&b, keys[a], vals[a])) goto done;
+    if (mmb_build(&b, &kd, 0)) goto done;
+    if (mmo_close_txn(&rd)) goto done;
+    if (alloc_out(out, &kd, &rd, 1)) goto done;
+    rc = 0;
+done:
+    mmb_free(&b); mmo_free(&kd); mmo_free(&rd); free(tbl);
+    return rc;
+}
+
+/* linearUnion general path (RelationMultiMap.java:733-801).  The pass-through paths
+ * (:583-730) return one input unchanged only when it already equals the union, so the
+ * value-level result is the general merge's in every case. */
+int or_keydeps_union(const or_deps *x, uint32_t a, const or_deps *y, uint32_t b,
+                     const uint64_t *tbl_msb, const uint64_t *tbl_lsb, const int32_t *tbl_node,
+                     or_deps *out)
+{
+    const uint32_t *lk = x->kd_keys + x->kd_key_off[a], *rk = y->kd_keys + y->kd_key_off[b];
+    uint32_t lkn = x->kd_key_off[a + 1] - x->kd_key_off[a], rkn = y->kd_key_off[b + 1] - y->kd_key_off[b];
+    const uint32_t *lv = x->kd_vals + x->kd_val_off[a], *rv = y->kd_vals + y->kd_val_off[b];
+    uint32_t lvn = x->kd_val_off[a + 1] - x->kd_val_off[a], rvn = y->kd_val_off[b + 1] - y->kd_val_off[b];
+    const int32_t *l = x->kd_k2v + x->kd_k2v_off[a], *r = y->kd_k2v + y->kd_k2v_off[b];
+    mm_out kd, rd;
+    int rc = -1;
+    uint32_t *ov = NULL, *rl = NULL, *rr = NULL;
+    if (mmo_init(&kd) || mmo_init(&rd)) goto done;
+    /* SortedArrays.linearUnion of values (left wins on ties) */
+    ov = (uint32_t *)malloc(((size_t)lvn + rvn + 1) * sizeof(uint32_t));
+    rl = (uint32_t *)malloc(((size_t)lvn + 1) * sizeof(uint32_t));
+    rr = (uint32_t *)malloc(((size_t)rvn + 1) * sizeof(uint32_t));
+    if (!ov || !rl || !rr) goto done;
+    uint32_t i = 0, j = 0, o = 0;
+    while (i < lvn && j < rvn) {
+        int c = or_ts_compare(tbl_msb[lv[i]], tbl_lsb[lv[i]], tbl_node[lv[i]], tbl_msb[rv[j]], tbl_lsb[rv[j]], tbl_node[rv[j]]);
+        if (c == 0) { rl[i++] = o; rr[j++] = o; ov[o++] = lv[i - 1]; }
+        else if (c < 0) { rl[i++] = o; ov[o++] = lv[i - 1]; }
+        else { rr[j++] = o; ov[o++] = rv[j - 1]; }
+    }
+    while (i < lvn) { rl[i++] = o; ov[o++] = lv[i - 1]; }
+    while (j < rvn) { rr[j++] = o; ov[o++] = rv[j - 1]; }
+    for (uint32_t v = 0; v < o; ++v) if (u32v_push(&kd.vals, ov[v])) goto done;
+    /* keys union + per-key union of remapped indices */
+    uint32_t lki = 0, rki = 0, lp = lkn, rp = rkn;
+    u32v okeys = {0};
+    i32v body = {0}; i32v hdr = {0};
+    while (lki < lkn || rki < rkn) {
+        int which = (lki < lkn && rki < rkn) ? (lk[lki] < rk[rki] ? -1 : lk[lki] > rk[rki] ? 1 : 0) : (lki < lkn ? -1 : 1);
+        if (which <= 0 && which != 0) {
+            if (u32v_push(&okeys, lk[lki])) goto done;
+            while (lp < (uint32_t)l[lki]) if (i32v_push(&body, (int32_t)rl[l[lp++]])) goto done;
+            ++lki;
+        } else if (which > 0) {
+            if (u32v_push(&okeys, rk[rki])) goto done;
+            while (rp < (uint32_t)r[rki]) if (i32v_push(&body, (int32_t)rr[r[rp++]])) goto done;
+            ++rki;
+        } else {
+            if (u32v_push(&okeys, lk[lki])) goto done;
+            while (lp < (uint32_t)l[lki] && rp < (uint32_t)r[rki]) {
+                int32_t nl = (int32_t)rl[l[lp]], nr = (int32_t)rr[r[rp]];
+                if (nl <= nr) { if (i32v_push(&body, nl)) goto done; lp++; if (nl == nr) rp++; }
+                else { if (i32v_push(&body, nr)) goto done; rp++; }
+            }
+            while (lp < (uint32_t)l[lki]) if (i32v_push(&body, (int32_t)rl[l[lp++]])) goto done;
+            while (rp < (uint32_t)r[rki]) if (i32v_push(&body, (int32_t)rr[r[rp++]])) goto done;
+            ++lki; ++rki;
+        }
+        if (i32v_push(&hdr, (int32_t)body.n)) goto done;
+    }
+    for (size_t k = 0; k < okeys.n; ++k) if (u32v_push(&kd.keys_lo, okeys.p[k])) goto done;
+    for (size_t k = 0; k < hdr.n; ++k) if (i32v_push(&kd.k2v, hdr.p[k] + (int32_t)okeys.n)) goto done;
+    for (size_t k = 0; k < body.n; ++k) if (i32v_push(&kd.k2v, body.p[k])) goto done;
+    free(okeys.p); free(body.p); free(hdr.p);
+    if (mmo_close_txn(&kd) || mmo_close_txn(&rd)) goto done;
+    if (alloc_out(out, &kd, &rd, 1)) goto done;
+    rc = 0;
+done:
+    free(ov); free(rl); free(rr);
+    mmo_free(&kd); mmo_free(&rd);
+    return rc;
+}
+
+uint32_t or_stab_key(uint32_t nr, const uint32_t *rs, const uint32_t *re, uint32_t key, uint32_t *out)
+{
+    uint32_t c = 0;
+    for (uint32_t i = 0; i < nr; ++i) if (range_intersects_key(rs[i], re[i], key)) out[c++] = i;
+    return c;
+}
+
+/* WaitingOn + levelling under "all STABLE, executeAt = txnId, none
+ * applied" (config 5): Command.WaitingOn.Update (local/Command.java:1426-1437) sets bits
+ * [0, |rangeDeps.txnIds|) for range deps and [R, R + |keyDeps.keys|) for key deps;
+ * Commands.updateWaitingOn (local/Commands.java:755-830) clears none because every dep j < i
+ * executes before i and none is applied.  Level: 0 if no dep executes before, else 1 + max. */
+int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level, uint32_t *wo_off, uint64_t **wo_words)
+{
+    size_t total = 0;
+    wo_off[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t bits = (d->rd_val_off[i + 1] - d->rd_val_off[i]) + (d->kd_key_off[i + 1] - d->kd_key_off[i]);
+        total += (bits + 63) / 64;
+        wo_off[i + 1] = (uint32_t)total;
+    }
+    uint64_t *w = (uint64_t *)calloc(total ? total : 1, sizeof(uint64_t));
+    if (!w) return -1;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t bits = (d->rd_val_off[i + 1] - d->rd_val_off[i]) + (d->kd_key_off[i + 1] - d->kd_key_off[i]);
+        for (uint32_t b = 0; b < bits; ++b) w[wo_off[i] + b / 64] |= 1ULL << (b & 63);
+        uint32_t lv = 0;
+        for (uint32_t v = d->kd_val_off[i]; v < d->kd_val_off[i + 1]; ++v) if (level[d->kd_vals[v]] + 1 > lv) lv = level[d->kd_vals[v]] + 1;
+        for (uint32_t v = d->rd_val_off[i]; v < d->rd_val_off[i + 1]; ++v) if (level[d->rd_vals[v]] + 1 > lv) lv = level[d->rd_vals[v]] + 1;
+        level[i] = lv;
+    }
+    *wo_words = w;
+    return 0;
+}

@@ -1,0 +1,110 @@
+/*
+ * oracle.h -- CPU restatement of the reference (ifesdjeen/cassandra-accord, accord-core)
+ * dependency-calculation hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is linked into, loaded by or called
+ * from the product library (libaccord_deps.so) or its host mirror.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it, and only as the
+ * checker / the timed CPU baseline.
+ *
+ * The reference is 100% Java and there is no JVM in this image, so it can
+ * be neither compiled nor imported: oracle/_ref does not exist.  Parity of this restatement
+ * is pinned by (1) restated reference property tests (KeyDepsTest canonical model,
+ * SearchableRangeListTest brute force, RangeDepsTest) and (2) hand-derived known-answer
+ * tests committed under tests/golden/ whose expected outputs cite the reference lines that
+ * justify them (SURVEY.md §8c list of required KATs).  CFK mapReduceActive has no reference
+ * test of its own (CommandsForKey.java:126 "TODO (required): randomised testing"), so for
+ * that row parity rests on the restatement + KATs.
+ *
+ * Two restatements of the deps calculation are provided:
+ *   - "literal": per-key CommandsForKey objects with sorted TxnInfo[] + committed[] rebuilt on
+ *     every status change (CommandsForKey.java:422-470, 880-944), the linear mapReduceActive
+ *     scan (:614-650), the linear range-command scan (InMemoryCommandStore.java:883-1016) and
+ *     the RelationMultiMap.AbstractBuilder (RelationMultiMap.java:88-271).  This is the
+ *     reference algorithm and is what bench.py times as the CPU baseline ("port").
+ *   - "fast": the same function computed from per-key histories in O(deps) -- used to check
+ *     the GPU at the full benchmark sizes; itself checked against "literal" in tests.
+ */
+#ifndef ACCORD_ORACLE_H
+#define ACCORD_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A seeded transaction stream, SoA, in TxnId order (SURVEY.md §8d "Synthetic stream").
+ * Key txns carry sorted unique key ordinals in key_off/key_ord; range txns carry sorted,
+ * de-overlapped (start,end] ranges in rng_off/rng_start/rng_end (IntKey semantics,
+ * Range.EndInclusive: Range.java:40-88). */
+typedef struct {
+    uint32_t n;
+    const uint64_t *msb;
+    const uint64_t *lsb;
+    const int32_t  *node;
+    const uint32_t *key_off;    /* [n+1] */
+    const uint32_t *key_ord;    /* [key_off[n]] */
+    const uint32_t *rng_off;    /* [n+1] or NULL */
+    const uint32_t *rng_start;  /* [rng_off[n]] */
+    const uint32_t *rng_end;
+    uint32_t window;            /* W of the status-at-time model */
+} or_stream;
+
+/* Per-txn PartialDeps in the exact reference layout (KeyDeps.java:150-187,
+ * RangeDeps.java:81-99): for txn i,
+ *   keys      = kd_keys[kd_key_off[i] .. kd_key_off[i+1])           (sorted unique ordinals)
+ *   txnIds    = kd_vals[kd_val_off[i] .. kd_val_off[i+1])           (indices into the stream)
+ *   keysToTxnIds = kd_k2v[kd_k2v_off[i] .. kd_k2v_off[i+1])         (exact int[] contents)
+ * and likewise for RangeDeps with ranges (rd_rng_start/rd_rng_end). */
+typedef struct {
+    uint32_t n;
+    uint32_t *kd_key_off, *kd_keys, *kd_val_off, *kd_vals, *kd_k2v_off;
+    int32_t  *kd_k2v;
+    uint32_t *rd_rng_off, *rd_rng_start, *rd_rng_end, *rd_val_off, *rd_vals, *rd_r2v_off;
+    int32_t  *rd_r2v;
+} or_deps;
+
+int  or_stream_deps_literal(const or_stream *s, or_deps *out);
+int  or_stream_deps_fast(const or_stream *s, or_deps *out);
+/* literal model restricted to the first `limit` txns (CPU-baseline sample) */
+int  or_stream_deps_literal_prefix(const or_stream *s, uint32_t limit, or_deps *out);
+void or_deps_free(or_deps *d);
+
+/* ---- primitives restated for the reference's own property tests ---- */
+
+/* Timestamp.compareTo (Timestamp.java:208-217) */
+int or_ts_compare(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
+/* Timestamp.equals (Timestamp.java:244-249) */
+int or_ts_equals(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
+
+/* KeyDeps.Builder (RelationMultiMap.AbstractBuilder) fed with `nadds` (key, value) adds in
+ * the given order; values are indices into a TxnId table (tbl_*).  Output is one KeyDeps in
+ * kd_* fields of `out` (n = 1).  Returns 0, or -1 if the builder throws
+ * ("Key ... has been visited more than once", RelationMultiMap.java:236-238). */
+int or_keydeps_build(uint32_t nadds, const uint32_t *keys, const uint32_t *vals,
+                     uint32_t ntbl, const uint64_t *tbl_msb, const uint64_t *tbl_lsb, const int32_t *tbl_node,
+                     or_deps *out);
+
+/* RelationMultiMap.linearUnion for KeyDeps (RelationMultiMap.java:561-816) of txn a of `x`
+ * and txn b of `y` (values are indices into the same table, compared via the table). */
+int or_keydeps_union(const or_deps *x, uint32_t a, const or_deps *y, uint32_t b,
+                     const uint64_t *tbl_msb, const uint64_t *tbl_lsb, const int32_t *tbl_node,
+                     or_deps *out);
+
+/* SearchableRangeList brute-force stabbing oracle (SearchableRangeListTest.java:61-115):
+ * ranges sorted by (start,end); writes the indices of the ranges containing `key`
+ * ((s,e] semantics) in ascending index order; returns the count. */
+uint32_t or_stab_key(uint32_t nr, const uint32_t *rs, const uint32_t *re, uint32_t key, uint32_t *out);
+
+/* WaitingOn levelling over the deps of a stream whose executeAt ==
+ * txnId and none applied: level[i] = 0 if no dep executes before i, else 1 + max level(dep).
+ * Also writes the WaitingOn bitset words (Command.java:1426-1437: range-dep txn bits then
+ * keyDeps key bits) into wo_words at wo_off[i] (in 64-bit words). */
+int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level,
+                  uint32_t *wo_off /* [n+1] */, uint64_t **wo_words /* malloc'd */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,221 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ (as the checker), __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from accord_amd import PartialDeps, Stream
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(_ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+
+_u32p = C.POINTER(C.c_uint32)
+_i32p = C.POINTER(C.c_int32)
+_u64p = C.POINTER(C.c_uint64)
+
+
+class _OrStream(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("msb", _u64p), ("lsb", _u64p), ("node", _i32p),
+                ("key_off", _u32p), ("key_ord", _u32p), ("rng_off", _u32p), ("rng_start", _u32p),
+                ("rng_end", _u32p), ("window", C.c_uint32)]
+
+
+class _OrDeps(C.Structure):
+    _fields_ = [("n", C.c_uint32),
+                ("kd_key_off", _u32p), ("kd_keys", _u32p), ("kd_val_off", _u32p), ("kd_vals", _u32p),
+                ("kd_k2v_off", _u32p), ("kd_k2v", _i32p),
+                ("rd_rng_off", _u32p), ("rd_rng_start", _u32p), ("rd_rng_end", _u32p), ("rd_val_off", _u32p),
+                ("rd_vals", _u32p), ("rd_r2v_off", _u32p), ("rd_r2v", _i32p)]
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+        L = C.CDLL(ORACLE_SO)
+        L.or_stream_deps_literal.argtypes = [C.POINTER(_OrStream), C.POINTER(_OrDeps)]
+        L.or_stream_deps_fast.argtypes = [C.POINTER(_OrStream), C.POINTER(_OrDeps)]
+        L.or_stream_deps_literal_prefix.argtypes = [C.POINTER(_OrStream), C.c_uint32, C.POINTER(_OrDeps)]
+        L.or_deps_free.argtypes = [C.POINTER(_OrDeps)]
+        L.or_deps_free.restype = None
+        L.or_ts_compare.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
+        L.or_ts_equals.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
+        L.or_keydeps_build.argtypes = [C.c_uint32, _u32p, _u32p, C.c_uint32, _u64p, _u64p, _i32p,
+                                       C.POINTER(_OrDeps)]
+        L.or_keydeps_union.argtypes = [C.POINTER(_OrDeps), C.c_uint32, C.POINTER(_OrDeps), C.c_uint32,
+                                       _u64p, _u64p, _i32p, C.POINTER(_OrDeps)]
+        L.or_stab_key.argtypes = [C.c_uint32, _u32p, _u32p, C.c_uint32, _u32p]
+        L.or_stab_key.restype = C.c_uint32
+        L.or_waiting_on.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p, _u32p, C.POINTER(_u64p)]
+        _LIB = L
+    return _LIB
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+
+def _to_partial(d: _OrDeps) -> PartialDeps:
+    n = d.n
+    kw = {}
+    for f in ("kd_key_off", "kd_val_off", "kd_k2v_off", "rd_rng_off", "rd_val_off", "rd_r2v_off"):
+        kw[f] = _arr(getattr(d, f), n + 1, np.uint32)
+    kw["kd_keys"] = _arr(d.kd_keys, int(kw["kd_key_off"][-1]), np.uint32)
+    kw["kd_vals"] = _arr(d.kd_vals, int(kw["kd_val_off"][-1]), np.uint32)
+    kw["kd_k2v"] = _arr(d.kd_k2v, int(kw["kd_k2v_off"][-1]), np.int32)
+    R = int(kw["rd_rng_off"][-1])
+    kw["rd_rng_start"] = _arr(d.rd_rng_start, R, np.uint32)
+    kw["rd_rng_end"] = _arr(d.rd_rng_end, R, np.uint32)
+    kw["rd_vals"] = _arr(d.rd_vals, int(kw["rd_val_off"][-1]), np.uint32)
+    kw["rd_r2v"] = _arr(d.rd_r2v, int(kw["rd_r2v_off"][-1]), np.int32)
+    return PartialDeps(**kw)
+
+
+def _or_stream(s: Stream, window: int):
+    keep = [np.ascontiguousarray(a) for a in (s.msb, s.lsb, s.node, s.key_off, s.key_ord, s.rng_off,
+                                              s.rng_start, s.rng_end)]
+    msb, lsb, node, ko, kord, ro, rs, re = keep
+    o = _OrStream()
+    o.n = s.n
+    o.msb = msb.ctypes.data_as(_u64p)
+    o.lsb = lsb.ctypes.data_as(_u64p)
+    o.node = node.ctypes.data_as(_i32p)
+    o.key_off = ko.ctypes.data_as(_u32p)
+    o.key_ord = kord.ctypes.data_as(_u32p)
+    o.rng_off = ro.ctypes.data_as(_u32p)
+    o.rng_start = rs.ctypes.data_as(_u32p)
+    o.rng_end = re.ctypes.data_as(_u32p)
+    o.window = window
+    return o, keep
+
+
+class OracleError(RuntimeError):
+    def __init__(self, rc):
+        super().__init__(f"oracle rc={rc}")
+        self.rc = rc
+
+
+def deps_literal(s: Stream, window: int, limit: int | None = None) -> PartialDeps:
+    o, keep = _or_stream(s, window)
+    d = _OrDeps()
+    if limit is None:
+        rc = lib().or_stream_deps_literal(C.byref(o), C.byref(d))
+    else:
+        rc = lib().or_stream_deps_literal_prefix(C.byref(o), limit, C.byref(d))
+    if rc != 0:
+        raise OracleError(rc)
+    try:
+        return _to_partial(d)
+    finally:
+        lib().or_deps_free(C.byref(d))
+
+
+def deps_fast(s: Stream, window: int) -> PartialDeps:
+    o, keep = _or_stream(s, window)
+    d = _OrDeps()
+    rc = lib().or_stream_deps_fast(C.byref(o), C.byref(d))
+    if rc != 0:
+        raise OracleError(rc)
+    try:
+        return _to_partial(d)
+    finally:
+        lib().or_deps_free(C.byref(d))
+
+
+def ts_compare(a, b) -> int:
+    return lib().or_ts_compare(a[0], a[1], a[2], b[0], b[1], b[2])
+
+
+def ts_equals(a, b) -> bool:
+    return bool(lib().or_ts_equals(a[0], a[1], a[2], b[0], b[1], b[2]))
+
+
+def keydeps_build(keys, vals, tbl_msb, tbl_lsb, tbl_node):
+    """KeyDeps.Builder over (key, value-index) adds; returns (keys, vals, k2v) or None on throw."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint32)
+    vals = np.ascontiguousarray(vals, dtype=np.uint32)
+    tm = np.ascontiguousarray(tbl_msb, dtype=np.uint64)
+    tl = np.ascontiguousarray(tbl_lsb, dtype=np.uint64)
+    tn = np.ascontiguousarray(tbl_node, dtype=np.int32)
+    d = _OrDeps()
+    rc = lib().or_keydeps_build(len(keys), keys.ctypes.data_as(_u32p), vals.ctypes.data_as(_u32p), len(tm),
+                                tm.ctypes.data_as(_u64p), tl.ctypes.data_as(_u64p), tn.ctypes.data_as(_i32p),
+                                C.byref(d))
+    if rc != 0:
+        return None
+    try:
+        return _to_partial(d).key_deps(0)
+    finally:
+        lib().or_deps_free(C.byref(d))
+
+
+def _single(keys, vals, k2v) -> PartialDeps:
+    z = np.zeros(2, dtype=np.uint32)
+    return PartialDeps(np.array([0, len(keys)], np.uint32), np.asarray(keys, np.uint32),
+                       np.array([0, len(vals)], np.uint32), np.asarray(vals, np.uint32),
+                       np.array([0, len(k2v)], np.uint32), np.asarray(k2v, np.int32),
+                       z.copy(), np.zeros(0, np.uint32), np.zeros(0, np.uint32), z.copy(), np.zeros(0, np.uint32),
+                       z.copy(), np.zeros(0, np.int32))
+
+
+def _c_deps(p: PartialDeps):
+    keep = [np.ascontiguousarray(getattr(p, f)) for f in PartialDeps.FIELDS]
+    d = _OrDeps()
+    d.n = p.n
+    for f, a in zip(PartialDeps.FIELDS, keep):
+        setattr(d, f, a.ctypes.data_as(_i32p if a.dtype == np.int32 else _u32p))
+    return d, keep
+
+
+def keydeps_union(a, b, tbl_msb, tbl_lsb, tbl_node):
+    """RelationMultiMap.linearUnion of two (keys, vals, k2v) KeyDeps."""
+    x, kx = _c_deps(_single(*a))
+    y, ky = _c_deps(_single(*b))
+    tm = np.ascontiguousarray(tbl_msb, dtype=np.uint64)
+    tl = np.ascontiguousarray(tbl_lsb, dtype=np.uint64)
+    tn = np.ascontiguousarray(tbl_node, dtype=np.int32)
+    d = _OrDeps()
+    rc = lib().or_keydeps_union(C.byref(x), 0, C.byref(y), 0, tm.ctypes.data_as(_u64p), tl.ctypes.data_as(_u64p),
+                                tn.ctypes.data_as(_i32p), C.byref(d))
+    if rc != 0:
+        raise OracleError(rc)
+    try:
+        return _to_partial(d).key_deps(0)
+    finally:
+        lib().or_deps_free(C.byref(d))
+
+
+def stab_key(starts, ends, key):
+    rs = np.ascontiguousarray(starts, dtype=np.uint32)
+    re = np.ascontiguousarray(ends, dtype=np.uint32)
+    out = np.zeros(max(1, len(rs)), dtype=np.uint32)
+    c = lib().or_stab_key(len(rs), rs.ctypes.data_as(_u32p), re.ctypes.data_as(_u32p), key, out.ctypes.data_as(_u32p))
+    return out[:c].copy()
+
+
+def waiting_on(p: PartialDeps):
+    d, keep = _c_deps(p)
+    n = p.n
+    level = np.zeros(max(1, n), dtype=np.uint32)
+    wo_off = np.zeros(n + 1, dtype=np.uint32)
+    words = _u64p()
+    rc = lib().or_waiting_on(C.byref(d), n, level.ctypes.data_as(_u32p), wo_off.ctypes.data_as(_u32p),
+                             C.byref(words))
+    if rc != 0:
+        raise OracleError(rc)
+    w = _arr(words, int(wo_off[-1]), np.uint64)
+    C.CDLL(None).free(words)
+    return level[:n].copy(), wo_off, w
