@@ -68,7 +68,8 @@ template <typename T> T *dup(const std::vector<T> &v) {
 
 extern "C" int32_t accord_workload_generate(const accord_workload_cfg *cfg, accord_batch *out)
 {
-    if (!cfg || !out || cfg->keyspace < 2 || cfg->keys_per_txn > cfg->keyspace || cfg->node_mod == 0)
+    if (!cfg || !out || cfg->keyspace < 1 || cfg->keys_per_txn > cfg->keyspace || cfg->node_mod == 0 ||
+        (cfg->range_frac > 0 && cfg->keyspace < 2))
         return ACCORD_ERR_ARG;
     std::memset(out, 0, sizeof(*out));
     const uint32_t n = cfg->n, ks = cfg->keyspace;

@@ -1,0 +1,99 @@
+"""The oracle's stream restatements: hand-derived KATs, literal == fast on seeded streams, and the
+committed golden regression vector."""
+import os
+
+import numpy as np
+import pytest
+
+from accord_amd import generate_stream, keydeps_str, rangedeps_str, Stream
+import oracle_lib as O
+from kat_util import GOLDEN, kat_stream, load_kats
+
+KATS = load_kats()
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+@pytest.mark.parametrize("impl", ["literal", "fast"])
+def test_kats(kat, impl):
+    s = kat_stream(kat)
+    fn = O.deps_literal if impl == "literal" else O.deps_fast
+    if "expect_error" in kat:
+        with pytest.raises(O.OracleError) as e:
+            fn(s, kat["window"])
+        assert e.value.rc == -2
+        return
+    d = fn(s, kat["window"])
+    got_key = [keydeps_str(*d.key_deps(i), s) for i in range(s.n)]
+    assert got_key == kat["expect_key"]
+    if "expect_range" in kat:
+        got_rng = [rangedeps_str(*d.range_deps(i), s) for i in range(s.n)]
+        assert got_rng == kat["expect_range"]
+
+
+CONFIGS = [
+    # n, k, keyspace, zipf, write_frac, window, seed, range_frac, range_len
+    (2000, 4, 200, 0.0, 0.5, 16, 1, 0.0, 0),
+    (3000, 8, 1000, 0.99, 0.5, 64, 2, 0.0, 0),
+    (2000, 3, 50, 0.99, 0.1, 8, 3, 0.0, 0),
+    (1500, 2, 30, 0.0, 0.9, 0, 4, 0.0, 0),
+    (4000, 8, 5000, 0.99, 0.5, 256, 5, 0.0, 0),
+    (1500, 4, 300, 0.0, 0.5, 16, 6, 0.2, 30),
+    (2000, 8, 1000, 0.99, 0.5, 64, 7, 0.2, 100),
+    (1000, 3, 60, 0.99, 0.3, 8, 8, 0.5, 10),
+    (3000, 8, 2000, 0.99, 0.5, 256, 9, 0.2, 1000),
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_literal_equals_fast(cfg):
+    n, k, ks, z, wf, W, seed, rf, rl = cfg
+    s = generate_stream(n, k, ks, z, wf, range_frac=rf, range_len_max=max(rl, 1), seed=seed)
+    a = O.deps_literal(s, W)
+    b = O.deps_fast(s, W)
+    assert a.first_difference(b) is None
+
+
+def test_literal_equals_fast_all_kinds():
+    s = generate_stream(2500, 3, 40, 0.0, 0.5, seed=13)
+    rng = np.random.default_rng(5)
+    kinds = rng.choice([0, 1, 2, 3, 4], size=s.n, p=[0.35, 0.35, 0.1, 0.1, 0.1]).astype(np.uint64)
+    lsb = (s.lsb & ~np.uint64(0xE)) | (kinds << np.uint64(1))
+    s2 = Stream(s.msb, lsb, s.node, s.key_off, s.key_ord, s.rng_off, s.rng_start, s.rng_end)
+    for W in (0, 7, 32):
+        assert O.deps_literal(s2, W).first_difference(O.deps_fast(s2, W)) is None
+
+
+def test_literal_prefix_matches_full_prefix():
+    s = generate_stream(3000, 8, 1000, 0.99, 0.5, seed=2)
+    a = O.deps_literal(s, 64, limit=1000)
+    b = O.deps_fast(s.prefix(1000), 64)
+    assert a.first_difference(b) is None
+
+
+def test_local_only_rejected():
+    s = generate_stream(50, 2, 10, seed=3)
+    lsb = s.lsb.copy()
+    lsb[7] = (lsb[7] & ~np.uint64(0xE)) | np.uint64(5 << 1)
+    bad = Stream(s.msb, lsb, s.node, s.key_off, s.key_ord, s.rng_off, s.rng_start, s.rng_end)
+    for fn in (O.deps_literal, O.deps_fast):
+        with pytest.raises(O.OracleError):
+            fn(bad, 8)
+
+
+def test_golden_vector():
+    path = os.path.join(GOLDEN, "stream_small.npz")
+    g = np.load(path)
+    s = Stream(*(g[f] for f in ("msb", "lsb", "node", "key_off", "key_ord", "rng_off", "rng_start", "rng_end")))
+    d = O.deps_literal(s, int(g["window"]))
+    for f in d.FIELDS:
+        assert np.array_equal(getattr(d, f), g["out_" + f]), f
+
+
+def test_waiting_on_levels_small():
+    # chain on one key, all writes: level(i) = i (each depends on all earlier, W large)
+    s = generate_stream(50, 1, 1, 0.0, 1.0, seed=1)
+    d = O.deps_fast(s, 1000)
+    level, wo_off, words = O.waiting_on(d)
+    assert list(level) == list(range(50))
+    # one bit per keyDeps key (one key) for every txn with deps
+    assert int(wo_off[-1]) == 49
