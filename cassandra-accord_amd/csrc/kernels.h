@@ -33,10 +33,8 @@ struct KeyDepsParams {
     const uint32_t *key_off, *key_ord;
     uint32_t key_lo, key_hi;
     uint32_t window;
-    // history
-    const uint32_t *hist;        // sorted entries (kind<<29 | txn)
-    const uint32_t *seg_start;   // [nkeys]
-    const uint32_t *seg_end;     // [nkeys]
+    const uint32_t *hist;              // key-major history entries (kind<<29 | txn)
+    const unsigned long long *poslo;   // txn-major per pair: (slice start << 32) | history position
     // count outputs
     uint32_t *cnt_keys, *cnt_vals, *cnt_k2v;
     // fill inputs/outputs
@@ -46,11 +44,16 @@ struct KeyDepsParams {
     DevStatus *status;
 };
 
+// txn-major validation + (key, entry) pair packing
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
-                          uint32_t *pair_key, uint32_t *pair_val, DevStatus *status, hipStream_t s);
-void launch_segments(uint32_t P, const uint32_t *sorted_keys, uint32_t *seg_start, uint32_t *seg_end, hipStream_t s);
+                          uint32_t *pair_key, uint32_t *pair_ent, DevStatus *status, hipStream_t s);
+size_t history_temp_bytes(uint32_t P);
+// key-major: history entries, segments, and per pair the [lo, pos) deps slice (txn-major poslo)
+void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
+                    const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
+                    uint32_t *seg_end, unsigned long long *poslo, void *temp, hipStream_t s);
 void launch_keydeps_count(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
 

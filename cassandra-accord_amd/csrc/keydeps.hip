@@ -38,45 +38,194 @@ __device__ __forceinline__ void record_error(DevStatus *st, uint32_t i, int32_t 
     atomicMin(&st->first, v);
 }
 
+// Txn-major validation and pair packing.  One wave owns 64 consecutive txns; the pairs of those
+// txns are then streamed 64 at a time (coalesced) and each lane finds its owner txn with a
+// shuffle binary search over the wave's key offsets.
 __global__ __launch_bounds__(256) void validate_pack_kernel(
     uint32_t n, const uint64_t *__restrict__ msb, const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
     const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ key_ord, const uint32_t *__restrict__ rng_off,
     const uint32_t *__restrict__ rng_start, const uint32_t *__restrict__ rng_end, uint32_t key_lo, uint32_t key_hi,
-    uint32_t *__restrict__ pair_key, uint32_t *__restrict__ pair_val, DevStatus *st)
+    uint32_t *__restrict__ pair_key, uint32_t *__restrict__ pair_ent, DevStatus *st)
 {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint64_t l = lsb[i];
-        const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
-        if (witness_mask(kind) == 0) record_error(st, i, ACCORD_ERR_KIND);
-        if (i > 0 && ts_cmp(msb[i - 1], lsb[i - 1], node[i - 1], msb[i], l, node[i]) >= 0)
-            record_error(st, i, ACCORD_ERR_UNSORTED);
-        const uint32_t k0 = key_off[i], k1 = key_off[i + 1];
-        const uint32_t r0 = rng_off ? rng_off[i] : 0, r1 = rng_off ? rng_off[i + 1] : 0;
-        if (k1 < k0 || r1 < r0) { record_error(st, i, ACCORD_ERR_ARG); continue; }
-        if ((domain == 1 && k1 != k0) || (domain == 0 && r1 != r0)) record_error(st, i, ACCORD_ERR_DOMAIN);
-        uint32_t prev = 0;
-        for (uint32_t p = k0; p < k1; ++p) {
-            const uint32_t key = key_ord[p];
-            const bool in_range = key >= key_lo && key < key_hi;
-            if ((p > k0 && key <= prev) || !in_range) record_error(st, i, ACCORD_ERR_KEYS);
-            prev = key;
-            pair_key[p] = in_range ? key - key_lo : 0u;      // keep the pipeline in bounds on error
-            pair_val[p] = (kind << ENT_KIND_SHIFT) | i;
+    const uint32_t lane = lane_id();
+    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t t0 = gw * 64; t0 < n; t0 += nw * 64) {
+        const uint32_t t = t0 + lane;
+        const bool valid = t < n;
+        const uint32_t cnt = min(64u, n - t0);
+        uint32_t ko = key_off[min(t, n)];
+        uint32_t ent = 0;
+        if (valid) {
+            const uint64_t l = lsb[t];
+            const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
+            ent = (kind << ENT_KIND_SHIFT) | t;
+            if (witness_mask(kind) == 0) record_error(st, t, ACCORD_ERR_KIND);
+            if (t > 0 && ts_cmp(msb[t - 1], lsb[t - 1], node[t - 1], msb[t], l, node[t]) >= 0)
+                record_error(st, t, ACCORD_ERR_UNSORTED);
+            const uint32_t k1 = key_off[t + 1];
+            const uint32_t r0 = rng_off ? rng_off[t] : 0, r1 = rng_off ? rng_off[t + 1] : 0;
+            if ((domain == 1 && k1 != ko) || (domain == 0 && r1 != r0)) record_error(st, t, ACCORD_ERR_DOMAIN);
+            if (rng_start)
+                for (uint32_t r = r0; r < r1; ++r)
+                    if (rng_start[r] >= rng_end[r] || (r > r0 && rng_end[r - 1] > rng_start[r]))
+                        record_error(st, t, ACCORD_ERR_RANGES);
         }
-        for (uint32_t r = r0; r < r1; ++r) {
-            if (rng_start[r] >= rng_end[r] || (r > r0 && rng_end[r - 1] > rng_start[r]))
-                record_error(st, i, ACCORD_ERR_RANGES);
+        const uint32_t pbase = __shfl(ko, 0, 64);
+        const uint32_t pend = key_off[t0 + cnt];
+        for (uint32_t p0 = pbase; p0 < pend; p0 += 64) {
+            const uint32_t p = p0 + lane;
+            uint32_t j = 0;                          // largest lane j < cnt with ko_j <= p
+#pragma unroll
+            for (uint32_t step = 32; step >= 1; step >>= 1) {
+                const uint32_t c = j + step;
+                const uint32_t kc = __shfl(ko, (int)(c & 63), 64);
+                if (c < cnt && kc <= p) j = c;
+            }
+            const uint32_t e = __shfl(ent, (int)j, 64);
+            const uint32_t kj = __shfl(ko, (int)j, 64);
+            if (p < pend) {
+                const uint32_t key = key_ord[p];
+                const bool in_range = key >= key_lo && key < key_hi;
+                if (!in_range || (p > kj && key_ord[p - 1] >= key)) record_error(st, t0 + j, ACCORD_ERR_KEYS);
+                pair_key[p] = in_range ? key - key_lo : 0u;      // keep the pipeline in bounds on error
+                pair_ent[p] = e;
+            }
         }
     }
 }
 
-__global__ __launch_bounds__(256) void segments_kernel(uint32_t P, const uint32_t *__restrict__ keys,
-                                                       uint32_t *__restrict__ seg_start, uint32_t *__restrict__ seg_end)
+// ---- history annotation (key-major) ----
+constexpr int HS_THREADS = 256;
+constexpr int HS_ITEMS = 16;
+constexpr uint32_t HS_TILE = HS_THREADS * HS_ITEMS;
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (l >= (uint32_t)d) v = max(v, t);
+    }
+    return v;
+}
+
+// hist[p] = entry of sorted pair p; segment bounds per key; tile-local inclusive max-scan of
+// (p+1 if entry p is a Write) -> the last Write at or before p, completed by a tile carry.
+__global__ __launch_bounds__(HS_THREADS) void history1_kernel(uint32_t P, const uint32_t *__restrict__ sorted_key,
+                                                              const uint32_t *__restrict__ sorted_pair,
+                                                              const uint32_t *__restrict__ pair_ent,
+                                                              uint32_t *__restrict__ hist, uint32_t *__restrict__ seg_start,
+                                                              uint32_t *__restrict__ seg_end, uint32_t *__restrict__ pw_local,
+                                                              uint32_t *__restrict__ tile_max)
+{
+    __shared__ uint32_t tile[HS_TILE];
+    __shared__ uint32_t wmax[HS_THREADS / 64];
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * HS_TILE;
+#pragma unroll 4
+    for (int j = 0; j < HS_ITEMS; ++j) {
+        const uint32_t p = base + j * HS_THREADS + tid;
+        uint32_t v = 0;
+        if (p < P) {
+            const uint32_t e = pair_ent[sorted_pair[p]];
+            hist[p] = e;
+            const uint32_t k = sorted_key[p];
+            if (p == 0 || sorted_key[p - 1] != k) seg_start[k] = p;
+            if (p == P - 1 || sorted_key[p + 1] != k) seg_end[k] = p + 1;
+            v = (e >> ENT_KIND_SHIFT) == 1u ? p + 1 : 0u;
+        }
+        tile[j * HS_THREADS + tid] = v;
+    }
+    __syncthreads();
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < HS_ITEMS; ++j) run = max(run, tile[tid * HS_ITEMS + j]);
+    const uint32_t incl = wave_incl_max(run);
+    if (lane_id() == 63) wmax[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t ex = __shfl_up(incl, 1, 64);
+    if (lane_id() == 0) ex = 0;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) ex = max(ex, wmax[w]);
+#pragma unroll
+    for (int j = 0; j < HS_ITEMS; ++j) {
+        ex = max(ex, tile[tid * HS_ITEMS + j]);
+        tile[tid * HS_ITEMS + j] = ex;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < HS_ITEMS; ++j) {
+        const uint32_t p = base + j * HS_THREADS + tid;
+        if (p < P) pw_local[p] = tile[j * HS_THREADS + tid];
+    }
+    if (tid == 0) {
+        uint32_t m = 0;
+        for (uint32_t w = 0; w < HS_THREADS / 64; ++w) m = max(m, wmax[w]);
+        tile_max[blockIdx.x] = m;
+    }
+}
+
+// exclusive max-scan of the tile maxima (one block)
+__global__ __launch_bounds__(256) void history_carry_kernel(uint32_t *__restrict__ tile_max, uint32_t tiles)
+{
+    __shared__ uint32_t wmax[4];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < tiles; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < tiles ? tile_max[i] : 0u;
+        const uint32_t incl = wave_incl_max(v);
+        if (lane_id() == 63) wmax[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t ex = __shfl_up(incl, 1, 64);
+        if (lane_id() == 0) ex = 0;
+        uint32_t blk = 0;
+        for (uint32_t w = 0; w < 4; ++w) {
+            if (w < (threadIdx.x >> 6)) ex = max(ex, wmax[w]);
+            blk = max(blk, wmax[w]);
+        }
+        if (i < tiles) tile_max[i] = max(carry, ex);
+        carry = max(carry, blk);
+        __syncthreads();
+    }
+}
+
+// Per history entry p (txn i on key k): the deps slice [lo, p) of (i, k) under the status-at-time
+// model.  lo = the last Write entry j < i-W of the segment (committed[] bound of
+// CommandsForKey.mapReduceActive :620-645), else the segment start.  Written txn-major.
+__global__ __launch_bounds__(256) void history2_kernel(uint32_t P, uint32_t window, const uint32_t *__restrict__ sorted_key,
+                                                       const uint32_t *__restrict__ sorted_pair,
+                                                       const uint32_t *__restrict__ hist,
+                                                       const uint32_t *__restrict__ seg_start,
+                                                       const uint32_t *__restrict__ pw_local,
+                                                       const uint32_t *__restrict__ carry,
+                                                       unsigned long long *__restrict__ poslo)
 {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-        const uint32_t k = keys[p];
-        if (p == 0 || keys[p - 1] != k) seg_start[k] = p;
-        if (p == P - 1 || keys[p + 1] != k) seg_end[k] = p + 1;
+        const uint32_t i = hist[p] & ENT_TXN_MASK;
+        const uint32_t a = seg_start[sorted_key[p]];
+        uint32_t lo = a;
+        if (i > window) {
+            const uint32_t thr = i - window;
+            // exponential search backwards for the first q in [a, p] with txn >= thr
+            uint32_t hi = p, lb = a, step = 1;
+            while (hi > a) {
+                const uint32_t probe = (hi - a > step) ? hi - step : a;
+                if ((hist[probe] & ENT_TXN_MASK) < thr) { lb = probe + 1; break; }
+                hi = probe;
+                step <<= 1;
+            }
+            uint32_t l = lb, h = hi;
+            while (l < h) {
+                const uint32_t m = (l + h) >> 1;
+                if ((hist[m] & ENT_TXN_MASK) < thr) l = m + 1; else h = m;
+            }
+            if (l > a) {
+                const uint32_t x = l - 1;
+                const uint32_t pw = max(pw_local[x], carry[x / HS_TILE]);   // (last Write <= x) + 1
+                if (pw > a) lo = pw - 1;
+            }
+        }
+        poslo[sorted_pair[p]] = ((unsigned long long)lo << 32) | p;
     }
 }
 
@@ -94,6 +243,43 @@ struct WaveLds {
     uint32_t pad[3];
 };
 
+// Candidates per lane per batch: one batch covers 64*KD_CB raw history entries with a single
+// round trip to memory (loads are issued before any is consumed).
+constexpr int KD_CB = 8;
+
+struct TxnMeta {
+    uint32_t k0, k1;
+    uint64_t lsb;
+};
+
+__device__ __forceinline__ TxnMeta load_meta(const KeyDepsParams &p, uint32_t i)
+{
+    TxnMeta m{0u, 0u, 0ull};
+    if (i < p.n) { m.k0 = p.key_off[i]; m.k1 = p.key_off[i + 1]; m.lsb = p.lsb[i]; }
+    return m;
+}
+
+template <int WPL>
+__device__ __forceinline__ void load_batch(const KeyDepsParams &p, const WaveLds<WPL> &L, uint32_t r0, uint32_t raw_total,
+                                           uint32_t (&e)[KD_CB], uint32_t (&sl)[KD_CB], uint32_t lane)
+{
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < KD_CB; ++c) {
+        const uint32_t r = r0 + c * 64 + lane;
+        e[c] = 0xFFFFFFFFu;               // sentinel: kind 7 is never witnessed
+        sl[c] = s;
+        if (r < raw_total) {
+            while (L.slot_rawbase[s + 1] <= r) ++s;
+            sl[c] = s;
+            e[c] = p.hist[L.slot_lo[s] + (r - L.slot_rawbase[s])];
+        }
+    }
+}
+
+// One wave builds one txn's KeyDeps.  Per txn the wave needs ONE memory round trip for its
+// candidates: the next txn's history slices (poslo) and the one after's offsets are prefetched
+// while the current txn is processed (vmcnt retires in order, so they ride with it).
 template <int WPL, bool FILL>
 __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
 {
@@ -102,11 +288,26 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
     WaveLds<WPL> &L = lds_all[w];
     const uint64_t lt = lanemask_lt();
     constexpr uint32_t SPAN = 64u * 64u * WPL;
+    const uint32_t S = gridDim.x * KD_WAVES;
 
-    for (uint32_t i = blockIdx.x * KD_WAVES + w; i < p.n; i += gridDim.x * KD_WAVES) {
-        const uint64_t lsb_i = p.lsb[i];
-        const uint32_t wmask = witness_mask((uint32_t)(lsb_i >> 1) & 7);
-        const uint32_t k0 = p.key_off[i], k = p.key_off[i + 1] - k0;
+    uint32_t i = blockIdx.x * KD_WAVES + w;
+    TxnMeta m0 = load_meta(p, i);
+    TxnMeta m1 = load_meta(p, i + S);
+    unsigned long long pl0 = 0;
+    if (i < p.n && lane < m0.k1 - m0.k0 && lane < KD_KCAP) pl0 = p.poslo[m0.k0 + lane];
+
+    for (; i < p.n; i += S) {
+        // ---- prefetch: offsets two txns ahead, history slices one txn ahead ----
+        const TxnMeta m2 = load_meta(p, i + 2 * S);
+        unsigned long long pl1 = 0;
+        if (i + S < p.n && lane < m1.k1 - m1.k0 && lane < KD_KCAP) pl1 = p.poslo[m1.k0 + lane];
+        const uint32_t k0 = m0.k0, k = m0.k1 - m0.k0;
+        const uint32_t wmask = witness_mask((uint32_t)(m0.lsb >> 1) & 7);
+        uint32_t my_key = 0;
+        if (FILL && lane < k && k <= KD_KCAP) my_key = p.key_ord[k0 + lane];
+        const unsigned long long pl = pl0;
+        m0 = m1; m1 = m2; pl0 = pl1;
+
         if (k > KD_KCAP) {
             if (!FILL && lane == 0) {
                 atomicAdd(&p.status->overflow, 1u);
@@ -116,33 +317,12 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
             continue;
         }
 
-        // ---- slots: segment of each key, [lo, pos) ----
+        // ---- slots: the deps slice [lo, pos) of each key, from the history annotation ----
         uint32_t raw = 0;
         if (lane < k) {
-            const uint32_t key = p.key_ord[k0 + lane] - p.key_lo;
-            const bool in_range = key < p.key_hi - p.key_lo;  // out-of-range keys fail validation
-            const uint32_t a = in_range ? p.seg_start[key] : 0u, b = in_range ? p.seg_end[key] : 0u;
-            uint32_t lo = a, hi = b;                       // pos = first entry with txn >= i
-            while (lo < hi) {
-                uint32_t m = (lo + hi) >> 1;
-                if ((p.hist[m] & ENT_TXN_MASK) < i) lo = m + 1; else hi = m;
-            }
-            const uint32_t pos = lo;
-            uint32_t start = a;
-            if (i > p.window) {                            // j < i-W are APPLIED
-                const uint32_t ab = i - p.window;
-                uint32_t l2 = a, h2 = pos;
-                while (l2 < h2) {
-                    uint32_t m = (l2 + h2) >> 1;
-                    if ((p.hist[m] & ENT_TXN_MASK) < ab) l2 = m + 1; else h2 = m;
-                }
-                int64_t q = (int64_t)l2 - 1;               // last applied entry; walk back to a Write
-                while (q >= (int64_t)a && (p.hist[q] >> ENT_KIND_SHIFT) != 1u) --q;
-                if (q >= (int64_t)a) start = (uint32_t)q;
-            }
+            const uint32_t pos = (uint32_t)pl, start = (uint32_t)(pl >> 32);
             raw = pos - start;
             L.slot_lo[lane] = start;
-            L.slot_key[lane] = key;
             L.slot_ne[lane] = 0;
         }
         const uint32_t incl = wave_incl_scan(raw);
@@ -153,18 +333,20 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
         if (lane == 0) { L.far_count = 0; L.slot_rawbase[k] = raw_total; }
         wave_lds_sync();
 
-        // ---- phase 1: witness filter, near bitmap / far list ----
+        // ---- phase 1: witness filter -> near bitmap / far list ----
         const int64_t base = (int64_t)i - (int64_t)SPAN;
+        const bool one_batch = raw_total <= 64u * KD_CB;
+        uint32_t e[KD_CB], sl[KD_CB];
         uint32_t witnessed_here = 0;
-        {
-            uint32_t s = 0;
-            for (uint32_t r = lane; r < raw_total; r += 64) {
-                while (L.slot_rawbase[s + 1] <= r) ++s;
-                const uint32_t e = p.hist[L.slot_lo[s] + (r - L.slot_rawbase[s])];
-                const uint32_t j = e & ENT_TXN_MASK;
-                if ((wmask >> (e >> ENT_KIND_SHIFT)) & 1u) {
+        for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
+            load_batch<WPL>(p, L, r0, raw_total, e, sl, lane);
+#pragma unroll
+            for (int c = 0; c < KD_CB; ++c) {
+                const uint32_t ev = e[c];
+                if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
+                    const uint32_t j = ev & ENT_TXN_MASK;
                     ++witnessed_here;
-                    L.slot_ne[s] = 1;
+                    L.slot_ne[sl[c]] = 1;
                     if ((int64_t)j >= base) {
                         const uint32_t b = (uint32_t)((int64_t)j - base);
                         atomicOr(&L.bitmap[b >> 6], 1ull << (b & 63));
@@ -217,7 +399,7 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
             continue;
         }
 
-        // ---- fill ----
+        // ---- fill: keys, then per witnessed entry its rank -> keysToTxnIds body and txnIds ----
         {
             uint32_t ex = incl2 - mysum;
 #pragma unroll
@@ -226,60 +408,37 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
         if (lane < k) L.slot_ns[lane] = (uint32_t)__popcll(ne_bal & lt);
         wave_lds_sync();
         const uint32_t key_base = p.kd_key_off[i], val_base = p.kd_val_off[i], k2v_base = p.kd_k2v_off[i];
-        if (lane < k && ne) p.kd_keys[key_base + L.slot_ns[lane]] = L.slot_key[lane] + p.key_lo;
-        // txnIds: far owners by rank, then near bits in order
-        for (uint32_t f = lane; f < F; f += 64) {
-            const uint32_t v = L.far[f];
-            if (v & 0x80000000u) {
-                const uint32_t x = v & 0x7FFFFFFFu;
-                uint32_t rank = 0;
-                for (uint32_t g = 0; g < F; ++g) {
-                    const uint32_t y = L.far[g];
-                    rank += ((y & 0x80000000u) && (y & 0x7FFFFFFFu) < x) ? 1u : 0u;
-                }
-                p.kd_vals[val_base + rank] = x;
-            }
-        }
+        if (lane < k && ne) p.kd_keys[key_base + L.slot_ns[lane]] = my_key;
+        uint32_t running = 0;
+        for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
+            if (!one_batch) load_batch<WPL>(p, L, r0, raw_total, e, sl, lane);
 #pragma unroll
-        for (int q = 0; q < WPL; ++q) {
-            unsigned long long word = L.bitmap[lane * WPL + q];
-            uint32_t o = val_base + far_u + L.wprefix[lane * WPL + q];
-            const int64_t wbase = base + (int64_t)(lane * WPL + q) * 64;
-            while (word) {
-                const int b = __builtin_ctzll(word);
-                p.kd_vals[o++] = (uint32_t)(wbase + b);
-                word &= word - 1;
-            }
-        }
-        // keysToTxnIds body (+ header at each non-empty slot's last witnessed entry)
-        {
-            uint32_t running = 0, s = 0;
-            for (uint32_t r0 = 0; r0 < raw_total; r0 += 64) {
-                const uint32_t r = r0 + lane;
-                bool wit = false;
+            for (int c = 0; c < KD_CB; ++c) {
+                const uint32_t r = r0 + c * 64 + lane;
+                const uint32_t ev = e[c];
+                const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
+                const uint32_t j = ev & ENT_TXN_MASK;
                 uint32_t rank = 0;
-                if (r < raw_total) {
-                    while (L.slot_rawbase[s + 1] <= r) ++s;
-                    const uint32_t e = p.hist[L.slot_lo[s] + (r - L.slot_rawbase[s])];
-                    const uint32_t j = e & ENT_TXN_MASK;
-                    wit = (wmask >> (e >> ENT_KIND_SHIFT)) & 1u;
-                    if (wit) {
-                        if ((int64_t)j >= base) {
-                            const uint32_t b = (uint32_t)((int64_t)j - base);
-                            rank = far_u + L.wprefix[b >> 6] + (uint32_t)__popcll(L.bitmap[b >> 6] & ((1ull << (b & 63)) - 1ull));
-                        } else {
-                            for (uint32_t g = 0; g < F; ++g) {
-                                const uint32_t y = L.far[g];
-                                rank += ((y & 0x80000000u) && (y & 0x7FFFFFFFu) < j) ? 1u : 0u;
-                            }
+                if (wit) {
+                    if ((int64_t)j >= base) {
+                        const uint32_t b = (uint32_t)((int64_t)j - base);
+                        rank = far_u + L.wprefix[b >> 6] + (uint32_t)__popcll(L.bitmap[b >> 6] & ((1ull << (b & 63)) - 1ull));
+                    } else {
+                        for (uint32_t g = 0; g < F; ++g) {
+                            const uint32_t y = L.far[g];
+                            rank += ((y & 0x80000000u) && (y & 0x7FFFFFFFu) < j) ? 1u : 0u;
                         }
                     }
                 }
                 const uint64_t bal = __ballot(wit);
                 const uint32_t pos = running + (uint32_t)__popcll(bal & lt);
-                if (wit) p.kd_k2v[k2v_base + kc + pos] = (int32_t)rank;
+                if (wit) {
+                    p.kd_k2v[k2v_base + kc + pos] = (int32_t)rank;
+                    p.kd_vals[val_base + rank] = j;         // every holder of j writes the same word
+                }
                 running += (uint32_t)__popcll(bal);
-                // header: a slot's end offset is known at the wave step holding its last raw entry
+                // header: a slot's end offset is known at the step holding its last raw entry
+                const uint32_t s = sl[c];
                 if (r < raw_total && r + 1 == L.slot_rawbase[s + 1] && L.slot_ne[s])
                     p.kd_k2v[k2v_base + L.slot_ns[s]] = (int32_t)(kc + pos + (wit ? 1u : 0u));
             }
@@ -305,21 +464,37 @@ void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
-                          uint32_t *pair_key, uint32_t *pair_val, DevStatus *status, hipStream_t s)
+                          uint32_t *pair_key, uint32_t *pair_ent, DevStatus *status, hipStream_t s)
 {
     if (n == 0) return;
     uint32_t blocks = (n + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
+    if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(validate_pack_kernel, dim3(blocks), dim3(256), 0, s, n, msb, lsb, node, key_off, key_ord,
-                       rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_val, status);
+                       rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_ent, status);
 }
 
-void launch_segments(uint32_t P, const uint32_t *sorted_keys, uint32_t *seg_start, uint32_t *seg_end, hipStream_t s)
+size_t history_temp_bytes(uint32_t P)
 {
+    const uint32_t tiles = (P + HS_TILE - 1) / HS_TILE;
+    return ((size_t)P + tiles + 64) * sizeof(uint32_t);
+}
+
+void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
+                    const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
+                    uint32_t *seg_end, unsigned long long *poslo, void *temp, hipStream_t s)
+{
+    (void)nkeys;
     if (P == 0) return;
+    const uint32_t tiles = (P + HS_TILE - 1) / HS_TILE;
+    uint32_t *pw_local = (uint32_t *)temp;
+    uint32_t *tile_max = pw_local + P;
+    hipLaunchKernelGGL(history1_kernel, dim3(tiles), dim3(HS_THREADS), 0, s, P, sorted_key, sorted_pair, pair_ent,
+                       hist, seg_start, seg_end, pw_local, tile_max);
+    hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tiles);
     uint32_t blocks = (P + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(segments_kernel, dim3(blocks), dim3(256), 0, s, P, sorted_keys, seg_start, seg_end);
+    hipLaunchKernelGGL(history2_kernel, dim3(blocks), dim3(256), 0, s, P, window, sorted_key, sorted_pair, hist,
+                       seg_start, pw_local, tile_max, poslo);
 }
 
 void launch_keydeps_count(const KeyDepsParams &p, int wpl, hipStream_t s) { launch_keydeps<false>(p, wpl, s); }

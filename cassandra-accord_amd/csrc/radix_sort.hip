@@ -1,9 +1,12 @@
-// Stable LSD radix sort of (u32 key, u32 value) pairs, 8-bit digits (K2 of SURVEY.md §7:
-// bucketing (key, txn) pairs into per-key CommandsForKey histories, CommandsForKey.java:415).
+// Stable LSD radix sort of (u32 key, u32 value) pairs (K2 of SURVEY.md §7: bucketing the
+// batch's (key, txn) pairs into per-key CommandsForKey histories, CommandsForKey.java:415).
 //
-// Per pass: upsweep (per-tile digit histogram in LDS) -> exclusive scan of the digit-major
-// [256][tiles] histogram -> downsweep (stable in-tile ranking with wave ballots, scatter).
-// Stability matters: entries of one key must stay in TxnId (= input) order.
+// Per pass (digit of <= 9 bits, so a 17-bit keyspace needs 2 passes):
+//   upsweep   : per-tile digit histogram in LDS -> digit-major [bins][tiles] counts
+//   scan      : exclusive scan of the counts (scan.hip) -> global offset per (digit, tile)
+//   downsweep : stable in-tile ranking with wave ballots, the tile is re-ordered by digit in LDS
+//               and written out as contiguous per-digit runs (coalesced stores).
+// Stability keeps the entries of one key in TxnId (= input) order.
 #include "device_common.h"
 #include "kernels.h"
 
@@ -11,68 +14,127 @@ namespace accord {
 
 namespace {
 constexpr int RS_THREADS = 256;
+constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
-constexpr int RS_BINS = 256;
+constexpr int RS_MAX_BITS = 9;
+constexpr int RS_MAX_BINS = 1 << RS_MAX_BITS;
 
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint32_t *__restrict__ keys, uint32_t n, int shift,
-                                                         uint32_t *__restrict__ hist, uint32_t tiles)
+                                                         uint32_t mask, uint32_t *__restrict__ hist, uint32_t tiles)
 {
-    __shared__ uint32_t h[RS_BINS];
-    const uint32_t tid = threadIdx.x;
-    h[tid] = 0;
+    __shared__ uint32_t h[RS_MAX_BINS];
+    const uint32_t tid = threadIdx.x, bins = mask + 1;
+    for (uint32_t b = tid; b < bins; b += RS_THREADS) h[b] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * RS_TILE;
 #pragma unroll 4
     for (int j = 0; j < RS_ITEMS; ++j) {
         uint32_t idx = base + j * RS_THREADS + tid;
-        if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & 0xFF], 1u);
+        if (idx < n) atomicAdd(&h[(keys[idx] >> shift) & mask], 1u);
     }
     __syncthreads();
-    hist[tid * tiles + blockIdx.x] = h[tid];
+    for (uint32_t b = tid; b < bins; b += RS_THREADS) hist[b * tiles + blockIdx.x] = h[b];
 }
 
+template <int BITS>
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                           uint32_t n, int shift, const uint32_t *__restrict__ offs,
-                                                           uint32_t tiles)
+                                                           uint32_t n, int shift, uint32_t mask,
+                                                           const uint32_t *__restrict__ offs, uint32_t tiles)
 {
-    __shared__ uint32_t run[RS_BINS];
-    __shared__ uint32_t wcnt[RS_THREADS / 64][RS_BINS];
-    const uint32_t tid = threadIdx.x, w = tid >> 6;
-    run[tid] = offs[tid * tiles + blockIdx.x];
+    constexpr uint32_t BINS = 1u << BITS;       // LDS sizing; digits use the runtime mask (<= BINS-1)
+    const uint32_t MASK = mask;
+    __shared__ uint32_t s_keys[RS_TILE];
+    __shared__ uint32_t s_vals[RS_TILE];
+    __shared__ uint32_t run[BINS];        // tile-local running count, then exclusive tile start
+    __shared__ uint32_t glob[BINS];       // global offset of this tile's digit-d run
+    __shared__ uint32_t wcnt[RS_WAVES][BINS];
+    __shared__ uint32_t wsum[RS_WAVES];
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    for (uint32_t b = tid; b < BINS; b += RS_THREADS) { run[b] = 0; glob[b] = b <= mask ? offs[b * tiles + blockIdx.x] : 0u; }
     const uint64_t lt = lanemask_lt();
     const uint32_t base = blockIdx.x * RS_TILE;
-    for (int r = 0; r < RS_ITEMS; ++r) {
-        if (base + r * RS_THREADS >= n) break;                 // block-uniform
+    const uint32_t tile_n = min((uint32_t)RS_TILE, n - base);
+
+    uint32_t key[RS_ITEMS], val[RS_ITEMS], lrank[RS_ITEMS];
 #pragma unroll
-        for (int ww = 0; ww < RS_THREADS / 64; ++ww) wcnt[ww][tid] = 0;
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const uint32_t idx = base + r * RS_THREADS + tid;
+        key[r] = idx < n ? kin[idx] : 0u;
+        val[r] = idx < n ? (vin ? vin[idx] : idx) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        for (uint32_t b = tid; b < RS_WAVES * BINS; b += RS_THREADS) (&wcnt[0][0])[b] = 0;
         __syncthreads();
         const uint32_t idx = base + r * RS_THREADS + tid;
         const bool valid = idx < n;
-        uint32_t key = 0, val = 0, d = 0;
-        if (valid) { key = kin[idx]; val = vin[idx]; d = (key >> shift) & 0xFF; }
+        const uint32_t d = (key[r] >> shift) & MASK;
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            uint64_t bb = __ballot(valid && ((d >> b) & 1));
+        for (int b = 0; b < BITS; ++b) {
+            const uint64_t bb = __ballot(valid && ((d >> b) & 1));
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
-        const uint32_t rank = __popcll(peers & lt);
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
         if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
         __syncthreads();
         if (valid) {
             uint32_t pos = run[d] + rank;
             for (uint32_t ww = 0; ww < w; ++ww) pos += wcnt[ww][d];
-            kout[pos] = key;
-            vout[pos] = val;
+            lrank[r] = pos;
         }
         __syncthreads();
-        uint32_t add = 0;
+        for (uint32_t b = tid; b < BINS; b += RS_THREADS) {
+            uint32_t add = 0;
 #pragma unroll
-        for (int ww = 0; ww < RS_THREADS / 64; ++ww) add += wcnt[ww][tid];
-        run[tid] += add;
+            for (int ww = 0; ww < RS_WAVES; ++ww) add += wcnt[ww][b];
+            run[b] += add;
+        }
+        __syncthreads();   // wcnt is cleared by the next round
+    }
+    __syncthreads();
+    // exclusive scan of the tile's digit counts (BINS <= 512: each thread owns <= 2 bins)
+    {
+        constexpr uint32_t PER = (BINS + RS_THREADS - 1) / RS_THREADS;
+        uint32_t c[PER], s = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t b = tid * PER + q;
+            c[q] = b < BINS ? run[b] : 0u;
+            s += c[q];
+        }
+        const uint32_t inc = wave_incl_scan(s);
+        if (lane == 63) wsum[w] = inc;
         __syncthreads();
+        uint32_t ex = inc - s;
+        for (uint32_t ww = 0; ww < w; ++ww) ex += wsum[ww];
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t b = tid * PER + q;
+            if (b < BINS) run[b] = ex;
+            ex += c[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        const uint32_t idx = base + r * RS_THREADS + tid;
+        if (idx < n) {
+            const uint32_t d = (key[r] >> shift) & MASK;
+            const uint32_t q = run[d] + lrank[r];
+            s_keys[q] = key[r];
+            s_vals[q] = val[r];
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < tile_n; q += RS_THREADS) {
+        const uint32_t k = s_keys[q];
+        const uint32_t d = (k >> shift) & MASK;
+        const uint32_t g = glob[d] + (q - run[d]);
+        kout[g] = k;
+        vout[g] = s_vals[q];
     }
 }
 } // namespace
@@ -80,7 +142,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
 size_t radix_sort_temp_bytes(uint32_t n)
 {
     uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
-    size_t hist = (size_t)RS_BINS * (tiles ? tiles : 1);
+    size_t hist = (size_t)RS_MAX_BINS * (tiles ? tiles : 1);
     size_t a = ((hist * 4 + (hist + 1) * 4) + 15) & ~(size_t)15;
     return a + 16 + scan_temp_bytes((uint32_t)hist);
 }
@@ -90,25 +152,32 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
 {
     if (n == 0) return;
     const uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
-    const size_t hist_n = (size_t)RS_BINS * tiles;
+    const size_t hist_cap = (size_t)RS_MAX_BINS * tiles;
     uint32_t *hist = (uint32_t *)temp;
-    uint32_t *offs = hist + hist_n;
-    const size_t a = ((hist_n * 4 + (hist_n + 1) * 4) + 15) & ~(size_t)15;
+    uint32_t *offs = hist + hist_cap;
+    const size_t a = ((hist_cap * 4 + (hist_cap + 1) * 4) + 15) & ~(size_t)15;
     unsigned long long *total = (unsigned long long *)((char *)temp + a);
     void *scan_tmp = (char *)temp + a + 16;
-    int passes = (bits + 7) / 8;
-    if (passes < 1) passes = 1;
-    // ping-pong so that the last pass lands in *_out
+    if (bits < 1) bits = 1;
+    const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
+    // ping-pong so that the last pass lands in *_out; vals_in == nullptr means identity values
     const uint32_t *ki = keys_in, *vi = vals_in;
+    int shift = 0;
     for (int p = 0; p < passes; ++p) {
+        const int pb = (bits - shift + (passes - p) - 1) / (passes - p);   // split bits evenly
+        const uint32_t mask = (1u << pb) - 1;
         const bool to_out = ((passes - 1 - p) % 2) == 0;
         uint32_t *ko = to_out ? keys_out : keys_tmp;
         uint32_t *vo = to_out ? vals_out : vals_tmp;
-        const int shift = p * 8;
-        hipLaunchKernelGGL(rs_upsweep, dim3(tiles), dim3(RS_THREADS), 0, s, ki, n, shift, hist, tiles);
+        const size_t hist_n = (size_t)(mask + 1) * tiles;
+        hipLaunchKernelGGL(rs_upsweep, dim3(tiles), dim3(RS_THREADS), 0, s, ki, n, shift, mask, hist, tiles);
         exclusive_scan_u32(hist, offs, (uint32_t)hist_n, total, scan_tmp, s);
-        hipLaunchKernelGGL(rs_downsweep, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, offs, tiles);
+        if (pb > 8)
+            hipLaunchKernelGGL(rs_downsweep<9>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, mask, offs, tiles);
+        else
+            hipLaunchKernelGGL(rs_downsweep<8>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, mask, offs, tiles);
         ki = ko; vi = vo;
+        shift += pb;
     }
 }
 

@@ -50,7 +50,8 @@ struct accord_store {
     bool has_batch = false, computed = false;
     DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
     // work
-    DevBuf pair_key, pair_val, sort_key, sort_val, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
+    DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
+    DevBuf hist, poslo, hist_tmp;
     DevBuf cnt_keys, cnt_vals, cnt_k2v, kd_key_off, kd_val_off, kd_k2v_off, scan_tmp, status_totals;
     // outputs
     DevBuf kd_keys, kd_vals, kd_k2v, rd_zero_off;
@@ -148,7 +149,7 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipSetDevice(s->cfg.device);
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
-                      &s->pair_key, &s->pair_val, &s->sort_key, &s->sort_val, &s->tmp_key, &s->tmp_val,
+                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->poslo, &s->hist_tmp,
                       &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off};
@@ -216,11 +217,14 @@ int32_t accord_deps_compute(accord_store *s)
     s->computed = false;
 
     HIPCHECK(s, s->pair_key.ensure((size_t)P * 4));
-    HIPCHECK(s, s->pair_val.ensure((size_t)P * 4));
+    HIPCHECK(s, s->pair_ent.ensure((size_t)P * 4));
     HIPCHECK(s, s->sort_key.ensure((size_t)P * 4));
-    HIPCHECK(s, s->sort_val.ensure((size_t)P * 4));
+    HIPCHECK(s, s->sort_pair.ensure((size_t)P * 4));
     HIPCHECK(s, s->tmp_key.ensure((size_t)P * 4));
     HIPCHECK(s, s->tmp_val.ensure((size_t)P * 4));
+    HIPCHECK(s, s->hist.ensure((size_t)P * 4));
+    HIPCHECK(s, s->poslo.ensure((size_t)P * 8));
+    HIPCHECK(s, s->hist_tmp.ensure(accord::history_temp_bytes(P)));
     HIPCHECK(s, s->seg_start.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->seg_end.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->radix_tmp.ensure(accord::radix_sort_temp_bytes(P)));
@@ -242,15 +246,17 @@ int32_t accord_deps_compute(accord_store *s)
     accord::launch_validate_pack(n, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->node.as<int32_t>(),
                                  s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->rng_off.as<uint32_t>(),
                                  nullptr, nullptr, s->cfg.key_lo, s->cfg.key_hi, s->pair_key.as<uint32_t>(),
-                                 s->pair_val.as<uint32_t>(), &dev->status, st);
+                                 s->pair_ent.as<uint32_t>(), &dev->status, st);
     record(s, EV_VALIDATE);
-    accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), s->pair_val.as<uint32_t>(), s->sort_key.as<uint32_t>(),
-                             s->sort_val.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(), P,
+    accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
+                             s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(), P,
                              bits_for(nkeys - 1), s->radix_tmp.p, st);
     record(s, EV_SORT);
     HIPCHECK(s, hipMemsetAsync(s->seg_start.p, 0, (size_t)nkeys * 4, st));
     HIPCHECK(s, hipMemsetAsync(s->seg_end.p, 0, (size_t)nkeys * 4, st));
-    accord::launch_segments(P, s->sort_key.as<uint32_t>(), s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(), st);
+    accord::launch_history(P, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
+                           s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
+                           s->seg_end.as<uint32_t>(), s->poslo.as<unsigned long long>(), s->hist_tmp.p, st);
     record(s, EV_SEGMENT);
 
     accord::KeyDepsParams kp{};
@@ -258,8 +264,8 @@ int32_t accord_deps_compute(accord_store *s)
     kp.msb = s->msb.as<uint64_t>(); kp.lsb = s->lsb.as<uint64_t>(); kp.node = s->node.as<int32_t>();
     kp.key_off = s->key_off.as<uint32_t>(); kp.key_ord = s->key_ord.as<uint32_t>();
     kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
-    kp.hist = s->sort_val.as<uint32_t>();
-    kp.seg_start = s->seg_start.as<uint32_t>(); kp.seg_end = s->seg_end.as<uint32_t>();
+    kp.hist = s->hist.as<uint32_t>();
+    kp.poslo = s->poslo.as<unsigned long long>();
     kp.cnt_keys = s->cnt_keys.as<uint32_t>(); kp.cnt_vals = s->cnt_vals.as<uint32_t>(); kp.cnt_k2v = s->cnt_k2v.as<uint32_t>();
     kp.status = &dev->status;
     accord::launch_keydeps_count(kp, s->wpl, st);
