@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--zipf", type=float, default=0.99)
     ap.add_argument("--window", type=int, default=256)
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--range-frac", type=float, default=0.0, help="config 3: 0.2")
+    ap.add_argument("--range-len", type=int, default=1000)
+    ap.add_argument("--write-frac", type=float, default=0.5)
     ap.add_argument("--cpu-sample", type=int, default=24_000, help="txns of the CPU-baseline prefix sample")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -69,7 +72,8 @@ def main():
     from accord_amd import CommandStore, generate_stream
 
     # ---- workload: every rank generates the config-2 stream with its own seed (weak scaling)
-    s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, 0.5, seed=args.seed + rank)
+    s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, args.write_frac,
+                        range_frac=args.range_frac, range_len_max=args.range_len, seed=args.seed + rank)
     stores_total = 8 * world
     # EvenSplit over [0, keyspace): store b owns [b*ks/S, (b+1)*ks/S); rank owns stores
     # [8*rank, 8*rank+8) -> one contiguous key block per rank.
@@ -97,7 +101,8 @@ def main():
     barrier()
     hip.hipDeviceSynchronize()
     t0 = time.perf_counter()
-    stage = {"validate": 0.0, "sort": 0.0, "segment": 0.0, "count": 0.0, "scan": 0.0, "fill": 0.0, "total": 0.0}
+    stage = {"validate": 0.0, "sort": 0.0, "segment": 0.0, "count": 0.0, "scan": 0.0, "fill": 0.0, "range_fill": 0.0,
+             "total": 0.0}
     for _ in range(args.steps):
         step()
         t = store.timing()
@@ -107,6 +112,7 @@ def main():
         stage["count"] += t.count_ms
         stage["scan"] += t.scan_ms
         stage["fill"] += t.fill_ms
+        stage["range_fill"] += t.range_ms
         stage["total"] += t.total_ms
     hip.hipDeviceSynchronize()
     barrier()
@@ -157,7 +163,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
         "data": "synthetic (SURVEY.md §8d stream, splitmix64 + Zipf rejection-inversion)",
-        "config": {"workload": "config2: 1M key txns x 8 keys, Zipf(0.99) over 100k keys, 50% writes, W=256",
+        "config": {"workload": workload_name(args),
                    "n_txns_per_gpu": args.n, "keys_per_txn": args.keys_per_txn, "keyspace": args.keyspace,
                    "zipf": args.zipf, "window": args.window, "seed": args.seed,
                    "stores": stores_total, "parallelism": f"keyspace-sharded x{world}"},
@@ -177,6 +183,14 @@ def main():
     store.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def workload_name(args):
+    if args.range_frac > 0:
+        return (f"config3: {args.n} txns ({args.range_frac:.0%} range txns, 1-2 ranges len<= {args.range_len}), "
+                f"{args.keys_per_txn} keys/key txn, Zipf({args.zipf}) over {args.keyspace} keys, W={args.window}")
+    return (f"config2: {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over {args.keyspace} keys, "
+            f"{args.write_frac:.0%} writes, W={args.window}")
 
 
 def restrict_to_keys(s, lo, hi):
@@ -201,7 +215,8 @@ def cpu_baseline(s, args):
         import oracle_lib
         from accord_amd import generate_stream
         if s is None:
-            s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, 0.5, seed=args.seed)
+            s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, args.write_frac,
+                                range_frac=args.range_frac, range_len_max=args.range_len, seed=args.seed)
         m = min(args.cpu_sample, s.n)
         t0 = time.perf_counter()
         oracle_lib.deps_literal(s, args.window, limit=m)

@@ -44,17 +44,51 @@ struct KeyDepsParams {
     DevStatus *status;
 };
 
-// txn-major validation + (key, entry) pair packing
+// txn-major validation + (key, entry) pair packing; range CSR owners and range-txn flags
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
-                          uint32_t *pair_key, uint32_t *pair_ent, DevStatus *status, hipStream_t s);
+                          uint32_t *pair_key, uint32_t *pair_ent, uint32_t *rng_owner, uint32_t *is_range,
+                          DevStatus *status, hipStream_t s);
+// range_txns[excl[i]] = i for every i with is_range[i]
+void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s);
 size_t history_temp_bytes(uint32_t P);
 // key-major: history entries, segments, and per pair the [lo, pos) deps slice (txn-major poslo)
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
                     uint32_t *seg_end, unsigned long long *poslo, void *temp, hipStream_t s);
+// history tile size of the Write max-scan carry (pw_local / pw_carry)
+constexpr uint32_t HISTORY_TILE = 4096;
 void launch_keydeps_count(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
+
+// ---- range txns (rangedeps.hip) ----
+struct RangeDepsParams {
+    uint32_t n;
+    const uint64_t *lsb;
+    const uint32_t *key_off, *key_ord;
+    const uint32_t *rng_off, *rng_start, *rng_end, *rng_owner;
+    uint32_t window, key_lo, key_hi;
+    // history (for range txns' KeyDeps)
+    const uint32_t *hist, *seg_start, *seg_end, *pw_local, *pw_carry;
+    uint32_t pw_tile;
+    uint32_t n_range_txns;
+    const uint32_t *range_txns;
+    // RangeDeps counts / outputs
+    uint32_t *cnt_rngs, *cnt_vals, *cnt_r2v;
+    const uint32_t *rd_rng_off, *rd_val_off, *rd_r2v_off;
+    uint32_t *rd_rng_start, *rd_rng_end, *rd_vals;
+    int32_t *rd_r2v;
+    // KeyDeps of range txns: counts / outputs (shared with the key-txn arrays)
+    uint32_t *cnt_keys, *cnt_vals_k, *cnt_k2v;
+    const uint32_t *kd_key_off, *kd_val_off, *kd_k2v_off;
+    uint32_t *kd_keys, *kd_vals;
+    int32_t *kd_k2v;
+    DevStatus *status;
+};
+void launch_rangedeps_count(const RangeDepsParams &p, hipStream_t s);
+void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s);
+void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s);
+void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s);
 
 } // namespace accord

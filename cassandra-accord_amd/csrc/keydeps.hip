@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
     uint32_t n, const uint64_t *__restrict__ msb, const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
     const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ key_ord, const uint32_t *__restrict__ rng_off,
     const uint32_t *__restrict__ rng_start, const uint32_t *__restrict__ rng_end, uint32_t key_lo, uint32_t key_hi,
-    uint32_t *__restrict__ pair_key, uint32_t *__restrict__ pair_ent, DevStatus *st)
+    uint32_t *__restrict__ pair_key, uint32_t *__restrict__ pair_ent, uint32_t *__restrict__ rng_owner,
+    uint32_t *__restrict__ is_range, DevStatus *st)
 {
     const uint32_t lane = lane_id();
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -70,6 +71,22 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
                 for (uint32_t r = r0; r < r1; ++r)
                     if (rng_start[r] >= rng_end[r] || (r > r0 && rng_end[r - 1] > rng_start[r]))
                         record_error(st, t, ACCORD_ERR_RANGES);
+        }
+        if (valid) is_range[t] = (uint32_t)(lsb[t] & 1);
+        if (rng_owner) {                             // owner txn of every range of the batch
+            const uint32_t ro = rng_off[min(t, n)];
+            const uint32_t rbase = __shfl(ro, 0, 64), rend = rng_off[t0 + cnt];
+            for (uint32_t q0 = rbase; q0 < rend; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                uint32_t j = 0;
+#pragma unroll
+                for (uint32_t step = 32; step >= 1; step >>= 1) {
+                    const uint32_t c = j + step;
+                    const uint32_t rc = __shfl(ro, (int)(c & 63), 64);
+                    if (c < cnt && rc <= q) j = c;
+                }
+                if (q < rend) rng_owner[q] = t0 + j;
+            }
         }
         const uint32_t pbase = __shfl(ko, 0, 64);
         const uint32_t pend = key_off[t0 + cnt];
@@ -99,6 +116,7 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
 constexpr int HS_THREADS = 256;
 constexpr int HS_ITEMS = 16;
 constexpr uint32_t HS_TILE = HS_THREADS * HS_ITEMS;
+static_assert(HS_TILE == HISTORY_TILE, "history tile");
 
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
 {
@@ -464,13 +482,29 @@ void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
-                          uint32_t *pair_key, uint32_t *pair_ent, DevStatus *status, hipStream_t s)
+                          uint32_t *pair_key, uint32_t *pair_ent, uint32_t *rng_owner, uint32_t *is_range,
+                          DevStatus *status, hipStream_t s)
 {
     if (n == 0) return;
     uint32_t blocks = (n + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(validate_pack_kernel, dim3(blocks), dim3(256), 0, s, n, msb, lsb, node, key_off, key_ord,
-                       rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_ent, status);
+                       rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_ent, rng_owner, is_range, status);
+}
+
+__global__ __launch_bounds__(256) void compact_flags_kernel(uint32_t n, const uint32_t *__restrict__ flags,
+                                                            const uint32_t *__restrict__ excl, uint32_t *__restrict__ out)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        if (flags[i]) out[excl[i]] = i;
+}
+
+void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s)
+{
+    if (n == 0) return;
+    uint32_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(compact_flags_kernel, dim3(blocks), dim3(256), 0, s, n, flags, excl, out);
 }
 
 size_t history_temp_bytes(uint32_t P)

@@ -32,11 +32,11 @@ struct DevBuf {
     template <typename T> T *as() const { return (T *)p; }
 };
 
-enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_COUNT_ALL };
+enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_RANGE, EV_COUNT_ALL };
 
 struct HostTotals {
     accord::DevStatus status;
-    unsigned long long totals[3];
+    unsigned long long totals[8];   // kd keys, kd vals, kd k2v, rd ranges, rd vals, rd r2v, range txns
 };
 
 } // namespace
@@ -52,9 +52,13 @@ struct accord_store {
     // work
     DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
     DevBuf hist, poslo, hist_tmp;
+    DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
+    DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v;
+    uint32_t n_range_txns = 0;
+    uint64_t tot_rngs = 0, tot_rvals = 0, tot_r2v = 0;
     DevBuf cnt_keys, cnt_vals, cnt_k2v, kd_key_off, kd_val_off, kd_k2v_off, scan_tmp, status_totals;
     // outputs
-    DevBuf kd_keys, kd_vals, kd_k2v, rd_zero_off;
+    DevBuf kd_keys, kd_vals, kd_k2v, rd_zero_off;  // rd_zero_off: unused, kept for ABI-compatible views
     uint64_t tot_keys = 0, tot_vals = 0, tot_k2v = 0;
     HostTotals *pinned = nullptr;
     hipEvent_t ev[EV_COUNT_ALL] = {};
@@ -152,7 +156,10 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->poslo, &s->hist_tmp,
                       &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
-                      &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off};
+                      &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
+                      &s->rng_owner, &s->is_range, &s->rt_excl, &s->range_txns, &s->cnt_rngs, &s->cnt_rvals,
+                      &s->cnt_r2v, &s->rd_rng_off, &s->rd_val_off, &s->rd_r2v_off, &s->rd_rng_start, &s->rd_rng_end,
+                      &s->rd_vals, &s->rd_r2v};
     for (DevBuf *b : bufs) b->release();
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventDestroy(ev);
@@ -183,9 +190,10 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
         return fail(s, ACCORD_ERR_ARG, "CSR offsets must start at 0");
     const uint32_t P = b->key_off[n];
     const uint32_t R = b->rng_off ? b->rng_off[n] : 0;
-    if (R != 0)
-        return fail(s, ACCORD_ERR_STATE, "range-domain txns are not supported by this build yet (RangeDeps path)");
-    s->n = n; s->P = P; s->R = R;
+    if (R && (!b->rng_start || !b->rng_end)) return fail(s, ACCORD_ERR_ARG, "range CSR without range bounds");
+    uint32_t nrt = 0;
+    for (uint32_t i = 0; i < n; ++i) nrt += (uint32_t)(b->lsb[i] & 1);
+    s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt;
     s->has_batch = false; s->computed = false;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
@@ -193,6 +201,8 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     HIPCHECK(s, s->key_off.ensure(((size_t)n + 1) * 4));
     HIPCHECK(s, s->key_ord.ensure((size_t)P * 4));
     HIPCHECK(s, s->rng_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->rng_start.ensure((size_t)R * 4));
+    HIPCHECK(s, s->rng_end.ensure((size_t)R * 4));
     if (n) {
         HIPCHECK(s, hipMemcpyAsync(s->msb.p, b->msb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
         HIPCHECK(s, hipMemcpyAsync(s->lsb.p, b->lsb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
@@ -200,7 +210,14 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     }
     HIPCHECK(s, hipMemcpyAsync(s->key_off.p, b->key_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
     if (P) HIPCHECK(s, hipMemcpyAsync(s->key_ord.p, b->key_ord, (size_t)P * 4, hipMemcpyHostToDevice, s->stream));
-    HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
+    if (b->rng_off)
+        HIPCHECK(s, hipMemcpyAsync(s->rng_off.p, b->rng_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
+    else
+        HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
+    if (R) {
+        HIPCHECK(s, hipMemcpyAsync(s->rng_start.p, b->rng_start, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rng_end.p, b->rng_end, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
+    }
     HIPCHECK(s, hipStreamSynchronize(s->stream));
     s->has_batch = true;
     return ACCORD_OK;
@@ -211,8 +228,9 @@ int32_t accord_deps_compute(accord_store *s)
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     if (!s->has_batch) return fail(s, ACCORD_ERR_STATE, "accord_deps_compute before accord_batch_upload");
     HIPCHECK(s, hipSetDevice(s->cfg.device));
-    const uint32_t n = s->n, P = s->P;
+    const uint32_t n = s->n, P = s->P, R = s->R, nrt = s->n_range_txns;
     const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    const size_t n1 = (size_t)n + 1;
     hipStream_t st = s->stream;
     s->computed = false;
 
@@ -231,22 +249,37 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->cnt_keys.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->cnt_vals.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->cnt_k2v.ensure((size_t)n * 4 + 4));
-    HIPCHECK(s, s->kd_key_off.ensure(((size_t)n + 1) * 4));
-    HIPCHECK(s, s->kd_val_off.ensure(((size_t)n + 1) * 4));
-    HIPCHECK(s, s->kd_k2v_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->cnt_rngs.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->cnt_rvals.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->cnt_r2v.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->kd_key_off.ensure(n1 * 4));
+    HIPCHECK(s, s->kd_val_off.ensure(n1 * 4));
+    HIPCHECK(s, s->kd_k2v_off.ensure(n1 * 4));
+    HIPCHECK(s, s->rd_rng_off.ensure(n1 * 4));
+    HIPCHECK(s, s->rd_val_off.ensure(n1 * 4));
+    HIPCHECK(s, s->rd_r2v_off.ensure(n1 * 4));
     HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n)));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
-    HIPCHECK(s, s->rd_zero_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->rng_owner.ensure((size_t)R * 4));
+    HIPCHECK(s, s->is_range.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->rt_excl.ensure(n1 * 4));
+    HIPCHECK(s, s->range_txns.ensure((size_t)nrt * 4 + 4));
 
     HostTotals *dev = s->status_totals.as<HostTotals>();
     record(s, EV_START);
     HIPCHECK(s, hipMemsetAsync(dev, 0xFF, sizeof(HostTotals), st));
     HIPCHECK(s, hipMemsetAsync(&dev->status.overflow, 0, sizeof(uint32_t), st));
-    HIPCHECK(s, hipMemsetAsync(s->rd_zero_off.p, 0, ((size_t)n + 1) * 4, st));
     accord::launch_validate_pack(n, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->node.as<int32_t>(),
                                  s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->rng_off.as<uint32_t>(),
-                                 nullptr, nullptr, s->cfg.key_lo, s->cfg.key_hi, s->pair_key.as<uint32_t>(),
-                                 s->pair_ent.as<uint32_t>(), &dev->status, st);
+                                 R ? s->rng_start.as<uint32_t>() : nullptr, R ? s->rng_end.as<uint32_t>() : nullptr,
+                                 s->cfg.key_lo, s->cfg.key_hi, s->pair_key.as<uint32_t>(), s->pair_ent.as<uint32_t>(),
+                                 R ? s->rng_owner.as<uint32_t>() : nullptr, s->is_range.as<uint32_t>(), &dev->status, st);
+    if (nrt) {
+        accord::exclusive_scan_u32(s->is_range.as<uint32_t>(), s->rt_excl.as<uint32_t>(), n, &dev->totals[6],
+                                   s->scan_tmp.p, st);
+        accord::launch_compact_flags(n, s->is_range.as<uint32_t>(), s->rt_excl.as<uint32_t>(),
+                                     s->range_txns.as<uint32_t>(), st);
+    }
     record(s, EV_VALIDATE);
     accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
                              s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(), P,
@@ -268,11 +301,36 @@ int32_t accord_deps_compute(accord_store *s)
     kp.poslo = s->poslo.as<unsigned long long>();
     kp.cnt_keys = s->cnt_keys.as<uint32_t>(); kp.cnt_vals = s->cnt_vals.as<uint32_t>(); kp.cnt_k2v = s->cnt_k2v.as<uint32_t>();
     kp.status = &dev->status;
+
+    accord::RangeDepsParams rp{};
+    rp.n = n; rp.lsb = kp.lsb; rp.key_off = kp.key_off; rp.key_ord = kp.key_ord;
+    rp.rng_off = s->rng_off.as<uint32_t>(); rp.rng_start = s->rng_start.as<uint32_t>();
+    rp.rng_end = s->rng_end.as<uint32_t>(); rp.rng_owner = s->rng_owner.as<uint32_t>();
+    rp.window = s->cfg.window; rp.key_lo = s->cfg.key_lo; rp.key_hi = s->cfg.key_hi;
+    rp.hist = kp.hist; rp.seg_start = s->seg_start.as<uint32_t>(); rp.seg_end = s->seg_end.as<uint32_t>();
+    rp.pw_local = s->hist_tmp.as<uint32_t>(); rp.pw_carry = rp.pw_local + P; rp.pw_tile = accord::HISTORY_TILE;
+    rp.n_range_txns = nrt; rp.range_txns = s->range_txns.as<uint32_t>();
+    rp.cnt_rngs = s->cnt_rngs.as<uint32_t>(); rp.cnt_vals = s->cnt_rvals.as<uint32_t>(); rp.cnt_r2v = s->cnt_r2v.as<uint32_t>();
+    rp.cnt_keys = kp.cnt_keys; rp.cnt_vals_k = kp.cnt_vals; rp.cnt_k2v = kp.cnt_k2v;
+    rp.status = &dev->status;
+
     accord::launch_keydeps_count(kp, s->wpl, st);
+    if (nrt) accord::launch_rangekeys_count(rp, st);
+    if (R) accord::launch_rangedeps_count(rp, st);
     record(s, EV_COUNT);
     accord::exclusive_scan_u32(kp.cnt_keys, s->kd_key_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
     accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[1], s->scan_tmp.p, st);
     accord::exclusive_scan_u32(kp.cnt_k2v, s->kd_k2v_off.as<uint32_t>(), n, &dev->totals[2], s->scan_tmp.p, st);
+    if (R) {
+        accord::exclusive_scan_u32(rp.cnt_rngs, s->rd_rng_off.as<uint32_t>(), n, &dev->totals[3], s->scan_tmp.p, st);
+        accord::exclusive_scan_u32(rp.cnt_vals, s->rd_val_off.as<uint32_t>(), n, &dev->totals[4], s->scan_tmp.p, st);
+        accord::exclusive_scan_u32(rp.cnt_r2v, s->rd_r2v_off.as<uint32_t>(), n, &dev->totals[5], s->scan_tmp.p, st);
+    } else {
+        HIPCHECK(s, hipMemsetAsync(s->rd_rng_off.p, 0, n1 * 4, st));
+        HIPCHECK(s, hipMemsetAsync(s->rd_val_off.p, 0, n1 * 4, st));
+        HIPCHECK(s, hipMemsetAsync(s->rd_r2v_off.p, 0, n1 * 4, st));
+        HIPCHECK(s, hipMemsetAsync(&dev->totals[3], 0, 3 * sizeof(unsigned long long), st));
+    }
     record(s, EV_SCAN);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
@@ -284,19 +342,33 @@ int32_t accord_deps_compute(accord_store *s)
         return fail(s, code, "%s (txn %u)", code_name(code), where);
     }
     if (h.status.overflow)
-        return fail(s, ACCORD_ERR_CAPACITY, "%u txns exceed the per-wave capacity (first: txn %u)", h.status.overflow,
-                    h.status.overflow_first);
-    for (int t = 0; t < 3; ++t)
+        return fail(s, ACCORD_ERR_CAPACITY, "%u txns exceed a per-txn capacity of this build (first: txn %u)",
+                    h.status.overflow, h.status.overflow_first);
+    for (int t = 0; t < 6; ++t)
         if (h.totals[t] >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "deps output exceeds 2^32 entries");
     s->tot_keys = h.totals[0]; s->tot_vals = h.totals[1]; s->tot_k2v = h.totals[2];
+    s->tot_rngs = h.totals[3]; s->tot_rvals = h.totals[4]; s->tot_r2v = h.totals[5];
     HIPCHECK(s, s->kd_keys.ensure(s->tot_keys * 4));
     HIPCHECK(s, s->kd_vals.ensure(s->tot_vals * 4));
     HIPCHECK(s, s->kd_k2v.ensure(s->tot_k2v * 4));
+    HIPCHECK(s, s->rd_rng_start.ensure(s->tot_rngs * 4));
+    HIPCHECK(s, s->rd_rng_end.ensure(s->tot_rngs * 4));
+    HIPCHECK(s, s->rd_vals.ensure(s->tot_rvals * 4));
+    HIPCHECK(s, s->rd_r2v.ensure(s->tot_r2v * 4));
     kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.kd_val_off = s->kd_val_off.as<uint32_t>();
     kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
     kp.kd_keys = s->kd_keys.as<uint32_t>(); kp.kd_vals = s->kd_vals.as<uint32_t>(); kp.kd_k2v = s->kd_k2v.as<int32_t>();
+    rp.kd_key_off = kp.kd_key_off; rp.kd_val_off = kp.kd_val_off; rp.kd_k2v_off = kp.kd_k2v_off;
+    rp.kd_keys = kp.kd_keys; rp.kd_vals = kp.kd_vals; rp.kd_k2v = kp.kd_k2v;
+    rp.rd_rng_off = s->rd_rng_off.as<uint32_t>(); rp.rd_val_off = s->rd_val_off.as<uint32_t>();
+    rp.rd_r2v_off = s->rd_r2v_off.as<uint32_t>();
+    rp.rd_rng_start = s->rd_rng_start.as<uint32_t>(); rp.rd_rng_end = s->rd_rng_end.as<uint32_t>();
+    rp.rd_vals = s->rd_vals.as<uint32_t>(); rp.rd_r2v = s->rd_r2v.as<int32_t>();
     accord::launch_keydeps_fill(kp, s->wpl, st);
     record(s, EV_FILL);
+    if (nrt) accord::launch_rangekeys_fill(rp, st);
+    if (R) accord::launch_rangedeps_fill(rp, st);
+    record(s, EV_RANGE);
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
 
@@ -308,8 +380,8 @@ int32_t accord_deps_compute(accord_store *s)
         s->timing.count_ms = el(EV_SEGMENT, EV_COUNT);
         s->timing.scan_ms = el(EV_COUNT, EV_SCAN);
         s->timing.fill_ms = el(EV_SCAN, EV_FILL);
-        s->timing.range_ms = 0;
-        s->timing.total_ms = el(EV_START, EV_FILL);
+        s->timing.range_ms = el(EV_FILL, EV_RANGE);
+        s->timing.total_ms = el(EV_START, EV_RANGE);
     }
     s->timing.pairs = P;
     s->timing.hist_entries = P;
@@ -334,7 +406,11 @@ int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
     d->kd_key_off = s->kd_key_off.as<uint32_t>(); d->kd_keys = s->kd_keys.as<uint32_t>();
     d->kd_val_off = s->kd_val_off.as<uint32_t>(); d->kd_vals = s->kd_vals.as<uint32_t>();
     d->kd_k2v_off = s->kd_k2v_off.as<uint32_t>(); d->kd_k2v = s->kd_k2v.as<int32_t>();
-    d->rd_rng_off = d->rd_val_off = d->rd_r2v_off = s->rd_zero_off.as<uint32_t>();
+    d->rd_rngs_total = s->tot_rngs; d->rd_vals_total = s->tot_rvals; d->rd_r2v_total = s->tot_r2v;
+    d->rd_rng_off = s->rd_rng_off.as<uint32_t>(); d->rd_val_off = s->rd_val_off.as<uint32_t>();
+    d->rd_r2v_off = s->rd_r2v_off.as<uint32_t>(); d->rd_rng_start = s->rd_rng_start.as<uint32_t>();
+    d->rd_rng_end = s->rd_rng_end.as<uint32_t>(); d->rd_vals = s->rd_vals.as<uint32_t>();
+    d->rd_r2v = s->rd_r2v.as<int32_t>();
     return ACCORD_OK;
 }
 
@@ -356,8 +432,9 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
     try {
         o->kd_key_off.resize(n1); o->kd_val_off.resize(n1); o->kd_k2v_off.resize(n1);
         o->kd_keys.resize(s->tot_keys + 1); o->kd_vals.resize(s->tot_vals + 1); o->kd_k2v.resize(s->tot_k2v + 1);
-        o->rd_rng_off.assign(n1, 0); o->rd_val_off.assign(n1, 0); o->rd_r2v_off.assign(n1, 0);
-        o->rd_rng_start.resize(1); o->rd_rng_end.resize(1); o->rd_vals.resize(1); o->rd_r2v.resize(1);
+        o->rd_rng_off.resize(n1); o->rd_val_off.resize(n1); o->rd_r2v_off.resize(n1);
+        o->rd_rng_start.resize(s->tot_rngs + 1); o->rd_rng_end.resize(s->tot_rngs + 1);
+        o->rd_vals.resize(s->tot_rvals + 1); o->rd_r2v.resize(s->tot_r2v + 1);
     } catch (...) {
         delete o;
         return fail(s, ACCORD_ERR_OOM, "out of host memory");
@@ -372,6 +449,13 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
     if (e == hipSuccess) e = cp(o->kd_keys.data(), s->kd_keys.p, s->tot_keys * 4);
     if (e == hipSuccess) e = cp(o->kd_vals.data(), s->kd_vals.p, s->tot_vals * 4);
     if (e == hipSuccess) e = cp(o->kd_k2v.data(), s->kd_k2v.p, s->tot_k2v * 4);
+    if (e == hipSuccess) e = cp(o->rd_rng_off.data(), s->rd_rng_off.p, n1 * 4);
+    if (e == hipSuccess) e = cp(o->rd_val_off.data(), s->rd_val_off.p, n1 * 4);
+    if (e == hipSuccess) e = cp(o->rd_r2v_off.data(), s->rd_r2v_off.p, n1 * 4);
+    if (e == hipSuccess) e = cp(o->rd_rng_start.data(), s->rd_rng_start.p, s->tot_rngs * 4);
+    if (e == hipSuccess) e = cp(o->rd_rng_end.data(), s->rd_rng_end.p, s->tot_rngs * 4);
+    if (e == hipSuccess) e = cp(o->rd_vals.data(), s->rd_vals.p, s->tot_rvals * 4);
+    if (e == hipSuccess) e = cp(o->rd_r2v.data(), s->rd_r2v.p, s->tot_r2v * 4);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
         delete o;
@@ -380,6 +464,7 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
     std::memset(out, 0, sizeof(*out));
     out->n = s->n;
     out->kd_keys_total = s->tot_keys; out->kd_vals_total = s->tot_vals; out->kd_k2v_total = s->tot_k2v;
+    out->rd_rngs_total = s->tot_rngs; out->rd_vals_total = s->tot_rvals; out->rd_r2v_total = s->tot_r2v;
     out->kd_key_off = o->kd_key_off.data(); out->kd_keys = o->kd_keys.data();
     out->kd_val_off = o->kd_val_off.data(); out->kd_vals = o->kd_vals.data();
     out->kd_k2v_off = o->kd_k2v_off.data(); out->kd_k2v = o->kd_k2v.data();

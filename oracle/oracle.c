@@ -711,6 +711,7 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
 
     /* range commands in TxnId order */
     for (uint32_t i = 0; i < n; ++i) if (domain_of(s->lsb[i]) == 1) if (u32v_push(&rcmd, i)) goto done;
+    size_t rc_first = 0;
 
     for (uint32_t i = 0; i < n; ++i) {
         int tk = witnesses_of(kind_of(s->lsb[i]));
@@ -768,10 +769,10 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
             mm_builder rb; mmb_init(&rb, NULL);
             /* collect (range code, txn) pairs then build canonical multimap directly */
             u32v rlo = {0}, rhi = {0}, rtx = {0};
-            for (size_t c = 0; c < rcmd.n; ++c) {
+            while (rc_first < rcmd.n && (int64_t)rcmd.p[rc_first] < applied_before) ++rc_first;   /* monotone in i */
+            for (size_t c = rc_first; c < rcmd.n; ++c) {
                 uint32_t j = rcmd.p[c];
                 if (j >= i) break;
-                if ((int64_t)j < applied_before) continue;
                 if (!kinds_test(tk, kind_of(s->lsb[j]))) continue;
                 for (uint32_t a = s->rng_off[j]; a < s->rng_off[j + 1]; ++a) {
                     uint32_t rs = s->rng_start[a], re = s->rng_end[a];
