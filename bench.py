@@ -3,15 +3,17 @@
 
 One "step" = one pass of the hot path over one batch: batched PreAccept deps for every txn of
 the stream (validate/pack -> (key, txn) radix bucketing into CommandsForKey histories ->
-segments -> per-txn conflict scan + KeyDeps linearisation, count and fill), with the batch
-already resident in HBM.  Workload (BASELINE.json configs[1]): 1,048,576 key txns, 8 keys
-each, Zipf(0.99) over 100,000 keys, 50% writes, window W=256, seed 2.
+history annotation -> per-txn conflict scan + KeyDeps linearisation, count and fill), with the
+batch already resident in HBM.  Default workload (BASELINE.json configs[1]): 1,048,576 key txns,
+8 keys each, Zipf(0.99) over 100,000 keys, 50% writes, window W=256, seed 2.
 
-Multi-GPU (`torchrun --nproc-per-node N`): the keyspace is split into 8*N CommandStores by
-EvenSplit (local/ShardDistributor.java:46-157); rank r owns a contiguous block of stores and
-computes the per-store KeyDeps of every txn restricted to its keys (weak scaling: each rank gets
-a stream of the config-2 size).  KeyDeps of key-disjoint stores need no data exchange to be
-complete per store; the coordinator-side union is a later row.
+Multi-GPU (`torchrun --nproc-per-node G`, config 4): one global stream of G x 1,048,576 txns
+(weak scaling: every GPU gets a config-2-sized share); the keyspace is split into 8G CommandStores
+by EvenSplit (local/ShardDistributor.java:46-157) and rank r owns the contiguous block of stores
+[8r, 8r+8).  A step is: compute the partial KeyDeps of the txns intersecting the rank's keys, one
+RCCL exchange (grouped send/recv over xGMI) that moves every txn's partial to its owner rank, and
+the on-device union of the G partials (PreAccept.reduce, messages/PreAccept.java:140-156) -- after
+the step every txn's node-level deps exist exactly once.
 """
 from __future__ import annotations
 
@@ -71,23 +73,28 @@ def main():
 
     from accord_amd import CommandStore, generate_stream
 
-    # ---- workload: every rank generates the config-2 stream with its own seed (weak scaling)
-    s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, args.write_frac,
-                        range_frac=args.range_frac, range_len_max=args.range_len, seed=args.seed + rank)
+    n_total = args.n * world
+    # one global stream (identical on every rank); weak scaling: n per GPU
+    s_full = generate_stream(n_total, args.keys_per_txn, args.keyspace, args.zipf, args.write_frac,
+                             range_frac=args.range_frac, range_len_max=args.range_len, seed=args.seed)
     stores_total = 8 * world
-    # EvenSplit over [0, keyspace): store b owns [b*ks/S, (b+1)*ks/S); rank owns stores
-    # [8*rank, 8*rank+8) -> one contiguous key block per rank.
+    # EvenSplit over [0, keyspace): store b owns [b*ks/S, (b+1)*ks/S); rank r owns stores [8r, 8r+8)
     key_lo = (8 * rank) * args.keyspace // stores_total
     key_hi = (8 * rank + 8) * args.keyspace // stores_total
-    if world > 1:
-        s = restrict_to_keys(s, key_lo, key_hi)
+    s = s_full if world == 1 else s_full.restrict_keys(key_lo, key_hi, drop_empty=True)
 
     store = CommandStore(device=0 if world == 1 else local_rank, key_lo=key_lo, key_hi=key_hi,
                          window=args.window, profile=True)
     store.upload(s)
+    if world > 1:
+        uid = [CommandStore.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        store.comm_init(world, rank, uid[0])
 
     def step():
         store.compute()
+        if world > 1:
+            store.exchange_merge(n_total)
 
     for _ in range(args.warmup):
         step()
@@ -102,7 +109,7 @@ def main():
     hip.hipDeviceSynchronize()
     t0 = time.perf_counter()
     stage = {"validate": 0.0, "sort": 0.0, "segment": 0.0, "count": 0.0, "scan": 0.0, "fill": 0.0, "range_fill": 0.0,
-             "total": 0.0}
+             "total": 0.0, "exchange": 0.0, "merge": 0.0}
     for _ in range(args.steps):
         step()
         t = store.timing()
@@ -114,6 +121,10 @@ def main():
         stage["fill"] += t.fill_ms
         stage["range_fill"] += t.range_ms
         stage["total"] += t.total_ms
+        if world > 1:
+            xms, mms = store.shard_timing()
+            stage["exchange"] += xms
+            stage["merge"] += mms
     hip.hipDeviceSynchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -125,7 +136,8 @@ def main():
     for k in stage:
         stage[k] /= max(1, args.steps)
 
-    # sizes for the byte model (from the device view totals of the last step)
+    # sizes for the byte model: the rank's own computed partial (before the exchange)
+    store.compute()
     view = store.device_view()
     n = s.n
     P = s.pairs
@@ -139,7 +151,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    txns_total = args.n * world * args.steps
+    txns_total = n_total * args.steps
     value = txns_total / elapsed
     B = algorithmic_bytes(n, P, kc, U, D)
     Bf = fill_kernel_bytes(n, P, kc, U, D)
@@ -148,7 +160,7 @@ def main():
 
     cpu = None
     if not args.no_cpu:
-        cpu = cpu_baseline(s if world == 1 else None, args)
+        cpu = cpu_baseline(s_full, args)
 
     line = {
         "metric": "PreAccept deps/sec (batched txns)",
@@ -166,7 +178,8 @@ def main():
         "config": {"workload": workload_name(args),
                    "n_txns_per_gpu": args.n, "keys_per_txn": args.keys_per_txn, "keyspace": args.keyspace,
                    "zipf": args.zipf, "window": args.window, "seed": args.seed,
-                   "stores": stores_total, "parallelism": f"keyspace-sharded x{world}"},
+                   "n_txns_total": n_total, "stores": stores_total,
+                   "parallelism": f"keyspace-sharded x{world}" + (" + RCCL exchange/union" if world > 1 else "")},
         "deps_per_s": D * world * args.steps / elapsed,
         "sizes": {"N": n, "P": P, "keys_out": kc, "U": U, "D": D},
         "stage_ms": stage,
@@ -193,19 +206,6 @@ def workload_name(args):
             f"{args.write_frac:.0%} writes, W={args.window}")
 
 
-def restrict_to_keys(s, lo, hi):
-    """Slice every txn's keys to the store block [lo, hi) (CommandStores.mapReduce fan-out,
-    local/CommandStores.java:575-592); txns with no key in the block keep an empty key set."""
-    from accord_amd import Stream
-    keep = (s.key_ord >= lo) & (s.key_ord < hi)
-    counts = np.add.reduceat(keep.astype(np.uint32), s.key_off[:-1].astype(np.int64)) if s.pairs else np.zeros(s.n, np.uint32)
-    empty = s.key_off[1:] == s.key_off[:-1]
-    counts = np.where(empty, 0, counts).astype(np.uint32)
-    key_off = np.zeros(s.n + 1, np.uint32)
-    np.cumsum(counts, out=key_off[1:])
-    return Stream(s.msb, s.lsb, s.node, key_off, s.key_ord[keep].copy(), s.rng_off, s.rng_start, s.rng_end)
-
-
 def cpu_baseline(s, args):
     """The oracle's literal restatement of the reference algorithm (sorted-array CommandsForKey
     copied/re-sorted on every status change, linear mapReduceActive scan, RelationMultiMap
@@ -213,10 +213,6 @@ def cpu_baseline(s, args):
     try:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
-        from accord_amd import generate_stream
-        if s is None:
-            s = generate_stream(args.n, args.keys_per_txn, args.keyspace, args.zipf, args.write_frac,
-                                range_frac=args.range_frac, range_len_max=args.range_len, seed=args.seed)
         m = min(args.cpu_sample, s.n)
         t0 = time.perf_counter()
         oracle_lib.deps_literal(s, args.window, limit=m)

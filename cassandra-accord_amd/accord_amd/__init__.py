@@ -43,7 +43,8 @@ EXPORTED_SYMBOLS = [
     "accord_store_create", "accord_store_destroy", "accord_last_error", "accord_store_stream",
     "accord_deps_batch", "accord_deps_release", "accord_batch_upload", "accord_deps_compute",
     "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
-    "accord_workload_generate", "accord_workload_free",
+    "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
+    "accord_comm_init", "accord_deps_exchange_merge", "accord_shard_timing",
 ]
 
 
@@ -81,7 +82,7 @@ class _StoreCfg(C.Structure):
 class _Batch(C.Structure):
     _fields_ = [("n", C.c_uint32), ("msb", _u64p), ("lsb", _u64p), ("node", _i32p),
                 ("key_off", _u32p), ("key_ord", _u32p), ("rng_off", _u32p),
-                ("rng_start", _u32p), ("rng_end", _u32p)]
+                ("rng_start", _u32p), ("rng_end", _u32p), ("txn_index", _u32p)]
 
 
 class _Deps(C.Structure):
@@ -136,6 +137,11 @@ def lib() -> C.CDLL:
         L.accord_workload_generate.argtypes = [C.POINTER(_WorkloadCfg), C.POINTER(_Batch)]
         L.accord_workload_free.argtypes = [C.POINTER(_Batch)]
         L.accord_workload_free.restype = None
+        L.accord_deps_merge.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_Deps), C.c_uint32]
+        L.accord_comm_unique_id.argtypes = [C.c_void_p]
+        L.accord_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+        L.accord_deps_exchange_merge.argtypes = [C.c_void_p, C.c_uint32]
+        L.accord_shard_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
             if f.restype is C.c_int:  # default
@@ -156,6 +162,7 @@ class Stream:
     rng_off: np.ndarray
     rng_start: np.ndarray
     rng_end: np.ndarray
+    txn_index: Optional[np.ndarray] = None   # global stream positions (store subsets)
 
     @property
     def n(self) -> int:
@@ -179,10 +186,34 @@ class Stream:
                       self.key_off[:m + 1].copy(), self.key_ord[:k1].copy(), self.rng_off[:m + 1].copy(),
                       self.rng_start[:r1].copy(), self.rng_end[:r1].copy())
 
+    def restrict_keys(self, lo: int, hi: int, drop_empty: bool = False) -> "Stream":
+        """Slice every txn's keys to the store block [lo, hi) (CommandStores.mapReduce fan-out,
+        local/CommandStores.java:575-592).  drop_empty keeps only the txns intersecting the block
+        and records their global positions in txn_index (key txns only)."""
+        keep = (self.key_ord >= lo) & (self.key_ord < hi)
+        csum = np.zeros(self.pairs + 1, np.int64)
+        np.cumsum(keep, out=csum[1:])
+        counts = (csum[self.key_off[1:].astype(np.int64)] - csum[self.key_off[:-1].astype(np.int64)]).astype(np.uint32)
+        kord = self.key_ord[keep].copy()
+        if not drop_empty:
+            ko = np.zeros(self.n + 1, np.uint32)
+            np.cumsum(counts, out=ko[1:])
+            return Stream(self.msb, self.lsb, self.node, ko, kord, self.rng_off, self.rng_start, self.rng_end)
+        if int(self.rng_off[-1]) != 0:
+            raise IllegalArgumentException(-1, "drop_empty restriction supports key txns only")
+        sel = np.nonzero(counts > 0)[0].astype(np.uint32)
+        ko = np.zeros(sel.size + 1, np.uint32)
+        np.cumsum(counts[sel], out=ko[1:])
+        base = np.zeros(sel.size + 1, np.uint32)
+        return Stream(self.msb[sel].copy(), self.lsb[sel].copy(), self.node[sel].copy(), ko, kord, base, 
+                      np.zeros(0, np.uint32), np.zeros(0, np.uint32), txn_index=sel)
+
     def c_batch(self) -> _Batch:
         self._keep = [np.ascontiguousarray(a) for a in (self.msb, self.lsb, self.node, self.key_off, self.key_ord,
                                                         self.rng_off, self.rng_start, self.rng_end)]
-        msb, lsb, node, ko, kord, ro, rs, re = self._keep
+        if self.txn_index is not None:
+            self._keep.append(np.ascontiguousarray(self.txn_index, dtype=np.uint32))
+        msb, lsb, node, ko, kord, ro, rs, re = self._keep[:8]
         b = _Batch()
         b.n = self.n
         b.msb = msb.ctypes.data_as(_u64p)
@@ -194,6 +225,7 @@ class Stream:
         b.rng_off = ro.ctypes.data_as(_u32p) if has_ranges else None
         b.rng_start = rs.ctypes.data_as(_u32p) if has_ranges else None
         b.rng_end = re.ctypes.data_as(_u32p) if has_ranges else None
+        b.txn_index = self._keep[8].ctypes.data_as(_u32p) if self.txn_index is not None else None
         return b
 
 
@@ -387,6 +419,37 @@ class CommandStore:
         for f in PartialDeps.FIELDS:
             out[f] = C.cast(getattr(d, f), C.c_void_p).value or 0
         return out
+
+    def _device_view_c(self) -> _Deps:
+        d = _Deps()
+        self._check(lib().accord_deps_device_view(self._h, C.byref(d)))
+        return d
+
+    def merge(self, parts, txn_lo: int = 0):
+        """Union of per-store partials (each a CommandStore on this GPU, key-disjoint, ordered by
+        key block) -- PreAccept.reduce; the result becomes this store's deps."""
+        arr = (_Deps * len(parts))(*[p._device_view_c() for p in parts])
+        self._check(lib().accord_deps_merge(self._h, len(parts), arr, txn_lo))
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        rc = lib().accord_comm_unique_id(buf)
+        if rc != ACCORD_OK:
+            _raise(rc, lib().accord_last_error(None).decode())
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = C.create_string_buffer(uid, 128)
+        self._check(lib().accord_comm_init(self._h, nranks, rank, buf))
+
+    def exchange_merge(self, n_total: int):
+        self._check(lib().accord_deps_exchange_merge(self._h, n_total))
+
+    def shard_timing(self):
+        a, b = C.c_float(), C.c_float()
+        self._check(lib().accord_shard_timing(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def timing(self) -> Timing:
         t = _Timing()

@@ -31,9 +31,10 @@ struct KeyDepsParams {
     const uint64_t *msb, *lsb;
     const int32_t *node;
     const uint32_t *key_off, *key_ord;
+    const uint32_t *txn_index;         // global stream positions or nullptr
     uint32_t key_lo, key_hi;
     uint32_t window;
-    const uint32_t *hist;              // key-major history entries (kind<<29 | txn)
+    const uint32_t *hist;              // key-major history entries (kind<<29 | global txn)
     const unsigned long long *poslo;   // txn-major per pair: (slice start << 32) | history position
     // count outputs
     uint32_t *cnt_keys, *cnt_vals, *cnt_k2v;
@@ -49,7 +50,7 @@ void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
                           uint32_t *pair_key, uint32_t *pair_ent, uint32_t *rng_owner, uint32_t *is_range,
-                          DevStatus *status, hipStream_t s);
+                          const uint32_t *txn_index, DevStatus *status, hipStream_t s);
 // range_txns[excl[i]] = i for every i with is_range[i]
 void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s);
 size_t history_temp_bytes(uint32_t P);
@@ -90,5 +91,31 @@ void launch_rangedeps_count(const RangeDepsParams &p, hipStream_t s);
 void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s);
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s);
 void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s);
+
+// ---- K6 merge (merge.hip) ----
+struct MergeParams {
+    uint32_t n;        // txns (aligned across parts)
+    uint32_t G;        // parts
+    uint32_t txn_lo;   // global stream position of txn 0
+    const uint32_t *const *key_off;
+    const uint32_t *const *keys;
+    const uint32_t *const *val_off;
+    const uint32_t *const *vals;
+    const uint32_t *const *k2v_off;
+    const int32_t *const *k2v;
+    uint32_t *cnt_keys, *cnt_vals, *cnt_k2v;
+    const uint32_t *out_key_off, *out_val_off, *out_k2v_off;
+    uint32_t *out_keys, *out_vals;
+    int32_t *out_k2v;
+    DevStatus *status;
+};
+void launch_merge_count(const MergeParams &p, hipStream_t s);
+// exp_off[a][t] = off[a][#subset txns with global position < t], t in [0, n_total]
+void launch_expand_offsets(uint32_t n, uint32_t n_total, const uint32_t *txn_index, uint32_t *ind, uint32_t *c,
+                           const uint32_t *const off[3], uint32_t *const exp_off[3], void *scan_tmp,
+                           unsigned long long *total, hipStream_t s);
+// bnd[a*(G+1) + d] = exp_off[a][d * n_total / G]
+void launch_boundaries(uint32_t G, uint32_t n_total, uint32_t *const exp_off[3], uint32_t *bnd, hipStream_t s);
+void launch_merge_fill(const MergeParams &p, hipStream_t s);
 
 } // namespace accord

@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
     const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ key_ord, const uint32_t *__restrict__ rng_off,
     const uint32_t *__restrict__ rng_start, const uint32_t *__restrict__ rng_end, uint32_t key_lo, uint32_t key_hi,
     uint32_t *__restrict__ pair_key, uint32_t *__restrict__ pair_ent, uint32_t *__restrict__ rng_owner,
-    uint32_t *__restrict__ is_range, DevStatus *st)
+    uint32_t *__restrict__ is_range, const uint32_t *__restrict__ txn_index, DevStatus *st)
 {
     const uint32_t lane = lane_id();
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -60,7 +60,9 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
         if (valid) {
             const uint64_t l = lsb[t];
             const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
-            ent = (kind << ENT_KIND_SHIFT) | t;
+            const uint32_t gi = txn_index ? txn_index[t] : t;      // global stream position
+            ent = (kind << ENT_KIND_SHIFT) | (gi & ENT_TXN_MASK);
+            if (gi > ENT_TXN_MASK || (txn_index && t > 0 && txn_index[t - 1] >= gi)) record_error(st, t, ACCORD_ERR_UNSORTED);
             if (witness_mask(kind) == 0) record_error(st, t, ACCORD_ERR_KIND);
             if (t > 0 && ts_cmp(msb[t - 1], lsb[t - 1], node[t - 1], msb[t], l, node[t]) >= 0)
                 record_error(st, t, ACCORD_ERR_UNSORTED);
@@ -334,6 +336,11 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
             }
             continue;
         }
+        if (k == 0) {                                   // range txn / no key in this store
+            if (!FILL && lane == 0) { p.cnt_keys[i] = 0; p.cnt_vals[i] = 0; p.cnt_k2v[i] = 0; }
+            continue;
+        }
+        const uint32_t gi = p.txn_index ? p.txn_index[i] : i;   // global stream position
 
         // ---- slots: the deps slice [lo, pos) of each key, from the history annotation ----
         uint32_t raw = 0;
@@ -352,7 +359,7 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
         wave_lds_sync();
 
         // ---- phase 1: witness filter -> near bitmap / far list ----
-        const int64_t base = (int64_t)i - (int64_t)SPAN;
+        const int64_t base = (int64_t)gi - (int64_t)SPAN;
         const bool one_batch = raw_total <= 64u * KD_CB;
         uint32_t e[KD_CB], sl[KD_CB];
         uint32_t witnessed_here = 0;
@@ -483,13 +490,14 @@ void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
                           uint32_t *pair_key, uint32_t *pair_ent, uint32_t *rng_owner, uint32_t *is_range,
-                          DevStatus *status, hipStream_t s)
+                          const uint32_t *txn_index, DevStatus *status, hipStream_t s)
 {
     if (n == 0) return;
     uint32_t blocks = (n + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(validate_pack_kernel, dim3(blocks), dim3(256), 0, s, n, msb, lsb, node, key_off, key_ord,
-                       rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_ent, rng_owner, is_range, status);
+                       rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_ent, rng_owner, is_range,
+                       txn_index, status);
 }
 
 __global__ __launch_bounds__(256) void compact_flags_kernel(uint32_t n, const uint32_t *__restrict__ flags,

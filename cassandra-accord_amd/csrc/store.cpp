@@ -1,7 +1,6 @@
 // C ABI implementation (include/accord_deps.h): one accord_store == one CommandStore == one
 // HIP stream, with a grow-only HBM arena for the batch, the per-key histories and the outputs.
-#include "../../include/accord_deps.h"
-#include "kernels.h"
+#include "store_impl.h"
 
 #include <hip/hip_runtime.h>
 
@@ -12,62 +11,9 @@
 #include <string>
 #include <vector>
 
-namespace {
+namespace accord_impl {
 
 thread_local std::string g_last_error;
-
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t bytes)
-    {
-        if (bytes <= cap && p) return hipSuccess;
-        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
-        size_t want = bytes < 256 ? 256 : bytes;
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) cap = want;
-        return e;
-    }
-    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
-    template <typename T> T *as() const { return (T *)p; }
-};
-
-enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_RANGE, EV_COUNT_ALL };
-
-struct HostTotals {
-    accord::DevStatus status;
-    unsigned long long totals[8];   // kd keys, kd vals, kd k2v, rd ranges, rd vals, rd r2v, range txns
-};
-
-} // namespace
-
-struct accord_store {
-    accord_store_cfg cfg{};
-    hipStream_t stream = nullptr;
-    std::string err;
-    // batch (device)
-    uint32_t n = 0, P = 0, R = 0;
-    bool has_batch = false, computed = false;
-    DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
-    // work
-    DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
-    DevBuf hist, poslo, hist_tmp;
-    DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
-    DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v;
-    uint32_t n_range_txns = 0;
-    uint64_t tot_rngs = 0, tot_rvals = 0, tot_r2v = 0;
-    DevBuf cnt_keys, cnt_vals, cnt_k2v, kd_key_off, kd_val_off, kd_k2v_off, scan_tmp, status_totals;
-    // outputs
-    DevBuf kd_keys, kd_vals, kd_k2v, rd_zero_off;  // rd_zero_off: unused, kept for ABI-compatible views
-    uint64_t tot_keys = 0, tot_vals = 0, tot_k2v = 0;
-    HostTotals *pinned = nullptr;
-    hipEvent_t ev[EV_COUNT_ALL] = {};
-    bool events = false;
-    accord_timing timing{};
-    int wpl = 1;
-};
-
-namespace {
 
 int32_t fail(accord_store *s, int32_t code, const char *fmt, ...)
 {
@@ -81,11 +27,9 @@ int32_t fail(accord_store *s, int32_t code, const char *fmt, ...)
     return code;
 }
 
-#define HIPCHECK(s, expr)                                                                             \
-    do {                                                                                              \
-        hipError_t e_ = (expr);                                                                       \
-        if (e_ != hipSuccess) return fail((s), ACCORD_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-    } while (0)
+} // namespace accord_impl
+
+namespace {
 
 int bits_for(uint32_t maxval)
 {
@@ -159,7 +103,10 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
                       &s->rng_owner, &s->is_range, &s->rt_excl, &s->range_txns, &s->cnt_rngs, &s->cnt_rvals,
                       &s->cnt_r2v, &s->rd_rng_off, &s->rd_val_off, &s->rd_r2v_off, &s->rd_rng_start, &s->rd_rng_end,
-                      &s->rd_vals, &s->rd_r2v};
+                      &s->rd_vals, &s->rd_r2v, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
+                      &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
+                      &s->m_zero};
+    accord_impl::shard_comm_destroy(s);
     for (DevBuf *b : bufs) b->release();
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventDestroy(ev);
@@ -171,7 +118,7 @@ int32_t accord_store_destroy(accord_store *s)
 
 const char *accord_last_error(const accord_store *s)
 {
-    return s ? s->err.c_str() : g_last_error.c_str();
+    return s ? s->err.c_str() : accord_impl::g_last_error.c_str();
 }
 
 void *accord_store_stream(accord_store *s) { return s ? (void *)s->stream : nullptr; }
@@ -193,8 +140,10 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     if (R && (!b->rng_start || !b->rng_end)) return fail(s, ACCORD_ERR_ARG, "range CSR without range bounds");
     uint32_t nrt = 0;
     for (uint32_t i = 0; i < n; ++i) nrt += (uint32_t)(b->lsb[i] & 1);
+    if (b->txn_index && nrt)
+        return fail(s, ACCORD_ERR_ARG, "txn_index (store subset of a stream) is supported for key txns only");
     s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt;
-    s->has_batch = false; s->computed = false;
+    s->has_batch = false; s->computed = false; s->merged = false;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
     HIPCHECK(s, s->node.ensure((size_t)n * 4));
@@ -218,6 +167,11 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
         HIPCHECK(s, hipMemcpyAsync(s->rng_start.p, b->rng_start, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
         HIPCHECK(s, hipMemcpyAsync(s->rng_end.p, b->rng_end, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
     }
+    s->has_txn_index = b->txn_index != nullptr;
+    if (s->has_txn_index) {
+        HIPCHECK(s, s->txn_index.ensure((size_t)n * 4));
+        if (n) HIPCHECK(s, hipMemcpyAsync(s->txn_index.p, b->txn_index, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
+    }
     HIPCHECK(s, hipStreamSynchronize(s->stream));
     s->has_batch = true;
     return ACCORD_OK;
@@ -233,6 +187,7 @@ int32_t accord_deps_compute(accord_store *s)
     const size_t n1 = (size_t)n + 1;
     hipStream_t st = s->stream;
     s->computed = false;
+    s->merged = false;
 
     HIPCHECK(s, s->pair_key.ensure((size_t)P * 4));
     HIPCHECK(s, s->pair_ent.ensure((size_t)P * 4));
@@ -273,7 +228,8 @@ int32_t accord_deps_compute(accord_store *s)
                                  s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->rng_off.as<uint32_t>(),
                                  R ? s->rng_start.as<uint32_t>() : nullptr, R ? s->rng_end.as<uint32_t>() : nullptr,
                                  s->cfg.key_lo, s->cfg.key_hi, s->pair_key.as<uint32_t>(), s->pair_ent.as<uint32_t>(),
-                                 R ? s->rng_owner.as<uint32_t>() : nullptr, s->is_range.as<uint32_t>(), &dev->status, st);
+                                 R ? s->rng_owner.as<uint32_t>() : nullptr, s->is_range.as<uint32_t>(),
+                                 s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr, &dev->status, st);
     if (nrt) {
         accord::exclusive_scan_u32(s->is_range.as<uint32_t>(), s->rt_excl.as<uint32_t>(), n, &dev->totals[6],
                                    s->scan_tmp.p, st);
@@ -296,6 +252,7 @@ int32_t accord_deps_compute(accord_store *s)
     kp.n = n;
     kp.msb = s->msb.as<uint64_t>(); kp.lsb = s->lsb.as<uint64_t>(); kp.node = s->node.as<int32_t>();
     kp.key_off = s->key_off.as<uint32_t>(); kp.key_ord = s->key_ord.as<uint32_t>();
+    kp.txn_index = s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr;
     kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
     kp.hist = s->hist.as<uint32_t>();
     kp.poslo = s->poslo.as<unsigned long long>();
@@ -401,6 +358,15 @@ int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
     if (!s || !d) return fail(s, ACCORD_ERR_ARG, "null argument");
     if (!s->computed) return fail(s, ACCORD_ERR_STATE, "no computed deps");
     std::memset(d, 0, sizeof(*d));
+    if (s->merged) {
+        d->n = s->m_n;
+        d->kd_keys_total = s->m_tot_keys; d->kd_vals_total = s->m_tot_vals; d->kd_k2v_total = s->m_tot_k2v;
+        d->kd_key_off = s->m_key_off.as<uint32_t>(); d->kd_keys = s->m_keys.as<uint32_t>();
+        d->kd_val_off = s->m_val_off.as<uint32_t>(); d->kd_vals = s->m_vals.as<uint32_t>();
+        d->kd_k2v_off = s->m_k2v_off.as<uint32_t>(); d->kd_k2v = s->m_k2v.as<int32_t>();
+        d->rd_rng_off = d->rd_val_off = d->rd_r2v_off = s->m_zero.as<uint32_t>();
+        return ACCORD_OK;
+    }
     d->n = s->n;
     d->kd_keys_total = s->tot_keys; d->kd_vals_total = s->tot_vals; d->kd_k2v_total = s->tot_k2v;
     d->kd_key_off = s->kd_key_off.as<uint32_t>(); d->kd_keys = s->kd_keys.as<uint32_t>();
@@ -426,15 +392,18 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
     if (!s || !out) return fail(s, ACCORD_ERR_ARG, "null argument");
     if (!s->computed) return fail(s, ACCORD_ERR_STATE, "no computed deps");
     HIPCHECK(s, hipSetDevice(s->cfg.device));
+    accord_deps v;
+    int32_t rc = accord_deps_device_view(s, &v);
+    if (rc) return rc;
     HostDepsOwner *o = new (std::nothrow) HostDepsOwner();
     if (!o) return fail(s, ACCORD_ERR_OOM, "out of host memory");
-    const size_t n1 = (size_t)s->n + 1;
+    const size_t n1 = (size_t)v.n + 1;
     try {
         o->kd_key_off.resize(n1); o->kd_val_off.resize(n1); o->kd_k2v_off.resize(n1);
-        o->kd_keys.resize(s->tot_keys + 1); o->kd_vals.resize(s->tot_vals + 1); o->kd_k2v.resize(s->tot_k2v + 1);
+        o->kd_keys.resize(v.kd_keys_total + 1); o->kd_vals.resize(v.kd_vals_total + 1); o->kd_k2v.resize(v.kd_k2v_total + 1);
         o->rd_rng_off.resize(n1); o->rd_val_off.resize(n1); o->rd_r2v_off.resize(n1);
-        o->rd_rng_start.resize(s->tot_rngs + 1); o->rd_rng_end.resize(s->tot_rngs + 1);
-        o->rd_vals.resize(s->tot_rvals + 1); o->rd_r2v.resize(s->tot_r2v + 1);
+        o->rd_rng_start.resize(v.rd_rngs_total + 1); o->rd_rng_end.resize(v.rd_rngs_total + 1);
+        o->rd_vals.resize(v.rd_vals_total + 1); o->rd_r2v.resize(v.rd_r2v_total + 1);
     } catch (...) {
         delete o;
         return fail(s, ACCORD_ERR_OOM, "out of host memory");
@@ -443,28 +412,28 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
         return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream) : hipSuccess;
     };
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = cp(o->kd_key_off.data(), s->kd_key_off.p, n1 * 4);
-    if (e == hipSuccess) e = cp(o->kd_val_off.data(), s->kd_val_off.p, n1 * 4);
-    if (e == hipSuccess) e = cp(o->kd_k2v_off.data(), s->kd_k2v_off.p, n1 * 4);
-    if (e == hipSuccess) e = cp(o->kd_keys.data(), s->kd_keys.p, s->tot_keys * 4);
-    if (e == hipSuccess) e = cp(o->kd_vals.data(), s->kd_vals.p, s->tot_vals * 4);
-    if (e == hipSuccess) e = cp(o->kd_k2v.data(), s->kd_k2v.p, s->tot_k2v * 4);
-    if (e == hipSuccess) e = cp(o->rd_rng_off.data(), s->rd_rng_off.p, n1 * 4);
-    if (e == hipSuccess) e = cp(o->rd_val_off.data(), s->rd_val_off.p, n1 * 4);
-    if (e == hipSuccess) e = cp(o->rd_r2v_off.data(), s->rd_r2v_off.p, n1 * 4);
-    if (e == hipSuccess) e = cp(o->rd_rng_start.data(), s->rd_rng_start.p, s->tot_rngs * 4);
-    if (e == hipSuccess) e = cp(o->rd_rng_end.data(), s->rd_rng_end.p, s->tot_rngs * 4);
-    if (e == hipSuccess) e = cp(o->rd_vals.data(), s->rd_vals.p, s->tot_rvals * 4);
-    if (e == hipSuccess) e = cp(o->rd_r2v.data(), s->rd_r2v.p, s->tot_r2v * 4);
+    if (e == hipSuccess) e = cp(o->kd_key_off.data(), v.kd_key_off, n1 * 4);
+    if (e == hipSuccess) e = cp(o->kd_val_off.data(), v.kd_val_off, n1 * 4);
+    if (e == hipSuccess) e = cp(o->kd_k2v_off.data(), v.kd_k2v_off, n1 * 4);
+    if (e == hipSuccess) e = cp(o->kd_keys.data(), v.kd_keys, v.kd_keys_total * 4);
+    if (e == hipSuccess) e = cp(o->kd_vals.data(), v.kd_vals, v.kd_vals_total * 4);
+    if (e == hipSuccess) e = cp(o->kd_k2v.data(), v.kd_k2v, v.kd_k2v_total * 4);
+    if (e == hipSuccess) e = cp(o->rd_rng_off.data(), v.rd_rng_off, n1 * 4);
+    if (e == hipSuccess) e = cp(o->rd_val_off.data(), v.rd_val_off, n1 * 4);
+    if (e == hipSuccess) e = cp(o->rd_r2v_off.data(), v.rd_r2v_off, n1 * 4);
+    if (e == hipSuccess) e = cp(o->rd_rng_start.data(), v.rd_rng_start, v.rd_rngs_total * 4);
+    if (e == hipSuccess) e = cp(o->rd_rng_end.data(), v.rd_rng_end, v.rd_rngs_total * 4);
+    if (e == hipSuccess) e = cp(o->rd_vals.data(), v.rd_vals, v.rd_vals_total * 4);
+    if (e == hipSuccess) e = cp(o->rd_r2v.data(), v.rd_r2v, v.rd_r2v_total * 4);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
         delete o;
         return fail(s, ACCORD_ERR_HIP, "download: %s", hipGetErrorString(e));
     }
     std::memset(out, 0, sizeof(*out));
-    out->n = s->n;
-    out->kd_keys_total = s->tot_keys; out->kd_vals_total = s->tot_vals; out->kd_k2v_total = s->tot_k2v;
-    out->rd_rngs_total = s->tot_rngs; out->rd_vals_total = s->tot_rvals; out->rd_r2v_total = s->tot_r2v;
+    out->n = v.n;
+    out->kd_keys_total = v.kd_keys_total; out->kd_vals_total = v.kd_vals_total; out->kd_k2v_total = v.kd_k2v_total;
+    out->rd_rngs_total = v.rd_rngs_total; out->rd_vals_total = v.rd_vals_total; out->rd_r2v_total = v.rd_r2v_total;
     out->kd_key_off = o->kd_key_off.data(); out->kd_keys = o->kd_keys.data();
     out->kd_val_off = o->kd_val_off.data(); out->kd_vals = o->kd_vals.data();
     out->kd_k2v_off = o->kd_k2v_off.data(); out->kd_k2v = o->kd_k2v.data();

@@ -1,0 +1,92 @@
+// Private definition of accord_store shared by the C ABI translation units.
+#pragma once
+#include "../../include/accord_deps.h"
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+namespace accord_impl {
+
+extern thread_local std::string g_last_error;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes)
+    {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <typename T> T *as() const { return (T *)p; }
+};
+
+struct HostTotals {
+    accord::DevStatus status;
+    unsigned long long totals[8];   // kd keys, kd vals, kd k2v, rd ranges, rd vals, rd r2v, range txns
+};
+
+} // namespace accord_impl
+using accord_impl::DevBuf;
+using accord_impl::HostTotals;
+
+enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_RANGE,
+             EV_XCHG_START, EV_XCHG_END, EV_MERGE_END, EV_COUNT_ALL };
+
+struct ShardComm;   // RCCL communicator + exchange buffers (shard.cpp)
+
+struct accord_store {
+    accord_store_cfg cfg{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    // batch (device)
+    uint32_t n = 0, P = 0, R = 0;
+    bool has_batch = false, computed = false;
+    DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
+    // work
+    DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
+    DevBuf hist, poslo, hist_tmp;
+    DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
+    DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v;
+    uint32_t n_range_txns = 0;
+    uint64_t tot_rngs = 0, tot_rvals = 0, tot_r2v = 0;
+    DevBuf cnt_keys, cnt_vals, cnt_k2v, kd_key_off, kd_val_off, kd_k2v_off, scan_tmp, status_totals;
+    // outputs
+    DevBuf kd_keys, kd_vals, kd_k2v, rd_zero_off;  // rd_zero_off: unused, kept for ABI-compatible views
+    uint64_t tot_keys = 0, tot_vals = 0, tot_k2v = 0;
+    DevBuf txn_index;              // global stream positions (nullptr = identity)
+    bool has_txn_index = false;
+    // merged (K6) result: replaces the computed partial as the store's current deps
+    bool merged = false;
+    uint32_t m_n = 0, m_txn_lo = 0;
+    DevBuf m_key_off, m_val_off, m_k2v_off, m_keys, m_vals, m_k2v, m_cnt_keys, m_cnt_vals, m_cnt_k2v, m_ptrs, m_zero;
+    uint64_t m_tot_keys = 0, m_tot_vals = 0, m_tot_k2v = 0;
+    float xchg_ms = 0, merge_ms = 0;
+    ShardComm *comm = nullptr;
+    HostTotals *pinned = nullptr;
+    hipEvent_t ev[EV_COUNT_ALL] = {};
+    bool events = false;
+    accord_timing timing{};
+    int wpl = 1;
+};
+
+
+namespace accord_impl {
+int32_t fail(accord_store *s, int32_t code, const char *fmt, ...);
+void shard_comm_destroy(accord_store *s);
+}
+using accord_impl::fail;
+
+#define HIPCHECK(s, expr)                                                                             \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) return fail((s), ACCORD_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)

@@ -74,6 +74,11 @@ typedef struct {
     const uint32_t *rng_off;    /* [n+1] CSR into rng_start/rng_end, or NULL (no range txns) */
     const uint32_t *rng_start;
     const uint32_t *rng_end;
+    /* [n] global stream position of each txn, strictly ascending, or NULL (= 0..n-1).  A store
+     * that receives only the txns intersecting its keys (CommandStores.mapReduce,
+     * local/CommandStores.java:575-592) passes their positions so the status-at-time window and
+     * the deps values (txnIds) stay in global stream coordinates.  Key txns only. */
+    const uint32_t *txn_index;
 } accord_batch;
 
 /* Per-txn PartialDeps, exact reference layout (KeyDeps.java:150-187, RangeDeps.java:81-99):
@@ -120,6 +125,23 @@ int32_t accord_deps_compute(accord_store *store);          /* enqueue + run the 
 int32_t accord_deps_device_view(accord_store *store, accord_deps *dev);  /* device pointers */
 int32_t accord_deps_download(accord_store *store, accord_deps *out);     /* D2H copy, host-owned */
 int32_t accord_store_timing(accord_store *store, accord_timing *t);
+
+/* ---- union of per-store partials (K6; PreAccept.reduce, messages/PreAccept.java:140-156) ----
+ * parts: G device views (accord_deps_device_view of stores on this GPU, or received buffers) of
+ * the same n txns, with key-disjoint parts ordered by key (CommandStores partition the keyspace).
+ * The union becomes this store's current deps (read with device_view / download); txnIds are
+ * global stream positions and txn_lo is the global position of txn 0 of the parts. */
+int32_t accord_deps_merge(accord_store *store, uint32_t nparts, const accord_deps *parts, uint32_t txn_lo);
+
+/* ---- multi-GPU: one store per rank over RCCL (xGMI) ----
+ * Rank r holds the partial deps of its key block for the txns intersecting it (batch txn_index =
+ * global stream positions).  accord_deps_exchange_merge sends every partial to the rank owning
+ * the txn (txn g -> rank floor(g*G/n_total)) with one grouped RCCL send/recv and unions the G parts
+ * there; afterwards the store's current deps are the full (node-level) deps of its own txns. */
+int32_t accord_comm_unique_id(void *id128);                  /* ncclGetUniqueId, 128 bytes */
+int32_t accord_comm_init(accord_store *store, int32_t nranks, int32_t rank, const void *id128);
+int32_t accord_deps_exchange_merge(accord_store *store, uint32_t n_total);
+int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merge_ms);
 
 /* ---- synthetic workload (SURVEY.md §8d stream; splitmix64 + Zipf rejection-inversion) ---- */
 typedef struct {
