@@ -37,10 +37,19 @@ def algorithmic_bytes(n, P, kc, U, D):
 
 
 def fill_kernel_bytes(n, P, kc, U, D):
-    """Algorithmic bytes of ONE launch of the fill kernel (keydeps_kernel<*, true>): reads lsb
-    (8N), key_off (4(N+1)), key_ord (4P), seg_start/seg_end (8P), each raw candidate once (4D),
-    the three offset arrays (12(N+1)); writes keys (4kc), txnIds (4U), keysToTxnIds (4(kc+D))."""
-    return 8 * n + 4 * (n + 1) + 4 * P + 8 * P + 4 * D + 12 * (n + 1) + 4 * kc + 4 * U + 4 * (kc + D)
+    """Algorithmic bytes of ONE launch of the fill kernel (keydeps_kernel<*>): reads lsb (8N),
+    key_off (4(N+1)), key_ord (4P), the pair slices poslo (8P), each raw candidate once (4D), the
+    three offset arrays (12(N+1)); writes the txnIds count (4N), keys (4kc), txnIds (4U) and
+    keysToTxnIds (4(kc+D))."""
+    return 8 * n + 4 * (n + 1) + 4 * P + 8 * P + 4 * D + 12 * (n + 1) + 4 * n + 4 * kc + 4 * U + 4 * (kc + D)
+
+
+# SURVEY.md §8d workloads
+PRESETS = {
+    2: dict(n=1 << 20, keys_per_txn=8, keyspace=100_000, seed=2, range_frac=0.0, write_frac=0.5),
+    3: dict(n=1 << 20, keys_per_txn=8, keyspace=100_000, seed=3, range_frac=0.2, write_frac=0.5),
+    5: dict(n=1 << 22, keys_per_txn=4, keyspace=10_000, seed=5, range_frac=0.0, write_frac=0.9),
+}
 
 
 def main():
@@ -48,18 +57,28 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1 << 20)
-    ap.add_argument("--keys-per-txn", type=int, default=8)
-    ap.add_argument("--keyspace", type=int, default=100_000)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 5),
+                    help="BASELINE.json configs[1] (2), configs[2] (3: 20%% range txns), configs[4] "
+                         "(5: 4M txns, deep chains, + WaitingOn levelling)")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--keys-per-txn", type=int, default=None)
+    ap.add_argument("--keyspace", type=int, default=None)
     ap.add_argument("--zipf", type=float, default=0.99)
     ap.add_argument("--window", type=int, default=256)
-    ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--range-frac", type=float, default=0.0, help="config 3: 0.2")
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--range-frac", type=float, default=None)
     ap.add_argument("--range-len", type=int, default=1000)
-    ap.add_argument("--write-frac", type=float, default=0.5)
-    ap.add_argument("--cpu-sample", type=int, default=24_000, help="txns of the CPU-baseline prefix sample")
+    ap.add_argument("--write-frac", type=float, default=None)
+    ap.add_argument("--cpu-sample", type=int, default=None, help="txns of the CPU-baseline prefix sample")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    preset = PRESETS[args.config]
+    for k, v in preset.items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    args.waiting_on = args.config == 5
+    if args.cpu_sample is None:
+        args.cpu_sample = 24_000
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -91,10 +110,15 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         store.comm_init(world, rank, uid[0])
 
+    if args.waiting_on and world > 1:
+        raise SystemExit("config 5 levels one full stream per GPU (replicas only): run it with --gpus 1")
+
     def step():
         store.compute()
         if world > 1:
             store.exchange_merge(n_total)
+        if args.waiting_on:
+            store.waiting_on_compute()
 
     for _ in range(args.warmup):
         step()
@@ -109,7 +133,7 @@ def main():
     hip.hipDeviceSynchronize()
     t0 = time.perf_counter()
     stage = {"validate": 0.0, "sort": 0.0, "segment": 0.0, "count": 0.0, "scan": 0.0, "fill": 0.0, "range_fill": 0.0,
-             "total": 0.0, "exchange": 0.0, "merge": 0.0}
+             "compact": 0.0, "total": 0.0, "exchange": 0.0, "merge": 0.0, "wo_bits": 0.0, "wo_preds": 0.0, "wo_level": 0.0}
     for _ in range(args.steps):
         step()
         t = store.timing()
@@ -120,11 +144,17 @@ def main():
         stage["scan"] += t.scan_ms
         stage["fill"] += t.fill_ms
         stage["range_fill"] += t.range_ms
+        stage["compact"] += t.compact_ms
         stage["total"] += t.total_ms
         if world > 1:
             xms, mms = store.shard_timing()
             stage["exchange"] += xms
             stage["merge"] += mms
+        if args.waiting_on:
+            a, b, c = store.waiting_on_timing()
+            stage["wo_bits"] += a
+            stage["wo_preds"] += b
+            stage["wo_level"] += c
     hip.hipDeviceSynchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -144,6 +174,11 @@ def main():
     kc = int(view["kd_keys_total"])
     U = int(view["kd_vals_total"])
     D = int(view["kd_k2v_total"]) - kc
+    wo_info = None
+    if args.waiting_on:
+        wo = store.waiting_on()
+        wo_info = {"max_level": wo.max_level, "reduced_edges": wo.preds_total,
+                   "bitset_words": int(wo.wo_off[-1]), "level_histogram_top": int(np.bincount(wo.level).max())}
 
     if rank != 0:
         store.close()
@@ -192,6 +227,8 @@ def main():
                               "formula": "SURVEY.md §8d B / device time of the whole pipeline"},
         "cpu_baseline": cpu,
     }
+    if wo_info is not None:
+        line["waiting_on"] = wo_info
     print(json.dumps(line))
     store.close()
     if dist is not None:
@@ -199,6 +236,10 @@ def main():
 
 
 def workload_name(args):
+    if args.waiting_on:
+        return (f"config5: {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over {args.keyspace} "
+                f"keys, {args.write_frac:.0%} writes, W={args.window}; deps + WaitingOn bitsets + levelling "
+                f"(all STABLE, executeAt = txnId)")
     if args.range_frac > 0:
         return (f"config3: {args.n} txns ({args.range_frac:.0%} range txns, 1-2 ranges len<= {args.range_len}), "
                 f"{args.keys_per_txn} keys/key txn, Zipf({args.zipf}) over {args.keyspace} keys, W={args.window}")
@@ -206,20 +247,48 @@ def workload_name(args):
             f"{args.write_frac:.0%} writes, W={args.window}")
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(s, args):
     """The oracle's literal restatement of the reference algorithm (sorted-array CommandsForKey
     copied/re-sorted on every status change, linear mapReduceActive scan, RelationMultiMap
-    builder) on the first --cpu-sample txns of the same stream, 1 thread."""
+    builder) on the first --cpu-sample txns of the same stream.  Key-only streams run the
+    reference's threading model: S = 8 CommandStores (EvenSplit of the keyspace), one thread per
+    store (impl/InMemoryCommandStore.java:1131-1148); ctypes releases the GIL for each store's
+    call.  The per-store partials are not unioned (the coordinator's job), which favours the CPU."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
+        from concurrent.futures import ThreadPoolExecutor
         m = min(args.cpu_sample, s.n)
+        pre = s.prefix(m)
+        multi = int(pre.rng_off[-1]) == 0 and not args.waiting_on
+        threads = min(8, os.cpu_count() or 1) if multi else 1
         t0 = time.perf_counter()
-        oracle_lib.deps_literal(s, args.window, limit=m)
+        if multi:
+            stores = [pre.restrict_keys(b * args.keyspace // 8, (b + 1) * args.keyspace // 8) for b in range(8)]
+            with ThreadPoolExecutor(threads) as ex:
+                list(ex.map(lambda st: oracle_lib.deps_literal(st, args.window), stores))
+        else:
+            d = oracle_lib.deps_literal(pre, args.window)
+            if args.waiting_on:
+                oracle_lib.waiting_on(d)
         dt = time.perf_counter() - t0
-        return {"value": m / dt, "unit": "txns/s", "cores": 1, "kind": "port",
-                "sample": f"first {m} txns of the config-2 stream (literal reference algorithm, "
-                          f"{dt:.1f} s; CFK history grows with the prefix so the full 1M run would be slower)"}
+        how = (f"8 stores on {threads} threads" if multi else "1 store, 1 thread") + \
+              (" + levelling" if args.waiting_on else "")
+        return {"value": m / dt, "unit": "txns/s", "cores": threads, "kind": "port",
+                "sample": f"first {m} txns of the config-{args.config} stream, literal reference algorithm, "
+                          f"{how}, {dt:.1f} s; CFK histories grow with the prefix so the full run would be slower",
+                "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "txns/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
 

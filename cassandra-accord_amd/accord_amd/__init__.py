@@ -24,7 +24,7 @@ import numpy as np
 
 __all__ = [
     "AccordError", "IllegalStateException", "IllegalArgumentException", "lib", "lib_path",
-    "Stream", "generate_stream", "CommandStore", "PartialDeps", "Timing",
+    "Stream", "generate_stream", "CommandStore", "PartialDeps", "Timing", "WaitingOn",
     "txn_id_str", "keydeps_str", "rangedeps_str", "EXPORTED_SYMBOLS",
 ]
 
@@ -45,6 +45,8 @@ EXPORTED_SYMBOLS = [
     "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
     "accord_comm_init", "accord_deps_exchange_merge", "accord_shard_timing",
+    "accord_waiting_on_compute", "accord_waiting_on_download", "accord_waiting_on_release",
+    "accord_waiting_on_timing",
 ]
 
 
@@ -96,10 +98,17 @@ class _Deps(C.Structure):
                 ("owner", C.c_void_p)]
 
 
+class _WaitingOn(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("max_level", C.c_uint32), ("words_total", C.c_uint64),
+                ("preds_total", C.c_uint64), ("level", _u32p), ("wo_off", _u32p), ("words", _u64p),
+                ("owner", C.c_void_p)]
+
+
 class _Timing(C.Structure):
     _fields_ = [("validate_ms", C.c_float), ("sort_ms", C.c_float), ("segment_ms", C.c_float),
                 ("count_ms", C.c_float), ("scan_ms", C.c_float), ("fill_ms", C.c_float),
                 ("range_ms", C.c_float), ("total_ms", C.c_float),
+                ("compact_ms", C.c_float), ("reserved_ms", C.c_float),
                 ("pairs", C.c_uint64), ("hist_entries", C.c_uint64)]
 
 
@@ -142,6 +151,11 @@ def lib() -> C.CDLL:
         L.accord_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
         L.accord_deps_exchange_merge.argtypes = [C.c_void_p, C.c_uint32]
         L.accord_shard_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.accord_waiting_on_compute.argtypes = [C.c_void_p]
+        L.accord_waiting_on_download.argtypes = [C.c_void_p, C.POINTER(_WaitingOn)]
+        L.accord_waiting_on_release.argtypes = [C.POINTER(_WaitingOn)]
+        L.accord_waiting_on_release.restype = None
+        L.accord_waiting_on_timing.argtypes = [C.c_void_p] + [C.POINTER(C.c_float)] * 3
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
             if f.restype is C.c_int:  # default
@@ -333,6 +347,20 @@ class PartialDeps:
 
 
 @dataclass
+class WaitingOn:
+    """Per-txn WaitingOn bitsets (Command.WaitingOn, local/Command.java:1403-1437: range-dep txn
+    bits, then key bits) and execution levels."""
+    level: np.ndarray
+    wo_off: np.ndarray
+    words: np.ndarray
+    max_level: int
+    preds_total: int
+
+    def bits(self, i: int) -> np.ndarray:
+        return self.words[self.wo_off[i]:self.wo_off[i + 1]]
+
+
+@dataclass
 class Timing:
     validate_ms: float
     sort_ms: float
@@ -344,6 +372,7 @@ class Timing:
     total_ms: float
     pairs: int
     hist_entries: int
+    compact_ms: float = 0.0
 
 
 class CommandStore:
@@ -451,11 +480,35 @@ class CommandStore:
         self._check(lib().accord_shard_timing(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def waiting_on_compute(self):
+        """WaitingOn bitsets + execution levels of the computed deps (device-resident)."""
+        self._check(lib().accord_waiting_on_compute(self._h))
+
+    def waiting_on_download(self) -> "WaitingOn":
+        w = _WaitingOn()
+        self._check(lib().accord_waiting_on_download(self._h, C.byref(w)))
+        try:
+            return WaitingOn(level=_arr(w.level, w.n, np.uint32).copy(),
+                             wo_off=_arr(w.wo_off, w.n + 1, np.uint32).copy(),
+                             words=_arr(w.words, w.words_total, np.uint64).copy(),
+                             max_level=int(w.max_level), preds_total=int(w.preds_total))
+        finally:
+            lib().accord_waiting_on_release(C.byref(w))
+
+    def waiting_on(self) -> "WaitingOn":
+        self.waiting_on_compute()
+        return self.waiting_on_download()
+
+    def waiting_on_timing(self):
+        a, b, c = C.c_float(), C.c_float(), C.c_float()
+        self._check(lib().accord_waiting_on_timing(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
     def timing(self) -> Timing:
         t = _Timing()
         self._check(lib().accord_store_timing(self._h, C.byref(t)))
         return Timing(t.validate_ms, t.sort_ms, t.segment_ms, t.count_ms, t.scan_ms, t.fill_ms, t.range_ms,
-                      t.total_ms, t.pairs, t.hist_entries)
+                      t.total_ms, t.pairs, t.hist_entries, t.compact_ms)
 
 
 # ---------------------------------------------------------------- string forms

@@ -36,11 +36,10 @@ struct KeyDepsParams {
     uint32_t window;
     const uint32_t *hist;              // key-major history entries (kind<<29 | global txn)
     const unsigned long long *poslo;   // txn-major per pair: (slice start << 32) | history position
-    // count outputs
-    uint32_t *cnt_keys, *cnt_vals, *cnt_k2v;
-    // fill inputs/outputs
-    const uint32_t *kd_key_off, *kd_val_off, *kd_k2v_off;
-    uint32_t *kd_keys, *kd_vals;
+    const uint32_t *cnt_vub;           // txnIds upper bound per txn (sizes pass / rangekeys count)
+    uint32_t *cnt_vals;                // out: exact txnIds count per txn
+    const uint32_t *kd_key_off, *vub_off, *kd_k2v_off;
+    uint32_t *kd_keys, *vgap;          // txnIds land at vgap[vub_off[i] ..], compacted afterwards
     int32_t *kd_k2v;
     DevStatus *status;
 };
@@ -55,13 +54,19 @@ void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
 void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s);
 size_t history_temp_bytes(uint32_t P);
 // key-major: history entries, segments, and per pair the [lo, pos) deps slice (txn-major poslo)
+// with its witnessed-entry count (txn-major wcnt)
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, unsigned long long *poslo, void *temp, hipStream_t s);
+                    uint32_t *seg_end, unsigned long long *poslo, uint32_t *wcnt, void *temp, hipStream_t s);
 // history tile size of the Write max-scan carry (pw_local / pw_carry)
 constexpr uint32_t HISTORY_TILE = 4096;
-void launch_keydeps_count(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
+// per txn: keys, txnIds upper bound and keysToTxnIds sizes from wcnt (no history scan)
+void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const uint32_t *wcnt, uint32_t *cnt_keys,
+                          uint32_t *cnt_vub, uint32_t *cnt_k2v, DevStatus *status, hipStream_t s);
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
+// vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
+void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
+                         uint32_t *vals, hipStream_t s);
 
 // ---- range txns (rangedeps.hip) ----
 struct RangeDepsParams {
@@ -117,5 +122,30 @@ void launch_expand_offsets(uint32_t n, uint32_t n_total, const uint32_t *txn_ind
 // bnd[a*(G+1) + d] = exp_off[a][d * n_total / G]
 void launch_boundaries(uint32_t G, uint32_t n_total, uint32_t *const exp_off[3], uint32_t *bnd, hipStream_t s);
 void launch_merge_fill(const MergeParams &p, hipStream_t s);
+
+// ---- WaitingOn bitsets + execution levelling (waiting_on.hip) ----
+struct WaitingOnParams {
+    uint32_t n;
+    const uint64_t *lsb;
+    const uint32_t *key_off;                       // txn-major pairs (poslo index)
+    const unsigned long long *poslo;
+    const uint32_t *hist, *pw_local, *pw_carry;
+    uint32_t pw_tile;
+    const uint32_t *kd_val_off, *kd_vals;          // full KeyDeps (non-reduced txns)
+    const uint32_t *rd_val_off, *rd_vals;          // RangeDeps txnIds
+    uint32_t *pred_cnt;
+    const uint32_t *pred_off;
+    uint32_t *preds;
+};
+void launch_wo_words_count(uint32_t n, const uint32_t *kd_key_off, const uint32_t *rd_val_off, uint32_t *cnt,
+                           hipStream_t s);
+void launch_wo_bits(uint32_t n, const uint32_t *kd_key_off, const uint32_t *rd_val_off, const uint32_t *wo_off,
+                    unsigned long long *words, hipStream_t s);
+void launch_wo_preds_count(const WaitingOnParams &p, hipStream_t s);
+void launch_wo_preds_fill(const WaitingOnParams &p, hipStream_t s);
+// level[i] for all i; info[0] = 1 + chunk that hit the defensive round bound (must stay 0),
+// info[1] = max level.  info must be zeroed before the launch.
+void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level, uint32_t *info,
+                   hipStream_t s);
 
 } // namespace accord

@@ -131,22 +131,51 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
     return v;
 }
 
+// Packed per-position class counters (16-bit fields, tile-local): Writes | Reads << 16 |
+// EphemeralReads << 32.  With the tile carries they give, for any history range, the number of
+// entries a txn kind witnesses (Ws = #W, RsOrWs = #W + #R, AnyGloballyVisible = len - #ER).
+__device__ __forceinline__ uint64_t class_bits(uint32_t kind)
+{
+    return kind == 1u ? 1ull : kind == 0u ? (1ull << 16) : kind == 2u ? (1ull << 32) : 0ull;
+}
+
+struct ClassCarry {
+    uint32_t w, r, er, pad;
+};
+
+// entries of [0, x] (global positions) witnessed by wmask
+__device__ __forceinline__ uint32_t witnessed_upto(const uint64_t *__restrict__ c_local,
+                                                   const ClassCarry *__restrict__ ccarry, uint32_t x, uint32_t wmask)
+{
+    const uint64_t c = c_local[x];
+    const ClassCarry cc = ccarry[x / HS_TILE];
+    const uint32_t w = (uint32_t)(c & 0xFFFFu) + cc.w;
+    if (wmask == 0x2u) return w;
+    if (wmask == 0x3u) return w + (uint32_t)((c >> 16) & 0xFFFFu) + cc.r;
+    return x + 1 - ((uint32_t)((c >> 32) & 0xFFFFu) + cc.er);
+}
+
 // hist[p] = entry of sorted pair p; segment bounds per key; tile-local inclusive max-scan of
-// (p+1 if entry p is a Write) -> the last Write at or before p, completed by a tile carry.
+// (p+1 if entry p is a Write) -> the last Write at or before p, and tile-local inclusive class
+// counts; both completed by tile carries.
 __global__ __launch_bounds__(HS_THREADS) void history1_kernel(uint32_t P, const uint32_t *__restrict__ sorted_key,
                                                               const uint32_t *__restrict__ sorted_pair,
                                                               const uint32_t *__restrict__ pair_ent,
                                                               uint32_t *__restrict__ hist, uint32_t *__restrict__ seg_start,
                                                               uint32_t *__restrict__ seg_end, uint32_t *__restrict__ pw_local,
-                                                              uint32_t *__restrict__ tile_max)
+                                                              uint32_t *__restrict__ tile_max, uint64_t *__restrict__ c_local,
+                                                              uint64_t *__restrict__ tile_cnt)
 {
     __shared__ uint32_t tile[HS_TILE];
+    __shared__ uint64_t ctile[HS_TILE];
     __shared__ uint32_t wmax[HS_THREADS / 64];
+    __shared__ uint64_t wcnt[HS_THREADS / 64];
     const uint32_t tid = threadIdx.x, base = blockIdx.x * HS_TILE;
 #pragma unroll 4
     for (int j = 0; j < HS_ITEMS; ++j) {
         const uint32_t p = base + j * HS_THREADS + tid;
         uint32_t v = 0;
+        uint64_t c = 0;
         if (p < P) {
             const uint32_t e = pair_ent[sorted_pair[p]];
             hist[p] = e;
@@ -154,74 +183,107 @@ __global__ __launch_bounds__(HS_THREADS) void history1_kernel(uint32_t P, const 
             if (p == 0 || sorted_key[p - 1] != k) seg_start[k] = p;
             if (p == P - 1 || sorted_key[p + 1] != k) seg_end[k] = p + 1;
             v = (e >> ENT_KIND_SHIFT) == 1u ? p + 1 : 0u;
+            c = class_bits(e >> ENT_KIND_SHIFT);
         }
         tile[j * HS_THREADS + tid] = v;
+        ctile[j * HS_THREADS + tid] = c;
     }
     __syncthreads();
     uint32_t run = 0;
+    uint64_t csum = 0;
 #pragma unroll
-    for (int j = 0; j < HS_ITEMS; ++j) run = max(run, tile[tid * HS_ITEMS + j]);
+    for (int j = 0; j < HS_ITEMS; ++j) {
+        run = max(run, tile[tid * HS_ITEMS + j]);
+        csum += ctile[tid * HS_ITEMS + j];
+    }
     const uint32_t incl = wave_incl_max(run);
-    if (lane_id() == 63) wmax[tid >> 6] = incl;
+    const uint64_t cincl = wave_incl_scan64(csum);
+    if (lane_id() == 63) { wmax[tid >> 6] = incl; wcnt[tid >> 6] = cincl; }
     __syncthreads();
     uint32_t ex = __shfl_up(incl, 1, 64);
+    uint64_t cex = cincl - csum;
     if (lane_id() == 0) ex = 0;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) ex = max(ex, wmax[w]);
+    for (uint32_t w = 0; w < (tid >> 6); ++w) { ex = max(ex, wmax[w]); cex += wcnt[w]; }
 #pragma unroll
     for (int j = 0; j < HS_ITEMS; ++j) {
         ex = max(ex, tile[tid * HS_ITEMS + j]);
         tile[tid * HS_ITEMS + j] = ex;
+        cex += ctile[tid * HS_ITEMS + j];
+        ctile[tid * HS_ITEMS + j] = cex;
     }
     __syncthreads();
 #pragma unroll 4
     for (int j = 0; j < HS_ITEMS; ++j) {
         const uint32_t p = base + j * HS_THREADS + tid;
-        if (p < P) pw_local[p] = tile[j * HS_THREADS + tid];
+        if (p < P) {
+            pw_local[p] = tile[j * HS_THREADS + tid];
+            c_local[p] = ctile[j * HS_THREADS + tid];
+        }
     }
     if (tid == 0) {
         uint32_t m = 0;
-        for (uint32_t w = 0; w < HS_THREADS / 64; ++w) m = max(m, wmax[w]);
+        uint64_t c = 0;
+        for (uint32_t w = 0; w < HS_THREADS / 64; ++w) { m = max(m, wmax[w]); c += wcnt[w]; }
         tile_max[blockIdx.x] = m;
+        tile_cnt[blockIdx.x] = c;
     }
 }
 
-// exclusive max-scan of the tile maxima (one block)
-__global__ __launch_bounds__(256) void history_carry_kernel(uint32_t *__restrict__ tile_max, uint32_t tiles)
+// exclusive max-scan of the tile maxima and exclusive sum-scan of the tile class counts (one block)
+__global__ __launch_bounds__(256) void history_carry_kernel(uint32_t *__restrict__ tile_max,
+                                                            const uint64_t *__restrict__ tile_cnt,
+                                                            ClassCarry *__restrict__ ccarry, uint32_t tiles)
 {
     __shared__ uint32_t wmax[4];
-    uint32_t carry = 0;
+    __shared__ uint32_t wsum[3][4];
+    uint32_t carry = 0, cw = 0, cr = 0, ce = 0;
     for (uint32_t base = 0; base < tiles; base += 256) {
         const uint32_t i = base + threadIdx.x;
         const uint32_t v = i < tiles ? tile_max[i] : 0u;
+        const uint64_t c = i < tiles ? tile_cnt[i] : 0ull;
+        const uint32_t vw = (uint32_t)(c & 0xFFFFu), vr = (uint32_t)((c >> 16) & 0xFFFFu), ve = (uint32_t)((c >> 32) & 0xFFFFu);
         const uint32_t incl = wave_incl_max(v);
-        if (lane_id() == 63) wmax[threadIdx.x >> 6] = incl;
+        const uint32_t iw = wave_incl_scan(vw), ir = wave_incl_scan(vr), ie = wave_incl_scan(ve);
+        const uint32_t wv = threadIdx.x >> 6;
+        if (lane_id() == 63) { wmax[wv] = incl; wsum[0][wv] = iw; wsum[1][wv] = ir; wsum[2][wv] = ie; }
         __syncthreads();
         uint32_t ex = __shfl_up(incl, 1, 64);
         if (lane_id() == 0) ex = 0;
-        uint32_t blk = 0;
+        uint32_t xw = iw - vw, xr = ir - vr, xe = ie - ve;
+        uint32_t blk = 0, bw = 0, br = 0, be = 0;
         for (uint32_t w = 0; w < 4; ++w) {
-            if (w < (threadIdx.x >> 6)) ex = max(ex, wmax[w]);
+            if (w < wv) { ex = max(ex, wmax[w]); xw += wsum[0][w]; xr += wsum[1][w]; xe += wsum[2][w]; }
             blk = max(blk, wmax[w]);
+            bw += wsum[0][w]; br += wsum[1][w]; be += wsum[2][w];
         }
-        if (i < tiles) tile_max[i] = max(carry, ex);
+        if (i < tiles) {
+            tile_max[i] = max(carry, ex);
+            ccarry[i] = ClassCarry{cw + xw, cr + xr, ce + xe, 0u};
+        }
         carry = max(carry, blk);
+        cw += bw; cr += br; ce += be;
         __syncthreads();
     }
 }
 
 // Per history entry p (txn i on key k): the deps slice [lo, p) of (i, k) under the status-at-time
 // model.  lo = the last Write entry j < i-W of the segment (committed[] bound of
-// CommandsForKey.mapReduceActive :620-645), else the segment start.  Written txn-major.
+// CommandsForKey.mapReduceActive :620-645), else the segment start.  Written txn-major, with the
+// number of slice entries kind(i) witnesses (the pair's share of keysToTxnIds).
 __global__ __launch_bounds__(256) void history2_kernel(uint32_t P, uint32_t window, const uint32_t *__restrict__ sorted_key,
                                                        const uint32_t *__restrict__ sorted_pair,
                                                        const uint32_t *__restrict__ hist,
                                                        const uint32_t *__restrict__ seg_start,
                                                        const uint32_t *__restrict__ pw_local,
                                                        const uint32_t *__restrict__ carry,
-                                                       unsigned long long *__restrict__ poslo)
+                                                       const uint64_t *__restrict__ c_local,
+                                                       const ClassCarry *__restrict__ ccarry,
+                                                       unsigned long long *__restrict__ poslo,
+                                                       uint32_t *__restrict__ wcnt)
 {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-        const uint32_t i = hist[p] & ENT_TXN_MASK;
+        const uint32_t ent = hist[p];
+        const uint32_t i = ent & ENT_TXN_MASK;
         const uint32_t a = seg_start[sorted_key[p]];
         uint32_t lo = a;
         if (i > window) {
@@ -245,7 +307,42 @@ __global__ __launch_bounds__(256) void history2_kernel(uint32_t P, uint32_t wind
                 if (pw > a) lo = pw - 1;
             }
         }
-        poslo[sorted_pair[p]] = ((unsigned long long)lo << 32) | p;
+        uint32_t cnt = 0;
+        if (p > lo) {
+            const uint32_t wmask = witness_mask(ent >> ENT_KIND_SHIFT);
+            cnt = witnessed_upto(c_local, ccarry, p - 1, wmask) - (lo ? witnessed_upto(c_local, ccarry, lo - 1, wmask) : 0u);
+        }
+        const uint32_t q = sorted_pair[p];
+        poslo[q] = ((unsigned long long)lo << 32) | p;
+        wcnt[q] = cnt;
+    }
+}
+
+// Per key txn: KeyDeps sizes from the per-pair witnessed counts.  keys = pairs with >= 1
+// witnessed entry, keysToTxnIds = keys + body; txnIds <= body (an upper bound: the fill pass
+// writes the exact count and the values are compacted afterwards).
+__global__ __launch_bounds__(256) void keydeps_sizes_kernel(uint32_t n, const uint32_t *__restrict__ key_off,
+                                                            const uint32_t *__restrict__ wcnt,
+                                                            uint32_t *__restrict__ cnt_keys,
+                                                            uint32_t *__restrict__ cnt_vub,
+                                                            uint32_t *__restrict__ cnt_k2v, DevStatus *status)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t k0 = key_off[i], k1 = key_off[i + 1];
+        uint32_t kc = 0, body = 0;
+        if (k1 - k0 > KD_KCAP) {
+            atomicAdd(&status->overflow, 1u);
+            atomicMin(&status->overflow_first, i);
+        } else {
+            for (uint32_t q = k0; q < k1; ++q) {
+                const uint32_t c = wcnt[q];
+                kc += c ? 1u : 0u;
+                body += c;
+            }
+        }
+        cnt_keys[i] = kc;
+        cnt_vub[i] = body;
+        cnt_k2v[i] = kc + body;
     }
 }
 
@@ -289,6 +386,7 @@ __device__ __forceinline__ void load_batch(const KeyDepsParams &p, const WaveLds
         const uint32_t r = r0 + c * 64 + lane;
         e[c] = 0xFFFFFFFFu;               // sentinel: kind 7 is never witnessed
         sl[c] = s;
+        if (r0 + c * 64 >= raw_total) continue;     // wave-uniform: no candidates left
         if (r < raw_total) {
             while (L.slot_rawbase[s + 1] <= r) ++s;
             sl[c] = s;
@@ -300,7 +398,7 @@ __device__ __forceinline__ void load_batch(const KeyDepsParams &p, const WaveLds
 // One wave builds one txn's KeyDeps.  Per txn the wave needs ONE memory round trip for its
 // candidates: the next txn's history slices (poslo) and the one after's offsets are prefetched
 // while the current txn is processed (vmcnt retires in order, so they ride with it).
-template <int WPL, bool FILL>
+template <int WPL>
 __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
 {
     __shared__ WaveLds<WPL> lds_all[KD_WAVES];
@@ -324,20 +422,16 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
         const uint32_t k0 = m0.k0, k = m0.k1 - m0.k0;
         const uint32_t wmask = witness_mask((uint32_t)(m0.lsb >> 1) & 7);
         uint32_t my_key = 0;
-        if (FILL && lane < k && k <= KD_KCAP) my_key = p.key_ord[k0 + lane];
+        if (lane < k && k <= KD_KCAP) my_key = p.key_ord[k0 + lane];
         const unsigned long long pl = pl0;
         m0 = m1; m1 = m2; pl0 = pl1;
 
-        if (k > KD_KCAP) {
-            if (!FILL && lane == 0) {
-                atomicAdd(&p.status->overflow, 1u);
-                atomicMin(&p.status->overflow_first, i);
-                p.cnt_keys[i] = 0; p.cnt_vals[i] = 0; p.cnt_k2v[i] = 0;
-            }
+        if (k > KD_KCAP) {                              // reported by the sizes pass
+            if (lane == 0) p.cnt_vals[i] = 0;
             continue;
         }
-        if (k == 0) {                                   // range txn / no key in this store
-            if (!FILL && lane == 0) { p.cnt_keys[i] = 0; p.cnt_vals[i] = 0; p.cnt_k2v[i] = 0; }
+        if (k == 0) {                                   // range txn (sized by rangekeys) / no key here
+            if (lane == 0) p.cnt_vals[i] = p.cnt_vub[i];
             continue;
         }
         const uint32_t gi = p.txn_index ? p.txn_index[i] : i;   // global stream position
@@ -362,15 +456,14 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
         const int64_t base = (int64_t)gi - (int64_t)SPAN;
         const bool one_batch = raw_total <= 64u * KD_CB;
         uint32_t e[KD_CB], sl[KD_CB];
-        uint32_t witnessed_here = 0;
         for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
             load_batch<WPL>(p, L, r0, raw_total, e, sl, lane);
 #pragma unroll
             for (int c = 0; c < KD_CB; ++c) {
+                if (r0 + c * 64 >= raw_total) break;    // wave-uniform early exit
                 const uint32_t ev = e[c];
                 if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
                     const uint32_t j = ev & ENT_TXN_MASK;
-                    ++witnessed_here;
                     L.slot_ne[sl[c]] = 1;
                     if ((int64_t)j >= base) {
                         const uint32_t b = (uint32_t)((int64_t)j - base);
@@ -385,10 +478,10 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
         wave_lds_sync();
         const uint32_t F = L.far_count;
         if (F > KD_FARCAP) {
-            if (!FILL && lane == 0) {
+            if (lane == 0) {
                 atomicAdd(&p.status->overflow, 1u);
                 atomicMin(&p.status->overflow_first, i);
-                p.cnt_keys[i] = 0; p.cnt_vals[i] = 0; p.cnt_k2v[i] = 0;
+                p.cnt_vals[i] = 0;
             }
             continue;
         }
@@ -407,22 +500,14 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
             for (uint32_t g = 0; g < f; ++g)
                 if ((L.far[g] & 0x7FFFFFFFu) == x) { owner = false; break; }
             far_u += owner ? 1u : 0u;
-            if (FILL && owner) L.far[f] = x | 0x80000000u;
+            if (owner) L.far[f] = x | 0x80000000u;
         }
         far_u = wave_sum(far_u);
         const uint32_t ne = lane < k ? L.slot_ne[lane] : 0u;
         const uint64_t ne_bal = __ballot(ne != 0);
         const uint32_t kc = (uint32_t)__popcll(ne_bal);
 
-        if (!FILL) {
-            const uint32_t body = wave_sum(witnessed_here);
-            if (lane == 0) {
-                p.cnt_keys[i] = kc;
-                p.cnt_vals[i] = far_u + near_u;
-                p.cnt_k2v[i] = kc + body;
-            }
-            continue;
-        }
+        if (lane == 0) p.cnt_vals[i] = far_u + near_u;
 
         // ---- fill: keys, then per witnessed entry its rank -> keysToTxnIds body and txnIds ----
         {
@@ -432,13 +517,14 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
         }
         if (lane < k) L.slot_ns[lane] = (uint32_t)__popcll(ne_bal & lt);
         wave_lds_sync();
-        const uint32_t key_base = p.kd_key_off[i], val_base = p.kd_val_off[i], k2v_base = p.kd_k2v_off[i];
+        const uint32_t key_base = p.kd_key_off[i], val_base = p.vub_off[i], k2v_base = p.kd_k2v_off[i];
         if (lane < k && ne) p.kd_keys[key_base + L.slot_ns[lane]] = my_key;
         uint32_t running = 0;
         for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
             if (!one_batch) load_batch<WPL>(p, L, r0, raw_total, e, sl, lane);
 #pragma unroll
             for (int c = 0; c < KD_CB; ++c) {
+                if (r0 + c * 64 >= raw_total) break;    // wave-uniform early exit
                 const uint32_t r = r0 + c * 64 + lane;
                 const uint32_t ev = e[c];
                 const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
@@ -459,7 +545,7 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
                 const uint32_t pos = running + (uint32_t)__popcll(bal & lt);
                 if (wit) {
                     p.kd_k2v[k2v_base + kc + pos] = (int32_t)rank;
-                    p.kd_vals[val_base + rank] = j;         // every holder of j writes the same word
+                    p.vgap[val_base + rank] = j;            // every holder of j writes the same word
                 }
                 running += (uint32_t)__popcll(bal);
                 // header: a slot's end offset is known at the step holding its last raw entry
@@ -471,16 +557,51 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
     }
 }
 
-template <bool FILL>
 void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
 {
     if (p.n == 0) return;
     uint32_t blocks = (p.n + KD_WAVES - 1) / KD_WAVES;
     if (blocks > 256u * 16u) blocks = 256u * 16u;
     switch (wpl) {
-    case 1: hipLaunchKernelGGL((keydeps_kernel<1, FILL>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
-    case 2: hipLaunchKernelGGL((keydeps_kernel<2, FILL>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
-    default: hipLaunchKernelGGL((keydeps_kernel<4, FILL>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
+    case 1: hipLaunchKernelGGL((keydeps_kernel<1>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((keydeps_kernel<2>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
+    default: hipLaunchKernelGGL((keydeps_kernel<4>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
+    }
+}
+
+// txnIds: gapped (upper-bound offsets) -> dense CSR.  A wave moves 16 consecutive txns at a time:
+// lanes 0..15 fetch their offsets, then every lane issues one load per txn (16 in flight) before
+// the stores, so the copy runs at streaming rate instead of one round trip per txn.
+constexpr int CV_TXNS = 16;
+__global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uint32_t *__restrict__ vub_off,
+                                                           const uint32_t *__restrict__ val_off,
+                                                           const uint32_t *__restrict__ vgap,
+                                                           uint32_t *__restrict__ vals)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t g = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); g * CV_TXNS < n; g += waves) {
+        const uint32_t t = g * CV_TXNS + (lane & (CV_TXNS - 1));
+        uint32_t src = 0, dst = 0, u = 0;
+        if (lane < CV_TXNS && t < n) { src = vub_off[t]; dst = val_off[t]; u = val_off[t + 1] - dst; }
+        uint32_t umax = u;
+#pragma unroll
+        for (int d = 1; d < CV_TXNS; d <<= 1) umax = max(umax, (uint32_t)__shfl_xor(umax, d, 64));
+        umax = __shfl(umax, 0, 64);
+        for (uint32_t x0 = 0; x0 < umax; x0 += 64) {
+            const uint32_t x = x0 + lane;
+            uint32_t v[CV_TXNS];
+#pragma unroll
+            for (int j = 0; j < CV_TXNS; ++j) {
+                const uint32_t uj = __shfl(u, j, 64), sj = __shfl(src, j, 64);
+                v[j] = x < uj ? vgap[sj + x] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < CV_TXNS; ++j) {
+                const uint32_t uj = __shfl(u, j, 64), dj = __shfl(dst, j, 64);
+                if (x < uj) vals[dj + x] = v[j];
+            }
+        }
     }
 }
 
@@ -517,29 +638,61 @@ void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *exc
 
 size_t history_temp_bytes(uint32_t P)
 {
-    const uint32_t tiles = (P + HS_TILE - 1) / HS_TILE;
-    return ((size_t)P + tiles + 64) * sizeof(uint32_t);
+    const size_t tiles = (P + HS_TILE - 1) / HS_TILE;
+    // pw_local[P] u32 | tile_max[tiles] u32 | (align 16) c_local[P] u64 | tile_cnt[tiles] u64 |
+    // ccarry[tiles] ClassCarry
+    size_t b = ((size_t)P + tiles) * 4;
+    b = (b + 15) & ~(size_t)15;
+    b += ((size_t)P + tiles) * 8;
+    b = (b + 15) & ~(size_t)15;
+    b += tiles * sizeof(ClassCarry) + 64;
+    return b;
 }
 
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, unsigned long long *poslo, void *temp, hipStream_t s)
+                    uint32_t *seg_end, unsigned long long *poslo, uint32_t *wcnt, void *temp, hipStream_t s)
 {
     (void)nkeys;
     if (P == 0) return;
     const uint32_t tiles = (P + HS_TILE - 1) / HS_TILE;
     uint32_t *pw_local = (uint32_t *)temp;
     uint32_t *tile_max = pw_local + P;
+    size_t off = ((size_t)P + tiles) * 4;
+    off = (off + 15) & ~(size_t)15;
+    uint64_t *c_local = (uint64_t *)((char *)temp + off);
+    uint64_t *tile_cnt = c_local + P;
+    off += ((size_t)P + tiles) * 8;
+    off = (off + 15) & ~(size_t)15;
+    ClassCarry *ccarry = (ClassCarry *)((char *)temp + off);
     hipLaunchKernelGGL(history1_kernel, dim3(tiles), dim3(HS_THREADS), 0, s, P, sorted_key, sorted_pair, pair_ent,
-                       hist, seg_start, seg_end, pw_local, tile_max);
-    hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tiles);
+                       hist, seg_start, seg_end, pw_local, tile_max, c_local, tile_cnt);
+    hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tile_cnt, ccarry, tiles);
     uint32_t blocks = (P + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(history2_kernel, dim3(blocks), dim3(256), 0, s, P, window, sorted_key, sorted_pair, hist,
-                       seg_start, pw_local, tile_max, poslo);
+                       seg_start, pw_local, tile_max, c_local, ccarry, poslo, wcnt);
 }
 
-void launch_keydeps_count(const KeyDepsParams &p, int wpl, hipStream_t s) { launch_keydeps<false>(p, wpl, s); }
-void launch_keydeps_fill(const KeyDepsParams &p, int wpl, hipStream_t s) { launch_keydeps<true>(p, wpl, s); }
+void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const uint32_t *wcnt, uint32_t *cnt_keys,
+                          uint32_t *cnt_vub, uint32_t *cnt_k2v, DevStatus *status, hipStream_t s)
+{
+    if (n == 0) return;
+    uint32_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(keydeps_sizes_kernel, dim3(blocks), dim3(256), 0, s, n, key_off, wcnt, cnt_keys, cnt_vub,
+                       cnt_k2v, status);
+}
+
+void launch_keydeps_fill(const KeyDepsParams &p, int wpl, hipStream_t s) { launch_keydeps(p, wpl, s); }
+
+void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
+                         uint32_t *vals, hipStream_t s)
+{
+    if (n == 0) return;
+    uint32_t blocks = (n + 4 * CV_TXNS - 1) / (4 * CV_TXNS);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(compact_vals_kernel, dim3(blocks), dim3(256), 0, s, n, vub_off, val_off, vgap, vals);
+}
 
 } // namespace accord

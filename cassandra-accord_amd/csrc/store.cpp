@@ -97,7 +97,7 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipSetDevice(s->cfg.device);
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
-                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->poslo, &s->hist_tmp,
+                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->poslo, &s->hist_tmp, &s->wcnt, &s->cnt_vub, &s->vub_off, &s->vgap,
                       &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
@@ -105,7 +105,8 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->cnt_r2v, &s->rd_rng_off, &s->rd_val_off, &s->rd_r2v_off, &s->rd_rng_start, &s->rd_rng_end,
                       &s->rd_vals, &s->rd_r2v, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
-                      &s->m_zero};
+                      &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
+                      &s->level, &s->wo_info};
     accord_impl::shard_comm_destroy(s);
     for (DevBuf *b : bufs) b->release();
     if (s->events)
@@ -188,6 +189,7 @@ int32_t accord_deps_compute(accord_store *s)
     hipStream_t st = s->stream;
     s->computed = false;
     s->merged = false;
+    s->wo_done = false;
 
     HIPCHECK(s, s->pair_key.ensure((size_t)P * 4));
     HIPCHECK(s, s->pair_ent.ensure((size_t)P * 4));
@@ -197,6 +199,9 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->tmp_val.ensure((size_t)P * 4));
     HIPCHECK(s, s->hist.ensure((size_t)P * 4));
     HIPCHECK(s, s->poslo.ensure((size_t)P * 8));
+    HIPCHECK(s, s->wcnt.ensure((size_t)P * 4));
+    HIPCHECK(s, s->cnt_vub.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->vub_off.ensure(n1 * 4));
     HIPCHECK(s, s->hist_tmp.ensure(accord::history_temp_bytes(P)));
     HIPCHECK(s, s->seg_start.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->seg_end.ensure((size_t)nkeys * 4));
@@ -245,7 +250,8 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, hipMemsetAsync(s->seg_end.p, 0, (size_t)nkeys * 4, st));
     accord::launch_history(P, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
                            s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
-                           s->seg_end.as<uint32_t>(), s->poslo.as<unsigned long long>(), s->hist_tmp.p, st);
+                           s->seg_end.as<uint32_t>(), s->poslo.as<unsigned long long>(), s->wcnt.as<uint32_t>(),
+                           s->hist_tmp.p, st);
     record(s, EV_SEGMENT);
 
     accord::KeyDepsParams kp{};
@@ -256,7 +262,8 @@ int32_t accord_deps_compute(accord_store *s)
     kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
     kp.hist = s->hist.as<uint32_t>();
     kp.poslo = s->poslo.as<unsigned long long>();
-    kp.cnt_keys = s->cnt_keys.as<uint32_t>(); kp.cnt_vals = s->cnt_vals.as<uint32_t>(); kp.cnt_k2v = s->cnt_k2v.as<uint32_t>();
+    kp.cnt_vub = s->cnt_vub.as<uint32_t>();
+    kp.cnt_vals = s->cnt_vals.as<uint32_t>();
     kp.status = &dev->status;
 
     accord::RangeDepsParams rp{};
@@ -268,16 +275,19 @@ int32_t accord_deps_compute(accord_store *s)
     rp.pw_local = s->hist_tmp.as<uint32_t>(); rp.pw_carry = rp.pw_local + P; rp.pw_tile = accord::HISTORY_TILE;
     rp.n_range_txns = nrt; rp.range_txns = s->range_txns.as<uint32_t>();
     rp.cnt_rngs = s->cnt_rngs.as<uint32_t>(); rp.cnt_vals = s->cnt_rvals.as<uint32_t>(); rp.cnt_r2v = s->cnt_r2v.as<uint32_t>();
-    rp.cnt_keys = kp.cnt_keys; rp.cnt_vals_k = kp.cnt_vals; rp.cnt_k2v = kp.cnt_k2v;
+    // range txns' KeyDeps: exact txnIds count into the upper-bound array (their bound is exact)
+    rp.cnt_keys = s->cnt_keys.as<uint32_t>(); rp.cnt_vals_k = s->cnt_vub.as<uint32_t>(); rp.cnt_k2v = s->cnt_k2v.as<uint32_t>();
     rp.status = &dev->status;
 
-    accord::launch_keydeps_count(kp, s->wpl, st);
+    // sizes: key txns from the per-pair witnessed counts, range txns by their own count pass
+    accord::launch_keydeps_sizes(n, kp.key_off, s->wcnt.as<uint32_t>(), rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
+                                 rp.cnt_k2v, &dev->status, st);
     if (nrt) accord::launch_rangekeys_count(rp, st);
     if (R) accord::launch_rangedeps_count(rp, st);
     record(s, EV_COUNT);
-    accord::exclusive_scan_u32(kp.cnt_keys, s->kd_key_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
-    accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[1], s->scan_tmp.p, st);
-    accord::exclusive_scan_u32(kp.cnt_k2v, s->kd_k2v_off.as<uint32_t>(), n, &dev->totals[2], s->scan_tmp.p, st);
+    accord::exclusive_scan_u32(rp.cnt_keys, s->kd_key_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
+    accord::exclusive_scan_u32(kp.cnt_vub, s->vub_off.as<uint32_t>(), n, &dev->totals[1], s->scan_tmp.p, st);
+    accord::exclusive_scan_u32(rp.cnt_k2v, s->kd_k2v_off.as<uint32_t>(), n, &dev->totals[2], s->scan_tmp.p, st);
     if (R) {
         accord::exclusive_scan_u32(rp.cnt_rngs, s->rd_rng_off.as<uint32_t>(), n, &dev->totals[3], s->scan_tmp.p, st);
         accord::exclusive_scan_u32(rp.cnt_vals, s->rd_val_off.as<uint32_t>(), n, &dev->totals[4], s->scan_tmp.p, st);
@@ -292,31 +302,40 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
 
-    const HostTotals &h = *s->pinned;
-    if (h.status.first != ~0ull) {
-        const uint32_t where = (uint32_t)(h.status.first >> 32);
-        const int32_t code = -(int32_t)(uint32_t)(h.status.first & 0xFFFFFFFFu);
-        return fail(s, code, "%s (txn %u)", code_name(code), where);
+    auto check_status = [&](const HostTotals &h) -> int32_t {
+        if (h.status.first != ~0ull) {
+            const uint32_t where = (uint32_t)(h.status.first >> 32);
+            const int32_t code = -(int32_t)(uint32_t)(h.status.first & 0xFFFFFFFFu);
+            return fail(s, code, "%s (txn %u)", code_name(code), where);
+        }
+        if (h.status.overflow)
+            return fail(s, ACCORD_ERR_CAPACITY, "%u txns exceed a per-txn capacity of this build (first: txn %u)",
+                        h.status.overflow, h.status.overflow_first);
+        return ACCORD_OK;
+    };
+    {
+        const HostTotals &h = *s->pinned;
+        int32_t rc = check_status(h);
+        if (rc) return rc;
+        for (int t = 0; t < 6; ++t)
+            if (h.totals[t] >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "deps output exceeds 2^32 entries");
+        s->tot_keys = h.totals[0]; s->tot_k2v = h.totals[2];
+        s->tot_rngs = h.totals[3]; s->tot_rvals = h.totals[4]; s->tot_r2v = h.totals[5];
     }
-    if (h.status.overflow)
-        return fail(s, ACCORD_ERR_CAPACITY, "%u txns exceed a per-txn capacity of this build (first: txn %u)",
-                    h.status.overflow, h.status.overflow_first);
-    for (int t = 0; t < 6; ++t)
-        if (h.totals[t] >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "deps output exceeds 2^32 entries");
-    s->tot_keys = h.totals[0]; s->tot_vals = h.totals[1]; s->tot_k2v = h.totals[2];
-    s->tot_rngs = h.totals[3]; s->tot_rvals = h.totals[4]; s->tot_r2v = h.totals[5];
+    const uint64_t vub_total = s->pinned->totals[1];
     HIPCHECK(s, s->kd_keys.ensure(s->tot_keys * 4));
-    HIPCHECK(s, s->kd_vals.ensure(s->tot_vals * 4));
+    HIPCHECK(s, s->vgap.ensure(vub_total * 4));
+    HIPCHECK(s, s->kd_vals.ensure(vub_total * 4));
     HIPCHECK(s, s->kd_k2v.ensure(s->tot_k2v * 4));
     HIPCHECK(s, s->rd_rng_start.ensure(s->tot_rngs * 4));
     HIPCHECK(s, s->rd_rng_end.ensure(s->tot_rngs * 4));
     HIPCHECK(s, s->rd_vals.ensure(s->tot_rvals * 4));
     HIPCHECK(s, s->rd_r2v.ensure(s->tot_r2v * 4));
-    kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.kd_val_off = s->kd_val_off.as<uint32_t>();
+    kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.vub_off = s->vub_off.as<uint32_t>();
     kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
-    kp.kd_keys = s->kd_keys.as<uint32_t>(); kp.kd_vals = s->kd_vals.as<uint32_t>(); kp.kd_k2v = s->kd_k2v.as<int32_t>();
-    rp.kd_key_off = kp.kd_key_off; rp.kd_val_off = kp.kd_val_off; rp.kd_k2v_off = kp.kd_k2v_off;
-    rp.kd_keys = kp.kd_keys; rp.kd_vals = kp.kd_vals; rp.kd_k2v = kp.kd_k2v;
+    kp.kd_keys = s->kd_keys.as<uint32_t>(); kp.vgap = s->vgap.as<uint32_t>(); kp.kd_k2v = s->kd_k2v.as<int32_t>();
+    rp.kd_key_off = kp.kd_key_off; rp.kd_val_off = kp.vub_off; rp.kd_k2v_off = kp.kd_k2v_off;
+    rp.kd_keys = kp.kd_keys; rp.kd_vals = kp.vgap; rp.kd_k2v = kp.kd_k2v;
     rp.rd_rng_off = s->rd_rng_off.as<uint32_t>(); rp.rd_val_off = s->rd_val_off.as<uint32_t>();
     rp.rd_r2v_off = s->rd_r2v_off.as<uint32_t>();
     rp.rd_rng_start = s->rd_rng_start.as<uint32_t>(); rp.rd_rng_end = s->rd_rng_end.as<uint32_t>();
@@ -326,8 +345,17 @@ int32_t accord_deps_compute(accord_store *s)
     if (nrt) accord::launch_rangekeys_fill(rp, st);
     if (R) accord::launch_rangedeps_fill(rp, st);
     record(s, EV_RANGE);
+    accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[7], s->scan_tmp.p, st);
+    accord::launch_compact_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, s->kd_vals.as<uint32_t>(), st);
+    record(s, EV_COMPACT);
+    HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
+    {
+        int32_t rc = check_status(*s->pinned);
+        if (rc) return rc;
+        s->tot_vals = s->pinned->totals[7];
+    }
 
     if (s->events) {
         auto el = [&](int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, s->ev[a], s->ev[b]); return ms; };
@@ -338,7 +366,8 @@ int32_t accord_deps_compute(accord_store *s)
         s->timing.scan_ms = el(EV_COUNT, EV_SCAN);
         s->timing.fill_ms = el(EV_SCAN, EV_FILL);
         s->timing.range_ms = el(EV_FILL, EV_RANGE);
-        s->timing.total_ms = el(EV_START, EV_RANGE);
+        s->timing.compact_ms = el(EV_RANGE, EV_COMPACT);
+        s->timing.total_ms = el(EV_START, EV_COMPACT);
     }
     s->timing.pairs = P;
     s->timing.hist_entries = P;

@@ -31,15 +31,17 @@ struct DevBuf {
 
 struct HostTotals {
     accord::DevStatus status;
-    unsigned long long totals[8];   // kd keys, kd vals, kd k2v, rd ranges, rd vals, rd r2v, range txns
+    unsigned long long totals[8];   // kd keys, kd vals bound, kd k2v, rd ranges, rd vals, rd r2v, range txns,
+                                    // kd vals
 };
 
 } // namespace accord_impl
 using accord_impl::DevBuf;
 using accord_impl::HostTotals;
 
-enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_RANGE,
-             EV_XCHG_START, EV_XCHG_END, EV_MERGE_END, EV_COUNT_ALL };
+enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_RANGE, EV_COMPACT,
+             EV_XCHG_START, EV_XCHG_END, EV_MERGE_END, EV_WO_START, EV_WO_BITS, EV_WO_PREDS, EV_WO_LEVEL,
+             EV_COUNT_ALL };
 
 struct ShardComm;   // RCCL communicator + exchange buffers (shard.cpp)
 
@@ -53,7 +55,7 @@ struct accord_store {
     DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
     // work
     DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
-    DevBuf hist, poslo, hist_tmp;
+    DevBuf hist, poslo, hist_tmp, wcnt, cnt_vub, vub_off, vgap;
     DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
     DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v;
     uint32_t n_range_txns = 0;
@@ -70,6 +72,12 @@ struct accord_store {
     DevBuf m_key_off, m_val_off, m_k2v_off, m_keys, m_vals, m_k2v, m_cnt_keys, m_cnt_vals, m_cnt_k2v, m_ptrs, m_zero;
     uint64_t m_tot_keys = 0, m_tot_vals = 0, m_tot_k2v = 0;
     float xchg_ms = 0, merge_ms = 0;
+    // WaitingOn + levelling (waiting_on_abi.cpp)
+    bool wo_done = false;
+    DevBuf wo_cnt, wo_off, wo_words, pred_cnt, pred_off, preds, level, wo_info;
+    uint64_t wo_words_total = 0, preds_total = 0;
+    uint32_t max_level = 0;
+    float wo_ms[3] = {0, 0, 0};
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
     hipEvent_t ev[EV_COUNT_ALL] = {};

@@ -103,6 +103,7 @@ typedef struct {
  * stream; zero unless the store was created with ACCORD_STORE_PROFILE). */
 typedef struct {
     float validate_ms, sort_ms, segment_ms, count_ms, scan_ms, fill_ms, range_ms, total_ms;
+    float compact_ms, reserved_ms;   /* txnIds compaction (gapped -> dense CSR) */
     uint64_t pairs, hist_entries;
 } accord_timing;
 
@@ -142,6 +143,31 @@ int32_t accord_comm_unique_id(void *id128);                  /* ncclGetUniqueId,
 int32_t accord_comm_init(accord_store *store, int32_t nranks, int32_t rank, const void *id128);
 int32_t accord_deps_exchange_merge(accord_store *store, uint32_t n_total);
 int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merge_ms);
+
+/* ---- WaitingOn + execution levelling (config 5) ----
+ * Over the store's current computed deps (full stream: no txn_index, not merged), with every txn
+ * STABLE, executeAt = txnId and none applied:
+ *   WaitingOn of txn i (Commands.initialiseWaitingOn, local/Commands.java:735-753; bit layout of
+ *   Command.WaitingOn, local/Command.java:1403-1437): bits [0, R_i) = its RangeDeps txnIds,
+ *   [R_i, R_i + K_i) = its KeyDeps keys, as u64 words words[wo_off[i] .. wo_off[i+1]);
+ *   level[i] = 0 without deps, else 1 + max level over its deps (the order in which CFK notify,
+ *   local/CommandsForKey.java:1501-1635, releases txns to ReadyToExecute). */
+typedef struct {
+    uint32_t  n;
+    uint32_t  max_level;
+    uint64_t  words_total;
+    uint64_t  preds_total;      /* edges of the reduced DAG the levelling ran on */
+    uint32_t *level;            /* [n] */
+    uint32_t *wo_off;           /* [n+1] word offsets */
+    uint64_t *words;            /* [words_total] */
+    void     *owner;            /* library-private */
+} accord_waiting_on;
+
+int32_t accord_waiting_on_compute(accord_store *store);                 /* device-resident */
+int32_t accord_waiting_on_download(accord_store *store, accord_waiting_on *out);
+void    accord_waiting_on_release(accord_waiting_on *wo);
+/* device ms of the last accord_waiting_on_compute: bitsets, reduced predecessors, levelling */
+int32_t accord_waiting_on_timing(accord_store *store, float *bits_ms, float *preds_ms, float *level_ms);
 
 /* ---- synthetic workload (SURVEY.md §8d stream; splitmix64 + Zipf rejection-inversion) ---- */
 typedef struct {

@@ -352,8 +352,8 @@ typedef struct {
     uint32_t *committed; uint32_t nc;  /* indices into txns, sorted by executeAt, :419 */
 } cfk_t;
 
-static const ts_t *g_sort_tbl;         /* qsort context (single-threaded oracle) */
-static const txninfo_t *g_sort_txns;
+static __thread const ts_t *g_sort_tbl;   /* qsort context (thread-local: one thread per store) */
+static __thread const txninfo_t *g_sort_txns;
 static int cmp_committed(const void *a, const void *b)
 {
     const txninfo_t *x = &g_sort_txns[*(const uint32_t *)a], *y = &g_sort_txns[*(const uint32_t *)b];
@@ -963,4 +963,83 @@ int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level, uint32_t *wo_of
     }
     *wo_words = w;
     return 0;
+}
+
+/* Event-driven restatement of execution readiness (validates the levelling abstraction, SURVEY.md
+ * §8a a13): every txn starts with its WaitingOn bits (Commands.initialiseWaitingOn,
+ * local/Commands.java:735-753).  A range-dep bit clears when that dep applies
+ * (Commands.updateWaitingOn -> WaitingOn.setAppliedOrInvalidated, :755-830); a key bit clears when
+ * every dep of that key executing before this txn has applied (CommandsForKey.notify,
+ * local/CommandsForKey.java:1501-1635 -> Commands.removeWaitingOnKeyAndMaybeExecute, :859-876).
+ * A txn with no bits left executes (maybeExecute, :656-733).  Synchronous rounds: all txns ready at
+ * round r execute and apply together; round[i] = r.  Independent of or_waiting_on's recurrence. */
+int or_waiting_on_events(const or_deps *d, uint32_t n, uint32_t *round_out)
+{
+    uint32_t *bits_left = (uint32_t *)calloc(n ? n : 1, sizeof(uint32_t));
+    uint32_t *radj_off = (uint32_t *)calloc((size_t)n + 1, sizeof(uint32_t));
+    uint32_t nkslot = d->kd_key_off[n];
+    uint32_t *slot_left = (uint32_t *)calloc(nkslot ? nkslot : 1, sizeof(uint32_t));
+    if (!bits_left || !radj_off || !slot_left) { free(bits_left); free(radj_off); free(slot_left); return -1; }
+    /* reverse edges: dep j -> (waiter i, slot); slot >= 0 key slot (global index), ~r range bit */
+    size_t E = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t kc = d->kd_key_off[i + 1] - d->kd_key_off[i];
+        const int32_t *k2v = d->kd_k2v + d->kd_k2v_off[i];
+        for (uint32_t q = 0; q < kc; ++q) {
+            uint32_t b = q == 0 ? kc : (uint32_t)k2v[q - 1], e = (uint32_t)k2v[q];
+            for (uint32_t x = b; x < e; ++x) radj_off[d->kd_vals[d->kd_val_off[i] + (uint32_t)k2v[x]] + 1]++;
+            slot_left[d->kd_key_off[i] + q] = e - b;
+            E += e - b;
+        }
+        for (uint32_t v = d->rd_val_off[i]; v < d->rd_val_off[i + 1]; ++v) { radj_off[d->rd_vals[v] + 1]++; ++E; }
+        bits_left[i] = kc + (d->rd_val_off[i + 1] - d->rd_val_off[i]);
+    }
+    for (uint32_t j = 0; j < n; ++j) radj_off[j + 1] += radj_off[j];
+    uint32_t *rw = (uint32_t *)malloc((E ? E : 1) * sizeof(uint32_t));
+    int64_t *rs = (int64_t *)malloc((E ? E : 1) * sizeof(int64_t));
+    uint32_t *fill = (uint32_t *)malloc(((size_t)n + 1) * sizeof(uint32_t));
+    uint32_t *frontier = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    uint32_t *nextf = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    if (!rw || !rs || !fill || !frontier || !nextf) {
+        free(bits_left); free(radj_off); free(slot_left); free(rw); free(rs); free(fill); free(frontier); free(nextf);
+        return -1;
+    }
+    memcpy(fill, radj_off, ((size_t)n + 1) * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t kc = d->kd_key_off[i + 1] - d->kd_key_off[i];
+        const int32_t *k2v = d->kd_k2v + d->kd_k2v_off[i];
+        for (uint32_t q = 0; q < kc; ++q) {
+            uint32_t b = q == 0 ? kc : (uint32_t)k2v[q - 1], e = (uint32_t)k2v[q];
+            for (uint32_t x = b; x < e; ++x) {
+                uint32_t j = d->kd_vals[d->kd_val_off[i] + (uint32_t)k2v[x]];
+                rw[fill[j]] = i; rs[fill[j]] = (int64_t)(d->kd_key_off[i] + q); fill[j]++;
+            }
+        }
+        for (uint32_t v = d->rd_val_off[i]; v < d->rd_val_off[i + 1]; ++v) {
+            uint32_t j = d->rd_vals[v];
+            rw[fill[j]] = i; rs[fill[j]] = -1; fill[j]++;
+        }
+    }
+    uint32_t nf = 0;
+    for (uint32_t i = 0; i < n; ++i) if (bits_left[i] == 0) frontier[nf++] = i;
+    uint32_t done = 0, r = 0;
+    while (nf) {
+        uint32_t nn = 0;
+        for (uint32_t f = 0; f < nf; ++f) round_out[frontier[f]] = r;     /* execute + apply */
+        for (uint32_t f = 0; f < nf; ++f) {
+            uint32_t j = frontier[f];
+            for (uint32_t x = radj_off[j]; x < radj_off[j + 1]; ++x) {
+                uint32_t i = rw[x];
+                int clear = 1;
+                if (rs[x] >= 0) clear = --slot_left[rs[x]] == 0;
+                if (clear && --bits_left[i] == 0) nextf[nn++] = i;
+            }
+        }
+        done += nf;
+        uint32_t *t = frontier; frontier = nextf; nextf = t;
+        nf = nn;
+        ++r;
+    }
+    free(bits_left); free(radj_off); free(slot_left); free(rw); free(rs); free(fill); free(frontier); free(nextf);
+    return done == n ? 0 : -7;   /* -7: a txn never became ready (cycle / missing dep) */
 }

@@ -104,6 +104,10 @@ uint32_t or_stab_key(uint32_t nr, const uint32_t *rs, const uint32_t *re, uint32
 int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level,
                   uint32_t *wo_off /* [n+1] */, uint64_t **wo_words /* malloc'd */);
 
+/* Event-driven readiness simulation (bits cleared by applies, CFK notify per key); round[i] is the
+ * synchronous round in which txn i executes.  Must equal or_waiting_on's level.  0 ok, -7 stuck. */
+int or_waiting_on_events(const or_deps *d, uint32_t n, uint32_t *round_out);
+
 #ifdef __cplusplus
 }
 #endif

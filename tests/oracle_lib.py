@@ -58,6 +58,7 @@ def lib():
         L.or_stab_key.argtypes = [C.c_uint32, _u32p, _u32p, C.c_uint32, _u32p]
         L.or_stab_key.restype = C.c_uint32
         L.or_waiting_on.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p, _u32p, C.POINTER(_u64p)]
+        L.or_waiting_on_events.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p]
         _LIB = L
     return _LIB
 
@@ -219,3 +220,14 @@ def waiting_on(p: PartialDeps):
     w = _arr(words, int(wo_off[-1]), np.uint64)
     C.CDLL(None).free(words)
     return level[:n].copy(), wo_off, w
+
+
+def waiting_on_events(p: PartialDeps):
+    """Event-driven readiness rounds (independent restatement; must equal waiting_on's levels)."""
+    d, keep = _c_deps(p)
+    n = p.n
+    rounds = np.zeros(max(1, n), dtype=np.uint32)
+    rc = lib().or_waiting_on_events(C.byref(d), n, rounds.ctypes.data_as(_u32p))
+    if rc != 0:
+        raise OracleError(rc)
+    return rounds[:n].copy()

@@ -97,3 +97,33 @@ def test_waiting_on_levels_small():
     assert list(level) == list(range(50))
     # one bit per keyDeps key (one key) for every txn with deps
     assert int(wo_off[-1]) == 49
+
+
+def with_random_kinds(s, seed, kinds=(0, 1, 2, 3, 4)):
+    """Same stream with random kinds on key txns (Read, Write, EphemeralRead, SyncPoint,
+    ExclusiveSyncPoint; Txn.Kind ordinals)."""
+    import dataclasses
+    rng = np.random.default_rng(seed)
+    lsb = s.lsb.astype(np.uint64).copy()
+    key_txn = (lsb & np.uint64(1)) == 0
+    k = rng.choice(np.asarray(kinds, dtype=np.uint64), size=s.n)
+    lsb[key_txn] = (lsb[key_txn] & ~np.uint64(0xE)) | (k[key_txn] << np.uint64(1))
+    return dataclasses.replace(s, lsb=lsb)
+
+
+@pytest.mark.parametrize("cfg", [(3000, 4, 40, 0.99, 0.9, 32, 7, 0.0, 0, False),
+                                 (3000, 4, 300, 0.0, 0.5, 8, 8, 0.2, 40, False),
+                                 (2500, 3, 60, 0.99, 0.5, 16, 9, 0.0, 0, True),
+                                 (2000, 4, 200, 0.5, 0.7, 64, 10, 0.1, 20, True)])
+def test_levels_equal_event_simulation(cfg):
+    # levelling abstraction (1 + max over deps) == synchronous readiness rounds of the
+    # WaitingOn/notify event model (SURVEY.md §8a a13)
+    n, k, ks, z, wf, W, seed, rf, rl, kinds = cfg
+    s = generate_stream(n, k, ks, z, wf, seed=seed, range_frac=rf, range_len_max=rl)
+    if kinds:
+        s = with_random_kinds(s, seed)
+    d = O.deps_fast(s, W)
+    level, _, _ = O.waiting_on(d)
+    rounds = O.waiting_on_events(d)
+    assert np.array_equal(level, rounds)
+    assert level.max() > 10
