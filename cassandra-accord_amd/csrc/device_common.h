@@ -20,15 +20,38 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
+// DPP row_shr:N inside each row of 16 lanes; lanes whose source is outside the row read 0.
+template <int N> __device__ __forceinline__ uint32_t dpp_row_shr(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + N, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t readlane(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Inclusive wave scans: Hillis-Steele inside rows of 16 with DPP (no LDS traffic), then the row
+// totals are added through three scalar readlanes.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 {
+    v += dpp_row_shr<1>(v);
+    v += dpp_row_shr<2>(v);
+    v += dpp_row_shr<4>(v);
+    v += dpp_row_shr<8>(v);
     const uint32_t l = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, 64);
-        if (l >= (uint32_t)d) v += t;
-    }
+    const uint32_t r0 = readlane(v, 15), r1 = readlane(v, 31), r2 = readlane(v, 47);
+    v += (l >= 16 ? r0 : 0u) + (l >= 32 ? r1 : 0u) + (l >= 48 ? r2 : 0u);
     return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
+{
+    v = max(v, dpp_row_shr<1>(v));
+    v = max(v, dpp_row_shr<2>(v));
+    v = max(v, dpp_row_shr<4>(v));
+    v = max(v, dpp_row_shr<8>(v));
+    const uint32_t l = lane_id();
+    const uint32_t r0 = readlane(v, 15), r1 = max(r0, readlane(v, 31)), r2 = max(r1, readlane(v, 47));
+    return l >= 48 ? max(v, r2) : l >= 32 ? max(v, r1) : l >= 16 ? max(v, r0) : v;
 }
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v)
 {
@@ -42,9 +65,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v)
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+    return readlane(wave_incl_scan(v), 63);
 }
 
 // ---- TxnId semantics (primitives/Timestamp.java:208-217, TxnId.java:124-157, Txn.java) ----

@@ -36,6 +36,7 @@ struct KeyDepsParams {
     uint32_t window;
     const uint32_t *hist;              // key-major history entries (kind<<29 | global txn)
     const unsigned long long *poslo;   // txn-major per pair: (slice start << 32) | history position
+    const uint32_t *wcnt;              // txn-major per pair: witnessed entries of the slice
     const uint32_t *cnt_vub;           // txnIds upper bound per txn (sizes pass / rangekeys count)
     uint32_t *cnt_vals;                // out: exact txnIds count per txn
     const uint32_t *kd_key_off, *vub_off, *kd_k2v_off;

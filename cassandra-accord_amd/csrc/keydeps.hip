@@ -120,17 +120,6 @@ constexpr int HS_ITEMS = 16;
 constexpr uint32_t HS_TILE = HS_THREADS * HS_ITEMS;
 static_assert(HS_TILE == HISTORY_TILE, "history tile");
 
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
-{
-    const uint32_t l = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, 64);
-        if (l >= (uint32_t)d) v = max(v, t);
-    }
-    return v;
-}
-
 // Packed per-position class counters (16-bit fields, tile-local): Writes | Reads << 16 |
 // EphemeralReads << 32.  With the tile carries they give, for any history range, the number of
 // entries a txn kind witnesses (Ws = #W, RsOrWs = #W + #R, AnyGloballyVisible = len - #ER).
@@ -270,36 +259,66 @@ __global__ __launch_bounds__(256) void history_carry_kernel(uint32_t *__restrict
 // model.  lo = the last Write entry j < i-W of the segment (committed[] bound of
 // CommandsForKey.mapReduceActive :620-645), else the segment start.  Written txn-major, with the
 // number of slice entries kind(i) witnesses (the pair's share of keysToTxnIds).
-__global__ __launch_bounds__(256) void history2_kernel(uint32_t P, uint32_t window, const uint32_t *__restrict__ sorted_key,
-                                                       const uint32_t *__restrict__ sorted_pair,
-                                                       const uint32_t *__restrict__ hist,
-                                                       const uint32_t *__restrict__ seg_start,
-                                                       const uint32_t *__restrict__ pw_local,
-                                                       const uint32_t *__restrict__ carry,
-                                                       const uint64_t *__restrict__ c_local,
-                                                       const ClassCarry *__restrict__ ccarry,
-                                                       unsigned long long *__restrict__ poslo,
-                                                       uint32_t *__restrict__ wcnt)
+// Block per tile of H2_TILE positions; the txn indices of the tile and of H2_HALO positions before
+// it are staged in LDS, so the backward search for the window bound runs on LDS (a global search
+// only when a segment's window reaches past the halo: keys hotter than H2_HALO entries per W txns).
+constexpr uint32_t H2_THREADS = 256, H2_TILE = 2048, H2_HALO = 2048;
+
+__global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32_t window, const uint32_t *__restrict__ sorted_key,
+                                                              const uint32_t *__restrict__ sorted_pair,
+                                                              const uint32_t *__restrict__ hist,
+                                                              const uint32_t *__restrict__ seg_start,
+                                                              const uint32_t *__restrict__ pw_local,
+                                                              const uint32_t *__restrict__ carry,
+                                                              const uint64_t *__restrict__ c_local,
+                                                              const ClassCarry *__restrict__ ccarry,
+                                                              unsigned long long *__restrict__ poslo,
+                                                              uint32_t *__restrict__ wcnt)
 {
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    __shared__ uint32_t tx[H2_HALO + H2_TILE];
+    const uint32_t base = blockIdx.x * H2_TILE;
+    const uint32_t lds_lo = base > H2_HALO ? base - H2_HALO : 0u;
+    const uint32_t end = min(P, base + H2_TILE);
+    for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) tx[x - lds_lo] = hist[x] & ENT_TXN_MASK;
+    __syncthreads();
+    for (uint32_t p = base + threadIdx.x; p < end; p += H2_THREADS) {
         const uint32_t ent = hist[p];
         const uint32_t i = ent & ENT_TXN_MASK;
         const uint32_t a = seg_start[sorted_key[p]];
         uint32_t lo = a;
         if (i > window) {
             const uint32_t thr = i - window;
-            // exponential search backwards for the first q in [a, p] with txn >= thr
-            uint32_t hi = p, lb = a, step = 1;
-            while (hi > a) {
-                const uint32_t probe = (hi - a > step) ? hi - step : a;
-                if ((hist[probe] & ENT_TXN_MASK) < thr) { lb = probe + 1; break; }
+            // first q in [a, p] with txn >= thr: exponential search backwards, on LDS down to lb
+            const uint32_t lb = max(a, lds_lo);
+            uint32_t hi = p, l = lb, step = 1;
+            bool found = false;
+            while (hi > lb) {
+                const uint32_t probe = (hi - lb > step) ? hi - step : lb;
+                if (tx[probe - lds_lo] < thr) { l = probe + 1; found = true; break; }
                 hi = probe;
                 step <<= 1;
             }
-            uint32_t l = lb, h = hi;
-            while (l < h) {
-                const uint32_t m = (l + h) >> 1;
-                if ((hist[m] & ENT_TXN_MASK) < thr) l = m + 1; else h = m;
+            if (found || lb == a) {
+                uint32_t h = hi;
+                while (l < h) {
+                    const uint32_t m = (l + h) >> 1;
+                    if (tx[m - lds_lo] < thr) l = m + 1; else h = m;
+                }
+                if (!found) l = hi;                     // every entry of [lb, p] is inside the window
+            } else {                                    // window reaches past the halo: global search
+                uint32_t gh = lb, gl = a;
+                uint32_t st = 1;
+                while (gh > a) {
+                    const uint32_t probe = (gh - a > st) ? gh - st : a;
+                    if ((hist[probe] & ENT_TXN_MASK) < thr) { gl = probe + 1; break; }
+                    gh = probe;
+                    st <<= 1;
+                }
+                while (gl < gh) {
+                    const uint32_t m = (gl + gh) >> 1;
+                    if ((hist[m] & ENT_TXN_MASK) < thr) gl = m + 1; else gh = m;
+                }
+                l = gl;
             }
             if (l > a) {
                 const uint32_t x = l - 1;
@@ -351,18 +370,13 @@ struct WaveLds {
     unsigned long long bitmap[64 * WPL];
     uint32_t wprefix[64 * WPL];
     uint32_t far[KD_FARCAP];          // value | (owner << 31)
-    uint32_t slot_lo[KD_KCAP];
-    uint32_t slot_rawbase[KD_KCAP + 1];
-    uint32_t slot_key[KD_KCAP];
-    uint32_t slot_ne[KD_KCAP];        // slot has >= 1 witnessed entry
-    uint32_t slot_ns[KD_KCAP];        // index among non-empty slots
     uint32_t far_count;
     uint32_t pad[3];
 };
 
 // Candidates per lane per batch: one batch covers 64*KD_CB raw history entries with a single
 // round trip to memory (loads are issued before any is consumed).
-constexpr int KD_CB = 8;
+constexpr int KD_CB = 4;
 
 struct TxnMeta {
     uint32_t k0, k1;
@@ -376,30 +390,44 @@ __device__ __forceinline__ TxnMeta load_meta(const KeyDepsParams &p, uint32_t i)
     return m;
 }
 
-template <int WPL>
-__device__ __forceinline__ void load_batch(const KeyDepsParams &p, const WaveLds<WPL> &L, uint32_t r0, uint32_t raw_total,
-                                           uint32_t (&e)[KD_CB], uint32_t (&sl)[KD_CB], uint32_t lane)
+// Raw candidate r (slot-major concatenation of the k slices) lives at hist[r + delta_s] where s is
+// its slot: s = #{q < k : end_q <= r}.  end/delta are per-lane registers of lanes q < k; the slot
+// search reads them as scalars (no LDS round trips), the delta by one lane permute.
+__device__ __forceinline__ void load_batch(const KeyDepsParams &p, uint32_t r0, uint32_t raw_total, uint32_t k,
+                                           uint32_t end, int32_t delta, uint32_t (&e)[KD_CB], uint32_t lane)
 {
-    uint32_t s = 0;
 #pragma unroll
     for (int c = 0; c < KD_CB; ++c) {
-        const uint32_t r = r0 + c * 64 + lane;
         e[c] = 0xFFFFFFFFu;               // sentinel: kind 7 is never witnessed
-        sl[c] = s;
         if (r0 + c * 64 >= raw_total) continue;     // wave-uniform: no candidates left
-        if (r < raw_total) {
-            while (L.slot_rawbase[s + 1] <= r) ++s;
-            sl[c] = s;
-            e[c] = p.hist[L.slot_lo[s] + (r - L.slot_rawbase[s])];
-        }
+        const uint32_t r = r0 + c * 64 + lane;
+        uint32_t s = 0;
+        for (uint32_t q = 0; q < k; ++q) s += (r >= (uint32_t)__builtin_amdgcn_readlane((int)end, (int)q)) ? 1u : 0u;
+        const int32_t d = __shfl(delta, (int)min(s, 63u), 64);
+        if (r < raw_total) e[c] = p.hist[(uint32_t)((int32_t)r + d)];
     }
 }
 
+// The slots of a txn: lane q < k holds end_q (inclusive scan of the slice lengths) and
+// delta_q = slice start - exclusive scan; raw_total = all candidates.
+__device__ __forceinline__ void slot_setup(unsigned long long pl, uint32_t k, uint32_t lane, uint32_t &incl,
+                                           int32_t &delta, uint32_t &raw_total)
+{
+    uint32_t raw = 0;
+    if (lane < k) raw = (uint32_t)pl - (uint32_t)(pl >> 32);
+    incl = wave_incl_scan(raw);
+    delta = lane < k ? (int32_t)(uint32_t)(pl >> 32) - (int32_t)(incl - raw) : 0;
+    raw_total = readlane(incl, 63);
+}
+
 // One wave builds one txn's KeyDeps.  Per txn the wave needs ONE memory round trip for its
-// candidates: the next txn's history slices (poslo) and the one after's offsets are prefetched
-// while the current txn is processed (vmcnt retires in order, so they ride with it).
+// candidates: the next txn's history slices (poslo, wcnt) and the one after's offsets are
+// prefetched while the current txn is processed (vmcnt retires in order, so they ride with it).
+// keys and the keysToTxnIds header come straight from the per-pair witnessed counts (wcnt); the
+// body position of a witnessed entry is its running ballot count; its value is its rank in the
+// txn's sorted unique txnIds (LDS bitmap over [i-SPAN, i) + far list).
 template <int WPL>
-__global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
+__global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void keydeps_kernel(KeyDepsParams p)
 {
     __shared__ WaveLds<WPL> lds_all[KD_WAVES];
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
@@ -408,23 +436,51 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
     constexpr uint32_t SPAN = 64u * 64u * WPL;
     const uint32_t S = gridDim.x * KD_WAVES;
 
+    // Software pipeline over the wave's txns i, i+S, i+2S, ...: offsets three txns ahead, slices
+    // (poslo, wcnt) two ahead, and the first batch of history candidates one ahead, so the
+    // candidate round trip of the next txn overlaps this txn's LDS work.
     uint32_t i = blockIdx.x * KD_WAVES + w;
-    TxnMeta m0 = load_meta(p, i);
-    TxnMeta m1 = load_meta(p, i + S);
-    unsigned long long pl0 = 0;
-    if (i < p.n && lane < m0.k1 - m0.k0 && lane < KD_KCAP) pl0 = p.poslo[m0.k0 + lane];
+    TxnMeta m0 = load_meta(p, i), m1 = load_meta(p, i + S), m2 = load_meta(p, i + 2 * S);
+    unsigned long long pl0 = 0, pl1 = 0;
+    uint32_t wc0 = 0, wc1 = 0;
+    if (i < p.n && lane < m0.k1 - m0.k0 && lane < KD_KCAP) { pl0 = p.poslo[m0.k0 + lane]; wc0 = p.wcnt[m0.k0 + lane]; }
+    if (i + S < p.n && lane < m1.k1 - m1.k0 && lane < KD_KCAP) { pl1 = p.poslo[m1.k0 + lane]; wc1 = p.wcnt[m1.k0 + lane]; }
+    uint32_t incl0, raw_total0;
+    int32_t delta0;
+    uint32_t e0[KD_CB];
+    {
+        const uint32_t k = m0.k1 - m0.k0;
+        slot_setup(pl0, (i < p.n && k <= KD_KCAP) ? k : 0u, lane, incl0, delta0, raw_total0);
+        load_batch(p, 0, raw_total0, k, incl0, delta0, e0, lane);
+    }
 
     for (; i < p.n; i += S) {
-        // ---- prefetch: offsets two txns ahead, history slices one txn ahead ----
-        const TxnMeta m2 = load_meta(p, i + 2 * S);
-        unsigned long long pl1 = 0;
-        if (i + S < p.n && lane < m1.k1 - m1.k0 && lane < KD_KCAP) pl1 = p.poslo[m1.k0 + lane];
+        // ---- prefetch ----
+        const TxnMeta m3 = load_meta(p, i + 3 * S);
+        unsigned long long pl2 = 0;
+        uint32_t wc2 = 0;
+        if (i + 2 * S < p.n && lane < m2.k1 - m2.k0 && lane < KD_KCAP) { pl2 = p.poslo[m2.k0 + lane]; wc2 = p.wcnt[m2.k0 + lane]; }
+        uint32_t incl1, raw_total1;
+        int32_t delta1;
+        uint32_t e1[KD_CB];
+        {
+            const uint32_t kn = m1.k1 - m1.k0;
+            slot_setup(pl1, (i + S < p.n && kn <= KD_KCAP) ? kn : 0u, lane, incl1, delta1, raw_total1);
+            load_batch(p, 0, raw_total1, kn, incl1, delta1, e1, lane);
+        }
+
+        // ---- this txn ----
         const uint32_t k0 = m0.k0, k = m0.k1 - m0.k0;
         const uint32_t wmask = witness_mask((uint32_t)(m0.lsb >> 1) & 7);
-        uint32_t my_key = 0;
-        if (lane < k && k <= KD_KCAP) my_key = p.key_ord[k0 + lane];
         const unsigned long long pl = pl0;
-        m0 = m1; m1 = m2; pl0 = pl1;
+        const uint32_t wc = wc0, incl = incl0, raw_total = raw_total0;
+        const int32_t delta = delta0;
+        uint32_t e[KD_CB];
+#pragma unroll
+        for (int c = 0; c < KD_CB; ++c) { e[c] = e0[c]; e0[c] = e1[c]; }
+        m0 = m1; m1 = m2; m2 = m3; pl0 = pl1; wc0 = wc1; pl1 = pl2; wc1 = wc2;
+        incl0 = incl1; delta0 = delta1; raw_total0 = raw_total1;
+        (void)pl;
 
         if (k > KD_KCAP) {                              // reported by the sizes pass
             if (lane == 0) p.cnt_vals[i] = 0;
@@ -434,37 +490,38 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
             if (lane == 0) p.cnt_vals[i] = p.cnt_vub[i];
             continue;
         }
+        uint32_t my_key = 0;
+        if (lane < k) my_key = p.key_ord[k0 + lane];
         const uint32_t gi = p.txn_index ? p.txn_index[i] : i;   // global stream position
+        const uint32_t key_base = p.kd_key_off[i], val_base = p.vub_off[i], k2v_base = p.kd_k2v_off[i];
 
-        // ---- slots: the deps slice [lo, pos) of each key, from the history annotation ----
-        uint32_t raw = 0;
-        if (lane < k) {
-            const uint32_t pos = (uint32_t)pl, start = (uint32_t)(pl >> 32);
-            raw = pos - start;
-            L.slot_lo[lane] = start;
-            L.slot_ne[lane] = 0;
+        // ---- keys and keysToTxnIds header from the witnessed counts ----
+        const bool ne = lane < k && wc != 0;
+        const uint64_t ne_bal = __ballot(ne);
+        const uint32_t kc = (uint32_t)__popcll(ne_bal);
+        const uint32_t wincl = wave_incl_scan(lane < k ? wc : 0u);
+        if (ne) {
+            const uint32_t ns = (uint32_t)__popcll(ne_bal & lt);
+            p.kd_keys[key_base + ns] = my_key;
+            p.kd_k2v[k2v_base + ns] = (int32_t)(kc + wincl);
         }
-        const uint32_t incl = wave_incl_scan(raw);
-        if (lane < k) L.slot_rawbase[lane] = incl - raw;
-        const uint32_t raw_total = __shfl(incl, 63, 64);
+
 #pragma unroll
         for (int q = 0; q < WPL; ++q) L.bitmap[lane * WPL + q] = 0ull;
-        if (lane == 0) { L.far_count = 0; L.slot_rawbase[k] = raw_total; }
+        if (lane == 0) L.far_count = 0;
         wave_lds_sync();
 
         // ---- phase 1: witness filter -> near bitmap / far list ----
         const int64_t base = (int64_t)gi - (int64_t)SPAN;
         const bool one_batch = raw_total <= 64u * KD_CB;
-        uint32_t e[KD_CB], sl[KD_CB];
         for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
-            load_batch<WPL>(p, L, r0, raw_total, e, sl, lane);
+            if (r0) load_batch(p, r0, raw_total, k, incl, delta, e, lane);
 #pragma unroll
             for (int c = 0; c < KD_CB; ++c) {
                 if (r0 + c * 64 >= raw_total) break;    // wave-uniform early exit
                 const uint32_t ev = e[c];
                 if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
                     const uint32_t j = ev & ENT_TXN_MASK;
-                    L.slot_ne[sl[c]] = 1;
                     if ((int64_t)j >= base) {
                         const uint32_t b = (uint32_t)((int64_t)j - base);
                         atomicOr(&L.bitmap[b >> 6], 1ull << (b & 63));
@@ -492,7 +549,7 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
 #pragma unroll
         for (int q = 0; q < WPL; ++q) { pc[q] = (uint32_t)__popcll(L.bitmap[lane * WPL + q]); mysum += pc[q]; }
         const uint32_t incl2 = wave_incl_scan(mysum);
-        const uint32_t near_u = __shfl(incl2, 63, 64);
+        const uint32_t near_u = readlane(incl2, 63);
         uint32_t far_u = 0;
         for (uint32_t f = lane; f < F; f += 64) {
             const uint32_t x = L.far[f] & 0x7FFFFFFFu;
@@ -503,29 +560,21 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
             if (owner) L.far[f] = x | 0x80000000u;
         }
         far_u = wave_sum(far_u);
-        const uint32_t ne = lane < k ? L.slot_ne[lane] : 0u;
-        const uint64_t ne_bal = __ballot(ne != 0);
-        const uint32_t kc = (uint32_t)__popcll(ne_bal);
-
         if (lane == 0) p.cnt_vals[i] = far_u + near_u;
 
-        // ---- fill: keys, then per witnessed entry its rank -> keysToTxnIds body and txnIds ----
+        // ---- fill: per witnessed entry its rank -> keysToTxnIds body and txnIds ----
         {
             uint32_t ex = incl2 - mysum;
 #pragma unroll
             for (int q = 0; q < WPL; ++q) { L.wprefix[lane * WPL + q] = ex; ex += pc[q]; }
         }
-        if (lane < k) L.slot_ns[lane] = (uint32_t)__popcll(ne_bal & lt);
         wave_lds_sync();
-        const uint32_t key_base = p.kd_key_off[i], val_base = p.vub_off[i], k2v_base = p.kd_k2v_off[i];
-        if (lane < k && ne) p.kd_keys[key_base + L.slot_ns[lane]] = my_key;
         uint32_t running = 0;
         for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
-            if (!one_batch) load_batch<WPL>(p, L, r0, raw_total, e, sl, lane);
+            if (!one_batch) load_batch(p, r0, raw_total, k, incl, delta, e, lane);
 #pragma unroll
             for (int c = 0; c < KD_CB; ++c) {
                 if (r0 + c * 64 >= raw_total) break;    // wave-uniform early exit
-                const uint32_t r = r0 + c * 64 + lane;
                 const uint32_t ev = e[c];
                 const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
                 const uint32_t j = ev & ENT_TXN_MASK;
@@ -548,10 +597,6 @@ __global__ __launch_bounds__(KD_THREADS) void keydeps_kernel(KeyDepsParams p)
                     p.vgap[val_base + rank] = j;            // every holder of j writes the same word
                 }
                 running += (uint32_t)__popcll(bal);
-                // header: a slot's end offset is known at the step holding its last raw entry
-                const uint32_t s = sl[c];
-                if (r < raw_total && r + 1 == L.slot_rawbase[s + 1] && L.slot_ne[s])
-                    p.kd_k2v[k2v_base + L.slot_ns[s]] = (int32_t)(kc + pos + (wit ? 1u : 0u));
             }
         }
     }
@@ -668,9 +713,8 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
     hipLaunchKernelGGL(history1_kernel, dim3(tiles), dim3(HS_THREADS), 0, s, P, sorted_key, sorted_pair, pair_ent,
                        hist, seg_start, seg_end, pw_local, tile_max, c_local, tile_cnt);
     hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tile_cnt, ccarry, tiles);
-    uint32_t blocks = (P + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(history2_kernel, dim3(blocks), dim3(256), 0, s, P, window, sorted_key, sorted_pair, hist,
+    hipLaunchKernelGGL(history2_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P, window,
+                       sorted_key, sorted_pair, hist,
                        seg_start, pw_local, tile_max, c_local, ccarry, poslo, wcnt);
 }
 

@@ -262,6 +262,7 @@ int32_t accord_deps_compute(accord_store *s)
     kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
     kp.hist = s->hist.as<uint32_t>();
     kp.poslo = s->poslo.as<unsigned long long>();
+    kp.wcnt = s->wcnt.as<uint32_t>();
     kp.cnt_vub = s->cnt_vub.as<uint32_t>();
     kp.cnt_vals = s->cnt_vals.as<uint32_t>();
     kp.status = &dev->status;

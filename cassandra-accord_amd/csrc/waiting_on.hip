@@ -145,17 +145,24 @@ __global__ __launch_bounds__(LV_THREADS) void level_kernel(uint32_t n, const uin
                 }
             }
         }
+        // gate: the latest in-chunk predecessor (the one a chain waits on); poll only it, then
+        // confirm the others once it is final
+        uint32_t gate = 0;
+#pragma unroll
+        for (int r = 0; r < LV_PREG; ++r)
+            if (r < (int)nslot) gate = max(gate, slot[r]);
         __syncthreads();
         uint32_t rounds = 0;
         while (true) {
             bool moved = false;
-            if (!done) {
+            if (!done && (nslot == 0 || __hip_atomic_load(&lv[gate], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)) {
                 bool ok = true;
                 uint32_t b2 = best;
 #pragma unroll
                 for (int r = 0; r < LV_PREG; ++r) {
                     if (r < (int)nslot) {
                         const uint32_t v = __hip_atomic_load(&lv[slot[r]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (v == 0 && ok) gate = slot[r];
                         ok = ok && v != 0;
                         b2 = max(b2, v);
                     }
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(LV_THREADS) void level_kernel(uint32_t n, const uin
             }
             if (__all(done)) break;
             if (++rounds > (1u << 22)) { sabort = 1; break; }   // defensive bound: never hit by a DAG
-            if (!__any(moved)) __builtin_amdgcn_s_sleep(1);
+            // no s_sleep: a chain hop is one LDS round trip of the waiting wave
         }
         __syncthreads();
         if (sabort) {
