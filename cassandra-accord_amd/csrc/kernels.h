@@ -26,6 +26,13 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, unsigned 
                         hipStream_t s);
 
 // ---- key deps pipeline (keydeps.hip) ----
+// Per (txn, key) pair, txn-major: the deps slice [lo, pos) of the key's history and the number of
+// its entries the txn's kind witnesses.  One 16-byte record so the key-major -> txn-major scatter
+// is a single store per pair.
+struct alignas(16) PairSlice {
+    uint32_t lo, pos, wcnt, pad;
+};
+
 struct KeyDepsParams {
     uint32_t n;
     const uint64_t *msb, *lsb;
@@ -35,8 +42,7 @@ struct KeyDepsParams {
     uint32_t key_lo, key_hi;
     uint32_t window;
     const uint32_t *hist;              // key-major history entries (kind<<29 | global txn)
-    const unsigned long long *poslo;   // txn-major per pair: (slice start << 32) | history position
-    const uint32_t *wcnt;              // txn-major per pair: witnessed entries of the slice
+    const PairSlice *slice;            // txn-major per pair
     const uint32_t *cnt_vub;           // txnIds upper bound per txn (sizes pass / rangekeys count)
     uint32_t *cnt_vals;                // out: exact txnIds count per txn
     const uint32_t *kd_key_off, *vub_off, *kd_k2v_off;
@@ -54,15 +60,14 @@ void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
 // range_txns[excl[i]] = i for every i with is_range[i]
 void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s);
 size_t history_temp_bytes(uint32_t P);
-// key-major: history entries, segments, and per pair the [lo, pos) deps slice (txn-major poslo)
-// with its witnessed-entry count (txn-major wcnt)
+// key-major: history entries, segments, and per pair its deps slice (txn-major PairSlice)
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, unsigned long long *poslo, uint32_t *wcnt, void *temp, hipStream_t s);
+                    uint32_t *seg_end, PairSlice *slice, void *temp, hipStream_t s);
 // history tile size of the Write max-scan carry (pw_local / pw_carry)
 constexpr uint32_t HISTORY_TILE = 4096;
-// per txn: keys, txnIds upper bound and keysToTxnIds sizes from wcnt (no history scan)
-void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const uint32_t *wcnt, uint32_t *cnt_keys,
+// per txn: keys, txnIds upper bound and keysToTxnIds sizes from the witnessed counts
+void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *slice, uint32_t *cnt_keys,
                           uint32_t *cnt_vub, uint32_t *cnt_k2v, DevStatus *status, hipStream_t s);
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
 // vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
@@ -128,8 +133,8 @@ void launch_merge_fill(const MergeParams &p, hipStream_t s);
 struct WaitingOnParams {
     uint32_t n;
     const uint64_t *lsb;
-    const uint32_t *key_off;                       // txn-major pairs (poslo index)
-    const unsigned long long *poslo;
+    const uint32_t *key_off;                       // txn-major pairs (slice index)
+    const PairSlice *slice;
     const uint32_t *hist, *pw_local, *pw_carry;
     uint32_t pw_tile;
     const uint32_t *kd_val_off, *kd_vals;          // full KeyDeps (non-reduced txns)

@@ -272,8 +272,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
                                                               const uint32_t *__restrict__ carry,
                                                               const uint64_t *__restrict__ c_local,
                                                               const ClassCarry *__restrict__ ccarry,
-                                                              unsigned long long *__restrict__ poslo,
-                                                              uint32_t *__restrict__ wcnt)
+                                                              PairSlice *__restrict__ slice)
 {
     __shared__ uint32_t tx[H2_HALO + H2_TILE];
     const uint32_t base = blockIdx.x * H2_TILE;
@@ -332,8 +331,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
             cnt = witnessed_upto(c_local, ccarry, p - 1, wmask) - (lo ? witnessed_upto(c_local, ccarry, lo - 1, wmask) : 0u);
         }
         const uint32_t q = sorted_pair[p];
-        poslo[q] = ((unsigned long long)lo << 32) | p;
-        wcnt[q] = cnt;
+        slice[q] = PairSlice{lo, p, cnt, 0u};
     }
 }
 
@@ -341,7 +339,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
 // witnessed entry, keysToTxnIds = keys + body; txnIds <= body (an upper bound: the fill pass
 // writes the exact count and the values are compacted afterwards).
 __global__ __launch_bounds__(256) void keydeps_sizes_kernel(uint32_t n, const uint32_t *__restrict__ key_off,
-                                                            const uint32_t *__restrict__ wcnt,
+                                                            const PairSlice *__restrict__ slice,
                                                             uint32_t *__restrict__ cnt_keys,
                                                             uint32_t *__restrict__ cnt_vub,
                                                             uint32_t *__restrict__ cnt_k2v, DevStatus *status)
@@ -354,7 +352,7 @@ __global__ __launch_bounds__(256) void keydeps_sizes_kernel(uint32_t n, const ui
             atomicMin(&status->overflow_first, i);
         } else {
             for (uint32_t q = k0; q < k1; ++q) {
-                const uint32_t c = wcnt[q];
+                const uint32_t c = slice[q].wcnt;
                 kc += c ? 1u : 0u;
                 body += c;
             }
@@ -370,6 +368,7 @@ struct WaveLds {
     unsigned long long bitmap[64 * WPL];
     uint32_t wprefix[64 * WPL];
     uint32_t far[KD_FARCAP];          // value | (owner << 31)
+    uint32_t far_rank[KD_FARCAP];     // rank of far[f]'s value among the txn's unique txnIds
     uint32_t far_count;
     uint32_t pad[3];
 };
@@ -377,6 +376,20 @@ struct WaveLds {
 // Candidates per lane per batch: one batch covers 64*KD_CB raw history entries with a single
 // round trip to memory (loads are issued before any is consumed).
 constexpr int KD_CB = 4;
+constexpr uint32_t KD_NONE = 0xFFFFFFFFu;     // candidate not witnessed (also: no candidate)
+constexpr uint32_t KD_FAR = 0x80000000u;      // witnessed far candidate: KD_FAR | far-list index
+
+// Global accesses with a 32-bit byte offset from a uniform base, so they compile to the
+// saddr + voffset form (no 64-bit address arithmetic per access).  Callers keep every array
+// below 4 GiB (checked by the store before launching).
+template <typename T> __device__ __forceinline__ T ldg(const T *base, uint32_t idx)
+{
+    return *(const T *)((const char *)base + (size_t)(uint32_t)(idx * (uint32_t)sizeof(T)));
+}
+template <typename T> __device__ __forceinline__ void stg(T *base, uint32_t idx, T v)
+{
+    *(T *)((char *)base + (size_t)(uint32_t)(idx * (uint32_t)sizeof(T))) = v;
+}
 
 struct TxnMeta {
     uint32_t k0, k1;
@@ -386,48 +399,67 @@ struct TxnMeta {
 __device__ __forceinline__ TxnMeta load_meta(const KeyDepsParams &p, uint32_t i)
 {
     TxnMeta m{0u, 0u, 0ull};
-    if (i < p.n) { m.k0 = p.key_off[i]; m.k1 = p.key_off[i + 1]; m.lsb = p.lsb[i]; }
+    if (i < p.n) { m.k0 = ldg(p.key_off, i); m.k1 = ldg(p.key_off, i + 1); m.lsb = ldg(p.lsb, i); }
     return m;
 }
 
+__device__ __forceinline__ void load_slice(const KeyDepsParams &p, const TxnMeta &m, bool valid, uint32_t lane,
+                                           uint32_t &lo, uint32_t &pos, uint32_t &wc)
+{
+    lo = pos = wc = 0;
+    if (valid && lane < m.k1 - m.k0 && lane < KD_KCAP) {
+        const PairSlice ps = ldg(p.slice, m.k0 + lane);
+        lo = ps.lo; pos = ps.pos; wc = ps.wcnt;
+    }
+}
+
 // Raw candidate r (slot-major concatenation of the k slices) lives at hist[r + delta_s] where s is
-// its slot: s = #{q < k : end_q <= r}.  end/delta are per-lane registers of lanes q < k; the slot
-// search reads them as scalars (no LDS round trips), the delta by one lane permute.
+// its slot: s = #{q < k : end_q <= r}.  end/delta are per-lane registers of lanes q < k.  The
+// slot of the window's first candidate is carried across windows; inside a 64-candidate window
+// only the slot boundaries that fall in it are compared (scalar reads of end), then one lane
+// permute fetches the slot's delta.
 __device__ __forceinline__ void load_batch(const KeyDepsParams &p, uint32_t r0, uint32_t raw_total, uint32_t k,
                                            uint32_t end, int32_t delta, uint32_t (&e)[KD_CB], uint32_t lane)
 {
+    uint32_t q = 0;                                   // uniform: slot of the window's first candidate
 #pragma unroll
     for (int c = 0; c < KD_CB; ++c) {
-        e[c] = 0xFFFFFFFFu;               // sentinel: kind 7 is never witnessed
-        if (r0 + c * 64 >= raw_total) continue;     // wave-uniform: no candidates left
-        const uint32_t r = r0 + c * 64 + lane;
-        uint32_t s = 0;
-        for (uint32_t q = 0; q < k; ++q) s += (r >= (uint32_t)__builtin_amdgcn_readlane((int)end, (int)q)) ? 1u : 0u;
+        e[c] = KD_NONE;
+        const uint32_t w0 = r0 + c * 64;
+        if (w0 >= raw_total) continue;                // wave-uniform: no candidates left
+        const uint32_t r = w0 + lane;
+        while (q < k && readlane(end, (int)q) <= w0) ++q;
+        uint32_t s = q;
+        for (uint32_t qq = q; qq < k; ++qq) {
+            const uint32_t eq = readlane(end, (int)qq);
+            if (eq >= w0 + 64) break;
+            s += r >= eq ? 1u : 0u;
+        }
         const int32_t d = __shfl(delta, (int)min(s, 63u), 64);
-        if (r < raw_total) e[c] = p.hist[(uint32_t)((int32_t)r + d)];
+        if (r < raw_total) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
     }
 }
 
 // The slots of a txn: lane q < k holds end_q (inclusive scan of the slice lengths) and
 // delta_q = slice start - exclusive scan; raw_total = all candidates.
-__device__ __forceinline__ void slot_setup(unsigned long long pl, uint32_t k, uint32_t lane, uint32_t &incl,
+__device__ __forceinline__ void slot_setup(uint32_t lo, uint32_t pos, uint32_t k, uint32_t lane, uint32_t &incl,
                                            int32_t &delta, uint32_t &raw_total)
 {
-    uint32_t raw = 0;
-    if (lane < k) raw = (uint32_t)pl - (uint32_t)(pl >> 32);
+    const uint32_t raw = lane < k ? pos - lo : 0u;
     incl = wave_incl_scan(raw);
-    delta = lane < k ? (int32_t)(uint32_t)(pl >> 32) - (int32_t)(incl - raw) : 0;
+    delta = lane < k ? (int32_t)lo - (int32_t)(incl - raw) : 0;
     raw_total = readlane(incl, 63);
 }
 
-// One wave builds one txn's KeyDeps.  Per txn the wave needs ONE memory round trip for its
-// candidates: the next txn's history slices (poslo, wcnt) and the one after's offsets are
-// prefetched while the current txn is processed (vmcnt retires in order, so they ride with it).
-// keys and the keysToTxnIds header come straight from the per-pair witnessed counts (wcnt); the
-// body position of a witnessed entry is its running ballot count; its value is its rank in the
-// txn's sorted unique txnIds (LDS bitmap over [i-SPAN, i) + far list).
+// One wave builds one txn's KeyDeps.  keys and the keysToTxnIds header come straight from the
+// per-pair witnessed counts (PairSlice.wcnt); the body position of a witnessed entry is its
+// running ballot count; its value is its rank in the txn's sorted unique txnIds (LDS bitmap over
+// [i-SPAN, i) + far list).
+// Software pipeline over the wave's txns i, i+S, i+2S, ...: offsets three txns ahead, slices two
+// ahead, and the first batch of history candidates one ahead, so the candidate round trip of the
+// next txn overlaps this txn's LDS work.
 template <int WPL>
-__global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void keydeps_kernel(KeyDepsParams p)
+__global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(WPL == 1 ? 8 : 4, 8))) void keydeps_kernel(KeyDepsParams p)
 {
     __shared__ WaveLds<WPL> lds_all[KD_WAVES];
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
@@ -436,64 +468,59 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     constexpr uint32_t SPAN = 64u * 64u * WPL;
     const uint32_t S = gridDim.x * KD_WAVES;
 
-    // Software pipeline over the wave's txns i, i+S, i+2S, ...: offsets three txns ahead, slices
-    // (poslo, wcnt) two ahead, and the first batch of history candidates one ahead, so the
-    // candidate round trip of the next txn overlaps this txn's LDS work.
     uint32_t i = blockIdx.x * KD_WAVES + w;
     TxnMeta m0 = load_meta(p, i), m1 = load_meta(p, i + S), m2 = load_meta(p, i + 2 * S);
-    unsigned long long pl0 = 0, pl1 = 0;
-    uint32_t wc0 = 0, wc1 = 0;
-    if (i < p.n && lane < m0.k1 - m0.k0 && lane < KD_KCAP) { pl0 = p.poslo[m0.k0 + lane]; wc0 = p.wcnt[m0.k0 + lane]; }
-    if (i + S < p.n && lane < m1.k1 - m1.k0 && lane < KD_KCAP) { pl1 = p.poslo[m1.k0 + lane]; wc1 = p.wcnt[m1.k0 + lane]; }
+    uint32_t lo0, pos0, wc0, lo1, pos1, wc1;
+    load_slice(p, m0, i < p.n, lane, lo0, pos0, wc0);
+    load_slice(p, m1, i + S < p.n, lane, lo1, pos1, wc1);
     uint32_t incl0, raw_total0;
     int32_t delta0;
     uint32_t e0[KD_CB];
     {
         const uint32_t k = m0.k1 - m0.k0;
-        slot_setup(pl0, (i < p.n && k <= KD_KCAP) ? k : 0u, lane, incl0, delta0, raw_total0);
+        slot_setup(lo0, pos0, (i < p.n && k <= KD_KCAP) ? k : 0u, lane, incl0, delta0, raw_total0);
         load_batch(p, 0, raw_total0, k, incl0, delta0, e0, lane);
     }
 
     for (; i < p.n; i += S) {
         // ---- prefetch ----
         const TxnMeta m3 = load_meta(p, i + 3 * S);
-        unsigned long long pl2 = 0;
-        uint32_t wc2 = 0;
-        if (i + 2 * S < p.n && lane < m2.k1 - m2.k0 && lane < KD_KCAP) { pl2 = p.poslo[m2.k0 + lane]; wc2 = p.wcnt[m2.k0 + lane]; }
+        uint32_t lo2, pos2, wc2;
+        load_slice(p, m2, i + 2 * S < p.n, lane, lo2, pos2, wc2);
         uint32_t incl1, raw_total1;
         int32_t delta1;
         uint32_t e1[KD_CB];
         {
             const uint32_t kn = m1.k1 - m1.k0;
-            slot_setup(pl1, (i + S < p.n && kn <= KD_KCAP) ? kn : 0u, lane, incl1, delta1, raw_total1);
+            slot_setup(lo1, pos1, (i + S < p.n && kn <= KD_KCAP) ? kn : 0u, lane, incl1, delta1, raw_total1);
             load_batch(p, 0, raw_total1, kn, incl1, delta1, e1, lane);
         }
 
         // ---- this txn ----
         const uint32_t k0 = m0.k0, k = m0.k1 - m0.k0;
         const uint32_t wmask = witness_mask((uint32_t)(m0.lsb >> 1) & 7);
-        const unsigned long long pl = pl0;
         const uint32_t wc = wc0, incl = incl0, raw_total = raw_total0;
         const int32_t delta = delta0;
         uint32_t e[KD_CB];
 #pragma unroll
         for (int c = 0; c < KD_CB; ++c) { e[c] = e0[c]; e0[c] = e1[c]; }
-        m0 = m1; m1 = m2; m2 = m3; pl0 = pl1; wc0 = wc1; pl1 = pl2; wc1 = wc2;
+        m0 = m1; m1 = m2; m2 = m3;
+        lo0 = lo1; pos0 = pos1; wc0 = wc1; lo1 = lo2; pos1 = pos2; wc1 = wc2;
         incl0 = incl1; delta0 = delta1; raw_total0 = raw_total1;
-        (void)pl;
 
         if (k > KD_KCAP) {                              // reported by the sizes pass
-            if (lane == 0) p.cnt_vals[i] = 0;
+            if (lane == 0) stg(p.cnt_vals, i, 0u);
             continue;
         }
         if (k == 0) {                                   // range txn (sized by rangekeys) / no key here
-            if (lane == 0) p.cnt_vals[i] = p.cnt_vub[i];
+            if (lane == 0) stg(p.cnt_vals, i, ldg(p.cnt_vub, i));
             continue;
         }
         uint32_t my_key = 0;
-        if (lane < k) my_key = p.key_ord[k0 + lane];
-        const uint32_t gi = p.txn_index ? p.txn_index[i] : i;   // global stream position
-        const uint32_t key_base = p.kd_key_off[i], val_base = p.vub_off[i], k2v_base = p.kd_k2v_off[i];
+        if (lane < k) my_key = ldg(p.key_ord, k0 + lane);
+        const uint32_t gi = p.txn_index ? ldg(p.txn_index, i) : i;   // global stream position
+        const uint32_t key_base = ldg(p.kd_key_off, i), val_base = ldg(p.vub_off, i), k2v_base = ldg(p.kd_k2v_off, i);
+        const uint32_t nb = SPAN - gi;                  // near bit of txn j: j + nb (< SPAN iff near)
 
         // ---- keys and keysToTxnIds header from the witnessed counts ----
         const bool ne = lane < k && wc != 0;
@@ -502,8 +529,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         const uint32_t wincl = wave_incl_scan(lane < k ? wc : 0u);
         if (ne) {
             const uint32_t ns = (uint32_t)__popcll(ne_bal & lt);
-            p.kd_keys[key_base + ns] = my_key;
-            p.kd_k2v[k2v_base + ns] = (int32_t)(kc + wincl);
+            stg(p.kd_keys, key_base + ns, my_key);
+            stg(p.kd_k2v, k2v_base + ns, (int32_t)(kc + wincl));
         }
 
 #pragma unroll
@@ -511,8 +538,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         if (lane == 0) L.far_count = 0;
         wave_lds_sync();
 
-        // ---- phase 1: witness filter -> near bitmap / far list ----
-        const int64_t base = (int64_t)gi - (int64_t)SPAN;
+        // ---- phase 1: witness filter -> near bitmap / far list; e[] becomes j / KD_FAR|f / KD_NONE ----
         const bool one_batch = raw_total <= 64u * KD_CB;
         for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
             if (r0) load_batch(p, r0, raw_total, k, incl, delta, e, lane);
@@ -520,16 +546,20 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             for (int c = 0; c < KD_CB; ++c) {
                 if (r0 + c * 64 >= raw_total) break;    // wave-uniform early exit
                 const uint32_t ev = e[c];
+                uint32_t out = KD_NONE;
                 if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
                     const uint32_t j = ev & ENT_TXN_MASK;
-                    if ((int64_t)j >= base) {
-                        const uint32_t b = (uint32_t)((int64_t)j - base);
+                    const uint32_t b = j + nb;
+                    if (b < SPAN) {
                         atomicOr(&L.bitmap[b >> 6], 1ull << (b & 63));
+                        out = j;
                     } else {
                         const uint32_t f = atomicAdd(&L.far_count, 1u);
                         if (f < KD_FARCAP) L.far[f] = j;
+                        out = KD_FAR | f;
                     }
                 }
+                e[c] = out;
             }
         }
         wave_lds_sync();
@@ -538,12 +568,12 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             if (lane == 0) {
                 atomicAdd(&p.status->overflow, 1u);
                 atomicMin(&p.status->overflow_first, i);
-                p.cnt_vals[i] = 0;
+                stg(p.cnt_vals, i, 0u);
             }
             continue;
         }
 
-        // ---- union: near popcounts, far owners ----
+        // ---- union: near popcounts, far owners and ranks ----
         uint32_t pc[WPL];
         uint32_t mysum = 0;
 #pragma unroll
@@ -551,50 +581,78 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         const uint32_t incl2 = wave_incl_scan(mysum);
         const uint32_t near_u = readlane(incl2, 63);
         uint32_t far_u = 0;
-        for (uint32_t f = lane; f < F; f += 64) {
-            const uint32_t x = L.far[f] & 0x7FFFFFFFu;
-            bool owner = true;
-            for (uint32_t g = 0; g < f; ++g)
-                if ((L.far[g] & 0x7FFFFFFFu) == x) { owner = false; break; }
-            far_u += owner ? 1u : 0u;
-            if (owner) L.far[f] = x | 0x80000000u;
+        if (F) {                                        // wave-uniform
+            constexpr uint32_t OWN = 0x80000000u;       // first occurrence of its value
+            for (uint32_t f = lane; f < F; f += 64) {
+                const uint32_t x = L.far[f] & ENT_TXN_MASK;
+                bool owner = true;
+                for (uint32_t g = 0; g < f; ++g)
+                    if ((L.far[g] & ENT_TXN_MASK) == x) { owner = false; break; }
+                far_u += owner ? 1u : 0u;
+                if (owner) L.far[f] = x | OWN;
+            }
+            wave_lds_sync();
+            for (uint32_t f = lane; f < F; f += 64) {   // far values all precede the near ones
+                const uint32_t x = L.far[f] & ENT_TXN_MASK;
+                uint32_t rk = 0;
+                for (uint32_t g = 0; g < F; ++g) {
+                    const uint32_t y = L.far[g];
+                    rk += ((y & OWN) && (y & ENT_TXN_MASK) < x) ? 1u : 0u;
+                }
+                L.far_rank[f] = rk;
+            }
+            far_u = wave_sum(far_u);
         }
-        far_u = wave_sum(far_u);
-        if (lane == 0) p.cnt_vals[i] = far_u + near_u;
+        if (lane == 0) stg(p.cnt_vals, i, far_u + near_u);
 
         // ---- fill: per witnessed entry its rank -> keysToTxnIds body and txnIds ----
         {
-            uint32_t ex = incl2 - mysum;
+            uint32_t ex = incl2 - mysum + far_u;
 #pragma unroll
             for (int q = 0; q < WPL; ++q) { L.wprefix[lane * WPL + q] = ex; ex += pc[q]; }
         }
         wave_lds_sync();
         uint32_t running = 0;
         for (uint32_t r0 = 0; r0 < raw_total; r0 += 64u * KD_CB) {
-            if (!one_batch) load_batch(p, r0, raw_total, k, incl, delta, e, lane);
+            if (!one_batch) {                           // rare: re-load and re-filter this batch
+                load_batch(p, r0, raw_total, k, incl, delta, e, lane);
+#pragma unroll
+                for (int c = 0; c < KD_CB; ++c) {
+                    const uint32_t ev = e[c];
+                    uint32_t out = KD_NONE;
+                    if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
+                        const uint32_t j = ev & ENT_TXN_MASK;
+                        if (j + nb < SPAN) {
+                            out = j;
+                        } else {
+                            for (uint32_t g = 0; g < F; ++g)
+                                if ((L.far[g] & ENT_TXN_MASK) == j) { out = KD_FAR | g; break; }
+                        }
+                    }
+                    e[c] = out;
+                }
+            }
 #pragma unroll
             for (int c = 0; c < KD_CB; ++c) {
                 if (r0 + c * 64 >= raw_total) break;    // wave-uniform early exit
                 const uint32_t ev = e[c];
-                const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
-                const uint32_t j = ev & ENT_TXN_MASK;
-                uint32_t rank = 0;
+                const bool wit = ev != KD_NONE;
+                uint32_t rank = 0, j = ev;
                 if (wit) {
-                    if ((int64_t)j >= base) {
-                        const uint32_t b = (uint32_t)((int64_t)j - base);
-                        rank = far_u + L.wprefix[b >> 6] + (uint32_t)__popcll(L.bitmap[b >> 6] & ((1ull << (b & 63)) - 1ull));
+                    if (ev & KD_FAR) {
+                        const uint32_t f = ev & ~KD_FAR;
+                        rank = L.far_rank[f];
+                        j = L.far[f] & ENT_TXN_MASK;
                     } else {
-                        for (uint32_t g = 0; g < F; ++g) {
-                            const uint32_t y = L.far[g];
-                            rank += ((y & 0x80000000u) && (y & 0x7FFFFFFFu) < j) ? 1u : 0u;
-                        }
+                        const uint32_t b = ev + nb;
+                        rank = L.wprefix[b >> 6] + (uint32_t)__popcll(L.bitmap[b >> 6] & ((1ull << (b & 63)) - 1ull));
                     }
                 }
                 const uint64_t bal = __ballot(wit);
                 const uint32_t pos = running + (uint32_t)__popcll(bal & lt);
                 if (wit) {
-                    p.kd_k2v[k2v_base + kc + pos] = (int32_t)rank;
-                    p.vgap[val_base + rank] = j;            // every holder of j writes the same word
+                    stg(p.kd_k2v, k2v_base + kc + pos, (int32_t)rank);
+                    stg(p.vgap, val_base + rank, j);    // every holder of j writes the same word
                 }
                 running += (uint32_t)__popcll(bal);
             }
@@ -696,7 +754,7 @@ size_t history_temp_bytes(uint32_t P)
 
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, unsigned long long *poslo, uint32_t *wcnt, void *temp, hipStream_t s)
+                    uint32_t *seg_end, PairSlice *slice, void *temp, hipStream_t s)
 {
     (void)nkeys;
     if (P == 0) return;
@@ -715,16 +773,16 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
     hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tile_cnt, ccarry, tiles);
     hipLaunchKernelGGL(history2_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P, window,
                        sorted_key, sorted_pair, hist,
-                       seg_start, pw_local, tile_max, c_local, ccarry, poslo, wcnt);
+                       seg_start, pw_local, tile_max, c_local, ccarry, slice);
 }
 
-void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const uint32_t *wcnt, uint32_t *cnt_keys,
+void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *slice, uint32_t *cnt_keys,
                           uint32_t *cnt_vub, uint32_t *cnt_k2v, DevStatus *status, hipStream_t s)
 {
     if (n == 0) return;
     uint32_t blocks = (n + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(keydeps_sizes_kernel, dim3(blocks), dim3(256), 0, s, n, key_off, wcnt, cnt_keys, cnt_vub,
+    hipLaunchKernelGGL(keydeps_sizes_kernel, dim3(blocks), dim3(256), 0, s, n, key_off, slice, cnt_keys, cnt_vub,
                        cnt_k2v, status);
 }
 

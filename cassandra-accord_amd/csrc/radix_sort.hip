@@ -37,6 +37,10 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint32_t *__restr
     for (uint32_t b = tid; b < bins; b += RS_THREADS) hist[b * tiles + blockIdx.x] = h[b];
 }
 
+// Downsweep: every wave ranks its own contiguous quarter of the tile (16 rounds of 64 items) with
+// wave ballots against a wave-private running digit count in LDS -- no block barrier per round --
+// then one block scan of the digit totals places each wave's runs, the tile is re-ordered by digit
+// in LDS and written out as contiguous per-digit runs.
 template <int BITS>
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
@@ -47,28 +51,29 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
     const uint32_t MASK = mask;
     __shared__ uint32_t s_keys[RS_TILE];
     __shared__ uint32_t s_vals[RS_TILE];
-    __shared__ uint32_t run[BINS];        // tile-local running count, then exclusive tile start
-    __shared__ uint32_t glob[BINS];       // global offset of this tile's digit-d run
-    __shared__ uint32_t wcnt[RS_WAVES][BINS];
+    __shared__ uint32_t run[BINS];              // exclusive tile start of digit d
+    __shared__ uint32_t glob[BINS];             // global offset of this tile's digit-d run
+    __shared__ uint32_t wcnt[RS_WAVES][BINS];   // wave-private running counts, then wave offsets
     __shared__ uint32_t wsum[RS_WAVES];
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    for (uint32_t b = tid; b < BINS; b += RS_THREADS) { run[b] = 0; glob[b] = b <= mask ? offs[b * tiles + blockIdx.x] : 0u; }
+    for (uint32_t b = tid; b < BINS; b += RS_THREADS) glob[b] = b <= mask ? offs[b * tiles + blockIdx.x] : 0u;
+    for (uint32_t b = tid; b < RS_WAVES * BINS; b += RS_THREADS) (&wcnt[0][0])[b] = 0;
     const uint64_t lt = lanemask_lt();
     const uint32_t base = blockIdx.x * RS_TILE;
     const uint32_t tile_n = min((uint32_t)RS_TILE, n - base);
+    const uint32_t wbase = base + w * (RS_ITEMS * 64);
 
     uint32_t key[RS_ITEMS], val[RS_ITEMS], lrank[RS_ITEMS];
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const uint32_t idx = base + r * RS_THREADS + tid;
+        const uint32_t idx = wbase + r * 64 + lane;
         key[r] = idx < n ? kin[idx] : 0u;
         val[r] = idx < n ? (vin ? vin[idx] : idx) : 0u;
     }
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        for (uint32_t b = tid; b < RS_WAVES * BINS; b += RS_THREADS) (&wcnt[0][0])[b] = 0;
-        __syncthreads();
-        const uint32_t idx = base + r * RS_THREADS + tid;
+        const uint32_t idx = wbase + r * 64 + lane;
         const bool valid = idx < n;
         const uint32_t d = (key[r] >> shift) & MASK;
         uint64_t peers = __ballot(valid);
@@ -78,32 +83,27 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
             peers &= ((d >> b) & 1) ? bb : ~bb;
         }
         const uint32_t rank = (uint32_t)__popcll(peers & lt);
-        if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = run[d] + rank;
-            for (uint32_t ww = 0; ww < w; ++ww) pos += wcnt[ww][d];
-            lrank[r] = pos;
-        }
-        __syncthreads();
-        for (uint32_t b = tid; b < BINS; b += RS_THREADS) {
-            uint32_t add = 0;
-#pragma unroll
-            for (int ww = 0; ww < RS_WAVES; ++ww) add += wcnt[ww][b];
-            run[b] += add;
-        }
-        __syncthreads();   // wcnt is cleared by the next round
+        const uint32_t before = valid ? wcnt[w][d] : 0u;
+        wave_lds_sync();
+        if (valid && rank == 0) wcnt[w][d] = before + (uint32_t)__popcll(peers);
+        lrank[r] = before + rank;                 // rank among this wave's items of digit d
+        wave_lds_sync();
     }
     __syncthreads();
-    // exclusive scan of the tile's digit counts (BINS <= 512: each thread owns <= 2 bins)
+    // digit totals of the tile, wave offsets per digit, exclusive scan over digits
     {
         constexpr uint32_t PER = (BINS + RS_THREADS - 1) / RS_THREADS;
         uint32_t c[PER], s = 0;
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t b = tid * PER + q;
-            c[q] = b < BINS ? run[b] : 0u;
-            s += c[q];
+            uint32_t tot = 0;
+            if (b < BINS) {
+#pragma unroll
+                for (int ww = 0; ww < RS_WAVES; ++ww) { const uint32_t x = wcnt[ww][b]; wcnt[ww][b] = tot; tot += x; }
+            }
+            c[q] = tot;
+            s += tot;
         }
         const uint32_t inc = wave_incl_scan(s);
         if (lane == 63) wsum[w] = inc;
@@ -120,10 +120,10 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const uint32_t idx = base + r * RS_THREADS + tid;
+        const uint32_t idx = wbase + r * 64 + lane;
         if (idx < n) {
             const uint32_t d = (key[r] >> shift) & MASK;
-            const uint32_t q = run[d] + lrank[r];
+            const uint32_t q = run[d] + wcnt[w][d] + lrank[r];
             s_keys[q] = key[r];
             s_vals[q] = val[r];
         }

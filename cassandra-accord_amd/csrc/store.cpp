@@ -97,7 +97,7 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipSetDevice(s->cfg.device);
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
-                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->poslo, &s->hist_tmp, &s->wcnt, &s->cnt_vub, &s->vub_off, &s->vgap,
+                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap,
                       &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
@@ -129,6 +129,7 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     if (!s || !b || !b->msb || !b->lsb || !b->node || !b->key_off || (!b->key_ord && b->n))
         return fail(s, ACCORD_ERR_ARG, "accord_batch_upload: null argument");
     if (b->n >= (1u << 29)) return fail(s, ACCORD_ERR_CAPACITY, "batch of %u txns exceeds 2^29", b->n);
+    if (b->key_off[b->n] >= (1u << 28)) return fail(s, ACCORD_ERR_CAPACITY, "batch of %u (txn, key) pairs exceeds 2^28", b->key_off[b->n]);
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     const uint32_t n = b->n;
     for (uint32_t i = 0; i < n; ++i)   // CSR sanity before anything indexes with it
@@ -198,8 +199,7 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->tmp_key.ensure((size_t)P * 4));
     HIPCHECK(s, s->tmp_val.ensure((size_t)P * 4));
     HIPCHECK(s, s->hist.ensure((size_t)P * 4));
-    HIPCHECK(s, s->poslo.ensure((size_t)P * 8));
-    HIPCHECK(s, s->wcnt.ensure((size_t)P * 4));
+    HIPCHECK(s, s->slice.ensure((size_t)P * sizeof(accord::PairSlice)));
     HIPCHECK(s, s->cnt_vub.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->vub_off.ensure(n1 * 4));
     HIPCHECK(s, s->hist_tmp.ensure(accord::history_temp_bytes(P)));
@@ -250,7 +250,7 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, hipMemsetAsync(s->seg_end.p, 0, (size_t)nkeys * 4, st));
     accord::launch_history(P, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
                            s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
-                           s->seg_end.as<uint32_t>(), s->poslo.as<unsigned long long>(), s->wcnt.as<uint32_t>(),
+                           s->seg_end.as<uint32_t>(), s->slice.as<accord::PairSlice>(),
                            s->hist_tmp.p, st);
     record(s, EV_SEGMENT);
 
@@ -261,8 +261,7 @@ int32_t accord_deps_compute(accord_store *s)
     kp.txn_index = s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr;
     kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
     kp.hist = s->hist.as<uint32_t>();
-    kp.poslo = s->poslo.as<unsigned long long>();
-    kp.wcnt = s->wcnt.as<uint32_t>();
+    kp.slice = s->slice.as<accord::PairSlice>();
     kp.cnt_vub = s->cnt_vub.as<uint32_t>();
     kp.cnt_vals = s->cnt_vals.as<uint32_t>();
     kp.status = &dev->status;
@@ -281,7 +280,7 @@ int32_t accord_deps_compute(accord_store *s)
     rp.status = &dev->status;
 
     // sizes: key txns from the per-pair witnessed counts, range txns by their own count pass
-    accord::launch_keydeps_sizes(n, kp.key_off, s->wcnt.as<uint32_t>(), rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
+    accord::launch_keydeps_sizes(n, kp.key_off, kp.slice, rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
                                  rp.cnt_k2v, &dev->status, st);
     if (nrt) accord::launch_rangekeys_count(rp, st);
     if (R) accord::launch_rangedeps_count(rp, st);
@@ -318,8 +317,9 @@ int32_t accord_deps_compute(accord_store *s)
         const HostTotals &h = *s->pinned;
         int32_t rc = check_status(h);
         if (rc) return rc;
+        // the device kernels address every output array with 32-bit byte offsets
         for (int t = 0; t < 6; ++t)
-            if (h.totals[t] >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "deps output exceeds 2^32 entries");
+            if (h.totals[t] >= (1ull << 30)) return fail(s, ACCORD_ERR_CAPACITY, "deps output exceeds 2^30 entries");
         s->tot_keys = h.totals[0]; s->tot_k2v = h.totals[2];
         s->tot_rngs = h.totals[3]; s->tot_rvals = h.totals[4]; s->tot_r2v = h.totals[5];
     }

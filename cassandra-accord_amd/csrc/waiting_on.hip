@@ -66,8 +66,8 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
         uint32_t o = FILL ? p.pred_off[i] : 0;
         if (reduce) {
             for (uint32_t q = p.key_off[i]; q < p.key_off[i + 1]; ++q) {
-                const unsigned long long pl = p.poslo[q];
-                const uint32_t pos = (uint32_t)pl, lo = (uint32_t)(pl >> 32);
+                const PairSlice ps = p.slice[q];
+                const uint32_t pos = ps.pos, lo = ps.lo;
                 if (pos == lo) continue;
                 const uint32_t x = pos - 1;
                 const uint32_t pw = max(p.pw_local[x], p.pw_carry[x / p.pw_tile]);   // (last Write <= x) + 1

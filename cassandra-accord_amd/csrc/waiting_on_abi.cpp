@@ -46,7 +46,7 @@ int32_t accord_waiting_on_compute(accord_store *s)
     p.n = n;
     p.lsb = s->lsb.as<uint64_t>();
     p.key_off = s->key_off.as<uint32_t>();
-    p.poslo = s->poslo.as<unsigned long long>();
+    p.slice = s->slice.as<accord::PairSlice>();
     p.hist = s->hist.as<uint32_t>();
     p.pw_local = s->hist_tmp.as<uint32_t>();
     p.pw_carry = p.pw_local + s->P;
