@@ -149,9 +149,11 @@ void launch_wo_bits(uint32_t n, const uint32_t *kd_key_off, const uint32_t *rd_v
                     unsigned long long *words, hipStream_t s);
 void launch_wo_preds_count(const WaitingOnParams &p, hipStream_t s);
 void launch_wo_preds_fill(const WaitingOnParams &p, hipStream_t s);
-// level[i] for all i; info[0] = 1 + chunk that hit the defensive round bound (must stay 0),
-// info[1] = max level.  info must be zeroed before the launch.
+// level[i] for all i; info[0] = 1 + chunks resolved when a wave hit the defensive spin bound
+// (must stay 0), info[1] = max level, info[2] = 1 if a predecessor does not precede its txn.
+// info must be zeroed before the launch; temp holds levels_temp_bytes(n).
+size_t levels_temp_bytes(uint32_t n);
 void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level, uint32_t *info,
-                   hipStream_t s);
+                   void *temp, hipStream_t s);
 
 } // namespace accord

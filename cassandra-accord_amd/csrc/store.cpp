@@ -106,7 +106,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rd_vals, &s->rd_r2v, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
-                      &s->level, &s->wo_info};
+                      &s->level, &s->wo_info, &s->lv_tmp};
     accord_impl::shard_comm_destroy(s);
     for (DevBuf *b : bufs) b->release();
     if (s->events)

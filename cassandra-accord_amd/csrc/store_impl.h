@@ -74,7 +74,7 @@ struct accord_store {
     float xchg_ms = 0, merge_ms = 0;
     // WaitingOn + levelling (waiting_on_abi.cpp)
     bool wo_done = false;
-    DevBuf wo_cnt, wo_off, wo_words, pred_cnt, pred_off, preds, level, wo_info;
+    DevBuf wo_cnt, wo_off, wo_words, pred_cnt, pred_off, preds, level, wo_info, lv_tmp;
     uint64_t wo_words_total = 0, preds_total = 0;
     uint32_t max_level = 0;
     float wo_ms[3] = {0, 0, 0};

@@ -14,12 +14,15 @@
 // of k's history in [lo, i).  Every Write w in that slice depends on every earlier witnessed entry
 // of the slice (their slices nest), so max level over the slice = max over {the last Write lw of
 // the slice} and, when i is a Write, the Reads after lw.  Only those are kept as predecessors.
-// Then one persistent workgroup sweeps the txns in order, 1024 at a time: a txn publishes its level
-// in LDS once all its predecessors have (frontier rounds with a ready flag per txn; predecessors
-// of earlier chunks are final in HBM).  The chain depth of the batch bounds this kernel.
+// The levels themselves come from a chunked max-plus closure of that DAG (see lv_closure_kernel /
+// lv_resolve_kernel below).
 #include "device_common.h"
 #include "kernels.h"
 #include "../../include/accord_deps.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 namespace accord {
 
@@ -101,102 +104,323 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
     }
 }
 
-constexpr int LV_THREADS = 1024;
-constexpr int LV_PREG = 8;        // in-chunk predecessors held in registers; more go the slow way
+// ---- execution levelling: chunked max-plus closure ----
+// The chain depth of the reduced DAG is a large fraction of n (config 5: ~0.36 n, the Write
+// chain of the hottest key), so resolving one level per step is hopeless.  Instead:
+//   pass 1 (parallel, one wave per chunk of 64 consecutive txns): the longest-path closure of the
+//     chunk's own sub-DAG, dist(i, j) for j -> ... -> i inside the chunk, and the chunk's far
+//     predecessors.  With v = level + 1 and basev(j) = 1 + max v over j's far predecessors (1
+//     without), v(i) = max over in-chunk ancestors j of i (and j = i) of basev(j) + dist(i, j).
+//     Columns of txns without far predecessors (basev = 1) fold into one constant per row.
+//   pass 2 (one workgroup, LV_WAVES waves, wave w owns chunks w, w + LV_WAVES, ...): per chunk
+//     gather the far predecessors' v (LDS ring of the last LV_RING txns, older ones from HBM,
+//     prefetched a round ahead), then one max-plus matrix-vector product (lane = row).  Columns
+//     whose predecessors lie in chunks <= x-2 are done while chunk x-1 is still being resolved by
+//     another wave; only the "late" columns (a predecessor in chunk x-1) sit on the critical path.
+constexpr uint32_t LC = 64;                 // txns per chunk
+constexpr int LV_REFS = 8;                  // far predecessors kept per entry column
+constexpr uint32_t LV_RING = 16384;         // pass-2 LDS ring of v (64 KiB)
+constexpr uint32_t LV_ROW = 68;             // closure row stride in LDS (bytes; 17 dwords)
+constexpr uint32_t REF_NONE = 0xFFFFFFFFu;
+// per-chunk record (u32 words): cst[64] | bq[16][64] | ref[LV_REFS][64] | node[64] | hdr[64]
+constexpr uint32_t RC_CST = 0, RC_BQ = 64, RC_REF = RC_BQ + 16 * 64, RC_NODE = RC_REF + LV_REFS * 64,
+                   RC_HDR = RC_NODE + 64, RC_WORDS = RC_HDR + 64;
+static_assert(LV_RING % LC == 0, "ring holds whole chunks");
+constexpr int LV_WAVES_MAX = 16;
+static_assert(LV_RING >= 2 * LC * LV_WAVES_MAX, "old predecessors must be final one round ahead");
 
-// One workgroup; txns in chunks of LV_THREADS.  At chunk start every lane folds its predecessors
-// from earlier chunks (final in HBM) into `best` and keeps the in-chunk ones as LDS slot indices
-// in registers.  Then lanes poll the slots (lv[s] = level + 1, 0 = pending) until all are final;
-// lanes never block (a wave retries in rounds, since lanes of one wave cannot wait on each
-// other) and the lowest pending txn of a chunk can always finish, so each chunk drains.
-// A hop along a dependency chain costs one LDS round trip.  info[0] = 1 + the chunk that hit the
-// (defensive) round bound, then all stop; info[1] = max level.
-__global__ __launch_bounds__(LV_THREADS) void level_kernel(uint32_t n, const uint32_t *__restrict__ pred_off,
-                                                           const uint32_t *__restrict__ preds,
-                                                           uint32_t *__restrict__ level, uint32_t *__restrict__ info)
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 {
-    __shared__ uint32_t lv[LV_THREADS];
-    __shared__ uint32_t smax, sabort;
-    const uint32_t t = threadIdx.x;
-    uint32_t mymax = 0;
-    if (t == 0) { smax = 0; sabort = 0; }
-    for (uint32_t base = 0; base < n; base += LV_THREADS) {
-        const uint32_t i = base + t;
-        lv[t] = 0;
-        bool done = i >= n;
-        uint32_t best = 0;                 // 1 + max over folded predecessors
-        uint32_t slot[LV_PREG];
-        uint32_t nslot = 0;
-        uint32_t slow_next = 0, slow_end = 0;   // in-chunk predecessors beyond LV_PREG (global list)
-        if (!done) {
-            const uint32_t q0 = pred_off[i], q1 = pred_off[i + 1];
-            for (uint32_t q = q0; q < q1; ++q) {
-                const uint32_t j = preds[q];
-                if (j < base) {
-                    best = max(best, level[j] + 1);
-                } else if (nslot < LV_PREG) {
+    const uint32_t lo = readlane((uint32_t)v, l), hi = readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Pass 1.  Record layout per row i (node order): cst = max over non-entry columns j reaching i of
+// 1 + b(i,j); bq = b(i, slot) bytes in slot order, b = dist + 1 (0 = j does not reach i).  Slots:
+// late entries, then early entries, then non-entries.  ref[s][slot] = the slot's far predecessors.
+// hdr = nl | ne << 8 | slow << 16 (slow: some entry has more than LV_REFS far predecessors).
+__global__ __launch_bounds__(256) void lv_closure_kernel(uint32_t n, uint32_t nchunks,
+                                                         const uint32_t *__restrict__ pred_off,
+                                                         const uint32_t *__restrict__ preds,
+                                                         uint32_t *__restrict__ rec, uint32_t *__restrict__ info)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t rows_all[4][64 * LV_ROW];
+    __shared__ uint32_t snode_all[4][64];
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t x = blockIdx.x * 4 + w;
+    if (x >= nchunks) return;                       // wave-uniform
+    uint8_t *rows = rows_all[w];
+    uint32_t *snode = snode_all[w];
+    const uint32_t base = x * LC, t = base + lane;
+    const bool valid = t < n;
+    uint64_t inmask = 0;
+    uint32_t ref[LV_REFS];
 #pragma unroll
-                    for (int r = 0; r < LV_PREG; ++r)
-                        if (r == (int)nslot) slot[r] = j - base;
-                    ++nslot;
-                } else {
-                    if (slow_end == 0) slow_next = q;
-                    slow_end = q + 1;
-                }
-            }
-        }
-        // gate: the latest in-chunk predecessor (the one a chain waits on); poll only it, then
-        // confirm the others once it is final
-        uint32_t gate = 0;
+    for (int s = 0; s < LV_REFS; ++s) ref[s] = REF_NONE;
+    uint32_t nfar = 0;
+    bool late = false, bad = false;
+    if (valid) {
+        const uint32_t q0 = pred_off[t], q1 = pred_off[t + 1];
+        for (uint32_t q = q0; q < q1; ++q) {
+            const uint32_t f = preds[q];
+            if (f >= t) { bad = true; continue; }
+            if (f >= base) { inmask |= 1ull << (f - base); continue; }
+            bool dup = false;
 #pragma unroll
-        for (int r = 0; r < LV_PREG; ++r)
-            if (r < (int)nslot) gate = max(gate, slot[r]);
-        __syncthreads();
-        uint32_t rounds = 0;
-        while (true) {
-            bool moved = false;
-            if (!done && (nslot == 0 || __hip_atomic_load(&lv[gate], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)) {
-                bool ok = true;
-                uint32_t b2 = best;
+            for (int s = 0; s < LV_REFS; ++s) dup = dup || ref[s] == f;
+            if (dup) continue;
+            late = late || f + LC >= base;
 #pragma unroll
-                for (int r = 0; r < LV_PREG; ++r) {
-                    if (r < (int)nslot) {
-                        const uint32_t v = __hip_atomic_load(&lv[slot[r]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (v == 0 && ok) gate = slot[r];
-                        ok = ok && v != 0;
-                        b2 = max(b2, v);
-                    }
-                }
-                while (ok && slow_next < slow_end) {
-                    const uint32_t j = preds[slow_next];
-                    if (j >= base) {
-                        const uint32_t v = __hip_atomic_load(&lv[j - base], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (v == 0) { ok = false; break; }
-                        best = max(best, v);
-                    }
-                    ++slow_next;
-                }
-                if (ok) {
-                    best = max(best, b2);
-                    __hip_atomic_store(&lv[t], best + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    level[i] = best;
-                    mymax = max(mymax, best);
-                    done = moved = true;
-                }
-            }
-            if (__all(done)) break;
-            if (++rounds > (1u << 22)) { sabort = 1; break; }   // defensive bound: never hit by a DAG
-            // no s_sleep: a chain hop is one LDS round trip of the waiting wave
-        }
-        __syncthreads();
-        if (sabort) {
-            if (t == 0) info[0] = 1 + base / LV_THREADS;
-            break;
+            for (int s = 0; s < LV_REFS; ++s)
+                if (s == (int)nfar) ref[s] = f;
+            ++nfar;
         }
     }
-    atomicMax(&smax, mymax);
+    if (bad) atomicOr(&info[2], 1u);
+    const bool entry = nfar > 0;
+    const uint64_t lm = __ballot(entry && late), em = __ballot(entry && !late);
+    const uint32_t nl = (uint32_t)__popcll(lm), ne = nl + (uint32_t)__popcll(em);
+    const uint64_t lt = lanemask_lt();
+    const uint32_t slot = entry ? (late ? (uint32_t)__popcll(lm & lt) : nl + (uint32_t)__popcll(em & lt))
+                                : ne + (uint32_t)__popcll(~(lm | em) & lt);
+    const bool slow = __ballot(nfar > (uint32_t)LV_REFS) != 0;
+    snode[slot] = lane;
+    wave_lds_sync();
+    const uint32_t mynode = snode[lane];           // the node of column slot `lane`
+
+    // closure, rows in node order; every lane owns one column (its own LDS bytes only)
+    for (uint32_t i = 0; i < LC; ++i) {
+        uint64_t mm = readlane64(inmask, (int)i);
+        uint32_t v = mynode == i ? 1u : 0u;
+        while (mm) {
+            const uint32_t p = (uint32_t)__builtin_ctzll(mm);
+            mm &= mm - 1;
+            const uint32_t bp = rows[p * LV_ROW + lane];
+            v = max(v, bp ? bp + 1u : 0u);
+        }
+        rows[i * LV_ROW + lane] = (uint8_t)v;
+    }
+    wave_lds_sync();
+
+    uint32_t *r = rec + (size_t)x * RC_WORDS;
+    uint32_t cst = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const uint32_t d = *(const uint32_t *)(rows + lane * LV_ROW + 4 * q);
+        r[RC_BQ + q * 64 + lane] = d;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t b = (d >> (8 * c)) & 0xFFu;
+            if ((uint32_t)(4 * q + c) >= ne && b) cst = max(cst, b + 1u);
+        }
+    }
+    r[RC_CST + lane] = cst;
+#pragma unroll
+    for (int s = 0; s < LV_REFS; ++s) r[RC_REF + s * 64 + slot] = ref[s];
+    r[RC_NODE + slot] = lane;
+    r[RC_HDR + lane] = nl | (ne << 8) | (slow ? 1u << 16 : 0u);
+}
+
+struct LvRec {
+    uint32_t cst, bq[16], ref[LV_REFS], node, hdr;
+};
+
+__device__ __forceinline__ void lv_load(const uint32_t *__restrict__ rec, uint32_t x, uint32_t nchunks, uint32_t lane,
+                                        LvRec &o)
+{
+    if (x >= nchunks) { o.hdr = 0; return; }
+    const uint32_t *r = rec + (size_t)x * RC_WORDS;
+    o.cst = r[RC_CST + lane];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) o.bq[q] = r[RC_BQ + q * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < LV_REFS; ++s) o.ref[s] = r[RC_REF + s * 64 + lane];
+    o.node = r[RC_NODE + lane];
+    o.hdr = r[RC_HDR + lane];
+}
+
+// Spin on the LDS count of resolved chunks; false once any wave gave up (defensive bound).
+__device__ __forceinline__ bool lv_wait(uint32_t *done, uint32_t *abort_flag, uint32_t target)
+{
+    uint32_t spins = 0;
+    while (__builtin_amdgcn_readfirstlane(
+               __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
+        if ((++spins & 255u) == 0) {            // rarely: another wave gave up, or the bound is hit
+            if (__builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                return false;
+            if (spins > (1u << 26)) {
+                __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+// Column slot m of row `lane` as a signed addend: b(row, m) (= dist + 1) when m reaches the row,
+// INT_MIN otherwise, so basev(m) + d never wins a signed max (basev < 2^31).
+__device__ __forceinline__ void lv_expand(const uint32_t (&bq)[16], int32_t (&d)[64])
+{
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+        const uint32_t b = (bq[m >> 2] >> (8 * (m & 3))) & 0xFFu;
+        d[m] = b ? (int32_t)b : INT32_MIN;
+    }
+}
+
+// acc = max(acc, basev(m) + d(row, m)) over column slots [lo, hi) widened to groups of 8.  Extra
+// columns are harmless: a non-entry column has basev 1 (its share is already in cst) and a column
+// seen with a partial basev only yields a lower bound of the row's value.
+__device__ __forceinline__ int32_t lv_matvec(int32_t acc, const int32_t (&d)[64], uint32_t bv, uint32_t lo,
+                                             uint32_t hi)
+{
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        if ((uint32_t)(8 * g) < hi && (uint32_t)(8 * g + 8) > lo) {      // wave-uniform
+#pragma unroll
+            for (int m = 8 * g; m < 8 * g + 8; m += 2) {
+                const int32_t s0 = (int32_t)readlane(bv, m), s1 = (int32_t)readlane(bv, m + 1);
+                acc = max(acc, max(s0 + d[m], s1 + d[m + 1]));
+            }
+        }
+    }
+    return acc;
+}
+
+struct LvShared {
+    uint32_t ring[LV_RING];
+    uint32_t done, abort_flag, maxlv;
+};
+
+// One chunk of pass 2.  The far predecessors older than the ring are final a whole round before
+// the chunk is processed, so plain loads are safe: every line of level[] read here holds only
+// entries written rounds ago by this workgroup (its own CU), never a line that is still changing.
+// Returns false on abort.
+template <int LV_WAVES>
+__device__ __forceinline__ bool lv_chunk(LvShared &S, uint32_t n, uint32_t x, const LvRec &cur, LvRec &nxt,
+                                         const uint32_t *__restrict__ rec, uint32_t nchunks,
+                                         const uint32_t *__restrict__ pred_off, const uint32_t *__restrict__ preds,
+                                         uint32_t *level, uint32_t lane, uint32_t &mymax,
+                                         unsigned long long *dbg)
+{
+#define LV_STAMP(k) do { if (dbg && lane == 0) dbg[(size_t)x * 5 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+    const uint32_t base = x * LC;
+    const uint32_t hdr = __builtin_amdgcn_readfirstlane(cur.hdr);
+    const uint32_t nl = hdr & 0xFFu, ne = (hdr >> 8) & 0xFFu;
+    const bool slow = (hdr >> 16) & 1u;
+    // issued unconditionally (index 0 when not an old predecessor) so the loads stay in flight
+    uint32_t oldv[LV_REFS];
+#pragma unroll
+    for (int s = 0; s < LV_REFS; ++s) {
+        const uint32_t f = cur.ref[s];
+        const bool old = !slow && f != REF_NONE && f + LV_RING < base;
+        oldv[s] = level[old ? f : 0u];
+    }
+    LV_STAMP(0);
+    int32_t d[64];
+    lv_expand(cur.bq, d);
+    int32_t acc = (int32_t)cur.cst;
+    uint32_t bv = 1, late_hi = nl;
+    if (!slow) {
+        // early columns: every predecessor in chunks <= x-2
+        if (!lv_wait(&S.done, &S.abort_flag, x ? x - 1 : 0)) return false;
+        LV_STAMP(1);
+        uint32_t rv[LV_REFS];
+#pragma unroll
+        for (int s = 0; s < LV_REFS; ++s) {              // LDS reads issued together
+            const uint32_t f = cur.ref[s];
+            rv[s] = S.ring[(f != REF_NONE && f + LC < base) ? f % LV_RING : 0u];
+        }
+        uint32_t e = 0;
+#pragma unroll
+        for (int s = 0; s < LV_REFS; ++s) {
+            const uint32_t f = cur.ref[s];
+            if (f == REF_NONE) continue;
+            e = max(e, f + LV_RING < base ? oldv[s] + 1u : f + LC < base ? rv[s] : 0u);
+        }
+        bv = e + 1u;
+        acc = lv_matvec(acc, d, bv, nl, ne);
+        LV_STAMP(2);
+        // late columns: a predecessor in chunk x-1 (the critical path: run at raised priority)
+        __builtin_amdgcn_s_setprio(2);
+        if (!lv_wait(&S.done, &S.abort_flag, x)) return false;
+        LV_STAMP(3);
+#pragma unroll
+        for (int s = 0; s < LV_REFS; ++s) {
+            const uint32_t f = cur.ref[s];
+            rv[s] = S.ring[(f != REF_NONE && f + LC >= base) ? f % LV_RING : 0u];
+        }
+        uint32_t l = 0;
+#pragma unroll
+        for (int s = 0; s < LV_REFS; ++s) {
+            const uint32_t f = cur.ref[s];
+            if (f != REF_NONE && f + LC >= base) l = max(l, rv[s]);
+        }
+        bv = max(bv, l + 1u);
+    } else {
+        // some entry has more predecessors than the record holds: walk its full list
+        if (!lv_wait(&S.done, &S.abort_flag, x)) return false;
+        __builtin_amdgcn_s_setprio(2);
+        uint32_t e = 0;
+        const uint32_t t = base + cur.node;
+        if (lane < ne && t < n) {
+            for (uint32_t q = pred_off[t], q1 = pred_off[t + 1]; q < q1; ++q) {
+                const uint32_t f = preds[q];
+                if (f >= base) continue;
+                e = max(e, f + LV_RING >= base ? S.ring[f % LV_RING] : level[f] + 1u);
+            }
+        }
+        bv = e + 1u;
+        late_hi = ne;
+    }
+    acc = lv_matvec(acc, d, bv, 0, late_hi);
+    const uint32_t t = base + lane;
+    if (t < n) {
+        const uint32_t v = (uint32_t)acc - 1u;
+        S.ring[t % LV_RING] = v;
+        level[t] = v - 1u;
+        mymax = max(mymax, v - 1u);
+    }
+    wave_lds_sync();
+    if (lane == 0) __hip_atomic_store(&S.done, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    LV_STAMP(4);
+#undef LV_STAMP
+    __builtin_amdgcn_s_setprio(0);
+    // the wave's next record: lands while the wave waits for its next chunk's inputs
+    lv_load(rec, x + LV_WAVES, nchunks, lane, nxt);
+    return true;
+}
+
+// Pass 2.  info[0] = 1 + chunks resolved when a wave gave up (must stay 0), info[1] = max level.
+// Two record register sets alternate (no loop-carried copy, so the next record's loads stay in
+// flight across the whole chunk).
+template <int LV_WAVES>
+__global__ __launch_bounds__(LV_WAVES * 64) void lv_resolve_kernel(uint32_t n, uint32_t nchunks,
+                                                                  const uint32_t *__restrict__ rec,
+                                                                  const uint32_t *__restrict__ pred_off,
+                                                                  const uint32_t *__restrict__ preds,
+                                                                  uint32_t *level, uint32_t *__restrict__ info,
+                                                                  unsigned long long *dbg)
+{
+    __shared__ LvShared S;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    if (threadIdx.x == 0) { S.done = 0; S.abort_flag = 0; S.maxlv = 0; }
     __syncthreads();
-    if (t == 0) info[1] = smax;
+    uint32_t mymax = 0;
+    LvRec ra, rb;
+    lv_load(rec, w, nchunks, lane, ra);
+    for (uint32_t x = w; x < nchunks; x += 2 * LV_WAVES) {
+        if (!lv_chunk<LV_WAVES>(S, n, x, ra, rb, rec, nchunks, pred_off, preds, level, lane, mymax, dbg)) break;
+        if (x + LV_WAVES >= nchunks) break;
+        if (!lv_chunk<LV_WAVES>(S, n, x + LV_WAVES, rb, ra, rec, nchunks, pred_off, preds, level, lane, mymax, dbg)) break;
+    }
+    atomicMax(&S.maxlv, mymax);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (S.abort_flag) info[0] = 1 + S.done;
+        info[1] = S.maxlv;
+    }
 }
 
 } // namespace
@@ -235,11 +459,43 @@ void launch_wo_preds_fill(const WaitingOnParams &p, hipStream_t s)
     hipLaunchKernelGGL(wo_preds_kernel<true>, dim3(b), dim3(256), 0, s, p);
 }
 
+size_t levels_temp_bytes(uint32_t n)
+{
+    const size_t chunks = (n + LC - 1) / LC;
+    return chunks * RC_WORDS * 4 + 64;
+}
+
 void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level, uint32_t *info,
-                   hipStream_t s)
+                   void *temp, hipStream_t s)
 {
     if (n == 0) return;
-    hipLaunchKernelGGL(level_kernel, dim3(1), dim3(LV_THREADS), 0, s, n, pred_off, preds, level, info);
+    const uint32_t nchunks = (n + LC - 1) / LC;
+    uint32_t *rec = (uint32_t *)temp;
+    hipLaunchKernelGGL(lv_closure_kernel, dim3((nchunks + 3) / 4), dim3(256), 0, s, n, nchunks, pred_off, preds, rec,
+                       info);
+    // ACCORD_LV_DEBUG=<file>: per-chunk s_memtime stamps of the resolve pass (development aid)
+    const char *dbg_path = getenv("ACCORD_LV_DEBUG");
+    unsigned long long *dbg = nullptr;
+    if (dbg_path && hipMalloc(&dbg, (size_t)nchunks * 5 * 8) != hipSuccess) dbg = nullptr;
+    const char *nw_env = getenv("ACCORD_LV_WAVES");
+    const int nw = nw_env ? atoi(nw_env) : 8;
+    if (nw == 4)
+        hipLaunchKernelGGL(lv_resolve_kernel<4>, dim3(1), dim3(4 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
+                           info, dbg);
+    else if (nw == 12)
+        hipLaunchKernelGGL(lv_resolve_kernel<12>, dim3(1), dim3(12 * 64), 0, s, n, nchunks, rec, pred_off, preds,
+                           level, info, dbg);
+    else
+        hipLaunchKernelGGL(lv_resolve_kernel<8>, dim3(1), dim3(8 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
+                           info, dbg);
+    if (dbg) {
+        std::vector<unsigned long long> h((size_t)nchunks * 5);
+        if (hipMemcpyAsync(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess) {
+            if (FILE *fp = fopen(dbg_path, "wb")) { fwrite(h.data(), 8, h.size(), fp); fclose(fp); }
+        }
+        (void)hipFree(dbg);
+    }
 }
 
 } // namespace accord

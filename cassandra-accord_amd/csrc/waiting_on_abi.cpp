@@ -38,6 +38,7 @@ int32_t accord_waiting_on_compute(accord_store *s)
     HIPCHECK(s, s->pred_cnt.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->pred_off.ensure(n1 * 4));
     HIPCHECK(s, s->level.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->lv_tmp.ensure(accord::levels_temp_bytes(n)));
     HIPCHECK(s, s->wo_info.ensure(64));
     HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n)));
     HostTotals *dev = s->status_totals.as<HostTotals>();
@@ -75,13 +76,15 @@ int32_t accord_waiting_on_compute(accord_store *s)
     accord::launch_wo_preds_fill(p, st);
     record(s, EV_WO_PREDS);
     HIPCHECK(s, hipMemsetAsync(s->wo_info.p, 0, 64, st));
-    accord::launch_levels(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(), st);
+    accord::launch_levels(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
+                         s->lv_tmp.p, st);
     record(s, EV_WO_LEVEL);
-    uint32_t info[2] = {0, 0};
+    uint32_t info[3] = {0, 0, 0};
     HIPCHECK(s, hipMemcpyAsync(info, s->wo_info.p, sizeof(info), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
-    if (info[0]) return fail(s, ACCORD_ERR_CAPACITY, "levelling did not drain (chunk %u)", info[0] - 1);
+    if (info[2]) return fail(s, ACCORD_ERR_STATE, "a dependency does not precede its txn");
+    if (info[0]) return fail(s, ACCORD_ERR_CAPACITY, "levelling did not drain (%u chunks resolved)", info[0] - 1);
     s->max_level = info[1];
     if (s->events) {
         auto el = [&](int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, s->ev[a], s->ev[b]); return ms; };

@@ -18,6 +18,8 @@ CASES = [
     (15000, 4, 300, 0.99, 0.7, 16, 54, 0.0, 0, True),        # SyncPoints keep full lists
     (10000, 2, 20, 0.0, 1.0, 1000, 55, 0.0, 0, False),       # deep chains (~1000 per key)
     (3000, 1, 1, 0.0, 1.0, 4096, 56, 0.0, 0, False),         # one key, all writes: level = i
+    (60000, 4, 50000, 0.99, 0.9, 256, 59, 0.0, 0, False),    # cold keys: predecessors beyond the LDS ring
+    (20000, 6, 40, 0.0, 0.3, 2000, 60, 0.0, 0, False),       # read-heavy: writes with many far predecessors
 ]
 
 
