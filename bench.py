@@ -193,6 +193,7 @@ def main():
     fill_gbs = Bf / (stage["fill"] * 1e-3) / 1e9 if stage["fill"] > 0 else None
     pipe_gbs = B / (stage["total"] * 1e-3) / 1e9 if stage["total"] > 0 else None
 
+    traffic = measured_traffic(args.config)
     cpu = None
     if not args.no_cpu:
         cpu = cpu_baseline(s_full, args)
@@ -220,7 +221,9 @@ def main():
         "stage_ms": stage,
         "roofline": {"kernel": "keydeps_kernel<1,true> (fill)", "bound": "hbm",
                      "achieved": fill_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None, "traffic": None,
+                     "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
+                     "traffic": traffic["traffic_bytes"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None,
                      "algorithmic_bytes_per_launch": Bf},
         "pipeline_roofline": {"bytes": B, "achieved": pipe_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                               "frac": (pipe_gbs / PEAK_HBM_GBS) if pipe_gbs else None,
@@ -245,6 +248,18 @@ def workload_name(args):
                 f"{args.keys_per_txn} keys/key txn, Zipf({args.zipf}) over {args.keyspace} keys, W={args.window}")
     return (f"config2: {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over {args.keyspace} keys, "
             f"{args.write_frac:.0%} writes, W={args.window}")
+
+
+def measured_traffic(config):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes of the
+    same workload (profiles/traffic_config<N>.json, written by scripts/traffic_json.py): PMC
+    counters need their own rocprofv3 run, so a bench run reports the last committed measurement."""
+    path = os.path.join(ROOT, "profiles", f"traffic_config{config}.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def _cpu_model():

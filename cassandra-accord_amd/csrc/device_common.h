@@ -9,6 +9,12 @@ __device__ __forceinline__ uint32_t lane_id()
 {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
+// Wave index inside the workgroup, as a wave-uniform (scalar) value: threadIdx.x >> 6 alone is a
+// VGPR to the compiler, which then treats every loop and branch derived from it as divergent.
+__device__ __forceinline__ uint32_t wave_id()
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // Order LDS traffic between lanes of ONE wave (waves of a workgroup run different txns, so a

@@ -421,6 +421,26 @@ __device__ __forceinline__ void load_slice(const KeyDepsParams &p, const TxnMeta
 __device__ __forceinline__ void load_batch(const KeyDepsParams &p, uint32_t r0, uint32_t raw_total, uint32_t k,
                                            uint32_t end, int32_t delta, uint32_t (&e)[KD_CB], uint32_t lane)
 {
+    if (k <= 8) {
+        // few slots: the boundaries and deltas sit in SGPRs; a candidate picks its delta by a
+        // compare/select chain (lanes >= k hold end = raw_total, never <= a valid candidate)
+        uint32_t eq[7];
+        int32_t dq[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dq[q] = (int32_t)readlane((uint32_t)delta, q);
+#pragma unroll
+        for (int q = 0; q < 7; ++q) eq[q] = readlane(end, q);
+#pragma unroll
+        for (int c = 0; c < KD_CB; ++c) {
+            e[c] = KD_NONE;
+            const uint32_t r = r0 + c * 64 + lane;
+            int32_t d = dq[0];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) d = r >= eq[q] ? dq[q + 1] : d;
+            if (r < raw_total) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
+        }
+        return;
+    }
     uint32_t q = 0;                                   // uniform: slot of the window's first candidate
 #pragma unroll
     for (int c = 0; c < KD_CB; ++c) {
@@ -458,11 +478,11 @@ __device__ __forceinline__ void slot_setup(uint32_t lo, uint32_t pos, uint32_t k
 // Software pipeline over the wave's txns i, i+S, i+2S, ...: offsets three txns ahead, slices two
 // ahead, and the first batch of history candidates one ahead, so the candidate round trip of the
 // next txn overlaps this txn's LDS work.
-template <int WPL>
-__global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(WPL == 1 ? 8 : 4, 8))) void keydeps_kernel(KeyDepsParams p)
+template <int WPL, int MINW = (WPL == 1 ? 8 : 4)>
+__global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void keydeps_kernel(KeyDepsParams p)
 {
     __shared__ WaveLds<WPL> lds_all[KD_WAVES];
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t w = wave_id(), lane = lane_id();
     WaveLds<WPL> &L = lds_all[w];
     const uint64_t lt = lanemask_lt();
     constexpr uint32_t SPAN = 64u * 64u * WPL;
@@ -666,6 +686,8 @@ void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
     uint32_t blocks = (p.n + KD_WAVES - 1) / KD_WAVES;
     if (blocks > 256u * 16u) blocks = 256u * 16u;
     switch (wpl) {
+    // 8 waves/SIMD caps the kernel at 80 SGPRs (some spill to VGPR lanes); measured faster than
+    // 7 or fewer waves without spills (latency-bound: occupancy wins)
     case 1: hipLaunchKernelGGL((keydeps_kernel<1>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
     case 2: hipLaunchKernelGGL((keydeps_kernel<2>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
     default: hipLaunchKernelGGL((keydeps_kernel<4>), dim3(blocks), dim3(KD_THREADS), 0, s, p); break;
@@ -683,7 +705,7 @@ __global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uin
 {
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t g = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); g * CV_TXNS < n; g += waves) {
+    for (uint32_t g = blockIdx.x * (blockDim.x / 64) + wave_id(); g * CV_TXNS < n; g += waves) {
         const uint32_t t = g * CV_TXNS + (lane & (CV_TXNS - 1));
         uint32_t src = 0, dst = 0, u = 0;
         if (lane < CV_TXNS && t < n) { src = vub_off[t]; dst = val_off[t]; u = val_off[t + 1] - dst; }

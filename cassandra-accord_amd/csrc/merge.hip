@@ -53,7 +53,7 @@ template <bool FILL>
 __global__ __launch_bounds__(MG_WAVES * 64) void merge_kernel(MergeParams p)
 {
     __shared__ MgLds lds_all[MG_WAVES];
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t w = wave_id(), lane = lane_id();
     MgLds &L = lds_all[w];
     constexpr uint32_t SPAN = 64u * 64u * MG_WPL;
     const uint32_t G = p.G;

@@ -60,7 +60,7 @@ template <bool FILL>
 __global__ __launch_bounds__(RD_WAVES * 64) void rangedeps_kernel(RangeDepsParams p)
 {
     __shared__ RdLds lds_all[RD_WAVES];
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t w = wave_id(), lane = lane_id();
     RdLds &L = lds_all[w];
     const uint64_t lt = lanemask_lt();
     for (uint32_t i = blockIdx.x * RD_WAVES + w; i < p.n; i += gridDim.x * RD_WAVES) {

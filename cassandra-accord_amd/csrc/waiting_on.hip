@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void lv_closure_kernel(uint32_t n, uint32_t nc
 {
     __shared__ __attribute__((aligned(16))) uint8_t rows_all[4][64 * LV_ROW];
     __shared__ uint32_t snode_all[4][64];
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t w = wave_id(), lane = lane_id();
     const uint32_t x = blockIdx.x * 4 + w;
     if (x >= nchunks) return;                       // wave-uniform
     uint8_t *rows = rows_all[w];
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(LV_WAVES * 64) void lv_resolve_kernel(uint32_t n, u
                                                                   unsigned long long *dbg)
 {
     __shared__ LvShared S;
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t w = wave_id(), lane = lane_id();
     if (threadIdx.x == 0) { S.done = 0; S.abort_flag = 0; S.maxlv = 0; }
     __syncthreads();
     uint32_t mymax = 0;
@@ -477,17 +477,9 @@ void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, 
     const char *dbg_path = getenv("ACCORD_LV_DEBUG");
     unsigned long long *dbg = nullptr;
     if (dbg_path && hipMalloc(&dbg, (size_t)nchunks * 5 * 8) != hipSuccess) dbg = nullptr;
-    const char *nw_env = getenv("ACCORD_LV_WAVES");
-    const int nw = nw_env ? atoi(nw_env) : 8;
-    if (nw == 4)
-        hipLaunchKernelGGL(lv_resolve_kernel<4>, dim3(1), dim3(4 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
-                           info, dbg);
-    else if (nw == 12)
-        hipLaunchKernelGGL(lv_resolve_kernel<12>, dim3(1), dim3(12 * 64), 0, s, n, nchunks, rec, pred_off, preds,
-                           level, info, dbg);
-    else
-        hipLaunchKernelGGL(lv_resolve_kernel<8>, dim3(1), dim3(8 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
-                           info, dbg);
+    // 8 waves (2 per SIMD): 4 and 12 measured within noise / slower (profiles/r01_v13)
+    hipLaunchKernelGGL(lv_resolve_kernel<8>, dim3(1), dim3(8 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
+                       info, dbg);
     if (dbg) {
         std::vector<unsigned long long> h((size_t)nchunks * 5);
         if (hipMemcpyAsync(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&

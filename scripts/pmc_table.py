@@ -10,7 +10,7 @@ def kname(s):
 
 
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for d in sys.argv[1:]:
+for d in [a.rstrip("/") for a in sys.argv[1:]]:
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
         agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in agg.items():
