@@ -102,3 +102,29 @@ __device__ __forceinline__ int ts_cmp(uint64_t am, uint64_t al, int32_t an, uint
 // History entry: txn index in the low 29 bits, entry kind in the top 3 bits.
 #define ENT_TXN_MASK 0x1FFFFFFFu
 #define ENT_KIND_SHIFT 29
+
+// Packed per-position class counters of the key-major history (16-bit fields, tile-local):
+// Writes | Reads << 16 | EphemeralReads << 32, completed by one ClassCarry per HISTORY_TILE
+// positions.  They give, for any history range, the number of entries a txn kind witnesses
+// (Ws = #W, RsOrWs = #W + #R, AnyGloballyVisible = len - #ER).
+__host__ __device__ __forceinline__ uint64_t class_bits(uint32_t kind)
+{
+    return kind == 1u ? 1ull : kind == 0u ? (1ull << 16) : kind == 2u ? (1ull << 32) : 0ull;
+}
+
+struct ClassCarry {
+    uint32_t w, r, er, pad;
+};
+
+// entries of [0, x] (global history positions) witnessed by wmask; tile = HISTORY_TILE
+__device__ __forceinline__ uint32_t witnessed_upto(const uint64_t *__restrict__ c_local,
+                                                   const ClassCarry *__restrict__ ccarry, uint32_t x, uint32_t wmask,
+                                                   uint32_t tile = 4096u)
+{
+    const uint64_t c = c_local[x];
+    const ClassCarry cc = ccarry[x / tile];
+    const uint32_t w = (uint32_t)(c & 0xFFFFu) + cc.w;
+    if (wmask == 0x2u) return w;
+    if (wmask == 0x3u) return w + (uint32_t)((c >> 16) & 0xFFFFu) + cc.r;
+    return x + 1 - ((uint32_t)((c >> 32) & 0xFFFFu) + cc.er);
+}

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "device_common.h"
+
 namespace accord {
 
 // device error word codes (first error wins; see include/accord_deps.h)
@@ -64,8 +66,16 @@ size_t history_temp_bytes(uint32_t P);
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
                     uint32_t *seg_end, PairSlice *slice, void *temp, hipStream_t s);
-// history tile size of the Write max-scan carry (pw_local / pw_carry)
+// history tile size of the Write max-scan carry (pw_local / pw_carry) and class-count carries
 constexpr uint32_t HISTORY_TILE = 4096;
+// Views into the history temp buffer launch_history leaves behind: (last Write <= x) + 1 =
+// max(pw_local[x], pw_carry[x / HISTORY_TILE]); witnessed counts via witnessed_upto(c_local, ccarry).
+struct HistoryViews {
+    uint32_t *pw_local, *pw_carry;
+    uint64_t *c_local;
+    ClassCarry *ccarry;
+};
+HistoryViews history_views(void *temp, uint32_t P);
 // per txn: keys, txnIds upper bound and keysToTxnIds sizes from the witnessed counts
 void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *slice, uint32_t *cnt_keys,
                           uint32_t *cnt_vub, uint32_t *cnt_k2v, DevStatus *status, hipStream_t s);
@@ -84,6 +94,14 @@ struct RangeDepsParams {
     // history (for range txns' KeyDeps)
     const uint32_t *hist, *seg_start, *seg_end, *pw_local, *pw_carry;
     uint32_t pw_tile;
+    const uint64_t *c_local;            // witnessed counts (HistoryViews)
+    const ClassCarry *ccarry;
+    uint4 *cp;                          // checkpoints: first history position with txn >= b << RK_CP_SHIFT
+                                        //   {position, its txn, (last Write before it) + 1, 0}
+    uint32_t nkeys, ncp;                //   per key (cp[b * nkeys + k]), ncp blocks
+    uint32_t *cnt_vals_exact;           // exact txnIds count per txn (range txns: written by the union pass)
+    const uint32_t *rk_off;             // per range txn: first of its stored key slices
+    uint2 *rk_slices;                   // (lo, raw | wcnt << 16) per key of every range txn's ranges
     uint32_t n_range_txns;
     const uint32_t *range_txns;
     // RangeDeps counts / outputs
@@ -100,8 +118,17 @@ struct RangeDepsParams {
 };
 void launch_rangedeps_count(const RangeDepsParams &p, hipStream_t s);
 void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s);
+// KeyDeps of range txns: checkpoints (needs the history of the batch), per-txn sizes, the body
+// filled with dep txn indices, then per txn the sorted unique txnIds (into kd_vals at the txnIds
+// upper-bound offsets) and the body rewritten to ranks.
+constexpr uint32_t RK_CP_SHIFT = 12;
+size_t rangekeys_cp_bytes(uint32_t n, uint32_t nkeys);
+void launch_rangekeys_checkpoints(uint32_t P, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s);
+// keys of every range txn's ranges (clipped to the store), for the stored-slice offsets
+void launch_rangekeys_nkeys(const RangeDepsParams &p, uint32_t *cnt, hipStream_t s);
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s);
 void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s);
+void launch_rangekeys_union(const RangeDepsParams &p, hipStream_t s);
 
 // ---- K6 merge (merge.hip) ----
 struct MergeParams {

@@ -120,30 +120,6 @@ constexpr int HS_ITEMS = 16;
 constexpr uint32_t HS_TILE = HS_THREADS * HS_ITEMS;
 static_assert(HS_TILE == HISTORY_TILE, "history tile");
 
-// Packed per-position class counters (16-bit fields, tile-local): Writes | Reads << 16 |
-// EphemeralReads << 32.  With the tile carries they give, for any history range, the number of
-// entries a txn kind witnesses (Ws = #W, RsOrWs = #W + #R, AnyGloballyVisible = len - #ER).
-__device__ __forceinline__ uint64_t class_bits(uint32_t kind)
-{
-    return kind == 1u ? 1ull : kind == 0u ? (1ull << 16) : kind == 2u ? (1ull << 32) : 0ull;
-}
-
-struct ClassCarry {
-    uint32_t w, r, er, pad;
-};
-
-// entries of [0, x] (global positions) witnessed by wmask
-__device__ __forceinline__ uint32_t witnessed_upto(const uint64_t *__restrict__ c_local,
-                                                   const ClassCarry *__restrict__ ccarry, uint32_t x, uint32_t wmask)
-{
-    const uint64_t c = c_local[x];
-    const ClassCarry cc = ccarry[x / HS_TILE];
-    const uint32_t w = (uint32_t)(c & 0xFFFFu) + cc.w;
-    if (wmask == 0x2u) return w;
-    if (wmask == 0x3u) return w + (uint32_t)((c >> 16) & 0xFFFFu) + cc.r;
-    return x + 1 - ((uint32_t)((c >> 32) & 0xFFFFu) + cc.er);
-}
-
 // hist[p] = entry of sorted pair p; segment bounds per key; tile-local inclusive max-scan of
 // (p+1 if entry p is a Write) -> the last Write at or before p, and tile-local inclusive class
 // counts; both completed by tile carries.
@@ -772,6 +748,21 @@ size_t history_temp_bytes(uint32_t P)
     b = (b + 15) & ~(size_t)15;
     b += tiles * sizeof(ClassCarry) + 64;
     return b;
+}
+
+HistoryViews history_views(void *temp, uint32_t P)
+{
+    const uint32_t tiles = (P + HS_TILE - 1) / HS_TILE;
+    HistoryViews v;
+    v.pw_local = (uint32_t *)temp;
+    v.pw_carry = v.pw_local + P;
+    size_t off = ((size_t)P + tiles) * 4;
+    off = (off + 15) & ~(size_t)15;
+    v.c_local = (uint64_t *)((char *)temp + off);
+    off += ((size_t)P + tiles) * 8;
+    off = (off + 15) & ~(size_t)15;
+    v.ccarry = (ClassCarry *)((char *)temp + off);
+    return v;
 }
 
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,

@@ -151,210 +151,389 @@ __global__ __launch_bounds__(RD_WAVES * 64) void rangedeps_kernel(RangeDepsParam
 }
 
 // ---------------------------------------------------------------------------------------------
-// KeyDeps of range txns: one block per range txn.  Every key in its ranges with a non-empty
-// history gets the same [lcw, pos) slice as a key txn (CommandsForKey.mapReduceActive
-// :614-650); the union of the witnessed entries is sorted in LDS (bitonic) and de-duplicated.
+// KeyDeps of range txns.  Every key of the txn's ranges with history before it contributes the
+// same [lcw, pos) slice as a key txn would (CommandsForKey.mapReduceActive :614-650): pos = first
+// entry with txn >= i, lcw = last Write before i-W.  Both are found from per-key checkpoints
+// (first history position at or after each 4096-txn block boundary) by a short gallop, so a query
+// costs a handful of loads instead of two binary searches over the key's whole history.
+//   count : per range txn (one wave), keys with witnessed deps and the body size
+//   fill  : keys, keysToTxnIds header, and the body holding the dep txn indices (key order)
+//   union : per range txn, the body sorted in LDS -> unique txnIds (kd_vals at the upper-bound
+//           offsets, compacted with the key txns' later) and the body rewritten to ranks
 // ---------------------------------------------------------------------------------------------
-constexpr int RK_THREADS = 256;
-constexpr uint32_t RK_SCAP = 2048;     // keys with entries per range txn
-constexpr uint32_t RK_CCAP = 8192;     // witnessed entries per range txn
+constexpr int RK_WAVES = 4;
+constexpr int RK_EMAX = 128;                   // largest union class: 8192 deps per range txn
 
-struct RkLds {
-    uint32_t slot_key[RK_SCAP];
-    uint32_t slot_lo[RK_SCAP];
-    uint32_t slot_base[RK_SCAP + 1];   // exclusive prefix of raw counts
-    uint32_t slot_cnt[RK_SCAP];        // witnessed per slot
-    uint32_t buf[RK_CCAP];             // witnessed txn indices (sorted in place)
-    uint32_t wsum[RK_THREADS / 64];
-    uint32_t nslots, raw_total, nwit, nuniq, overflow;
-};
-
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, uint32_t &total)
+// cp[b * K + k] = {x, txn(x), pw(x), 0}: x = first position of key k's segment [a, c) with
+// txn(x) >= b << RK_CP_SHIFT (c if none; txn then ~0), pw(x) = (last Write at or before x - 1) + 1
+// (global history positions, 0 if none).  Thread per history position: it owns the blocks
+// between its predecessor and itself.
+__device__ __forceinline__ uint32_t rk_pw_before(const RangeDepsParams &p, uint32_t x)
 {
-    const uint32_t tid = threadIdx.x, w = tid >> 6;
-    const uint32_t inc = wave_incl_scan(v);
-    if (lane_id() == 63) wsum[w] = inc;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < RK_THREADS / 64; ++q) { if (q < w) off += wsum[q]; tot += wsum[q]; }
-    total = tot;
-    __syncthreads();
-    return off + inc - v;
+    return x ? max(p.pw_local[x - 1], p.pw_carry[(x - 1) / p.pw_tile]) : 0u;
 }
 
-template <bool FILL>
-__global__ __launch_bounds__(RK_THREADS) void rangekeys_kernel(RangeDepsParams p)
+__global__ __launch_bounds__(256) void rk_checkpoint_kernel(uint32_t P, const uint32_t *__restrict__ sorted_key,
+                                                            RangeDepsParams p)
 {
-    __shared__ RkLds L;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t li = blockIdx.x; li < p.n_range_txns; li += gridDim.x) {
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x) {
+        const uint32_t k = sorted_key[x];
+        const uint32_t a = p.seg_start[k], c = p.seg_end[k];
+        const uint32_t t = p.hist[x] & ENT_TXN_MASK;
+        const uint32_t b_lo = x == a ? 0u : ((p.hist[x - 1] & ENT_TXN_MASK) >> RK_CP_SHIFT) + 1u;
+        const uint32_t b_hi = min(t >> RK_CP_SHIFT, p.ncp - 1u);
+        if (b_lo <= b_hi) {
+            const uint4 v = make_uint4(x, t, rk_pw_before(p, x), 0u);
+            for (uint32_t b = b_lo; b <= b_hi; ++b) p.cp[(size_t)b * p.nkeys + k] = v;
+        }
+        if (x + 1 == c && (t >> RK_CP_SHIFT) + 1u < p.ncp) {
+            const uint4 v = make_uint4(c, 0xFFFFFFFFu, rk_pw_before(p, c), 0u);
+            for (uint32_t b = (t >> RK_CP_SHIFT) + 1u; b < p.ncp; ++b) p.cp[(size_t)b * p.nkeys + k] = v;
+        }
+    }
+}
+
+// first position q in [from, to) with txn(q) >= t, given txn(from - 1) < t: gallop then bisect
+__device__ __forceinline__ uint32_t rk_first_ge(const uint32_t *__restrict__ hist, uint32_t from, uint32_t to,
+                                                uint32_t t)
+{
+    uint32_t lo = from, step = 1;
+    while (lo < to && (hist[lo] & ENT_TXN_MASK) < t) {
+        const uint32_t probe = lo + step;
+        if (probe >= to || (hist[probe] & ENT_TXN_MASK) >= t) {
+            uint32_t l = lo + 1, h = min(probe, to);
+            while (l < h) {
+                const uint32_t m = (l + h) >> 1;
+                if ((hist[m] & ENT_TXN_MASK) < t) l = m + 1; else h = m;
+            }
+            return l;
+        }
+        lo = probe + 1;
+        step <<= 1;
+    }
+    return lo;
+}
+
+struct RkSlice {
+    uint32_t lo, raw, wcnt;
+};
+
+// The deps slices of range txn i on U keys per lane (store-relative kk[u], valid[u]): raw entries
+// [lo, lo + raw), of which wcnt are witnessed by wmask.  The checkpoints at blocks i and i - W
+// usually give both bounds and the Write bound outright (coalesced loads, consecutive keys);
+// only keys with entries between a checkpoint and the bound gallop.  Short slices count their
+// witnessed entries directly (one cache line), long ones through the class counts.
+constexpr uint32_t RK_SHORT = 8;
+template <int U>
+__device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, const uint32_t (&kk)[U],
+                                          const bool (&valid)[U], uint32_t wmask, RkSlice (&out)[U])
+{
+    const bool windowed = i > p.window;
+    const uint32_t thr = windowed ? i - p.window : 0u;
+    const size_t row1 = (size_t)(i >> RK_CP_SHIFT) * p.nkeys, row2 = (size_t)(thr >> RK_CP_SHIFT) * p.nkeys;
+    uint32_t a[U], c[U];
+    uint4 e1[U], e2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        a[u] = c[u] = 0;
+        e1[u] = e2[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (valid[u]) {
+            a[u] = p.seg_start[kk[u]]; c[u] = p.seg_end[kk[u]];
+            e1[u] = p.cp[row1 + kk[u]]; e2[u] = p.cp[row2 + kk[u]];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        out[u] = RkSlice{0u, 0u, 0u};
+        if (!(valid[u] && a[u] < c[u])) continue;
+        const uint32_t pos = e1[u].y >= i ? e1[u].x : rk_first_ge(p.hist, e1[u].x + 1, c[u], i);
+        if (pos == a[u]) continue;
+        uint32_t pw = 0;
+        if (windowed) {
+            if (e2[u].y >= thr || e2[u].x >= pos) {
+                pw = min(e2[u].x, pos) == e2[u].x ? e2[u].z : rk_pw_before(p, pos);
+            } else {
+                pw = rk_pw_before(p, rk_first_ge(p.hist, e2[u].x + 1, pos, thr));
+            }
+        }
+        const uint32_t lo = windowed && pw > a[u] ? pw - 1 : a[u];
+        out[u].lo = lo;
+        out[u].raw = pos - lo;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t raw = out[u].raw;
+        if (raw == 0) continue;
+        uint32_t wc = 0;
+        if (raw <= RK_SHORT) {
+            for (uint32_t r = 0; r < raw; ++r) wc += (wmask >> (p.hist[out[u].lo + r] >> ENT_KIND_SHIFT)) & 1u;
+        } else {
+            const uint32_t lo = out[u].lo, pos = lo + raw;
+            wc = witnessed_upto(p.c_local, p.ccarry, pos - 1, wmask, p.pw_tile) -
+                 (lo ? witnessed_upto(p.c_local, p.ccarry, lo - 1, wmask, p.pw_tile) : 0u);
+        }
+        out[u].wcnt = wc;
+    }
+}
+
+// Stored slice (count pass -> fill pass): lo, and raw | wcnt << 16; RK_SLICE_WIDE marks a slice
+// too long for 16-bit fields (the fill pass recomputes it).
+constexpr uint32_t RK_SLICE_WIDE = 0xFFFFFFFFu;
+
+// Per range txn (one wave): count pass computes and stores every key's slice (keys of its ranges
+// in ascending order, clipped to the store) and the KeyDeps sizes; the fill pass writes keys, the
+// keysToTxnIds header and the body holding the dep txn indices (key order).
+template <bool FILL>
+__global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParams p)
+{
+    constexpr int U = 2;                             // keys per lane per step
+    __shared__ uint32_t rex_all[RK_WAVES][64], rlo_all[RK_WAVES][64];
+    const uint32_t w = wave_id(), lane = lane_id();
+    uint32_t *rex = rex_all[w], *rlo = rlo_all[w];
+    const uint64_t lt = lanemask_lt();
+    for (uint32_t li = blockIdx.x * RK_WAVES + w; li < p.n_range_txns; li += gridDim.x * RK_WAVES) {
         const uint32_t i = p.range_txns[li];
         const uint32_t wmask = witness_mask((uint32_t)(p.lsb[i] >> 1) & 7);
         const uint32_t q0 = p.rng_off[i], q1 = p.rng_off[i + 1];
-        if (tid == 0) { L.nslots = 0; L.raw_total = 0; L.overflow = 0; }
-        __syncthreads();
-        // ---- slots: keys of the ranges (ascending) with entries before i ----
-        uint32_t nslots = 0, raw_base = 0;
+        uint2 *slices = p.rk_slices + p.rk_off[li];
+        uint32_t key_base = 0, k2v_base = 0, kc_total = 0;
+        if (FILL) {
+            key_base = p.kd_key_off[i];
+            kc_total = p.kd_key_off[i + 1] - key_base;
+            k2v_base = p.kd_k2v_off[i];
+        }
+        uint32_t kc = 0, body = 0, kidx = 0;
         for (uint32_t r = q0; r < q1; ++r) {
-            const uint32_t ks = p.rng_start[r] + 1, ke = p.rng_end[r];   // keys (s, e]
-            for (uint32_t c0 = ks; c0 <= ke; c0 += RK_THREADS) {
-                const uint32_t key = c0 + tid;
-                uint32_t raw = 0, lo = 0;
-                if (key <= ke && key >= p.key_lo && key < p.key_hi) {
-                    const uint32_t kk = key - p.key_lo;
-                    const uint32_t a = p.seg_start[kk], b = p.seg_end[kk];
-                    if (a < b && (p.hist[a] & ENT_TXN_MASK) < i) {
-                        uint32_t l = a, h = b;               // pos = first entry with txn >= i
-                        while (l < h) { const uint32_t m = (l + h) >> 1; if ((p.hist[m] & ENT_TXN_MASK) < i) l = m + 1; else h = m; }
-                        const uint32_t pos = l;
-                        lo = a;
-                        if (i > p.window) {
-                            const uint32_t thr = i - p.window;
-                            uint32_t l2 = a, h2 = pos;
-                            while (l2 < h2) { const uint32_t m = (l2 + h2) >> 1; if ((p.hist[m] & ENT_TXN_MASK) < thr) l2 = m + 1; else h2 = m; }
-                            if (l2 > a) {
-                                const uint32_t x = l2 - 1;
-                                const uint32_t pw = max(p.pw_local[x], p.pw_carry[x / p.pw_tile]);
-                                if (pw > a) lo = pw - 1;
-                            }
+            const uint32_t ks = max(p.rng_start[r] + 1, p.key_lo), ke = min(p.rng_end[r], p.key_hi - 1);   // keys (s, e]
+            if (ks > ke) continue;
+            for (uint32_t c0 = ks; c0 <= ke && c0 >= ks; c0 += 64 * U) {
+                RkSlice sl[U];
+                uint32_t kk[U];
+                bool valid[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t key = c0 + 64 * u + lane;
+                    valid[u] = key <= ke && key >= ks;
+                    kk[u] = valid[u] ? key - p.key_lo : 0u;
+                }
+                if (!FILL) {
+                    rk_slices<U>(p, i, kk, valid, wmask, sl);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (valid[u]) {
+                            const bool narrow = sl[u].raw < 65536u;
+                            slices[kidx + (c0 - ks) + 64 * u + lane] =
+                                make_uint2(sl[u].lo, narrow ? sl[u].raw | (sl[u].wcnt << 16) : RK_SLICE_WIDE);
                         }
-                        raw = pos - lo;
+                        kc += (uint32_t)__popcll(__ballot(sl[u].wcnt > 0));
+                        body += wave_sum(sl[u].wcnt);
+                    }
+                    continue;
+                }
+                bool wide = false;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    sl[u] = RkSlice{0u, 0u, 0u};
+                    if (valid[u]) {
+                        const uint2 v = slices[kidx + (c0 - ks) + 64 * u + lane];
+                        if (v.y == RK_SLICE_WIDE) wide = true;
+                        else sl[u] = RkSlice{v.x, v.y & 0xFFFFu, v.y >> 16};
                     }
                 }
-                uint32_t tot;
-                const uint32_t flag = raw > 0 ? 1u : 0u;
-                const uint32_t sidx = nslots + block_excl_scan(flag, L.wsum, tot);
-                const uint32_t nflag = tot;
-                const uint32_t rbase = raw_base + block_excl_scan(raw, L.wsum, tot);
-                if (flag && sidx < RK_SCAP) {
-                    L.slot_key[sidx] = key;
-                    L.slot_lo[sidx] = lo;
-                    L.slot_base[sidx] = rbase;
-                    L.slot_cnt[sidx] = 0;
+                if (__ballot(wide)) {                 // rare: recompute the long slices
+                    RkSlice re[U];
+                    rk_slices<U>(p, i, kk, valid, wmask, re);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (re[u].raw >= 65536u) sl[u] = re[u];
                 }
-                nslots += nflag;
-                raw_base += tot;
-            }
-        }
-        if (nslots > RK_SCAP) {
-            if (!FILL && tid == 0) { rd_overflow(p.status, i); p.cnt_keys[i] = 0; p.cnt_vals_k[i] = 0; p.cnt_k2v[i] = 0; }
-            __syncthreads();
-            continue;
-        }
-        if (tid == 0) L.slot_base[nslots] = raw_base;
-        __syncthreads();
-        // ---- candidates: witnessed entries in key order ----
-        const uint32_t raw_total = raw_base;
-        uint32_t nwit = 0;
-        for (uint32_t c0 = 0; c0 < raw_total; c0 += RK_THREADS) {
-            const uint32_t r = c0 + tid;
-            bool wit = false;
-            uint32_t j = 0, s = 0;
-            if (r < raw_total) {
-                uint32_t l = 0, h = nslots;                  // slot: last base <= r
-                while (h - l > 1) { const uint32_t m = (l + h) >> 1; if (L.slot_base[m] <= r) l = m; else h = m; }
-                s = l;
-                const uint32_t e = p.hist[L.slot_lo[s] + (r - L.slot_base[s])];
-                j = e & ENT_TXN_MASK;
-                wit = (wmask >> (e >> ENT_KIND_SHIFT)) & 1u;
-            }
-            uint32_t tot;
-            const uint32_t pos = nwit + block_excl_scan(wit ? 1u : 0u, L.wsum, tot);
-            if (wit) {
-                atomicAdd(&L.slot_cnt[s], 1u);
-                if (pos < RK_CCAP) L.buf[pos] = j;
-            }
-            nwit += tot;
-        }
-        if (nwit > RK_CCAP) {
-            if (!FILL && tid == 0) { rd_overflow(p.status, i); p.cnt_keys[i] = 0; p.cnt_vals_k[i] = 0; p.cnt_k2v[i] = 0; }
-            __syncthreads();
-            continue;
-        }
-        // ---- sort + unique (bitonic over the next power of two) ----
-        uint32_t np2 = 1;
-        while (np2 < nwit) np2 <<= 1;
-        for (uint32_t x = nwit + tid; x < np2; x += RK_THREADS) L.buf[x] = 0xFFFFFFFFu;
-        __syncthreads();
-        for (uint32_t size = 2; size <= np2; size <<= 1) {
-            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-                for (uint32_t t = tid; t < np2 / 2; t += RK_THREADS) {
-                    const uint32_t x = 2 * t - (t & (stride - 1));
-                    const uint32_t y = x + stride;
-                    const bool up = (x & size) == 0;
-                    const uint32_t a = L.buf[x], b = L.buf[y];
-                    if ((a > b) == up) { L.buf[x] = b; L.buf[y] = a; }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t key = c0 + 64 * u + lane;
+                    const bool has = sl[u].wcnt > 0;
+                    const uint64_t hb = __ballot(has);
+                    const uint32_t raw = has ? sl[u].raw : 0u;   // witnessed-free slices: no candidates
+                    const uint32_t wincl = wave_incl_scan(sl[u].wcnt);
+                    if (has) {
+                        const uint32_t ns = kc + (uint32_t)__popcll(hb & lt);
+                        p.kd_keys[key_base + ns] = key;
+                        p.kd_k2v[k2v_base + ns] = (int32_t)(kc_total + body + wincl);
+                    }
+                    const uint32_t rincl = wave_incl_scan(raw);
+                    const uint32_t rtot = readlane(rincl, 63);
+                    rex[lane] = rincl - raw;
+                    rlo[lane] = sl[u].lo;
+                    wave_lds_sync();
+                    // candidates of these 64 keys in key order; body position = running witnessed count
+                    uint32_t run = body;
+                    for (uint32_t w0 = 0; w0 < rtot; w0 += 64) {
+                        const uint32_t rr = w0 + lane;
+                        bool wit = false;
+                        uint32_t j = 0;
+                        if (rr < rtot) {
+                            uint32_t sidx = 0;       // last slot with rex <= rr (rex[0] = 0)
+#pragma unroll
+                            for (uint32_t step = 32; step >= 1; step >>= 1)
+                                if (sidx + step <= 63 && rex[sidx + step] <= rr) sidx += step;
+                            const uint32_t e = p.hist[rlo[sidx] + (rr - rex[sidx])];
+                            j = e & ENT_TXN_MASK;
+                            wit = (wmask >> (e >> ENT_KIND_SHIFT)) & 1u;
+                        }
+                        const uint64_t wb = __ballot(wit);
+                        if (wit) p.kd_k2v[k2v_base + kc_total + run + (uint32_t)__popcll(wb & lt)] = (int32_t)j;
+                        run += (uint32_t)__popcll(wb);
+                    }
+                    wave_lds_sync();
+                    kc += (uint32_t)__popcll(hb);
+                    body += readlane(wincl, 63);
                 }
-                __syncthreads();
+            }
+            kidx += ke - ks + 1;
+        }
+        if (!FILL && lane == 0) {
+            p.cnt_keys[i] = kc;
+            p.cnt_vals_k[i] = body;        // txnIds upper bound (exact count: the union pass)
+            p.cnt_k2v[i] = kc + body;
+        }
+    }
+}
+
+// keys of every range txn's ranges (clipped to the store): the offsets of its stored slices
+__global__ __launch_bounds__(256) void rk_nkeys_kernel(RangeDepsParams p, uint32_t *__restrict__ cnt)
+{
+    for (uint32_t li = blockIdx.x * blockDim.x + threadIdx.x; li < p.n_range_txns; li += gridDim.x * blockDim.x) {
+        const uint32_t i = p.range_txns[li];
+        uint32_t c = 0;
+        for (uint32_t r = p.rng_off[i]; r < p.rng_off[i + 1]; ++r) {
+            const uint32_t ks = max(p.rng_start[r] + 1, p.key_lo), ke = min(p.rng_end[r], p.key_hi - 1);
+            if (ks <= ke) c += ke - ks + 1;
+        }
+        cnt[li] = c;
+    }
+}
+
+// Bitonic sort of 64*E keys held in registers, blocked layout (element g = lane*E + r): strides
+// >= E exchange between lanes (shuffle), strides < E swap registers of the same lane.
+template <int E> __device__ __forceinline__ void wave_bitonic(uint32_t (&v)[E], uint32_t lane)
+{
+    for (uint32_t k = 2; k <= 64u * E; k <<= 1) {
+        for (uint32_t j = k >> 1; j >= (uint32_t)E; j >>= 1) {          // cross-lane
+            const uint32_t m = j / E;
+            const bool keep_min = ((lane & m) == 0) == (((lane * E) & k) == 0);
+#pragma unroll
+            for (int r = 0; r < E; ++r) {
+                const uint32_t o = (uint32_t)__shfl_xor((int)v[r], (int)m, 64);
+                v[r] = keep_min ? min(v[r], o) : max(v[r], o);
             }
         }
-        // in-place unique
-        uint32_t nuniq = 0;
-        for (uint32_t c0 = 0; c0 < nwit; c0 += RK_THREADS) {
-            const uint32_t x = c0 + tid;
-            const uint32_t v = x < nwit ? L.buf[x] : 0u;
-            const bool f = x < nwit && (x == 0 || L.buf[x - 1] != v);
-            uint32_t tot;
-            const uint32_t u = nuniq + block_excl_scan(f ? 1u : 0u, L.wsum, tot);   // contains barriers
-            if (f) L.buf[u] = v;
-            nuniq += tot;
-            __syncthreads();
+#pragma unroll
+        for (int j = E / 2; j >= 1; j >>= 1) {                          // in-lane
+            if ((uint32_t)j < k) {
+#pragma unroll
+                for (int r = 0; r < E; ++r) {
+                    if ((r & j) == 0) {
+                        const bool asc = ((lane * E + (uint32_t)r) & k) == 0;
+                        const uint32_t a = v[r], b = v[r | j];
+                        const uint32_t lo = min(a, b), hi = max(a, b);
+                        v[r] = asc ? lo : hi;
+                        v[r | j] = asc ? hi : lo;
+                    }
+                }
+            }
         }
-        // non-empty slots
-        uint32_t kc = 0;
-        for (uint32_t c0 = 0; c0 < nslots; c0 += RK_THREADS) {
-            const uint32_t s = c0 + tid;
-            const uint32_t f = (s < nslots && L.slot_cnt[s] > 0) ? 1u : 0u;
-            uint32_t tot;
-            (void)block_excl_scan(f, L.wsum, tot);
-            kc += tot;
+    }
+}
+
+// One range txn's union with E keys per lane (D <= 64*E): sort the body's dep txn indices, write
+// the unique ones (txnIds, ascending = TxnId order) and replace every body entry by its rank.
+template <int E>
+__device__ __forceinline__ void rk_union(const RangeDepsParams &p, uint32_t i, uint32_t D, uint32_t k2v_base, uint32_t *ubuf,
+                                         uint32_t lane)
+{
+    uint32_t v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const uint32_t g = lane * E + (uint32_t)r;
+        v[r] = g < D ? (uint32_t)p.kd_k2v[k2v_base + g] : 0xFFFFFFFFu;
+    }
+    wave_bitonic<E>(v, lane);
+    const uint32_t prev_last = (uint32_t)__shfl_up((int)v[E - 1], 1, 64);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const uint32_t g = lane * E + (uint32_t)r;
+        const uint32_t prev = r ? v[r - 1] : prev_last;
+        cnt += (g < D && (g == 0 || v[r] != prev)) ? 1u : 0u;
+    }
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t U = readlane(incl, 63);
+    const uint32_t vb = p.kd_val_off[i];                  // txnIds upper-bound offsets
+    uint32_t idx = incl - cnt;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const uint32_t g = lane * E + (uint32_t)r;
+        const uint32_t prev = r ? v[r - 1] : prev_last;
+        if (g < D && (g == 0 || v[r] != prev)) {
+            ubuf[idx] = v[r];
+            p.kd_vals[vb + idx] = v[r];
+            ++idx;
         }
-        if (!FILL) {
-            if (tid == 0) { p.cnt_keys[i] = kc; p.cnt_vals_k[i] = nuniq; p.cnt_k2v[i] = kc + nwit; }
-            __syncthreads();
+    }
+    if (lane == 0) p.cnt_vals_exact[i] = U;
+    wave_lds_sync();
+    // ranks: four lower-bound searches per lane in lockstep (one LDS round trip per step)
+    for (uint32_t x0 = 0; x0 < D; x0 += 256) {
+        uint32_t j[4], l[4], h[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t x = x0 + (uint32_t)q * 64 + lane;
+            j[q] = x < D ? (uint32_t)p.kd_k2v[k2v_base + x] : 0u;
+            l[q] = 0;
+            h[q] = U;
+        }
+        for (uint32_t span = U; span > 0; span >>= 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (l[q] < h[q]) {
+                    const uint32_t m = (l[q] + h[q]) >> 1;
+                    if (ubuf[m] < j[q]) l[q] = m + 1; else h[q] = m;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            // a search may need one step more than log2(U) iterations of the halving span
+            while (l[q] < h[q]) {
+                const uint32_t m = (l[q] + h[q]) >> 1;
+                if (ubuf[m] < j[q]) l[q] = m + 1; else h[q] = m;
+            }
+            const uint32_t x = x0 + (uint32_t)q * 64 + lane;
+            if (x < D) p.kd_k2v[k2v_base + x] = (int32_t)l[q];
+        }
+    }
+    wave_lds_sync();
+}
+
+// Union pass: one wave per range txn whose body size D lies in (DLO, 64*E]; one launch per size
+// class, so each runs with the registers and LDS (64*E words per wave) of its own class.
+template <int E, uint32_t DLO>
+__global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_union_kernel(RangeDepsParams p)
+{
+    __shared__ uint32_t buf_all[RK_WAVES][64 * E];
+    const uint32_t w = wave_id(), lane = lane_id();
+    uint32_t *buf = buf_all[w];
+    for (uint32_t li = blockIdx.x * RK_WAVES + w; li < p.n_range_txns; li += gridDim.x * RK_WAVES) {
+        const uint32_t i = p.range_txns[li];
+        const uint32_t key_base = p.kd_key_off[i], kc = p.kd_key_off[i + 1] - key_base;
+        const uint32_t k2v_base = p.kd_k2v_off[i] + kc;
+        const uint32_t D = p.kd_k2v_off[i + 1] - p.kd_k2v_off[i] - kc;
+        if (DLO == 0 && D == 0) { if (lane == 0) p.cnt_vals_exact[i] = 0; continue; }
+        if (D <= DLO) continue;
+        if (D > 64u * E) {
+            if (E == RK_EMAX && lane == 0) rd_overflow(p.status, i);   // beyond the largest class
             continue;
         }
-        const uint32_t key_base = p.kd_key_off[i], val_base = p.kd_val_off[i], k2v_base = p.kd_k2v_off[i];
-        for (uint32_t x = tid; x < nuniq; x += RK_THREADS) p.kd_vals[val_base + x] = L.buf[x];
-        // keys + header: non-empty slots in order, end offset = kc + witnessed through the slot
-        uint32_t ns = 0, wrun = 0;
-        for (uint32_t c0 = 0; c0 < nslots; c0 += RK_THREADS) {
-            const uint32_t s = c0 + tid;
-            const uint32_t cnt = s < nslots ? L.slot_cnt[s] : 0u;
-            uint32_t tot1, tot2;
-            const uint32_t idx = ns + block_excl_scan(cnt > 0 ? 1u : 0u, L.wsum, tot1);
-            const uint32_t wend = wrun + block_excl_scan(cnt, L.wsum, tot2) + cnt;
-            if (cnt > 0) {
-                p.kd_keys[key_base + idx] = L.slot_key[s];
-                p.kd_k2v[k2v_base + idx] = (int32_t)(kc + wend);
-            }
-            ns += tot1;
-            wrun += tot2;
-        }
-        // body: re-walk the candidates in key order; rank = index in the unique sorted txnIds
-        uint32_t wpos = 0;
-        for (uint32_t c0 = 0; c0 < raw_total; c0 += RK_THREADS) {
-            const uint32_t r = c0 + tid;
-            bool wit = false;
-            uint32_t j = 0;
-            if (r < raw_total) {
-                uint32_t l = 0, h = nslots;
-                while (h - l > 1) { const uint32_t m = (l + h) >> 1; if (L.slot_base[m] <= r) l = m; else h = m; }
-                const uint32_t e = p.hist[L.slot_lo[l] + (r - L.slot_base[l])];
-                j = e & ENT_TXN_MASK;
-                wit = (wmask >> (e >> ENT_KIND_SHIFT)) & 1u;
-            }
-            uint32_t tot;
-            const uint32_t pos = wpos + block_excl_scan(wit ? 1u : 0u, L.wsum, tot);
-            if (wit) {
-                uint32_t l = 0, h = nuniq;
-                while (l < h) { const uint32_t m = (l + h) >> 1; if (L.buf[m] < j) l = m + 1; else h = m; }
-                p.kd_k2v[k2v_base + kc + pos] = (int32_t)l;
-            }
-            wpos += tot;
-        }
-        __syncthreads();
+        rk_union<E>(p, i, D, k2v_base, buf, lane);
     }
 }
 
@@ -376,18 +555,55 @@ void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s)
     hipLaunchKernelGGL(rangedeps_kernel<true>, dim3(blocks), dim3(RD_WAVES * 64), 0, s, p);
 }
 
+size_t rangekeys_cp_bytes(uint32_t n, uint32_t nkeys)
+{
+    const size_t ncp = n ? ((size_t)(n - 1) >> RK_CP_SHIFT) + 1 : 1;
+    return ncp * nkeys * sizeof(uint4) + 64;
+}
+
+void launch_rangekeys_checkpoints(uint32_t P, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s)
+{
+    if (p.n_range_txns == 0 || P == 0) return;
+    uint32_t blocks = (P + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(rk_checkpoint_kernel, dim3(blocks), dim3(256), 0, s, P, sorted_key, p);
+}
+
+static uint32_t rk_blocks(uint32_t nrt)
+{
+    uint32_t b = (nrt + RK_WAVES - 1) / RK_WAVES;
+    return b > 4096u ? 4096u : b;
+}
+
+void launch_rangekeys_nkeys(const RangeDepsParams &p, uint32_t *cnt, hipStream_t s)
+{
+    if (p.n_range_txns == 0) return;
+    uint32_t blocks = (p.n_range_txns + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(rk_nkeys_kernel, dim3(blocks), dim3(256), 0, s, p, cnt);
+}
+
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n_range_txns == 0) return;
-    uint32_t blocks = p.n_range_txns < 2048 ? p.n_range_txns : 2048;
-    hipLaunchKernelGGL(rangekeys_kernel<false>, dim3(blocks), dim3(RK_THREADS), 0, s, p);
+    hipLaunchKernelGGL(rangekeys_kernel<false>, dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
 }
 
 void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n_range_txns == 0) return;
-    uint32_t blocks = p.n_range_txns < 2048 ? p.n_range_txns : 2048;
-    hipLaunchKernelGGL(rangekeys_kernel<true>, dim3(blocks), dim3(RK_THREADS), 0, s, p);
+    hipLaunchKernelGGL(rangekeys_kernel<true>, dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
+}
+
+void launch_rangekeys_union(const RangeDepsParams &p, hipStream_t s)
+{
+    if (p.n_range_txns == 0) return;
+    const dim3 g(rk_blocks(p.n_range_txns)), b(RK_WAVES * 64);
+    hipLaunchKernelGGL((rangekeys_union_kernel<4, 0>), g, b, 0, s, p);
+    hipLaunchKernelGGL((rangekeys_union_kernel<16, 256>), g, b, 0, s, p);
+    hipLaunchKernelGGL((rangekeys_union_kernel<32, 1024>), g, b, 0, s, p);
+    hipLaunchKernelGGL((rangekeys_union_kernel<64, 2048>), g, b, 0, s, p);
+    hipLaunchKernelGGL((rangekeys_union_kernel<RK_EMAX, 4096>), g, b, 0, s, p);
 }
 
 } // namespace accord

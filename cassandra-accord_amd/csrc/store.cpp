@@ -2,6 +2,8 @@
 // HIP stream, with a grow-only HBM arena for the batch, the per-key histories and the outputs.
 #include "store_impl.h"
 
+#include <algorithm>
+
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -103,7 +105,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
                       &s->rng_owner, &s->is_range, &s->rt_excl, &s->range_txns, &s->cnt_rngs, &s->cnt_rvals,
                       &s->cnt_r2v, &s->rd_rng_off, &s->rd_val_off, &s->rd_r2v_off, &s->rd_rng_start, &s->rd_rng_end,
-                      &s->rd_vals, &s->rd_r2v, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
+                      &s->rd_vals, &s->rd_r2v, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp};
@@ -145,6 +147,18 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     if (b->txn_index && nrt)
         return fail(s, ACCORD_ERR_ARG, "txn_index (store subset of a stream) is supported for key txns only");
     s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt;
+    s->rk_keys_total = 0;                // sizes the range txns' stored key slices
+    if (nrt && b->rng_off)
+        for (uint32_t i = 0; i < n; ++i)
+            if (b->lsb[i] & 1)
+                for (uint32_t r = b->rng_off[i]; r < b->rng_off[i + 1]; ++r) {
+                    const uint64_t ks = std::max<uint64_t>((uint64_t)b->rng_start[r] + 1, s->cfg.key_lo);
+                    const uint64_t ke = std::min<uint64_t>(b->rng_end[r], (uint64_t)s->cfg.key_hi - 1);
+                    if (ks <= ke) s->rk_keys_total += ke - ks + 1;
+                }
+    if (s->rk_keys_total >= (1ull << 32))
+        return fail(s, ACCORD_ERR_CAPACITY, "range txns cover %llu (txn, key) pairs, over 2^32",
+                    (unsigned long long)s->rk_keys_total);
     s->has_batch = false; s->computed = false; s->merged = false;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
@@ -272,7 +286,23 @@ int32_t accord_deps_compute(accord_store *s)
     rp.rng_end = s->rng_end.as<uint32_t>(); rp.rng_owner = s->rng_owner.as<uint32_t>();
     rp.window = s->cfg.window; rp.key_lo = s->cfg.key_lo; rp.key_hi = s->cfg.key_hi;
     rp.hist = kp.hist; rp.seg_start = s->seg_start.as<uint32_t>(); rp.seg_end = s->seg_end.as<uint32_t>();
-    rp.pw_local = s->hist_tmp.as<uint32_t>(); rp.pw_carry = rp.pw_local + P; rp.pw_tile = accord::HISTORY_TILE;
+    {
+        const accord::HistoryViews hv = accord::history_views(s->hist_tmp.p, P);
+        rp.pw_local = hv.pw_local; rp.pw_carry = hv.pw_carry; rp.pw_tile = accord::HISTORY_TILE;
+        rp.c_local = hv.c_local; rp.ccarry = hv.ccarry;
+    }
+    rp.nkeys = nkeys;
+    rp.ncp = n ? ((n - 1) >> accord::RK_CP_SHIFT) + 1 : 1;
+    rp.cnt_vals_exact = s->cnt_vals.as<uint32_t>();
+    if (nrt) {
+        HIPCHECK(s, s->rk_cp.ensure(accord::rangekeys_cp_bytes(n, nkeys)));
+        HIPCHECK(s, s->rk_cnt.ensure((size_t)nrt * 4 + 4));
+        HIPCHECK(s, s->rk_off.ensure(((size_t)nrt + 1) * 4));
+        HIPCHECK(s, s->rk_slices.ensure(s->rk_keys_total * 8 + 8));
+        rp.cp = s->rk_cp.as<uint4>();
+        rp.rk_off = s->rk_off.as<uint32_t>();
+        rp.rk_slices = s->rk_slices.as<uint2>();
+    }
     rp.n_range_txns = nrt; rp.range_txns = s->range_txns.as<uint32_t>();
     rp.cnt_rngs = s->cnt_rngs.as<uint32_t>(); rp.cnt_vals = s->cnt_rvals.as<uint32_t>(); rp.cnt_r2v = s->cnt_r2v.as<uint32_t>();
     // range txns' KeyDeps: exact txnIds count into the upper-bound array (their bound is exact)
@@ -280,6 +310,12 @@ int32_t accord_deps_compute(accord_store *s)
     rp.status = &dev->status;
 
     // sizes: key txns from the per-pair witnessed counts, range txns by their own count pass
+    if (nrt) {
+        accord::launch_rangekeys_checkpoints(P, s->sort_key.as<uint32_t>(), rp, st);
+        accord::launch_rangekeys_nkeys(rp, s->rk_cnt.as<uint32_t>(), st);
+        accord::exclusive_scan_u32(s->rk_cnt.as<uint32_t>(), s->rk_off.as<uint32_t>(), nrt, &dev->totals[6],
+                                   s->scan_tmp.p, st);
+    }
     accord::launch_keydeps_sizes(n, kp.key_off, kp.slice, rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
                                  rp.cnt_k2v, &dev->status, st);
     if (nrt) accord::launch_rangekeys_count(rp, st);
@@ -343,7 +379,10 @@ int32_t accord_deps_compute(accord_store *s)
     rp.rd_vals = s->rd_vals.as<uint32_t>(); rp.rd_r2v = s->rd_r2v.as<int32_t>();
     accord::launch_keydeps_fill(kp, s->wpl, st);
     record(s, EV_FILL);
-    if (nrt) accord::launch_rangekeys_fill(rp, st);
+    if (nrt) {
+        accord::launch_rangekeys_fill(rp, st);
+        accord::launch_rangekeys_union(rp, st);
+    }
     if (R) accord::launch_rangedeps_fill(rp, st);
     record(s, EV_RANGE);
     accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[7], s->scan_tmp.p, st);

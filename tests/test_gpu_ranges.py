@@ -38,6 +38,7 @@ def test_kats_on_gpu(gpu_device, kat):
     (3000, 8, 2000, 0.99, 0.5, 256, 9, 0.2, 1000),
     (2000, 2, 500, 0.0, 0.5, 0, 10, 0.3, 50),
     (500, 2, 100, 0.0, 0.5, 1000, 11, 0.9, 20),
+    (800, 4, 8000, 0.0, 0.9, 64, 12, 0.3, 3000),       # range txns with 2k-6k deps (largest union classes)
 ])
 def test_mixed_vs_literal(gpu_device, n, k, ks, z, wf, W, seed, rf, rl):
     s = generate_stream(n, k, ks, z, wf, range_frac=rf, range_len_max=rl, seed=seed)
