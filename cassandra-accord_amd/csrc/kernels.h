@@ -51,6 +51,8 @@ struct KeyDepsParams {
     uint32_t *kd_keys, *vgap;          // txnIds land at vgap[vub_off[i] ..], compacted afterwards
     int32_t *kd_k2v;
     DevStatus *status;
+    // fast path / fallback: the txns the fast kernel could not take, processed by the general one
+    uint32_t *fb_list, *fb_count;
 };
 
 // txn-major validation + (key, entry) pair packing; range CSR owners and range-txn flags
@@ -79,7 +81,10 @@ HistoryViews history_views(void *temp, uint32_t P);
 // per txn: keys, txnIds upper bound and keysToTxnIds sizes from the witnessed counts
 void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *slice, uint32_t *cnt_keys,
                           uint32_t *cnt_vub, uint32_t *cnt_k2v, DevStatus *status, hipStream_t s);
-void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, hipStream_t s);
+// fill = fast kernel over every txn (k <= 8, <= 256 candidates, deps in the near span) + the general
+// kernel over the txns it hands back (p.fb_list / p.fb_count, count zeroed before the launch)
+size_t keydeps_fast_temp_bytes(uint32_t n);
+void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, void *recs, hipStream_t s);
 // vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
                          uint32_t *vals, hipStream_t s);

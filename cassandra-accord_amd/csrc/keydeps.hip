@@ -372,10 +372,13 @@ struct TxnMeta {
     uint64_t lsb;
 };
 
-__device__ __forceinline__ TxnMeta load_meta(const KeyDepsParams &p, uint32_t i)
+__device__ __forceinline__ TxnMeta load_meta(const KeyDepsParams &p, uint32_t t, uint32_t limit)
 {
     TxnMeta m{0u, 0u, 0ull};
-    if (i < p.n) { m.k0 = ldg(p.key_off, i); m.k1 = ldg(p.key_off, i + 1); m.lsb = ldg(p.lsb, i); }
+    if (t < limit) {
+        const uint32_t i = p.fb_list ? p.fb_list[t] : t;
+        m.k0 = ldg(p.key_off, i); m.k1 = ldg(p.key_off, i + 1); m.lsb = ldg(p.lsb, i);
+    }
     return m;
 }
 
@@ -464,31 +467,34 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
     constexpr uint32_t SPAN = 64u * 64u * WPL;
     const uint32_t S = gridDim.x * KD_WAVES;
 
-    uint32_t i = blockIdx.x * KD_WAVES + w;
-    TxnMeta m0 = load_meta(p, i), m1 = load_meta(p, i + S), m2 = load_meta(p, i + 2 * S);
+    // positions t of the txns to process: every txn, or (fallback after the fast kernel) a list
+    const uint32_t limit = p.fb_list ? *p.fb_count : p.n;
+    uint32_t t = blockIdx.x * KD_WAVES + w;
+    TxnMeta m0 = load_meta(p, t, limit), m1 = load_meta(p, t + S, limit), m2 = load_meta(p, t + 2 * S, limit);
     uint32_t lo0, pos0, wc0, lo1, pos1, wc1;
-    load_slice(p, m0, i < p.n, lane, lo0, pos0, wc0);
-    load_slice(p, m1, i + S < p.n, lane, lo1, pos1, wc1);
+    load_slice(p, m0, t < limit, lane, lo0, pos0, wc0);
+    load_slice(p, m1, t + S < limit, lane, lo1, pos1, wc1);
     uint32_t incl0, raw_total0;
     int32_t delta0;
     uint32_t e0[KD_CB];
     {
         const uint32_t k = m0.k1 - m0.k0;
-        slot_setup(lo0, pos0, (i < p.n && k <= KD_KCAP) ? k : 0u, lane, incl0, delta0, raw_total0);
+        slot_setup(lo0, pos0, (t < limit && k <= KD_KCAP) ? k : 0u, lane, incl0, delta0, raw_total0);
         load_batch(p, 0, raw_total0, k, incl0, delta0, e0, lane);
     }
 
-    for (; i < p.n; i += S) {
+    for (; t < limit; t += S) {
+        const uint32_t i = p.fb_list ? p.fb_list[t] : t;
         // ---- prefetch ----
-        const TxnMeta m3 = load_meta(p, i + 3 * S);
+        const TxnMeta m3 = load_meta(p, t + 3 * S, limit);
         uint32_t lo2, pos2, wc2;
-        load_slice(p, m2, i + 2 * S < p.n, lane, lo2, pos2, wc2);
+        load_slice(p, m2, t + 2 * S < limit, lane, lo2, pos2, wc2);
         uint32_t incl1, raw_total1;
         int32_t delta1;
         uint32_t e1[KD_CB];
         {
             const uint32_t kn = m1.k1 - m1.k0;
-            slot_setup(lo1, pos1, (i + S < p.n && kn <= KD_KCAP) ? kn : 0u, lane, incl1, delta1, raw_total1);
+            slot_setup(lo1, pos1, (t + S < limit && kn <= KD_KCAP) ? kn : 0u, lane, incl1, delta1, raw_total1);
             load_batch(p, 0, raw_total1, kn, incl1, delta1, e1, lane);
         }
 
@@ -656,6 +662,253 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fast fill: the common txn of a key batch -- k <= 8 keys, <= 256 raw candidates, <= 64 deps older
+// than the near span -- with nothing else on its path: a 32-byte per-txn record (one load), the pair
+// slices, one batch of candidates located by a compare/select chain, LDS bitmap union, ranks.
+// Anything else (more keys or candidates, more far deps) is appended to a list the
+// general keydeps_kernel processes afterwards; its outputs are identical, so a txn abandoned
+// half-way (after its keys were written) is simply redone.
+// ---------------------------------------------------------------------------------------------
+struct alignas(32) TxnRec {
+    uint32_t k0, k, kind, gi, key_base, val_base, k2v_base, pad;
+};
+
+__global__ __launch_bounds__(256) void txnrec_kernel(KeyDepsParams p, TxnRec *__restrict__ out)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x) {
+        TxnRec r;
+        r.k0 = p.key_off[i];
+        r.k = p.key_off[i + 1] - r.k0;
+        r.kind = (uint32_t)(p.lsb[i] >> 1) & 7;
+        r.gi = p.txn_index ? p.txn_index[i] : i;
+        r.key_base = p.kd_key_off[i];
+        r.val_base = p.vub_off[i];
+        r.k2v_base = p.kd_k2v_off[i];
+        r.pad = 0;
+        out[i] = r;
+    }
+}
+
+constexpr uint32_t FK_RAW = 64u * KD_CB;     // raw candidates the fast path takes
+
+// inclusive scan over lanes 0..7 (row 0 of the wave; lanes >= 8 get partial sums)
+__device__ __forceinline__ uint32_t scan8(uint32_t v)
+{
+    v += dpp_row_shr<1>(v);
+    v += dpp_row_shr<2>(v);
+    v += dpp_row_shr<4>(v);
+    return v;
+}
+
+struct FkTxn {
+    uint32_t rec;                     // lane f < 8: TxnRec field f
+    uint32_t lo, pos, wc, key;        // lane q < k: its pair slice and key ordinal
+};
+
+__device__ __forceinline__ uint32_t fk_rec(const TxnRec *__restrict__ recs, uint32_t t, uint32_t n, uint32_t lane)
+{
+    return (t < n && lane < 8) ? ldg((const uint32_t *)recs, t * 8u + lane) : 0u;
+}
+
+__device__ __forceinline__ void fk_slices(const KeyDepsParams &p, FkTxn &x, uint32_t lane)
+{
+    const uint32_t k0 = readlane(x.rec, 0), k = readlane(x.rec, 1);
+    x.lo = x.pos = x.wc = x.key = 0;
+    if (k <= 8 && lane < k) {
+        const PairSlice ps = ldg(p.slice, k0 + lane);
+        x.lo = ps.lo; x.pos = ps.pos; x.wc = ps.wcnt;
+        x.key = ldg(p.key_ord, k0 + lane);
+    }
+}
+
+// slot plan (end = inclusive raw prefix, delta = slice start - exclusive prefix) and the raw
+// candidates of a txn with k <= 8 and <= FK_RAW of them (else e[] stays empty)
+__device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn &x, uint32_t lane,
+                                             uint32_t (&e)[KD_CB])
+{
+    const uint32_t k = readlane(x.rec, 1);
+    const uint32_t raw = (k <= 8 && lane < k) ? x.pos - x.lo : 0u;
+    const uint32_t incl = scan8(raw);
+    const int32_t delta = (int32_t)x.lo - (int32_t)(incl - raw);
+    const uint32_t rt = readlane(incl, 7);
+    uint32_t eq[7];
+    int32_t dq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dq[q] = (int32_t)readlane((uint32_t)delta, q);
+#pragma unroll
+    for (int q = 0; q < 7; ++q) eq[q] = q + 1 < (int)k ? readlane(incl, q) : 0xFFFFFFFFu;
+    const bool take = k <= 8 && rt <= FK_RAW;
+#pragma unroll
+    for (int c = 0; c < KD_CB; ++c) {
+        e[c] = KD_NONE;
+        const uint32_t r = c * 64 + lane;
+        int32_t d = dq[0];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) d = r >= eq[q] ? dq[q + 1] : d;
+        if (take && r < rt) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
+    }
+    return rt;
+}
+
+template <int WPL>
+__global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void keydeps_fast_kernel(
+    KeyDepsParams p, const TxnRec *__restrict__ recs)
+{
+    __shared__ unsigned long long bm_all[KD_WAVES][64 * WPL];
+    __shared__ uint32_t wp_all[KD_WAVES][64 * WPL];
+    __shared__ uint32_t fr_all[KD_WAVES][64];       // far deps: value, then its rank
+    const uint32_t w = wave_id(), lane = lane_id();
+    unsigned long long *bm = bm_all[w];
+    uint32_t *wp = wp_all[w], *fr = fr_all[w];
+    const uint64_t lt = lanemask_lt();
+    constexpr uint32_t SPAN = 64u * 64u * WPL;
+    const uint32_t S = gridDim.x * KD_WAVES, n = p.n;
+
+    // software pipeline: records three txns ahead, slices two ahead, candidates one ahead
+    uint32_t t = blockIdx.x * KD_WAVES + w;
+    FkTxn a, b, c;
+    a.rec = fk_rec(recs, t, n, lane);
+    b.rec = fk_rec(recs, t + S, n, lane);
+    c.rec = fk_rec(recs, t + 2 * S, n, lane);
+    fk_slices(p, a, lane);
+    fk_slices(p, b, lane);
+    uint32_t ea[KD_CB];
+    uint32_t rta = fk_cands(p, a, lane, ea);
+
+    for (; t < n; t += S) {
+        FkTxn d;
+        d.rec = fk_rec(recs, t + 3 * S, n, lane);
+        fk_slices(p, c, lane);
+        uint32_t eb[KD_CB];
+        const uint32_t rtb = fk_cands(p, b, lane, eb);
+
+        do {   // ---- txn t (break = done with it) ----
+            const uint32_t k = readlane(a.rec, 1);
+            if (k == 0) {                             // range txn / no key in this store
+                if (lane == 0) stg(p.cnt_vals, t, 0u);
+                break;
+            }
+            bool fallback = k > 8 || rta > FK_RAW;
+            const uint32_t kind = readlane(a.rec, 2), gi = readlane(a.rec, 3);
+            const uint32_t wmask = witness_mask(kind);
+            const uint32_t nb = SPAN - gi;            // near bit of txn j: j + nb (< SPAN iff near)
+            uint32_t F = 0;                           // far deps (older than the near span)
+            uint32_t fidx[KD_CB];
+            if (!fallback) {
+#pragma unroll
+                for (int q = 0; q < WPL; ++q) bm[lane * WPL + q] = 0ull;
+                wave_lds_sync();
+#pragma unroll
+                for (int cc = 0; cc < KD_CB; ++cc) {
+                    fidx[cc] = 0;
+                    if ((uint32_t)cc * 64 >= rta) break;   // wave-uniform
+                    const uint32_t ev = ea[cc];
+                    const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
+                    const uint32_t j = ev & ENT_TXN_MASK;
+                    const uint32_t bit = j + nb;
+                    const bool nr = wit && bit < SPAN;
+                    if (nr) atomicOr(&bm[bit >> 6], 1ull << (bit & 63));
+                    const uint64_t fb = __ballot(wit && !nr);
+                    if (fb) {                             // wave-uniform
+                        const uint32_t f = F + (uint32_t)__popcll(fb & lt);
+                        if (wit && !nr && f < 64) fr[f] = j;
+                        fidx[cc] = f;
+                        F += (uint32_t)__popcll(fb);
+                    }
+                }
+                fallback = F > 64;
+            }
+            if (fallback) {
+                if (lane == 0) p.fb_list[atomicAdd(p.fb_count, 1u)] = t;
+                break;
+            }
+            wave_lds_sync();
+            // far deps: de-duplicated ranks (all of them precede the near span in TxnId order)
+            uint32_t far_u = 0;
+            if (F) {                                      // wave-uniform
+                const uint32_t x = lane < F ? fr[lane] : 0xFFFFFFFFu;
+                bool own = lane < F;
+                for (uint32_t g = 0; g < F; ++g)
+                    own = own && !(g < lane && readlane(x, (int)g) == x);
+                const uint64_t om = __ballot(own);
+                far_u = (uint32_t)__popcll(om);
+                uint32_t rk = 0;
+                for (uint64_t m = om; m; m &= m - 1)
+                    rk += readlane(x, (int)__builtin_ctzll(m)) < x ? 1u : 0u;
+                wave_lds_sync();
+                if (lane < F) fr[lane] = rk;
+                if (own) stg(p.vgap, readlane(a.rec, 5) + rk, x);
+            }
+            // union: popcounts -> per-word rank prefix (after the far deps); |txnIds|
+            uint32_t pc[WPL], mysum = 0;
+#pragma unroll
+            for (int q = 0; q < WPL; ++q) { pc[q] = (uint32_t)__popcll(bm[lane * WPL + q]); mysum += pc[q]; }
+            const uint32_t incl = wave_incl_scan(mysum);
+            {
+                uint32_t ex = incl - mysum + far_u;
+#pragma unroll
+                for (int q = 0; q < WPL; ++q) { wp[lane * WPL + q] = ex; ex += pc[q]; }
+            }
+            if (lane == 0) stg(p.cnt_vals, t, readlane(incl, 63) + far_u);
+            // keys and keysToTxnIds header from the witnessed counts
+            const uint32_t key_base = readlane(a.rec, 4), val_base = readlane(a.rec, 5), k2v_base = readlane(a.rec, 6);
+            const bool ne = lane < k && a.wc != 0;
+            const uint64_t hb = __ballot(ne);
+            const uint32_t kc = (uint32_t)__popcll(hb);
+            const uint32_t wincl = scan8(lane < k ? a.wc : 0u);
+            if (ne) {
+                const uint32_t ns = (uint32_t)__popcll(hb & lt);
+                stg(p.kd_keys, key_base + ns, a.key);
+                stg(p.kd_k2v, k2v_base + ns, (int32_t)(kc + wincl));
+            }
+            wave_lds_sync();
+            // body: rank of every witnessed entry; txnIds at their ranks
+            uint32_t run = 0;
+#pragma unroll
+            for (int cc = 0; cc < KD_CB; ++cc) {
+                if ((uint32_t)cc * 64 >= rta) break;
+                const uint32_t ev = ea[cc];
+                const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
+                const uint32_t j = ev & ENT_TXN_MASK;
+                const bool nr = wit && j + nb < SPAN;
+                const uint32_t bit = nr ? j + nb : 0u;
+                uint32_t rank = wp[bit >> 6] + (uint32_t)__popcll(bm[bit >> 6] & ((1ull << (bit & 63)) - 1ull));
+                if (F && wit && !nr) rank = fr[fidx[cc]];
+                const uint64_t wb = __ballot(wit);
+                if (wit) {
+                    stg(p.kd_k2v, k2v_base + kc + run + (uint32_t)__popcll(wb & lt), (int32_t)rank);
+                    if (nr) stg(p.vgap, val_base + rank, j);  // every holder of j writes the same word
+                }
+                run += (uint32_t)__popcll(wb);
+            }
+        } while (0);
+
+        // rotate the pipeline (after the txn: a register copy waits for the loads it copies)
+        a = b; b = c; c = d;
+        rta = rtb;
+#pragma unroll
+        for (int cc = 0; cc < KD_CB; ++cc) ea[cc] = eb[cc];
+    }
+}
+
+void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_t s)
+{
+    if (p.n == 0) return;
+    uint32_t rb = (p.n + 255) / 256;
+    if (rb > 4096) rb = 4096;
+    hipLaunchKernelGGL(txnrec_kernel, dim3(rb), dim3(256), 0, s, p, (TxnRec *)recs);
+    uint32_t blocks = (p.n + KD_WAVES - 1) / KD_WAVES;
+    if (blocks > 256u * 16u) blocks = 256u * 16u;
+    switch (wpl) {
+    case 1: hipLaunchKernelGGL((keydeps_fast_kernel<1>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs); break;
+    case 2: hipLaunchKernelGGL((keydeps_fast_kernel<2>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs); break;
+    default: hipLaunchKernelGGL((keydeps_fast_kernel<4>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs); break;
+    }
+}
+
+size_t fk_temp_bytes(uint32_t n) { return (size_t)n * sizeof(TxnRec) + 64; }
+
 void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
 {
     if (p.n == 0) return;
@@ -799,7 +1052,22 @@ void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *
                        cnt_k2v, status);
 }
 
-void launch_keydeps_fill(const KeyDepsParams &p, int wpl, hipStream_t s) { launch_keydeps(p, wpl, s); }
+size_t keydeps_fast_temp_bytes(uint32_t n) { return fk_temp_bytes(n); }
+
+void launch_keydeps_fill(const KeyDepsParams &p, int wpl, void *recs, hipStream_t s)
+{
+    // fast path over every txn; the general kernel over the fallback list (fb_count zeroed by the
+    // caller).  Windows past 512 txns put most txns over the fast path's 256 candidates: general only.
+    if (p.window > 512u) {
+        KeyDepsParams q = p;
+        q.fb_list = nullptr;
+        q.fb_count = nullptr;
+        launch_keydeps(q, wpl, s);
+        return;
+    }
+    launch_keydeps_fast(p, wpl, recs, s);
+    launch_keydeps(p, wpl, s);
+}
 
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
                          uint32_t *vals, hipStream_t s)

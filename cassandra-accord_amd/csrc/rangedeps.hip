@@ -71,6 +71,19 @@ __global__ __launch_bounds__(RD_WAVES * 64) void rangedeps_kernel(RangeDepsParam
         const uint32_t q1 = key_query ? p.key_off[i + 1] : p.rng_off[i + 1];
         const uint32_t r_lo = p.rng_off[i > p.window ? i - p.window : 0], r_hi = p.rng_off[i];
         uint32_t H = 0;
+        // up to 8 query keys / ranges: held wave-uniform, every candidate tested by compares
+        const uint32_t nq = q1 - q0;
+        const bool few = nq <= 8;
+        uint32_t qa[8], qb[8];                           // key: (key, key); range: (start, end)
+        {
+            uint32_t va = 0, vb = 0;
+            if (few && lane < nq) {
+                va = key_query ? p.key_ord[q0 + lane] : p.rng_start[q0 + lane];
+                vb = key_query ? va : p.rng_end[q0 + lane];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { qa[q] = readlane(va, q); qb[q] = readlane(vb, q); }
+        }
         if (q1 > q0) {
             for (uint32_t r0 = r_lo; r0 < r_hi; r0 += 64) {
                 const uint32_t r = r0 + lane;
@@ -80,7 +93,16 @@ __global__ __launch_bounds__(RD_WAVES * 64) void rangedeps_kernel(RangeDepsParam
                     j = p.rng_owner[r];
                     s = p.rng_start[r];
                     e = p.rng_end[r];
-                    hit = ((wmask >> ((uint32_t)(p.lsb[j] >> 1) & 7)) & 1u) && rd_hits(p, s, e, key_query, q0, q1);
+                    bool inter = false;
+                    if (few) {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q)
+                            inter = inter || ((uint32_t)q < nq && (key_query ? (qa[q] > s && qa[q] <= e)
+                                                                             : (s < qb[q] && qa[q] < e)));
+                    } else {
+                        inter = rd_hits(p, s, e, key_query, q0, q1);
+                    }
+                    hit = inter && ((wmask >> ((uint32_t)(p.lsb[j] >> 1) & 7)) & 1u);
                 }
                 const uint64_t bal = __ballot(hit);
                 const uint32_t h = H + (uint32_t)__popcll(bal & lt);

@@ -99,7 +99,7 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipSetDevice(s->cfg.device);
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
-                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap,
+                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list,
                       &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
@@ -377,7 +377,12 @@ int32_t accord_deps_compute(accord_store *s)
     rp.rd_r2v_off = s->rd_r2v_off.as<uint32_t>();
     rp.rd_rng_start = s->rd_rng_start.as<uint32_t>(); rp.rd_rng_end = s->rd_rng_end.as<uint32_t>();
     rp.rd_vals = s->rd_vals.as<uint32_t>(); rp.rd_r2v = s->rd_r2v.as<int32_t>();
-    accord::launch_keydeps_fill(kp, s->wpl, st);
+    HIPCHECK(s, s->fk_recs.ensure(accord::keydeps_fast_temp_bytes(n)));
+    HIPCHECK(s, s->fk_list.ensure((size_t)n * 4 + 64));
+    kp.fb_count = s->fk_list.as<uint32_t>();
+    kp.fb_list = kp.fb_count + 16;
+    HIPCHECK(s, hipMemsetAsync(kp.fb_count, 0, 4, st));
+    accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {
         accord::launch_rangekeys_fill(rp, st);

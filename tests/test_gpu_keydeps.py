@@ -30,6 +30,8 @@ def check(s, window, keyspace, literal=False):
     (4000, 8, 5000, 0.99, 0.5, 256, 7),
     (5000, 1, 3, 0.0, 0.0, 32, 8),      # all reads: deps empty
     (5000, 1, 3, 0.0, 1.0, 32, 9),      # all writes: long chains
+    (3000, 12, 500, 0.99, 0.5, 64, 10),  # more than 8 keys per txn (general kernel)
+    (1500, 40, 2000, 0.0, 0.5, 128, 14),
 ])
 def test_small_vs_literal(gpu_device, n, k, ks, z, wf, W, seed):
     s = generate_stream(n, k, ks, z, wf, seed=seed)
