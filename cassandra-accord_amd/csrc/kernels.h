@@ -86,8 +86,9 @@ void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *
 size_t keydeps_fast_temp_bytes(uint32_t n);
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, void *recs, hipStream_t s);
 // vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
+size_t compact_temp_bytes(uint64_t max_total);
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
-                         uint32_t *vals, hipStream_t s);
+                         uint32_t *vals, uint64_t max_total, void *temp, hipStream_t s);
 
 // ---- range txns (rangedeps.hip) ----
 struct RangeDepsParams {
@@ -105,6 +106,7 @@ struct RangeDepsParams {
                                         //   {position, its txn, (last Write before it) + 1, 0}
     uint32_t nkeys, ncp;                //   per key (cp[b * nkeys + k]), ncp blocks
     uint32_t *cnt_vals_exact;           // exact txnIds count per txn (range txns: written by the union pass)
+    uint32_t *rd_big_list, *rd_big_count;   // txns with more range hits than the main pass holds
     const uint32_t *rk_off;             // per range txn: first of its stored key slices
     uint2 *rk_slices;                   // (lo, raw | wcnt << 16) per key of every range txn's ranges
     uint32_t n_range_txns;

@@ -923,39 +923,62 @@ void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
     }
 }
 
-// txnIds: gapped (upper-bound offsets) -> dense CSR.  A wave moves 16 consecutive txns at a time:
-// lanes 0..15 fetch their offsets, then every lane issues one load per txn (16 in flight) before
-// the stores, so the copy runs at streaming rate instead of one round trip per txn.
-constexpr int CV_TXNS = 16;
+// txnIds: gapped (upper-bound offsets) -> dense CSR, flat over the output: a block owns CV_OUT
+// consecutive outputs, takes its first txn from bstart (cv_bstart_kernel), stages windows of
+// CV_WIN txns' offsets in LDS and maps every output to its txn by an LDS search -- coalesced stores,
+// mostly coalesced loads, and no idle lanes whatever the mix of small and large txnIds lists.
+constexpr uint32_t CV_OUT = 4096, CV_WIN = 256;
+constexpr int CV_ILP = 4;
+// bstart[b] = the last txn t with val_off[t] <= b * CV_OUT (thread per txn; the blocks whose first
+// output lies in [val_off[t], val_off[t+1]) are t's)
+__global__ __launch_bounds__(256) void cv_bstart_kernel(uint32_t n, const uint32_t *__restrict__ val_off,
+                                                        uint32_t *__restrict__ bstart)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const uint32_t a = val_off[t], e = val_off[t + 1];
+        for (uint32_t b = (a + CV_OUT - 1) / CV_OUT; b * CV_OUT < e; ++b) bstart[b] = t;
+    }
+}
+
 __global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uint32_t *__restrict__ vub_off,
                                                            const uint32_t *__restrict__ val_off,
                                                            const uint32_t *__restrict__ vgap,
+                                                           const uint32_t *__restrict__ bstart,
                                                            uint32_t *__restrict__ vals)
 {
-    const uint32_t lane = lane_id();
-    const uint32_t waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t g = blockIdx.x * (blockDim.x / 64) + wave_id(); g * CV_TXNS < n; g += waves) {
-        const uint32_t t = g * CV_TXNS + (lane & (CV_TXNS - 1));
-        uint32_t src = 0, dst = 0, u = 0;
-        if (lane < CV_TXNS && t < n) { src = vub_off[t]; dst = val_off[t]; u = val_off[t + 1] - dst; }
-        uint32_t umax = u;
+    __shared__ uint32_t s_off[CV_WIN + 1], s_src[CV_WIN];
+    const uint32_t total = val_off[n];
+    const uint32_t o0 = blockIdx.x * CV_OUT;
+    if (o0 >= total) return;                          // block-uniform
+    const uint32_t o1 = min(total, o0 + CV_OUT);
+    uint32_t t0 = bstart[blockIdx.x], o = o0;         // last txn with val_off <= o0
+    while (o < o1) {                                  // block-uniform
+        const uint32_t tw = t0 + threadIdx.x;
+        s_off[threadIdx.x] = tw <= n ? val_off[tw] : 0xFFFFFFFFu;
+        s_src[threadIdx.x] = tw < n ? vub_off[tw] : 0u;
+        if (threadIdx.x == 0) s_off[CV_WIN] = t0 + CV_WIN <= n ? val_off[t0 + CV_WIN] : 0xFFFFFFFFu;
+        __syncthreads();
+        const uint32_t oe = min(o1, s_off[CV_WIN]);   // outputs of this window's txns
+        for (uint32_t x0 = o + threadIdx.x; x0 < oe; x0 += 256 * CV_ILP) {
+            uint32_t v[CV_ILP];                       // CV_ILP independent gathers in flight per lane
 #pragma unroll
-        for (int d = 1; d < CV_TXNS; d <<= 1) umax = max(umax, (uint32_t)__shfl_xor(umax, d, 64));
-        umax = __shfl(umax, 0, 64);
-        for (uint32_t x0 = 0; x0 < umax; x0 += 64) {
-            const uint32_t x = x0 + lane;
-            uint32_t v[CV_TXNS];
+            for (int j = 0; j < CV_ILP; ++j) {
+                const uint32_t x = x0 + j * 256;
+                uint32_t l = 0, h = CV_WIN;           // last slot with s_off <= x
 #pragma unroll
-            for (int j = 0; j < CV_TXNS; ++j) {
-                const uint32_t uj = __shfl(u, j, 64), sj = __shfl(src, j, 64);
-                v[j] = x < uj ? vgap[sj + x] : 0u;
+                for (int it = 0; it < 8; ++it) {
+                    const uint32_t m = (l + h) >> 1;
+                    if (h - l > 1) { if (s_off[m] <= x) l = m; else h = m; }
+                }
+                v[j] = x < oe ? vgap[s_src[l] + (x - s_off[l])] : 0u;
             }
 #pragma unroll
-            for (int j = 0; j < CV_TXNS; ++j) {
-                const uint32_t uj = __shfl(u, j, 64), dj = __shfl(dst, j, 64);
-                if (x < uj) vals[dj + x] = v[j];
-            }
+            for (int j = 0; j < CV_ILP; ++j)
+                if (x0 + j * 256 < oe) vals[x0 + j * 256] = v[j];
         }
+        __syncthreads();
+        o = oe;
+        t0 += CV_WIN;
     }
 }
 
@@ -1069,13 +1092,19 @@ void launch_keydeps_fill(const KeyDepsParams &p, int wpl, void *recs, hipStream_
     launch_keydeps(p, wpl, s);
 }
 
+size_t compact_temp_bytes(uint64_t max_total) { return ((max_total + CV_OUT - 1) / CV_OUT + 1) * 4 + 64; }
+
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
-                         uint32_t *vals, hipStream_t s)
+                         uint32_t *vals, uint64_t max_total, void *temp, hipStream_t s)
 {
-    if (n == 0) return;
-    uint32_t blocks = (n + 4 * CV_TXNS - 1) / (4 * CV_TXNS);
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(compact_vals_kernel, dim3(blocks), dim3(256), 0, s, n, vub_off, val_off, vgap, vals);
+    if (n == 0 || max_total == 0) return;
+    const uint64_t blocks = (max_total + CV_OUT - 1) / CV_OUT;   // blocks past the exact total exit
+    uint32_t *bstart = (uint32_t *)temp;
+    uint32_t sb = (n + 255) / 256;
+    if (sb > 4096) sb = 4096;
+    hipLaunchKernelGGL(cv_bstart_kernel, dim3(sb), dim3(256), 0, s, n, val_off, bstart);
+    hipLaunchKernelGGL(compact_vals_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, n, vub_off, val_off, vgap, bstart,
+                       vals);
 }
 
 } // namespace accord

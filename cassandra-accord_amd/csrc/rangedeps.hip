@@ -20,7 +20,8 @@ namespace accord {
 namespace {
 
 constexpr int RD_WAVES = 4;
-constexpr uint32_t RD_HCAP = 512;
+constexpr uint32_t RD_HCAP = 256;            // hits per txn in the main pass (5 KiB of LDS per wave)
+constexpr uint32_t RD_HCAP_BIG = 2048;       // txns with more hits: a one-wave-per-block pass over a list
 
 __device__ __forceinline__ void rd_overflow(DevStatus *st, uint32_t i)
 {
@@ -28,11 +29,11 @@ __device__ __forceinline__ void rd_overflow(DevStatus *st, uint32_t i)
     atomicMin(&st->overflow_first, i);
 }
 
-struct RdLds {
-    unsigned long long code[RD_HCAP];   // start << 32 | end
-    uint32_t j[RD_HCAP];
-    uint32_t jrank[RD_HCAP];
-    uint32_t first[RD_HCAP];            // first hit (lowest txn) of its range
+template <uint32_t HCAP> struct RdLds {
+    unsigned long long code[HCAP];      // start << 32 | end
+    uint32_t j[HCAP];
+    uint32_t jrank[HCAP];
+    uint32_t first[HCAP];               // first hit (lowest txn) of its range
 };
 
 // Does (s, e] intersect the query of txn i?  Key query: some key k with s < k <= e.  Range query:
@@ -56,14 +57,19 @@ __device__ __forceinline__ bool rd_hits(const RangeDepsParams &p, uint32_t s, ui
     return lo < q1 && p.rng_start[lo] < e;
 }
 
-template <bool FILL>
-__global__ __launch_bounds__(RD_WAVES * 64) void rangedeps_kernel(RangeDepsParams p)
+// Main pass (LIST = false): every txn, hits up to HCAP; a txn with more is appended to a list in
+// the count pass and skipped (by both passes).  Big pass (LIST = true): the listed txns with
+// RD_HCAP_BIG hits of LDS; more than that is reported as overflow.
+template <bool FILL, uint32_t HCAP, int WAVES, bool LIST>
+__global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p)
 {
-    __shared__ RdLds lds_all[RD_WAVES];
+    __shared__ RdLds<HCAP> lds_all[WAVES];
     const uint32_t w = wave_id(), lane = lane_id();
-    RdLds &L = lds_all[w];
+    RdLds<HCAP> &L = lds_all[w];
     const uint64_t lt = lanemask_lt();
-    for (uint32_t i = blockIdx.x * RD_WAVES + w; i < p.n; i += gridDim.x * RD_WAVES) {
+    const uint32_t limit = LIST ? *p.rd_big_count : p.n;
+    for (uint32_t it = blockIdx.x * WAVES + w; it < limit; it += gridDim.x * WAVES) {
+        const uint32_t i = LIST ? p.rd_big_list[it] : it;
         const uint64_t lsb_i = p.lsb[i];
         const uint32_t wmask = witness_mask((uint32_t)(lsb_i >> 1) & 7);
         const bool key_query = (lsb_i & 1) == 0;
@@ -106,17 +112,21 @@ __global__ __launch_bounds__(RD_WAVES * 64) void rangedeps_kernel(RangeDepsParam
                 }
                 const uint64_t bal = __ballot(hit);
                 const uint32_t h = H + (uint32_t)__popcll(bal & lt);
-                if (hit && h < RD_HCAP) {
+                if (hit && h < HCAP) {
                     L.code[h] = ((unsigned long long)s << 32) | e;
                     L.j[h] = j;
                 }
                 H += (uint32_t)__popcll(bal);
             }
         }
-        if (H > RD_HCAP) {
+        if (H > HCAP) {
             if (!FILL && lane == 0) {
-                rd_overflow(p.status, i);
-                p.cnt_rngs[i] = 0; p.cnt_vals[i] = 0; p.cnt_r2v[i] = 0;
+                if (LIST) {
+                    rd_overflow(p.status, i);
+                    p.cnt_rngs[i] = 0; p.cnt_vals[i] = 0; p.cnt_r2v[i] = 0;
+                } else {
+                    p.rd_big_list[atomicAdd(p.rd_big_count, 1u)] = i;
+                }
             }
             continue;
         }
@@ -566,7 +576,8 @@ void launch_rangedeps_count(const RangeDepsParams &p, hipStream_t s)
     if (p.n == 0) return;
     uint32_t blocks = (p.n + RD_WAVES - 1) / RD_WAVES;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(rangedeps_kernel<false>, dim3(blocks), dim3(RD_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangedeps_kernel<false, RD_HCAP, RD_WAVES, false>), dim3(blocks), dim3(RD_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangedeps_kernel<false, RD_HCAP_BIG, 1, true>), dim3(256), dim3(64), 0, s, p);
 }
 
 void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s)
@@ -574,7 +585,8 @@ void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s)
     if (p.n == 0) return;
     uint32_t blocks = (p.n + RD_WAVES - 1) / RD_WAVES;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(rangedeps_kernel<true>, dim3(blocks), dim3(RD_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangedeps_kernel<true, RD_HCAP, RD_WAVES, false>), dim3(blocks), dim3(RD_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangedeps_kernel<true, RD_HCAP_BIG, 1, true>), dim3(256), dim3(64), 0, s, p);
 }
 
 size_t rangekeys_cp_bytes(uint32_t n, uint32_t nkeys)

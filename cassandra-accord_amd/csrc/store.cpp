@@ -99,13 +99,13 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipSetDevice(s->cfg.device);
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
-                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list,
+                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list, &s->cv_tmp,
                       &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
                       &s->rng_owner, &s->is_range, &s->rt_excl, &s->range_txns, &s->cnt_rngs, &s->cnt_rvals,
                       &s->cnt_r2v, &s->rd_rng_off, &s->rd_val_off, &s->rd_r2v_off, &s->rd_rng_start, &s->rd_rng_end,
-                      &s->rd_vals, &s->rd_r2v, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
+                      &s->rd_vals, &s->rd_r2v, &s->rd_big, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp};
@@ -319,7 +319,13 @@ int32_t accord_deps_compute(accord_store *s)
     accord::launch_keydeps_sizes(n, kp.key_off, kp.slice, rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
                                  rp.cnt_k2v, &dev->status, st);
     if (nrt) accord::launch_rangekeys_count(rp, st);
-    if (R) accord::launch_rangedeps_count(rp, st);
+    if (R) {
+        HIPCHECK(s, s->rd_big.ensure((size_t)n * 4 + 64));
+        rp.rd_big_count = s->rd_big.as<uint32_t>();
+        rp.rd_big_list = rp.rd_big_count + 16;
+        HIPCHECK(s, hipMemsetAsync(rp.rd_big_count, 0, 4, st));
+        accord::launch_rangedeps_count(rp, st);
+    }
     record(s, EV_COUNT);
     accord::exclusive_scan_u32(rp.cnt_keys, s->kd_key_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
     accord::exclusive_scan_u32(kp.cnt_vub, s->vub_off.as<uint32_t>(), n, &dev->totals[1], s->scan_tmp.p, st);
@@ -391,7 +397,9 @@ int32_t accord_deps_compute(accord_store *s)
     if (R) accord::launch_rangedeps_fill(rp, st);
     record(s, EV_RANGE);
     accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[7], s->scan_tmp.p, st);
-    accord::launch_compact_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, s->kd_vals.as<uint32_t>(), st);
+    HIPCHECK(s, s->cv_tmp.ensure(accord::compact_temp_bytes(vub_total)));
+    accord::launch_compact_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, s->kd_vals.as<uint32_t>(),
+                                vub_total, s->cv_tmp.p, st);
     record(s, EV_COMPACT);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
