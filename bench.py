@@ -37,7 +37,8 @@ def algorithmic_bytes(n, P, kc, U, D):
 
 
 def fill_kernel_bytes(n, P, kc, U, D):
-    """Algorithmic bytes of ONE launch of the fill kernel (keydeps_kernel<*>): reads lsb (8N),
+    """Algorithmic bytes of ONE pass of the fill stage (txnrec_kernel + keydeps_fast_kernel<1> +
+    keydeps_kernel<1,8> over the fast kernel's fallback list; every txn is filled once): reads lsb (8N),
     key_off (4(N+1)), key_ord (4P), the pair slices poslo (8P), each raw candidate once (4D), the
     three offset arrays (12(N+1)); writes the txnIds count (4N), keys (4kc), txnIds (4U) and
     keysToTxnIds (4(kc+D))."""
@@ -174,11 +175,27 @@ def main():
     kc = int(view["kd_keys_total"])
     U = int(view["kd_vals_total"])
     D = int(view["kd_k2v_total"]) - kc
+    fill_sizes = (n, P, kc, U, D)
+    if s.rng_off[-1] > 0:
+        # the fill stage only builds key txns' KeyDeps (range txns' come from range_fill): size the
+        # roofline unit by the key txns alone
+        dd = store.download()
+        key_txn = ~s.domains().astype(bool)
+        d_keys = np.diff(dd.kd_key_off.astype(np.int64))[key_txn]
+        d_vals = np.diff(dd.kd_val_off.astype(np.int64))[key_txn]
+        d_k2v = np.diff(dd.kd_k2v_off.astype(np.int64))[key_txn]
+        kc_k = int(d_keys.sum())
+        fill_sizes = (int(key_txn.sum()), int(np.diff(s.key_off.astype(np.int64))[key_txn].sum()), kc_k,
+                      int(d_vals.sum()), int(d_k2v.sum()) - kc_k)
     wo_info = None
     if args.waiting_on:
         wo = store.waiting_on()
         wo_info = {"max_level": wo.max_level, "reduced_edges": wo.preds_total,
                    "bitset_words": int(wo.wo_off[-1]), "level_histogram_top": int(np.bincount(wo.level).max())}
+
+    boundary = None
+    if world == 1 and not args.waiting_on:
+        boundary = boundary_rate(store, s)
 
     if rank != 0:
         store.close()
@@ -189,7 +206,7 @@ def main():
     txns_total = n_total * args.steps
     value = txns_total / elapsed
     B = algorithmic_bytes(n, P, kc, U, D)
-    Bf = fill_kernel_bytes(n, P, kc, U, D)
+    Bf = fill_kernel_bytes(*fill_sizes)
     fill_gbs = Bf / (stage["fill"] * 1e-3) / 1e9 if stage["fill"] > 0 else None
     pipe_gbs = B / (stage["total"] * 1e-3) / 1e9 if stage["total"] > 0 else None
 
@@ -219,7 +236,8 @@ def main():
         "deps_per_s": D * world * args.steps / elapsed,
         "sizes": {"N": n, "P": P, "keys_out": kc, "U": U, "D": D},
         "stage_ms": stage,
-        "roofline": {"kernel": "keydeps_kernel<1,true> (fill)", "bound": "hbm",
+        "roofline": {"kernel": "fill stage: txnrec_kernel + keydeps_fast_kernel<1> + keydeps_kernel<1,8>",
+                     "bound": "hbm",
                      "achieved": fill_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,
                      "traffic": traffic["traffic_bytes"] if traffic else None,
@@ -232,6 +250,8 @@ def main():
     }
     if wo_info is not None:
         line["waiting_on"] = wo_info
+    if boundary is not None:
+        line["boundary_inclusive"] = boundary
     print(json.dumps(line))
     store.close()
     if dist is not None:
@@ -248,6 +268,25 @@ def workload_name(args):
                 f"{args.keys_per_txn} keys/key txn, Zipf({args.zipf}) over {args.keyspace} keys, W={args.window}")
     return (f"config2: {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over {args.keyspace} keys, "
             f"{args.write_frac:.0%} writes, W={args.window}")
+
+
+def boundary_rate(store, s):
+    """PCIe-inclusive rate of the C-ABI entry accord_deps_batch (host SoA batch in, host CSR out:
+    H2D upload + pipeline + D2H of every output array), as a Java caller would see it.  Reported
+    next to `value`, never as it; the second of two calls is timed (the first sizes the buffers)."""
+    import ctypes as C
+    from accord_amd import _Deps, lib
+    b = s.c_batch()
+    ms = None
+    for _ in range(2):
+        d = _Deps()
+        t0 = time.perf_counter()
+        rc = lib().accord_deps_batch(store._h, C.byref(b), C.byref(d))
+        ms = (time.perf_counter() - t0) * 1e3
+        lib().accord_deps_release(C.byref(d))
+        if rc != 0:
+            return None
+    return {"ms": ms, "txns_per_s": s.n / (ms * 1e-3), "path": "accord_deps_batch, host buffers in and out"}
 
 
 def measured_traffic(config):

@@ -18,6 +18,6 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
 done
 rc=$?
 cd "$R"
-[ $rc -eq 0 ] && python3 scripts/traffic_json.py "$O/pmc1" "$O/pmc2" "keydeps_kernel<1," "profiles/$TAG" "$O/traffic_config2.json"
+[ $rc -eq 0 ] && python3 scripts/traffic_json.py "$O/pmc1" "$O/pmc2" "txnrec_kernel,keydeps_fast_kernel<,keydeps_kernel<" "profiles/$TAG" "$O/traffic_config2.json"
 echo "rc=$rc"; tail -2 "$O/pytest_gpu.log"
 exit $rc

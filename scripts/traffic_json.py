@@ -1,7 +1,7 @@
-"""Per-launch HBM traffic of the roofline kernel from rocprofv3 --pmc passes (FETCH_SIZE and
+"""Per-step HBM traffic of the roofline unit (one or more kernels, comma-separated substrings) from rocprofv3 --pmc passes (FETCH_SIZE and
 WRITE_SIZE in separate runs; values in KB per dispatch).  gfx950 correction (MI355X_MICROARCH.md,
 HBM): FETCH_SIZE reports half the bytes of wide coalesced reads, so traffic = 2*FETCH + WRITE; the
-raw counters are kept next to it.  Usage: traffic_json.py <fetch_dir> <write_dir> <kernel-substr>
+raw counters are kept next to it.  Usage: traffic_json.py <fetch_dir> <write_dir> <substr[,substr..]>
 <profile-dir-to-cite> <out.json>"""
 import csv
 import json
@@ -18,10 +18,16 @@ def per_dispatch(d, counter, ksub):
     return sum(vals) / len(vals), len(vals)
 
 
-fetch_dir, write_dir, ksub, cite, out = sys.argv[1:6]
-fkb, nf = per_dispatch(fetch_dir, "FETCH_SIZE", ksub)
-wkb, nw = per_dispatch(write_dir, "WRITE_SIZE", ksub)
-doc = {"kernel": ksub, "fetch_size_kb": fkb, "write_size_kb": wkb, "dispatches": [nf, nw],
+fetch_dir, write_dir, ksubs, cite, out = sys.argv[1:6]
+fkb = wkb = 0.0
+per = {}
+for ksub in ksubs.split(","):        # every kernel of the unit runs once per step
+    f, nf = per_dispatch(fetch_dir, "FETCH_SIZE", ksub)
+    w, nw = per_dispatch(write_dir, "WRITE_SIZE", ksub)
+    per[ksub] = {"fetch_size_kb": f, "write_size_kb": w, "dispatches": [nf, nw]}
+    fkb += f
+    wkb += w
+doc = {"kernel": ksubs, "fetch_size_kb": fkb, "write_size_kb": wkb, "per_kernel": per,
        "traffic_bytes": (2 * fkb + wkb) * 1024.0,
        "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of wide reads)",
        "source": cite}
