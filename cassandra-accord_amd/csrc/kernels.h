@@ -18,8 +18,10 @@ struct DevStatus {
 size_t radix_sort_temp_bytes(uint32_t n);
 // Stable LSD sort of (key, val) by key over `bits` low bits.  Result ends in keys_out/vals_out.
 // keys_tmp/vals_tmp are ping-pong buffers of n entries.
+// ents_in (optional, may be null) is a second value carried the same way into ents_out.
 void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys_out, uint32_t *vals_out,
-                      uint32_t *keys_tmp, uint32_t *vals_tmp, uint32_t n, int bits, void *temp, hipStream_t s);
+                      uint32_t *keys_tmp, uint32_t *vals_tmp, const uint32_t *ents_in, uint32_t *ents_out,
+                      uint32_t *ents_tmp, uint32_t n, int bits, void *temp, hipStream_t s);
 
 // ---- scan (scan.hip) ----
 size_t scan_temp_bytes(uint32_t n);
@@ -66,7 +68,7 @@ void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *exc
 size_t history_temp_bytes(uint32_t P);
 // key-major: history entries, segments, and per pair its deps slice (txn-major PairSlice)
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
-                    const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
+                    const uint32_t *sorted_pair, const uint32_t *hist, uint32_t *seg_start,
                     uint32_t *seg_end, PairSlice *slice, void *temp, hipStream_t s);
 // history tile size of the Write max-scan carry (pw_local / pw_carry) and class-count carries
 constexpr uint32_t HISTORY_TILE = 4096;

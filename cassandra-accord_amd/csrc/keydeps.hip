@@ -120,75 +120,75 @@ constexpr int HS_ITEMS = 16;
 constexpr uint32_t HS_TILE = HS_THREADS * HS_ITEMS;
 static_assert(HS_TILE == HISTORY_TILE, "history tile");
 
-// hist[p] = entry of sorted pair p; segment bounds per key; tile-local inclusive max-scan of
-// (p+1 if entry p is a Write) -> the last Write at or before p, and tile-local inclusive class
-// counts; both completed by tile carries.
+// Segment bounds per key; tile-local inclusive max-scan of (p+1 if entry p is a Write) -> the last
+// Write at or before p, and tile-local inclusive class counts; both completed by tile carries.
+// hist (key-major entries) comes out of the radix sort.  Every wave owns a contiguous quarter of
+// the tile and scans it in 16 coalesced rounds with wave scans and a running carry held in
+// registers; one block step adds the preceding waves' totals.
 __global__ __launch_bounds__(HS_THREADS) void history1_kernel(uint32_t P, const uint32_t *__restrict__ sorted_key,
-                                                              const uint32_t *__restrict__ sorted_pair,
-                                                              const uint32_t *__restrict__ pair_ent,
-                                                              uint32_t *__restrict__ hist, uint32_t *__restrict__ seg_start,
+                                                              const uint32_t *__restrict__ hist,
+                                                              uint32_t *__restrict__ seg_start,
                                                               uint32_t *__restrict__ seg_end, uint32_t *__restrict__ pw_local,
                                                               uint32_t *__restrict__ tile_max, uint64_t *__restrict__ c_local,
                                                               uint64_t *__restrict__ tile_cnt)
 {
-    __shared__ uint32_t tile[HS_TILE];
-    __shared__ uint64_t ctile[HS_TILE];
     __shared__ uint32_t wmax[HS_THREADS / 64];
     __shared__ uint64_t wcnt[HS_THREADS / 64];
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * HS_TILE;
-#pragma unroll 4
-    for (int j = 0; j < HS_ITEMS; ++j) {
-        const uint32_t p = base + j * HS_THREADS + tid;
+    const uint32_t w = wave_id(), lane = lane_id();
+    const uint32_t wb = blockIdx.x * HS_TILE + w * (HS_ITEMS * 64);
+    uint32_t e[HS_ITEMS], k[HS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < HS_ITEMS; ++r) {
+        const uint32_t p = wb + r * 64 + lane;
+        e[r] = p < P ? hist[p] : 0u;
+        k[r] = p < P ? sorted_key[p] : 0xFFFFFFFFu;
+    }
+    uint32_t run = 0;
+    uint64_t crun = 0;
+    uint64_t cc[HS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < HS_ITEMS; ++r) {
+        const uint32_t p = wb + r * 64 + lane;
+        constexpr uint32_t EDGE = 0xFFFFFFFEu;       // neighbour outside the register rows: load it
+        uint32_t kp = __shfl_up(k[r], 1, 64), kn = __shfl_down(k[r], 1, 64);
+        const uint32_t kprev_row = __shfl(k[r > 0 ? r - 1 : 0], 63, 64);
+        const uint32_t knext_row = __shfl(k[r + 1 < HS_ITEMS ? r + 1 : r], 0, 64);
+        if (lane == 0) kp = r > 0 ? kprev_row : EDGE;
+        if (lane == 63) kn = r + 1 < HS_ITEMS ? knext_row : EDGE;
         uint32_t v = 0;
         uint64_t c = 0;
         if (p < P) {
-            const uint32_t e = pair_ent[sorted_pair[p]];
-            hist[p] = e;
-            const uint32_t k = sorted_key[p];
-            if (p == 0 || sorted_key[p - 1] != k) seg_start[k] = p;
-            if (p == P - 1 || sorted_key[p + 1] != k) seg_end[k] = p + 1;
-            v = (e >> ENT_KIND_SHIFT) == 1u ? p + 1 : 0u;
-            c = class_bits(e >> ENT_KIND_SHIFT);
+            if (kp == EDGE) kp = p > 0 ? sorted_key[p - 1] : 0xFFFFFFFFu;
+            if (kn == EDGE) kn = p + 1 < P ? sorted_key[p + 1] : 0xFFFFFFFFu;
+            if (kp != k[r]) seg_start[k[r]] = p;
+            if (kn != k[r]) seg_end[k[r]] = p + 1;
+            v = (e[r] >> ENT_KIND_SHIFT) == 1u ? p + 1 : 0u;
+            c = class_bits(e[r] >> ENT_KIND_SHIFT);
         }
-        tile[j * HS_THREADS + tid] = v;
-        ctile[j * HS_THREADS + tid] = c;
+        v = max(run, wave_incl_max(v));
+        c = crun + wave_incl_scan64(c);
+        run = readlane(v, 63);
+        crun = (uint64_t)readlane((uint32_t)c, 63) | ((uint64_t)readlane((uint32_t)(c >> 32), 63) << 32);
+        e[r] = v;                                    // wave-local running values
+        cc[r] = c;
     }
+    if (lane == 0) { wmax[w] = run; wcnt[w] = crun; }
     __syncthreads();
-    uint32_t run = 0;
-    uint64_t csum = 0;
+    uint32_t ex = 0;
+    uint64_t cex = 0;
+    for (uint32_t u = 0; u < w; ++u) { ex = max(ex, wmax[u]); cex += wcnt[u]; }
 #pragma unroll
-    for (int j = 0; j < HS_ITEMS; ++j) {
-        run = max(run, tile[tid * HS_ITEMS + j]);
-        csum += ctile[tid * HS_ITEMS + j];
-    }
-    const uint32_t incl = wave_incl_max(run);
-    const uint64_t cincl = wave_incl_scan64(csum);
-    if (lane_id() == 63) { wmax[tid >> 6] = incl; wcnt[tid >> 6] = cincl; }
-    __syncthreads();
-    uint32_t ex = __shfl_up(incl, 1, 64);
-    uint64_t cex = cincl - csum;
-    if (lane_id() == 0) ex = 0;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) { ex = max(ex, wmax[w]); cex += wcnt[w]; }
-#pragma unroll
-    for (int j = 0; j < HS_ITEMS; ++j) {
-        ex = max(ex, tile[tid * HS_ITEMS + j]);
-        tile[tid * HS_ITEMS + j] = ex;
-        cex += ctile[tid * HS_ITEMS + j];
-        ctile[tid * HS_ITEMS + j] = cex;
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < HS_ITEMS; ++j) {
-        const uint32_t p = base + j * HS_THREADS + tid;
+    for (int r = 0; r < HS_ITEMS; ++r) {
+        const uint32_t p = wb + r * 64 + lane;
         if (p < P) {
-            pw_local[p] = tile[j * HS_THREADS + tid];
-            c_local[p] = ctile[j * HS_THREADS + tid];
+            pw_local[p] = max(e[r], ex);
+            c_local[p] = cc[r] + cex;
         }
     }
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
         uint32_t m = 0;
         uint64_t c = 0;
-        for (uint32_t w = 0; w < HS_THREADS / 64; ++w) { m = max(m, wmax[w]); c += wcnt[w]; }
+        for (uint32_t u = 0; u < HS_THREADS / 64; ++u) { m = max(m, wmax[u]); c += wcnt[u]; }
         tile_max[blockIdx.x] = m;
         tile_cnt[blockIdx.x] = c;
     }
@@ -235,10 +235,12 @@ __global__ __launch_bounds__(256) void history_carry_kernel(uint32_t *__restrict
 // model.  lo = the last Write entry j < i-W of the segment (committed[] bound of
 // CommandsForKey.mapReduceActive :620-645), else the segment start.  Written txn-major, with the
 // number of slice entries kind(i) witnesses (the pair's share of keysToTxnIds).
-// Block per tile of H2_TILE positions; the txn indices of the tile and of H2_HALO positions before
-// it are staged in LDS, so the backward search for the window bound runs on LDS (a global search
-// only when a segment's window reaches past the halo: keys hotter than H2_HALO entries per W txns).
-constexpr uint32_t H2_THREADS = 256, H2_TILE = 2048, H2_HALO = 2048;
+// Block per tile of H2_TILE positions; the entries of the tile and of H2_HALO positions before it
+// are staged in LDS, so the backward search for the window bound runs on LDS (a global search only
+// when a segment's window reaches past the halo: keys hotter than H2_HALO entries per W txns).
+// Each thread handles H2_ITEMS positions in stages (loads of every item issued before any is
+// consumed), so the dependent round trips are paid once per stage, not once per item.
+constexpr uint32_t H2_THREADS = 256, H2_TILE = 2048, H2_HALO = 2048, H2_ITEMS = H2_TILE / H2_THREADS;
 
 __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32_t window, const uint32_t *__restrict__ sorted_key,
                                                               const uint32_t *__restrict__ sorted_pair,
@@ -254,37 +256,53 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
     const uint32_t base = blockIdx.x * H2_TILE;
     const uint32_t lds_lo = base > H2_HALO ? base - H2_HALO : 0u;
     const uint32_t end = min(P, base + H2_TILE);
-    for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) tx[x - lds_lo] = hist[x] & ENT_TXN_MASK;
+    uint32_t key[H2_ITEMS], q[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        key[j] = p < end ? sorted_key[p] : 0u;
+        q[j] = p < end ? sorted_pair[p] : 0u;
+    }
+    for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) tx[x - lds_lo] = hist[x];
+    uint32_t a[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        a[j] = p < end ? seg_start[key[j]] : 0u;
+    }
     __syncthreads();
-    for (uint32_t p = base + threadIdx.x; p < end; p += H2_THREADS) {
-        const uint32_t ent = hist[p];
-        const uint32_t i = ent & ENT_TXN_MASK;
-        const uint32_t a = seg_start[sorted_key[p]];
-        uint32_t lo = a;
-        if (i > window) {
+    // window bound: l = first position in [a, p] whose txn >= i - W (only when i > W)
+    uint32_t ent[H2_ITEMS], l[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        ent[j] = p < end ? tx[p - lds_lo] : 0u;
+        const uint32_t i = ent[j] & ENT_TXN_MASK;
+        l[j] = a[j];
+        if (p < end && i > window) {
             const uint32_t thr = i - window;
-            // first q in [a, p] with txn >= thr: exponential search backwards, on LDS down to lb
-            const uint32_t lb = max(a, lds_lo);
-            uint32_t hi = p, l = lb, step = 1;
+            // exponential search backwards, on LDS down to lb
+            const uint32_t lb = max(a[j], lds_lo);
+            uint32_t hi = p, lo = lb, step = 1;
             bool found = false;
             while (hi > lb) {
                 const uint32_t probe = (hi - lb > step) ? hi - step : lb;
-                if (tx[probe - lds_lo] < thr) { l = probe + 1; found = true; break; }
+                if ((tx[probe - lds_lo] & ENT_TXN_MASK) < thr) { lo = probe + 1; found = true; break; }
                 hi = probe;
                 step <<= 1;
             }
-            if (found || lb == a) {
+            if (found || lb == a[j]) {
                 uint32_t h = hi;
-                while (l < h) {
-                    const uint32_t m = (l + h) >> 1;
-                    if (tx[m - lds_lo] < thr) l = m + 1; else h = m;
+                while (lo < h) {
+                    const uint32_t m = (lo + h) >> 1;
+                    if ((tx[m - lds_lo] & ENT_TXN_MASK) < thr) lo = m + 1; else h = m;
                 }
-                if (!found) l = hi;                     // every entry of [lb, p] is inside the window
+                if (!found) lo = hi;                    // every entry of [lb, p] is inside the window
             } else {                                    // window reaches past the halo: global search
-                uint32_t gh = lb, gl = a;
+                uint32_t gh = lb, gl = a[j];
                 uint32_t st = 1;
-                while (gh > a) {
-                    const uint32_t probe = (gh - a > st) ? gh - st : a;
+                while (gh > a[j]) {
+                    const uint32_t probe = (gh - a[j] > st) ? gh - st : a[j];
                     if ((hist[probe] & ENT_TXN_MASK) < thr) { gl = probe + 1; break; }
                     gh = probe;
                     st <<= 1;
@@ -293,21 +311,37 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
                     const uint32_t m = (gl + gh) >> 1;
                     if ((hist[m] & ENT_TXN_MASK) < thr) gl = m + 1; else gh = m;
                 }
-                l = gl;
+                lo = gl;
             }
-            if (l > a) {
-                const uint32_t x = l - 1;
-                const uint32_t pw = max(pw_local[x], carry[x / HS_TILE]);   // (last Write <= x) + 1
-                if (pw > a) lo = pw - 1;
-            }
+            l[j] = lo;
         }
-        uint32_t cnt = 0;
-        if (p > lo) {
-            const uint32_t wmask = witness_mask(ent >> ENT_KIND_SHIFT);
-            cnt = witnessed_upto(c_local, ccarry, p - 1, wmask) - (lo ? witnessed_upto(c_local, ccarry, lo - 1, wmask) : 0u);
+    }
+    // lo = the last Write before l (if any, inside the segment), else the segment start
+    uint32_t pw[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        pw[j] = 0;
+        if (l[j] > a[j]) {
+            const uint32_t x = l[j] - 1;
+            pw[j] = max(pw_local[x], carry[x / HS_TILE]);   // (last Write <= x) + 1
         }
-        const uint32_t q = sorted_pair[p];
-        slice[q] = PairSlice{lo, p, cnt, 0u};
+    }
+    uint32_t cnt[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        l[j] = pw[j] > a[j] ? pw[j] - 1 : a[j];         // now: lo
+        cnt[j] = 0;
+        if (p < end && p > l[j]) {
+            const uint32_t wmask = witness_mask(ent[j] >> ENT_KIND_SHIFT);
+            cnt[j] = witnessed_upto(c_local, ccarry, p - 1, wmask) -
+                     (l[j] ? witnessed_upto(c_local, ccarry, l[j] - 1, wmask) : 0u);
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        if (p < end) slice[q[j]] = PairSlice{l[j], p, cnt[j], 0u};
     }
 }
 
@@ -1042,7 +1076,7 @@ HistoryViews history_views(void *temp, uint32_t P)
 }
 
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
-                    const uint32_t *sorted_pair, const uint32_t *pair_ent, uint32_t *hist, uint32_t *seg_start,
+                    const uint32_t *sorted_pair, const uint32_t *hist, uint32_t *seg_start,
                     uint32_t *seg_end, PairSlice *slice, void *temp, hipStream_t s)
 {
     (void)nkeys;
@@ -1057,8 +1091,7 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
     off += ((size_t)P + tiles) * 8;
     off = (off + 15) & ~(size_t)15;
     ClassCarry *ccarry = (ClassCarry *)((char *)temp + off);
-    hipLaunchKernelGGL(history1_kernel, dim3(tiles), dim3(HS_THREADS), 0, s, P, sorted_key, sorted_pair, pair_ent,
-                       hist, seg_start, seg_end, pw_local, tile_max, c_local, tile_cnt);
+    hipLaunchKernelGGL(history1_kernel, dim3(tiles), dim3(HS_THREADS), 0, s, P, sorted_key, hist, seg_start, seg_end, pw_local, tile_max, c_local, tile_cnt);
     hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tile_cnt, ccarry, tiles);
     hipLaunchKernelGGL(history2_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P, window,
                        sorted_key, sorted_pair, hist,

@@ -6,7 +6,9 @@
 //   scan      : exclusive scan of the counts (scan.hip) -> global offset per (digit, tile)
 //   downsweep : stable in-tile ranking with wave ballots, the tile is re-ordered by digit in LDS
 //               and written out as contiguous per-digit runs (coalesced stores).
-// Stability keeps the entries of one key in TxnId (= input) order.
+// Stability keeps the entries of one key in TxnId (= input) order.  An optional second value
+// (the history entry of each pair) rides along, so the key-major history is produced by the sort
+// itself instead of by a random gather afterwards.
 #include "device_common.h"
 #include "kernels.h"
 
@@ -44,6 +46,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint32_t *__restr
 template <int BITS>
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                           const uint32_t *__restrict__ ein, uint32_t *__restrict__ eout,
                                                            uint32_t n, int shift, uint32_t mask,
                                                            const uint32_t *__restrict__ offs, uint32_t tiles)
 {
@@ -63,12 +66,13 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
     const uint32_t tile_n = min((uint32_t)RS_TILE, n - base);
     const uint32_t wbase = base + w * (RS_ITEMS * 64);
 
-    uint32_t key[RS_ITEMS], val[RS_ITEMS], lrank[RS_ITEMS];
+    uint32_t key[RS_ITEMS], val[RS_ITEMS], ent[RS_ITEMS], lrank[RS_ITEMS];
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
         const uint32_t idx = wbase + r * 64 + lane;
         key[r] = idx < n ? kin[idx] : 0u;
         val[r] = idx < n ? (vin ? vin[idx] : idx) : 0u;
+        ent[r] = (ein && idx < n) ? ein[idx] : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -136,6 +140,22 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
         kout[g] = k;
         vout[g] = s_vals[q];
     }
+    if (ein) {                                   // second value: same placement through s_vals
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RS_ITEMS; ++r) {
+            const uint32_t idx = wbase + r * 64 + lane;
+            if (idx < n) {
+                const uint32_t d = (key[r] >> shift) & MASK;
+                s_vals[run[d] + wcnt[w][d] + lrank[r]] = ent[r];
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < tile_n; q += RS_THREADS) {
+            const uint32_t d = (s_keys[q] >> shift) & MASK;
+            eout[glob[d] + (q - run[d])] = s_vals[q];
+        }
+    }
 }
 } // namespace
 
@@ -148,7 +168,8 @@ size_t radix_sort_temp_bytes(uint32_t n)
 }
 
 void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys_out, uint32_t *vals_out,
-                      uint32_t *keys_tmp, uint32_t *vals_tmp, uint32_t n, int bits, void *temp, hipStream_t s)
+                      uint32_t *keys_tmp, uint32_t *vals_tmp, const uint32_t *ents_in, uint32_t *ents_out,
+                      uint32_t *ents_tmp, uint32_t n, int bits, void *temp, hipStream_t s)
 {
     if (n == 0) return;
     const uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
@@ -161,7 +182,7 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
     if (bits < 1) bits = 1;
     const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
     // ping-pong so that the last pass lands in *_out; vals_in == nullptr means identity values
-    const uint32_t *ki = keys_in, *vi = vals_in;
+    const uint32_t *ki = keys_in, *vi = vals_in, *ei = ents_in;
     int shift = 0;
     for (int p = 0; p < passes; ++p) {
         const int pb = (bits - shift + (passes - p) - 1) / (passes - p);   // split bits evenly
@@ -169,14 +190,15 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
         const bool to_out = ((passes - 1 - p) % 2) == 0;
         uint32_t *ko = to_out ? keys_out : keys_tmp;
         uint32_t *vo = to_out ? vals_out : vals_tmp;
+        uint32_t *eo = ents_in ? (to_out ? ents_out : ents_tmp) : nullptr;
         const size_t hist_n = (size_t)(mask + 1) * tiles;
         hipLaunchKernelGGL(rs_upsweep, dim3(tiles), dim3(RS_THREADS), 0, s, ki, n, shift, mask, hist, tiles);
         exclusive_scan_u32(hist, offs, (uint32_t)hist_n, total, scan_tmp, s);
         if (pb > 8)
-            hipLaunchKernelGGL(rs_downsweep<9>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, mask, offs, tiles);
+            hipLaunchKernelGGL(rs_downsweep<9>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
         else
-            hipLaunchKernelGGL(rs_downsweep<8>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, shift, mask, offs, tiles);
-        ki = ko; vi = vo;
+            hipLaunchKernelGGL(rs_downsweep<8>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
+        ki = ko; vi = vo; ei = eo;
         shift += pb;
     }
 }

@@ -99,7 +99,7 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipSetDevice(s->cfg.device);
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
-                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list, &s->cv_tmp,
+                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->tmp_ent, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list, &s->cv_tmp,
                       &s->seg_start, &s->seg_end, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
@@ -212,6 +212,7 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->sort_pair.ensure((size_t)P * 4));
     HIPCHECK(s, s->tmp_key.ensure((size_t)P * 4));
     HIPCHECK(s, s->tmp_val.ensure((size_t)P * 4));
+    HIPCHECK(s, s->tmp_ent.ensure((size_t)P * 4));
     HIPCHECK(s, s->hist.ensure((size_t)P * 4));
     HIPCHECK(s, s->slice.ensure((size_t)P * sizeof(accord::PairSlice)));
     HIPCHECK(s, s->cnt_vub.ensure((size_t)n * 4 + 4));
@@ -257,13 +258,14 @@ int32_t accord_deps_compute(accord_store *s)
     }
     record(s, EV_VALIDATE);
     accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
-                             s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(), P,
+                             s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
+                             s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), P,
                              bits_for(nkeys - 1), s->radix_tmp.p, st);
     record(s, EV_SORT);
     HIPCHECK(s, hipMemsetAsync(s->seg_start.p, 0, (size_t)nkeys * 4, st));
     HIPCHECK(s, hipMemsetAsync(s->seg_end.p, 0, (size_t)nkeys * 4, st));
     accord::launch_history(P, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
-                           s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
+                           s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
                            s->seg_end.as<uint32_t>(), s->slice.as<accord::PairSlice>(),
                            s->hist_tmp.p, st);
     record(s, EV_SEGMENT);

@@ -54,7 +54,7 @@ struct accord_store {
     bool has_batch = false, computed = false;
     DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
     // work
-    DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, seg_start, seg_end, radix_tmp;
+    DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, tmp_ent, seg_start, seg_end, radix_tmp;
     DevBuf hist, slice, hist_tmp, cnt_vub, vub_off, vgap, fk_recs, fk_list, cv_tmp;
     DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
     DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v, rd_big, rk_cp, rk_cnt, rk_off, rk_slices;
