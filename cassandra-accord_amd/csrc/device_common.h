@@ -78,14 +78,13 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 // Kind ordinals: Read 0, Write 1, EphemeralRead 2, SyncPoint 3, ExclusiveSyncPoint 4, LocalOnly 5
 // witnesses(): Read/EphemeralRead -> Ws, Write -> RsOrWs, SyncPoints -> AnyGloballyVisible.
 // Encoded as a bitmask over entry kinds: Ws = {W}, RsOrWs = {R,W}, AnyGV = {R,W,SP,ESP}.
+// Read, EphemeralRead -> {W}; Write -> {R, W}; SyncPoint, ExclusiveSyncPoint -> {R, W, SP, XSP};
+// LocalOnly / invalid -> {} (rejected by validation).  One byte per kind of a 64-bit table: a shift
+// and a mask instead of a branch chain.
 __host__ __device__ __forceinline__ uint32_t witness_mask(uint32_t kind)
 {
-    switch (kind) {
-    case 0: case 2: return 0x2u;
-    case 1: return 0x3u;
-    case 3: case 4: return 0x1Bu;
-    default: return 0u;      // LocalOnly / invalid: rejected by validation
-    }
+    constexpr uint64_t T = 0x02ull | 0x03ull << 8 | 0x02ull << 16 | 0x1Bull << 24 | 0x1Bull << 32;
+    return (uint32_t)(T >> ((kind & 7u) * 8u)) & 0xFFu;
 }
 
 __device__ __forceinline__ int ts_cmp(uint64_t am, uint64_t al, int32_t an, uint64_t bm, uint64_t bl, int32_t bn)

@@ -724,7 +724,8 @@ __global__ __launch_bounds__(256) void txnrec_kernel(KeyDepsParams p, TxnRec *__
     }
 }
 
-constexpr uint32_t FK_RAW = 64u * KD_CB;     // raw candidates the fast path takes
+constexpr int FK_CB = 6;                      // candidate batches of 64 a fast-path txn may use
+constexpr uint32_t FK_RAW = 64u * FK_CB;      // raw candidates the fast path takes
 
 // inclusive scan over lanes 0..7 (row 0 of the wave; lanes >= 8 get partial sums)
 __device__ __forceinline__ uint32_t scan8(uint32_t v)
@@ -756,31 +757,33 @@ __device__ __forceinline__ void fk_slices(const KeyDepsParams &p, FkTxn &x, uint
     }
 }
 
-// slot plan (end = inclusive raw prefix, delta = slice start - exclusive prefix) and the raw
-// candidates of a txn with k <= 8 and <= FK_RAW of them (else e[] stays empty)
+// The raw candidates of a txn with k <= 8 and <= FK_RAW of them (else e[] stays empty): candidate r
+// lies in slot q = #{q' >= 1 : excl_q' <= r} (empty slots fall out: their boundary equals the next
+// slot's), and sits at hist[r + lo_q - excl_q]; the slot's delta comes from lane q by bpermute.
 __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn &x, uint32_t lane,
-                                             uint32_t (&e)[KD_CB])
+                                             uint32_t (&e)[FK_CB])
 {
     const uint32_t k = readlane(x.rec, 1);
     const uint32_t raw = (k <= 8 && lane < k) ? x.pos - x.lo : 0u;
     const uint32_t incl = scan8(raw);
-    const int32_t delta = (int32_t)x.lo - (int32_t)(incl - raw);
+    const uint32_t excl = incl - raw;
+    const int32_t delta = (int32_t)x.lo - (int32_t)excl;
     const uint32_t rt = readlane(incl, 7);
     uint32_t eq[7];
-    int32_t dq[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dq[q] = (int32_t)readlane((uint32_t)delta, q);
-#pragma unroll
-    for (int q = 0; q < 7; ++q) eq[q] = q + 1 < (int)k ? readlane(incl, q) : 0xFFFFFFFFu;
+    for (int q = 0; q < 7; ++q) eq[q] = readlane(excl, q + 1);
     const bool take = k <= 8 && rt <= FK_RAW;
 #pragma unroll
-    for (int c = 0; c < KD_CB; ++c) {
-        e[c] = KD_NONE;
-        const uint32_t r = c * 64 + lane;
-        int32_t d = dq[0];
+    for (int c = 0; c < FK_CB; ++c) e[c] = KD_NONE;
 #pragma unroll
-        for (int q = 0; q < 7; ++q) d = r >= eq[q] ? dq[q + 1] : d;
-        if (take && r < rt) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
+    for (int c = 0; c < FK_CB; ++c) {
+        if (!take || (uint32_t)c * 64u >= rt) break;   // wave-uniform
+        const uint32_t r = c * 64 + lane;
+        uint32_t slot = 0;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) slot += r >= eq[q] ? 1u : 0u;
+        const int32_t d = __builtin_amdgcn_ds_bpermute((int)(slot << 2), delta);
+        if (r < rt) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
     }
     return rt;
 }
@@ -807,14 +810,14 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     c.rec = fk_rec(recs, t + 2 * S, n, lane);
     fk_slices(p, a, lane);
     fk_slices(p, b, lane);
-    uint32_t ea[KD_CB];
+    uint32_t ea[FK_CB];
     uint32_t rta = fk_cands(p, a, lane, ea);
 
     for (; t < n; t += S) {
         FkTxn d;
         d.rec = fk_rec(recs, t + 3 * S, n, lane);
         fk_slices(p, c, lane);
-        uint32_t eb[KD_CB];
+        uint32_t eb[FK_CB];
         const uint32_t rtb = fk_cands(p, b, lane, eb);
 
         do {   // ---- txn t (break = done with it) ----
@@ -828,13 +831,13 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             const uint32_t wmask = witness_mask(kind);
             const uint32_t nb = SPAN - gi;            // near bit of txn j: j + nb (< SPAN iff near)
             uint32_t F = 0;                           // far deps (older than the near span)
-            uint32_t fidx[KD_CB];
+            uint32_t fidx[FK_CB];
             if (!fallback) {
 #pragma unroll
                 for (int q = 0; q < WPL; ++q) bm[lane * WPL + q] = 0ull;
                 wave_lds_sync();
 #pragma unroll
-                for (int cc = 0; cc < KD_CB; ++cc) {
+                for (int cc = 0; cc < FK_CB; ++cc) {
                     fidx[cc] = 0;
                     if ((uint32_t)cc * 64 >= rta) break;   // wave-uniform
                     const uint32_t ev = ea[cc];
@@ -861,18 +864,22 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             // far deps: de-duplicated ranks (all of them precede the near span in TxnId order)
             uint32_t far_u = 0;
             if (F) {                                      // wave-uniform
+                // the first holder of every value owns it; rank = distinct values below it
                 const uint32_t x = lane < F ? fr[lane] : 0xFFFFFFFFu;
-                bool own = lane < F;
-                for (uint32_t g = 0; g < F; ++g)
-                    own = own && !(g < lane && readlane(x, (int)g) == x);
-                const uint64_t om = __ballot(own);
-                far_u = (uint32_t)__popcll(om);
+                uint64_t om = 0;
                 uint32_t rk = 0;
-                for (uint64_t m = om; m; m &= m - 1)
-                    rk += readlane(x, (int)__builtin_ctzll(m)) < x ? 1u : 0u;
+                for (uint32_t g = 0; g < F; ++g) {
+                    const uint32_t xg = readlane(x, (int)g);
+                    const uint64_t m = __ballot(x == xg);
+                    if ((uint32_t)__builtin_ctzll(m) == g) {   // g is xg's first holder (uniform)
+                        om |= 1ull << g;
+                        rk += xg < x ? 1u : 0u;
+                    }
+                }
+                far_u = (uint32_t)__popcll(om);
                 wave_lds_sync();
                 if (lane < F) fr[lane] = rk;
-                if (own) stg(p.vgap, readlane(a.rec, 5) + rk, x);
+                if ((om >> lane) & 1ull) stg(p.vgap, readlane(a.rec, 5) + rk, x);
             }
             // union: popcounts -> per-word rank prefix (after the far deps); |txnIds|
             uint32_t pc[WPL], mysum = 0;
@@ -900,7 +907,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             // body: rank of every witnessed entry; txnIds at their ranks
             uint32_t run = 0;
 #pragma unroll
-            for (int cc = 0; cc < KD_CB; ++cc) {
+            for (int cc = 0; cc < FK_CB; ++cc) {
                 if ((uint32_t)cc * 64 >= rta) break;
                 const uint32_t ev = ea[cc];
                 const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
@@ -922,7 +929,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         a = b; b = c; c = d;
         rta = rtb;
 #pragma unroll
-        for (int cc = 0; cc < KD_CB; ++cc) ea[cc] = eb[cc];
+        for (int cc = 0; cc < FK_CB; ++cc) ea[cc] = eb[cc];
     }
 }
 

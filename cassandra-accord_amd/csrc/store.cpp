@@ -411,6 +411,11 @@ int32_t accord_deps_compute(accord_store *s)
         if (rc) return rc;
         s->tot_vals = s->pinned->totals[7];
     }
+    if (getenv("ACCORD_FILL_STATS")) {                 // dev aid: txns the fast fill handed on
+        uint32_t fb = 0;
+        HIPCHECK(s, hipMemcpy(&fb, kp.fb_count, 4, hipMemcpyDeviceToHost));
+        fprintf(stderr, "fill: %u of %u txns took the general kernel\n", fb, n);
+    }
 
     if (s->events) {
         auto el = [&](int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, s->ev[a], s->ev[b]); return ms; };
