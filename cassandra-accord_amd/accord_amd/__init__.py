@@ -46,7 +46,8 @@ EXPORTED_SYMBOLS = [
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
     "accord_comm_init", "accord_deps_exchange_merge", "accord_shard_timing",
     "accord_waiting_on_compute", "accord_waiting_on_download", "accord_waiting_on_release",
-    "accord_waiting_on_timing",
+    "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
+    "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
 ]
 
 
@@ -104,6 +105,12 @@ class _WaitingOn(C.Structure):
                 ("owner", C.c_void_p)]
 
 
+class _Inverse(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("kd_total", C.c_uint64), ("rd_total", C.c_uint64),
+                ("kd_t2k_off", _u32p), ("kd_t2k", _i32p), ("rd_t2r_off", _u32p), ("rd_t2r", _i32p),
+                ("owner", C.c_void_p)]
+
+
 class _Timing(C.Structure):
     _fields_ = [("validate_ms", C.c_float), ("sort_ms", C.c_float), ("segment_ms", C.c_float),
                 ("count_ms", C.c_float), ("scan_ms", C.c_float), ("fill_ms", C.c_float),
@@ -156,6 +163,13 @@ def lib() -> C.CDLL:
         L.accord_waiting_on_release.argtypes = [C.POINTER(_WaitingOn)]
         L.accord_waiting_on_release.restype = None
         L.accord_waiting_on_timing.argtypes = [C.c_void_p] + [C.POINTER(C.c_float)] * 3
+        L.accord_deps_union.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_Deps)]
+        L.accord_deps_slice.argtypes = [C.c_void_p, C.POINTER(_Deps), _u32p, _u32p, _u32p, C.c_uint32]
+        L.accord_deps_invert.argtypes = [C.c_void_p, C.POINTER(_Deps), C.POINTER(_Inverse)]
+        L.accord_deps_inverse_release.argtypes = [C.POINTER(_Inverse)]
+        L.accord_deps_inverse_release.restype = None
+        L.accord_ops_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
+        L.accord_deps_upload.argtypes = [C.c_void_p, C.POINTER(_Deps)]
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
             if f.restype is C.c_int:  # default
@@ -479,6 +493,53 @@ class CommandStore:
         a, b = C.c_float(), C.c_float()
         self._check(lib().accord_shard_timing(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+    # deps-set operations (a9 general union, a10 slice / invert); sources are CommandStores on this
+    # device whose current deps index the same TxnId table
+    def union(self, parts):
+        """Deps.merge of the current deps of `parts` (keys may overlap: KeyDeps.merge /
+        RangeDeps.merge -> RelationMultiMap.linearUnion); the result becomes this store's deps."""
+        arr = (_Deps * len(parts))(*[p._device_view_c() for p in parts])
+        self._check(lib().accord_deps_union(self._h, len(parts), arr))
+
+    def slice(self, src: "CommandStore", sel_start, sel_end, sel_off=None):
+        """KeyDeps.slice + RangeDeps.slice of src's deps to (start, end] select ranges (shared, or
+        per txn with sel_off[n+1]); the result becomes this store's deps."""
+        v = src._device_view_c()
+        ss = np.ascontiguousarray(sel_start, dtype=np.uint32)
+        se = np.ascontiguousarray(sel_end, dtype=np.uint32)
+        so = None if sel_off is None else np.ascontiguousarray(sel_off, dtype=np.uint32)
+        self._check(lib().accord_deps_slice(self._h, C.byref(v), None if so is None else so.ctypes.data_as(_u32p),
+                                            ss.ctypes.data_as(_u32p), se.ctypes.data_as(_u32p), len(ss)))
+
+    def invert(self, src: "CommandStore"):
+        """txnIdsToKeys / txnIdsToRanges of src's deps (RelationMultiMap.invert):
+        (kd_off[n+1], kd_ints, rd_off[n+1], rd_ints)."""
+        v = src._device_view_c()
+        w = _Inverse()
+        self._check(lib().accord_deps_invert(self._h, C.byref(v), C.byref(w)))
+        try:
+            return (_arr(w.kd_t2k_off, w.n + 1, np.uint32), _arr(w.kd_t2k, w.kd_total, np.int32),
+                    _arr(w.rd_t2r_off, w.n + 1, np.uint32), _arr(w.rd_t2r, w.rd_total, np.int32))
+        finally:
+            lib().accord_deps_inverse_release(C.byref(w))
+
+    def upload_deps(self, p: "PartialDeps"):
+        """A host PartialDeps set becomes this store's current deps (e.g. replica replies)."""
+        keep = [np.ascontiguousarray(getattr(p, f)) for f in PartialDeps.FIELDS]
+        d = _Deps()
+        d.n = p.n
+        for f, a in zip(PartialDeps.FIELDS, keep):
+            setattr(d, f, a.ctypes.data_as(_i32p if a.dtype == np.int32 else _u32p))
+        d.kd_keys_total = int(p.kd_key_off[-1]); d.kd_vals_total = int(p.kd_val_off[-1])
+        d.kd_k2v_total = int(p.kd_k2v_off[-1]); d.rd_rngs_total = int(p.rd_rng_off[-1])
+        d.rd_vals_total = int(p.rd_val_off[-1]); d.rd_r2v_total = int(p.rd_r2v_off[-1])
+        self._check(lib().accord_deps_upload(self._h, C.byref(d)))
+
+    def ops_ms(self) -> float:
+        f = C.c_float()
+        self._check(lib().accord_ops_timing(self._h, C.byref(f)))
+        return f.value
 
     def waiting_on_compute(self):
         """WaitingOn bitsets + execution levels of the computed deps (device-resident)."""

@@ -1,0 +1,385 @@
+// C ABI of the deps-set operations (include/accord_deps.h: accord_deps_union / _slice / _invert;
+// SURVEY.md §8a a9, a10).  Host orchestration only: every pass runs in depset.hip on the store's
+// stream, with one host read of the sizes between count and fill passes.
+#include "store_impl.h"
+
+#include <cstring>
+#include <new>
+#include <vector>
+
+namespace {
+
+enum Tmp { T_VLEN, T_KLEN, T_BLEN, T_VEOFF, T_KEOFF, T_BEOFF, T_VOWN, T_VLST, T_KOWN, T_KLST, T_CNTV, T_CNTK,
+           T_VRANK, T_KRANK, T_RB, T_BOWN, T_BTOT, T_BSZ, T_BSCAN, T_PTRS, T_SCAN, T_TOT, T_SEL0, T_SEL1 };
+
+struct SideView {   // one side of one host-described device view
+    const uint32_t *key_off, *lo, *hi, *val_off, *vals, *x_off;
+    const int32_t *x;
+};
+
+SideView side_of(const accord_deps &d, bool range)
+{
+    if (!range) return SideView{d.kd_key_off, d.kd_keys, nullptr, d.kd_val_off, d.kd_vals, d.kd_k2v_off, d.kd_k2v};
+    return SideView{d.rd_rng_off, d.rd_rng_start, d.rd_rng_end, d.rd_val_off, d.rd_vals, d.rd_r2v_off, d.rd_r2v};
+}
+
+// device pointer table of G views' side -> DsSide
+int32_t make_side(accord_store *s, const std::vector<SideView> &v, bool range, DevBuf &buf, accord::DsSide &S)
+{
+    const size_t G = v.size();
+    std::vector<const void *> tbl(7 * G);
+    for (size_t g = 0; g < G; ++g) {
+        if (!v[g].key_off || !v[g].val_off || !v[g].x_off)
+            return fail(s, ACCORD_ERR_ARG, "deps view %zu has no %s offsets", g, range ? "RangeDeps" : "KeyDeps");
+        tbl[0 * G + g] = v[g].key_off; tbl[1 * G + g] = v[g].lo; tbl[2 * G + g] = v[g].hi;
+        tbl[3 * G + g] = v[g].val_off; tbl[4 * G + g] = v[g].vals; tbl[5 * G + g] = v[g].x_off;
+        tbl[6 * G + g] = v[g].x;
+    }
+    HIPCHECK(s, buf.ensure(tbl.size() * sizeof(void *)));
+    HIPCHECK(s, hipMemcpyAsync(buf.p, tbl.data(), tbl.size() * sizeof(void *), hipMemcpyHostToDevice, s->stream));
+    const void *const *p = (const void *const *)buf.p;
+    S.key_off = (const uint32_t *const *)(p + 0 * G); S.lo = (const uint32_t *const *)(p + 1 * G);
+    S.hi = (const uint32_t *const *)(p + 2 * G); S.val_off = (const uint32_t *const *)(p + 3 * G);
+    S.vals = (const uint32_t *const *)(p + 4 * G); S.x_off = (const uint32_t *const *)(p + 5 * G);
+    S.x = (const int32_t *const *)(p + 6 * G);
+    S.G = (uint32_t)G;
+    S.range = range;
+    return ACCORD_OK;
+}
+
+// exclusive scans with their totals read back in one sync
+struct Scans {
+    accord_store *s;
+    int k = 0;
+    unsigned long long *dev;
+    int32_t add(const uint32_t *in, uint32_t *out, uint32_t n)
+    {
+        HIPCHECK(s, s->op_tmp[T_SCAN].ensure(accord::scan_temp_bytes(n)));
+        accord::exclusive_scan_u32(in, out, n, dev + k++, s->op_tmp[T_SCAN].p, s->stream);
+        return ACCORD_OK;
+    }
+    int32_t read(unsigned long long *h)
+    {
+        HIPCHECK(s, hipMemcpyAsync(s->pinned->totals, dev, (size_t)k * 8, hipMemcpyDeviceToHost, s->stream));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+        for (int i = 0; i < k; ++i) h[i] = s->pinned->totals[i];
+        k = 0;
+        return ACCORD_OK;
+    }
+};
+
+int32_t scans_init(accord_store *s, Scans &sc)
+{
+    sc.s = s;
+    HIPCHECK(s, s->op_tmp[T_TOT].ensure(8 * 8));
+    sc.dev = s->op_tmp[T_TOT].as<unsigned long long>();
+    return ACCORD_OK;
+}
+
+#define RC(expr) do { int32_t rc_ = (expr); if (rc_) return rc_; } while (0)
+
+int32_t check_views(accord_store *s, uint32_t np, const accord_deps *parts)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (!parts || np == 0) return fail(s, ACCORD_ERR_ARG, "no deps sets");
+    for (uint32_t g = 1; g < np; ++g)
+        if (parts[g].n != parts[0].n) return fail(s, ACCORD_ERR_ARG, "deps sets cover different txn counts");
+    if ((uint64_t)parts[0].n + 1 >= (1ull << 31)) return fail(s, ACCORD_ERR_CAPACITY, "too many txns");
+    return ACCORD_OK;
+}
+
+// Union of one side of G parts into the given output buffers of `o`.
+int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool range, DepSet &o)
+{
+    const uint32_t n = parts[0].n;
+    const size_t nG = (size_t)n * G, n1 = (size_t)n + 1;
+    if (nG >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "union of %u x %u lists", n, G);
+    std::vector<SideView> v(G);
+    for (uint32_t g = 0; g < G; ++g) v[g] = side_of(parts[g], range);
+    accord::DsUnionParams p{};
+    p.n = n;
+    RC(make_side(s, v, range, s->op_tmp[T_PTRS], p.S));
+    DevBuf *T = s->op_tmp;
+    for (int b : {T_VLEN, T_KLEN, T_BLEN, T_VLST, T_KLST, T_BTOT}) HIPCHECK(s, T[b].ensure(nG * 4 + 4));
+    for (int b : {T_VEOFF, T_KEOFF, T_BEOFF}) HIPCHECK(s, T[b].ensure(nG * 4 + 4));
+    HIPCHECK(s, T[T_CNTV].ensure(n1 * 4)); HIPCHECK(s, T[T_CNTK].ensure(n1 * 4));
+    p.vlen = T[T_VLEN].as<uint32_t>(); p.klen = T[T_KLEN].as<uint32_t>(); p.blen = T[T_BLEN].as<uint32_t>();
+    p.veoff = T[T_VEOFF].as<uint32_t>(); p.keoff = T[T_KEOFF].as<uint32_t>(); p.beoff = T[T_BEOFF].as<uint32_t>();
+    Scans sc;
+    RC(scans_init(s, sc));
+    accord::launch_union_lens(p, s->stream);
+    RC(sc.add(p.vlen, T[T_VEOFF].as<uint32_t>(), (uint32_t)nG));
+    RC(sc.add(p.klen, T[T_KEOFF].as<uint32_t>(), (uint32_t)nG));
+    RC(sc.add(p.blen, T[T_BEOFF].as<uint32_t>(), (uint32_t)nG));
+    unsigned long long tot[3];
+    RC(sc.read(tot));
+    const uint64_t V = tot[0], K = tot[1], B = tot[2];
+    if (V >= (1ull << 32) || K >= (1ull << 32) || B >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "union input over 2^32 elements");
+    HIPCHECK(s, T[T_VOWN].ensure(V * 4 + 4)); HIPCHECK(s, T[T_VRANK].ensure(V * 4 + 4));
+    HIPCHECK(s, T[T_KOWN].ensure(K * 4 + 4)); HIPCHECK(s, T[T_KRANK].ensure(K * 4 + 4));
+    HIPCHECK(s, T[T_RB].ensure(B * 4 + 4)); HIPCHECK(s, T[T_BOWN].ensure(B * 4 + 4));
+    p.vown = T[T_VOWN].as<uint32_t>(); p.vlst = T[T_VLST].as<uint32_t>();
+    p.kown = T[T_KOWN].as<uint32_t>(); p.klst = T[T_KLST].as<uint32_t>();
+    p.cnt_vals = T[T_CNTV].as<uint32_t>(); p.cnt_keys = T[T_CNTK].as<uint32_t>();
+    accord::launch_union_owners(p, s->stream);
+    DevBuf &key_off = range ? o.rng_off : o.key_off, &val_off = range ? o.rval_off : o.val_off, &x_off = range ? o.r_off : o.x_off;
+    HIPCHECK(s, key_off.ensure(n1 * 4)); HIPCHECK(s, val_off.ensure(n1 * 4)); HIPCHECK(s, x_off.ensure(n1 * 4));
+    RC(sc.add(p.cnt_vals, val_off.as<uint32_t>(), n));
+    RC(sc.add(p.cnt_keys, key_off.as<uint32_t>(), n));
+    RC(sc.read(tot));
+    const uint64_t UV = tot[0], UK = tot[1];
+    DevBuf &lo = range ? o.rng_start : o.keys, &vals = range ? o.rvals : o.vals, &x = range ? o.r : o.x;
+    HIPCHECK(s, lo.ensure(UK * 4 + 4)); HIPCHECK(s, vals.ensure(UV * 4 + 4));
+    if (range) HIPCHECK(s, o.rng_end.ensure(UK * 4 + 4));
+    HIPCHECK(s, T[T_BSZ].ensure(UK * 4 + 4)); HIPCHECK(s, T[T_BSCAN].ensure(UK * 4 + 8));
+    HIPCHECK(s, hipMemsetAsync(T[T_BSZ].p, 0, UK * 4 + 4, s->stream));
+    p.out_val_off = val_off.as<uint32_t>(); p.out_key_off = key_off.as<uint32_t>();
+    p.vrank = T[T_VRANK].as<uint32_t>(); p.krank = T[T_KRANK].as<uint32_t>(); p.rb = T[T_RB].as<uint32_t>();
+    p.bown = T[T_BOWN].as<uint32_t>(); p.btot = T[T_BTOT].as<uint32_t>(); p.bsz = T[T_BSZ].as<uint32_t>();
+    p.out_vals = vals.as<uint32_t>(); p.out_lo = lo.as<uint32_t>(); p.out_hi = range ? o.rng_end.as<uint32_t>() : nullptr;
+    accord::launch_union_ranks(p, s->stream);
+    RC(sc.add(p.bsz, T[T_BSCAN].as<uint32_t>(), (uint32_t)UK));
+    RC(sc.read(tot));
+    const uint64_t UB = tot[0];
+    HIPCHECK(s, x.ensure((UK + UB) * 4 + 4));
+    p.bscan = T[T_BSCAN].as<uint32_t>();
+    p.out_x_off = x_off.as<uint32_t>(); p.out_x = x.as<int32_t>();
+    if (n == 0) HIPCHECK(s, hipMemsetAsync(x_off.p, 0, 4, s->stream));
+    accord::launch_union_write(p, s->stream);
+    HIPCHECK(s, hipGetLastError());
+    if (range) { o.tot_rngs = UK; o.tot_rvals = UV; o.tot_r = UK + UB; }
+    else { o.tot_keys = UK; o.tot_vals = UV; o.tot_x = UK + UB; }
+    return ACCORD_OK;
+}
+
+int32_t slice_side(accord_store *s, const accord_deps &src, bool range, const uint32_t *d_sel_off,
+                   const uint32_t *d_ss, const uint32_t *d_se, uint32_t nsel, DepSet &o)
+{
+    const uint32_t n = src.n;
+    const size_t n1 = (size_t)n + 1;
+    const uint64_t K = range ? src.rd_rngs_total : src.kd_keys_total, V = range ? src.rd_vals_total : src.kd_vals_total;
+    accord::DsSliceParams p{};
+    p.n = n;
+    std::vector<SideView> v{side_of(src, range)};
+    RC(make_side(s, v, range, s->op_tmp[T_PTRS], p.S));
+    DevBuf *T = s->op_tmp;
+    HIPCHECK(s, T[T_KRANK].ensure(K * 4 + 4));          // ksel
+    HIPCHECK(s, T[T_VLST].ensure(n1 * 4));              // mode
+    HIPCHECK(s, T[T_CNTK].ensure(n1 * 4)); HIPCHECK(s, T[T_CNTV].ensure(n1 * 4)); HIPCHECK(s, T[T_KLST].ensure(n1 * 4));
+    HIPCHECK(s, T[T_VOWN].ensure(V * 4 + 4));           // used
+    HIPCHECK(s, T[T_VRANK].ensure(V * 4 + 4));          // remap
+    HIPCHECK(s, hipMemsetAsync(T[T_VOWN].p, 0, V * 4 + 4, s->stream));
+    p.sel_off = d_sel_off; p.sel_start = d_ss; p.sel_end = d_se; p.nsel = nsel;
+    p.ksel = T[T_KRANK].as<uint32_t>(); p.mode = T[T_VLST].as<uint32_t>();
+    p.cnt_keys = T[T_CNTK].as<uint32_t>(); p.cnt_vals = T[T_CNTV].as<uint32_t>(); p.cnt_x = T[T_KLST].as<uint32_t>();
+    p.used = T[T_VOWN].as<uint32_t>(); p.remap = T[T_VRANK].as<uint32_t>();
+    accord::launch_slice_select(p, s->stream);
+    DevBuf &key_off = range ? o.rng_off : o.key_off, &val_off = range ? o.rval_off : o.val_off, &x_off = range ? o.r_off : o.x_off;
+    HIPCHECK(s, key_off.ensure(n1 * 4)); HIPCHECK(s, val_off.ensure(n1 * 4)); HIPCHECK(s, x_off.ensure(n1 * 4));
+    Scans sc;
+    RC(scans_init(s, sc));
+    RC(sc.add(p.cnt_keys, key_off.as<uint32_t>(), n));
+    RC(sc.add(p.cnt_vals, val_off.as<uint32_t>(), n));
+    RC(sc.add(p.cnt_x, x_off.as<uint32_t>(), n));
+    unsigned long long tot[3];
+    RC(sc.read(tot));
+    DevBuf &lo = range ? o.rng_start : o.keys, &vals = range ? o.rvals : o.vals, &x = range ? o.r : o.x;
+    HIPCHECK(s, lo.ensure(tot[0] * 4 + 4)); HIPCHECK(s, vals.ensure(tot[1] * 4 + 4)); HIPCHECK(s, x.ensure(tot[2] * 4 + 4));
+    if (range) HIPCHECK(s, o.rng_end.ensure(tot[0] * 4 + 4));
+    p.out_key_off = key_off.as<uint32_t>(); p.out_val_off = val_off.as<uint32_t>(); p.out_x_off = x_off.as<uint32_t>();
+    p.out_lo = lo.as<uint32_t>(); p.out_hi = range ? o.rng_end.as<uint32_t>() : nullptr;
+    p.out_vals = vals.as<uint32_t>(); p.out_x = x.as<int32_t>();
+    accord::launch_slice_write(p, s->stream);
+    HIPCHECK(s, hipGetLastError());
+    if (range) { o.tot_rngs = tot[0]; o.tot_rvals = tot[1]; o.tot_r = tot[2]; }
+    else { o.tot_keys = tot[0]; o.tot_vals = tot[1]; o.tot_x = tot[2]; }
+    return ACCORD_OK;
+}
+
+void op_begin(accord_store *s)
+{
+    if (s->events) (void)hipEventRecord(s->ev[EV_OP_START], s->stream);
+}
+int32_t op_end(accord_store *s)
+{
+    if (s->events) {
+        (void)hipEventRecord(s->ev[EV_OP_END], s->stream);
+        (void)hipEventSynchronize(s->ev[EV_OP_END]);
+        (void)hipEventElapsedTime(&s->ops_ms, s->ev[EV_OP_START], s->ev[EV_OP_END]);
+    }
+    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    return ACCORD_OK;
+}
+
+DepSet &next_set(accord_store *s)
+{
+    return s->ds[s->ds_cur == 0 ? 1 : 0];
+}
+
+void publish(accord_store *s, DepSet &o, uint32_t n)
+{
+    o.n = n;
+    s->ds_cur = (&o == &s->ds[0]) ? 0 : 1;
+    s->computed = true;
+    s->wo_done = false;
+}
+
+struct InverseOwner {
+    std::vector<uint32_t> koff, roff;
+    std::vector<int32_t> k, r;
+};
+
+} // namespace
+
+extern "C" {
+
+int32_t accord_deps_union(accord_store *s, uint32_t nparts, const accord_deps *parts)
+{
+    RC(check_views(s, nparts, parts));
+    if (nparts > 64) return fail(s, ACCORD_ERR_CAPACITY, "union of %u sets (1..64 supported)", nparts);
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    op_begin(s);
+    DepSet &o = next_set(s);
+    RC(union_side(s, parts, nparts, false, o));
+    RC(union_side(s, parts, nparts, true, o));
+    RC(op_end(s));
+    publish(s, o, parts[0].n);
+    return ACCORD_OK;
+}
+
+int32_t accord_deps_slice(accord_store *s, const accord_deps *src, const uint32_t *sel_off, const uint32_t *sel_start,
+                          const uint32_t *sel_end, uint32_t nsel)
+{
+    RC(check_views(s, 1, src));
+    const uint32_t n = src->n;
+    const uint64_t total = sel_off ? sel_off[n] : nsel;
+    if (total && (!sel_start || !sel_end)) return fail(s, ACCORD_ERR_ARG, "select ranges without bounds");
+    if (sel_off && sel_off[0] != 0) return fail(s, ACCORD_ERR_ARG, "select CSR must start at 0");
+    // Ranges invariants (AbstractRanges.sortAndDeoverlap): non-empty, sorted, de-overlapped
+    for (uint32_t t = 0; t < (sel_off ? n : 1); ++t) {
+        const uint64_t a = sel_off ? sel_off[t] : 0, b = sel_off ? sel_off[t + 1] : nsel;
+        if (b < a) return fail(s, ACCORD_ERR_ARG, "select CSR offsets decrease at txn %u", t);
+        for (uint64_t q = a; q < b; ++q) {
+            if (sel_start[q] >= sel_end[q]) return fail(s, ACCORD_ERR_RANGES, "empty select range (%u,%u]", sel_start[q], sel_end[q]);
+            if (q > a && sel_start[q] < sel_end[q - 1]) return fail(s, ACCORD_ERR_RANGES, "select ranges not sorted/de-overlapped");
+        }
+    }
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    op_begin(s);
+    DevBuf *T = s->op_tmp;
+    HIPCHECK(s, T[T_SEL0].ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, T[T_SEL1].ensure(total * 8 + 8));
+    uint32_t *d_off = sel_off ? T[T_SEL0].as<uint32_t>() : nullptr;
+    uint32_t *d_ss = T[T_SEL1].as<uint32_t>(), *d_se = d_ss + total;
+    if (sel_off) HIPCHECK(s, hipMemcpyAsync(d_off, sel_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
+    if (total) {
+        HIPCHECK(s, hipMemcpyAsync(d_ss, sel_start, total * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(d_se, sel_end, total * 4, hipMemcpyHostToDevice, s->stream));
+    }
+    DepSet &o = next_set(s);
+    RC(slice_side(s, *src, false, d_off, d_ss, d_se, nsel, o));
+    RC(slice_side(s, *src, true, d_off, d_ss, d_se, nsel, o));
+    RC(op_end(s));
+    publish(s, o, n);
+    return ACCORD_OK;
+}
+
+int32_t accord_deps_invert(accord_store *s, const accord_deps *src, accord_deps_inverse *out)
+{
+    RC(check_views(s, 1, src));
+    if (!out) return fail(s, ACCORD_ERR_ARG, "null output");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    const uint32_t n = src->n;
+    InverseOwner *own = new (std::nothrow) InverseOwner();
+    if (!own) return fail(s, ACCORD_ERR_OOM, "out of host memory");
+    op_begin(s);
+    int32_t rc = ACCORD_OK;
+    for (int side = 0; side < 2 && rc == ACCORD_OK; ++side) {
+        const bool range = side == 1;
+        const uint64_t total = range ? src->rd_vals_total + src->rd_r2v_total - src->rd_rngs_total
+                                     : src->kd_vals_total + src->kd_k2v_total - src->kd_keys_total;
+        const uint64_t V = range ? src->rd_vals_total : src->kd_vals_total;
+        accord::DsInvertParams p{};
+        p.n = n;
+        std::vector<SideView> v{side_of(*src, range)};
+        if ((rc = make_side(s, v, range, s->op_tmp[T_PTRS], p.S))) break;
+        DevBuf *T = s->op_tmp;
+        hipError_t e = T[T_VLEN].ensure(((size_t)n + 1) * 4);
+        if (e == hipSuccess) e = T[T_RB].ensure(total * 4 + 4);
+        if (e == hipSuccess) e = T[T_VRANK].ensure(V * 4 + 4);
+        if (e == hipSuccess) e = hipMemsetAsync(T[T_RB].p, 0, total * 4 + 4, s->stream);
+        if (e != hipSuccess) { rc = fail(s, ACCORD_ERR_HIP, "invert: %s", hipGetErrorString(e)); break; }
+        p.out_off = T[T_VLEN].as<uint32_t>(); p.out = T[T_RB].as<int32_t>(); p.cursor = T[T_VRANK].as<uint32_t>();
+        accord::launch_invert(p, s->stream);
+        std::vector<uint32_t> &ho = range ? own->roff : own->koff;
+        std::vector<int32_t> &hv = range ? own->r : own->k;
+        try { ho.resize((size_t)n + 1); hv.resize(total + 1); } catch (...) { rc = fail(s, ACCORD_ERR_OOM, "out of host memory"); break; }
+        e = hipMemcpyAsync(ho.data(), p.out_off, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s->stream);
+        if (e == hipSuccess && total) e = hipMemcpyAsync(hv.data(), p.out, total * 4, hipMemcpyDeviceToHost, s->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e != hipSuccess) rc = fail(s, ACCORD_ERR_HIP, "invert: %s", hipGetErrorString(e));
+        if (range) out->rd_total = total; else out->kd_total = total;
+    }
+    if (rc == ACCORD_OK) rc = op_end(s);
+    if (rc != ACCORD_OK) { delete own; return rc; }
+    out->n = n;
+    out->kd_t2k_off = own->koff.data(); out->kd_t2k = own->k.data();
+    out->rd_t2r_off = own->roff.data(); out->rd_t2r = own->r.data();
+    out->owner = own;
+    return ACCORD_OK;
+}
+
+int32_t accord_deps_upload(accord_store *s, const accord_deps *h)
+{
+    RC(check_views(s, 1, h));
+    const uint32_t n = h->n;
+    const size_t n1 = (size_t)n + 1;
+    if (!h->kd_key_off || !h->kd_val_off || !h->kd_k2v_off || !h->rd_rng_off || !h->rd_val_off || !h->rd_r2v_off)
+        return fail(s, ACCORD_ERR_ARG, "accord_deps_upload: missing offsets");
+    const uint32_t *offs[6] = {h->kd_key_off, h->kd_val_off, h->kd_k2v_off, h->rd_rng_off, h->rd_val_off, h->rd_r2v_off};
+    const uint64_t tots[6] = {h->kd_keys_total, h->kd_vals_total, h->kd_k2v_total, h->rd_rngs_total, h->rd_vals_total, h->rd_r2v_total};
+    for (int a = 0; a < 6; ++a) {
+        if (offs[a][0] != 0 || offs[a][n] != tots[a]) return fail(s, ACCORD_ERR_ARG, "accord_deps_upload: offsets/totals mismatch");
+        for (uint32_t t = 0; t < n; ++t)
+            if (offs[a][t + 1] < offs[a][t]) return fail(s, ACCORD_ERR_ARG, "accord_deps_upload: offsets decrease at txn %u", t);
+    }
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    DepSet &o = next_set(s);
+    struct { DevBuf *d; const void *src; size_t bytes; } cp[] = {
+        {&o.key_off, h->kd_key_off, n1 * 4}, {&o.keys, h->kd_keys, h->kd_keys_total * 4},
+        {&o.val_off, h->kd_val_off, n1 * 4}, {&o.vals, h->kd_vals, h->kd_vals_total * 4},
+        {&o.x_off, h->kd_k2v_off, n1 * 4}, {&o.x, h->kd_k2v, h->kd_k2v_total * 4},
+        {&o.rng_off, h->rd_rng_off, n1 * 4}, {&o.rng_start, h->rd_rng_start, h->rd_rngs_total * 4},
+        {&o.rng_end, h->rd_rng_end, h->rd_rngs_total * 4}, {&o.rval_off, h->rd_val_off, n1 * 4},
+        {&o.rvals, h->rd_vals, h->rd_vals_total * 4}, {&o.r_off, h->rd_r2v_off, n1 * 4},
+        {&o.r, h->rd_r2v, h->rd_r2v_total * 4}};
+    for (auto &c : cp) {
+        HIPCHECK(s, c.d->ensure(c.bytes + 4));
+        if (c.bytes) {
+            if (!c.src) return fail(s, ACCORD_ERR_ARG, "accord_deps_upload: null data array");
+            HIPCHECK(s, hipMemcpyAsync(c.d->p, c.src, c.bytes, hipMemcpyHostToDevice, s->stream));
+        }
+    }
+    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    o.tot_keys = h->kd_keys_total; o.tot_vals = h->kd_vals_total; o.tot_x = h->kd_k2v_total;
+    o.tot_rngs = h->rd_rngs_total; o.tot_rvals = h->rd_vals_total; o.tot_r = h->rd_r2v_total;
+    publish(s, o, n);
+    return ACCORD_OK;
+}
+
+void accord_deps_inverse_release(accord_deps_inverse *inv)
+{
+    if (!inv) return;
+    delete (InverseOwner *)inv->owner;
+    std::memset(inv, 0, sizeof(*inv));
+}
+
+int32_t accord_ops_timing(accord_store *s, float *ms)
+{
+    if (!s || !ms) return fail(s, ACCORD_ERR_ARG, "null argument");
+    *ms = s->ops_ms;
+    return ACCORD_OK;
+}
+
+} // extern "C"

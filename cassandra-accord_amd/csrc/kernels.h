@@ -165,6 +165,57 @@ void launch_expand_offsets(uint32_t n, uint32_t n_total, const uint32_t *txn_ind
 void launch_boundaries(uint32_t G, uint32_t n_total, uint32_t *const exp_off[3], uint32_t *bnd, hipStream_t s);
 void launch_merge_fill(const MergeParams &p, hipStream_t s);
 
+// ---- deps-set operations: union / slice / invert (depset.hip) ----
+// One side (KeyDeps: lo = key ordinals, hi unused; RangeDeps: ranges (lo, hi]) of G device deps
+// sets, as device pointer tables indexed by part.  Offsets may start anywhere (element g of a
+// data array is at index off[t] - off[0]).
+struct DsSide {
+    const uint32_t *const *key_off, *const *lo, *const *hi, *const *val_off, *const *vals, *const *x_off;
+    const int32_t *const *x;
+    uint32_t G;
+    bool range;
+};
+struct DsUnionParams {
+    uint32_t n;
+    DsSide S;
+    uint32_t *vlen, *klen, *blen;                   // per (txn, part)
+    const uint32_t *veoff, *keoff, *beoff;          // element scratch offsets per (txn, part)
+    uint32_t *vown, *vlst, *kown, *klst;            // owner prefixes / owners per list
+    uint32_t *cnt_vals, *cnt_keys;                  // union sizes per txn
+    const uint32_t *out_val_off, *out_key_off;
+    uint32_t *vrank, *krank, *rb, *bown, *btot, *bsz;
+    const uint32_t *bscan;                          // exclusive scan of bsz (union keys + 1)
+    uint32_t *out_vals, *out_lo, *out_hi, *out_x_off;
+    int32_t *out_x;
+};
+struct DsSliceParams {
+    uint32_t n;
+    DsSide S;                                       // G = 1
+    const uint32_t *sel_off, *sel_start, *sel_end;  // device; sel_off null = nsel shared ranges
+    uint32_t nsel;
+    uint32_t *ksel, *mode, *cnt_keys, *cnt_vals, *cnt_x, *used, *remap;
+    const uint32_t *out_key_off, *out_val_off, *out_x_off;
+    uint32_t *out_lo, *out_hi, *out_vals;
+    int32_t *out_x;
+};
+struct DsInvertParams {
+    uint32_t n;
+    DsSide S;                                       // G = 1
+    uint32_t *out_off;                              // [n+1]
+    int32_t *out;                                   // zeroed before the launch
+    uint32_t *cursor;                               // per txnId element
+};
+// union: lens -> (scan veoff/keoff/beoff) -> owners -> (scan union sizes) -> ranks + body owners +
+// body sizes (bsz zeroed) -> (scan bsz) -> write
+void launch_union_lens(const DsUnionParams &p, hipStream_t s);
+void launch_union_owners(const DsUnionParams &p, hipStream_t s);
+void launch_union_ranks(const DsUnionParams &p, hipStream_t s);
+void launch_union_write(const DsUnionParams &p, hipStream_t s);
+// slice: select + mark (used zeroed) + counts -> (scans) -> write
+void launch_slice_select(const DsSliceParams &p, hipStream_t s);
+void launch_slice_write(const DsSliceParams &p, hipStream_t s);
+void launch_invert(const DsInvertParams &p, hipStream_t s);
+
 // ---- WaitingOn bitsets + execution levelling (waiting_on.hip) ----
 struct WaitingOnParams {
     uint32_t n;

@@ -116,6 +116,7 @@ int32_t merge_parts(accord_store *s, const std::vector<Part> &parts, uint32_t n,
     s->m_n = n;
     s->m_txn_lo = txn_lo;
     s->merged = true;
+    s->ds_cur = -1;
     s->wo_done = false;
     s->computed = true;
     return ACCORD_OK;

@@ -111,6 +111,8 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->level, &s->wo_info, &s->lv_tmp};
     accord_impl::shard_comm_destroy(s);
     for (DevBuf *b : bufs) b->release();
+    for (DepSet &d : s->ds) d.release();
+    for (DevBuf &b : s->op_tmp) b.release();
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventDestroy(ev);
     if (s->pinned) (void)hipHostFree(s->pinned);
@@ -159,7 +161,7 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     if (s->rk_keys_total >= (1ull << 32))
         return fail(s, ACCORD_ERR_CAPACITY, "range txns cover %llu (txn, key) pairs, over 2^32",
                     (unsigned long long)s->rk_keys_total);
-    s->has_batch = false; s->computed = false; s->merged = false;
+    s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
     HIPCHECK(s, s->node.ensure((size_t)n * 4));
@@ -204,6 +206,7 @@ int32_t accord_deps_compute(accord_store *s)
     hipStream_t st = s->stream;
     s->computed = false;
     s->merged = false;
+    s->ds_cur = -1;
     s->wo_done = false;
 
     HIPCHECK(s, s->pair_key.ensure((size_t)P * 4));
@@ -447,6 +450,19 @@ int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
     if (!s || !d) return fail(s, ACCORD_ERR_ARG, "null argument");
     if (!s->computed) return fail(s, ACCORD_ERR_STATE, "no computed deps");
     std::memset(d, 0, sizeof(*d));
+    if (s->ds_cur >= 0) {
+        const DepSet &x = s->ds[s->ds_cur];
+        d->n = x.n;
+        d->kd_keys_total = x.tot_keys; d->kd_vals_total = x.tot_vals; d->kd_k2v_total = x.tot_x;
+        d->rd_rngs_total = x.tot_rngs; d->rd_vals_total = x.tot_rvals; d->rd_r2v_total = x.tot_r;
+        d->kd_key_off = x.key_off.as<uint32_t>(); d->kd_keys = x.keys.as<uint32_t>();
+        d->kd_val_off = x.val_off.as<uint32_t>(); d->kd_vals = x.vals.as<uint32_t>();
+        d->kd_k2v_off = x.x_off.as<uint32_t>(); d->kd_k2v = x.x.as<int32_t>();
+        d->rd_rng_off = x.rng_off.as<uint32_t>(); d->rd_rng_start = x.rng_start.as<uint32_t>();
+        d->rd_rng_end = x.rng_end.as<uint32_t>(); d->rd_val_off = x.rval_off.as<uint32_t>();
+        d->rd_vals = x.rvals.as<uint32_t>(); d->rd_r2v_off = x.r_off.as<uint32_t>(); d->rd_r2v = x.r.as<int32_t>();
+        return ACCORD_OK;
+    }
     if (s->merged) {
         d->n = s->m_n;
         d->kd_keys_total = s->m_tot_keys; d->kd_vals_total = s->m_tot_vals; d->kd_k2v_total = s->m_tot_k2v;

@@ -35,13 +35,27 @@ struct HostTotals {
                                     // kd vals
 };
 
+// A device-resident PartialDeps set (result of accord_deps_union / accord_deps_slice).
+struct DepSet {
+    uint32_t n = 0;
+    DevBuf key_off, keys, val_off, vals, x_off, x;                      // KeyDeps
+    DevBuf rng_off, rng_start, rng_end, rval_off, rvals, r_off, r;      // RangeDeps
+    uint64_t tot_keys = 0, tot_vals = 0, tot_x = 0, tot_rngs = 0, tot_rvals = 0, tot_r = 0;
+    void release()
+    {
+        DevBuf *b[] = {&key_off, &keys, &val_off, &vals, &x_off, &x, &rng_off, &rng_start, &rng_end, &rval_off, &rvals, &r_off, &r};
+        for (DevBuf *p : b) p->release();
+    }
+};
+
 } // namespace accord_impl
 using accord_impl::DevBuf;
+using accord_impl::DepSet;
 using accord_impl::HostTotals;
 
 enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_RANGE, EV_COMPACT,
              EV_XCHG_START, EV_XCHG_END, EV_MERGE_END, EV_WO_START, EV_WO_BITS, EV_WO_PREDS, EV_WO_LEVEL,
-             EV_COUNT_ALL };
+             EV_OP_START, EV_OP_END, EV_COUNT_ALL };
 
 struct ShardComm;   // RCCL communicator + exchange buffers (shard.cpp)
 
@@ -79,6 +93,12 @@ struct accord_store {
     uint64_t wo_words_total = 0, preds_total = 0;
     uint32_t max_level = 0;
     float wo_ms[3] = {0, 0, 0};
+    // deps-set operations (depset_abi.cpp): results double-buffered so an op may read the current
+    // set; ds_cur >= 0 makes ds[ds_cur] the store's current deps
+    DepSet ds[2];
+    int ds_cur = -1;
+    DevBuf op_tmp[24];
+    float ops_ms = 0;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
     hipEvent_t ev[EV_COUNT_ALL] = {};

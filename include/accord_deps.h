@@ -144,6 +144,51 @@ int32_t accord_comm_init(accord_store *store, int32_t nranks, int32_t rank, cons
 int32_t accord_deps_exchange_merge(accord_store *store, uint32_t n_total);
 int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merge_ms);
 
+/* ---- deps-set operations on device ----
+ * Sources are device views (accord_deps_device_view) of stores on this store's device; the values
+ * of all sources index the same TxnId table sorted ascending (the batch / stream), so TxnId order
+ * is index order.  union and slice make their result this store's current deps (read it with
+ * accord_deps_device_view / accord_deps_download; a source may be this store's own current deps).
+ *
+ * accord_deps_union: Deps.merge / PartialDeps.with of nparts (1..64) sets of the same n txns, KeyDeps
+ *   and RangeDeps, keys may overlap -- RelationMultiMap.linearUnion (utils/RelationMultiMap.java:
+ *   561-816) via KeyDeps.merge (primitives/KeyDeps.java:115-140) / RangeDeps.merge
+ *   (primitives/RangeDeps.java:101-126): the coordinator-side merge of replica replies
+ *   (coordinate/CoordinateTransaction.java:75,81) and the general PreAccept.reduce. */
+int32_t accord_deps_union(accord_store *store, uint32_t nparts, const accord_deps *parts);
+
+/* accord_deps_upload: a host PartialDeps set (e.g. the replies a coordinator received, decoded with
+ *   KeyDeps/RangeDeps.SerializerSupport) becomes this store's current deps (H2D copy, sync). */
+int32_t accord_deps_upload(accord_store *store, const accord_deps *host);
+
+/* accord_deps_slice: KeyDeps.slice (primitives/KeyDeps.java:189-236) and RangeDeps.slice
+ *   (primitives/RangeDeps.java:545-565, incl. trimUnusedValues, utils/RelationMultiMap.java:491-532)
+ *   of every txn of src to Ranges: (sel_start, sel_end] sorted and de-overlapped, host pointers;
+ *   sel_off[n+1] gives each txn its own ranges, or sel_off == NULL applies the same nsel ranges to
+ *   every txn (Accept/Commit message construction per destination shard, messages/Accept.java:65-72). */
+int32_t accord_deps_slice(accord_store *store, const accord_deps *src, const uint32_t *sel_off,
+                          const uint32_t *sel_start, const uint32_t *sel_end, uint32_t nsel);
+
+/* accord_deps_invert: txnIdsToKeys (KeyDeps.java:350-362) and txnIdsToRanges (RangeDeps.java:537-543)
+ *   of every txn of src -- RelationMultiMap.invert (utils/RelationMultiMap.java:907-938): per txn
+ *   |txnIds| end offsets (absolute, the first starting at |txnIds|), then per txnId its key (range)
+ *   indices ascending.  Computed on device, returned in host memory owned by the library. */
+typedef struct {
+    uint32_t  n;
+    uint32_t  reserved;
+    uint64_t  kd_total, rd_total;
+    uint32_t *kd_t2k_off;       /* [n+1] */
+    int32_t  *kd_t2k;           /* [kd_total] */
+    uint32_t *rd_t2r_off;       /* [n+1] */
+    int32_t  *rd_t2r;           /* [rd_total] */
+    void     *owner;            /* library-private */
+} accord_deps_inverse;
+
+int32_t accord_deps_invert(accord_store *store, const accord_deps *src, accord_deps_inverse *out);
+void    accord_deps_inverse_release(accord_deps_inverse *inv);
+/* device ms of the last union / slice / invert (ACCORD_STORE_PROFILE stores, else 0) */
+int32_t accord_ops_timing(accord_store *store, float *ms);
+
 /* ---- WaitingOn + execution levelling (config 5) ----
  * Over the store's current computed deps (full stream: no txn_index, not merged), with every txn
  * STABLE, executeAt = txnId and none applied:

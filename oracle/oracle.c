@@ -1043,3 +1043,346 @@ int or_waiting_on_events(const or_deps *d, uint32_t n, uint32_t *round_out)
     free(bits_left); free(radj_off); free(slot_left); free(rw); free(rs); free(fill); free(frontier); free(nextf);
     return done == n ? 0 : -7;   /* -7: a txn never became ready (cycle / missing dep) */
 }
+
+/* ==========================================================================================
+ * Deps-set operations over every txn of an or_deps set.
+ * Values are indices into one TxnId table sorted ascending (the stream the deps were computed
+ * from, whose order the stream drivers validate), so Timestamp.compareTo order == index order.
+ * Keys are u64 codes as in the builder: a key ordinal, or start<<32|end for a range (Range.compare
+ * order, Range.java:310-317).
+ * ========================================================================================== */
+
+typedef struct {
+    uint64_t *keys; uint32_t nk;
+    const uint32_t *vals; uint32_t nv;
+    const int32_t *k2v; uint32_t nx;        /* keysToValues: nk end offsets + body */
+} mm_view;
+
+static int view_of(const or_deps *d, uint32_t i, int range, mm_view *v)
+{
+    if (!range) {
+        v->nk = d->kd_key_off[i + 1] - d->kd_key_off[i];
+        v->vals = d->kd_vals + d->kd_val_off[i]; v->nv = d->kd_val_off[i + 1] - d->kd_val_off[i];
+        v->k2v = d->kd_k2v + d->kd_k2v_off[i]; v->nx = d->kd_k2v_off[i + 1] - d->kd_k2v_off[i];
+    } else {
+        v->nk = d->rd_rng_off[i + 1] - d->rd_rng_off[i];
+        v->vals = d->rd_vals + d->rd_val_off[i]; v->nv = d->rd_val_off[i + 1] - d->rd_val_off[i];
+        v->k2v = d->rd_r2v + d->rd_r2v_off[i]; v->nx = d->rd_r2v_off[i + 1] - d->rd_r2v_off[i];
+    }
+    v->keys = (uint64_t *)malloc(((size_t)v->nk + 1) * sizeof(uint64_t));
+    if (!v->keys) return -1;
+    for (uint32_t a = 0; a < v->nk; ++a)
+        v->keys[a] = range ? ((uint64_t)d->rd_rng_start[d->rd_rng_off[i] + a] << 32 | d->rd_rng_end[d->rd_rng_off[i] + a])
+                           : d->kd_keys[d->kd_key_off[i] + a];
+    return 0;
+}
+
+/* append one multimap (keys, vals, keysToValues verbatim) to o */
+static int mmo_emit(mm_out *o, int range, const uint64_t *keys, uint32_t nk, const uint32_t *vals, uint32_t nv,
+                    const int32_t *k2v, uint32_t nx)
+{
+    for (uint32_t a = 0; a < nk; ++a) {
+        if (u32v_push(&o->keys_lo, range ? (uint32_t)(keys[a] >> 32) : (uint32_t)keys[a])) return -1;
+        if (range && u32v_push(&o->keys_hi, (uint32_t)keys[a])) return -1;
+    }
+    for (uint32_t v = 0; v < nv; ++v) if (u32v_push(&o->vals, vals[v])) return -1;
+    for (uint32_t x = 0; x < nx; ++x) if (i32v_push(&o->k2v, k2v[x])) return -1;
+    return mmo_close_txn(o);
+}
+
+static uint32_t body_start(const int32_t *k2v, uint32_t nk, uint32_t a) { return a == 0 ? nk : (uint32_t)k2v[a - 1]; }
+
+/* RelationMultiMap.linearUnion (utils/RelationMultiMap.java:561-816) of two multimaps: values are
+ * SortedArrays.linearUnion'd (utils/SortedArrays.java:152-281, left wins on ties), keys are unioned
+ * in key order and each key's list is the union of both sides' indices remapped into the union
+ * (remapToSuperset, :1197-1223).  The pass-through branches (:583-730) return one input only when
+ * it already equals the union, so this is the value-level result in every case.  isEmpty() of
+ * either side returns the other (KeyDeps.with, KeyDeps.java:238-241; RangeDeps.with :567-570). */
+static int mm_union2(const mm_view *l, const mm_view *r, uint64_t **ok, uint32_t *onk, u32v *ov, i32v *ox)
+{
+    const mm_view *only = NULL;
+    if (l->nx == l->nk || r->nx == r->nk) only = l->nx == l->nk ? r : l;
+    ov->n = 0; ox->n = 0;
+    *ok = (uint64_t *)malloc(((size_t)l->nk + r->nk + 1) * sizeof(uint64_t));
+    if (!*ok) return -1;
+    if (only) {
+        memcpy(*ok, only->keys, (size_t)only->nk * sizeof(uint64_t)); *onk = only->nk;
+        for (uint32_t v = 0; v < only->nv; ++v) if (u32v_push(ov, only->vals[v])) return -1;
+        for (uint32_t x = 0; x < only->nx; ++x) if (i32v_push(ox, only->k2v[x])) return -1;
+        return 0;
+    }
+    uint32_t *rl = (uint32_t *)malloc(((size_t)l->nv + 1) * 4), *rr = (uint32_t *)malloc(((size_t)r->nv + 1) * 4);
+    i32v body = {0};
+    int rc = -1;
+    if (!rl || !rr) goto done;
+    {
+        uint32_t i = 0, j = 0, o = 0;
+        while (i < l->nv || j < r->nv) {
+            if (j == r->nv || (i < l->nv && l->vals[i] < r->vals[j])) { rl[i] = o; if (u32v_push(ov, l->vals[i++])) goto done; }
+            else if (i == l->nv || r->vals[j] < l->vals[i]) { rr[j] = o; if (u32v_push(ov, r->vals[j++])) goto done; }
+            else { rl[i] = rr[j] = o; if (u32v_push(ov, l->vals[i])) goto done; ++i; ++j; }
+            ++o;
+        }
+    }
+    {
+        uint32_t a = 0, b = 0, nk = 0;
+        uint32_t *hdr = (uint32_t *)malloc(((size_t)l->nk + r->nk + 1) * 4);
+        if (!hdr) goto done;
+        while (a < l->nk || b < r->nk) {
+            int which = a == l->nk ? 1 : b == r->nk ? -1 : (l->keys[a] < r->keys[b] ? -1 : l->keys[a] > r->keys[b] ? 1 : 0);
+            uint32_t lp = 0, le = 0, rp = 0, re = 0;
+            if (which <= 0) { lp = body_start(l->k2v, l->nk, a); le = (uint32_t)l->k2v[a]; }
+            if (which >= 0) { rp = body_start(r->k2v, r->nk, b); re = (uint32_t)r->k2v[b]; }
+            (*ok)[nk] = which <= 0 ? l->keys[a] : r->keys[b];
+            while (lp < le || rp < re) {
+                int32_t x = lp < le ? (int32_t)rl[l->k2v[lp]] : INT32_MAX, y = rp < re ? (int32_t)rr[r->k2v[rp]] : INT32_MAX;
+                if (x <= y) { if (i32v_push(&body, x)) { free(hdr); goto done; } ++lp; if (x == y) ++rp; }
+                else { if (i32v_push(&body, y)) { free(hdr); goto done; } ++rp; }
+            }
+            hdr[nk++] = (uint32_t)body.n;
+            if (which <= 0) ++a;
+            if (which >= 0) ++b;
+        }
+        *onk = nk;
+        for (uint32_t k = 0; k < nk; ++k) if (i32v_push(ox, (int32_t)(hdr[k] + nk))) { free(hdr); goto done; }
+        for (size_t x = 0; x < body.n; ++x) if (i32v_push(ox, body.p[x])) { free(hdr); goto done; }
+        free(hdr);
+    }
+    rc = 0;
+done:
+    free(rl); free(rr); free(body.p);
+    return rc;
+}
+
+/* Deps.merge / PartialDeps.with over G sets of the same n txns (KeyDeps.merge KeyDeps.java:115-140,
+ * RangeDeps.merge RangeDeps.java:101-126: a LinearMerger == left fold of linearUnion). */
+int or_deps_union(uint32_t G, const or_deps *parts, or_deps *out)
+{
+    if (G == 0) return -1;
+    const uint32_t n = parts[0].n;
+    mm_out kd, rd;
+    int rc = -1;
+    if (mmo_init(&kd) || mmo_init(&rd)) goto fail;
+    for (uint32_t i = 0; i < n; ++i) {
+        for (int range = 0; range < 2; ++range) {
+            mm_view acc;
+            if (view_of(&parts[0], i, range, &acc)) goto fail;
+            uint64_t *akeys = acc.keys;
+            u32v av = {0}; i32v ax = {0};
+            for (uint32_t v = 0; v < acc.nv; ++v) if (u32v_push(&av, acc.vals[v])) goto fail;
+            for (uint32_t x = 0; x < acc.nx; ++x) if (i32v_push(&ax, acc.k2v[x])) goto fail;
+            for (uint32_t g = 1; g < G; ++g) {
+                mm_view r, l = {akeys, acc.nk, av.p, (uint32_t)av.n, ax.p, (uint32_t)ax.n};
+                if (view_of(&parts[g], i, range, &r)) goto fail;
+                uint64_t *nkeys; uint32_t nnk; u32v nv = {0}; i32v nx = {0};
+                int e = mm_union2(&l, &r, &nkeys, &nnk, &nv, &nx);
+                free(r.keys);
+                if (e) goto fail;
+                free(akeys); free(av.p); free(ax.p);
+                akeys = nkeys; acc.nk = nnk; av = nv; ax = nx;
+            }
+            int e = mmo_emit(range ? &rd : &kd, range, akeys, acc.nk, av.p, (uint32_t)av.n, ax.p, (uint32_t)ax.n);
+            free(akeys); free(av.p); free(ax.p);
+            if (e) goto fail;
+        }
+    }
+    if (alloc_out(out, &kd, &rd, n)) goto fail;
+    rc = 0;
+fail:
+    mmo_free(&kd); mmo_free(&rd);
+    return rc;
+}
+
+/* trimUnusedValues (utils/RelationMultiMap.java:491-532): keep the values referenced by the body
+ * in their order, rewrite the body to the kept positions. */
+static int trim_and_emit(mm_out *o, int range, const uint64_t *keys, uint32_t nk, const uint32_t *vals, uint32_t nv,
+                         int32_t *k2v, uint32_t nx)
+{
+    int32_t *remap = (int32_t *)malloc(((size_t)nv + 1) * sizeof(int32_t));
+    uint32_t *kept = (uint32_t *)malloc(((size_t)nv + 1) * sizeof(uint32_t));
+    if (!remap || !kept) { free(remap); free(kept); return -1; }
+    for (uint32_t v = 0; v < nv; ++v) remap[v] = 0;
+    for (uint32_t x = nk; x < nx; ++x) remap[k2v[x]] = 1;
+    uint32_t m = 0;
+    for (uint32_t v = 0; v < nv; ++v) { if (remap[v]) { kept[m] = vals[v]; remap[v] = (int32_t)m++; } else remap[v] = -1; }
+    if (m < nv) for (uint32_t x = nk; x < nx; ++x) k2v[x] = remap[k2v[x]];
+    int e = mmo_emit(o, range, keys, nk, m < nv ? kept : vals, m < nv ? m : nv, k2v, nx);
+    free(remap); free(kept);
+    return e;
+}
+
+static int range_contains_key(uint32_t s, uint32_t e, uint64_t key) { return (uint64_t)s < key && key <= (uint64_t)e; }
+
+/* KeyDeps.slice (primitives/KeyDeps.java:189-236): keys.slice(ranges) keeps the keys inside the
+ * select ranges ((s,e] containment), copies their lists and trims unused txnIds; an empty KeyDeps,
+ * or a selection of every key, returns the input unchanged; no key selected gives the empty
+ * KeyDeps (no keys, no txnIds, no ints). */
+static int keydeps_slice_one(mm_out *o, const mm_view *v, const uint32_t *ss, const uint32_t *se, uint32_t ns)
+{
+    if (v->nx == v->nk) return mmo_emit(o, 0, v->keys, v->nk, v->vals, v->nv, v->k2v, v->nx);
+    uint64_t *sk = (uint64_t *)malloc(((size_t)v->nk + 1) * sizeof(uint64_t));
+    uint32_t *sa = (uint32_t *)malloc(((size_t)v->nk + 1) * sizeof(uint32_t));
+    if (!sk || !sa) { free(sk); free(sa); return -1; }
+    uint32_t m = 0;
+    for (uint32_t a = 0; a < v->nk; ++a)
+        for (uint32_t q = 0; q < ns; ++q)
+            if (range_contains_key(ss[q], se[q], v->keys[a])) { sk[m] = v->keys[a]; sa[m++] = a; break; }
+    int e;
+    if (m == 0) e = mmo_emit(o, 0, NULL, 0, NULL, 0, NULL, 0);
+    else if (m == v->nk) e = mmo_emit(o, 0, v->keys, v->nk, v->vals, v->nv, v->k2v, v->nx);
+    else {
+        uint32_t off = m;
+        for (uint32_t j = 0; j < m; ++j) off += (uint32_t)v->k2v[sa[j]] - body_start(v->k2v, v->nk, sa[j]);
+        int32_t *trg = (int32_t *)malloc(((size_t)off + 1) * sizeof(int32_t));
+        if (!trg) { free(sk); free(sa); return -1; }
+        off = m;
+        for (uint32_t j = 0; j < m; ++j) {
+            for (uint32_t x = body_start(v->k2v, v->nk, sa[j]); x < (uint32_t)v->k2v[sa[j]]; ++x) trg[off++] = v->k2v[x];
+            trg[j] = (int32_t)off;
+        }
+        e = trim_and_emit(o, 0, sk, m, v->vals, v->nv, trg, off);
+        free(trg);
+    }
+    free(sk); free(sa);
+    return e;
+}
+
+/* RangeDeps.slice (primitives/RangeDeps.java:545-565) with the RangeAndMapCollector
+ * (:727-848) driven by SearchableRangeList/CheckpointIntervalArray.forEach
+ * (utils/CheckpointIntervalArray.java:100-221) once per select range with the running minIndex
+ * (RangeDeps.java:192-197).  Per select range (qs, qe]:
+ *   end   = first index >= minIndex whose start >= qe (CEIL on start), nothing if end <= minIndex;
+ *   floor = CEIL(qs) on start within [minIndex, n) (exact: lowest equal start) or, if absent, the
+ *           insertion point - 1; start = floor, stepped forward once if that range ends <= qs;
+ *   the checkpoint + scan matches are {i in [minIndex, floor) : end_i > qs} (the match set the
+ *           checkpoint index guarantees: SearchableRangeListTest.java:98-112), buffered
+ *           out-of-order; the run [max(start,minIndex), end) is reported through forEachRange,
+ *           whose accept() first flushes the buffered matches (sorted) and then copies the run;
+ *   minIndex = end.
+ * Buffered matches are only flushed by a later non-empty run: matches still buffered after the
+ * last select range are dropped (collector has no final flush, RangeDeps.java:550-563).  The
+ * output ranges are ascending by index; all ranges selected returns the input unchanged. */
+static int rangedeps_slice_one(mm_out *o, const or_deps *d, uint32_t i, const mm_view *v,
+                               const uint32_t *ss, const uint32_t *se, uint32_t ns)
+{
+    const uint32_t n = v->nk;
+    const uint32_t *rs = d->rd_rng_start + d->rd_rng_off[i], *re = d->rd_rng_end + d->rd_rng_off[i];
+    if (v->nx == v->nk) return mmo_emit(o, 1, NULL, 0, v->vals, v->nv, NULL, 0);   /* RangeDeps(NO_RANGES, txnIds, NO_INTS) */
+    uint8_t *sel = (uint8_t *)calloc((size_t)n + 1, 1), *pend = (uint8_t *)calloc((size_t)n + 1, 1);
+    if (!sel || !pend) { free(sel); free(pend); return -1; }
+    uint32_t minIndex = 0;
+    for (uint32_t q = 0; q < ns; ++q) {
+        if (n == 0 || minIndex == n) continue;
+        uint32_t end = minIndex;
+        while (end < n && rs[end] < se[q]) ++end;            /* starts are ascending */
+        if (end <= minIndex) continue;
+        uint32_t ins = minIndex;
+        while (ins < n && rs[ins] < ss[q]) ++ins;
+        int64_t floor, start;
+        if (ins < n && rs[ins] == ss[q]) floor = start = ins;
+        else {
+            floor = start = (int64_t)ins - 1;
+            if (start < 0) start = floor = 0;
+            else if (re[start] <= ss[q]) ++start;
+        }
+        if (start < minIndex) start = minIndex;
+        for (int64_t x = minIndex; x < floor; ++x) if (re[x] > ss[q]) pend[x] = 1;
+        if ((uint32_t)start != end) {
+            for (uint32_t x = 0; x < n; ++x) if (pend[x] && x < (uint32_t)start) { sel[x] = 1; pend[x] = 0; }
+            for (uint32_t x = (uint32_t)start; x < end; ++x) sel[x] = 1;
+            memset(pend, 0, n);   /* buffered entries >= fromIndex are dropped (binarySearch cut) */
+        }
+        minIndex = end;
+    }
+    uint32_t m = 0;
+    for (uint32_t x = 0; x < n; ++x) m += sel[x];
+    int e;
+    if (m == 0) e = mmo_emit(o, 1, NULL, 0, NULL, 0, NULL, 0);
+    else if (m == n) e = mmo_emit(o, 1, v->keys, v->nk, v->vals, v->nv, v->k2v, v->nx);
+    else {
+        uint64_t *sk = (uint64_t *)malloc(((size_t)m + 1) * sizeof(uint64_t));
+        uint32_t off = m;
+        for (uint32_t x = 0; x < n; ++x) if (sel[x]) off += (uint32_t)v->k2v[x] - body_start(v->k2v, n, x);
+        int32_t *trg = (int32_t *)malloc(((size_t)off + 1) * sizeof(int32_t));
+        if (!sk || !trg) { free(sk); free(trg); free(sel); free(pend); return -1; }
+        uint32_t j = 0;
+        off = m;
+        for (uint32_t x = 0; x < n; ++x) {
+            if (!sel[x]) continue;
+            sk[j] = v->keys[x];
+            for (uint32_t y = body_start(v->k2v, n, x); y < (uint32_t)v->k2v[x]; ++y) trg[off++] = v->k2v[y];
+            trg[j++] = (int32_t)off;
+        }
+        e = trim_and_emit(o, 1, sk, m, v->vals, v->nv, trg, off);
+        free(sk); free(trg);
+    }
+    free(sel); free(pend);
+    return e;
+}
+
+int or_deps_slice(const or_deps *d, const uint32_t *sel_off, const uint32_t *sel_start, const uint32_t *sel_end,
+                  uint32_t nsel, or_deps *out)
+{
+    const uint32_t n = d->n;
+    mm_out kd, rd;
+    int rc = -1;
+    if (mmo_init(&kd) || mmo_init(&rd)) goto fail;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t q0 = sel_off ? sel_off[i] : 0, ns = sel_off ? sel_off[i + 1] - sel_off[i] : nsel;
+        mm_view v;
+        if (view_of(d, i, 0, &v)) goto fail;
+        int e = keydeps_slice_one(&kd, &v, sel_start + q0, sel_end + q0, ns);
+        free(v.keys);
+        if (e) goto fail;
+        if (view_of(d, i, 1, &v)) goto fail;
+        e = rangedeps_slice_one(&rd, d, i, &v, sel_start + q0, sel_end + q0, ns);
+        free(v.keys);
+        if (e) goto fail;
+    }
+    if (alloc_out(out, &kd, &rd, n)) goto fail;
+    rc = 0;
+fail:
+    mmo_free(&kd); mmo_free(&rd);
+    return rc;
+}
+
+/* RelationMultiMap.invert (utils/RelationMultiMap.java:907-938) of every txn's keysToTxnIds
+ * (range = 0) or rangesToTxnIds (range = 1): txnIdsToKeys with |txnIds| end offsets (absolute,
+ * first starting at |txnIds|) then, per txnId, its key indices ascending.  off[n+1] (caller) and
+ * *out (malloc'd). */
+int or_deps_invert(const or_deps *d, int range, uint32_t *off, int32_t **out)
+{
+    const uint32_t n = d->n;
+    size_t total = 0;
+    off[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        mm_view v;
+        if (view_of(d, i, range, &v)) return -1;
+        free(v.keys);
+        total += (size_t)v.nv + (v.nx - v.nk);
+        off[i + 1] = (uint32_t)total;
+    }
+    int32_t *o = (int32_t *)calloc(total ? total : 1, sizeof(int32_t));
+    if (!o) return -1;
+    for (uint32_t i = 0; i < n; ++i) {
+        mm_view v;
+        if (view_of(d, i, range, &v)) { free(o); return -1; }
+        free(v.keys);
+        int32_t *trg = o + off[i];
+        const int32_t *src = v.k2v;
+        const uint32_t tk = v.nv, sk = v.nk, sl = v.nx;
+        if (tk == 0) continue;
+        for (uint32_t x = sk; x < sl; ++x) trg[src[x]]++;
+        trg[0] += (int32_t)tk;
+        for (uint32_t k = 1; k < tk; ++k) trg[k] += trg[k - 1];
+        memmove(trg + 1, trg, (size_t)(tk - 1) * sizeof(int32_t));
+        trg[0] = (int32_t)tk;
+        uint32_t k = 0;
+        for (uint32_t x = sk; x < sl; ++x) {
+            while (x == (uint32_t)src[k]) ++k;
+            trg[trg[src[x]]++] = (int32_t)k;
+        }
+    }
+    *out = o;
+    return 0;
+}

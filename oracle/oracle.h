@@ -108,6 +108,17 @@ int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level,
  * synchronous round in which txn i executes.  Must equal or_waiting_on's level.  0 ok, -7 stuck. */
 int or_waiting_on_events(const or_deps *d, uint32_t n, uint32_t *round_out);
 
+/* ---- deps-set operations over every txn of a set; values index one
+ * TxnId table sorted ascending (index order == Timestamp order) ---- */
+/* Deps.merge / linearUnion of G sets of the same n txns (KeyDeps + RangeDeps; keys may overlap) */
+int or_deps_union(uint32_t G, const or_deps *parts, or_deps *out);
+/* KeyDeps.slice + RangeDeps.slice (+ trimUnusedValues) to select ranges (s,e]: per txn
+ * sel_off[n+1] CSR, or sel_off NULL = the same nsel ranges for every txn */
+int or_deps_slice(const or_deps *d, const uint32_t *sel_off, const uint32_t *sel_start, const uint32_t *sel_end,
+                  uint32_t nsel, or_deps *out);
+/* RelationMultiMap.invert of keysToTxnIds (range 0) / rangesToTxnIds (range 1) of every txn */
+int or_deps_invert(const or_deps *d, int range, uint32_t *off /* [n+1] */, int32_t **out /* malloc'd */);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,9 @@ def lib():
         L.or_stab_key.restype = C.c_uint32
         L.or_waiting_on.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p, _u32p, C.POINTER(_u64p)]
         L.or_waiting_on_events.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p]
+        L.or_deps_union.argtypes = [C.c_uint32, C.POINTER(_OrDeps), C.POINTER(_OrDeps)]
+        L.or_deps_slice.argtypes = [C.POINTER(_OrDeps), _u32p, _u32p, _u32p, C.c_uint32, C.POINTER(_OrDeps)]
+        L.or_deps_invert.argtypes = [C.POINTER(_OrDeps), C.c_int, _u32p, C.POINTER(_i32p)]
         _LIB = L
     return _LIB
 
@@ -231,3 +234,47 @@ def waiting_on_events(p: PartialDeps):
     if rc != 0:
         raise OracleError(rc)
     return rounds[:n].copy()
+
+
+def deps_union(parts):
+    """Deps.merge (left fold of RelationMultiMap.linearUnion) of G PartialDeps of the same txns."""
+    cs = [_c_deps(p) for p in parts]
+    arr = (_OrDeps * len(parts))(*[c[0] for c in cs])
+    d = _OrDeps()
+    rc = lib().or_deps_union(len(parts), arr, C.byref(d))
+    if rc != 0:
+        raise OracleError(rc)
+    try:
+        return _to_partial(d)
+    finally:
+        lib().or_deps_free(C.byref(d))
+
+
+def deps_slice(p: PartialDeps, sel_start, sel_end, sel_off=None):
+    """KeyDeps.slice + RangeDeps.slice of every txn to select ranges (per-txn CSR or shared)."""
+    d, keep = _c_deps(p)
+    ss = np.ascontiguousarray(sel_start, dtype=np.uint32)
+    se = np.ascontiguousarray(sel_end, dtype=np.uint32)
+    so = None if sel_off is None else np.ascontiguousarray(sel_off, dtype=np.uint32)
+    o = _OrDeps()
+    rc = lib().or_deps_slice(C.byref(d), None if so is None else so.ctypes.data_as(_u32p), ss.ctypes.data_as(_u32p),
+                             se.ctypes.data_as(_u32p), len(ss), C.byref(o))
+    if rc != 0:
+        raise OracleError(rc)
+    try:
+        return _to_partial(o)
+    finally:
+        lib().or_deps_free(C.byref(o))
+
+
+def deps_invert(p: PartialDeps, range_side: bool = False):
+    """RelationMultiMap.invert of every txn: (off[n+1], ints) of txnIdsToKeys / txnIdsToRanges."""
+    d, keep = _c_deps(p)
+    off = np.zeros(p.n + 1, dtype=np.uint32)
+    out = _i32p()
+    rc = lib().or_deps_invert(C.byref(d), 1 if range_side else 0, off.ctypes.data_as(_u32p), C.byref(out))
+    if rc != 0:
+        raise OracleError(rc)
+    a = _arr(out, int(off[-1]), np.int32)
+    C.CDLL(None).free(out)
+    return off, a
