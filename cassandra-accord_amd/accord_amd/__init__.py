@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
@@ -85,7 +86,8 @@ class _StoreCfg(C.Structure):
 class _Batch(C.Structure):
     _fields_ = [("n", C.c_uint32), ("msb", _u64p), ("lsb", _u64p), ("node", _i32p),
                 ("key_off", _u32p), ("key_ord", _u32p), ("rng_off", _u32p),
-                ("rng_start", _u32p), ("rng_end", _u32p), ("txn_index", _u32p)]
+                ("rng_start", _u32p), ("rng_end", _u32p), ("txn_index", _u32p),
+                ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p)]
 
 
 class _Deps(C.Structure):
@@ -191,6 +193,11 @@ class Stream:
     rng_start: np.ndarray
     rng_end: np.ndarray
     txn_index: Optional[np.ndarray] = None   # global stream positions (store subsets)
+    # Accept batches (messages/Accept.java:113-117): startedBefore = executeAt per txn
+    # (msb, lsb, node); None = PreAccept (startedBefore = txnId)
+    exec_msb: Optional[np.ndarray] = None
+    exec_lsb: Optional[np.ndarray] = None
+    exec_node: Optional[np.ndarray] = None
 
     @property
     def n(self) -> int:
@@ -210,9 +217,34 @@ class Stream:
         m = min(m, self.n)
         k1 = int(self.key_off[m])
         r1 = int(self.rng_off[m])
+        ex = {}
+        if self.exec_msb is not None:
+            ex = dict(exec_msb=self.exec_msb[:m].copy(), exec_lsb=self.exec_lsb[:m].copy(),
+                      exec_node=self.exec_node[:m].copy())
         return Stream(self.msb[:m].copy(), self.lsb[:m].copy(), self.node[:m].copy(),
                       self.key_off[:m + 1].copy(), self.key_ord[:k1].copy(), self.rng_off[:m + 1].copy(),
-                      self.rng_start[:r1].copy(), self.rng_end[:r1].copy())
+                      self.rng_start[:r1].copy(), self.rng_end[:r1].copy(), **ex)
+
+    def accept(self, frac: float = 1.0, max_delay: int = 64, node_mod: int = 7, seed: int = 1) -> "Stream":
+        """The Accept batch of the same txns (messages/Accept.java:113-117): a `frac` of them get an
+        executeAt later than their TxnId (hlc + U[0, max_delay], Timestamp flags 0, a seeded node;
+        never before the TxnId), the rest executeAt = txnId (p1 = null, PreAccept-equivalent)."""
+        rng = np.random.default_rng(seed)
+        n = self.n
+        em, el, en = self.msb.copy(), self.lsb.copy(), self.node.copy()
+        pick = rng.random(n) < frac
+        delay = rng.integers(0, max_delay + 1, n).astype(np.uint64)
+        node = rng.integers(1, node_mod + 1, n).astype(np.int32)
+        hlc = (self.lsb >> np.uint64(16)) + delay
+        cand_lsb = hlc << np.uint64(16)
+        # Timestamp.compareTo (primitives/Timestamp.java:208-217) with equal msb: hlc, the identity
+        # flags (lsb & 0x1E; the candidate's are 0), then the signed node id
+        flags = self.lsb & np.uint64(0x1E)
+        later = (delay > 0) | ((flags == 0) & (node > self.node))
+        use = pick & later
+        el[use] = cand_lsb[use]
+        en[use] = node[use]
+        return dataclasses.replace(self, exec_msb=em, exec_lsb=el, exec_node=en)
 
     def restrict_keys(self, lo: int, hi: int, drop_empty: bool = False) -> "Stream":
         """Slice every txn's keys to the store block [lo, hi) (CommandStores.mapReduce fan-out,
@@ -223,18 +255,22 @@ class Stream:
         np.cumsum(keep, out=csum[1:])
         counts = (csum[self.key_off[1:].astype(np.int64)] - csum[self.key_off[:-1].astype(np.int64)]).astype(np.uint32)
         kord = self.key_ord[keep].copy()
+        accept = self.exec_msb is not None
         if not drop_empty:
             ko = np.zeros(self.n + 1, np.uint32)
             np.cumsum(counts, out=ko[1:])
-            return Stream(self.msb, self.lsb, self.node, ko, kord, self.rng_off, self.rng_start, self.rng_end)
+            return Stream(self.msb, self.lsb, self.node, ko, kord, self.rng_off, self.rng_start, self.rng_end,
+                          exec_msb=self.exec_msb, exec_lsb=self.exec_lsb, exec_node=self.exec_node)
         if int(self.rng_off[-1]) != 0:
             raise IllegalArgumentException(-1, "drop_empty restriction supports key txns only")
         sel = np.nonzero(counts > 0)[0].astype(np.uint32)
         ko = np.zeros(sel.size + 1, np.uint32)
         np.cumsum(counts[sel], out=ko[1:])
         base = np.zeros(sel.size + 1, np.uint32)
-        return Stream(self.msb[sel].copy(), self.lsb[sel].copy(), self.node[sel].copy(), ko, kord, base, 
-                      np.zeros(0, np.uint32), np.zeros(0, np.uint32), txn_index=sel)
+        ex = dict(exec_msb=self.exec_msb[sel].copy(), exec_lsb=self.exec_lsb[sel].copy(),
+                  exec_node=self.exec_node[sel].copy()) if accept else {}
+        return Stream(self.msb[sel].copy(), self.lsb[sel].copy(), self.node[sel].copy(), ko, kord, base,
+                      np.zeros(0, np.uint32), np.zeros(0, np.uint32), txn_index=sel, **ex)
 
     def c_batch(self) -> _Batch:
         self._keep = [np.ascontiguousarray(a) for a in (self.msb, self.lsb, self.node, self.key_off, self.key_ord,
@@ -254,7 +290,15 @@ class Stream:
         b.rng_start = rs.ctypes.data_as(_u32p) if has_ranges else None
         b.rng_end = re.ctypes.data_as(_u32p) if has_ranges else None
         b.txn_index = self._keep[8].ctypes.data_as(_u32p) if self.txn_index is not None else None
+        if self.exec_msb is not None:
+            ex = [np.ascontiguousarray(self.exec_msb, dtype=np.uint64), np.ascontiguousarray(self.exec_lsb, dtype=np.uint64),
+                  np.ascontiguousarray(self.exec_node, dtype=np.int32)]
+            self._keep += ex
+            b.exec_msb = ex[0].ctypes.data_as(_u64p)
+            b.exec_lsb = ex[1].ctypes.data_as(_u64p)
+            b.exec_node = ex[2].ctypes.data_as(_i32p)
         return b
+
 
 
 def _arr(ptr, n, dtype):

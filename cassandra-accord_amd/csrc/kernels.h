@@ -55,6 +55,9 @@ struct KeyDepsParams {
     DevStatus *status;
     // fast path / fallback: the txns the fast kernel could not take, processed by the general one
     uint32_t *fb_list, *fb_count;
+    // Accept batch: per txn the global position bounding its candidates (txns started before its
+    // executeAt); nullptr = PreAccept (bound = own position).  The txn itself is never a dep (p1).
+    const uint32_t *bound_g;
 };
 
 // txn-major validation + (key, entry) pair packing; range CSR owners and range-txn flags
@@ -63,13 +66,19 @@ void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
                           uint32_t *pair_key, uint32_t *pair_ent, uint32_t *rng_owner, uint32_t *is_range,
                           const uint32_t *txn_index, DevStatus *status, hipStream_t s);
+// Accept batch: bound_l[t] = #batch txns with txnId < executeAt[t], bound_g[t] = its global
+// position, pair_bound[p] = bound_g of p's txn; executeAt < txnId -> ACCORD_ERR_ARG
+void launch_accept_bounds(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
+                          const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode, const uint32_t *key_off,
+                          const uint32_t *txn_index, uint32_t *bound_l, uint32_t *bound_g, uint32_t *pair_bound,
+                          DevStatus *status, hipStream_t s);
 // range_txns[excl[i]] = i for every i with is_range[i]
 void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s);
 size_t history_temp_bytes(uint32_t P);
 // key-major: history entries, segments, and per pair its deps slice (txn-major PairSlice)
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, PairSlice *slice, void *temp, hipStream_t s);
+                    uint32_t *seg_end, PairSlice *slice, void *temp, const uint32_t *pair_bound, hipStream_t s);
 // history tile size of the Write max-scan carry (pw_local / pw_carry) and class-count carries
 constexpr uint32_t HISTORY_TILE = 4096;
 // Views into the history temp buffer launch_history leaves behind: (last Write <= x) + 1 =
@@ -113,6 +122,7 @@ struct RangeDepsParams {
     uint2 *rk_slices;                   // (lo, raw | wcnt << 16) per key of every range txn's ranges
     uint32_t n_range_txns;
     const uint32_t *range_txns;
+    const uint32_t *bound_l;            // Accept batch: txns started before executeAt (nullptr = i)
     // RangeDeps counts / outputs
     uint32_t *cnt_rngs, *cnt_vals, *cnt_r2v;
     const uint32_t *rd_rng_off, *rd_val_off, *rd_r2v_off;

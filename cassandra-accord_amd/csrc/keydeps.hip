@@ -114,6 +114,32 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
     }
 }
 
+// Accept batches (Accept.calculatePartialDeps, messages/Accept.java:113-117): the candidates of txn
+// t are the registered txns with txnId < executeAt[t] (CommandsForKey.insertPos :1698-1703), i.e.
+// the batch prefix [0, bound_l[t]) -- found by a binary search over the sorted batch TxnIds.
+// bound_g is that bound in global stream positions (store subsets), pair_bound the same per pair.
+__global__ __launch_bounds__(256) void accept_bounds_kernel(
+    uint32_t n, const uint64_t *__restrict__ msb, const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
+    const uint64_t *__restrict__ emsb, const uint64_t *__restrict__ elsb, const int32_t *__restrict__ enode,
+    const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ txn_index, uint32_t *__restrict__ bound_l,
+    uint32_t *__restrict__ bound_g, uint32_t *__restrict__ pair_bound, DevStatus *st)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const uint64_t em = emsb[t], el = elsb[t];
+        const int32_t en = enode[t];
+        if (ts_cmp(em, el, en, msb[t], lsb[t], node[t]) < 0) record_error(st, t, ACCORD_ERR_ARG);
+        uint32_t lo = t, hi = n;                     // txnId[t] <= executeAt: the bound is past t
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (ts_cmp(msb[m], lsb[m], node[m], em, el, en) < 0) lo = m + 1; else hi = m;
+        }
+        const uint32_t g = !txn_index ? lo : (lo < n ? txn_index[lo] : txn_index[n - 1] + 1u);
+        bound_l[t] = lo;
+        bound_g[t] = g;
+        for (uint32_t q = key_off[t]; q < key_off[t + 1]; ++q) pair_bound[q] = g;
+    }
+}
+
 // ---- history annotation (key-major) ----
 constexpr int HS_THREADS = 256;
 constexpr int HS_ITEMS = 16;
@@ -250,6 +276,8 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
                                                               const uint32_t *__restrict__ carry,
                                                               const uint64_t *__restrict__ c_local,
                                                               const ClassCarry *__restrict__ ccarry,
+                                                              const uint32_t *__restrict__ seg_end,
+                                                              const uint32_t *__restrict__ pair_bound,
                                                               PairSlice *__restrict__ slice)
 {
     __shared__ uint32_t tx[H2_HALO + H2_TILE];
@@ -326,22 +354,50 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
             pw[j] = max(pw_local[x], carry[x / HS_TILE]);   // (last Write <= x) + 1
         }
     }
+    // upper bound: the pair's own position (PreAccept), or for an Accept the first entry whose txn
+    // is not started before executeAt (pair_bound); the txn itself is then inside and not counted
+    uint32_t hi[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        hi[j] = p;
+        if (pair_bound && p < end) {
+            const uint32_t b = pair_bound[q[j]], c = seg_end[key[j]];
+            uint32_t x = p + 1, step = 1;
+            while (x < c && (hist[x] & ENT_TXN_MASK) < b) {   // gallop, then bisect
+                const uint32_t probe = x + step;
+                if (probe >= c || (hist[probe] & ENT_TXN_MASK) >= b) {
+                    uint32_t l2 = x + 1, h2 = min(probe, c);
+                    while (l2 < h2) {
+                        const uint32_t m = (l2 + h2) >> 1;
+                        if ((hist[m] & ENT_TXN_MASK) < b) l2 = m + 1; else h2 = m;
+                    }
+                    x = l2;
+                    break;
+                }
+                x = probe + 1;
+                step <<= 1;
+            }
+            hi[j] = (b > (ent[j] & ENT_TXN_MASK)) ? x : p;
+        }
+    }
     uint32_t cnt[H2_ITEMS];
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
         l[j] = pw[j] > a[j] ? pw[j] - 1 : a[j];         // now: lo
         cnt[j] = 0;
-        if (p < end && p > l[j]) {
-            const uint32_t wmask = witness_mask(ent[j] >> ENT_KIND_SHIFT);
-            cnt[j] = witnessed_upto(c_local, ccarry, p - 1, wmask) -
+        if (p < end && hi[j] > l[j]) {
+            const uint32_t kind = ent[j] >> ENT_KIND_SHIFT, wmask = witness_mask(kind);
+            cnt[j] = witnessed_upto(c_local, ccarry, hi[j] - 1, wmask) -
                      (l[j] ? witnessed_upto(c_local, ccarry, l[j] - 1, wmask) : 0u);
+            if (hi[j] > p) cnt[j] -= (wmask >> kind) & 1u;   // p1: the txn itself
         }
     }
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
-        if (p < end) slice[q[j]] = PairSlice{l[j], p, cnt[j], 0u};
+        if (p < end) slice[q[j]] = PairSlice{l[j], hi[j], cnt[j], 0u};
     }
 }
 
@@ -556,7 +612,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
         if (lane < k) my_key = ldg(p.key_ord, k0 + lane);
         const uint32_t gi = p.txn_index ? ldg(p.txn_index, i) : i;   // global stream position
         const uint32_t key_base = ldg(p.kd_key_off, i), val_base = ldg(p.vub_off, i), k2v_base = ldg(p.kd_k2v_off, i);
-        const uint32_t nb = SPAN - gi;                  // near bit of txn j: j + nb (< SPAN iff near)
+        // near bit of txn j: j + nb (< SPAN iff near); candidates precede the bound (Accept: executeAt)
+        const uint32_t nb = SPAN - (p.bound_g ? ldg(p.bound_g, i) : gi);
 
         // ---- keys and keysToTxnIds header from the witnessed counts ----
         const bool ne = lane < k && wc != 0;
@@ -583,7 +640,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
                 if (r0 + c * 64 >= raw_total) break;    // wave-uniform early exit
                 const uint32_t ev = e[c];
                 uint32_t out = KD_NONE;
-                if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
+                if (((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && (ev & ENT_TXN_MASK) != gi) {   // p1
                     const uint32_t j = ev & ENT_TXN_MASK;
                     const uint32_t b = j + nb;
                     if (b < SPAN) {
@@ -656,7 +713,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
                 for (int c = 0; c < KD_CB; ++c) {
                     const uint32_t ev = e[c];
                     uint32_t out = KD_NONE;
-                    if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
+                    if (((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && (ev & ENT_TXN_MASK) != gi) {
                         const uint32_t j = ev & ENT_TXN_MASK;
                         if (j + nb < SPAN) {
                             out = j;
@@ -705,7 +762,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
 // half-way (after its keys were written) is simply redone.
 // ---------------------------------------------------------------------------------------------
 struct alignas(32) TxnRec {
-    uint32_t k0, k, kind, gi, key_base, val_base, k2v_base, pad;
+    uint32_t k0, k, kind, gi, key_base, val_base, k2v_base, bound;
 };
 
 __global__ __launch_bounds__(256) void txnrec_kernel(KeyDepsParams p, TxnRec *__restrict__ out)
@@ -719,7 +776,7 @@ __global__ __launch_bounds__(256) void txnrec_kernel(KeyDepsParams p, TxnRec *__
         r.key_base = p.kd_key_off[i];
         r.val_base = p.vub_off[i];
         r.k2v_base = p.kd_k2v_off[i];
-        r.pad = 0;
+        r.bound = p.bound_g ? p.bound_g[i] : r.gi;   // candidates precede it (Accept: executeAt)
         out[i] = r;
     }
 }
@@ -829,7 +886,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             bool fallback = k > 8 || rta > FK_RAW;
             const uint32_t kind = readlane(a.rec, 2), gi = readlane(a.rec, 3);
             const uint32_t wmask = witness_mask(kind);
-            const uint32_t nb = SPAN - gi;            // near bit of txn j: j + nb (< SPAN iff near)
+            const uint32_t nb = SPAN - readlane(a.rec, 7);   // near bit of txn j: j + nb (< SPAN iff near)
             uint32_t F = 0;                           // far deps (older than the near span)
             uint32_t fidx[FK_CB];
             if (!fallback) {
@@ -841,8 +898,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                     fidx[cc] = 0;
                     if ((uint32_t)cc * 64 >= rta) break;   // wave-uniform
                     const uint32_t ev = ea[cc];
-                    const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
                     const uint32_t j = ev & ENT_TXN_MASK;
+                    const bool wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;   // p1
                     const uint32_t bit = j + nb;
                     const bool nr = wit && bit < SPAN;
                     if (nr) atomicOr(&bm[bit >> 6], 1ull << (bit & 63));
@@ -910,8 +967,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             for (int cc = 0; cc < FK_CB; ++cc) {
                 if ((uint32_t)cc * 64 >= rta) break;
                 const uint32_t ev = ea[cc];
-                const bool wit = (wmask >> (ev >> ENT_KIND_SHIFT)) & 1u;
                 const uint32_t j = ev & ENT_TXN_MASK;
+                const bool wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;   // p1
                 const bool nr = wit && j + nb < SPAN;
                 const uint32_t bit = nr ? j + nb : 0u;
                 uint32_t rank = wp[bit >> 6] + (uint32_t)__popcll(bm[bit >> 6] & ((1ull << (bit & 63)) - 1ull));
@@ -1046,6 +1103,18 @@ __global__ __launch_bounds__(256) void compact_flags_kernel(uint32_t n, const ui
         if (flags[i]) out[excl[i]] = i;
 }
 
+void launch_accept_bounds(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
+                          const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode, const uint32_t *key_off,
+                          const uint32_t *txn_index, uint32_t *bound_l, uint32_t *bound_g, uint32_t *pair_bound,
+                          DevStatus *status, hipStream_t s)
+{
+    if (n == 0) return;
+    uint32_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(accept_bounds_kernel, dim3(blocks), dim3(256), 0, s, n, msb, lsb, node, emsb, elsb, enode, key_off,
+                       txn_index, bound_l, bound_g, pair_bound, status);
+}
+
 void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s)
 {
     if (n == 0) return;
@@ -1084,7 +1153,7 @@ HistoryViews history_views(void *temp, uint32_t P)
 
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, PairSlice *slice, void *temp, hipStream_t s)
+                    uint32_t *seg_end, PairSlice *slice, void *temp, const uint32_t *pair_bound, hipStream_t s)
 {
     (void)nkeys;
     if (P == 0) return;
@@ -1102,7 +1171,7 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
     hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tile_cnt, ccarry, tiles);
     hipLaunchKernelGGL(history2_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P, window,
                        sorted_key, sorted_pair, hist,
-                       seg_start, pw_local, tile_max, c_local, ccarry, slice);
+                       seg_start, pw_local, tile_max, c_local, ccarry, seg_end, pair_bound, slice);
 }
 
 void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *slice, uint32_t *cnt_keys,

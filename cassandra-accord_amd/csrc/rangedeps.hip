@@ -75,7 +75,9 @@ __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p
         const bool key_query = (lsb_i & 1) == 0;
         const uint32_t q0 = key_query ? p.key_off[i] : p.rng_off[i];
         const uint32_t q1 = key_query ? p.key_off[i + 1] : p.rng_off[i + 1];
-        const uint32_t r_lo = p.rng_off[i > p.window ? i - p.window : 0], r_hi = p.rng_off[i];
+        // live range commands: started in the window and before the bound (i; Accept: executeAt)
+        const uint32_t r_lo = p.rng_off[i > p.window ? i - p.window : 0];
+        const uint32_t r_hi = p.rng_off[p.bound_l ? p.bound_l[i] : i];
         uint32_t H = 0;
         // up to 8 query keys / ranges: held wave-uniform, every candidate tested by compares
         const uint32_t nq = q1 - q0;
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p
                     } else {
                         inter = rd_hits(p, s, e, key_query, q0, q1);
                     }
-                    hit = inter && ((wmask >> ((uint32_t)(p.lsb[j] >> 1) & 7)) & 1u);
+                    hit = inter && j != i && ((wmask >> ((uint32_t)(p.lsb[j] >> 1) & 7)) & 1u);   // p1
                 }
                 const uint64_t bal = __ballot(hit);
                 const uint32_t h = H + (uint32_t)__popcll(bal & lt);
@@ -262,7 +264,10 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
 {
     const bool windowed = i > p.window;
     const uint32_t thr = windowed ? i - p.window : 0u;
-    const size_t row1 = (size_t)(i >> RK_CP_SHIFT) * p.nkeys, row2 = (size_t)(thr >> RK_CP_SHIFT) * p.nkeys;
+    // slices end at the first entry with txn >= eb (i; Accept: the txns started before executeAt)
+    const uint32_t eb = p.bound_l ? p.bound_l[i] : i;
+    const bool past = (eb >> RK_CP_SHIFT) >= p.ncp;     // eb == n on a block boundary: whole segment
+    const size_t row1 = (size_t)(past ? 0u : eb >> RK_CP_SHIFT) * p.nkeys, row2 = (size_t)(thr >> RK_CP_SHIFT) * p.nkeys;
     uint32_t a[U], c[U];
     uint4 e1[U], e2[U];
 #pragma unroll
@@ -278,7 +283,7 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
     for (int u = 0; u < U; ++u) {
         out[u] = RkSlice{0u, 0u, 0u};
         if (!(valid[u] && a[u] < c[u])) continue;
-        const uint32_t pos = e1[u].y >= i ? e1[u].x : rk_first_ge(p.hist, e1[u].x + 1, c[u], i);
+        const uint32_t pos = past ? c[u] : e1[u].y >= eb ? e1[u].x : rk_first_ge(p.hist, e1[u].x + 1, c[u], eb);
         if (pos == a[u]) continue;
         uint32_t pw = 0;
         if (windowed) {

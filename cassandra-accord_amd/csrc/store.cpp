@@ -190,6 +190,19 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
         HIPCHECK(s, s->txn_index.ensure((size_t)n * 4));
         if (n) HIPCHECK(s, hipMemcpyAsync(s->txn_index.p, b->txn_index, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
     }
+    if ((b->exec_msb != nullptr) != (b->exec_lsb != nullptr) || (b->exec_msb != nullptr) != (b->exec_node != nullptr))
+        return fail(s, ACCORD_ERR_ARG, "executeAt needs all of exec_msb, exec_lsb, exec_node");
+    s->has_exec = b->exec_msb != nullptr;
+    if (s->has_exec) {
+        HIPCHECK(s, s->exec_msb.ensure((size_t)n * 8));
+        HIPCHECK(s, s->exec_lsb.ensure((size_t)n * 8));
+        HIPCHECK(s, s->exec_node.ensure((size_t)n * 4));
+        if (n) {
+            HIPCHECK(s, hipMemcpyAsync(s->exec_msb.p, b->exec_msb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
+            HIPCHECK(s, hipMemcpyAsync(s->exec_lsb.p, b->exec_lsb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
+            HIPCHECK(s, hipMemcpyAsync(s->exec_node.p, b->exec_node, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
+        }
+    }
     HIPCHECK(s, hipStreamSynchronize(s->stream));
     s->has_batch = true;
     return ACCORD_OK;
@@ -259,6 +272,18 @@ int32_t accord_deps_compute(accord_store *s)
         accord::launch_compact_flags(n, s->is_range.as<uint32_t>(), s->rt_excl.as<uint32_t>(),
                                      s->range_txns.as<uint32_t>(), st);
     }
+    const uint32_t *bound_l = nullptr, *bound_g = nullptr, *pair_bound = nullptr;
+    if (s->has_exec) {
+        HIPCHECK(s, s->bound_l.ensure((size_t)n * 4 + 4));
+        HIPCHECK(s, s->bound_g.ensure((size_t)n * 4 + 4));
+        HIPCHECK(s, s->pair_bound.ensure((size_t)P * 4 + 4));
+        accord::launch_accept_bounds(n, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->node.as<int32_t>(),
+                                     s->exec_msb.as<uint64_t>(), s->exec_lsb.as<uint64_t>(), s->exec_node.as<int32_t>(),
+                                     s->key_off.as<uint32_t>(), s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr,
+                                     s->bound_l.as<uint32_t>(), s->bound_g.as<uint32_t>(), s->pair_bound.as<uint32_t>(),
+                                     &dev->status, st);
+        bound_l = s->bound_l.as<uint32_t>(); bound_g = s->bound_g.as<uint32_t>(); pair_bound = s->pair_bound.as<uint32_t>();
+    }
     record(s, EV_VALIDATE);
     accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
                              s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
@@ -270,7 +295,7 @@ int32_t accord_deps_compute(accord_store *s)
     accord::launch_history(P, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
                            s->seg_end.as<uint32_t>(), s->slice.as<accord::PairSlice>(),
-                           s->hist_tmp.p, st);
+                           s->hist_tmp.p, pair_bound, st);
     record(s, EV_SEGMENT);
 
     accord::KeyDepsParams kp{};
@@ -284,8 +309,10 @@ int32_t accord_deps_compute(accord_store *s)
     kp.cnt_vub = s->cnt_vub.as<uint32_t>();
     kp.cnt_vals = s->cnt_vals.as<uint32_t>();
     kp.status = &dev->status;
+    kp.bound_g = bound_g;
 
     accord::RangeDepsParams rp{};
+    rp.bound_l = bound_l;
     rp.n = n; rp.lsb = kp.lsb; rp.key_off = kp.key_off; rp.key_ord = kp.key_ord;
     rp.rng_off = s->rng_off.as<uint32_t>(); rp.rng_start = s->rng_start.as<uint32_t>();
     rp.rng_end = s->rng_end.as<uint32_t>(); rp.rng_owner = s->rng_owner.as<uint32_t>();

@@ -81,6 +81,10 @@ struct accord_store {
     uint64_t tot_keys = 0, tot_vals = 0, tot_k2v = 0;
     DevBuf txn_index;              // global stream positions (nullptr = identity)
     bool has_txn_index = false;
+    // Accept batch: executeAt per txn; bound_l / bound_g = txns started before it (local index,
+    // global position), pair_bound = bound_g per (txn, key) pair
+    DevBuf exec_msb, exec_lsb, exec_node, bound_l, bound_g, pair_bound;
+    bool has_exec = false;
     // merged (K6) result: replaces the computed partial as the store's current deps
     bool merged = false;
     uint32_t m_n = 0, m_txn_lo = 0;

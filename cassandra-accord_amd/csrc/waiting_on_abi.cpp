@@ -28,6 +28,8 @@ int32_t accord_waiting_on_compute(accord_store *s)
     if (!s->computed) return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_compute before accord_deps_compute");
     if (s->merged || s->has_txn_index)
         return fail(s, ACCORD_ERR_STATE, "WaitingOn levelling runs on a full stream's deps (gather to one store first)");
+    if (s->has_exec)   // the levelling model is defined on PreAccept deps
+        return fail(s, ACCORD_ERR_STATE, "WaitingOn levelling runs on a PreAccept batch's deps, not an Accept batch");
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     const uint32_t n = s->n;
     const size_t n1 = (size_t)n + 1;

@@ -79,6 +79,15 @@ typedef struct {
      * local/CommandStores.java:575-592) passes their positions so the status-at-time window and
      * the deps values (txnIds) stay in global stream coordinates.  Key txns only. */
     const uint32_t *txn_index;
+    /* Accept batches (Accept.calculatePartialDeps, messages/Accept.java:113-117): [n] the
+     * executeAt of each txn (a Timestamp: msb, lsb, node), passed as startedBefore to
+     * mapReduceActive, with p1 = txnId excluded unless executeAt.equals(txnId)
+     * (messages/PreAccept.java:253-259).  Every txn of the batch started before a txn's executeAt
+     * is registered when it computes (PREACCEPTED inside the window, as SURVEY.md §8d).  All three
+     * NULL = a PreAccept batch (startedBefore = txnId).  executeAt < txnId -> ACCORD_ERR_ARG. */
+    const uint64_t *exec_msb;
+    const uint64_t *exec_lsb;
+    const int32_t  *exec_node;
 } accord_batch;
 
 /* Per-txn PartialDeps, exact reference layout (KeyDeps.java:150-187, RangeDeps.java:81-99):
@@ -114,9 +123,10 @@ const char *accord_last_error(const accord_store *store);   /* NULL store: last 
 void       *accord_store_stream(accord_store *store);        /* the store's hipStream_t */
 
 /* ---- synchronous batch entry: host in, host out ----
- * CommandStore.calculateDepsBatch(TxnId[], Seekables[], ...) -> PartialDeps[]: identical to
- * calling PreAccept.calculatePartialDeps (messages/PreAccept.java:245-265) for every txn in
- * TxnId order under the status-at-time model with window cfg.window. */
+ * CommandStore.calculateDepsBatch(TxnId[], Seekables[], Timestamp[] executeAt, ...) ->
+ * PartialDeps[]: identical to calling PreAccept.calculatePartialDeps (messages/PreAccept.java:
+ * 245-265; via Accept.calculatePartialDeps, messages/Accept.java:113-117, when the batch carries
+ * executeAt) for every txn in TxnId order under the status-at-time model with window cfg.window. */
 int32_t accord_deps_batch(accord_store *store, const accord_batch *batch, accord_deps *out);
 void    accord_deps_release(accord_deps *deps);
 

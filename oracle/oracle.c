@@ -530,9 +530,48 @@ static int validate(const or_stream *s, uint32_t n)
     return 0;
 }
 
+/* Accept batches: startedBefore of txn i (executeAt for Accept, messages/Accept.java:113-117;
+ * the txnId itself for PreAccept, messages/PreAccept.java:245-265) */
+static ts_t started_before(const or_stream *s, uint32_t i)
+{
+    ts_t t;
+    if (s->exec_msb) { t.msb = s->exec_msb[i]; t.lsb = s->exec_lsb[i]; t.node = s->exec_node[i]; }
+    else { t.msb = s->msb[i]; t.lsb = s->lsb[i]; t.node = s->node[i]; }
+    return t;
+}
+
+/* p1 of calculatePartialDeps: executeAt.equals(txnId) ? null : txnId (PreAccept.java:259) */
+static long p1_of(const or_stream *s, uint32_t i)
+{
+    if (!s->exec_msb) return -1;
+    return or_ts_equals(s->exec_msb[i], s->exec_lsb[i], s->exec_node[i], s->msb[i], s->lsb[i], s->node[i]) ? -1 : (long)i;
+}
+
+/* number of stream txns j < n with txnId_j < ts (TxnIds are strictly ascending): the txns a
+ * startedBefore bound admits (CommandsForKey.insertPos, :1698-1703) */
+static uint32_t bound_of(const or_stream *s, uint32_t n, const ts_t *ts)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint32_t m = (lo + hi) / 2;
+        if (or_ts_compare(s->msb[m], s->lsb[m], s->node[m], ts->msb, ts->lsb, ts->node) < 0) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+/* an Accept's executeAt never precedes its txnId (Commands.accept, local/Commands.java) */
+static int validate_exec(const or_stream *s, uint32_t n)
+{
+    if (!s->exec_msb) return 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (or_ts_compare(s->exec_msb[i], s->exec_lsb[i], s->exec_node[i], s->msb[i], s->lsb[i], s->node[i]) < 0) return -1;
+    return 0;
+}
+
 static int stream_literal(const or_stream *s, uint32_t n, or_deps *out)
 {
     int rc = validate(s, n);
+    if (!rc) rc = validate_exec(s, n);
     if (rc) return rc;
     ts_t *tbl = (ts_t *)malloc((size_t)(n ? n : 1) * sizeof(ts_t));
     if (!tbl) return -1;
@@ -549,7 +588,12 @@ static int stream_literal(const or_stream *s, uint32_t n, or_deps *out)
     rc = -1;
     if (!cfks || !rcs || mmo_init(&kd) || mmo_init(&rd)) goto done;
 
+    uint32_t reg = 0;                        /* txns [0, reg) are registered */
     for (uint32_t i = 0; i < n; ++i) {
+        const ts_t sb_i = started_before(s, i);
+        const long p1 = p1_of(s, i);
+        uint32_t reg_to = bound_of(s, n, &sb_i);  /* an Accept sees every txn started before executeAt */
+        if (reg_to < i + 1) reg_to = i + 1;
         /* 1. status at time i: txn j = i-W-1 leaves the window -> APPLIED (executeAt=txnId) if a
          *    key txn, Erased if a range txn. */
         if (i >= s->window + 1) {
@@ -565,34 +609,40 @@ static int stream_literal(const or_stream *s, uint32_t n, or_deps *out)
                 }
             }
         }
-        /* 2. register txn i as PREACCEPTED (SafeCommandStore.updateCommandsForKey :212-239 ->
+        /* 2. register txns [reg, reg_to) -- txn i, and for an Accept every txn started before its
+         *    executeAt -- as PREACCEPTED (SafeCommandStore.updateCommandsForKey :212-239 ->
          *    CommandsForKey.insert; range txns -> InMemoryCommandStore rangeCommands :739-762) */
-        int kind_i = kind_of(s->lsb[i]);
-        if (domain_of(s->lsb[i]) == 0) {
-            if (is_globally_visible(kind_i) == 1)
-                for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p)
-                    if (cfk_insert(&cfks[s->key_ord[p]], tbl, i, S_PREACCEPTED)) goto done;
-        } else {
-            rcs[nrc].txn = i; rcs[nrc].erased = 0; rcs[nrc].r0 = s->rng_off[i]; rcs[nrc].r1 = s->rng_off[i + 1];
-            ++nrc;
+        for (; reg < reg_to; ++reg) {
+            const uint32_t g = reg;
+            const int kind_g = kind_of(s->lsb[g]);
+            if (domain_of(s->lsb[g]) == 0) {
+                if (is_globally_visible(kind_g) == 1)
+                    for (uint32_t p = s->key_off[g]; p < s->key_off[g + 1]; ++p)
+                        if (cfk_insert(&cfks[s->key_ord[p]], tbl, g, S_PREACCEPTED)) goto done;
+            } else {
+                rcs[nrc].txn = g; rcs[nrc].erased = 0; rcs[nrc].r0 = s->rng_off[g]; rcs[nrc].r1 = s->rng_off[g + 1];
+                ++nrc;
+            }
         }
 
-        /* 3. calculatePartialDeps (messages/PreAccept.java:245-265): startedBefore = executeAt =
-         *    txnId, p1 = null, keys first then ranges (SafeCommandStore.java:269-274). */
+        /* 3. calculatePartialDeps (messages/PreAccept.java:245-265): startedBefore = executeAt
+         *    (= txnId for PreAccept, the Accept's executeAt otherwise), p1 = txnId unless they are
+         *    equal, keys first then ranges (SafeCommandStore.java:269-274). */
+        int kind_i = kind_of(s->lsb[i]);
         int test_kinds = witnesses_of(kind_i);
         mmb_reset(&kb); mmb_reset(&rb);
-        const ts_t *sb = &tbl[i];
+        const ts_t *sb = &sb_i;
         if (domain_of(s->lsb[i]) == 0) {
             for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) {
                 uint32_t key = s->key_ord[p];
-                if (cfk_map_reduce_active(&cfks[key], tbl, sb, test_kinds, key, &kb, -1)) goto done;
+                if (cfk_map_reduce_active(&cfks[key], tbl, sb, test_kinds, key, &kb, p1)) goto done;
             }
         } else {
             /* mapReduceForKey Range case (InMemoryCommandStore.java:274-289): every CFK key in
              * each (start,end] in ascending order */
             for (uint32_t r = s->rng_off[i]; r < s->rng_off[i + 1]; ++r)
                 for (uint32_t key = s->rng_start[r] + 1; key <= s->rng_end[r] && key < nkeys; ++key)
-                    if (cfks[key].n && cfk_map_reduce_active(&cfks[key], tbl, sb, test_kinds, key, &kb, -1)) goto done;
+                    if (cfks[key].n && cfk_map_reduce_active(&cfks[key], tbl, sb, test_kinds, key, &kb, p1)) goto done;
         }
         /* mapReduceRangesInternal: TreeMap<Range, List<TxnInfo>> collect by Range.compare */
         ncoll = 0;
@@ -600,6 +650,7 @@ static int stream_literal(const or_stream *s, uint32_t n, or_deps *out)
             const rangecmd_t *cmd = &rcs[c];
             if (cmd->erased) continue;                                         /* :891 */
             if (ts_cmp(&tbl[cmd->txn], sb) >= 0) continue;                     /* :901-902 */
+            if (p1 >= 0 && (uint32_t)p1 == cmd->txn) continue;                 /* p1 filter */
             if (!kinds_test(test_kinds, kind_of(s->lsb[cmd->txn]))) continue;  /* :927 */
             for (uint32_t a = cmd->r0; a < cmd->r1; ++a) {                     /* foldl :953-959 */
                 uint32_t rs = s->rng_start[a], re = s->rng_end[a];
@@ -676,7 +727,9 @@ int or_stream_deps_literal_prefix(const or_stream *s, uint32_t limit, or_deps *o
  * j < i-W (else the start of the history): CommandsForKey.java:620-645 with every j < i-W
  * APPLIED at executeAt=txnId (so committed[] is the history prefix before i-W) and every
  * i-W <= j < i PREACCEPTED.  Range commands: live iff j >= i-W, no pruning (InMemoryCommandStore
- * .java:883-1016).
+ * .java:883-1016).  Accept batches replace the upper bound i by `bound` = the txns started before
+ * executeAt (all registered, PREACCEPTED when j >= i-W) and drop the txn itself (p1); every
+ * APPLIED entry still precedes executeAt, so lcw is unchanged.
  * ------------------------------------------------------------------------------------------ */
 static int cmp_u32(const void *a, const void *b)
 {
@@ -688,6 +741,7 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
 {
     uint32_t n = s->n;
     int rc = validate(s, n);
+    if (!rc) rc = validate_exec(s, n);
     if (rc) return rc;
     uint32_t nkeys = max_key(s, n) + 1;
     uint32_t P = s->key_off[n];
@@ -716,6 +770,9 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
     for (uint32_t i = 0; i < n; ++i) {
         int tk = witnesses_of(kind_of(s->lsb[i]));
         int64_t applied_before = (int64_t)i - (int64_t)s->window;    /* j < i-W are applied */
+        const ts_t sb_i = started_before(s, i);
+        const uint32_t bound = bound_of(s, n, &sb_i);     /* candidates j < bound (= i: PreAccept) */
+        const long p1 = p1_of(s, i);                       /* excluded (Accept: the txn itself) */
         lists.n = 0; lens.n = 0; heads.n = 0;
         u32v qkeys = {0};
         /* keys queried: own keys, or every key inside own ranges (CFKs that exist) */
@@ -730,8 +787,8 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
         for (uint32_t q = 0; q < qkeys.n; ++q) {
             uint32_t key = qkeys.p[q];
             uint32_t a = hoff[key], b = hoff[key + 1];
-            uint32_t lo = a, hi = b;                      /* p = lower_bound(i) */
-            while (lo < hi) { uint32_t m = (lo + hi) / 2; if (hist[m] < i) lo = m + 1; else hi = m; }
+            uint32_t lo = a, hi = b;                      /* p = lower_bound(bound) */
+            while (lo < hi) { uint32_t m = (lo + hi) / 2; if (hist[m] < bound) lo = m + 1; else hi = m; }
             uint32_t p = lo;
             uint32_t start = a;
             if (applied_before > 0) {
@@ -743,7 +800,8 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
             }
             uint32_t before = (uint32_t)lists.n;
             for (uint32_t e = start; e < p; ++e)
-                if (kinds_test(tk, kind_of(s->lsb[hist[e]]))) if (u32v_push(&lists, hist[e])) goto done;
+                if (kinds_test(tk, kind_of(s->lsb[hist[e]])) && (p1 < 0 || hist[e] != (uint32_t)p1))
+                    if (u32v_push(&lists, hist[e])) goto done;
             uint32_t c = (uint32_t)lists.n - before;
             if (c) { if (u32v_push(&lens, c) || u32v_push(&heads, key)) goto done; ++kc; }
         }
@@ -772,7 +830,8 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
             while (rc_first < rcmd.n && (int64_t)rcmd.p[rc_first] < applied_before) ++rc_first;   /* monotone in i */
             for (size_t c = rc_first; c < rcmd.n; ++c) {
                 uint32_t j = rcmd.p[c];
-                if (j >= i) break;
+                if (j >= bound) break;
+                if (p1 >= 0 && j == (uint32_t)p1) continue;
                 if (!kinds_test(tk, kind_of(s->lsb[j]))) continue;
                 for (uint32_t a = s->rng_off[j]; a < s->rng_off[j + 1]; ++a) {
                     uint32_t rs = s->rng_start[a], re = s->rng_end[a];

@@ -49,6 +49,12 @@ typedef struct {
     const uint32_t *rng_start;  /* [rng_off[n]] */
     const uint32_t *rng_end;
     uint32_t window;            /* W of the status-at-time model */
+    /* Accept batches (messages/Accept.java:113-117): per txn the startedBefore = executeAt
+     * passed to PreAccept.calculatePartialDeps (p1 = txnId when executeAt != txnId).  NULL =
+     * PreAccept (startedBefore = txnId).  executeAt must not precede its txnId. */
+    const uint64_t *exec_msb;
+    const uint64_t *exec_lsb;
+    const int32_t  *exec_node;
 } or_stream;
 
 /* Per-txn PartialDeps in the exact reference layout (KeyDeps.java:150-187,

@@ -24,6 +24,10 @@ def kat_stream(kat) -> Stream:
     key_off = np.zeros(n + 1, np.uint32)
     rng_off = np.zeros(n + 1, np.uint32)
     keys, rs, re = [], [], []
+    accept = any("exec" in t for t in txns)
+    emsb = np.zeros(n, np.uint64)
+    elsb = np.zeros(n, np.uint64)
+    enode = np.zeros(n, np.int32)
     for i, t in enumerate(txns):
         hlc = t.get("hlc", 1_000_000 + i)
         is_range = "ranges" in t
@@ -38,8 +42,17 @@ def kat_stream(kat) -> Stream:
             re.append(b)
         key_off[i + 1] = len(keys)
         rng_off[i + 1] = len(rs)
+        # Accept: startedBefore = executeAt (a Timestamp: hlc, flags, node), default = the txnId
+        e = t.get("exec")
+        emsb[i], elsb[i], enode[i] = msb[i], lsb[i], node[i]
+        if e is not None:
+            ehlc = e["hlc"]
+            emsb[i] = (1 << 15) | (ehlc >> 48)
+            elsb[i] = ((ehlc << 16) | e.get("flags", 0)) & ((1 << 64) - 1)
+            enode[i] = e["node"]
+    ex = dict(exec_msb=emsb, exec_lsb=elsb, exec_node=enode) if accept else {}
     return Stream(msb, lsb, node, key_off, np.array(keys, np.uint32), rng_off, np.array(rs, np.uint32),
-                  np.array(re, np.uint32))
+                  np.array(re, np.uint32), **ex)
 
 
 def max_key(s: Stream) -> int:

@@ -24,7 +24,8 @@ _u64p = C.POINTER(C.c_uint64)
 class _OrStream(C.Structure):
     _fields_ = [("n", C.c_uint32), ("msb", _u64p), ("lsb", _u64p), ("node", _i32p),
                 ("key_off", _u32p), ("key_ord", _u32p), ("rng_off", _u32p), ("rng_start", _u32p),
-                ("rng_end", _u32p), ("window", C.c_uint32)]
+                ("rng_end", _u32p), ("window", C.c_uint32),
+                ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p)]
 
 
 class _OrDeps(C.Structure):
@@ -103,6 +104,13 @@ def _or_stream(s: Stream, window: int):
     o.rng_start = rs.ctypes.data_as(_u32p)
     o.rng_end = re.ctypes.data_as(_u32p)
     o.window = window
+    if s.exec_msb is not None:
+        ex = [np.ascontiguousarray(s.exec_msb, dtype=np.uint64), np.ascontiguousarray(s.exec_lsb, dtype=np.uint64),
+              np.ascontiguousarray(s.exec_node, dtype=np.int32)]
+        keep += ex
+        o.exec_msb = ex[0].ctypes.data_as(_u64p)
+        o.exec_lsb = ex[1].ctypes.data_as(_u64p)
+        o.exec_node = ex[2].ctypes.data_as(_i32p)
     return o, keep
 
 
