@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = [
     "accord_waiting_on_compute", "accord_waiting_on_download", "accord_waiting_on_release",
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
+    "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
 ]
 
 
@@ -76,6 +77,11 @@ def _raise(code: int, msg: str):
 _u32p = C.POINTER(C.c_uint32)
 _i32p = C.POINTER(C.c_int32)
 _u64p = C.POINTER(C.c_uint64)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class _MaxConflictsOut(C.Structure):
+    _fields_ = [("msb", _u64p), ("lsb", _u64p), ("node", _i32p), ("present", _u8p), ("fast", _u8p)]
 
 
 class _StoreCfg(C.Structure):
@@ -172,6 +178,9 @@ def lib() -> C.CDLL:
         L.accord_deps_inverse_release.restype = None
         L.accord_ops_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
         L.accord_deps_upload.argtypes = [C.c_void_p, C.POINTER(_Deps)]
+        L.accord_max_conflicts_fold.argtypes = [C.c_void_p, C.POINTER(_MaxConflictsOut)]
+        L.accord_max_conflicts_reset.argtypes = [C.c_void_p]
+        L.accord_max_conflicts_state.argtypes = [C.c_void_p, _u64p, _u64p, _i32p, _u8p]
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
             if f.restype is C.c_int:  # default
@@ -486,6 +495,7 @@ class CommandStore:
     def upload(self, s: Stream):
         b = s.c_batch()
         self._check(lib().accord_batch_upload(self._h, C.byref(b)))
+        self._n_uploaded = len(s.msb)
 
     def compute(self):
         self._check(lib().accord_deps_compute(self._h))
@@ -497,6 +507,35 @@ class CommandStore:
             return PartialDeps.from_c(d)
         finally:
             lib().accord_deps_release(C.byref(d))
+
+    # MaxConflicts (include/accord_deps.h; local/MaxConflicts.java, local/CommandStore.java:320-349)
+    def max_conflicts_fold(self, s: "Stream | None" = None, download: bool = True):
+        """For every txn of the uploaded batch (or `s`, uploaded first): minNonConflicting =
+        maxConflicts.get(keys) before the txn's own update, and the fast-path test.  Returns
+        (msb, lsb, node, present, fast) numpy arrays, or None when download is False."""
+        if s is not None:
+            self.upload(s)
+        if not download:
+            self._check(lib().accord_max_conflicts_fold(self._h, None))
+            return None
+        n = self._n_uploaded if s is None else len(s.msb)
+        msb = np.zeros(n, np.uint64); lsb = np.zeros(n, np.uint64); node = np.zeros(n, np.int32)
+        present = np.zeros(n, np.uint8); fast = np.zeros(n, np.uint8)
+        o = _MaxConflictsOut(msb.ctypes.data_as(_u64p), lsb.ctypes.data_as(_u64p), node.ctypes.data_as(_i32p),
+                             present.ctypes.data_as(_u8p), fast.ctypes.data_as(_u8p))
+        self._check(lib().accord_max_conflicts_fold(self._h, C.byref(o)))
+        return msb, lsb, node, present, fast
+
+    def max_conflicts_reset(self):
+        self._check(lib().accord_max_conflicts_reset(self._h))
+
+    def max_conflicts_state(self):
+        nk = self.key_hi - self.key_lo
+        msb = np.zeros(nk, np.uint64); lsb = np.zeros(nk, np.uint64); node = np.zeros(nk, np.int32)
+        present = np.zeros(nk, np.uint8)
+        self._check(lib().accord_max_conflicts_state(self._h, msb.ctypes.data_as(_u64p), lsb.ctypes.data_as(_u64p),
+                                                     node.ctypes.data_as(_i32p), present.ctypes.data_as(_u8p)))
+        return msb, lsb, node, present
 
     def device_view(self) -> dict:
         d = _Deps()

@@ -1,0 +1,348 @@
+// MaxConflicts fold on the device: the executeAt-proposal input of
+// CommandStore.preaccept (local/CommandStore.java:320-349) for a batch of key txns in TxnId order.
+//
+//   minNonConflicting[t] = MaxConflicts.get(keys_t)            (local/MaxConflicts.java:46-49)
+//                        = foldl(keys_t, Timestamp::max, NONE) over the keys that hold an entry
+//   fast[t]              = txnId_t.compareTo(minNonConflicting[t]) >= 0    (:345, epoch excluded)
+//   then, for globally visible kinds, MaxConflicts.update(keys_t, executeAt_t)
+//                        (local/SafeCommandStore.java:192-210, local/CommandStore.java:280-289)
+//
+// The sequential map updates become one segmented scan: the (key, pair) list is radix-sorted by key
+// (stable, so each key's pairs stay in stream order) and every pair gets the exclusive prefix of
+// its key segment under the operator "later wins only if strictly greater" (Timestamp.max(old, new)
+// inside ReducingIntervalMap.merge keeps the old value on ties), seeded with the store's current
+// per-key value.  A per-txn pass then folds its pairs in key order with ">=" (foldl applies
+// Timestamp.max(value, acc), so a tie takes the later key's value).  The per-key map is a dense
+// array over the store's key ordinals, resident in HBM between batches (CommandStore.maxConflicts).
+//
+// Bytes per pair: key ordinal 4 + sort (≈3 passes × 16) + scan read 4+4+24 + prefix write 24 +
+// fold read 24 ≈ 130 B; HBM-bound integer work, no MFMA.
+#include "store_impl.h"
+
+#include <algorithm>
+#include <vector>
+
+namespace {
+
+struct TsV {                 // one MaxConflicts value: Timestamp bits + "entry present"
+    uint64_t msb, lsb;
+    int32_t node;
+    uint32_t has;
+};
+
+constexpr uint32_t MC_TILE = 1024;   // one element per thread, 16 waves
+constexpr uint32_t MC_CARRY_THREADS = 1024;
+
+__device__ __forceinline__ int tcmp(const TsV &a, const TsV &b)
+{
+    return ts_cmp(a.msb, a.lsb, a.node, b.msb, b.lsb, b.node);
+}
+// a earlier, b later: the merge's Timestamp.max(old, new) keeps old unless new is strictly greater
+__device__ __forceinline__ TsV max_keep_old(const TsV &a, const TsV &b)
+{
+    if (!b.has) return a;
+    if (!a.has) return b;
+    return tcmp(b, a) > 0 ? b : a;
+}
+
+struct Comp {                // segmented-scan composite: head seen in the span, value of the open segment
+    TsV v;
+    uint32_t head;
+};
+__device__ __forceinline__ Comp comp(const Comp &a, const Comp &b)
+{
+    if (b.head) return b;
+    Comp r;
+    r.v = max_keep_old(a.v, b.v);
+    r.head = a.head;
+    return r;
+}
+
+__device__ __forceinline__ void record_error(accord::DevStatus *st, uint32_t i, int32_t code)
+{
+    unsigned long long v = ((unsigned long long)i << 32) | (uint32_t)(-code);
+    atomicMin(&st->first, v);
+}
+
+// txn-major: validate (key domain, kind, keys sorted-unique inside the store) and pack
+// (key, pair) for the sort
+__global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t n, const uint64_t *__restrict__ lsb,
+                                                      const uint32_t *__restrict__ key_off,
+                                                      const uint32_t *__restrict__ key_ord, uint32_t key_lo,
+                                                      uint32_t key_hi, uint32_t *__restrict__ pk,
+                                                      uint32_t *__restrict__ pv, accord::DevStatus *st)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint64_t l = lsb[t];
+    const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
+    if (domain != 0) record_error(st, t, ACCORD_ERR_DOMAIN);
+    if (kind > 4) record_error(st, t, ACCORD_ERR_KIND);
+    const uint32_t b = key_off[t], e = key_off[t + 1];
+    uint32_t prev = 0;
+    for (uint32_t p = b; p < e; ++p) {
+        const uint32_t k = key_ord[p];
+        if (k < key_lo || k >= key_hi || (p > b && k <= prev)) record_error(st, t, ACCORD_ERR_KEYS);
+        pk[p] = (k >= key_lo && k < key_hi) ? k - key_lo : 0;
+        pv[p] = p;
+        prev = k;
+    }
+}
+
+// pair -> txn (for the scan's element values)
+__global__ void __launch_bounds__(256) mc_owner_kernel(uint32_t n, const uint32_t *__restrict__ key_off,
+                                                       uint32_t *__restrict__ owner)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    for (uint32_t p = key_off[t]; p < key_off[t + 1]; ++p) owner[p] = t;
+}
+
+__device__ __forceinline__ TsV elem_value(uint32_t t, const uint64_t *lsb, const uint64_t *vm, const uint64_t *vl,
+                                          const int32_t *vn)
+{
+    TsV v;
+    const uint32_t kind = (uint32_t)(lsb[t] >> 1) & 7;
+    v.has = kind != 2u;          // EphemeralRead is not globally visible (LocalOnly rejected)
+    v.msb = vm[t]; v.lsb = vl[t]; v.node = vn[t];
+    return v;
+}
+
+// Tile-local segmented inclusive scan in LDS.  mode 0: write the tile composite.  mode 1: apply the
+// tile's carry, write each pair's exclusive prefix (pair order) and each segment's final value.
+template <int MODE>
+__global__ void __launch_bounds__(MC_TILE) mc_scan_kernel(
+    uint32_t P, const uint32_t *__restrict__ sk, const uint32_t *__restrict__ sv, const uint32_t *__restrict__ owner,
+    const uint64_t *__restrict__ lsb, const uint64_t *__restrict__ vm, const uint64_t *__restrict__ vl,
+    const int32_t *__restrict__ vn, const TsV *__restrict__ state, Comp *__restrict__ tile_comp,
+    const TsV *__restrict__ carry, TsV *__restrict__ prefix, TsV *__restrict__ state_out)
+{
+    __shared__ Comp buf[MC_TILE];
+    const uint32_t q = blockIdx.x * MC_TILE + threadIdx.x;
+    const bool live = q < P;
+    Comp c;
+    c.head = 0;
+    c.v.has = 0; c.v.msb = 0; c.v.lsb = 0; c.v.node = 0;
+    uint32_t key = 0;
+    TsV seed;
+    seed.has = 0; seed.msb = 0; seed.lsb = 0; seed.node = 0;
+    if (live) {
+        key = sk[q];
+        const uint32_t p = sv[q];
+        TsV v = elem_value(owner[p], lsb, vm, vl, vn);
+        c.head = (q == 0 || sk[q - 1] != key) ? 1u : 0u;
+        if (c.head) {
+            seed = state[key];
+            v = max_keep_old(seed, v);
+        }
+        c.v = v;
+    }
+    buf[threadIdx.x] = c;
+    __syncthreads();
+    for (uint32_t off = 1; off < MC_TILE; off <<= 1) {
+        Comp x = c;
+        if (threadIdx.x >= off) x = comp(buf[threadIdx.x - off], c);
+        __syncthreads();
+        buf[threadIdx.x] = x;
+        c = x;
+        __syncthreads();
+    }
+    if (MODE == 0) {
+        if (threadIdx.x == MC_TILE - 1) tile_comp[blockIdx.x] = c;
+        return;
+    }
+    if (!live) return;
+    const TsV cin = carry[blockIdx.x];
+    const TsV incl = c.head ? c.v : max_keep_old(cin, c.v);
+    TsV excl;
+    bool own_head = q == 0 || sk[q - 1] != key;
+    if (own_head) excl = seed;
+    else if (threadIdx.x == 0) excl = cin;
+    else {
+        const Comp pc = buf[threadIdx.x - 1];
+        excl = pc.head ? pc.v : max_keep_old(cin, pc.v);
+    }
+    prefix[sv[q]] = excl;
+    if (q + 1 == P || sk[q + 1] != key) state_out[key] = incl;
+}
+
+// Exclusive scan of the tile composites (one block): carry[t] = value open at the start of tile t
+__global__ void __launch_bounds__(MC_CARRY_THREADS) mc_carry_kernel(uint32_t ntiles, const Comp *__restrict__ tc,
+                                                                    TsV *__restrict__ carry)
+{
+    __shared__ Comp buf[MC_CARRY_THREADS];
+    const uint32_t per = (ntiles + MC_CARRY_THREADS - 1) / MC_CARRY_THREADS;
+    const uint32_t b = min(ntiles, threadIdx.x * per), e = min(ntiles, b + per);
+    Comp c;
+    c.head = 0; c.v.has = 0; c.v.msb = 0; c.v.lsb = 0; c.v.node = 0;
+    for (uint32_t i = b; i < e; ++i) c = comp(c, tc[i]);
+    buf[threadIdx.x] = c;
+    __syncthreads();
+    for (uint32_t off = 1; off < MC_CARRY_THREADS; off <<= 1) {
+        Comp x = c;
+        if (threadIdx.x >= off) x = comp(buf[threadIdx.x - off], c);
+        __syncthreads();
+        buf[threadIdx.x] = x;
+        c = x;
+        __syncthreads();
+    }
+    Comp run;
+    if (threadIdx.x == 0) { run.head = 0; run.v.has = 0; run.v.msb = 0; run.v.lsb = 0; run.v.node = 0; }
+    else run = buf[threadIdx.x - 1];
+    for (uint32_t i = b; i < e; ++i) {
+        carry[i] = run.v;
+        run = comp(run, tc[i]);
+    }
+}
+
+// txn-major fold of the pairs' prefixes in key order: foldl(keys, Timestamp::max(value, acc), NONE)
+__global__ void __launch_bounds__(256) mc_fold_kernel(uint32_t n, const uint64_t *__restrict__ msb,
+                                                      const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
+                                                      const uint32_t *__restrict__ key_off, const TsV *__restrict__ prefix,
+                                                      uint64_t *__restrict__ om, uint64_t *__restrict__ ol,
+                                                      int32_t *__restrict__ on, uint8_t *__restrict__ ohas,
+                                                      uint8_t *__restrict__ ofast)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    TsV acc;
+    acc.has = 0; acc.msb = 0; acc.lsb = 0; acc.node = 0;
+    for (uint32_t p = key_off[t]; p < key_off[t + 1]; ++p) {
+        const TsV x = prefix[p];
+        if (x.has && (!acc.has || tcmp(x, acc) >= 0)) acc = x;
+    }
+    om[t] = acc.msb; ol[t] = acc.lsb; on[t] = acc.node; ohas[t] = (uint8_t)acc.has;
+    ofast[t] = (uint8_t)(ts_cmp(msb[t], lsb[t], node[t], acc.msb, acc.lsb, acc.node) >= 0);
+}
+
+inline uint32_t bits_for_mc(uint32_t v)
+{
+    uint32_t b = 1;
+    while (b < 32 && (v >> b)) ++b;
+    return b;
+}
+
+} // namespace
+
+// --------------------------------------------------------------------------------- C ABI
+
+static int32_t mc_ensure_state(accord_store *s)
+{
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    if (s->mc_state.p) return ACCORD_OK;
+    HIPCHECK(s, s->mc_state.ensure((size_t)nkeys * sizeof(TsV)));
+    HIPCHECK(s, s->mc_state2.ensure((size_t)nkeys * sizeof(TsV)));
+    HIPCHECK(s, hipMemsetAsync(s->mc_state.p, 0, (size_t)nkeys * sizeof(TsV), s->stream));
+    return ACCORD_OK;
+}
+
+extern "C" int32_t accord_max_conflicts_reset(accord_store *s)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    int32_t rc = mc_ensure_state(s);
+    if (rc) return rc;
+    HIPCHECK(s, hipMemsetAsync(s->mc_state.p, 0, (size_t)(s->cfg.key_hi - s->cfg.key_lo) * sizeof(TsV), s->stream));
+    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    return ACCORD_OK;
+}
+
+extern "C" int32_t accord_max_conflicts_fold(accord_store *s, accord_max_conflicts_out *out)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (!s->has_batch) return fail(s, ACCORD_ERR_STATE, "accord_max_conflicts_fold before accord_batch_upload");
+    if (s->R) return fail(s, ACCORD_ERR_DOMAIN, "accord_max_conflicts_fold: range txns are not supported yet");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    int32_t rc = mc_ensure_state(s);
+    if (rc) return rc;
+    const uint32_t n = s->n, P = s->P, nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    hipStream_t st = s->stream;
+    DevBuf *T = s->op_tmp;   // pk, pv, sk, sv, tk, tv, owner, prefix, tile comps, carry, radix temp, outputs
+    HIPCHECK(s, T[0].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[1].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[2].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[3].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[4].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[5].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[6].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[7].ensure((size_t)P * sizeof(TsV) + 32));
+    const uint32_t ntiles = (P + MC_TILE - 1) / MC_TILE;
+    HIPCHECK(s, T[8].ensure((size_t)ntiles * sizeof(Comp) + 64));
+    HIPCHECK(s, T[9].ensure((size_t)ntiles * sizeof(TsV) + 32));
+    HIPCHECK(s, T[10].ensure(accord::radix_sort_temp_bytes(P)));
+    HIPCHECK(s, s->mc_out.ensure((size_t)n * 22 + 64));
+    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    uint64_t *om = s->mc_out.as<uint64_t>(), *ol = om + n;
+    int32_t *on = (int32_t *)(ol + n);
+    uint8_t *ohas = (uint8_t *)(on + n), *ofast = ohas + n;
+    const uint64_t *vm = s->has_exec ? s->exec_msb.as<uint64_t>() : s->msb.as<uint64_t>();
+    const uint64_t *vl = s->has_exec ? s->exec_lsb.as<uint64_t>() : s->lsb.as<uint64_t>();
+    const int32_t *vn = s->has_exec ? s->exec_node.as<int32_t>() : s->node.as<int32_t>();
+
+    if (s->events) HIPCHECK(s, hipEventRecord(s->ev[EV_OP_START], st));
+    HIPCHECK(s, hipMemsetAsync(dev, 0xFF, sizeof(HostTotals), st));
+    if (n) {
+        const uint32_t g = (n + 255) / 256;
+        mc_pack_kernel<<<g, 256, 0, st>>>(n, s->lsb.as<uint64_t>(), s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(),
+                                          s->cfg.key_lo, s->cfg.key_hi, T[0].as<uint32_t>(), T[1].as<uint32_t>(),
+                                          &dev->status);
+        mc_owner_kernel<<<g, 256, 0, st>>>(n, s->key_off.as<uint32_t>(), T[6].as<uint32_t>());
+    }
+    if (P) {
+        accord::radix_sort_pairs(T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[2].as<uint32_t>(), T[3].as<uint32_t>(),
+                                 T[4].as<uint32_t>(), T[5].as<uint32_t>(), nullptr, nullptr, nullptr, P,
+                                 (int)bits_for_mc(nkeys ? nkeys - 1 : 0), T[10].p, st);
+        HIPCHECK(s, hipMemcpyAsync(s->mc_state2.p, s->mc_state.p, (size_t)nkeys * sizeof(TsV), hipMemcpyDeviceToDevice, st));
+        mc_scan_kernel<0><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[6].as<uint32_t>(),
+                                                      s->lsb.as<uint64_t>(), vm, vl, vn, s->mc_state.as<TsV>(),
+                                                      T[8].as<Comp>(), nullptr, nullptr, nullptr);
+        mc_carry_kernel<<<1, MC_CARRY_THREADS, 0, st>>>(ntiles, T[8].as<Comp>(), T[9].as<TsV>());
+        mc_scan_kernel<1><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[6].as<uint32_t>(),
+                                                      s->lsb.as<uint64_t>(), vm, vl, vn, s->mc_state.as<TsV>(),
+                                                      nullptr, T[9].as<TsV>(), T[7].as<TsV>(), s->mc_state2.as<TsV>());
+    }
+    if (n)
+        mc_fold_kernel<<<(n + 255) / 256, 256, 0, st>>>(n, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(),
+                                                        s->node.as<int32_t>(), s->key_off.as<uint32_t>(), T[7].as<TsV>(),
+                                                        om, ol, on, ohas, ofast);
+    if (s->events) HIPCHECK(s, hipEventRecord(s->ev[EV_OP_END], st));
+    HIPCHECK(s, hipGetLastError());
+    accord::DevStatus hs;
+    HIPCHECK(s, hipMemcpyAsync(&hs, &dev->status, sizeof(hs), hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    if (hs.first != ~0ull) {
+        const uint32_t txn = (uint32_t)(hs.first >> 32);
+        const int32_t code = -(int32_t)(uint32_t)hs.first;
+        return fail(s, code, "accord_max_conflicts_fold: txn %u rejected (code %d)", txn, code);
+    }
+    if (P) std::swap(s->mc_state, s->mc_state2);   // the batch's updates become the store's map
+    if (s->events) HIPCHECK(s, hipEventElapsedTime(&s->ops_ms, s->ev[EV_OP_START], s->ev[EV_OP_END]));
+    if (out) {
+        if (out->msb) HIPCHECK(s, hipMemcpyAsync(out->msb, om, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+        if (out->lsb) HIPCHECK(s, hipMemcpyAsync(out->lsb, ol, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+        if (out->node) HIPCHECK(s, hipMemcpyAsync(out->node, on, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+        if (out->present) HIPCHECK(s, hipMemcpyAsync(out->present, ohas, n, hipMemcpyDeviceToHost, st));
+        if (out->fast) HIPCHECK(s, hipMemcpyAsync(out->fast, ofast, n, hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+    }
+    return ACCORD_OK;
+}
+
+extern "C" int32_t accord_max_conflicts_state(accord_store *s, uint64_t *msb, uint64_t *lsb, int32_t *node,
+                                              uint8_t *present)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (!msb || !lsb || !node || !present) return fail(s, ACCORD_ERR_ARG, "null output array");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    int32_t rc = mc_ensure_state(s);
+    if (rc) return rc;
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    std::vector<TsV> h(nkeys);
+    HIPCHECK(s, hipMemcpyAsync(h.data(), s->mc_state.p, (size_t)nkeys * sizeof(TsV), hipMemcpyDeviceToHost, s->stream));
+    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    for (uint32_t k = 0; k < nkeys; ++k) {
+        msb[k] = h[k].msb; lsb[k] = h[k].lsb; node[k] = h[k].node; present[k] = (uint8_t)(h[k].has != 0);
+    }
+    return ACCORD_OK;
+}

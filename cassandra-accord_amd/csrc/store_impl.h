@@ -102,6 +102,8 @@ struct accord_store {
     DepSet ds[2];
     int ds_cur = -1;
     DevBuf op_tmp[24];
+    // MaxConflicts (maxconflicts.hip): per-key map (double-buffered) and the last fold's outputs
+    DevBuf mc_state, mc_state2, mc_out;
     float ops_ms = 0;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;

@@ -199,6 +199,30 @@ void    accord_deps_inverse_release(accord_deps_inverse *inv);
 /* device ms of the last union / slice / invert (ACCORD_STORE_PROFILE stores, else 0) */
 int32_t accord_ops_timing(accord_store *store, float *ms);
 
+/* ---- MaxConflicts fold ----
+ * Replaces, for the uploaded batch of key txns in stream order, the per-PreAccept
+ *   Timestamp minNonConflicting = maxConflicts.get(keys)          (local/CommandStore.java:344,
+ *                                                                  local/MaxConflicts.java:46-49)
+ *   permitFastPath && txnId.compareTo(minNonConflicting) >= 0     (local/CommandStore.java:345)
+ * followed by CommandStore.updateMaxConflicts(prev, updated) with the command's executeAt
+ * (local/CommandStore.java:280-289, local/SafeCommandStore.java:192-210: globally visible kinds
+ * only).  executeAt = the batch's exec_* when given (Accept batch), else txnId (fast path).  The
+ * map lives on the device with the store (CommandStore.maxConflicts, empty at create) and carries
+ * over between batches.  present[i] = 0 means Timestamp.NONE (no entry on any key).  The epoch
+ * check and rejectBefore/preAcceptTimeout expiry (:328-331) are time-dependent and stay in Java.
+ * Range txns: ACCORD_ERR_DOMAIN (not supported yet). */
+typedef struct {
+    uint64_t *msb, *lsb;        /* [n] minNonConflicting (host arrays, caller-owned; NULL = skip) */
+    int32_t  *node;
+    uint8_t  *present;          /* [n] */
+    uint8_t  *fast;             /* [n] txnId >= minNonConflicting */
+} accord_max_conflicts_out;
+int32_t accord_max_conflicts_fold(accord_store *store, accord_max_conflicts_out *out);
+int32_t accord_max_conflicts_reset(accord_store *store);     /* MaxConflicts.EMPTY */
+/* the per-key map, [key_hi - key_lo] entries (present = 0: no entry) */
+int32_t accord_max_conflicts_state(accord_store *store, uint64_t *msb, uint64_t *lsb, int32_t *node,
+                                   uint8_t *present);
+
 /* ---- WaitingOn + execution levelling (config 5) ----
  * Over the store's current computed deps (full stream: no txn_index, not merged), with every txn
  * STABLE, executeAt = txnId and none applied:

@@ -1445,3 +1445,52 @@ int or_deps_invert(const or_deps *d, int range, uint32_t *off, int32_t **out)
     *out = o;
     return 0;
 }
+
+/* ---- MaxConflicts fold (test infrastructure) ------------------------------------------------
+ * Literal restatement of the per-PreAccept executeAt proposal input for key txns:
+ *   CommandStore.preaccept reads  minNonConflicting = maxConflicts.get(keys)
+ *     (local/CommandStore.java:344, MaxConflicts.get = foldl(keys, Timestamp::max, NONE),
+ *      local/MaxConflicts.java:46-49; foldl visits only keys with a map entry, in key order, as
+ *      fold(value, acc): utils/ReducingRangeMap.java:55-57,117-140; Timestamp.max(a, b) =
+ *      a.compareTo(b) >= 0 ? a : b, primitives/Timestamp.java:265-268),
+ *   fast path iff txnId.compareTo(minNonConflicting) >= 0 (:345, epoch check excluded), and then
+ *   the command's executeAt is merged in (SafeCommandStore.update -> updateMaxConflicts,
+ *   local/SafeCommandStore.java:192-210 only for isGloballyVisible kinds, primitives/Txn.java:187-200;
+ *   CommandStore.updateMaxConflicts -> MaxConflicts.update = merge(this, create(keys, executeAt))
+ *   with Timestamp::max(old, new), local/CommandStore.java:280-289, local/MaxConflicts.java:68-80).
+ * The map is one entry per key ordinal (st_has = 0: no entry).  exec_* NULL: executeAt = txnId.
+ * Returns 0, or -4 for a key outside [key_lo, key_lo + nkeys). */
+int or_max_conflicts(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
+                     const uint32_t *key_off, const uint32_t *key_ord, const uint64_t *exec_msb,
+                     const uint64_t *exec_lsb, const int32_t *exec_node, uint32_t key_lo, uint32_t nkeys,
+                     uint64_t *st_msb, uint64_t *st_lsb, int32_t *st_node, uint8_t *st_has,
+                     uint64_t *o_msb, uint64_t *o_lsb, int32_t *o_node, uint8_t *o_has, uint8_t *o_fast)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        int has = 0;
+        uint64_t am = 0, al = 0;    /* Timestamp.NONE */
+        int32_t an = 0;
+        for (uint32_t p = key_off[i]; p < key_off[i + 1]; ++p) {
+            if (key_ord[p] < key_lo || key_ord[p] - key_lo >= nkeys) return -4;
+            uint32_t k = key_ord[p] - key_lo;
+            if (!st_has[k]) continue;
+            if (!has || or_ts_compare(st_msb[k], st_lsb[k], st_node[k], am, al, an) >= 0) {
+                am = st_msb[k]; al = st_lsb[k]; an = st_node[k];
+            }
+            has = 1;
+        }
+        o_msb[i] = am; o_lsb[i] = al; o_node[i] = an; o_has[i] = (uint8_t)has;
+        o_fast[i] = (uint8_t)(or_ts_compare(msb[i], lsb[i], node[i], am, al, an) >= 0);
+        if (is_globally_visible(kind_of(lsb[i])) != 1) continue;
+        const uint64_t em = exec_msb ? exec_msb[i] : msb[i], el = exec_msb ? exec_lsb[i] : lsb[i];
+        const int32_t en = exec_msb ? exec_node[i] : node[i];
+        for (uint32_t p = key_off[i]; p < key_off[i + 1]; ++p) {
+            uint32_t k = key_ord[p] - key_lo;
+            /* merge keeps the old value unless the new one is strictly greater */
+            if (!st_has[k] || or_ts_compare(em, el, en, st_msb[k], st_lsb[k], st_node[k]) > 0) {
+                st_msb[k] = em; st_lsb[k] = el; st_node[k] = en; st_has[k] = 1;
+            }
+        }
+    }
+    return 0;
+}

@@ -19,6 +19,7 @@ ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
 _u32p = C.POINTER(C.c_uint32)
 _i32p = C.POINTER(C.c_int32)
 _u64p = C.POINTER(C.c_uint64)
+_u8p = C.POINTER(C.c_uint8)
 
 
 class _OrStream(C.Structure):
@@ -50,6 +51,9 @@ def lib():
         L.or_stream_deps_literal_prefix.argtypes = [C.POINTER(_OrStream), C.c_uint32, C.POINTER(_OrDeps)]
         L.or_deps_free.argtypes = [C.POINTER(_OrDeps)]
         L.or_deps_free.restype = None
+        L.or_max_conflicts.argtypes = ([C.c_uint32, _u64p, _u64p, _i32p, _u32p, _u32p, _u64p, _u64p, _i32p,
+                                        C.c_uint32, C.c_uint32, _u64p, _u64p, _i32p, _u8p]
+                                       + [_u64p, _u64p, _i32p, _u8p, _u8p])
         L.or_ts_compare.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         L.or_ts_equals.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         L.or_keydeps_build.argtypes = [C.c_uint32, _u32p, _u32p, C.c_uint32, _u64p, _u64p, _i32p,
@@ -286,3 +290,33 @@ def deps_invert(p: PartialDeps, range_side: bool = False):
     a = _arr(out, int(off[-1]), np.int32)
     C.CDLL(None).free(out)
     return off, a
+
+
+def max_conflicts(s, key_lo: int, nkeys: int, state=None):
+    """or_max_conflicts: per-txn (msb, lsb, node, present, fast) and the updated per-key map.
+    `state` = (msb, lsb, node, present) arrays of nkeys entries (None = MaxConflicts.EMPTY)."""
+    import numpy as np
+    n = len(s.msb)
+    if state is None:
+        state = (np.zeros(nkeys, np.uint64), np.zeros(nkeys, np.uint64), np.zeros(nkeys, np.int32),
+                 np.zeros(nkeys, np.uint8))
+    st = tuple(np.array(a, copy=True) for a in state)
+    msb = np.ascontiguousarray(s.msb, np.uint64); lsb = np.ascontiguousarray(s.lsb, np.uint64)
+    node = np.ascontiguousarray(s.node, np.int32)
+    ko = np.ascontiguousarray(s.key_off, np.uint32); kk = np.ascontiguousarray(s.key_ord, np.uint32)
+    ex = getattr(s, "exec_msb", None)
+    em = el = en = None
+    if ex is not None:
+        em = np.ascontiguousarray(s.exec_msb, np.uint64); el = np.ascontiguousarray(s.exec_lsb, np.uint64)
+        en = np.ascontiguousarray(s.exec_node, np.int32)
+    out = (np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(n, np.int32), np.zeros(n, np.uint8),
+           np.zeros(n, np.uint8))
+    p = lambda a, t: None if a is None else a.ctypes.data_as(t)
+    rc = lib().or_max_conflicts(n, p(msb, _u64p), p(lsb, _u64p), p(node, _i32p), p(ko, _u32p), p(kk, _u32p),
+                                p(em, _u64p), p(el, _u64p), p(en, _i32p), key_lo, nkeys,
+                                p(st[0], _u64p), p(st[1], _u64p), p(st[2], _i32p), p(st[3], _u8p),
+                                p(out[0], _u64p), p(out[1], _u64p), p(out[2], _i32p), p(out[3], _u8p),
+                                p(out[4], _u8p))
+    if rc != 0:
+        raise OracleError(rc)
+    return out, st

@@ -1,0 +1,152 @@
+"""MaxConflicts fold (local/MaxConflicts.java:46-80,
+local/CommandStore.java:280-289,320-349, local/SafeCommandStore.java:192-210).
+
+CPU half: the oracle restatement (or_max_conflicts) against hand-derived known answers.  GPU half
+(`-m gpu`): accord_max_conflicts_fold through the C ABI, bit-exact against the oracle on seeded
+PreAccept and Accept streams, the per-key map carried across batches, tie handling and errors.
+The reference has no MaxConflicts test of its own; parity rests on the restatement + these KATs."""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from accord_amd import Stream, generate_stream
+import oracle_lib as O
+
+KIND = {"R": 0, "W": 1, "ER": 2, "SP": 3}
+
+
+def mk(txns, execs=None):
+    """txns: [(hlc, kind, node, [keys])] in TxnId order (epoch 1); execs: [(hlc, node, low16)] or None."""
+    n = len(txns)
+    msb = np.full(n, 1 << 16, np.uint64)          # epoch 1 in the msb's high bits (Timestamp.java:77-79)
+    lsb = np.array([(h << 16) | (KIND[k] << 1) for h, k, _, _ in txns], np.uint64)
+    node = np.array([nd for _, _, nd, _ in txns], np.int32)
+    key_off = np.zeros(n + 1, np.uint32)
+    key_off[1:] = np.cumsum([len(ks) for *_, ks in txns])
+    key_ord = np.array([k for *_, ks in txns for k in ks], np.uint32)
+    z = np.zeros(n + 1, np.uint32)
+    s = Stream(msb, lsb, node, key_off, key_ord, z, np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+    if execs is not None:
+        s = dataclasses.replace(s, exec_msb=msb.copy(),
+                                exec_lsb=np.array([(h << 16) | lo for h, _, lo in execs], np.uint64),
+                                exec_node=np.array([nd for _, nd, _ in execs], np.int32))
+    return s
+
+
+def test_kat_empty_map_is_none_and_fast():
+    (m, l, nd, present, fast), st = O.max_conflicts(mk([(10, "W", 1, [0, 3])]), 0, 8)
+    assert present.tolist() == [0] and fast.tolist() == [1] and (m[0], l[0], nd[0]) == (0, 0, 0)
+    assert st[3].tolist() == [1, 0, 0, 1, 0, 0, 0, 0]
+
+
+def test_kat_max_over_keys_and_ephemeral_read_invisible():
+    # t0 W{1} t1 ER{2} t2 R{1,2}: t2 sees t0 on key 1 only (ER is not globally visible, Txn.java:187-200)
+    s = mk([(10, "W", 1, [1]), (11, "ER", 1, [2]), (12, "R", 2, [1, 2])])
+    (m, l, nd, present, fast), st = O.max_conflicts(s, 0, 4)
+    assert present.tolist() == [0, 0, 1] and fast.tolist() == [1, 1, 1]
+    assert (l[2] >> 16, nd[2]) == (10, 1)
+    assert st[3].tolist() == [0, 1, 1, 0]   # t2 itself lands on keys 1 and 2
+
+
+def test_kat_accept_executeat_forces_slow_path():
+    # t0's executeAt (hlc 50) lies after t1's TxnId (hlc 20): t1 is not fast, t2 (hlc 60) is
+    s = mk([(10, "W", 1, [0]), (20, "W", 1, [0]), (60, "R", 1, [0])], execs=[(50, 3, 0), (20, 1, 2), (60, 1, 0)])
+    (m, l, nd, present, fast), _ = O.max_conflicts(s, 0, 1)
+    assert fast.tolist() == [1, 0, 1]
+    assert (l[1] >> 16, nd[1]) == (50, 3) and (l[2] >> 16, nd[2]) == (50, 3)
+
+
+def test_kat_ties_merge_keeps_old_fold_takes_later_key():
+    # two executeAts that compare equal (bit 5 of lsb is outside the compared flags) but differ in bits
+    s = mk([(10, "W", 1, [0]), (11, "W", 1, [0, 1]), (12, "R", 1, [0, 1])],
+           execs=[(40, 2, 0x20), (40, 2, 0x00), (12, 1, 0)])
+    (m, l, nd, present, fast), st = O.max_conflicts(s, 0, 2)
+    # key 0 keeps t0's bits (merge: Timestamp.max(old, new) keeps old on a tie); key 1 holds t1's
+    assert st[1][0] & 0xFFFF == 0x20 and st[1][1] & 0xFFFF == 0x00
+    # t2 folds key 0 then key 1 with Timestamp.max(value, acc): the tie takes key 1's value
+    assert l[2] & 0xFFFF == 0x00
+
+
+def test_kat_state_carries_over():
+    a = mk([(10, "W", 1, [0])])
+    _, st = O.max_conflicts(a, 0, 2)
+    (m, l, nd, present, fast), _ = O.max_conflicts(mk([(5, "R", 1, [0])]), 0, 2, st)
+    assert present.tolist() == [1] and fast.tolist() == [0]
+
+
+# ------------------------------------------------------------------------------------------ GPU
+def gpu_fold(streams, keyspace):
+    from accord_amd import CommandStore
+    outs = []
+    with CommandStore(device=0, key_lo=0, key_hi=keyspace, window=0) as st:
+        for s in streams:
+            outs.append(st.max_conflicts_fold(s))
+        return outs, st.max_conflicts_state()
+
+
+def check(streams, keyspace):
+    got, gst = gpu_fold(streams, keyspace)
+    state = None
+    for s, g in zip(streams, got):
+        want, state = O.max_conflicts(s, 0, keyspace, state)
+        for a, b, name in zip(g, want, ("msb", "lsb", "node", "present", "fast")):
+            assert np.array_equal(a, b), (name, int(np.flatnonzero(a != b)[0]))
+    for a, b in zip(gst, state):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", [test_kat_empty_map_is_none_and_fast, test_kat_max_over_keys_and_ephemeral_read_invisible])
+def test_gpu_kat_streams(gpu_device, fn):
+    s = {test_kat_empty_map_is_none_and_fast: mk([(10, "W", 1, [0, 3])]),
+         test_kat_max_over_keys_and_ephemeral_read_invisible: mk([(10, "W", 1, [1]), (11, "ER", 1, [2]), (12, "R", 2, [1, 2])])}[fn]
+    check([s], 8)
+
+
+@pytest.mark.gpu
+def test_gpu_ties_and_accept(gpu_device):
+    check([mk([(10, "W", 1, [0]), (11, "W", 1, [0, 1]), (12, "R", 1, [0, 1])],
+              execs=[(40, 2, 0x20), (40, 2, 0x00), (12, 1, 0)])], 2)
+    check([mk([(10, "W", 1, [0]), (20, "W", 1, [0]), (60, "R", 1, [0])], execs=[(50, 3, 0), (20, 1, 2), (60, 1, 0)])], 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,ks,z,seed,frac,delay", [
+    (1, 1, 10, 0.0, 1, 0.0, 0),
+    (5000, 4, 300, 0.0, 2, 0.0, 0),
+    (20000, 8, 2000, 0.99, 3, 1.0, 500),
+    (30000, 8, 50, 0.99, 4, 0.7, 5000),       # hot keys: segments span many 1024-pair tiles
+    (4000, 12, 100000, 0.99, 5, 0.5, 64),
+    (50000, 1, 3, 0.0, 6, 1.0, 100000),
+])
+def test_gpu_vs_oracle(gpu_device, n, k, ks, z, seed, frac, delay):
+    s = generate_stream(n, k, ks, z, 0.5, seed=seed)
+    if frac:
+        s = s.accept(frac=frac, max_delay=delay, seed=seed)
+    check([s], ks)
+
+
+@pytest.mark.gpu
+def test_gpu_state_across_batches(gpu_device):
+    s = generate_stream(30000, 8, 3000, 0.99, 0.5, seed=8).accept(frac=0.5, max_delay=2000, seed=8)
+    check([s.prefix(10000), s.prefix(30000), s.prefix(7)], 3000)
+
+
+@pytest.mark.gpu
+def test_gpu_config2_full(gpu_device):
+    s = generate_stream(1 << 20, 8, 100_000, 0.99, 0.5, seed=2)
+    check([s], 100_000)
+
+
+@pytest.mark.gpu
+def test_gpu_errors(gpu_device):
+    from accord_amd import CommandStore, AccordError
+    with CommandStore(device=0, key_lo=0, key_hi=4, window=0) as st:
+        with pytest.raises(AccordError):
+            st.max_conflicts_fold(mk([(10, "W", 1, [5])]))      # key outside the store
+        # a rejected batch leaves the map untouched
+        assert st.max_conflicts_state()[3].sum() == 0
+        s = generate_stream(200, 2, 4, 0.0, 0.5, range_frac=0.5, range_len_max=2, seed=1)
+        with pytest.raises(AccordError):
+            st.max_conflicts_fold(s)
