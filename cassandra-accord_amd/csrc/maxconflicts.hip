@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t n, const uint64_t
                                                       const uint32_t *__restrict__ key_off,
                                                       const uint32_t *__restrict__ key_ord, uint32_t key_lo,
                                                       uint32_t key_hi, uint32_t *__restrict__ pk,
-                                                      uint32_t *__restrict__ pv, accord::DevStatus *st)
+                                                      uint32_t *__restrict__ pv, uint32_t *__restrict__ pe,
+                                                      accord::DevStatus *st)
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
@@ -84,18 +85,10 @@ __global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t n, const uint64_t
         const uint32_t k = key_ord[p];
         if (k < key_lo || k >= key_hi || (p > b && k <= prev)) record_error(st, t, ACCORD_ERR_KEYS);
         pk[p] = (k >= key_lo && k < key_hi) ? k - key_lo : 0;
-        pv[p] = p;
+        pv[p] = t;
+        pe[p] = p;
         prev = k;
     }
-}
-
-// pair -> txn (for the scan's element values)
-__global__ void __launch_bounds__(256) mc_owner_kernel(uint32_t n, const uint32_t *__restrict__ key_off,
-                                                       uint32_t *__restrict__ owner)
-{
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    for (uint32_t p = key_off[t]; p < key_off[t + 1]; ++p) owner[p] = t;
 }
 
 __device__ __forceinline__ TsV elem_value(uint32_t t, const uint64_t *lsb, const uint64_t *vm, const uint64_t *vl,
@@ -112,7 +105,8 @@ __device__ __forceinline__ TsV elem_value(uint32_t t, const uint64_t *lsb, const
 // tile's carry, write each pair's exclusive prefix (pair order) and each segment's final value.
 template <int MODE>
 __global__ void __launch_bounds__(MC_TILE) mc_scan_kernel(
-    uint32_t P, const uint32_t *__restrict__ sk, const uint32_t *__restrict__ sv, const uint32_t *__restrict__ owner,
+    uint32_t P, const uint32_t *__restrict__ sk, const uint32_t *__restrict__ sv, const uint32_t *__restrict__ se,
+    TsV *__restrict__ svals,
     const uint64_t *__restrict__ lsb, const uint64_t *__restrict__ vm, const uint64_t *__restrict__ vl,
     const int32_t *__restrict__ vn, const TsV *__restrict__ state, Comp *__restrict__ tile_comp,
     const TsV *__restrict__ carry, TsV *__restrict__ prefix, TsV *__restrict__ state_out)
@@ -128,8 +122,10 @@ __global__ void __launch_bounds__(MC_TILE) mc_scan_kernel(
     seed.has = 0; seed.msb = 0; seed.lsb = 0; seed.node = 0;
     if (live) {
         key = sk[q];
-        const uint32_t p = sv[q];
-        TsV v = elem_value(owner[p], lsb, vm, vl, vn);
+        // mode 0 gathers the txn's value once and leaves it in sorted order for mode 1
+        TsV v;
+        if (MODE == 0) { v = elem_value(sv[q], lsb, vm, vl, vn); svals[q] = v; }
+        else v = svals[q];
         c.head = (q == 0 || sk[q - 1] != key) ? 1u : 0u;
         if (c.head) {
             seed = state[key];
@@ -162,7 +158,7 @@ __global__ void __launch_bounds__(MC_TILE) mc_scan_kernel(
         const Comp pc = buf[threadIdx.x - 1];
         excl = pc.head ? pc.v : max_keep_old(cin, pc.v);
     }
-    prefix[sv[q]] = excl;
+    prefix[se[q]] = excl;
     if (q + 1 == P || sk[q + 1] != key) state_out[key] = incl;
 }
 
@@ -257,7 +253,7 @@ extern "C" int32_t accord_max_conflicts_fold(accord_store *s, accord_max_conflic
     if (rc) return rc;
     const uint32_t n = s->n, P = s->P, nkeys = s->cfg.key_hi - s->cfg.key_lo;
     hipStream_t st = s->stream;
-    DevBuf *T = s->op_tmp;   // pk, pv, sk, sv, tk, tv, owner, prefix, tile comps, carry, radix temp, outputs
+    DevBuf *T = s->op_tmp;   // pk, pv(txn), sk, sv, tk, tv, pe(pair), prefix, tile comps, carry, radix temp, se, te, sorted values
     HIPCHECK(s, T[0].ensure((size_t)P * 4 + 4));
     HIPCHECK(s, T[1].ensure((size_t)P * 4 + 4));
     HIPCHECK(s, T[2].ensure((size_t)P * 4 + 4));
@@ -270,6 +266,9 @@ extern "C" int32_t accord_max_conflicts_fold(accord_store *s, accord_max_conflic
     HIPCHECK(s, T[8].ensure((size_t)ntiles * sizeof(Comp) + 64));
     HIPCHECK(s, T[9].ensure((size_t)ntiles * sizeof(TsV) + 32));
     HIPCHECK(s, T[10].ensure(accord::radix_sort_temp_bytes(P)));
+    HIPCHECK(s, T[11].ensure((size_t)P * 4 + 4));                 // sorted pair index
+    HIPCHECK(s, T[12].ensure((size_t)P * 4 + 4));                 // its ping-pong buffer
+    HIPCHECK(s, T[13].ensure((size_t)P * sizeof(TsV) + 32));      // values in sorted order
     HIPCHECK(s, s->mc_out.ensure((size_t)n * 22 + 64));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     HostTotals *dev = s->status_totals.as<HostTotals>();
@@ -286,19 +285,19 @@ extern "C" int32_t accord_max_conflicts_fold(accord_store *s, accord_max_conflic
         const uint32_t g = (n + 255) / 256;
         mc_pack_kernel<<<g, 256, 0, st>>>(n, s->lsb.as<uint64_t>(), s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(),
                                           s->cfg.key_lo, s->cfg.key_hi, T[0].as<uint32_t>(), T[1].as<uint32_t>(),
-                                          &dev->status);
-        mc_owner_kernel<<<g, 256, 0, st>>>(n, s->key_off.as<uint32_t>(), T[6].as<uint32_t>());
+                                          T[6].as<uint32_t>(), &dev->status);
     }
     if (P) {
         accord::radix_sort_pairs(T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[2].as<uint32_t>(), T[3].as<uint32_t>(),
-                                 T[4].as<uint32_t>(), T[5].as<uint32_t>(), nullptr, nullptr, nullptr, P,
+                                 T[4].as<uint32_t>(), T[5].as<uint32_t>(), T[6].as<uint32_t>(), T[11].as<uint32_t>(),
+                                 T[12].as<uint32_t>(), P,
                                  (int)bits_for_mc(nkeys ? nkeys - 1 : 0), T[10].p, st);
         HIPCHECK(s, hipMemcpyAsync(s->mc_state2.p, s->mc_state.p, (size_t)nkeys * sizeof(TsV), hipMemcpyDeviceToDevice, st));
-        mc_scan_kernel<0><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[6].as<uint32_t>(),
+        mc_scan_kernel<0><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(), T[13].as<TsV>(),
                                                       s->lsb.as<uint64_t>(), vm, vl, vn, s->mc_state.as<TsV>(),
                                                       T[8].as<Comp>(), nullptr, nullptr, nullptr);
         mc_carry_kernel<<<1, MC_CARRY_THREADS, 0, st>>>(ntiles, T[8].as<Comp>(), T[9].as<TsV>());
-        mc_scan_kernel<1><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[6].as<uint32_t>(),
+        mc_scan_kernel<1><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(), T[13].as<TsV>(),
                                                       s->lsb.as<uint64_t>(), vm, vl, vn, s->mc_state.as<TsV>(),
                                                       nullptr, T[9].as<TsV>(), T[7].as<TsV>(), s->mc_state2.as<TsV>());
     }
