@@ -50,6 +50,7 @@ EXPORTED_SYMBOLS = [
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
+    "accord_max_conflicts_fold_from",
 ]
 
 
@@ -81,7 +82,8 @@ _u8p = C.POINTER(C.c_uint8)
 
 
 class _MaxConflictsOut(C.Structure):
-    _fields_ = [("msb", _u64p), ("lsb", _u64p), ("node", _i32p), ("present", _u8p), ("fast", _u8p)]
+    _fields_ = [("msb", _u64p), ("lsb", _u64p), ("node", _i32p), ("present", _u8p), ("fast", _u8p),
+                ("folded", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class _StoreCfg(C.Structure):
@@ -179,6 +181,8 @@ def lib() -> C.CDLL:
         L.accord_ops_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
         L.accord_deps_upload.argtypes = [C.c_void_p, C.POINTER(_Deps)]
         L.accord_max_conflicts_fold.argtypes = [C.c_void_p, C.POINTER(_MaxConflictsOut)]
+        L.accord_max_conflicts_fold_from.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_int32,
+                                                     C.POINTER(_MaxConflictsOut)]
         L.accord_max_conflicts_reset.argtypes = [C.c_void_p]
         L.accord_max_conflicts_state.argtypes = [C.c_void_p, _u64p, _u64p, _i32p, _u8p]
         for name in EXPORTED_SYMBOLS:
@@ -509,22 +513,35 @@ class CommandStore:
             lib().accord_deps_release(C.byref(d))
 
     # MaxConflicts (include/accord_deps.h; local/MaxConflicts.java, local/CommandStore.java:320-349)
-    def max_conflicts_fold(self, s: "Stream | None" = None, download: bool = True):
+    def max_conflicts_fold(self, s: "Stream | None" = None, download: bool = True, first: int = 0,
+                           exec_at=None, out=None):
         """For every txn of the uploaded batch (or `s`, uploaded first): minNonConflicting =
         maxConflicts.get(keys) before the txn's own update, and the fast-path test.  Returns
-        (msb, lsb, node, present, fast) numpy arrays, or None when download is False."""
+        (msb, lsb, node, present, fast, folded): numpy arrays over the batch and the number of txns
+        merged so far -- the fold stops at the first globally visible slow-path txn of a PreAccept
+        batch (its executeAt is the caller's uniqueNow); continue with first=folded and exec_at =
+        (msb, lsb, node) of that txn's executeAt, passing the previous result as `out`."""
         if s is not None:
             self.upload(s)
         if not download:
             self._check(lib().accord_max_conflicts_fold(self._h, None))
             return None
         n = self._n_uploaded if s is None else len(s.msb)
-        msb = np.zeros(n, np.uint64); lsb = np.zeros(n, np.uint64); node = np.zeros(n, np.int32)
-        present = np.zeros(n, np.uint8); fast = np.zeros(n, np.uint8)
+        if out is None:
+            msb = np.zeros(n, np.uint64); lsb = np.zeros(n, np.uint64); node = np.zeros(n, np.int32)
+            present = np.zeros(n, np.uint8); fast = np.zeros(n, np.uint8)
+        else:
+            msb, lsb, node, present, fast = out[:5]
         o = _MaxConflictsOut(msb.ctypes.data_as(_u64p), lsb.ctypes.data_as(_u64p), node.ctypes.data_as(_i32p),
-                             present.ctypes.data_as(_u8p), fast.ctypes.data_as(_u8p))
-        self._check(lib().accord_max_conflicts_fold(self._h, C.byref(o)))
-        return msb, lsb, node, present, fast
+                             present.ctypes.data_as(_u8p), fast.ctypes.data_as(_u8p), 0, 0)
+        if exec_at is None:
+            if first != 0:
+                raise IllegalArgumentException(-1, "a continued fold needs the executeAt of txn `first`")
+            self._check(lib().accord_max_conflicts_fold(self._h, C.byref(o)))
+        else:
+            em, el, en = exec_at
+            self._check(lib().accord_max_conflicts_fold_from(self._h, first, int(em), int(el), int(en), C.byref(o)))
+        return msb, lsb, node, present, fast, int(o.folded)
 
     def max_conflicts_reset(self):
         self._check(lib().accord_max_conflicts_reset(self._h))

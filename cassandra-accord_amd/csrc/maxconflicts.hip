@@ -64,40 +64,54 @@ __device__ __forceinline__ void record_error(accord::DevStatus *st, uint32_t i, 
     atomicMin(&st->first, v);
 }
 
-// txn-major: validate (key domain, kind, keys sorted-unique inside the store) and pack
-// (key, pair) for the sort
-__global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t n, const uint64_t *__restrict__ lsb,
+// txn-major over txns [first, last): validate (key domain, kind, keys sorted-unique inside the
+// store) and pack (key, txn, pair) for the sort; pair indices relative to key_off[first].
+// ExclusiveSyncPoint in the key domain is rejected: CommandStore.preaccept hands its keys to
+// markExclusiveSyncPoint as Ranges (local/CommandStore.java:335-339), so it has no key-domain
+// MaxConflicts reading.
+__global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ lsb,
                                                       const uint32_t *__restrict__ key_off,
                                                       const uint32_t *__restrict__ key_ord, uint32_t key_lo,
                                                       uint32_t key_hi, uint32_t *__restrict__ pk,
                                                       uint32_t *__restrict__ pv, uint32_t *__restrict__ pe,
                                                       accord::DevStatus *st)
 {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
+    const uint32_t t = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= last) return;
     const uint64_t l = lsb[t];
     const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
     if (domain != 0) record_error(st, t, ACCORD_ERR_DOMAIN);
-    if (kind > 4) record_error(st, t, ACCORD_ERR_KIND);
+    if (kind >= 4) record_error(st, t, ACCORD_ERR_KIND);
+    const uint32_t pbase = key_off[first];
     const uint32_t b = key_off[t], e = key_off[t + 1];
     uint32_t prev = 0;
     for (uint32_t p = b; p < e; ++p) {
         const uint32_t k = key_ord[p];
         if (k < key_lo || k >= key_hi || (p > b && k <= prev)) record_error(st, t, ACCORD_ERR_KEYS);
-        pk[p] = (k >= key_lo && k < key_hi) ? k - key_lo : 0;
-        pv[p] = t;
-        pe[p] = p;
+        pk[p - pbase] = (k >= key_lo && k < key_hi) ? k - key_lo : 0;
+        pv[p - pbase] = t;
+        pe[p - pbase] = p - pbase;
         prev = k;
     }
 }
 
-__device__ __forceinline__ TsV elem_value(uint32_t t, const uint64_t *lsb, const uint64_t *vm, const uint64_t *vl,
-                                          const int32_t *vn)
+// The executeAt a txn merges: the caller's value for txn ov_t (the continuation point of
+// accord_max_conflicts_fold_from), else the batch's exec_* (Accept batch) or the TxnId.
+struct McValues {
+    const uint64_t *vm, *vl;
+    const int32_t *vn;
+    uint32_t ov_t;
+    uint64_t ov_msb, ov_lsb;
+    int32_t ov_node;
+};
+
+__device__ __forceinline__ TsV elem_value(uint32_t t, const uint64_t *lsb, const McValues &mv)
 {
     TsV v;
     const uint32_t kind = (uint32_t)(lsb[t] >> 1) & 7;
     v.has = kind != 2u;          // EphemeralRead is not globally visible (LocalOnly rejected)
-    v.msb = vm[t]; v.lsb = vl[t]; v.node = vn[t];
+    if (t == mv.ov_t) { v.msb = mv.ov_msb; v.lsb = mv.ov_lsb; v.node = mv.ov_node; }
+    else { v.msb = mv.vm[t]; v.lsb = mv.vl[t]; v.node = mv.vn[t]; }
     return v;
 }
 
@@ -107,8 +121,7 @@ template <int MODE>
 __global__ void __launch_bounds__(MC_TILE) mc_scan_kernel(
     uint32_t P, const uint32_t *__restrict__ sk, const uint32_t *__restrict__ sv, const uint32_t *__restrict__ se,
     TsV *__restrict__ svals,
-    const uint64_t *__restrict__ lsb, const uint64_t *__restrict__ vm, const uint64_t *__restrict__ vl,
-    const int32_t *__restrict__ vn, const TsV *__restrict__ state, Comp *__restrict__ tile_comp,
+    const uint64_t *__restrict__ lsb, McValues mv, const TsV *__restrict__ state, Comp *__restrict__ tile_comp,
     const TsV *__restrict__ carry, TsV *__restrict__ prefix, TsV *__restrict__ state_out)
 {
     __shared__ Comp buf[MC_TILE];
@@ -124,7 +137,7 @@ __global__ void __launch_bounds__(MC_TILE) mc_scan_kernel(
         key = sk[q];
         // mode 0 gathers the txn's value once and leaves it in sorted order for mode 1
         TsV v;
-        if (MODE == 0) { v = elem_value(sv[q], lsb, vm, vl, vn); svals[q] = v; }
+        if (MODE == 0) { v = elem_value(sv[q], lsb, mv); svals[q] = v; }
         else v = svals[q];
         c.head = (q == 0 || sk[q - 1] != key) ? 1u : 0u;
         if (c.head) {
@@ -191,24 +204,32 @@ __global__ void __launch_bounds__(MC_CARRY_THREADS) mc_carry_kernel(uint32_t nti
     }
 }
 
-// txn-major fold of the pairs' prefixes in key order: foldl(keys, Timestamp::max(value, acc), NONE)
-__global__ void __launch_bounds__(256) mc_fold_kernel(uint32_t n, const uint64_t *__restrict__ msb,
+// txn-major fold of the pairs' prefixes in key order: foldl(keys, Timestamp::max(value, acc), NONE).
+// *stop = the first globally visible txn that takes the slow path with no executeAt known here: its
+// executeAt is time.uniqueNow(minNonConflicting) (local/CommandStore.java:348), chosen by the caller,
+// so neither it nor any later txn of the batch may be merged before the caller supplies it.
+__global__ void __launch_bounds__(256) mc_fold_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ msb,
                                                       const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
                                                       const uint32_t *__restrict__ key_off, const TsV *__restrict__ prefix,
                                                       uint64_t *__restrict__ om, uint64_t *__restrict__ ol,
                                                       int32_t *__restrict__ on, uint8_t *__restrict__ ohas,
-                                                      uint8_t *__restrict__ ofast)
+                                                      uint8_t *__restrict__ ofast, uint32_t known_exec, uint32_t ov_t,
+                                                      uint32_t *__restrict__ stop)
 {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
+    const uint32_t t = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= last) return;
+    const uint32_t pbase = key_off[first];
     TsV acc;
     acc.has = 0; acc.msb = 0; acc.lsb = 0; acc.node = 0;
     for (uint32_t p = key_off[t]; p < key_off[t + 1]; ++p) {
-        const TsV x = prefix[p];
+        const TsV x = prefix[p - pbase];
         if (x.has && (!acc.has || tcmp(x, acc) >= 0)) acc = x;
     }
     om[t] = acc.msb; ol[t] = acc.lsb; on[t] = acc.node; ohas[t] = (uint8_t)acc.has;
-    ofast[t] = (uint8_t)(ts_cmp(msb[t], lsb[t], node[t], acc.msb, acc.lsb, acc.node) >= 0);
+    const bool fast = ts_cmp(msb[t], lsb[t], node[t], acc.msb, acc.lsb, acc.node) >= 0;
+    ofast[t] = (uint8_t)fast;
+    const uint32_t kind = (uint32_t)(lsb[t] >> 1) & 7;
+    if (!fast && !known_exec && t != ov_t && kind != 2u) atomicMin(stop, t);
 }
 
 inline uint32_t bits_for_mc(uint32_t v)
@@ -243,24 +264,68 @@ extern "C" int32_t accord_max_conflicts_reset(accord_store *s)
     return ACCORD_OK;
 }
 
-extern "C" int32_t accord_max_conflicts_fold(accord_store *s, accord_max_conflicts_out *out)
+namespace {
+
+// One fold pass over txns [first, last): pack, stable sort by key, segmented scan seeded by the
+// store's map (written into mc_state2), and -- with outputs -- the per-txn fold and the stop index.
+int32_t mc_pass(accord_store *s, uint32_t first, uint32_t last, const McValues &mv, bool outputs, uint32_t *stop_dev)
+{
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    hipStream_t st = s->stream;
+    DevBuf *T = s->op_tmp;
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    uint64_t *om = s->mc_out.as<uint64_t>(), *ol = om + s->n;
+    int32_t *on = (int32_t *)(ol + s->n);
+    uint8_t *ohas = (uint8_t *)(on + s->n), *ofast = ohas + s->n;
+    std::vector<uint32_t> ko(2);
+    // pair range of [first, last): key_off is on the device; the host copy of the batch offsets
+    // is not kept, so read the two bounds
+    HIPCHECK(s, hipMemcpyAsync(&ko[0], s->key_off.as<uint32_t>() + first, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipMemcpyAsync(&ko[1], s->key_off.as<uint32_t>() + last, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    const uint32_t P = ko[1] - ko[0], nt = last - first;
+    const uint32_t ntiles = (P + MC_TILE - 1) / MC_TILE;
+    HIPCHECK(s, hipMemcpyAsync(s->mc_state2.p, s->mc_state.p, (size_t)nkeys * sizeof(TsV), hipMemcpyDeviceToDevice, st));
+    if (nt)
+        mc_pack_kernel<<<(nt + 255) / 256, 256, 0, st>>>(first, last, s->lsb.as<uint64_t>(), s->key_off.as<uint32_t>(),
+                                                         s->key_ord.as<uint32_t>(), s->cfg.key_lo, s->cfg.key_hi,
+                                                         T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[6].as<uint32_t>(),
+                                                         &dev->status);
+    if (P) {
+        accord::radix_sort_pairs(T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[2].as<uint32_t>(), T[3].as<uint32_t>(),
+                                 T[4].as<uint32_t>(), T[5].as<uint32_t>(), T[6].as<uint32_t>(), T[11].as<uint32_t>(),
+                                 T[12].as<uint32_t>(), P, (int)bits_for_mc(nkeys ? nkeys - 1 : 0), T[10].p, st);
+        mc_scan_kernel<0><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(),
+                                                      T[13].as<TsV>(), s->lsb.as<uint64_t>(), mv, s->mc_state.as<TsV>(),
+                                                      T[8].as<Comp>(), nullptr, nullptr, nullptr);
+        mc_carry_kernel<<<1, MC_CARRY_THREADS, 0, st>>>(ntiles, T[8].as<Comp>(), T[9].as<TsV>());
+        mc_scan_kernel<1><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(),
+                                                      T[13].as<TsV>(), s->lsb.as<uint64_t>(), mv, s->mc_state.as<TsV>(),
+                                                      nullptr, T[9].as<TsV>(), T[7].as<TsV>(), s->mc_state2.as<TsV>());
+    }
+    if (outputs && nt)
+        mc_fold_kernel<<<(nt + 255) / 256, 256, 0, st>>>(first, last, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(),
+                                                         s->node.as<int32_t>(), s->key_off.as<uint32_t>(), T[7].as<TsV>(),
+                                                         om, ol, on, ohas, ofast, s->has_exec ? 1u : 0u, mv.ov_t, stop_dev);
+    HIPCHECK(s, hipGetLastError());
+    return ACCORD_OK;
+}
+
+int32_t mc_fold(accord_store *s, uint32_t first, bool override, uint64_t ov_msb, uint64_t ov_lsb, int32_t ov_node,
+                accord_max_conflicts_out *out)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     if (!s->has_batch) return fail(s, ACCORD_ERR_STATE, "accord_max_conflicts_fold before accord_batch_upload");
     if (s->R) return fail(s, ACCORD_ERR_DOMAIN, "accord_max_conflicts_fold: range txns are not supported yet");
+    if (first != s->mc_next || first >= s->n + (s->n == 0 ? 1u : 0u))
+        return fail(s, ACCORD_ERR_STATE, "MaxConflicts fold of this batch must continue at txn %u (asked: %u)", s->mc_next, first);
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     int32_t rc = mc_ensure_state(s);
     if (rc) return rc;
-    const uint32_t n = s->n, P = s->P, nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    const uint32_t n = s->n, P = s->P;
     hipStream_t st = s->stream;
     DevBuf *T = s->op_tmp;   // pk, pv(txn), sk, sv, tk, tv, pe(pair), prefix, tile comps, carry, radix temp, se, te, sorted values
-    HIPCHECK(s, T[0].ensure((size_t)P * 4 + 4));
-    HIPCHECK(s, T[1].ensure((size_t)P * 4 + 4));
-    HIPCHECK(s, T[2].ensure((size_t)P * 4 + 4));
-    HIPCHECK(s, T[3].ensure((size_t)P * 4 + 4));
-    HIPCHECK(s, T[4].ensure((size_t)P * 4 + 4));
-    HIPCHECK(s, T[5].ensure((size_t)P * 4 + 4));
-    HIPCHECK(s, T[6].ensure((size_t)P * 4 + 4));
+    for (int b = 0; b < 7; ++b) HIPCHECK(s, T[b].ensure((size_t)P * 4 + 4));
     HIPCHECK(s, T[7].ensure((size_t)P * sizeof(TsV) + 32));
     const uint32_t ntiles = (P + MC_TILE - 1) / MC_TILE;
     HIPCHECK(s, T[8].ensure((size_t)ntiles * sizeof(Comp) + 64));
@@ -272,60 +337,64 @@ extern "C" int32_t accord_max_conflicts_fold(accord_store *s, accord_max_conflic
     HIPCHECK(s, s->mc_out.ensure((size_t)n * 22 + 64));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     HostTotals *dev = s->status_totals.as<HostTotals>();
-    uint64_t *om = s->mc_out.as<uint64_t>(), *ol = om + n;
-    int32_t *on = (int32_t *)(ol + n);
-    uint8_t *ohas = (uint8_t *)(on + n), *ofast = ohas + n;
-    const uint64_t *vm = s->has_exec ? s->exec_msb.as<uint64_t>() : s->msb.as<uint64_t>();
-    const uint64_t *vl = s->has_exec ? s->exec_lsb.as<uint64_t>() : s->lsb.as<uint64_t>();
-    const int32_t *vn = s->has_exec ? s->exec_node.as<int32_t>() : s->node.as<int32_t>();
+    uint32_t *stop_dev = (uint32_t *)&dev->totals[7];
+    McValues mv;
+    mv.vm = s->has_exec ? s->exec_msb.as<uint64_t>() : s->msb.as<uint64_t>();
+    mv.vl = s->has_exec ? s->exec_lsb.as<uint64_t>() : s->lsb.as<uint64_t>();
+    mv.vn = s->has_exec ? s->exec_node.as<int32_t>() : s->node.as<int32_t>();
+    mv.ov_t = override ? first : 0xFFFFFFFFu;
+    mv.ov_msb = ov_msb; mv.ov_lsb = ov_lsb; mv.ov_node = ov_node;
 
     if (s->events) HIPCHECK(s, hipEventRecord(s->ev[EV_OP_START], st));
     HIPCHECK(s, hipMemsetAsync(dev, 0xFF, sizeof(HostTotals), st));
-    if (n) {
-        const uint32_t g = (n + 255) / 256;
-        mc_pack_kernel<<<g, 256, 0, st>>>(n, s->lsb.as<uint64_t>(), s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(),
-                                          s->cfg.key_lo, s->cfg.key_hi, T[0].as<uint32_t>(), T[1].as<uint32_t>(),
-                                          T[6].as<uint32_t>(), &dev->status);
-    }
-    if (P) {
-        accord::radix_sort_pairs(T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[2].as<uint32_t>(), T[3].as<uint32_t>(),
-                                 T[4].as<uint32_t>(), T[5].as<uint32_t>(), T[6].as<uint32_t>(), T[11].as<uint32_t>(),
-                                 T[12].as<uint32_t>(), P,
-                                 (int)bits_for_mc(nkeys ? nkeys - 1 : 0), T[10].p, st);
-        HIPCHECK(s, hipMemcpyAsync(s->mc_state2.p, s->mc_state.p, (size_t)nkeys * sizeof(TsV), hipMemcpyDeviceToDevice, st));
-        mc_scan_kernel<0><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(), T[13].as<TsV>(),
-                                                      s->lsb.as<uint64_t>(), vm, vl, vn, s->mc_state.as<TsV>(),
-                                                      T[8].as<Comp>(), nullptr, nullptr, nullptr);
-        mc_carry_kernel<<<1, MC_CARRY_THREADS, 0, st>>>(ntiles, T[8].as<Comp>(), T[9].as<TsV>());
-        mc_scan_kernel<1><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(), T[13].as<TsV>(),
-                                                      s->lsb.as<uint64_t>(), vm, vl, vn, s->mc_state.as<TsV>(),
-                                                      nullptr, T[9].as<TsV>(), T[7].as<TsV>(), s->mc_state2.as<TsV>());
-    }
-    if (n)
-        mc_fold_kernel<<<(n + 255) / 256, 256, 0, st>>>(n, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(),
-                                                        s->node.as<int32_t>(), s->key_off.as<uint32_t>(), T[7].as<TsV>(),
-                                                        om, ol, on, ohas, ofast);
+    rc = mc_pass(s, first, n, mv, true, stop_dev);
+    if (rc) return rc;
     if (s->events) HIPCHECK(s, hipEventRecord(s->ev[EV_OP_END], st));
-    HIPCHECK(s, hipGetLastError());
-    accord::DevStatus hs;
-    HIPCHECK(s, hipMemcpyAsync(&hs, &dev->status, sizeof(hs), hipMemcpyDeviceToHost, st));
+    struct { accord::DevStatus status; uint32_t stop; } hs;
+    HIPCHECK(s, hipMemcpyAsync(&hs.status, &dev->status, sizeof(hs.status), hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipMemcpyAsync(&hs.stop, stop_dev, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
-    if (hs.first != ~0ull) {
-        const uint32_t txn = (uint32_t)(hs.first >> 32);
-        const int32_t code = -(int32_t)(uint32_t)hs.first;
+    if (hs.status.first != ~0ull) {
+        const uint32_t txn = (uint32_t)(hs.status.first >> 32);
+        const int32_t code = -(int32_t)(uint32_t)hs.status.first;
         return fail(s, code, "accord_max_conflicts_fold: txn %u rejected (code %d)", txn, code);
     }
-    if (P) std::swap(s->mc_state, s->mc_state2);   // the batch's updates become the store's map
+    const uint32_t folded = hs.stop < n ? hs.stop : n;
+    // a slow-path txn without a known executeAt: only [first, folded) may enter the map
+    if (folded < n && folded > first) {
+        rc = mc_pass(s, first, folded, mv, false, nullptr);
+        if (rc) return rc;
+    }
+    if (folded > first) std::swap(s->mc_state, s->mc_state2);   // the merged txns' updates become the store's map
+    s->mc_next = folded;
     if (s->events) HIPCHECK(s, hipEventElapsedTime(&s->ops_ms, s->ev[EV_OP_START], s->ev[EV_OP_END]));
     if (out) {
-        if (out->msb) HIPCHECK(s, hipMemcpyAsync(out->msb, om, (size_t)n * 8, hipMemcpyDeviceToHost, st));
-        if (out->lsb) HIPCHECK(s, hipMemcpyAsync(out->lsb, ol, (size_t)n * 8, hipMemcpyDeviceToHost, st));
-        if (out->node) HIPCHECK(s, hipMemcpyAsync(out->node, on, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-        if (out->present) HIPCHECK(s, hipMemcpyAsync(out->present, ohas, n, hipMemcpyDeviceToHost, st));
-        if (out->fast) HIPCHECK(s, hipMemcpyAsync(out->fast, ofast, n, hipMemcpyDeviceToHost, st));
+        uint64_t *om = s->mc_out.as<uint64_t>(), *ol = om + n;
+        int32_t *on = (int32_t *)(ol + n);
+        uint8_t *ohas = (uint8_t *)(on + n), *ofast = ohas + n;
+        const size_t m = (size_t)n - first;
+        if (out->msb && m) HIPCHECK(s, hipMemcpyAsync(out->msb + first, om + first, m * 8, hipMemcpyDeviceToHost, st));
+        if (out->lsb && m) HIPCHECK(s, hipMemcpyAsync(out->lsb + first, ol + first, m * 8, hipMemcpyDeviceToHost, st));
+        if (out->node && m) HIPCHECK(s, hipMemcpyAsync(out->node + first, on + first, m * 4, hipMemcpyDeviceToHost, st));
+        if (out->present && m) HIPCHECK(s, hipMemcpyAsync(out->present + first, ohas + first, m, hipMemcpyDeviceToHost, st));
+        if (out->fast && m) HIPCHECK(s, hipMemcpyAsync(out->fast + first, ofast + first, m, hipMemcpyDeviceToHost, st));
         HIPCHECK(s, hipStreamSynchronize(st));
+        out->folded = folded;
     }
     return ACCORD_OK;
+}
+
+} // namespace
+
+extern "C" int32_t accord_max_conflicts_fold(accord_store *s, accord_max_conflicts_out *out)
+{
+    return mc_fold(s, 0, false, 0, 0, 0, out);
+}
+
+extern "C" int32_t accord_max_conflicts_fold_from(accord_store *s, uint32_t first, uint64_t exec_msb, uint64_t exec_lsb,
+                                                  int32_t exec_node, accord_max_conflicts_out *out)
+{
+    return mc_fold(s, first, true, exec_msb, exec_lsb, exec_node, out);
 }
 
 extern "C" int32_t accord_max_conflicts_state(accord_store *s, uint64_t *msb, uint64_t *lsb, int32_t *node,

@@ -31,7 +31,7 @@ struct ShardComm {
     int nranks = 1, rank = 0;
     DevBuf ind, cscan, exp[3], bnd, counts, allcounts, recv;
     unsigned long long *total = nullptr;
-    DevBuf total_buf;
+    DevBuf total_buf, flag;
 };
 
 namespace accord_impl {
@@ -42,7 +42,7 @@ void shard_comm_destroy(accord_store *s)
     ShardComm *c = s->comm;
     if (c->comm) (void)ncclCommDestroy(c->comm);
     DevBuf *bufs[] = {&c->ind, &c->cscan, &c->exp[0], &c->exp[1], &c->exp[2], &c->bnd, &c->counts, &c->allcounts,
-                      &c->recv, &c->total_buf};
+                      &c->recv, &c->total_buf, &c->flag};
     for (DevBuf *b : bufs) b->release();
     delete c;
     s->comm = nullptr;
@@ -122,6 +122,15 @@ int32_t merge_parts(accord_store *s, const std::vector<Part> &parts, uint32_t n,
     return ACCORD_OK;
 }
 
+#define NCCLGROUPCHECK(s, expr)                                                                  \
+    do {                                                                                         \
+        ncclResult_t r_ = (expr);                                                                \
+        if (r_ != ncclSuccess) {                                                                 \
+            (void)ncclGroupEnd();                                                                \
+            return fail((s), ACCORD_ERR_HIP, "%s: %s", #expr, ncclGetErrorString(r_));           \
+        }                                                                                        \
+    } while (0)
+
 #define NCCLCHECK(s, expr)                                                                       \
     do {                                                                                         \
         ncclResult_t r_ = (expr);                                                                \
@@ -172,6 +181,11 @@ int32_t accord_comm_init(accord_store *s, int32_t nranks, int32_t rank, const vo
         delete c;
         return fail(s, ACCORD_ERR_HIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
     }
+    if (c->flag.ensure(16) != hipSuccess) {
+        (void)ncclCommDestroy(c->comm);
+        delete c;
+        return fail(s, ACCORD_ERR_OOM, "accord_comm_init: flag buffer");
+    }
     c->nranks = nranks;
     c->rank = rank;
     s->comm = c;
@@ -182,24 +196,52 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     if (!s->comm) return fail(s, ACCORD_ERR_STATE, "accord_deps_exchange_merge before accord_comm_init");
-    if (!s->computed || s->merged) return fail(s, ACCORD_ERR_STATE, "exchange needs a freshly computed partial");
-    if (s->tot_rngs || s->tot_rvals) return fail(s, ACCORD_ERR_STATE, "exchange of RangeDeps is not supported by this build");
-    if (!s->has_txn_index && s->n != n_total) return fail(s, ACCORD_ERR_ARG, "batch without txn_index must be the whole stream");
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     ShardComm *c = s->comm;
     const uint32_t G = (uint32_t)c->nranks, me = (uint32_t)c->rank, n = s->n;
     hipStream_t st = s->stream;
-    if (s->events) (void)hipEventRecord(s->ev[EV_XCHG_START], st);
 
-    // 1. partial offsets expanded to every global txn position
-    HIPCHECK(s, c->ind.ensure((size_t)n_total * 4 + 4));
-    HIPCHECK(s, c->cscan.ensure(((size_t)n_total + 1) * 4));
-    for (int a = 0; a < 3; ++a) HIPCHECK(s, c->exp[a].ensure(((size_t)n_total + 1) * 4));
-    HIPCHECK(s, c->bnd.ensure((size_t)3 * (G + 1) * 4));
-    HIPCHECK(s, c->total_buf.ensure(16));
-    HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n_total)));
+    // Every rank must reach the same collectives: the local checks and allocations run first, then
+    // one all-reduce (max) of their status agrees whether every rank goes ahead; a rank that failed
+    // keeps its own message, the others report that a peer failed.
+    std::vector<uint32_t> bnd(3 * (G + 1));
+    uint32_t *exp_off[3] = {nullptr, nullptr, nullptr};
+    auto prepare = [&]() -> int32_t {
+        if (!s->computed || s->merged) return fail(s, ACCORD_ERR_STATE, "exchange needs a freshly computed partial");
+        if (s->tot_rngs || s->tot_rvals) return fail(s, ACCORD_ERR_STATE, "exchange of RangeDeps is not supported by this build");
+        if (!s->has_txn_index && s->n != n_total) return fail(s, ACCORD_ERR_ARG, "batch without txn_index must be the whole stream");
+        // 1. partial offsets expanded to every global txn position
+        HIPCHECK(s, c->ind.ensure((size_t)n_total * 4 + 4));
+        HIPCHECK(s, c->cscan.ensure(((size_t)n_total + 1) * 4));
+        for (int a = 0; a < 3; ++a) HIPCHECK(s, c->exp[a].ensure(((size_t)n_total + 1) * 4));
+        HIPCHECK(s, c->bnd.ensure((size_t)3 * (G + 1) * 4));
+        HIPCHECK(s, c->total_buf.ensure(16));
+        HIPCHECK(s, c->counts.ensure(3 * (size_t)G * 8));
+        HIPCHECK(s, c->allcounts.ensure(3 * (size_t)G * 8 * G));
+        HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n_total)));
+        return ACCORD_OK;
+    };
+    // flag buffer: allocated by accord_comm_init, so agreeing cannot itself fail on one rank only
+    auto agree = [&](int32_t local_rc) -> int32_t {
+        const int32_t flag = local_rc ? 1 : 0;
+        int32_t *dflag = (int32_t *)c->flag.p;
+        int32_t any = 0;
+        if (hipMemcpyAsync(dflag, &flag, 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+            ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclMax, c->comm, st) != ncclSuccess ||
+            hipMemcpyAsync(&any, dflag, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return fail(s, ACCORD_ERR_HIP, "accord_deps_exchange_merge: status all-reduce failed");
+        if (local_rc) return local_rc;
+        if (any) return fail(s, ACCORD_ERR_STATE, "accord_deps_exchange_merge: a peer rank rejected the exchange");
+        return ACCORD_OK;
+    };
+    {
+        int32_t rc = agree(prepare());
+        if (rc) return rc;
+    }
+    if (s->events) (void)hipEventRecord(s->ev[EV_XCHG_START], st);
     const uint32_t *off[3] = {s->kd_key_off.as<uint32_t>(), s->kd_val_off.as<uint32_t>(), s->kd_k2v_off.as<uint32_t>()};
-    uint32_t *exp_off[3] = {c->exp[0].as<uint32_t>(), c->exp[1].as<uint32_t>(), c->exp[2].as<uint32_t>()};
+    for (int a = 0; a < 3; ++a) exp_off[a] = c->exp[a].as<uint32_t>();
     if (s->has_txn_index) {
         accord::launch_expand_offsets(n, n_total, s->txn_index.as<uint32_t>(), c->ind.as<uint32_t>(),
                                       c->cscan.as<uint32_t>(), off, exp_off, s->scan_tmp.p,
@@ -209,7 +251,6 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
             HIPCHECK(s, hipMemcpyAsync(exp_off[a], off[a], ((size_t)n_total + 1) * 4, hipMemcpyDeviceToDevice, st));
     }
     accord::launch_boundaries(G, n_total, exp_off, c->bnd.as<uint32_t>(), st);
-    std::vector<uint32_t> bnd(3 * (G + 1));
     HIPCHECK(s, hipMemcpyAsync(bnd.data(), c->bnd.p, bnd.size() * 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
 
@@ -218,8 +259,6 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
     std::vector<unsigned long long> mine(3 * (size_t)G);
     for (uint32_t d = 0; d < G; ++d)
         for (int a = 0; a < 3; ++a) mine[3 * d + a] = bnd[a * (G + 1) + d + 1] - bnd[a * (G + 1) + d];
-    HIPCHECK(s, c->counts.ensure(mine.size() * 8));
-    HIPCHECK(s, c->allcounts.ensure(mine.size() * 8 * G));
     HIPCHECK(s, hipMemcpyAsync(c->counts.p, mine.data(), mine.size() * 8, hipMemcpyHostToDevice, st));
     NCCLCHECK(s, ncclAllGather(c->counts.p, c->allcounts.p, mine.size(), ncclUint64, c->comm, st));
     std::vector<unsigned long long> all(mine.size() * G);
@@ -234,7 +273,12 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
         const unsigned long long *cnt = &all[(size_t)src * 3 * G + 3 * me];
         rbase[src + 1] = rbase[src] + 3 * ((size_t)nh + 1) + cnt[0] + cnt[1] + cnt[2];
     }
-    HIPCHECK(s, c->recv.ensure(rbase[G] * 4 + 16));
+    {
+        const hipError_t e = c->recv.ensure(rbase[G] * 4 + 16);
+        int32_t rc = agree(e == hipSuccess ? ACCORD_OK
+                                           : fail(s, ACCORD_ERR_OOM, "exchange receive buffer: %s", hipGetErrorString(e)));
+        if (rc) return rc;
+    }
     uint32_t *R = c->recv.as<uint32_t>();
     std::vector<Part> parts(G);
     for (uint32_t src = 0; src < G; ++src) {
@@ -261,8 +305,8 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
                     return fail(s, ACCORD_ERR_HIP, "local exchange copy failed");
                 }
             } else {
-                NCCLCHECK(s, ncclSend(so, (size_t)nd + 1, ncclUint32, (int)d, c->comm, st));
-                if (dc) NCCLCHECK(s, ncclSend(sd, dc, ncclUint32, (int)d, c->comm, st));
+                NCCLGROUPCHECK(s, ncclSend(so, (size_t)nd + 1, ncclUint32, (int)d, c->comm, st));
+                if (dc) NCCLGROUPCHECK(s, ncclSend(sd, dc, ncclUint32, (int)d, c->comm, st));
             }
         }
     }
@@ -272,8 +316,8 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
         for (int a = 0; a < 3; ++a) {
             uint32_t *ro = (uint32_t *)(a == 0 ? parts[src].key_off : a == 1 ? parts[src].val_off : parts[src].k2v_off);
             uint32_t *rd = (uint32_t *)(a == 0 ? parts[src].keys : a == 1 ? parts[src].vals : (const uint32_t *)parts[src].k2v);
-            NCCLCHECK(s, ncclRecv(ro, (size_t)nh + 1, ncclUint32, (int)src, c->comm, st));
-            if (cnt[a]) NCCLCHECK(s, ncclRecv(rd, cnt[a], ncclUint32, (int)src, c->comm, st));
+            NCCLGROUPCHECK(s, ncclRecv(ro, (size_t)nh + 1, ncclUint32, (int)src, c->comm, st));
+            if (cnt[a]) NCCLGROUPCHECK(s, ncclRecv(rd, cnt[a], ncclUint32, (int)src, c->comm, st));
         }
     }
     NCCLCHECK(s, ncclGroupEnd());

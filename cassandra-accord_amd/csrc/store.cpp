@@ -161,7 +161,7 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     if (s->rk_keys_total >= (1ull << 32))
         return fail(s, ACCORD_ERR_CAPACITY, "range txns cover %llu (txn, key) pairs, over 2^32",
                     (unsigned long long)s->rk_keys_total);
-    s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1;
+    s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->mc_next = 0;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
     HIPCHECK(s, s->node.ensure((size_t)n * 4));

@@ -104,6 +104,7 @@ struct accord_store {
     DevBuf op_tmp[24];
     // MaxConflicts (maxconflicts.hip): per-key map (double-buffered) and the last fold's outputs
     DevBuf mc_state, mc_state2, mc_out;
+    uint32_t mc_next = 0;          // next txn of the uploaded batch the fold continues at
     float ops_ms = 0;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;

@@ -206,18 +206,32 @@ int32_t accord_ops_timing(accord_store *store, float *ms);
  *   permitFastPath && txnId.compareTo(minNonConflicting) >= 0     (local/CommandStore.java:345)
  * followed by CommandStore.updateMaxConflicts(prev, updated) with the command's executeAt
  * (local/CommandStore.java:280-289, local/SafeCommandStore.java:192-210: globally visible kinds
- * only).  executeAt = the batch's exec_* when given (Accept batch), else txnId (fast path).  The
- * map lives on the device with the store (CommandStore.maxConflicts, empty at create) and carries
- * over between batches.  present[i] = 0 means Timestamp.NONE (no entry on any key).  The epoch
- * check and rejectBefore/preAcceptTimeout expiry (:328-331) are time-dependent and stay in Java.
+ * only).  The map lives on the device with the store (CommandStore.maxConflicts, empty at create)
+ * and carries over between batches.  present[i] = 0 means Timestamp.NONE (no entry on any key).
+ * The epoch check and rejectBefore/preAcceptTimeout expiry (:328-331) are time-dependent and stay
+ * in Java.
+ *
+ * executeAt of txn t = the batch's exec_* (Accept batch), else txnId when t takes the fast path.  A
+ * globally visible txn that takes the slow path in a PreAccept batch gets
+ * time.uniqueNow(minNonConflicting) (:348), a clock value only the caller can choose, and every
+ * later txn of the batch depends on it.  The fold therefore stops there: out->folded = the first
+ * such txn f (n when none).  Txns [first, f) are merged into the map; the outputs of txns
+ * [first, f] are final (f's own reading does not depend on f's executeAt).  The caller picks f's
+ * executeAt and continues with accord_max_conflicts_fold_from(store, f, executeAt, out), which
+ * merges it and folds on from there.  Folding a batch again from an earlier txn is ACCORD_ERR_STATE.
+ * ExclusiveSyncPoint in the key domain: ACCORD_ERR_KIND (preaccept casts its keys to Ranges, :335-339).
  * Range txns: ACCORD_ERR_DOMAIN (not supported yet). */
 typedef struct {
     uint64_t *msb, *lsb;        /* [n] minNonConflicting (host arrays, caller-owned; NULL = skip) */
     int32_t  *node;
     uint8_t  *present;          /* [n] */
     uint8_t  *fast;             /* [n] txnId >= minNonConflicting */
+    uint32_t  folded;           /* out: txns of the batch merged so far (see above) */
+    uint32_t  reserved;
 } accord_max_conflicts_out;
 int32_t accord_max_conflicts_fold(accord_store *store, accord_max_conflicts_out *out);
+int32_t accord_max_conflicts_fold_from(accord_store *store, uint32_t first, uint64_t exec_msb, uint64_t exec_lsb,
+                                       int32_t exec_node, accord_max_conflicts_out *out);
 int32_t accord_max_conflicts_reset(accord_store *store);     /* MaxConflicts.EMPTY */
 /* the per-key map, [key_hi - key_lo] entries (present = 0: no entry) */
 int32_t accord_max_conflicts_state(accord_store *store, uint64_t *msb, uint64_t *lsb, int32_t *node,

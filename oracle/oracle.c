@@ -1464,12 +1464,20 @@ int or_max_conflicts(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const
                      const uint32_t *key_off, const uint32_t *key_ord, const uint64_t *exec_msb,
                      const uint64_t *exec_lsb, const int32_t *exec_node, uint32_t key_lo, uint32_t nkeys,
                      uint64_t *st_msb, uint64_t *st_lsb, int32_t *st_node, uint8_t *st_has,
-                     uint64_t *o_msb, uint64_t *o_lsb, int32_t *o_node, uint8_t *o_has, uint8_t *o_fast)
+                     uint64_t *o_msb, uint64_t *o_lsb, int32_t *o_node, uint8_t *o_has, uint8_t *o_fast,
+                     uint32_t first, int has_override, uint64_t ov_msb, uint64_t ov_lsb, int32_t ov_node,
+                     uint32_t *folded)
 {
-    for (uint32_t i = 0; i < n; ++i) {
+    *folded = n;
+    for (uint32_t i = first; i < n; ++i) {
+        /* CommandStore.preaccept (local/CommandStore.java:320-349): ExclusiveSyncPoint returns before
+         * reading maxConflicts and treats its keys as Ranges (:335-339) -- no key-domain form */
+        const int kind = kind_of(lsb[i]);
+        if (kind >= 4 || (lsb[i] & 1)) return (lsb[i] & 1) ? -5 : -3;
         int has = 0;
         uint64_t am = 0, al = 0;    /* Timestamp.NONE */
         int32_t an = 0;
+        /* MaxConflicts.get = foldl(keys, Timestamp::max, NONE) (local/MaxConflicts.java:46-49) */
         for (uint32_t p = key_off[i]; p < key_off[i + 1]; ++p) {
             if (key_ord[p] < key_lo || key_ord[p] - key_lo >= nkeys) return -4;
             uint32_t k = key_ord[p] - key_lo;
@@ -1480,10 +1488,16 @@ int or_max_conflicts(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const
             has = 1;
         }
         o_msb[i] = am; o_lsb[i] = al; o_node[i] = an; o_has[i] = (uint8_t)has;
-        o_fast[i] = (uint8_t)(or_ts_compare(msb[i], lsb[i], node[i], am, al, an) >= 0);
-        if (is_globally_visible(kind_of(lsb[i])) != 1) continue;
-        const uint64_t em = exec_msb ? exec_msb[i] : msb[i], el = exec_msb ? exec_lsb[i] : lsb[i];
-        const int32_t en = exec_msb ? exec_node[i] : node[i];
+        const int fast = or_ts_compare(msb[i], lsb[i], node[i], am, al, an) >= 0;
+        o_fast[i] = (uint8_t)fast;
+        /* updateMaxConflicts: globally visible kinds only (local/SafeCommandStore.java:198-209) */
+        if (is_globally_visible(kind) != 1) continue;
+        uint64_t em, el;
+        int32_t en;
+        if (i == first && has_override) { em = ov_msb; el = ov_lsb; en = ov_node; }
+        else if (exec_msb) { em = exec_msb[i]; el = exec_lsb[i]; en = exec_node[i]; }
+        else if (fast) { em = msb[i]; el = lsb[i]; en = node[i]; }
+        else { *folded = i; return 0; }   /* executeAt = time.uniqueNow(minNonConflicting) (:348): the caller's */
         for (uint32_t p = key_off[i]; p < key_off[i + 1]; ++p) {
             uint32_t k = key_ord[p] - key_lo;
             /* merge keeps the old value unless the new one is strictly greater */

@@ -53,7 +53,8 @@ def lib():
         L.or_deps_free.restype = None
         L.or_max_conflicts.argtypes = ([C.c_uint32, _u64p, _u64p, _i32p, _u32p, _u32p, _u64p, _u64p, _i32p,
                                         C.c_uint32, C.c_uint32, _u64p, _u64p, _i32p, _u8p]
-                                       + [_u64p, _u64p, _i32p, _u8p, _u8p])
+                                       + [_u64p, _u64p, _i32p, _u8p, _u8p]
+                                       + [C.c_uint32, C.c_int, C.c_uint64, C.c_uint64, C.c_int32, _u32p])
         L.or_ts_compare.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         L.or_ts_equals.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         L.or_keydeps_build.argtypes = [C.c_uint32, _u32p, _u32p, C.c_uint32, _u64p, _u64p, _i32p,
@@ -292,10 +293,11 @@ def deps_invert(p: PartialDeps, range_side: bool = False):
     return off, a
 
 
-def max_conflicts(s, key_lo: int, nkeys: int, state=None):
-    """or_max_conflicts: per-txn (msb, lsb, node, present, fast) and the updated per-key map.
-    `state` = (msb, lsb, node, present) arrays of nkeys entries (None = MaxConflicts.EMPTY)."""
-    import numpy as np
+def max_conflicts(s, key_lo: int, nkeys: int, state=None, first: int = 0, exec_at=None, out=None):
+    """or_max_conflicts: per-txn (msb, lsb, node, present, fast), the updated per-key map and the
+    number of txns merged (`folded`: the fold stops at a slow-path txn whose executeAt is unknown).
+    `state` = (msb, lsb, node, present) arrays of nkeys entries (None = MaxConflicts.EMPTY);
+    first/exec_at continue a stopped fold with the caller's executeAt for txn `first`."""
     n = len(s.msb)
     if state is None:
         state = (np.zeros(nkeys, np.uint64), np.zeros(nkeys, np.uint64), np.zeros(nkeys, np.int32),
@@ -309,14 +311,20 @@ def max_conflicts(s, key_lo: int, nkeys: int, state=None):
     if ex is not None:
         em = np.ascontiguousarray(s.exec_msb, np.uint64); el = np.ascontiguousarray(s.exec_lsb, np.uint64)
         en = np.ascontiguousarray(s.exec_node, np.int32)
-    out = (np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(n, np.int32), np.zeros(n, np.uint8),
-           np.zeros(n, np.uint8))
+    if out is None:
+        out = (np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(n, np.int32), np.zeros(n, np.uint8),
+               np.zeros(n, np.uint8))
+    else:
+        out = tuple(np.array(a, copy=True) for a in out[:5])
+    folded = C.c_uint32(0)
+    ov = exec_at if exec_at is not None else (0, 0, 0)
     p = lambda a, t: None if a is None else a.ctypes.data_as(t)
     rc = lib().or_max_conflicts(n, p(msb, _u64p), p(lsb, _u64p), p(node, _i32p), p(ko, _u32p), p(kk, _u32p),
                                 p(em, _u64p), p(el, _u64p), p(en, _i32p), key_lo, nkeys,
                                 p(st[0], _u64p), p(st[1], _u64p), p(st[2], _i32p), p(st[3], _u8p),
                                 p(out[0], _u64p), p(out[1], _u64p), p(out[2], _i32p), p(out[3], _u8p),
-                                p(out[4], _u8p))
+                                p(out[4], _u8p), first, 1 if exec_at is not None else 0, int(ov[0]), int(ov[1]),
+                                int(ov[2]), C.byref(folded))
     if rc != 0:
         raise OracleError(rc)
-    return out, st
+    return out, st, int(folded.value)

@@ -69,3 +69,27 @@ def test_waiting_on_requires_full_stream(gpu_device):
         st.compute()
         with pytest.raises(IllegalStateException):
             st.waiting_on()
+
+
+@pytest.mark.timeout(900)
+def test_config5_full_size(gpu_device):
+    """BASELINE.json configs[4] at full size: 4,194,304 key txns, k = 4 over
+    10,000 keys, Zipf(0.99), 90% writes, W = 256, seed 5 -- deps byte-compared with the fast oracle,
+    then level[], wo_off and every bitset word with or_waiting_on over those deps."""
+    n, ks, W = 1 << 22, 10_000, 256
+    s = generate_stream(n, 4, ks, 0.99, 0.9, seed=5)
+    with CommandStore(device=0, key_lo=0, key_hi=ks, window=W) as st:
+        st.upload(s)
+        st.compute()
+        wo = st.waiting_on()
+        d = st.download()
+    want = O.deps_fast(s, W)
+    diff = d.first_difference(want)
+    assert diff is None, diff
+    del want
+    level, wo_off, words = O.waiting_on(d)
+    assert np.array_equal(wo.wo_off, wo_off)
+    assert np.array_equal(wo.words, words)
+    bad = np.nonzero(wo.level != level)[0]
+    assert bad.size == 0, (bad[:5], wo.level[bad[:5]], level[bad[:5]])
+    assert wo.max_level == int(level.max(initial=0))

@@ -13,7 +13,29 @@ import pytest
 from accord_amd import Stream, generate_stream
 import oracle_lib as O
 
-KIND = {"R": 0, "W": 1, "ER": 2, "SP": 3}
+KIND = {"R": 0, "W": 1, "ER": 2, "SP": 3, "XSP": 4}
+
+
+def unique_now(minimum, node=9):
+    """Stand-in for NodeTimeService.uniqueNow(atLeast) (local/CommandStore.java:348): a Timestamp
+    strictly after `minimum` -- the next hlc, flags 0, this node's id."""
+    m, l, _ = minimum
+    return int(m), ((int(l) >> 16) + 1) << 16, node
+
+
+def fold_all(fold, n):
+    """Drive a fold to the end of the batch the way a caller does: every stop is a globally visible
+    slow-path txn; give it uniqueNow(minNonConflicting) and continue.  `fold(first, exec_at, out)`
+    returns (out5, folded).  Returns the outputs and the executeAts chosen."""
+    out, folded = fold(0, None, None)
+    chosen = {}
+    while folded < n:
+        ex = unique_now((out[0][folded], out[1][folded], out[2][folded]))
+        chosen[folded] = ex
+        out, f2 = fold(folded, ex, out)
+        assert f2 > folded
+        folded = f2
+    return out, chosen
 
 
 def mk(txns, execs=None):
@@ -35,7 +57,7 @@ def mk(txns, execs=None):
 
 
 def test_kat_empty_map_is_none_and_fast():
-    (m, l, nd, present, fast), st = O.max_conflicts(mk([(10, "W", 1, [0, 3])]), 0, 8)
+    (m, l, nd, present, fast), st, _ = O.max_conflicts(mk([(10, "W", 1, [0, 3])]), 0, 8)
     assert present.tolist() == [0] and fast.tolist() == [1] and (m[0], l[0], nd[0]) == (0, 0, 0)
     assert st[3].tolist() == [1, 0, 0, 1, 0, 0, 0, 0]
 
@@ -43,7 +65,7 @@ def test_kat_empty_map_is_none_and_fast():
 def test_kat_max_over_keys_and_ephemeral_read_invisible():
     # t0 W{1} t1 ER{2} t2 R{1,2}: t2 sees t0 on key 1 only (ER is not globally visible, Txn.java:187-200)
     s = mk([(10, "W", 1, [1]), (11, "ER", 1, [2]), (12, "R", 2, [1, 2])])
-    (m, l, nd, present, fast), st = O.max_conflicts(s, 0, 4)
+    (m, l, nd, present, fast), st, _ = O.max_conflicts(s, 0, 4)
     assert present.tolist() == [0, 0, 1] and fast.tolist() == [1, 1, 1]
     assert (l[2] >> 16, nd[2]) == (10, 1)
     assert st[3].tolist() == [0, 1, 1, 0]   # t2 itself lands on keys 1 and 2
@@ -52,8 +74,8 @@ def test_kat_max_over_keys_and_ephemeral_read_invisible():
 def test_kat_accept_executeat_forces_slow_path():
     # t0's executeAt (hlc 50) lies after t1's TxnId (hlc 20): t1 is not fast, t2 (hlc 60) is
     s = mk([(10, "W", 1, [0]), (20, "W", 1, [0]), (60, "R", 1, [0])], execs=[(50, 3, 0), (20, 1, 2), (60, 1, 0)])
-    (m, l, nd, present, fast), _ = O.max_conflicts(s, 0, 1)
-    assert fast.tolist() == [1, 0, 1]
+    (m, l, nd, present, fast), _, folded = O.max_conflicts(s, 0, 1)
+    assert fast.tolist() == [1, 0, 1] and folded == 3    # Accept batch: every executeAt is known
     assert (l[1] >> 16, nd[1]) == (50, 3) and (l[2] >> 16, nd[2]) == (50, 3)
 
 
@@ -61,7 +83,7 @@ def test_kat_ties_merge_keeps_old_fold_takes_later_key():
     # two executeAts that compare equal (bit 5 of lsb is outside the compared flags) but differ in bits
     s = mk([(10, "W", 1, [0]), (11, "W", 1, [0, 1]), (12, "R", 1, [0, 1])],
            execs=[(40, 2, 0x20), (40, 2, 0x00), (12, 1, 0)])
-    (m, l, nd, present, fast), st = O.max_conflicts(s, 0, 2)
+    (m, l, nd, present, fast), st, _ = O.max_conflicts(s, 0, 2)
     # key 0 keeps t0's bits (merge: Timestamp.max(old, new) keeps old on a tie); key 1 holds t1's
     assert st[1][0] & 0xFFFF == 0x20 and st[1][1] & 0xFFFF == 0x00
     # t2 folds key 0 then key 1 with Timestamp.max(value, acc): the tie takes key 1's value
@@ -70,9 +92,39 @@ def test_kat_ties_merge_keeps_old_fold_takes_later_key():
 
 def test_kat_state_carries_over():
     a = mk([(10, "W", 1, [0])])
-    _, st = O.max_conflicts(a, 0, 2)
-    (m, l, nd, present, fast), _ = O.max_conflicts(mk([(5, "R", 1, [0])]), 0, 2, st)
+    _, st, _ = O.max_conflicts(a, 0, 2)
+    (m, l, nd, present, fast), _, folded = O.max_conflicts(mk([(5, "R", 1, [0])]), 0, 2, st)
     assert present.tolist() == [1] and fast.tolist() == [0]
+    assert folded == 0                    # slow-path read: its executeAt is the caller's uniqueNow
+
+
+def advice_stream():
+    # key 0 = A holds hlc 100 from an earlier batch, key 1 = B is empty.  t1 (hlc 50, {A, B}) is slow:
+    # the reference merges its executeAt uniqueNow(100) >= 101 on B too, so t2 (hlc 60, {B}) is slow
+    # as well -- folding with executeAt = txnId for t1 would make t2 fast (a wrong fast-path decision).
+    return mk([(100, "W", 1, [0])]), mk([(50, "W", 1, [0, 1]), (60, "W", 1, [1])])
+
+
+def test_kat_slow_path_executeat_is_merged_before_later_txns():
+    first, second = advice_stream()
+    _, st0, _ = O.max_conflicts(first, 0, 2)
+    state = st0
+
+    def fold(f, ex, out):
+        nonlocal state
+        o, state, folded = O.max_conflicts(second, 0, 2, state, first=f, exec_at=ex, out=out)
+        return o, folded
+    out, folded = fold(0, None, None)
+    assert folded == 0 and out[4][0] == 0                    # t1 stops the fold: slow, executeAt unknown
+    (m, l, nd, present, fast), chosen = fold_all(fold, 2)
+    assert fast.tolist() == [0, 0]                           # t2 sees t1's uniqueNow(100) on B
+    assert (l[1] >> 16) == 101 and chosen[0][1] >> 16 == 101
+
+
+def test_kat_exclusive_sync_point_key_domain_rejected():
+    with pytest.raises(O.OracleError) as e:
+        O.max_conflicts(mk([(10, "XSP", 1, [0])]), 0, 1)
+    assert e.value.rc == -3
 
 
 # ------------------------------------------------------------------------------------------ GPU
@@ -81,19 +133,52 @@ def gpu_fold(streams, keyspace):
     outs = []
     with CommandStore(device=0, key_lo=0, key_hi=keyspace, window=0) as st:
         for s in streams:
-            outs.append(st.max_conflicts_fold(s))
+            st.upload(s)
+
+            def fold(f, ex, out):
+                r = st.max_conflicts_fold(first=f, exec_at=ex, out=out)
+                return r[:5], r[5]
+            outs.append(fold_all(fold, s.n))
         return outs, st.max_conflicts_state()
 
 
 def check(streams, keyspace):
     got, gst = gpu_fold(streams, keyspace)
     state = None
-    for s, g in zip(streams, got):
-        want, state = O.max_conflicts(s, 0, keyspace, state)
+    for s, (g, gchosen) in zip(streams, got):
+        st0 = state
+
+        def fold(f, ex, out):
+            nonlocal state
+            o, state, folded = O.max_conflicts(s, 0, keyspace, state if f else st0, first=f, exec_at=ex, out=out)
+            return o, folded
+        want, chosen = fold_all(fold, s.n)
+        assert chosen == gchosen
         for a, b, name in zip(g, want, ("msb", "lsb", "node", "present", "fast")):
             assert np.array_equal(a, b), (name, int(np.flatnonzero(a != b)[0]))
     for a, b in zip(gst, state):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_slow_path_stops_and_continues(gpu_device):
+    first, second = advice_stream()
+    check([first, second], 2)
+    # a PreAccept stream whose later batches are slow on many keys: many stops and continuations
+    s = generate_stream(3000, 3, 40, 0.0, 0.5, seed=11)
+    check([s.prefix(1500).accept(frac=1.0, max_delay=400, seed=3), s], 40)
+
+
+@pytest.mark.gpu
+def test_gpu_refold_and_xsp_rejected(gpu_device):
+    from accord_amd import CommandStore, AccordError
+    with CommandStore(device=0, key_lo=0, key_hi=4, window=0) as st:
+        st.upload(mk([(10, "W", 1, [0])]))
+        assert st.max_conflicts_fold()[5] == 1
+        with pytest.raises(AccordError):
+            st.max_conflicts_fold()                         # the batch is already merged
+        with pytest.raises(AccordError):
+            st.max_conflicts_fold(mk([(20, "XSP", 1, [1])]))
 
 
 @pytest.mark.gpu
