@@ -194,8 +194,11 @@ def main():
                    "bitset_words": int(wo.wo_off[-1]), "level_histogram_top": int(np.bincount(wo.level).max())}
 
     boundary = None
+    resident = None
     if world == 1 and not args.waiting_on:
         boundary = boundary_rate(store, s)
+        if s.rng_off[-1] == 0:
+            resident = resident_split(s, args, stage["total"])
 
     if rank != 0:
         store.close()
@@ -252,6 +255,8 @@ def main():
         line["waiting_on"] = wo_info
     if boundary is not None:
         line["boundary_inclusive"] = boundary
+    if resident is not None:
+        line["resident_batches"] = resident
     print(json.dumps(line))
     store.close()
     if dist is not None:
@@ -287,6 +292,33 @@ def boundary_rate(store, s):
         if rc != 0:
             return None
     return {"ms": ms, "txns_per_s": s.n / (ms * 1e-3), "path": "accord_deps_batch, host buffers in and out"}
+
+
+def resident_split(s, args, single_ms, batches=8, reps=3):
+    """The same stream fed as `batches` consecutive batches to one resident store (CommandsForKey
+    state kept in HBM across batches, deps identical to the single batch): device time of the
+    computes (HIP events) and host wall time around them (uploads excluded), per full stream,
+    against the single-batch device time."""
+    from accord_amd import CommandStore
+    pts = [i * s.n // batches for i in range(batches + 1)]
+    parts = [s.slice(a, b) for a, b in zip(pts[:-1], pts[1:])]
+    dev, wall = [], []
+    with CommandStore(device=0, key_lo=0, key_hi=args.keyspace, window=args.window, profile=True,
+                      resident=True) as st:
+        for _ in range(reps + 1):
+            st.reset()
+            d = w = 0.0
+            for p in parts:
+                st.upload(p)
+                t0 = time.perf_counter()
+                st.compute()
+                w += time.perf_counter() - t0
+                d += st.timing().total_ms
+            dev.append(d)
+            wall.append(w * 1e3)
+    dev, wall = min(dev[1:]), min(wall[1:])
+    return {"batches": batches, "device_ms": dev, "compute_wall_ms": wall, "single_batch_device_ms": single_ms,
+            "device_ratio": dev / single_ms if single_ms else None}
 
 
 def measured_traffic(config):

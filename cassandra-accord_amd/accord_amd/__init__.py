@@ -39,6 +39,7 @@ ERR = {
     -7: "CAPACITY", -8: "HIP", -9: "OOM", -10: "STATE",
 }
 STORE_PROFILE = 1
+STORE_RESIDENT = 2
 
 EXPORTED_SYMBOLS = [
     "accord_store_create", "accord_store_destroy", "accord_last_error", "accord_store_stream",
@@ -50,7 +51,7 @@ EXPORTED_SYMBOLS = [
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
-    "accord_max_conflicts_fold_from",
+    "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset",
 ]
 
 
@@ -121,6 +122,11 @@ class _Inverse(C.Structure):
                 ("owner", C.c_void_p)]
 
 
+class _StoreState(C.Structure):
+    _fields_ = [("next_global", C.c_uint64), ("carry_entries", C.c_uint64), ("txns_registered", C.c_uint64),
+                ("reserved", C.c_uint64)]
+
+
 class _Timing(C.Structure):
     _fields_ = [("validate_ms", C.c_float), ("sort_ms", C.c_float), ("segment_ms", C.c_float),
                 ("count_ms", C.c_float), ("scan_ms", C.c_float), ("fill_ms", C.c_float),
@@ -184,6 +190,8 @@ def lib() -> C.CDLL:
         L.accord_max_conflicts_fold_from.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_int32,
                                                      C.POINTER(_MaxConflictsOut)]
         L.accord_max_conflicts_reset.argtypes = [C.c_void_p]
+        L.accord_store_state.argtypes = [C.c_void_p, C.POINTER(_StoreState)]
+        L.accord_store_reset.argtypes = [C.c_void_p]
         L.accord_max_conflicts_state.argtypes = [C.c_void_p, _u64p, _u64p, _i32p, _u8p]
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
@@ -225,6 +233,20 @@ class Stream:
 
     def domains(self) -> np.ndarray:
         return (self.lsb & np.uint64(1)).astype(np.uint8)
+
+    def slice(self, a: int, b: int) -> "Stream":
+        """Txns [a, b) as a batch of their own (CSR rebased); txn_index / executeAt follow."""
+        k0, k1 = int(self.key_off[a]), int(self.key_off[b])
+        r0, r1 = int(self.rng_off[a]), int(self.rng_off[b])
+        ex = {}
+        if self.exec_msb is not None:
+            ex = dict(exec_msb=self.exec_msb[a:b].copy(), exec_lsb=self.exec_lsb[a:b].copy(),
+                      exec_node=self.exec_node[a:b].copy())
+        ti = None if self.txn_index is None else self.txn_index[a:b].copy()
+        return Stream(self.msb[a:b].copy(), self.lsb[a:b].copy(), self.node[a:b].copy(),
+                      (self.key_off[a:b + 1] - self.key_off[a]).astype(np.uint32), self.key_ord[k0:k1].copy(),
+                      (self.rng_off[a:b + 1] - self.rng_off[a]).astype(np.uint32), self.rng_start[r0:r1].copy(),
+                      self.rng_end[r0:r1].copy(), txn_index=ti, **ex)
 
     def prefix(self, m: int) -> "Stream":
         m = min(m, self.n)
@@ -402,6 +424,22 @@ class PartialDeps:
         kw["rd_r2v"] = _arr(d.rd_r2v, int(kw["rd_r2v_off"][-1]), np.int32)
         return PartialDeps(**kw)
 
+    @staticmethod
+    def concat(parts) -> "PartialDeps":
+        """The PartialDeps of consecutive batches as one (offset arrays rebased)."""
+        kw = {}
+        for f in PartialDeps.FIELDS:
+            arrs = [getattr(p, f) for p in parts]
+            if f.endswith("_off"):
+                out, base = [np.zeros(1, np.uint32)], 0
+                for a in arrs:
+                    out.append((a[1:].astype(np.int64) + base).astype(np.uint32))
+                    base += int(a[-1])
+                kw[f] = np.concatenate(out)
+            else:
+                kw[f] = np.concatenate(arrs) if arrs else np.zeros(0, np.uint32)
+        return PartialDeps(**kw)
+
     def equals(self, other: "PartialDeps") -> bool:
         return all(np.array_equal(getattr(self, f), getattr(other, f)) for f in self.FIELDS)
 
@@ -450,8 +488,11 @@ class CommandStore:
     """One CommandStore == one HIP stream on one device (impl/InMemoryCommandStore.java:89)."""
 
     def __init__(self, device: int = 0, key_lo: int = 0, key_hi: int = 100_000, window: int = 256,
-                 profile: bool = False):
-        cfg = _StoreCfg(device, key_lo, key_hi, window, STORE_PROFILE if profile else 0, 0)
+                 profile: bool = False, resident: bool = False):
+        """resident=True: the store keeps its CommandsForKey state across batches (every batch
+        continues the store's stream; deps values are global stream positions)."""
+        flags = (STORE_PROFILE if profile else 0) | (STORE_RESIDENT if resident else 0)
+        cfg = _StoreCfg(device, key_lo, key_hi, window, flags, 0)
         h = C.c_void_p()
         rc = lib().accord_store_create(C.byref(cfg), C.byref(h))
         if rc != ACCORD_OK:
@@ -459,6 +500,17 @@ class CommandStore:
         self._h = h
         self.window = window
         self.key_lo, self.key_hi = key_lo, key_hi
+
+    def state(self) -> dict:
+        """Resident CFK state: next global position, carried history entries."""
+        st = _StoreState()
+        self._check(lib().accord_store_state(self._h, C.byref(st)))
+        return {"next_global": st.next_global, "carry_entries": st.carry_entries,
+                "txns_registered": st.txns_registered}
+
+    def reset(self):
+        """Back to an empty CommandStore (resident state cleared)."""
+        self._check(lib().accord_store_reset(self._h))
 
     def close(self):
         if getattr(self, "_h", None):

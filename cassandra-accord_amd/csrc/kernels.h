@@ -60,12 +60,19 @@ struct KeyDepsParams {
     const uint32_t *bound_g;
 };
 
+// Where a batch sits in the store's stream: global positions start at min_gi, and (has_prev) the
+// first TxnId must follow the last one the (resident) store holds.
+struct StreamPos {
+    uint32_t min_gi, has_prev;
+    uint64_t prev_msb, prev_lsb;
+    int32_t prev_node, pad;
+};
 // txn-major validation + (key, entry) pair packing; range CSR owners and range-txn flags
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
                           uint32_t *pair_key, uint32_t *pair_ent, uint32_t *rng_owner, uint32_t *is_range,
-                          const uint32_t *txn_index, DevStatus *status, hipStream_t s);
+                          const uint32_t *txn_index, const StreamPos &sp, DevStatus *status, hipStream_t s);
 // Accept batch: bound_l[t] = #batch txns with txnId < executeAt[t], bound_g[t] = its global
 // position, pair_bound[p] = bound_g of p's txn; executeAt < txnId -> ACCORD_ERR_ARG
 void launch_accept_bounds(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
@@ -75,10 +82,12 @@ void launch_accept_bounds(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
 // range_txns[excl[i]] = i for every i with is_range[i]
 void launch_compact_flags(uint32_t n, const uint32_t *flags, const uint32_t *excl, uint32_t *out, hipStream_t s);
 size_t history_temp_bytes(uint32_t P);
-// key-major: history entries, segments, and per pair its deps slice (txn-major PairSlice)
+// key-major: history entries, segments, and per pair its deps slice (txn-major PairSlice).  P counts
+// the combined history; sorted_pair values < carry are a resident store's carried entries (no slice).
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, PairSlice *slice, void *temp, const uint32_t *pair_bound, hipStream_t s);
+                    uint32_t *seg_end, PairSlice *slice, void *temp, const uint32_t *pair_bound, uint32_t carry,
+                    hipStream_t s);
 // history tile size of the Write max-scan carry (pw_local / pw_carry) and class-count carries
 constexpr uint32_t HISTORY_TILE = 4096;
 // Views into the history temp buffer launch_history leaves behind: (last Write <= x) + 1 =
@@ -100,6 +109,15 @@ void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, void *
 size_t compact_temp_bytes(uint64_t max_total);
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
                          uint32_t *vals, uint64_t max_total, void *temp, hipStream_t s);
+
+// ---- resident CFK state across batches (resident.hip) ----
+void launch_gen_index(uint32_t n, uint32_t base, uint32_t *out, hipStream_t s);
+size_t carry_temp_bytes(uint32_t P, uint32_t nkeys);
+// the entries of the combined history a later batch can still reach (per key: from the last Write
+// with txn < thr, else everything) -> out_key/out_ent, key-major; their count in *total
+void launch_carry(uint32_t P, uint32_t nkeys, uint32_t thr, const uint32_t *sorted_key, const uint32_t *hist,
+                  const uint32_t *seg_start, const uint32_t *seg_end, const HistoryViews &hv, void *temp,
+                  uint32_t *out_key, uint32_t *out_ent, unsigned long long *total, hipStream_t s);
 
 // ---- range txns (rangedeps.hip) ----
 struct RangeDepsParams {

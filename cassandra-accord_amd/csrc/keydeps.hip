@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
     const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ key_ord, const uint32_t *__restrict__ rng_off,
     const uint32_t *__restrict__ rng_start, const uint32_t *__restrict__ rng_end, uint32_t key_lo, uint32_t key_hi,
     uint32_t *__restrict__ pair_key, uint32_t *__restrict__ pair_ent, uint32_t *__restrict__ rng_owner,
-    uint32_t *__restrict__ is_range, const uint32_t *__restrict__ txn_index, DevStatus *st)
+    uint32_t *__restrict__ is_range, const uint32_t *__restrict__ txn_index, StreamPos sp, DevStatus *st)
 {
     const uint32_t lane = lane_id();
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -62,7 +62,11 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
             const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
             const uint32_t gi = txn_index ? txn_index[t] : t;      // global stream position
             ent = (kind << ENT_KIND_SHIFT) | (gi & ENT_TXN_MASK);
-            if (gi > ENT_TXN_MASK || (txn_index && t > 0 && txn_index[t - 1] >= gi)) record_error(st, t, ACCORD_ERR_UNSORTED);
+            if (gi > ENT_TXN_MASK || (txn_index && t > 0 && txn_index[t - 1] >= gi) || gi < sp.min_gi)
+                record_error(st, t, ACCORD_ERR_UNSORTED);
+            // a resident store continues its stream: the batch starts after the last TxnId it holds
+            if (t == 0 && sp.has_prev && ts_cmp(sp.prev_msb, sp.prev_lsb, sp.prev_node, msb[0], l, node[0]) >= 0)
+                record_error(st, t, ACCORD_ERR_UNSORTED);
             if (witness_mask(kind) == 0) record_error(st, t, ACCORD_ERR_KIND);
             if (t > 0 && ts_cmp(msb[t - 1], lsb[t - 1], node[t - 1], msb[t], l, node[t]) >= 0)
                 record_error(st, t, ACCORD_ERR_UNSORTED);
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
                                                               const ClassCarry *__restrict__ ccarry,
                                                               const uint32_t *__restrict__ seg_end,
                                                               const uint32_t *__restrict__ pair_bound,
-                                                              PairSlice *__restrict__ slice)
+                                                              PairSlice *__restrict__ slice, uint32_t ncarry)
 {
     __shared__ uint32_t tx[H2_HALO + H2_TILE];
     const uint32_t base = blockIdx.x * H2_TILE;
@@ -289,7 +293,10 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
         key[j] = p < end ? sorted_key[p] : 0u;
-        q[j] = p < end ? sorted_pair[p] : 0u;
+        // combined history of a resident store: [carried entries | batch pairs]; carried entries
+        // (index < ncarry) are history only and get no slice (q = ~0)
+        const uint32_t v = p < end ? sorted_pair[p] : 0u;
+        q[j] = v >= ncarry ? v - ncarry : 0xFFFFFFFFu;
     }
     for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) tx[x - lds_lo] = hist[x];
     uint32_t a[H2_ITEMS];
@@ -361,7 +368,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
         hi[j] = p;
-        if (pair_bound && p < end) {
+        if (pair_bound && p < end && q[j] != 0xFFFFFFFFu) {
             const uint32_t b = pair_bound[q[j]], c = seg_end[key[j]];
             uint32_t x = p + 1, step = 1;
             while (x < c && (hist[x] & ENT_TXN_MASK) < b) {   // gallop, then bisect
@@ -397,7 +404,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
-        if (p < end) slice[q[j]] = PairSlice{l[j], hi[j], cnt[j], 0u};
+        if (p < end && q[j] != 0xFFFFFFFFu) slice[q[j]] = PairSlice{l[j], hi[j], cnt[j], 0u};
     }
 }
 
@@ -1086,14 +1093,14 @@ void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
                           const uint32_t *rng_start, const uint32_t *rng_end, uint32_t key_lo, uint32_t key_hi,
                           uint32_t *pair_key, uint32_t *pair_ent, uint32_t *rng_owner, uint32_t *is_range,
-                          const uint32_t *txn_index, DevStatus *status, hipStream_t s)
+                          const uint32_t *txn_index, const StreamPos &sp, DevStatus *status, hipStream_t s)
 {
     if (n == 0) return;
     uint32_t blocks = (n + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(validate_pack_kernel, dim3(blocks), dim3(256), 0, s, n, msb, lsb, node, key_off, key_ord,
                        rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_ent, rng_owner, is_range,
-                       txn_index, status);
+                       txn_index, sp, status);
 }
 
 __global__ __launch_bounds__(256) void compact_flags_kernel(uint32_t n, const uint32_t *__restrict__ flags,
@@ -1153,7 +1160,8 @@ HistoryViews history_views(void *temp, uint32_t P)
 
 void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t *sorted_key,
                     const uint32_t *sorted_pair, const uint32_t *hist, uint32_t *seg_start,
-                    uint32_t *seg_end, PairSlice *slice, void *temp, const uint32_t *pair_bound, hipStream_t s)
+                    uint32_t *seg_end, PairSlice *slice, void *temp, const uint32_t *pair_bound, uint32_t carry,
+                    hipStream_t s)
 {
     (void)nkeys;
     if (P == 0) return;
@@ -1171,7 +1179,7 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
     hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tile_cnt, ccarry, tiles);
     hipLaunchKernelGGL(history2_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P, window,
                        sorted_key, sorted_pair, hist,
-                       seg_start, pw_local, tile_max, c_local, ccarry, seg_end, pair_bound, slice);
+                       seg_start, pw_local, tile_max, c_local, ccarry, seg_end, pair_bound, slice, carry);
 }
 
 void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *slice, uint32_t *cnt_keys,

@@ -85,6 +85,7 @@ int32_t accord_store_create(const accord_store_cfg *cfg, accord_store **out)
         return fail(nullptr, ACCORD_ERR_HIP, "pinned alloc: %s", hipGetErrorString(e));
     }
     s->events = (cfg->flags & ACCORD_STORE_PROFILE) != 0;
+    s->resident = (cfg->flags & ACCORD_STORE_RESIDENT) != 0;
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventCreate(&ev);
     uint32_t span_need = cfg->window + 2048;
@@ -108,7 +109,8 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rd_vals, &s->rd_r2v, &s->rd_big, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
-                      &s->level, &s->wo_info, &s->lv_tmp};
+                      &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
+                      &s->carry_tmp};
     accord_impl::shard_comm_destroy(s);
     for (DevBuf *b : bufs) b->release();
     for (DepSet &d : s->ds) d.release();
@@ -148,6 +150,8 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     for (uint32_t i = 0; i < n; ++i) nrt += (uint32_t)(b->lsb[i] & 1);
     if (b->txn_index && nrt)
         return fail(s, ACCORD_ERR_ARG, "txn_index (store subset of a stream) is supported for key txns only");
+    if (s->resident && nrt)
+        return fail(s, ACCORD_ERR_STATE, "range txns in a resident store are not supported by this build");
     s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt;
     s->rk_keys_total = 0;                // sizes the range txns' stored key slices
     if (nrt && b->rng_off)
@@ -162,6 +166,7 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
         return fail(s, ACCORD_ERR_CAPACITY, "range txns cover %llu (txn, key) pairs, over 2^32",
                     (unsigned long long)s->rk_keys_total);
     s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->mc_next = 0;
+    s->b_registered = false;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
     HIPCHECK(s, s->node.ensure((size_t)n * 4));
@@ -185,11 +190,21 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
         HIPCHECK(s, hipMemcpyAsync(s->rng_start.p, b->rng_start, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
         HIPCHECK(s, hipMemcpyAsync(s->rng_end.p, b->rng_end, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
     }
-    s->has_txn_index = b->txn_index != nullptr;
+    s->user_txn_index = b->txn_index != nullptr;
+    s->has_txn_index = s->user_txn_index || s->resident;
     if (s->has_txn_index) {
-        HIPCHECK(s, s->txn_index.ensure((size_t)n * 4));
-        if (n) HIPCHECK(s, hipMemcpyAsync(s->txn_index.p, b->txn_index, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, s->txn_index.ensure((size_t)n * 4 + 4));
+        if (s->user_txn_index) {
+            if (n) HIPCHECK(s, hipMemcpyAsync(s->txn_index.p, b->txn_index, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
+        } else {
+            accord::launch_gen_index(n, s->next_global, s->txn_index.as<uint32_t>(), s->stream);   // resident: next_global + t
+        }
     }
+    // where the batch ends in the stream (committed to the store when its compute succeeds)
+    s->b_end = !s->resident ? n : (n == 0 ? s->next_global : (s->user_txn_index ? b->txn_index[n - 1] + 1u : s->next_global + n));
+    if (s->resident && n && (uint64_t)s->next_global + n > (1ull << 29))
+        return fail(s, ACCORD_ERR_CAPACITY, "resident store stream exceeds 2^29 txns");
+    if (n) { s->b_last_msb = b->msb[n - 1]; s->b_last_lsb = b->lsb[n - 1]; s->b_last_node = b->node[n - 1]; }
     if ((b->exec_msb != nullptr) != (b->exec_lsb != nullptr) || (b->exec_msb != nullptr) != (b->exec_node != nullptr))
         return fail(s, ACCORD_ERR_ARG, "executeAt needs all of exec_msb, exec_lsb, exec_node");
     s->has_exec = b->exec_msb != nullptr;
@@ -212,6 +227,7 @@ int32_t accord_deps_compute(accord_store *s)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     if (!s->has_batch) return fail(s, ACCORD_ERR_STATE, "accord_deps_compute before accord_batch_upload");
+    if (s->b_registered) return fail(s, ACCORD_ERR_STATE, "the uploaded batch is already part of the resident store's stream");
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     const uint32_t n = s->n, P = s->P, R = s->R, nrt = s->n_range_txns;
     const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
@@ -222,21 +238,30 @@ int32_t accord_deps_compute(accord_store *s)
     s->ds_cur = -1;
     s->wo_done = false;
 
-    HIPCHECK(s, s->pair_key.ensure((size_t)P * 4));
-    HIPCHECK(s, s->pair_ent.ensure((size_t)P * 4));
-    HIPCHECK(s, s->sort_key.ensure((size_t)P * 4));
-    HIPCHECK(s, s->sort_pair.ensure((size_t)P * 4));
-    HIPCHECK(s, s->tmp_key.ensure((size_t)P * 4));
-    HIPCHECK(s, s->tmp_val.ensure((size_t)P * 4));
-    HIPCHECK(s, s->tmp_ent.ensure((size_t)P * 4));
-    HIPCHECK(s, s->hist.ensure((size_t)P * 4));
+    // history = [entries a resident store carried over | this batch's pairs], key-major after the sort
+    const uint32_t C = s->resident ? s->carry_n : 0u;
+    const uint32_t PH = C + P;
+    if ((uint64_t)C + P >= (1ull << 28)) return fail(s, ACCORD_ERR_CAPACITY, "history of %u + %u entries exceeds 2^28", C, P);
+    HIPCHECK(s, s->pair_key.ensure((size_t)PH * 4));
+    HIPCHECK(s, s->pair_ent.ensure((size_t)PH * 4));
+    HIPCHECK(s, s->sort_key.ensure((size_t)PH * 4));
+    HIPCHECK(s, s->sort_pair.ensure((size_t)PH * 4));
+    HIPCHECK(s, s->tmp_key.ensure((size_t)PH * 4));
+    HIPCHECK(s, s->tmp_val.ensure((size_t)PH * 4));
+    HIPCHECK(s, s->tmp_ent.ensure((size_t)PH * 4));
+    HIPCHECK(s, s->hist.ensure((size_t)PH * 4));
     HIPCHECK(s, s->slice.ensure((size_t)P * sizeof(accord::PairSlice)));
     HIPCHECK(s, s->cnt_vub.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->vub_off.ensure(n1 * 4));
-    HIPCHECK(s, s->hist_tmp.ensure(accord::history_temp_bytes(P)));
+    HIPCHECK(s, s->hist_tmp.ensure(accord::history_temp_bytes(PH)));
     HIPCHECK(s, s->seg_start.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->seg_end.ensure((size_t)nkeys * 4));
-    HIPCHECK(s, s->radix_tmp.ensure(accord::radix_sort_temp_bytes(P)));
+    HIPCHECK(s, s->radix_tmp.ensure(accord::radix_sort_temp_bytes(PH)));
+    if (s->resident) {
+        HIPCHECK(s, s->cy_key2.ensure((size_t)PH * 4 + 4));
+        HIPCHECK(s, s->cy_ent2.ensure((size_t)PH * 4 + 4));
+        HIPCHECK(s, s->carry_tmp.ensure(accord::carry_temp_bytes(PH, nkeys)));
+    }
     HIPCHECK(s, s->cnt_keys.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->cnt_vals.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->cnt_k2v.ensure((size_t)n * 4 + 4));
@@ -260,12 +285,20 @@ int32_t accord_deps_compute(accord_store *s)
     record(s, EV_START);
     HIPCHECK(s, hipMemsetAsync(dev, 0xFF, sizeof(HostTotals), st));
     HIPCHECK(s, hipMemsetAsync(&dev->status.overflow, 0, sizeof(uint32_t), st));
+    if (C) {
+        HIPCHECK(s, hipMemcpyAsync(s->pair_key.p, s->cy_key.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHECK(s, hipMemcpyAsync(s->pair_ent.p, s->cy_ent.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
+    }
+    accord::StreamPos sp{};
+    sp.min_gi = s->resident ? s->next_global : 0u;
+    sp.has_prev = (s->resident && s->has_prev) ? 1u : 0u;
+    sp.prev_msb = s->prev_msb; sp.prev_lsb = s->prev_lsb; sp.prev_node = s->prev_node;
     accord::launch_validate_pack(n, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->node.as<int32_t>(),
                                  s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->rng_off.as<uint32_t>(),
                                  R ? s->rng_start.as<uint32_t>() : nullptr, R ? s->rng_end.as<uint32_t>() : nullptr,
-                                 s->cfg.key_lo, s->cfg.key_hi, s->pair_key.as<uint32_t>(), s->pair_ent.as<uint32_t>(),
+                                 s->cfg.key_lo, s->cfg.key_hi, s->pair_key.as<uint32_t>() + C, s->pair_ent.as<uint32_t>() + C,
                                  R ? s->rng_owner.as<uint32_t>() : nullptr, s->is_range.as<uint32_t>(),
-                                 s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr, &dev->status, st);
+                                 s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr, sp, &dev->status, st);
     if (nrt) {
         accord::exclusive_scan_u32(s->is_range.as<uint32_t>(), s->rt_excl.as<uint32_t>(), n, &dev->totals[6],
                                    s->scan_tmp.p, st);
@@ -287,15 +320,15 @@ int32_t accord_deps_compute(accord_store *s)
     record(s, EV_VALIDATE);
     accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
                              s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
-                             s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), P,
+                             s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), PH,
                              bits_for(nkeys - 1), s->radix_tmp.p, st);
     record(s, EV_SORT);
     HIPCHECK(s, hipMemsetAsync(s->seg_start.p, 0, (size_t)nkeys * 4, st));
     HIPCHECK(s, hipMemsetAsync(s->seg_end.p, 0, (size_t)nkeys * 4, st));
-    accord::launch_history(P, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
+    accord::launch_history(PH, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
                            s->seg_end.as<uint32_t>(), s->slice.as<accord::PairSlice>(),
-                           s->hist_tmp.p, pair_bound, st);
+                           s->hist_tmp.p, pair_bound, C, st);
     record(s, EV_SEGMENT);
 
     accord::KeyDepsParams kp{};
@@ -319,7 +352,7 @@ int32_t accord_deps_compute(accord_store *s)
     rp.window = s->cfg.window; rp.key_lo = s->cfg.key_lo; rp.key_hi = s->cfg.key_hi;
     rp.hist = kp.hist; rp.seg_start = s->seg_start.as<uint32_t>(); rp.seg_end = s->seg_end.as<uint32_t>();
     {
-        const accord::HistoryViews hv = accord::history_views(s->hist_tmp.p, P);
+        const accord::HistoryViews hv = accord::history_views(s->hist_tmp.p, PH);
         rp.pw_local = hv.pw_local; rp.pw_carry = hv.pw_carry; rp.pw_tile = accord::HISTORY_TILE;
         rp.c_local = hv.c_local; rp.ccarry = hv.ccarry;
     }
@@ -432,6 +465,14 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->cv_tmp.ensure(accord::compact_temp_bytes(vub_total)));
     accord::launch_compact_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, s->kd_vals.as<uint32_t>(),
                                 vub_total, s->cv_tmp.p, st);
+    if (s->resident) {
+        // what the next batch needs of this history (the stream ends at b_end)
+        const uint32_t thr = s->b_end > s->cfg.window ? s->b_end - s->cfg.window : 0u;
+        accord::launch_carry(PH, nkeys, thr, s->sort_key.as<uint32_t>(), s->hist.as<uint32_t>(),
+                             s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(),
+                             accord::history_views(s->hist_tmp.p, PH), s->carry_tmp.p, s->cy_key2.as<uint32_t>(),
+                             s->cy_ent2.as<uint32_t>(), &dev->totals[8], st);
+    }
     record(s, EV_COMPACT);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
@@ -440,6 +481,17 @@ int32_t accord_deps_compute(accord_store *s)
         int32_t rc = check_status(*s->pinned);
         if (rc) return rc;
         s->tot_vals = s->pinned->totals[7];
+    }
+    if (s->resident) {      // the batch is part of the store's stream now
+        std::swap(s->cy_key, s->cy_key2);
+        std::swap(s->cy_ent, s->cy_ent2);
+        s->carry_n = (uint32_t)s->pinned->totals[8];
+        s->next_global = s->b_end;
+        if (n) {
+            s->has_prev = true;
+            s->prev_msb = s->b_last_msb; s->prev_lsb = s->b_last_lsb; s->prev_node = s->b_last_node;
+        }
+        s->b_registered = true;   // computing it again would register it twice
     }
     if (getenv("ACCORD_FILL_STATS")) {                 // dev aid: txns the fast fill handed on
         uint32_t fb = 0;
@@ -460,8 +512,27 @@ int32_t accord_deps_compute(accord_store *s)
         s->timing.total_ms = el(EV_START, EV_COMPACT);
     }
     s->timing.pairs = P;
-    s->timing.hist_entries = P;
+    s->timing.hist_entries = PH;
     s->computed = true;
+    return ACCORD_OK;
+}
+
+int32_t accord_store_state(accord_store *s, accord_store_state_info *info)
+{
+    if (!s || !info) return fail(s, ACCORD_ERR_ARG, "null argument");
+    std::memset(info, 0, sizeof(*info));
+    info->next_global = s->next_global;
+    info->carry_entries = s->carry_n;
+    info->txns_registered = s->next_global;
+    return ACCORD_OK;
+}
+
+int32_t accord_store_reset(accord_store *s)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    s->next_global = 0; s->carry_n = 0; s->has_prev = false;
+    s->prev_msb = s->prev_lsb = 0; s->prev_node = 0;
+    s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->wo_done = false;
     return ACCORD_OK;
 }
 

@@ -31,8 +31,8 @@ struct DevBuf {
 
 struct HostTotals {
     accord::DevStatus status;
-    unsigned long long totals[8];   // kd keys, kd vals bound, kd k2v, rd ranges, rd vals, rd r2v, range txns,
-                                    // kd vals
+    unsigned long long totals[10];  // kd keys, kd vals bound, kd k2v, rd ranges, rd vals, rd r2v, range txns,
+                                    // kd vals, resident carry entries, spare
 };
 
 // A device-resident PartialDeps set (result of accord_deps_union / accord_deps_slice).
@@ -80,7 +80,21 @@ struct accord_store {
     DevBuf kd_keys, kd_vals, kd_k2v, rd_zero_off;  // rd_zero_off: unused, kept for ABI-compatible views
     uint64_t tot_keys = 0, tot_vals = 0, tot_k2v = 0;
     DevBuf txn_index;              // global stream positions (nullptr = identity)
-    bool has_txn_index = false;
+    bool has_txn_index = false;    // device txn_index valid (given by the caller, or generated)
+    bool user_txn_index = false;   // given by the caller (a store subset of a stream)
+    // resident CommandsForKey state (ACCORD_STORE_RESIDENT, resident.hip): the stream continues
+    // across batches at global position next_global after TxnId prev_*; cy_* = the carried
+    // key-major history entries (cy_key relative key ordinal, cy_ent kind<<29 | global txn)
+    bool resident = false, has_prev = false;
+    uint32_t next_global = 0, carry_n = 0;
+    uint64_t prev_msb = 0, prev_lsb = 0;
+    int32_t prev_node = 0;
+    DevBuf cy_key, cy_ent, cy_key2, cy_ent2, carry_tmp;
+    // the uploaded batch: its carried-entry prefix, where it ends (global) and its last TxnId
+    uint32_t b_end = 0;
+    bool b_registered = false;     // the uploaded batch was computed into the resident stream
+    uint64_t b_last_msb = 0, b_last_lsb = 0;
+    int32_t b_last_node = 0;
     // Accept batch: executeAt per txn; bound_l / bound_g = txns started before it (local index,
     // global position), pair_bound = bound_g per (txn, key) pair
     DevBuf exec_msb, exec_lsb, exec_node, bound_l, bound_g, pair_bound;

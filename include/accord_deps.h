@@ -48,6 +48,10 @@ extern "C" {
 #define ACCORD_ERR_STATE      -10   /* call out of sequence */
 
 #define ACCORD_STORE_PROFILE   1u   /* record HIP events around every kernel */
+/* The store keeps its CommandsForKey state across batches (CommandStore semantics: every batch
+ * continues the store's stream; see accord_store_resident below).  Without it every uploaded
+ * batch is a stream of its own. */
+#define ACCORD_STORE_RESIDENT  2u
 
 typedef struct accord_store accord_store;
 
@@ -56,7 +60,7 @@ typedef struct {
     uint32_t key_lo;        /* store owns key ordinals [key_lo, key_hi) (CommandStores slice) */
     uint32_t key_hi;
     uint32_t window;        /* W of the status-at-time model */
-    uint32_t flags;         /* ACCORD_STORE_PROFILE */
+    uint32_t flags;         /* ACCORD_STORE_PROFILE | ACCORD_STORE_RESIDENT */
     uint32_t reserved;
 } accord_store_cfg;
 
@@ -121,6 +125,25 @@ int32_t     accord_store_create(const accord_store_cfg *cfg, accord_store **out)
 int32_t     accord_store_destroy(accord_store *store);
 const char *accord_last_error(const accord_store *store);   /* NULL store: last global error */
 void       *accord_store_stream(accord_store *store);        /* the store's hipStream_t */
+
+/* ---- resident CommandsForKey state (ACCORD_STORE_RESIDENT) ----
+ * A resident store is one CommandStore over its whole life: batch b continues the stream of
+ * batches 0..b-1 (its first TxnId must follow the last one registered, ACCORD_ERR_UNSORTED
+ * otherwise), every txn keeps its global stream position (txn_index given, or next_global + t),
+ * and deps values are global positions -- the output of b consecutive batches is the output of
+ * one batch over their concatenation.  Between batches the store keeps, per key, the history
+ * entries a later txn can reach (CommandsForKey.txns from the last Write before the window on;
+ * older entries are pruned for good, as committed entries below maxCommittedBefore are,
+ * local/CommandsForKey.java:620-645,1654-1684).  A rejected batch leaves the state unchanged.
+ * Key txns only in this build (a range txn in a resident store: ACCORD_ERR_STATE). */
+typedef struct {
+    uint64_t next_global;       /* global position of the next txn */
+    uint64_t carry_entries;     /* history entries kept for later batches */
+    uint64_t txns_registered;   /* == next_global unless batches carried txn_index gaps */
+    uint64_t reserved;
+} accord_store_state_info;
+int32_t accord_store_state(accord_store *store, accord_store_state_info *info);
+int32_t accord_store_reset(accord_store *store);               /* back to an empty CommandStore */
 
 /* ---- synchronous batch entry: host in, host out ----
  * CommandStore.calculateDepsBatch(TxnId[], Seekables[], Timestamp[] executeAt, ...) ->

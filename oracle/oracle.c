@@ -549,13 +549,15 @@ static long p1_of(const or_stream *s, uint32_t i)
 
 /* number of stream txns j < n with txnId_j < ts (TxnIds are strictly ascending): the txns a
  * startedBefore bound admits (CommandsForKey.insertPos, :1698-1703) */
-static uint32_t bound_of(const or_stream *s, uint32_t n, const ts_t *ts)
+static uint32_t bound_of(const or_stream *s, uint32_t n, const ts_t *ts, uint32_t i)
 {
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
         uint32_t m = (lo + hi) / 2;
         if (or_ts_compare(s->msb[m], s->lsb[m], s->node[m], ts->msb, ts->lsb, ts->node) < 0) lo = m + 1; else hi = m;
     }
+    /* batch by batch: txns of later batches are not registered yet */
+    if (s->batch_end && lo > s->batch_end[i]) lo = s->batch_end[i];
     return lo;
 }
 
@@ -592,7 +594,7 @@ static int stream_literal(const or_stream *s, uint32_t n, or_deps *out)
     for (uint32_t i = 0; i < n; ++i) {
         const ts_t sb_i = started_before(s, i);
         const long p1 = p1_of(s, i);
-        uint32_t reg_to = bound_of(s, n, &sb_i);  /* an Accept sees every txn started before executeAt */
+        uint32_t reg_to = bound_of(s, n, &sb_i, i);  /* an Accept sees every txn started before executeAt */
         if (reg_to < i + 1) reg_to = i + 1;
         /* 1. status at time i: txn j = i-W-1 leaves the window -> APPLIED (executeAt=txnId) if a
          *    key txn, Erased if a range txn. */
@@ -771,7 +773,7 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
         int tk = witnesses_of(kind_of(s->lsb[i]));
         int64_t applied_before = (int64_t)i - (int64_t)s->window;    /* j < i-W are applied */
         const ts_t sb_i = started_before(s, i);
-        const uint32_t bound = bound_of(s, n, &sb_i);     /* candidates j < bound (= i: PreAccept) */
+        const uint32_t bound = bound_of(s, n, &sb_i, i);     /* candidates j < bound (= i: PreAccept) */
         const long p1 = p1_of(s, i);                       /* excluded (Accept: the txn itself) */
         lists.n = 0; lens.n = 0; heads.n = 0;
         u32v qkeys = {0};

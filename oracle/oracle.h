@@ -55,6 +55,10 @@ typedef struct {
     const uint64_t *exec_msb;
     const uint64_t *exec_lsb;
     const int32_t  *exec_node;
+    /* a resident store fed the stream batch by batch (include/accord_deps.h ACCORD_STORE_RESIDENT):
+     * txn i only sees txns registered when its batch is computed, i.e. positions < batch_end[i].
+     * Matters for Accept batches whose executeAt lies past their batch.  NULL = one batch. */
+    const uint32_t *batch_end;
 } or_stream;
 
 /* Per-txn PartialDeps in the exact reference layout (KeyDeps.java:150-187,

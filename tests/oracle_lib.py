@@ -26,7 +26,7 @@ class _OrStream(C.Structure):
     _fields_ = [("n", C.c_uint32), ("msb", _u64p), ("lsb", _u64p), ("node", _i32p),
                 ("key_off", _u32p), ("key_ord", _u32p), ("rng_off", _u32p), ("rng_start", _u32p),
                 ("rng_end", _u32p), ("window", C.c_uint32),
-                ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p)]
+                ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p), ("batch_end", _u32p)]
 
 
 class _OrDeps(C.Structure):
@@ -94,7 +94,7 @@ def _to_partial(d: _OrDeps) -> PartialDeps:
     return PartialDeps(**kw)
 
 
-def _or_stream(s: Stream, window: int):
+def _or_stream(s: Stream, window: int, batch_end=None):
     keep = [np.ascontiguousarray(a) for a in (s.msb, s.lsb, s.node, s.key_off, s.key_ord, s.rng_off,
                                               s.rng_start, s.rng_end)]
     msb, lsb, node, ko, kord, ro, rs, re = keep
@@ -116,6 +116,10 @@ def _or_stream(s: Stream, window: int):
         o.exec_msb = ex[0].ctypes.data_as(_u64p)
         o.exec_lsb = ex[1].ctypes.data_as(_u64p)
         o.exec_node = ex[2].ctypes.data_as(_i32p)
+    if batch_end is not None:
+        be = np.ascontiguousarray(batch_end, dtype=np.uint32)
+        keep.append(be)
+        o.batch_end = be.ctypes.data_as(_u32p)
     return o, keep
 
 
@@ -125,8 +129,16 @@ class OracleError(RuntimeError):
         self.rc = rc
 
 
-def deps_literal(s: Stream, window: int, limit: int | None = None) -> PartialDeps:
-    o, keep = _or_stream(s, window)
+def batch_ends(sizes):
+    """batch_end[i] for a stream fed as consecutive batches of the given sizes."""
+    ends = np.cumsum(np.asarray(sizes, np.int64))
+    return np.repeat(ends, sizes).astype(np.uint32)
+
+
+def deps_literal(s: Stream, window: int, limit: int | None = None, batch_end=None) -> PartialDeps:
+    """Literal restatement (real CFK objects, per-status-change copies).  batch_end: the stream is
+    fed batch by batch to one resident store (see batch_ends)."""
+    o, keep = _or_stream(s, window, batch_end)
     d = _OrDeps()
     if limit is None:
         rc = lib().or_stream_deps_literal(C.byref(o), C.byref(d))
@@ -140,8 +152,8 @@ def deps_literal(s: Stream, window: int, limit: int | None = None) -> PartialDep
         lib().or_deps_free(C.byref(d))
 
 
-def deps_fast(s: Stream, window: int) -> PartialDeps:
-    o, keep = _or_stream(s, window)
+def deps_fast(s: Stream, window: int, batch_end=None) -> PartialDeps:
+    o, keep = _or_stream(s, window, batch_end)
     d = _OrDeps()
     rc = lib().or_stream_deps_fast(C.byref(o), C.byref(d))
     if rc != 0:
