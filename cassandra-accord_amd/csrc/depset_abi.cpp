@@ -54,7 +54,7 @@ struct Scans {
     unsigned long long *dev;
     int32_t add(const uint32_t *in, uint32_t *out, uint32_t n)
     {
-        HIPCHECK(s, s->op_tmp[T_SCAN].ensure(accord::scan_temp_bytes(n)));
+        HIPCHECK(s, s->op_tmp[T_SCAN].ensure_zeroed(accord::scan_temp_bytes(n), s->stream));
         accord::exclusive_scan_u32(in, out, n, dev + k++, s->op_tmp[T_SCAN].p, s->stream);
         return ACCORD_OK;
     }

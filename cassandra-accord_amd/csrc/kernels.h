@@ -16,18 +16,40 @@ struct DevStatus {
 
 // ---- radix sort (radix_sort.hip) ----
 size_t radix_sort_temp_bytes(uint32_t n);
+uint32_t radix_sort_scan_len(uint32_t n);   // longest scan the sort runs (size its scan state for it)
 // Stable LSD sort of (key, val) by key over `bits` low bits.  Result ends in keys_out/vals_out.
 // keys_tmp/vals_tmp are ping-pong buffers of n entries.
 // ents_in (optional, may be null) is a second value carried the same way into ents_out.
 void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys_out, uint32_t *vals_out,
                       uint32_t *keys_tmp, uint32_t *vals_tmp, const uint32_t *ents_in, uint32_t *ents_out,
-                      uint32_t *ents_tmp, uint32_t n, int bits, void *temp, hipStream_t s);
+                      uint32_t *ents_tmp, uint32_t n, int bits, void *temp, void *scan_state, hipStream_t s);
+
+// ---- small fills in one launch (scan.hip): descriptor k sets words [0, d[k].words) of d[k].p ----
+struct FillDesc {
+    uint32_t *p;
+    uint32_t words, value;
+};
+struct FillList {
+    FillDesc d[12];
+    uint32_t nd = 0;
+    void add(void *p, size_t bytes, uint32_t value)
+    {
+        if (bytes >= 4) d[nd++] = FillDesc{(uint32_t *)p, (uint32_t)(bytes / 4), value};
+    }
+};
+void launch_fill_words(const FillList &L, hipStream_t s);
 
 // ---- scan (scan.hip) ----
+// temp: a scan-state buffer of at least scan_temp_bytes(n) bytes, ZERO when allocated
+// (DevBuf::ensure_zeroed) and used for nothing else, starting at the same address for every scan
+// that shares it (the store's scan_tmp); scans sharing it must run in stream order (it resets itself).
 size_t scan_temp_bytes(uint32_t n);
 // out[i] = sum(in[0..i)), i in [0, n]; out has n+1 entries; total also written to *total_dev (u64).
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, unsigned long long *total_dev, void *temp,
                         hipStream_t s);
+// the same for na (1..4) arrays of n counts in one launch (total[k] may be null)
+void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *out, unsigned long long *const *total,
+                          uint32_t n, void *temp, hipStream_t s);
 
 // ---- key deps pipeline (keydeps.hip) ----
 // Per (txn, key) pair, txn-major: the deps slice [lo, pos) of the key's history and the number of
@@ -112,12 +134,12 @@ void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *va
 
 // ---- resident CFK state across batches (resident.hip) ----
 void launch_gen_index(uint32_t n, uint32_t base, uint32_t *out, hipStream_t s);
-size_t carry_temp_bytes(uint32_t P, uint32_t nkeys);
+size_t carry_temp_bytes(uint32_t P, uint32_t nkeys);   // scan state separate (scan of P flags)
 // the entries of the combined history a later batch can still reach (per key: from the last Write
 // with txn < thr, else everything) -> out_key/out_ent, key-major; their count in *total
 void launch_carry(uint32_t P, uint32_t nkeys, uint32_t thr, const uint32_t *sorted_key, const uint32_t *hist,
                   const uint32_t *seg_start, const uint32_t *seg_end, const HistoryViews &hv, void *temp,
-                  uint32_t *out_key, uint32_t *out_ent, unsigned long long *total, hipStream_t s);
+                  void *scan_state, uint32_t *out_key, uint32_t *out_ent, unsigned long long *total, hipStream_t s);
 
 // ---- range txns (rangedeps.hip) ----
 struct RangeDepsParams {

@@ -294,7 +294,7 @@ int32_t mc_pass(accord_store *s, uint32_t first, uint32_t last, const McValues &
     if (P) {
         accord::radix_sort_pairs(T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[2].as<uint32_t>(), T[3].as<uint32_t>(),
                                  T[4].as<uint32_t>(), T[5].as<uint32_t>(), T[6].as<uint32_t>(), T[11].as<uint32_t>(),
-                                 T[12].as<uint32_t>(), P, (int)bits_for_mc(nkeys ? nkeys - 1 : 0), T[10].p, st);
+                                 T[12].as<uint32_t>(), P, (int)bits_for_mc(nkeys ? nkeys - 1 : 0), T[10].p, s->scan_tmp.p, st);
         mc_scan_kernel<0><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(),
                                                       T[13].as<TsV>(), s->lsb.as<uint64_t>(), mv, s->mc_state.as<TsV>(),
                                                       T[8].as<Comp>(), nullptr, nullptr, nullptr);
@@ -331,6 +331,7 @@ int32_t mc_fold(accord_store *s, uint32_t first, bool override, uint64_t ov_msb,
     HIPCHECK(s, T[8].ensure((size_t)ntiles * sizeof(Comp) + 64));
     HIPCHECK(s, T[9].ensure((size_t)ntiles * sizeof(TsV) + 32));
     HIPCHECK(s, T[10].ensure(accord::radix_sort_temp_bytes(P)));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max(P, accord::radix_sort_scan_len(P))), s->stream));
     HIPCHECK(s, T[11].ensure((size_t)P * 4 + 4));                 // sorted pair index
     HIPCHECK(s, T[12].ensure((size_t)P * 4 + 4));                 // its ping-pong buffer
     HIPCHECK(s, T[13].ensure((size_t)P * sizeof(TsV) + 32));      // values in sorted order

@@ -164,12 +164,18 @@ size_t radix_sort_temp_bytes(uint32_t n)
     uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
     size_t hist = (size_t)RS_MAX_BINS * (tiles ? tiles : 1);
     size_t a = ((hist * 4 + (hist + 1) * 4) + 15) & ~(size_t)15;
-    return a + 16 + scan_temp_bytes((uint32_t)hist);
+    return a + 16;
+}
+
+uint32_t radix_sort_scan_len(uint32_t n)
+{
+    uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
+    return (uint32_t)RS_MAX_BINS * (tiles ? tiles : 1);
 }
 
 void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys_out, uint32_t *vals_out,
                       uint32_t *keys_tmp, uint32_t *vals_tmp, const uint32_t *ents_in, uint32_t *ents_out,
-                      uint32_t *ents_tmp, uint32_t n, int bits, void *temp, hipStream_t s)
+                      uint32_t *ents_tmp, uint32_t n, int bits, void *temp, void *scan_state, hipStream_t s)
 {
     if (n == 0) return;
     const uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
@@ -178,7 +184,6 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
     uint32_t *offs = hist + hist_cap;
     const size_t a = ((hist_cap * 4 + (hist_cap + 1) * 4) + 15) & ~(size_t)15;
     unsigned long long *total = (unsigned long long *)((char *)temp + a);
-    void *scan_tmp = (char *)temp + a + 16;
     if (bits < 1) bits = 1;
     const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
     // ping-pong so that the last pass lands in *_out; vals_in == nullptr means identity values
@@ -193,7 +198,7 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
         uint32_t *eo = ents_in ? (to_out ? ents_out : ents_tmp) : nullptr;
         const size_t hist_n = (size_t)(mask + 1) * tiles;
         hipLaunchKernelGGL(rs_upsweep, dim3(tiles), dim3(RS_THREADS), 0, s, ki, n, shift, mask, hist, tiles);
-        exclusive_scan_u32(hist, offs, (uint32_t)hist_n, total, scan_tmp, s);
+        exclusive_scan_u32(hist, offs, (uint32_t)hist_n, total, scan_state, s);
         if (pb > 8)
             hipLaunchKernelGGL(rs_downsweep<9>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
         else

@@ -1,5 +1,20 @@
-// Exclusive prefix sum of u32 counts (CSR offsets of the per-txn PartialDeps and radix digit
-// offsets).  Three launches: tile reduce -> scan of tile sums (one block) -> tile scan + apply.
+// Exclusive prefix sums of u32 counts (CSR offsets of the per-txn PartialDeps, radix digit offsets,
+// stream compaction).  One launch per scan, up to four arrays of the same length at once: a
+// single-pass scan with decoupled look-back.
+//
+//   * a block takes the next tile id from a counter (ids follow start order, so a block only ever
+//     waits on tiles whose blocks are already running), reduces its 4096 items per array and
+//     publishes the aggregate; wave 0 then walks back over the predecessors' status words 64 tiles
+//     at a time until it meets an inclusive prefix, publishes its own inclusive prefix, and the
+//     block writes its tile of offsets;
+//   * a status word is one 8-byte agent-scope atomic (flag | epoch | value), so no payload has to be
+//     ordered behind it (MI355X_MICROARCH.md, inter-workgroup visibility: the 8-B granule);
+//   * the state buffer is self-resetting: it must be zero when allocated (DevBuf::ensure_zeroed),
+//     the epoch in its header tells this launch's statuses from stale ones, and the block that
+//     draws the last tile id -- every other block has drawn its id and published by the time its
+//     look-back completes -- rewinds the counter and advances the epoch for the next launch;
+//   * a look-back that spins for too long falls back to summing the predecessors' inputs itself,
+//     so termination does not depend on dispatch order.
 // Totals are carried in u64 so an overflow of the u32 offset space is detectable on the host.
 #include "device_common.h"
 #include "kernels.h"
@@ -9,111 +24,244 @@ namespace accord {
 namespace {
 constexpr int SC_THREADS = 256;
 constexpr int SC_ITEMS = 16;
-constexpr int SC_TILE = SC_THREADS * SC_ITEMS;
+constexpr uint32_t SC_TILE = SC_THREADS * SC_ITEMS;
+constexpr int SC_MAX_ARRAYS = 4;
 
-__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum, uint64_t *total)
+// status word: flag (2 bits: 0 none, 1 aggregate, 2 inclusive prefix) | epoch (22 bits) | value (40)
+constexpr uint64_t ST_VALUE_MASK = (1ull << 40) - 1;
+constexpr uint32_t ST_EPOCH_MASK = (1u << 22) - 1;
+__device__ __forceinline__ uint64_t st_make(uint32_t flag, uint32_t epoch, uint64_t v)
 {
-    const uint32_t tid = threadIdx.x, w = tid >> 6, l = lane_id();
-    uint64_t inc = wave_incl_scan64(v);
-    if (l == 63) wsum[w] = inc;
-    __syncthreads();
-    uint64_t off = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < SC_THREADS / 64; ++i) {
-        if ((uint32_t)i < w) off += wsum[i];
-        tot += wsum[i];
-    }
-    *total = tot;
-    __syncthreads();
-    return off + inc - v;
+    return ((uint64_t)flag << 62) | ((uint64_t)(epoch & ST_EPOCH_MASK) << 40) | (v & ST_VALUE_MASK);
 }
 
-__global__ __launch_bounds__(SC_THREADS) void sc_reduce(const uint32_t *__restrict__ in, uint32_t n,
-                                                        unsigned long long *__restrict__ sums)
+struct ScanHeader {
+    uint32_t counter;    // next tile id (0 between launches)
+    uint32_t epoch;      // epoch of the previous launch
+    uint32_t pad[2];
+};
+
+struct ScanArgs {
+    const uint32_t *in[SC_MAX_ARRAYS];
+    uint32_t *out[SC_MAX_ARRAYS];
+    unsigned long long *total[SC_MAX_ARRAYS];
+};
+
+__device__ __forceinline__ uint64_t ld_status(const uint64_t *p)
 {
-    __shared__ uint64_t wsum[SC_THREADS / 64];
-    const uint32_t base = blockIdx.x * SC_TILE;
-    uint64_t acc = 0;
-#pragma unroll 4
-    for (int j = 0; j < SC_ITEMS; ++j) {
-        uint32_t idx = base + j * SC_THREADS + threadIdx.x;
-        if (idx < n) acc += in[idx];
-    }
-    for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, 64);
-    if (lane_id() == 0) wsum[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (int i = 0; i < SC_THREADS / 64; ++i) t += wsum[i];
-        sums[blockIdx.x] = t;
-    }
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t *p, uint64_t v)
+{
+    (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(SC_THREADS) void sc_scan_sums(unsigned long long *__restrict__ sums, uint32_t m,
-                                                           unsigned long long *__restrict__ total)
+template <int NA>
+__global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_t n, uint32_t tiles,
+                                                             ScanHeader *__restrict__ hdr, uint64_t *__restrict__ status)
 {
-    __shared__ uint64_t wsum[SC_THREADS / 64];
-    uint64_t carry = 0;
-    for (uint32_t base = 0; base < m; base += SC_THREADS) {
-        uint32_t idx = base + threadIdx.x;
-        uint64_t v = idx < m ? sums[idx] : 0;
-        uint64_t tot;
-        uint64_t ex = block_excl_scan64(v, wsum, &tot);
-        if (idx < m) sums[idx] = carry + ex;
-        carry += tot;
+    __shared__ uint32_t s_id, s_epoch;
+    __shared__ uint64_t s_wsum[NA][SC_THREADS / 64];
+    __shared__ uint64_t s_excl[NA];
+    __shared__ uint32_t tile[NA][SC_TILE];
+    const uint32_t tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    if (tid == 0) {
+        s_id = atomicAdd(&hdr->counter, 1u);
+        s_epoch = (__hip_atomic_load(&hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & ST_EPOCH_MASK;
     }
-    if (threadIdx.x == 0) *total = carry;
-}
+    __syncthreads();
+    const uint32_t b = s_id, e = s_epoch;
+    if (b >= tiles) return;      // only a corrupted state buffer hands out more ids than tiles
+    const uint32_t base = b * SC_TILE;
 
-__global__ __launch_bounds__(SC_THREADS) void sc_apply(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                                       uint32_t n, const unsigned long long *__restrict__ sums,
-                                                       const unsigned long long *__restrict__ total)
+    // load the tile (coalesced), then each thread owns 16 consecutive items
+    uint64_t local[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) {
+            const uint32_t idx = base + j * SC_THREADS + tid;
+            tile[k][j * SC_THREADS + tid] = idx < n ? a.in[k][idx] : 0u;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) acc += tile[k][tid * SC_ITEMS + j];
+        local[k] = acc;
+    }
+    // block scan of the per-thread sums
+    uint64_t incl[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        incl[k] = wave_incl_scan64(local[k]);
+        if (lane == 63) s_wsum[k][w] = incl[k];
+    }
+    __syncthreads();
+    uint64_t agg[NA], woff[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        uint64_t t = 0, o = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < SC_THREADS / 64; ++q) {
+            if (q < w) o += s_wsum[k][q];
+            t += s_wsum[k][q];
+        }
+        agg[k] = t;
+        woff[k] = o;
+    }
+    // publish + look back (wave 0)
+    if (w == 0) {
+        uint64_t excl[NA];
+#pragma unroll
+        for (int k = 0; k < NA; ++k) excl[k] = 0;
+        if (b == 0) {
+#pragma unroll
+            for (int k = 0; k < NA; ++k)
+                if (lane == 0) st_status(&status[(size_t)k * tiles + 0], st_make(2, e, agg[k]));
+        } else {
+#pragma unroll
+            for (int k = 0; k < NA; ++k)
+                if (lane == 0) st_status(&status[(size_t)k * tiles + b], st_make(1, e, agg[k]));
+            int32_t j = (int32_t)b - 1;       // walk back from here
+            uint32_t spins = 0;
+            bool done = false;
+            while (!done) {
+                const int32_t t = j - (int32_t)lane;
+                // a tile counts once all its arrays carry the same flag of this epoch (an
+                // aggregate, or the inclusive prefix); tiles before 0 are an empty prefix
+                uint32_t fmin = 2, fmax = 2;
+                uint64_t val[NA];
+#pragma unroll
+                for (int k = 0; k < NA; ++k) {
+                    val[k] = 0;
+                    if (t >= 0) {
+                        const uint64_t sw = ld_status(&status[(size_t)k * tiles + t]);
+                        const bool cur = (uint32_t)((sw >> 40) & ST_EPOCH_MASK) == e;
+                        const uint32_t f = cur ? (uint32_t)(sw >> 62) : 0u;
+                        fmin = min(fmin, f);
+                        fmax = k == 0 ? f : max(fmax, f);
+                        val[k] = sw & ST_VALUE_MASK;
+                    }
+                }
+                const uint32_t flag = fmin == fmax ? fmin : 0u;
+                const uint64_t pm = __ballot(flag == 2);          // lanes holding an inclusive prefix
+                const uint64_t nm = __ballot(flag == 0);          // lanes not published yet
+                const uint32_t first_p = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
+                const uint64_t below = first_p >= 64 ? ~0ull : ((1ull << first_p) - 1);
+                if (nm & below) {                                  // a predecessor is still working
+                    if (++spins > (1u << 20)) break;               // defensive: fall back below
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                spins = 0;
+#pragma unroll
+                for (int k = 0; k < NA; ++k) {
+                    uint64_t v = lane <= first_p ? val[k] : 0ull;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+                    excl[k] += v;
+                }
+                if (first_p < 64) done = true;
+                else j -= 64;
+            }
+            if (!done) {                       // dispatch order gave no progress: sum the inputs
+#pragma unroll
+                for (int k = 0; k < NA; ++k) {
+                    uint64_t v = 0;
+                    for (uint32_t x = lane; x < base; x += 64) v += a.in[k][x];
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+                    excl[k] = v;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NA; ++k)
+                if (lane == 0) st_status(&status[(size_t)k * tiles + b], st_make(2, e, excl[k] + agg[k]));
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < NA; ++k) s_excl[k] = excl[k];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        uint64_t run = s_excl[k] + woff[k] + incl[k] - local[k];
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) {
+            const uint32_t v = tile[k][tid * SC_ITEMS + j];
+            tile[k][tid * SC_ITEMS + j] = (uint32_t)run;
+            run += v;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) {
+            const uint32_t idx = base + j * SC_THREADS + tid;
+            if (idx < n) a.out[k][idx] = tile[k][j * SC_THREADS + tid];
+        }
+    }
+    if (b == tiles - 1 && tid == 0) {
+#pragma unroll
+        for (int k = 0; k < NA; ++k) {
+            const uint64_t tot = s_excl[k] + agg[k];
+            a.out[k][n] = (uint32_t)tot;
+            if (a.total[k]) *a.total[k] = tot;
+        }
+        // every block has drawn its id and published: rewind for the next launch
+        hdr->counter = 0u;
+        __hip_atomic_store(&hdr->epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__global__ __launch_bounds__(256) void fill_words_kernel(FillList L)
 {
-    __shared__ uint32_t tile[SC_TILE];
-    __shared__ uint64_t wsum[SC_THREADS / 64];
-    const uint32_t base = blockIdx.x * SC_TILE, tid = threadIdx.x;
-#pragma unroll
-    for (int j = 0; j < SC_ITEMS; ++j) {
-        uint32_t idx = base + j * SC_THREADS + tid;
-        tile[j * SC_THREADS + tid] = idx < n ? in[idx] : 0;
-    }
-    __syncthreads();
-    uint64_t local = 0;
-#pragma unroll
-    for (int j = 0; j < SC_ITEMS; ++j) local += tile[tid * SC_ITEMS + j];
-    uint64_t tot;
-    uint64_t run = block_excl_scan64(local, wsum, &tot) + sums[blockIdx.x];
-#pragma unroll
-    for (int j = 0; j < SC_ITEMS; ++j) {
-        uint32_t v = tile[tid * SC_ITEMS + j];
-        tile[tid * SC_ITEMS + j] = (uint32_t)run;
-        run += v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < SC_ITEMS; ++j) {
-        uint32_t idx = base + j * SC_THREADS + tid;
-        if (idx < n) out[idx] = tile[j * SC_THREADS + tid];
-    }
-    if (blockIdx.x == gridDim.x - 1 && tid == 0) out[n] = (uint32_t)*total;
+    const FillDesc d = L.d[blockIdx.y];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.words; i += gridDim.x * blockDim.x) d.p[i] = d.value;
 }
 } // namespace
 
+void launch_fill_words(const FillList &L, hipStream_t s)
+{
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k < L.nd; ++k) mx = L.d[k].words > mx ? L.d[k].words : mx;
+    if (L.nd == 0 || mx == 0) return;
+    uint32_t bx = (mx + 255) / 256;
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(fill_words_kernel, dim3(bx, L.nd), dim3(256), 0, s, L);
+}
+
 size_t scan_temp_bytes(uint32_t n)
 {
+    const uint32_t tiles = (n + SC_TILE - 1) / SC_TILE;
+    return sizeof(ScanHeader) + (size_t)SC_MAX_ARRAYS * (tiles ? tiles : 1) * sizeof(uint64_t);
+}
+
+void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *out, unsigned long long *const *total,
+                          uint32_t n, void *temp, hipStream_t s)
+{
     uint32_t tiles = (n + SC_TILE - 1) / SC_TILE;
-    return ((size_t)(tiles ? tiles : 1) + 2) * sizeof(unsigned long long);
+    if (tiles == 0) tiles = 1;
+    ScanArgs a{};
+    for (int k = 0; k < na; ++k) { a.in[k] = in[k]; a.out[k] = out[k]; a.total[k] = total[k]; }
+    ScanHeader *hdr = (ScanHeader *)temp;
+    uint64_t *status = (uint64_t *)((char *)temp + sizeof(ScanHeader));
+    switch (na) {
+    case 1: hipLaunchKernelGGL(sc_single_pass<1>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
+    case 2: hipLaunchKernelGGL(sc_single_pass<2>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
+    case 3: hipLaunchKernelGGL(sc_single_pass<3>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
+    default: hipLaunchKernelGGL(sc_single_pass<4>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
+    }
 }
 
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, unsigned long long *total_dev, void *temp,
                         hipStream_t s)
 {
-    uint32_t tiles = (n + SC_TILE - 1) / SC_TILE;
-    if (tiles == 0) tiles = 1;
-    unsigned long long *sums = (unsigned long long *)temp;
-    hipLaunchKernelGGL(sc_reduce, dim3(tiles), dim3(SC_THREADS), 0, s, in, n, sums);
-    hipLaunchKernelGGL(sc_scan_sums, dim3(1), dim3(SC_THREADS), 0, s, sums, tiles, total_dev);
-    hipLaunchKernelGGL(sc_apply, dim3(tiles), dim3(SC_THREADS), 0, s, in, out, n, sums, total_dev);
+    exclusive_scan_multi(1, &in, &out, &total_dev, n, temp, s);
 }
 
 } // namespace accord

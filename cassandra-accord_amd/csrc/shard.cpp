@@ -67,7 +67,7 @@ int32_t merge_parts(accord_store *s, const std::vector<Part> &parts, uint32_t n,
     HIPCHECK(s, s->m_val_off.ensure(n1 * 4));
     HIPCHECK(s, s->m_k2v_off.ensure(n1 * 4));
     HIPCHECK(s, s->m_zero.ensure(n1 * 4));
-    HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n)));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n), s->stream));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     std::vector<const void *> tbl(6 * (size_t)G);
     for (uint32_t g = 0; g < G; ++g) {
@@ -218,7 +218,7 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
         HIPCHECK(s, c->total_buf.ensure(16));
         HIPCHECK(s, c->counts.ensure(3 * (size_t)G * 8));
         HIPCHECK(s, c->allcounts.ensure(3 * (size_t)G * 8 * G));
-        HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n_total)));
+        HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n_total), s->stream));
         return ACCORD_OK;
     };
     // flag buffer: allocated by accord_comm_init, so agreeing cannot itself fail on one rank only

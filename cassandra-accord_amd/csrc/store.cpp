@@ -274,17 +274,38 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->rd_rng_off.ensure(n1 * 4));
     HIPCHECK(s, s->rd_val_off.ensure(n1 * 4));
     HIPCHECK(s, s->rd_r2v_off.ensure(n1 * 4));
-    HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n)));
+    // the store's scan state, shared by every scan of the pipeline (radix digit offsets, CSR offsets,
+    // carry compaction): sized for the longest
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max({n, PH, accord::radix_sort_scan_len(PH)})), s->stream));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     HIPCHECK(s, s->rng_owner.ensure((size_t)R * 4));
     HIPCHECK(s, s->is_range.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->rt_excl.ensure(n1 * 4));
     HIPCHECK(s, s->range_txns.ensure((size_t)nrt * 4 + 4));
 
+    HIPCHECK(s, s->fk_list.ensure((size_t)n * 4 + 64));
+    if (R) HIPCHECK(s, s->rd_big.ensure((size_t)n * 4 + 64));
+
     HostTotals *dev = s->status_totals.as<HostTotals>();
     record(s, EV_START);
-    HIPCHECK(s, hipMemsetAsync(dev, 0xFF, sizeof(HostTotals), st));
-    HIPCHECK(s, hipMemsetAsync(&dev->status.overflow, 0, sizeof(uint32_t), st));
+    {   // every small initialisation of the pipeline in one launch
+        accord::FillList fl;
+        fl.add(&dev->status.first, sizeof(dev->status.first), 0xFFFFFFFFu);
+        fl.add(&dev->status.overflow, 4, 0u);
+        fl.add(&dev->status.overflow_first, 4, 0xFFFFFFFFu);
+        fl.add(s->seg_start.p, (size_t)nkeys * 4, 0u);
+        fl.add(s->seg_end.p, (size_t)nkeys * 4, 0u);
+        fl.add(s->fk_list.p, 4, 0u);                                   // fallback list count
+        if (R) {
+            fl.add(s->rd_big.p, 4, 0u);                                 // big range-hit list count
+        } else {
+            fl.add(s->rd_rng_off.p, n1 * 4, 0u);
+            fl.add(s->rd_val_off.p, n1 * 4, 0u);
+            fl.add(s->rd_r2v_off.p, n1 * 4, 0u);
+            fl.add(&dev->totals[3], 3 * sizeof(unsigned long long), 0u);
+        }
+        accord::launch_fill_words(fl, st);
+    }
     if (C) {
         HIPCHECK(s, hipMemcpyAsync(s->pair_key.p, s->cy_key.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
         HIPCHECK(s, hipMemcpyAsync(s->pair_ent.p, s->cy_ent.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
@@ -321,10 +342,8 @@ int32_t accord_deps_compute(accord_store *s)
     accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
                              s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
                              s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), PH,
-                             bits_for(nkeys - 1), s->radix_tmp.p, st);
+                             bits_for(nkeys - 1), s->radix_tmp.p, s->scan_tmp.p, st);
     record(s, EV_SORT);
-    HIPCHECK(s, hipMemsetAsync(s->seg_start.p, 0, (size_t)nkeys * 4, st));
-    HIPCHECK(s, hipMemsetAsync(s->seg_end.p, 0, (size_t)nkeys * 4, st));
     accord::launch_history(PH, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
                            s->seg_end.as<uint32_t>(), s->slice.as<accord::PairSlice>(),
@@ -385,25 +404,22 @@ int32_t accord_deps_compute(accord_store *s)
                                  rp.cnt_k2v, &dev->status, st);
     if (nrt) accord::launch_rangekeys_count(rp, st);
     if (R) {
-        HIPCHECK(s, s->rd_big.ensure((size_t)n * 4 + 64));
         rp.rd_big_count = s->rd_big.as<uint32_t>();
         rp.rd_big_list = rp.rd_big_count + 16;
-        HIPCHECK(s, hipMemsetAsync(rp.rd_big_count, 0, 4, st));
         accord::launch_rangedeps_count(rp, st);
     }
     record(s, EV_COUNT);
-    accord::exclusive_scan_u32(rp.cnt_keys, s->kd_key_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
-    accord::exclusive_scan_u32(kp.cnt_vub, s->vub_off.as<uint32_t>(), n, &dev->totals[1], s->scan_tmp.p, st);
-    accord::exclusive_scan_u32(rp.cnt_k2v, s->kd_k2v_off.as<uint32_t>(), n, &dev->totals[2], s->scan_tmp.p, st);
+    {   // KeyDeps offsets (and RangeDeps offsets) in one launch each
+        const uint32_t *in[3] = {rp.cnt_keys, kp.cnt_vub, rp.cnt_k2v};
+        uint32_t *out[3] = {s->kd_key_off.as<uint32_t>(), s->vub_off.as<uint32_t>(), s->kd_k2v_off.as<uint32_t>()};
+        unsigned long long *tot[3] = {&dev->totals[0], &dev->totals[1], &dev->totals[2]};
+        accord::exclusive_scan_multi(3, in, out, tot, n, s->scan_tmp.p, st);
+    }
     if (R) {
-        accord::exclusive_scan_u32(rp.cnt_rngs, s->rd_rng_off.as<uint32_t>(), n, &dev->totals[3], s->scan_tmp.p, st);
-        accord::exclusive_scan_u32(rp.cnt_vals, s->rd_val_off.as<uint32_t>(), n, &dev->totals[4], s->scan_tmp.p, st);
-        accord::exclusive_scan_u32(rp.cnt_r2v, s->rd_r2v_off.as<uint32_t>(), n, &dev->totals[5], s->scan_tmp.p, st);
-    } else {
-        HIPCHECK(s, hipMemsetAsync(s->rd_rng_off.p, 0, n1 * 4, st));
-        HIPCHECK(s, hipMemsetAsync(s->rd_val_off.p, 0, n1 * 4, st));
-        HIPCHECK(s, hipMemsetAsync(s->rd_r2v_off.p, 0, n1 * 4, st));
-        HIPCHECK(s, hipMemsetAsync(&dev->totals[3], 0, 3 * sizeof(unsigned long long), st));
+        const uint32_t *in[3] = {rp.cnt_rngs, rp.cnt_vals, rp.cnt_r2v};
+        uint32_t *out[3] = {s->rd_rng_off.as<uint32_t>(), s->rd_val_off.as<uint32_t>(), s->rd_r2v_off.as<uint32_t>()};
+        unsigned long long *tot[3] = {&dev->totals[3], &dev->totals[4], &dev->totals[5]};
+        accord::exclusive_scan_multi(3, in, out, tot, n, s->scan_tmp.p, st);
     }
     record(s, EV_SCAN);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
@@ -449,10 +465,8 @@ int32_t accord_deps_compute(accord_store *s)
     rp.rd_rng_start = s->rd_rng_start.as<uint32_t>(); rp.rd_rng_end = s->rd_rng_end.as<uint32_t>();
     rp.rd_vals = s->rd_vals.as<uint32_t>(); rp.rd_r2v = s->rd_r2v.as<int32_t>();
     HIPCHECK(s, s->fk_recs.ensure(accord::keydeps_fast_temp_bytes(n)));
-    HIPCHECK(s, s->fk_list.ensure((size_t)n * 4 + 64));
     kp.fb_count = s->fk_list.as<uint32_t>();
     kp.fb_list = kp.fb_count + 16;
-    HIPCHECK(s, hipMemsetAsync(kp.fb_count, 0, 4, st));
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {
@@ -470,7 +484,7 @@ int32_t accord_deps_compute(accord_store *s)
         const uint32_t thr = s->b_end > s->cfg.window ? s->b_end - s->cfg.window : 0u;
         accord::launch_carry(PH, nkeys, thr, s->sort_key.as<uint32_t>(), s->hist.as<uint32_t>(),
                              s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(),
-                             accord::history_views(s->hist_tmp.p, PH), s->carry_tmp.p, s->cy_key2.as<uint32_t>(),
+                             accord::history_views(s->hist_tmp.p, PH), s->carry_tmp.p, s->scan_tmp.p, s->cy_key2.as<uint32_t>(),
                              s->cy_ent2.as<uint32_t>(), &dev->totals[8], st);
     }
     record(s, EV_COMPACT);

@@ -25,6 +25,15 @@ struct DevBuf {
         if (e == hipSuccess) cap = want;
         return e;
     }
+    // the same, and every (re)allocation starts zeroed, in `stream` order (scan-state buffers rely
+    // on it; the store's streams are non-blocking, so a null-stream memset would not be ordered)
+    hipError_t ensure_zeroed(size_t bytes, hipStream_t stream)
+    {
+        if (bytes <= cap && p) return hipSuccess;
+        hipError_t e = ensure(bytes);
+        if (e == hipSuccess) e = hipMemsetAsync(p, 0, cap, stream);
+        return e;
+    }
     void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
     template <typename T> T *as() const { return (T *)p; }
 };

@@ -42,7 +42,7 @@ int32_t accord_waiting_on_compute(accord_store *s)
     HIPCHECK(s, s->level.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->lv_tmp.ensure(accord::levels_temp_bytes(n)));
     HIPCHECK(s, s->wo_info.ensure(64));
-    HIPCHECK(s, s->scan_tmp.ensure(accord::scan_temp_bytes(n)));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n), s->stream));
     HostTotals *dev = s->status_totals.as<HostTotals>();
 
     accord::WaitingOnParams p{};
