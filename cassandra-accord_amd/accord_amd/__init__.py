@@ -40,6 +40,7 @@ ERR = {
 }
 STORE_PROFILE = 1
 STORE_RESIDENT = 2
+WINDOW_NONE = 0xFFFFFFFF     # no status-at-time model: statuses from CommandStore.register
 
 EXPORTED_SYMBOLS = [
     "accord_store_create", "accord_store_destroy", "accord_last_error", "accord_store_stream",
@@ -51,7 +52,7 @@ EXPORTED_SYMBOLS = [
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
-    "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset",
+    "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset", "accord_txn_register",
 ]
 
 
@@ -192,6 +193,7 @@ def lib() -> C.CDLL:
         L.accord_max_conflicts_reset.argtypes = [C.c_void_p]
         L.accord_store_state.argtypes = [C.c_void_p, C.POINTER(_StoreState)]
         L.accord_store_reset.argtypes = [C.c_void_p]
+        L.accord_txn_register.argtypes = [C.c_void_p, C.c_uint32, _u64p, _u64p, _i32p, _u8p, _u64p, _u64p, _i32p]
         L.accord_max_conflicts_state.argtypes = [C.c_void_p, _u64p, _u64p, _i32p, _u8p]
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
@@ -507,6 +509,21 @@ class CommandStore:
         self._check(lib().accord_store_state(self._h, C.byref(st)))
         return {"next_global": st.next_global, "carry_entries": st.carry_entries,
                 "txns_registered": st.txns_registered}
+
+    def register(self, msb, lsb, node, status, exec_msb=None, exec_lsb=None, exec_node=None):
+        """InternalStatus events (CommandsForKey.update) for txns this resident store holds, named by
+        TxnId (strictly ascending); window must be WINDOW_NONE.  status: 0 TRANSITIVELY_KNOWN ..
+        7 INVALID_OR_TRUNCATED; executeAt for ACCEPTED..APPLIED."""
+        a = [np.ascontiguousarray(msb, np.uint64), np.ascontiguousarray(lsb, np.uint64),
+             np.ascontiguousarray(node, np.int32), np.ascontiguousarray(status, np.uint8)]
+        e = None if exec_msb is None else [np.ascontiguousarray(exec_msb, np.uint64),
+                                           np.ascontiguousarray(exec_lsb, np.uint64),
+                                           np.ascontiguousarray(exec_node, np.int32)]
+        self._check(lib().accord_txn_register(self._h, len(a[0]), a[0].ctypes.data_as(_u64p), a[1].ctypes.data_as(_u64p),
+                                              a[2].ctypes.data_as(_i32p), a[3].ctypes.data_as(_u8p),
+                                              None if e is None else e[0].ctypes.data_as(_u64p),
+                                              None if e is None else e[1].ctypes.data_as(_u64p),
+                                              None if e is None else e[2].ctypes.data_as(_i32p)))
 
     def reset(self):
         """Back to an empty CommandStore (resident state cleared)."""

@@ -136,10 +136,13 @@ void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *va
 void launch_gen_index(uint32_t n, uint32_t base, uint32_t *out, hipStream_t s);
 size_t carry_temp_bytes(uint32_t P, uint32_t nkeys);   // scan state separate (scan of P flags)
 // the entries of the combined history a later batch can still reach (per key: from the last Write
-// with txn < thr, else everything) -> out_key/out_ent, key-major; their count in *total
+// with txn < thr, else everything; or, flags_given, the keep flags already in carry_flags(temp))
+// -> out_key/out_ent, key-major; their count in *total
+uint32_t *carry_flags(void *temp, uint32_t nkeys);   // [P + 1] keep flags inside the carry temp
 void launch_carry(uint32_t P, uint32_t nkeys, uint32_t thr, const uint32_t *sorted_key, const uint32_t *hist,
                   const uint32_t *seg_start, const uint32_t *seg_end, const HistoryViews &hv, void *temp,
-                  void *scan_state, uint32_t *out_key, uint32_t *out_ent, unsigned long long *total, hipStream_t s);
+                  void *scan_state, uint32_t *out_key, uint32_t *out_ent, unsigned long long *total, bool flags_given,
+                  hipStream_t s);
 
 // ---- range txns (rangedeps.hip) ----
 struct RangeDepsParams {

@@ -84,6 +84,8 @@ void launch_gen_index(uint32_t n, uint32_t base, uint32_t *out, hipStream_t s)
     if (n) hipLaunchKernelGGL(gen_index_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, base, out);
 }
 
+uint32_t *carry_flags(void *temp, uint32_t nkeys) { return (uint32_t *)temp + nkeys; }
+
 size_t carry_temp_bytes(uint32_t P, uint32_t nkeys)
 {
     return ((size_t)nkeys + 2ull * ((size_t)P + 1)) * 4 + 64;
@@ -91,18 +93,21 @@ size_t carry_temp_bytes(uint32_t P, uint32_t nkeys)
 
 void launch_carry(uint32_t P, uint32_t nkeys, uint32_t thr, const uint32_t *sorted_key, const uint32_t *hist,
                   const uint32_t *seg_start, const uint32_t *seg_end, const HistoryViews &hv, void *temp,
-                  void *scan_state, uint32_t *out_key, uint32_t *out_ent, unsigned long long *total, hipStream_t s)
+                  void *scan_state, uint32_t *out_key, uint32_t *out_ent, unsigned long long *total, bool flags_given,
+                  hipStream_t s)
 {
     uint32_t *keep = (uint32_t *)temp;
-    uint32_t *flag = keep + nkeys;
+    uint32_t *flag = carry_flags(temp, nkeys);
     uint32_t *off = flag + P + 1;
     if (P == 0) {
         (void)hipMemsetAsync(total, 0, sizeof(*total), s);
         return;
     }
-    hipLaunchKernelGGL(carry_keep_kernel, dim3(grid_for(nkeys)), dim3(256), 0, s, nkeys, thr, hist, seg_start, seg_end,
-                       hv.pw_local, hv.pw_carry, HISTORY_TILE, keep);
-    hipLaunchKernelGGL(carry_mark_kernel, dim3(grid_for(P)), dim3(256), 0, s, P, sorted_key, keep, flag);
+    if (!flags_given) {
+        hipLaunchKernelGGL(carry_keep_kernel, dim3(grid_for(nkeys)), dim3(256), 0, s, nkeys, thr, hist, seg_start,
+                           seg_end, hv.pw_local, hv.pw_carry, HISTORY_TILE, keep);
+        hipLaunchKernelGGL(carry_mark_kernel, dim3(grid_for(P)), dim3(256), 0, s, P, sorted_key, keep, flag);
+    }
     exclusive_scan_u32(flag, off, P, total, scan_state, s);
     hipLaunchKernelGGL(carry_scatter_kernel, dim3(grid_for(P)), dim3(256), 0, s, P, flag, off, sorted_key, hist, out_key,
                        out_ent);

@@ -1,0 +1,405 @@
+// Real status events for a resident store (SURVEY.md §8a a4, §8b accord_txn_register, §8f row 1).
+//
+// A store created with ACCORD_STORE_RESIDENT and window ACCORD_WINDOW_NONE has no status-at-time
+// model: a txn enters its keys' CommandsForKey PREACCEPTED when its batch is computed and keeps that
+// status until accord_txn_register reports another (CommandsForKey.update, local/CommandsForKey.java:
+// 652-706).  The store holds, per global position, the txn's InternalStatus and executeAt, and a
+// TxnId-sorted table to find a txn by TxnId.
+//
+// Deps of a (txn, key) pair whose key history holds an entry with a registered status follow the
+// general mapReduceActive (:614-650) instead of the contiguous-slice fast path:
+//   maxCommittedBefore = max executeAt over COMMITTED/STABLE/APPLIED Writes with executeAt <
+//                        startedBefore (the committed[] search of :620-624; executeAt >= TxnId, so
+//                        only entries before the pair's bound can qualify)
+//   emitted            = entries before the bound whose kind is witnessed, not TRANSITIVELY_KNOWN /
+//                        INVALID_OR_TRUNCATED, and (if committed) executeAt >= maxCommittedBefore
+// The emitted entries of every such pair are written to an extension of the history array and the
+// pair's slice is pointed at them, so the fill kernels are unchanged.
+// Between batches an entry leaves the resident state when its txn is INVALID_OR_TRUNCATED (a
+// truncated committed Write no longer bounds maxCommittedBefore, so nothing else can be dropped
+// without knowing the future events).
+#include "store_impl.h"
+
+#include <algorithm>
+#include <vector>
+
+namespace {
+
+constexpr uint8_t ST_TK = 0, ST_PREACCEPTED = 2, ST_ACCEPTED = 3, ST_COMMITTED = 4, ST_APPLIED = 6, ST_INVALID = 7;
+
+__device__ __forceinline__ bool committed(uint32_t st) { return st >= ST_COMMITTED && st <= ST_APPLIED; }
+
+struct Ts {
+    uint64_t msb, lsb;
+    int32_t node;
+};
+
+__device__ __forceinline__ int tcmp(const Ts &a, const Ts &b) { return ts_cmp(a.msb, a.lsb, a.node, b.msb, b.lsb, b.node); }
+
+struct StatusView {
+    const uint8_t *status;            // [next_global] InternalStatus by global position
+    const uint64_t *emsb, *elsb;      // executeAt by global position
+    const int32_t *enode;
+    uint32_t known;                   // positions >= known are this batch's txns: PREACCEPTED
+};
+
+__device__ __forceinline__ uint32_t status_of(const StatusView &v, uint32_t g)
+{
+    return g < v.known ? v.status[g] : ST_PREACCEPTED;
+}
+__device__ __forceinline__ Ts exec_of(const StatusView &v, uint32_t g)
+{
+    return Ts{v.emsb[g], v.elsb[g], v.enode[g]};
+}
+
+__device__ __forceinline__ void record_error(accord::DevStatus *st, uint32_t i, int32_t code)
+{
+    unsigned long long v = ((unsigned long long)i << 32) | (uint32_t)(-code);
+    atomicMin(&st->first, v);
+}
+
+// keys whose carried history holds a txn with a registered status
+__global__ __launch_bounds__(256) void flag_keys_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
+                                                        const uint32_t *__restrict__ cent, StatusView v,
+                                                        uint32_t *__restrict__ flag)
+{
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x)
+        if (status_of(v, cent[c] & ENT_TXN_MASK) != ST_PREACCEPTED) flag[ckey[c]] = 1u;
+}
+
+struct GenParams {
+    uint32_t n, key_lo;
+    const uint64_t *msb, *lsb;
+    const int32_t *node;
+    const uint64_t *xmsb, *xlsb;      // Accept batch executeAt (nullptr: startedBefore = TxnId)
+    const int32_t *xnode;
+    const uint32_t *key_off, *key_ord, *txn_index, *flag, *hist;
+    accord::PairSlice *slice;
+    uint32_t *gcnt;
+    const uint32_t *goff;
+    uint32_t *hist2;
+    uint32_t ext_base;                // first extension position of hist2
+    StatusView v;
+};
+
+// One pair: maxCommittedBefore, then count (FILL = false) or write (FILL = true) the emitted entries.
+template <bool FILL>
+__device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q)
+{
+    const accord::PairSlice sl = p.slice[q];
+    const uint64_t l = p.lsb[t];
+    const uint32_t wmask = witness_mask((uint32_t)(l >> 1) & 7);
+    Ts sb{p.msb[t], l, p.node[t]};
+    bool p1 = false;    // p1 = executeAt.equals(txnId) ? null : txnId (messages/PreAccept.java:259)
+    if (p.xmsb) {
+        const Ts x{p.xmsb[t], p.xlsb[t], p.xnode[t]};
+        p1 = !(x.msb == sb.msb && ((x.lsb ^ sb.lsb) & 0xFFFFFFFFFFFF001Eull) == 0 && x.node == sb.node);
+        sb = x;
+    }
+    const uint32_t self = p.txn_index[t];
+    // segment start: the slice of a W = infinity history starts at the key's first entry
+    const uint32_t lo = sl.lo, hi = sl.pos;
+    bool has_mcb = false;
+    Ts mcb{0, 0, 0};
+    for (uint32_t x = lo; x < hi; ++x) {
+        const uint32_t e = p.hist[x], g = e & ENT_TXN_MASK;
+        if ((e >> ENT_KIND_SHIFT) != 1u) continue;    // Writes only
+        const uint32_t st = status_of(p.v, g);
+        if (!committed(st)) continue;
+        const Ts ex = exec_of(p.v, g);
+        if (tcmp(ex, sb) >= 0) continue;
+        if (!has_mcb || tcmp(ex, mcb) > 0) { mcb = ex; has_mcb = true; }
+    }
+    uint32_t c = 0;
+    const uint32_t out = FILL ? p.ext_base + p.goff[q] : 0u;
+    for (uint32_t x = lo; x < hi; ++x) {
+        const uint32_t e = p.hist[x], g = e & ENT_TXN_MASK;
+        if (!((wmask >> (e >> ENT_KIND_SHIFT)) & 1u)) continue;
+        if (p1 && g == self) continue;
+        const uint32_t st = status_of(p.v, g);
+        if (st == ST_TK || st == ST_INVALID) continue;
+        if (committed(st) && has_mcb && tcmp(exec_of(p.v, g), mcb) < 0) continue;
+        if (FILL) p.hist2[out + c] = e;
+        ++c;
+    }
+    if (FILL) p.slice[q] = accord::PairSlice{out, out + c, c, 0u};
+    else p.gcnt[q] = c;
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void general_kernel(GenParams p)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < p.n; t += gridDim.x * blockDim.x)
+        for (uint32_t q = p.key_off[t]; q < p.key_off[t + 1]; ++q) {
+            if (!p.flag[p.key_ord[q] - p.key_lo]) { if (!FILL) p.gcnt[q] = 0; continue; }
+            general_pair<FILL>(p, t, q);
+        }
+}
+
+// carry flags of a registered-status store: an entry stays until its txn is INVALID_OR_TRUNCATED
+// (CommandsForKey drops truncated txns, local/CommandsForKey.java:1654-1684; every other entry can
+// still be emitted or bound maxCommittedBefore after later events)
+__global__ __launch_bounds__(256) void prune_mark_kernel(uint32_t P, const uint32_t *__restrict__ hist, StatusView v,
+                                                         uint32_t *__restrict__ keep_flag)
+{
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x)
+        keep_flag[x] = status_of(v, hist[x] & ENT_TXN_MASK) != ST_INVALID ? 1u : 0u;
+}
+
+// ---- registration ----
+struct RegParams {
+    uint32_t n, tx_n;
+    const uint64_t *msb, *lsb;
+    const int32_t *node;
+    const uint8_t *status;
+    const uint64_t *emsb, *elsb;
+    const int32_t *enode;
+    const uint64_t *tmsb, *tlsb;       // the store's TxnIds, ascending
+    const int32_t *tnode;
+    const uint32_t *tg;                // their global positions
+    uint8_t *st;                       // by global position
+    uint64_t *xmsb, *xlsb;
+    int32_t *xnode;
+    uint32_t *pos;                     // out: global position of every event
+    accord::DevStatus *err;
+};
+
+__global__ __launch_bounds__(256) void reg_check_kernel(RegParams p)
+{
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += gridDim.x * blockDim.x) {
+        const Ts id{p.msb[r], p.lsb[r], p.node[r]};
+        if (r > 0 && ts_cmp(p.msb[r - 1], p.lsb[r - 1], p.node[r - 1], id.msb, id.lsb, id.node) >= 0)
+            record_error(p.err, r, ACCORD_ERR_UNSORTED);
+        const uint32_t nw = p.status[r];
+        if (nw > ST_INVALID) { record_error(p.err, r, ACCORD_ERR_ARG); continue; }
+        uint32_t lo = 0, hi = p.tx_n;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (ts_cmp(p.tmsb[m], p.tlsb[m], p.tnode[m], id.msb, id.lsb, id.node) < 0) lo = m + 1; else hi = m;
+        }
+        if (lo >= p.tx_n || ts_cmp(p.tmsb[lo], p.tlsb[lo], p.tnode[lo], id.msb, id.lsb, id.node) != 0) {
+            record_error(p.err, r, ACCORD_ERR_ARG);       // not a txn of this store
+            continue;
+        }
+        const uint32_t g = p.tg[lo];
+        p.pos[r] = g;
+        const uint32_t cur = p.st[g];
+        if (nw < cur) { record_error(p.err, r, ACCORD_ERR_STATE); continue; }   // statuses never go back
+        if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) {
+            const Ts ex{p.emsb[r], p.elsb[r], p.enode[r]};
+            if (ts_cmp(ex.msb, ex.lsb, ex.node, id.msb, id.lsb, id.node) < 0) record_error(p.err, r, ACCORD_ERR_ARG);
+            if (committed(cur) && (ex.msb != p.xmsb[g] || ex.lsb != p.xlsb[g] || ex.node != p.xnode[g]))
+                record_error(p.err, r, ACCORD_ERR_STATE);  // a committed executeAt never changes
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void reg_apply_kernel(RegParams p)
+{
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += gridDim.x * blockDim.x) {
+        const uint32_t g = p.pos[r], nw = p.status[r];
+        p.st[g] = (uint8_t)nw;
+        if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) { p.xmsb[g] = p.emsb[r]; p.xlsb[g] = p.elsb[r]; p.xnode[g] = p.enode[r]; }
+    }
+}
+
+// a computed batch joins the store: TxnId table (ascending) + PREACCEPTED at executeAt = TxnId
+__global__ __launch_bounds__(256) void join_kernel(uint32_t n, uint32_t tx_n, const uint64_t *__restrict__ msb,
+                                                   const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
+                                                   const uint32_t *__restrict__ gidx, uint64_t *__restrict__ tmsb,
+                                                   uint64_t *__restrict__ tlsb, int32_t *__restrict__ tnode,
+                                                   uint32_t *__restrict__ tg, uint8_t *__restrict__ st,
+                                                   uint64_t *__restrict__ xmsb, uint64_t *__restrict__ xlsb,
+                                                   int32_t *__restrict__ xnode)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const uint32_t g = gidx[t];
+        tmsb[tx_n + t] = msb[t]; tlsb[tx_n + t] = lsb[t]; tnode[tx_n + t] = node[t]; tg[tx_n + t] = g;
+        st[g] = ST_PREACCEPTED;
+        xmsb[g] = msb[t]; xlsb[g] = lsb[t]; xnode[g] = node[t];
+    }
+}
+
+inline uint32_t grid_for(uint64_t n)
+{
+    uint64_t b = (n + 255) / 256;
+    return (uint32_t)(b < 1 ? 1 : b > 8192 ? 8192 : b);
+}
+
+// grow a buffer keeping its first `keep` bytes (the store's tables)
+hipError_t grow_keep(DevBuf &b, size_t bytes, size_t keep, hipStream_t s)
+{
+    if (bytes <= b.cap && b.p) return hipSuccess;
+    size_t want = std::max(bytes, b.cap * 2);
+    void *np = nullptr;
+    hipError_t e = hipMalloc(&np, want);
+    if (e != hipSuccess) return e;
+    if (keep && b.p) {
+        e = hipMemcpyAsync(np, b.p, keep, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { (void)hipFree(np); return e; }
+    }
+    if (b.p) (void)hipFree(b.p);
+    b.p = np;
+    b.cap = want;
+    return hipSuccess;
+}
+
+StatusView view_of(accord_store *s)
+{
+    StatusView v;
+    v.status = s->rg_status.as<uint8_t>();
+    v.emsb = s->rg_emsb.as<uint64_t>(); v.elsb = s->rg_elsb.as<uint64_t>(); v.enode = s->rg_enode.as<int32_t>();
+    v.known = s->next_global;
+    return v;
+}
+
+} // namespace
+
+namespace accord_impl {
+
+bool registered_mode(const accord_store *s) { return s->resident && s->cfg.window == ACCORD_WINDOW_NONE; }
+
+// After the segment stage of a registered-status store: pairs on keys with registered entries get
+// their emitted entries materialised; returns the history array the fill must read.
+int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill)
+{
+    const uint32_t n = s->n, P = s->P, nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    hipStream_t st = s->stream;
+    *hist_for_fill = s->hist.as<uint32_t>();
+    if (C == 0 || s->next_global == 0) return ACCORD_OK;       // nothing registered can be on a key yet
+    HIPCHECK(s, s->rg_flag.ensure((size_t)nkeys * 4 + 4));
+    HIPCHECK(s, s->rg_gcnt.ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, s->rg_goff.ensure(((size_t)P + 1) * 4));
+    HIPCHECK(s, hipMemsetAsync(s->rg_flag.p, 0, (size_t)nkeys * 4, st));
+    const StatusView v = view_of(s);
+    hipLaunchKernelGGL(flag_keys_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->pair_key.as<uint32_t>(),
+                       s->pair_ent.as<uint32_t>(), v, s->rg_flag.as<uint32_t>());
+    GenParams g{};
+    g.n = n; g.key_lo = s->cfg.key_lo;
+    g.msb = s->msb.as<uint64_t>(); g.lsb = s->lsb.as<uint64_t>(); g.node = s->node.as<int32_t>();
+    if (s->has_exec) { g.xmsb = s->exec_msb.as<uint64_t>(); g.xlsb = s->exec_lsb.as<uint64_t>(); g.xnode = s->exec_node.as<int32_t>(); }
+    g.key_off = s->key_off.as<uint32_t>(); g.key_ord = s->key_ord.as<uint32_t>();
+    g.txn_index = s->txn_index.as<uint32_t>(); g.flag = s->rg_flag.as<uint32_t>(); g.hist = s->hist.as<uint32_t>();
+    g.slice = s->slice.as<accord::PairSlice>();
+    g.gcnt = s->rg_gcnt.as<uint32_t>(); g.goff = s->rg_goff.as<uint32_t>();
+    g.v = v;
+    if (n) hipLaunchKernelGGL(general_kernel<false>, dim3(grid_for(n)), dim3(256), 0, st, g);
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    accord::exclusive_scan_u32(g.gcnt, s->rg_goff.as<uint32_t>(), P, &dev->totals[9], s->scan_tmp.p, st);
+    unsigned long long X = 0;
+    HIPCHECK(s, hipMemcpyAsync(&X, &dev->totals[9], 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    if (X == 0) return ACCORD_OK;
+    if ((uint64_t)PH + X >= (1ull << 31)) return fail(s, ACCORD_ERR_CAPACITY, "general deps of %llu entries", X);
+    HIPCHECK(s, s->rg_hist2.ensure(((size_t)PH + X) * 4));
+    HIPCHECK(s, hipMemcpyAsync(s->rg_hist2.p, s->hist.p, (size_t)PH * 4, hipMemcpyDeviceToDevice, st));
+    g.hist2 = s->rg_hist2.as<uint32_t>();
+    g.ext_base = PH;
+    if (n) hipLaunchKernelGGL(general_kernel<true>, dim3(grid_for(n)), dim3(256), 0, st, g);
+    *hist_for_fill = s->rg_hist2.as<uint32_t>();
+    return ACCORD_OK;
+}
+
+// Carry flags of a registered-status store (the keep flags launch_carry scans), per history entry.
+int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag)
+{
+    if (PH)
+        hipLaunchKernelGGL(prune_mark_kernel, dim3(grid_for(PH)), dim3(256), 0, s->stream, PH, s->hist.as<uint32_t>(),
+                           view_of(s), keep_flag);
+    return ACCORD_OK;
+}
+
+// A computed batch of a registered-status store joins its txn tables (after the compute succeeded).
+int32_t status_join_batch(accord_store *s)
+{
+    const uint32_t n = s->n;
+    if (n == 0) return ACCORD_OK;
+    hipStream_t st = s->stream;
+    const size_t tx = s->rg_tx_n, G = s->b_end;
+    HIPCHECK(s, grow_keep(s->rg_tmsb, (tx + n) * 8, tx * 8, st));
+    HIPCHECK(s, grow_keep(s->rg_tlsb, (tx + n) * 8, tx * 8, st));
+    HIPCHECK(s, grow_keep(s->rg_tnode, (tx + n) * 4, tx * 4, st));
+    HIPCHECK(s, grow_keep(s->rg_tg, (tx + n) * 4, tx * 4, st));
+    const size_t known = s->rg_known;
+    HIPCHECK(s, grow_keep(s->rg_status, G, known, st));
+    HIPCHECK(s, grow_keep(s->rg_emsb, G * 8, known * 8, st));
+    HIPCHECK(s, grow_keep(s->rg_elsb, G * 8, known * 8, st));
+    HIPCHECK(s, grow_keep(s->rg_enode, G * 4, known * 4, st));
+    if (G > known)   // positions no txn of this store holds (txn_index gaps): never looked at
+        HIPCHECK(s, hipMemsetAsync(s->rg_status.as<uint8_t>() + known, ST_PREACCEPTED, G - known, st));
+    hipLaunchKernelGGL(join_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, (uint32_t)tx, s->msb.as<uint64_t>(),
+                       s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
+                       s->rg_tmsb.as<uint64_t>(), s->rg_tlsb.as<uint64_t>(), s->rg_tnode.as<int32_t>(),
+                       s->rg_tg.as<uint32_t>(), s->rg_status.as<uint8_t>(), s->rg_emsb.as<uint64_t>(),
+                       s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>());
+    HIPCHECK(s, hipStreamSynchronize(st));
+    s->rg_tx_n = (uint32_t)(tx + n);
+    s->rg_known = (uint32_t)G;
+    return ACCORD_OK;
+}
+
+} // namespace accord_impl
+
+extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64_t *msb, const uint64_t *lsb,
+                                       const int32_t *node, const uint8_t *status, const uint64_t *exec_msb,
+                                       const uint64_t *exec_lsb, const int32_t *exec_node)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (!accord_impl::registered_mode(s))
+        return fail(s, ACCORD_ERR_STATE, "accord_txn_register needs a resident store with window ACCORD_WINDOW_NONE");
+    if (n == 0) return ACCORD_OK;
+    if (!msb || !lsb || !node || !status) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: null argument");
+    bool need_exec = false;
+    for (uint32_t r = 0; r < n; ++r) {
+        if (status[r] > ST_INVALID) return fail(s, ACCORD_ERR_ARG, "event %u: InternalStatus ordinal %u", r, status[r]);
+        need_exec |= status[r] >= ST_ACCEPTED && status[r] <= ST_APPLIED;
+    }
+    if (need_exec && (!exec_msb || !exec_lsb || !exec_node))
+        return fail(s, ACCORD_ERR_ARG, "ACCEPTED..APPLIED events need an executeAt");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    hipStream_t st = s->stream;
+    DevBuf *T = s->op_tmp;
+    HIPCHECK(s, T[0].ensure((size_t)n * 8)); HIPCHECK(s, T[1].ensure((size_t)n * 8)); HIPCHECK(s, T[2].ensure((size_t)n * 4));
+    HIPCHECK(s, T[3].ensure((size_t)n)); HIPCHECK(s, T[4].ensure((size_t)n * 8)); HIPCHECK(s, T[5].ensure((size_t)n * 8));
+    HIPCHECK(s, T[6].ensure((size_t)n * 4)); HIPCHECK(s, T[7].ensure((size_t)n * 4));
+    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
+    HIPCHECK(s, hipMemcpyAsync(T[0].p, msb, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    HIPCHECK(s, hipMemcpyAsync(T[1].p, lsb, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    HIPCHECK(s, hipMemcpyAsync(T[2].p, node, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    HIPCHECK(s, hipMemcpyAsync(T[3].p, status, n, hipMemcpyHostToDevice, st));
+    if (need_exec) {
+        HIPCHECK(s, hipMemcpyAsync(T[4].p, exec_msb, (size_t)n * 8, hipMemcpyHostToDevice, st));
+        HIPCHECK(s, hipMemcpyAsync(T[5].p, exec_lsb, (size_t)n * 8, hipMemcpyHostToDevice, st));
+        HIPCHECK(s, hipMemcpyAsync(T[6].p, exec_node, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    }
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    HIPCHECK(s, hipMemsetAsync(&dev->status, 0xFF, sizeof(dev->status), st));
+    RegParams p{};
+    p.n = n; p.tx_n = s->rg_tx_n;
+    p.msb = T[0].as<uint64_t>(); p.lsb = T[1].as<uint64_t>(); p.node = T[2].as<int32_t>(); p.status = T[3].as<uint8_t>();
+    p.emsb = T[4].as<uint64_t>(); p.elsb = T[5].as<uint64_t>(); p.enode = T[6].as<int32_t>();
+    p.tmsb = s->rg_tmsb.as<uint64_t>(); p.tlsb = s->rg_tlsb.as<uint64_t>(); p.tnode = s->rg_tnode.as<int32_t>();
+    p.tg = s->rg_tg.as<uint32_t>();
+    p.st = s->rg_status.as<uint8_t>();
+    p.xmsb = s->rg_emsb.as<uint64_t>(); p.xlsb = s->rg_elsb.as<uint64_t>(); p.xnode = s->rg_enode.as<int32_t>();
+    p.pos = T[7].as<uint32_t>();
+    p.err = &dev->status;
+    if (p.tx_n == 0) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: the store holds no txn yet");
+    hipLaunchKernelGGL(reg_check_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
+    accord::DevStatus hs;
+    HIPCHECK(s, hipMemcpyAsync(&hs, &dev->status, sizeof(hs), hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    if (hs.first != ~0ull) {
+        const uint32_t r = (uint32_t)(hs.first >> 32);
+        const int32_t code = -(int32_t)(uint32_t)hs.first;
+        const char *why = code == ACCORD_ERR_UNSORTED ? "TxnIds not strictly ascending"
+                        : code == ACCORD_ERR_STATE ? "status goes back, or a committed executeAt changes"
+                        : "unknown TxnId, or executeAt before TxnId";
+        return fail(s, code, "accord_txn_register: event %u rejected (%s); nothing applied", r, why);
+    }
+    hipLaunchKernelGGL(reg_apply_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
+    HIPCHECK(s, hipStreamSynchronize(st));
+    HIPCHECK(s, hipGetLastError());
+    return ACCORD_OK;
+}

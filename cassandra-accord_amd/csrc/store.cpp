@@ -88,7 +88,7 @@ int32_t accord_store_create(const accord_store_cfg *cfg, accord_store **out)
     s->resident = (cfg->flags & ACCORD_STORE_RESIDENT) != 0;
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventCreate(&ev);
-    uint32_t span_need = cfg->window + 2048;
+    const uint64_t span_need = (uint64_t)cfg->window + 2048;
     s->wpl = span_need <= 4096 ? 1 : span_need <= 8192 ? 2 : 4;
     *out = s;
     return ACCORD_OK;
@@ -110,7 +110,8 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
-                      &s->carry_tmp};
+                      &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
+                      &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2};
     accord_impl::shard_comm_destroy(s);
     for (DevBuf *b : bufs) b->release();
     for (DepSet &d : s->ds) d.release();
@@ -357,6 +358,12 @@ int32_t accord_deps_compute(accord_store *s)
     kp.txn_index = s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr;
     kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
     kp.hist = s->hist.as<uint32_t>();
+    if (accord_impl::registered_mode(s)) {   // pairs on keys with registered statuses: general filter
+        const uint32_t *h = nullptr;
+        int32_t rc = accord_impl::status_general_pairs(s, C, PH, &h);
+        if (rc) return rc;
+        kp.hist = h;
+    }
     kp.slice = s->slice.as<accord::PairSlice>();
     kp.cnt_vub = s->cnt_vub.as<uint32_t>();
     kp.cnt_vals = s->cnt_vals.as<uint32_t>();
@@ -482,10 +489,15 @@ int32_t accord_deps_compute(accord_store *s)
     if (s->resident) {
         // what the next batch needs of this history (the stream ends at b_end)
         const uint32_t thr = s->b_end > s->cfg.window ? s->b_end - s->cfg.window : 0u;
+        const bool reg = accord_impl::registered_mode(s);
+        if (reg) {
+            int32_t rc = accord_impl::status_prune_flags(s, PH, accord::carry_flags(s->carry_tmp.p, nkeys));
+            if (rc) return rc;
+        }
         accord::launch_carry(PH, nkeys, thr, s->sort_key.as<uint32_t>(), s->hist.as<uint32_t>(),
                              s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(),
                              accord::history_views(s->hist_tmp.p, PH), s->carry_tmp.p, s->scan_tmp.p, s->cy_key2.as<uint32_t>(),
-                             s->cy_ent2.as<uint32_t>(), &dev->totals[8], st);
+                             s->cy_ent2.as<uint32_t>(), &dev->totals[8], reg, st);
     }
     record(s, EV_COMPACT);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
@@ -497,6 +509,10 @@ int32_t accord_deps_compute(accord_store *s)
         s->tot_vals = s->pinned->totals[7];
     }
     if (s->resident) {      // the batch is part of the store's stream now
+        if (accord_impl::registered_mode(s)) {
+            int32_t rc = accord_impl::status_join_batch(s);
+            if (rc) return rc;
+        }
         std::swap(s->cy_key, s->cy_key2);
         std::swap(s->cy_ent, s->cy_ent2);
         s->carry_n = (uint32_t)s->pinned->totals[8];
@@ -545,6 +561,7 @@ int32_t accord_store_reset(accord_store *s)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     s->next_global = 0; s->carry_n = 0; s->has_prev = false;
+    s->rg_tx_n = 0; s->rg_known = 0;
     s->prev_msb = s->prev_lsb = 0; s->prev_node = 0;
     s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->wo_done = false;
     return ACCORD_OK;

@@ -99,6 +99,12 @@ struct accord_store {
     uint64_t prev_msb = 0, prev_lsb = 0;
     int32_t prev_node = 0;
     DevBuf cy_key, cy_ent, cy_key2, cy_ent2, carry_tmp;
+    // registered statuses (status.hip; resident + ACCORD_WINDOW_NONE): TxnId table sorted
+    // (rg_t*, rg_tx_n entries, rg_tg = global position), InternalStatus + executeAt by global
+    // position (rg_known positions), per-batch work
+    DevBuf rg_tmsb, rg_tlsb, rg_tnode, rg_tg, rg_status, rg_emsb, rg_elsb, rg_enode;
+    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2;
+    uint32_t rg_tx_n = 0, rg_known = 0;
     // the uploaded batch: its carried-entry prefix, where it ends (global) and its last TxnId
     uint32_t b_end = 0;
     bool b_registered = false;     // the uploaded batch was computed into the resident stream
@@ -141,6 +147,11 @@ struct accord_store {
 namespace accord_impl {
 int32_t fail(accord_store *s, int32_t code, const char *fmt, ...);
 void shard_comm_destroy(accord_store *s);
+// registered statuses (status.hip)
+bool registered_mode(const accord_store *s);
+int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill);
+int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
+int32_t status_join_batch(accord_store *s);
 }
 using accord_impl::fail;
 

@@ -59,7 +59,8 @@ typedef struct {
     int32_t  device;        /* HIP device ordinal */
     uint32_t key_lo;        /* store owns key ordinals [key_lo, key_hi) (CommandStores slice) */
     uint32_t key_hi;
-    uint32_t window;        /* W of the status-at-time model */
+    uint32_t window;        /* W of the status-at-time model; ACCORD_WINDOW_NONE: none
+                               (statuses from accord_txn_register, resident stores) */
     uint32_t flags;         /* ACCORD_STORE_PROFILE | ACCORD_STORE_RESIDENT */
     uint32_t reserved;
 } accord_store_cfg;
@@ -136,6 +137,31 @@ void       *accord_store_stream(accord_store *store);        /* the store's hipS
  * older entries are pruned for good, as committed entries below maxCommittedBefore are,
  * local/CommandsForKey.java:620-645,1654-1684).  A rejected batch leaves the state unchanged.
  * Key txns only in this build (a range txn in a resident store: ACCORD_ERR_STATE). */
+/* Real status events (SURVEY.md §8b accord_txn_register): a resident store created with window
+ * ACCORD_WINDOW_NONE has no status-at-time model -- every txn enters its keys' CommandsForKey
+ * PREACCEPTED when its batch is computed (CommandsForKey.insert, local/CommandsForKey.java:880-944)
+ * and keeps that status until an event changes it: CommandsForKey.update(prev, next) with the new
+ * InternalStatus and executeAt (:652-706; ordinals below, :194-203).  mapReduceActive then runs in
+ * full (:614-650): maxCommittedBefore over the COMMITTED/STABLE/APPLIED Writes' executeAt, the
+ * prune of committed entries below it, TRANSITIVELY_KNOWN / INVALID_OR_TRUNCATED never emitted.
+ * Events name txns the store holds by TxnId (strictly ascending within a call); statuses never go
+ * back and a committed executeAt never changes (ACCORD_ERR_STATE; the checkState of :674-690); an
+ * event for ACCEPTED..APPLIED carries an executeAt >= TxnId.  A rejected call applies nothing.
+ * An entry leaves the resident state when its txn becomes INVALID_OR_TRUNCATED (CommandsForKey drops
+ * truncated txns, :1654-1684). */
+#define ACCORD_WINDOW_NONE          0xFFFFFFFFu
+#define ACCORD_ST_TRANSITIVELY_KNOWN 0
+#define ACCORD_ST_HISTORICAL         1
+#define ACCORD_ST_PREACCEPTED        2
+#define ACCORD_ST_ACCEPTED           3
+#define ACCORD_ST_COMMITTED          4
+#define ACCORD_ST_STABLE             5
+#define ACCORD_ST_APPLIED            6
+#define ACCORD_ST_INVALID_OR_TRUNCATED 7
+int32_t accord_txn_register(accord_store *store, uint32_t n, const uint64_t *msb, const uint64_t *lsb,
+                            const int32_t *node, const uint8_t *status, const uint64_t *exec_msb,
+                            const uint64_t *exec_lsb, const int32_t *exec_node);
+
 typedef struct {
     uint64_t next_global;       /* global position of the next txn */
     uint64_t carry_entries;     /* history entries kept for later batches */

@@ -598,8 +598,8 @@ static int stream_literal(const or_stream *s, uint32_t n, or_deps *out)
         if (reg_to < i + 1) reg_to = i + 1;
         /* 1. status at time i: txn j = i-W-1 leaves the window -> APPLIED (executeAt=txnId) if a
          *    key txn, Erased if a range txn. */
-        if (i >= s->window + 1) {
-            uint32_t j = i - s->window - 1;
+        if ((uint64_t)i >= (uint64_t)s->window + 1) {
+            uint32_t j = (uint32_t)((uint64_t)i - s->window - 1);
             if (domain_of(s->lsb[j]) == 0) {
                 if (is_globally_visible(kind_of(s->lsb[j])) == 1)
                     for (uint32_t p = s->key_off[j]; p < s->key_off[j + 1]; ++p)
@@ -1510,3 +1510,179 @@ int or_max_conflicts(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const
     }
     return 0;
 }
+
+/* ==========================================================================================
+ * Stateful literal CommandStore (test infrastructure): a resident store fed batch by batch,
+ * with real status events in between.  Key txns only.  Every txn a batch carries is inserted
+ * into its keys' CommandsForKey as PREACCEPTED when it is processed (CommandsForKey.insert,
+ * local/CommandsForKey.java:880-944, via SafeCommandStore.updateCommandsForKey :212-239); an
+ * event (accord_txn_register) is CommandsForKey.update(prev, next) with the new InternalStatus
+ * and executeAt on every key of the txn (:652-706, the committed[] index rebuilt by the
+ * constructor :422-470).  There is no status-at-time model: a txn keeps PREACCEPTED until an
+ * event changes it.  Deps values are global positions (the order txns entered the store).
+ * ========================================================================================== */
+struct or_lstore {
+    uint32_t nkeys;
+    cfk_t *cfks;
+    ts_t *tbl;                 /* TxnIds by global position */
+    uint32_t *koff, *kord;     /* keys of every registered txn (CSR by global position) */
+    uint32_t n, cap, nk, kcap;
+    uint8_t *status;           /* current InternalStatus of every txn */
+    ts_t *exec;
+};
+
+or_lstore *or_lstore_create(uint32_t nkeys)
+{
+    or_lstore *s = (or_lstore *)calloc(1, sizeof(or_lstore));
+    if (!s) return NULL;
+    s->nkeys = nkeys;
+    s->cfks = (cfk_t *)calloc(nkeys ? nkeys : 1, sizeof(cfk_t));
+    s->koff = (uint32_t *)calloc(1, sizeof(uint32_t));
+    if (!s->cfks || !s->koff) { or_lstore_free(s); return NULL; }
+    return s;
+}
+
+void or_lstore_free(or_lstore *s)
+{
+    if (!s) return;
+    if (s->cfks) for (uint32_t k = 0; k < s->nkeys; ++k) { free(s->cfks[k].txns); free(s->cfks[k].committed); }
+    free(s->cfks); free(s->tbl); free(s->koff); free(s->kord); free(s->status); free(s->exec);
+    free(s);
+}
+
+static int lstore_reserve(or_lstore *s, uint32_t n, uint32_t nk)
+{
+    if (n > s->cap) {
+        uint32_t c = s->cap ? s->cap : 1024;
+        while (c < n) c *= 2;
+        ts_t *t = (ts_t *)realloc(s->tbl, (size_t)c * sizeof(ts_t));
+        if (!t) return -1;
+        s->tbl = t;
+        uint32_t *ko = (uint32_t *)realloc(s->koff, ((size_t)c + 1) * sizeof(uint32_t));
+        if (!ko) return -1;
+        s->koff = ko;
+        uint8_t *st = (uint8_t *)realloc(s->status, c);
+        if (!st) return -1;
+        s->status = st;
+        ts_t *ex = (ts_t *)realloc(s->exec, (size_t)c * sizeof(ts_t));
+        if (!ex) return -1;
+        s->exec = ex;
+        s->cap = c;
+    }
+    if (nk > s->kcap) {
+        uint32_t c = s->kcap ? s->kcap : 4096;
+        while (c < nk) c *= 2;
+        uint32_t *kk = (uint32_t *)realloc(s->kord, (size_t)c * sizeof(uint32_t));
+        if (!kk) return -1;
+        s->kord = kk;
+        s->kcap = c;
+    }
+    return 0;
+}
+
+int or_lstore_batch(or_lstore *s, const or_stream *b, or_deps *out)
+{
+    const uint32_t n = b->n;
+    int rc = validate(b, n);
+    if (!rc) rc = validate_exec(b, n);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (domain_of(b->lsb[i]) != 0) return -5;                                   /* key txns only */
+        for (uint32_t p = b->key_off[i]; p < b->key_off[i + 1]; ++p) if (b->key_ord[p] >= s->nkeys) return -4;
+    }
+    if (n && s->n && or_ts_compare(s->tbl[s->n - 1].msb, s->tbl[s->n - 1].lsb, s->tbl[s->n - 1].node,
+                                   b->msb[0], b->lsb[0], b->node[0]) >= 0) return -2;
+    const uint32_t base = s->n;
+    if (lstore_reserve(s, base + n, s->koff[base] + b->key_off[n])) return -1;
+    for (uint32_t i = 0; i < n; ++i) {                 /* the batch's TxnIds and keys (not registered yet) */
+        ts_t t = {b->msb[i], b->lsb[i], b->node[i]};
+        s->tbl[base + i] = t;
+        s->koff[base + i + 1] = s->koff[base + i] + (b->key_off[i + 1] - b->key_off[i]);
+        memcpy(s->kord + s->koff[base + i], b->key_ord + b->key_off[i], (b->key_off[i + 1] - b->key_off[i]) * 4);
+        s->status[base + i] = S_PREACCEPTED;
+        s->exec[base + i] = t;
+    }
+    mm_builder kb;
+    mm_out kd, rd;
+    mmb_init(&kb, s->tbl);
+    if (mmo_init(&kd) || mmo_init(&rd)) return -1;
+    rc = -1;
+    uint32_t reg = 0;                                  /* batch txns [0, reg) are inserted */
+    for (uint32_t i = 0; i < n; ++i) {
+        const ts_t sb = started_before(b, i);
+        const long p1 = p1_of(b, i) >= 0 ? (long)(base + i) : -1;
+        uint32_t reg_to = bound_of(b, n, &sb, i);      /* an Accept sees the batch txns started before executeAt */
+        if (reg_to < i + 1) reg_to = i + 1;
+        for (; reg < reg_to; ++reg) {
+            const uint32_t g = base + reg;
+            if (is_globally_visible(kind_of(b->lsb[reg])) == 1)
+                for (uint32_t p = b->key_off[reg]; p < b->key_off[reg + 1]; ++p)
+                    if (cfk_insert(&s->cfks[b->key_ord[p]], s->tbl, g, S_PREACCEPTED)) goto done;
+        }
+        const int test_kinds = witnesses_of(kind_of(b->lsb[i]));
+        mmb_reset(&kb);
+        for (uint32_t p = b->key_off[i]; p < b->key_off[i + 1]; ++p) {
+            const uint32_t key = b->key_ord[p];
+            if (cfk_map_reduce_active(&s->cfks[key], s->tbl, &sb, test_kinds, key, &kb, p1)) goto done;
+        }
+        if (mmb_build(&kb, &kd, 0)) goto done;
+        if (mmo_close_txn(&rd)) goto done;             /* no RangeDeps */
+    }
+    s->n = base + n;
+    if (alloc_out(out, &kd, &rd, n)) goto done;
+    rc = 0;
+done:
+    if (rc) s->n = base;
+    mmb_free(&kb);
+    mmo_free(&kd); mmo_free(&rd);
+    return rc;
+}
+
+/* a status event for each of n txns (strictly ascending TxnIds, all known to the store):
+ * InternalStatus ordinals (local/CommandsForKey.java:194-203); executeAt for ACCEPTED and above.
+ * Statuses never go back; a committed executeAt never changes (the checkState of :674-690). */
+int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
+                       const uint8_t *status, const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode)
+{
+    uint32_t *pos = (uint32_t *)malloc((size_t)(n ? n : 1) * sizeof(uint32_t));
+    if (!pos) return -1;
+    for (uint32_t r = 0; r < n; ++r) {                 /* validate everything before changing anything */
+        if (r && or_ts_compare(msb[r - 1], lsb[r - 1], node[r - 1], msb[r], lsb[r], node[r]) >= 0) { free(pos); return -2; }
+        if (status[r] > S_INVALID_OR_TRUNCATED) { free(pos); return -1; }
+        uint32_t lo = 0, hi = s->n;
+        while (lo < hi) {
+            uint32_t m = (lo + hi) / 2;
+            if (or_ts_compare(s->tbl[m].msb, s->tbl[m].lsb, s->tbl[m].node, msb[r], lsb[r], node[r]) < 0) lo = m + 1; else hi = m;
+        }
+        if (lo >= s->n || !or_ts_equals(s->tbl[lo].msb, s->tbl[lo].lsb, s->tbl[lo].node, msb[r], lsb[r], node[r])) { free(pos); return -1; }
+        const uint32_t g = lo;
+        const uint8_t cur = s->status[g], nw = status[r];
+        if (nw < cur) { free(pos); return -10; }
+        const int has_info = nw >= S_ACCEPTED && nw <= S_APPLIED;
+        if (has_info) {
+            if (!emsb) { free(pos); return -1; }
+            if (or_ts_compare(emsb[r], elsb[r], enode[r], s->tbl[g].msb, s->tbl[g].lsb, s->tbl[g].node) < 0) { free(pos); return -1; }
+            const int cur_committed = cur >= S_COMMITTED && cur <= S_APPLIED;
+            if (cur_committed && (emsb[r] != s->exec[g].msb || elsb[r] != s->exec[g].lsb || enode[r] != s->exec[g].node)) {
+                free(pos); return -10;
+            }
+        }
+        pos[r] = g;
+    }
+    for (uint32_t r = 0; r < n; ++r) {
+        const uint32_t g = pos[r];
+        const uint8_t nw = status[r];
+        const int has_info = nw >= S_ACCEPTED && nw <= S_APPLIED;
+        ts_t ex = s->exec[g];
+        if (has_info) { ex.msb = emsb[r]; ex.lsb = elsb[r]; ex.node = enode[r]; }
+        s->status[g] = nw;
+        s->exec[g] = ex;
+        if (is_globally_visible(kind_of(s->tbl[g].lsb)) != 1) continue;   /* never inserted into CFK */
+        for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p)
+            if (cfk_update_status(&s->cfks[s->kord[p]], s->tbl, g, nw, &ex)) { free(pos); return -1; }
+    }
+    free(pos);
+    return 0;
+}
+
+uint32_t or_lstore_size(const or_lstore *s) { return s->n; }

@@ -81,6 +81,17 @@ int  or_stream_deps_fast(const or_stream *s, or_deps *out);
 int  or_stream_deps_literal_prefix(const or_stream *s, uint32_t limit, or_deps *out);
 void or_deps_free(or_deps *d);
 
+/* ---- stateful literal CommandStore (resident store + status events, key txns only) ---- */
+typedef struct or_lstore or_lstore;
+or_lstore *or_lstore_create(uint32_t nkeys);
+void       or_lstore_free(or_lstore *s);
+/* one batch in TxnId order after everything the store holds; values are global positions */
+int        or_lstore_batch(or_lstore *s, const or_stream *b, or_deps *out);
+/* InternalStatus events (0 TRANSITIVELY_KNOWN .. 7 INVALID_OR_TRUNCATED) for known txns */
+int        or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
+                              const uint8_t *status, const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode);
+uint32_t   or_lstore_size(const or_lstore *s);
+
 /* ---- primitives restated for the reference's own property tests ---- */
 
 /* Timestamp.compareTo (Timestamp.java:208-217) */

@@ -340,3 +340,59 @@ def max_conflicts(s, key_lo: int, nkeys: int, state=None, first: int = 0, exec_a
     if rc != 0:
         raise OracleError(rc)
     return out, st, int(folded.value)
+
+
+class LStore:
+    """Stateful literal CommandStore (or_lstore_*): batches fed in order, InternalStatus events in
+    between; deps values are global positions.  Key txns only."""
+    TK, HISTORICAL, PREACCEPTED, ACCEPTED, COMMITTED, STABLE, APPLIED, INVALID = range(8)
+
+    def __init__(self, nkeys: int):
+        L = lib()
+        if not getattr(L, "_lstore_typed", False):
+            L.or_lstore_create.argtypes = [C.c_uint32]
+            L.or_lstore_create.restype = C.c_void_p
+            L.or_lstore_free.argtypes = [C.c_void_p]
+            L.or_lstore_free.restype = None
+            L.or_lstore_batch.argtypes = [C.c_void_p, C.POINTER(_OrStream), C.POINTER(_OrDeps)]
+            L.or_lstore_register.argtypes = [C.c_void_p, C.c_uint32, _u64p, _u64p, _i32p, _u8p, _u64p, _u64p, _i32p]
+            L.or_lstore_size.argtypes = [C.c_void_p]
+            L.or_lstore_size.restype = C.c_uint32
+            L._lstore_typed = True
+        self._h = L.or_lstore_create(nkeys)
+
+    def close(self):
+        if self._h:
+            lib().or_lstore_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def size(self) -> int:
+        return lib().or_lstore_size(self._h)
+
+    def batch(self, s: Stream) -> PartialDeps:
+        o, keep = _or_stream(s, 0)
+        d = _OrDeps()
+        rc = lib().or_lstore_batch(self._h, C.byref(o), C.byref(d))
+        if rc != 0:
+            raise OracleError(rc)
+        try:
+            return _to_partial(d)
+        finally:
+            lib().or_deps_free(C.byref(d))
+
+    def register(self, msb, lsb, node, status, exec_msb=None, exec_lsb=None, exec_node=None):
+        a = [np.ascontiguousarray(msb, np.uint64), np.ascontiguousarray(lsb, np.uint64),
+             np.ascontiguousarray(node, np.int32), np.ascontiguousarray(status, np.uint8)]
+        e = None if exec_msb is None else [np.ascontiguousarray(exec_msb, np.uint64),
+                                           np.ascontiguousarray(exec_lsb, np.uint64),
+                                           np.ascontiguousarray(exec_node, np.int32)]
+        rc = lib().or_lstore_register(self._h, len(a[0]), a[0].ctypes.data_as(_u64p), a[1].ctypes.data_as(_u64p),
+                                      a[2].ctypes.data_as(_i32p), a[3].ctypes.data_as(_u8p),
+                                      None if e is None else e[0].ctypes.data_as(_u64p),
+                                      None if e is None else e[1].ctypes.data_as(_u64p),
+                                      None if e is None else e[2].ctypes.data_as(_i32p))
+        if rc != 0:
+            raise OracleError(rc)
