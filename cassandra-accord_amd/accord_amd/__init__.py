@@ -53,7 +53,9 @@ EXPORTED_SYMBOLS = [
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
     "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset", "accord_txn_register",
+    "accord_deps_visit",
 ]
+VISIT_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32)
 
 
 class AccordError(RuntimeError):
@@ -193,6 +195,7 @@ def lib() -> C.CDLL:
         L.accord_max_conflicts_reset.argtypes = [C.c_void_p]
         L.accord_store_state.argtypes = [C.c_void_p, C.POINTER(_StoreState)]
         L.accord_store_reset.argtypes = [C.c_void_p]
+        L.accord_deps_visit.argtypes = [C.POINTER(_Deps), C.c_uint32, VISIT_FN, C.c_void_p]
         L.accord_txn_register.argtypes = [C.c_void_p, C.c_uint32, _u64p, _u64p, _i32p, _u8p, _u64p, _u64p, _i32p]
         L.accord_max_conflicts_state.argtypes = [C.c_void_p, _u64p, _u64p, _i32p, _u8p]
         for name in EXPORTED_SYMBOLS:
@@ -441,6 +444,33 @@ class PartialDeps:
             else:
                 kw[f] = np.concatenate(arrs) if arrs else np.zeros(0, np.uint32)
         return PartialDeps(**kw)
+
+    def to_c(self):
+        """A host accord_deps view of this set (arrays kept alive by the returned tuple)."""
+        keep = [np.ascontiguousarray(getattr(self, f)) for f in PartialDeps.FIELDS]
+        d = _Deps()
+        d.n = self.n
+        for f, a in zip(PartialDeps.FIELDS, keep):
+            setattr(d, f, a.ctypes.data_as(_i32p if a.dtype == np.int32 else _u32p))
+        d.kd_keys_total = int(self.kd_key_off[-1]); d.kd_vals_total = int(self.kd_val_off[-1])
+        d.kd_k2v_total = int(self.kd_k2v_off[-1]); d.rd_rngs_total = int(self.rd_rng_off[-1])
+        d.rd_vals_total = int(self.rd_val_off[-1]); d.rd_r2v_total = int(self.rd_r2v_off[-1])
+        return d, keep
+
+    def visit(self, i: int):
+        """SafeCommandStore.mapReduceActive replay of txn i through the C ABI (accord_deps_visit):
+        [(is_range, key_or_start, range_end, txn_value)] in the visitor contract order."""
+        d, keep = self.to_c()
+        seen = []
+
+        def cb(ctx, is_range, a, b, v):
+            seen.append((is_range, a, b, v))
+            return 0
+        f = VISIT_FN(cb)
+        rc = lib().accord_deps_visit(C.byref(d), i, f, None)
+        if rc != ACCORD_OK:
+            _raise(rc, lib().accord_last_error(None).decode())
+        return seen
 
     def equals(self, other: "PartialDeps") -> bool:
         return all(np.array_equal(getattr(self, f), getattr(other, f)) for f in self.FIELDS)

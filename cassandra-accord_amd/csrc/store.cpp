@@ -113,6 +113,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
                       &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2};
     accord_impl::shard_comm_destroy(s);
+    accord_impl::pinned_arena_destroy(s);
     for (DevBuf *b : bufs) b->release();
     for (DepSet &d : s->ds) d.release();
     for (DevBuf &b : s->op_tmp) b.release();
@@ -614,66 +615,106 @@ int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
     return ACCORD_OK;
 }
 
-struct HostDepsOwner {
-    std::vector<uint32_t> kd_key_off, kd_keys, kd_val_off, kd_vals, kd_k2v_off;
-    std::vector<int32_t> kd_k2v;
-    std::vector<uint32_t> rd_rng_off, rd_rng_start, rd_rng_end, rd_val_off, rd_vals, rd_r2v_off;
-    std::vector<int32_t> rd_r2v;
+} // extern "C"
+
+namespace accord_impl {
+
+// Host memory of downloaded deps: one pinned block per result.  A store keeps its last block as a
+// reusable arena (page-locked allocation of ~1 GB costs far more than the copy); a result still
+// held when the next download starts gets a block of its own.
+struct PinnedBlock {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool leased = false;      // a result points into it
+    bool orphan = false;      // its store is gone: free it on release
 };
+
+void pinned_arena_destroy(accord_store *s)
+{
+    PinnedBlock *a = s->dl_arena;
+    s->dl_arena = nullptr;
+    if (!a) return;
+    if (a->leased) { a->orphan = true; return; }
+    if (a->p) (void)hipHostFree(a->p);
+    delete a;
+}
+
+} // namespace accord_impl
+
+namespace {
+
+struct HostDepsOwner {
+    accord_impl::PinnedBlock *block = nullptr;
+    bool arena = false;       // block is its store's arena (returned on release), else owned
+};
+
+} // namespace
+
+extern "C" {
 
 int32_t accord_deps_download(accord_store *s, accord_deps *out)
 {
+    using accord_impl::PinnedBlock;
     if (!s || !out) return fail(s, ACCORD_ERR_ARG, "null argument");
     if (!s->computed) return fail(s, ACCORD_ERR_STATE, "no computed deps");
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     accord_deps v;
     int32_t rc = accord_deps_device_view(s, &v);
     if (rc) return rc;
+    const size_t n1 = (size_t)v.n + 1;
+    // layout: 13 arrays, each 64-byte aligned
+    const size_t cnt[13] = {n1, v.kd_keys_total, n1, v.kd_vals_total, n1, v.kd_k2v_total,
+                            n1, v.rd_rngs_total, v.rd_rngs_total, n1, v.rd_vals_total, n1, v.rd_r2v_total};
+    const void *src[13] = {v.kd_key_off, v.kd_keys, v.kd_val_off, v.kd_vals, v.kd_k2v_off, v.kd_k2v,
+                           v.rd_rng_off, v.rd_rng_start, v.rd_rng_end, v.rd_val_off, v.rd_vals, v.rd_r2v_off, v.rd_r2v};
+    size_t off[13], total = 0;
+    for (int a = 0; a < 13; ++a) { off[a] = total; total += (cnt[a] * 4 + 63) & ~(size_t)63; }
+    total += 64;
     HostDepsOwner *o = new (std::nothrow) HostDepsOwner();
     if (!o) return fail(s, ACCORD_ERR_OOM, "out of host memory");
-    const size_t n1 = (size_t)v.n + 1;
-    try {
-        o->kd_key_off.resize(n1); o->kd_val_off.resize(n1); o->kd_k2v_off.resize(n1);
-        o->kd_keys.resize(v.kd_keys_total + 1); o->kd_vals.resize(v.kd_vals_total + 1); o->kd_k2v.resize(v.kd_k2v_total + 1);
-        o->rd_rng_off.resize(n1); o->rd_val_off.resize(n1); o->rd_r2v_off.resize(n1);
-        o->rd_rng_start.resize(v.rd_rngs_total + 1); o->rd_rng_end.resize(v.rd_rngs_total + 1);
-        o->rd_vals.resize(v.rd_vals_total + 1); o->rd_r2v.resize(v.rd_r2v_total + 1);
-    } catch (...) {
-        delete o;
-        return fail(s, ACCORD_ERR_OOM, "out of host memory");
+    PinnedBlock *blk = s->dl_arena;
+    if (blk && !blk->leased && blk->cap < total) {       // grow the arena (page-locked, no zero fill)
+        (void)hipHostFree(blk->p);
+        blk->p = nullptr; blk->cap = 0;
     }
-    auto cp = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
-        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s->stream) : hipSuccess;
-    };
+    if (!blk || blk->leased) {
+        blk = new (std::nothrow) PinnedBlock();
+        if (!blk) { delete o; return fail(s, ACCORD_ERR_OOM, "out of host memory"); }
+        if (!s->dl_arena) s->dl_arena = blk; else o->arena = false;
+    }
+    o->arena = blk == s->dl_arena;
+    if (!blk->p) {
+        const size_t want = total + total / 8;           // headroom for the next, slightly larger batch
+        if (hipHostMalloc(&blk->p, want, hipHostMallocDefault) != hipSuccess) {
+            blk->p = nullptr;
+            if (!o->arena) delete blk;
+            delete o;
+            return fail(s, ACCORD_ERR_OOM, "page-locked host allocation of %zu bytes failed", want);
+        }
+        blk->cap = want;
+    }
+    char *base = (char *)blk->p;
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = cp(o->kd_key_off.data(), v.kd_key_off, n1 * 4);
-    if (e == hipSuccess) e = cp(o->kd_val_off.data(), v.kd_val_off, n1 * 4);
-    if (e == hipSuccess) e = cp(o->kd_k2v_off.data(), v.kd_k2v_off, n1 * 4);
-    if (e == hipSuccess) e = cp(o->kd_keys.data(), v.kd_keys, v.kd_keys_total * 4);
-    if (e == hipSuccess) e = cp(o->kd_vals.data(), v.kd_vals, v.kd_vals_total * 4);
-    if (e == hipSuccess) e = cp(o->kd_k2v.data(), v.kd_k2v, v.kd_k2v_total * 4);
-    if (e == hipSuccess) e = cp(o->rd_rng_off.data(), v.rd_rng_off, n1 * 4);
-    if (e == hipSuccess) e = cp(o->rd_val_off.data(), v.rd_val_off, n1 * 4);
-    if (e == hipSuccess) e = cp(o->rd_r2v_off.data(), v.rd_r2v_off, n1 * 4);
-    if (e == hipSuccess) e = cp(o->rd_rng_start.data(), v.rd_rng_start, v.rd_rngs_total * 4);
-    if (e == hipSuccess) e = cp(o->rd_rng_end.data(), v.rd_rng_end, v.rd_rngs_total * 4);
-    if (e == hipSuccess) e = cp(o->rd_vals.data(), v.rd_vals, v.rd_vals_total * 4);
-    if (e == hipSuccess) e = cp(o->rd_r2v.data(), v.rd_r2v, v.rd_r2v_total * 4);
+    for (int a = 0; a < 13 && e == hipSuccess; ++a)
+        if (cnt[a]) e = hipMemcpyAsync(base + off[a], src[a], cnt[a] * 4, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
+        if (!o->arena) { (void)hipHostFree(blk->p); delete blk; }
         delete o;
         return fail(s, ACCORD_ERR_HIP, "download: %s", hipGetErrorString(e));
     }
+    blk->leased = true;
+    o->block = blk;
     std::memset(out, 0, sizeof(*out));
     out->n = v.n;
     out->kd_keys_total = v.kd_keys_total; out->kd_vals_total = v.kd_vals_total; out->kd_k2v_total = v.kd_k2v_total;
     out->rd_rngs_total = v.rd_rngs_total; out->rd_vals_total = v.rd_vals_total; out->rd_r2v_total = v.rd_r2v_total;
-    out->kd_key_off = o->kd_key_off.data(); out->kd_keys = o->kd_keys.data();
-    out->kd_val_off = o->kd_val_off.data(); out->kd_vals = o->kd_vals.data();
-    out->kd_k2v_off = o->kd_k2v_off.data(); out->kd_k2v = o->kd_k2v.data();
-    out->rd_rng_off = o->rd_rng_off.data(); out->rd_rng_start = o->rd_rng_start.data();
-    out->rd_rng_end = o->rd_rng_end.data(); out->rd_val_off = o->rd_val_off.data();
-    out->rd_vals = o->rd_vals.data(); out->rd_r2v_off = o->rd_r2v_off.data(); out->rd_r2v = o->rd_r2v.data();
+    uint32_t *ptr[13];
+    for (int a = 0; a < 13; ++a) ptr[a] = (uint32_t *)(base + off[a]);
+    out->kd_key_off = ptr[0]; out->kd_keys = ptr[1]; out->kd_val_off = ptr[2]; out->kd_vals = ptr[3];
+    out->kd_k2v_off = ptr[4]; out->kd_k2v = (int32_t *)ptr[5];
+    out->rd_rng_off = ptr[6]; out->rd_rng_start = ptr[7]; out->rd_rng_end = ptr[8]; out->rd_val_off = ptr[9];
+    out->rd_vals = ptr[10]; out->rd_r2v_off = ptr[11]; out->rd_r2v = (int32_t *)ptr[12];
     out->owner = o;
     return ACCORD_OK;
 }
@@ -681,8 +722,49 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
 void accord_deps_release(accord_deps *d)
 {
     if (!d) return;
-    delete (HostDepsOwner *)d->owner;
+    HostDepsOwner *o = (HostDepsOwner *)d->owner;
+    if (o) {
+        accord_impl::PinnedBlock *blk = o->block;
+        if (blk) {
+            blk->leased = false;
+            if (!o->arena || blk->orphan) {
+                if (blk->p) (void)hipHostFree(blk->p);
+                delete blk;
+            }
+        }
+        delete o;
+    }
     std::memset(d, 0, sizeof(*d));
+}
+
+int32_t accord_deps_visit(const accord_deps *d, uint32_t txn, accord_visit_fn fn, void *ctx)
+{
+    if (!d || !fn) return fail(nullptr, ACCORD_ERR_ARG, "accord_deps_visit: null argument");
+    if (txn >= d->n) return fail(nullptr, ACCORD_ERR_ARG, "accord_deps_visit: txn %u of %u", txn, d->n);
+    // keys ascending, each key's txnIds ascending (KeyDeps: header = end offsets from keyCount)
+    const uint32_t k0 = d->kd_key_off[txn], nk = d->kd_key_off[txn + 1] - k0;
+    const uint32_t *vals = d->kd_vals + d->kd_val_off[txn];
+    const int32_t *x = d->kd_k2v + d->kd_k2v_off[txn];
+    for (uint32_t k = 0; k < nk; ++k) {
+        const uint32_t from = k == 0 ? nk : (uint32_t)x[k - 1], to = (uint32_t)x[k];
+        for (uint32_t b = from; b < to; ++b) {
+            const int32_t rc = fn(ctx, 0u, d->kd_keys[k0 + k], 0u, vals[x[b]]);
+            if (rc) return rc;
+        }
+    }
+    // then ranges in Range.compare order, each range's txnIds ascending
+    if (!d->rd_rng_off) return ACCORD_OK;
+    const uint32_t r0 = d->rd_rng_off[txn], nr = d->rd_rng_off[txn + 1] - r0;
+    const uint32_t *rvals = d->rd_vals + d->rd_val_off[txn];
+    const int32_t *y = d->rd_r2v + d->rd_r2v_off[txn];
+    for (uint32_t r = 0; r < nr; ++r) {
+        const uint32_t from = r == 0 ? nr : (uint32_t)y[r - 1], to = (uint32_t)y[r];
+        for (uint32_t b = from; b < to; ++b) {
+            const int32_t rc = fn(ctx, 1u, d->rd_rng_start[r0 + r], d->rd_rng_end[r0 + r], rvals[y[b]]);
+            if (rc) return rc;
+        }
+    }
+    return ACCORD_OK;
 }
 
 int32_t accord_deps_batch(accord_store *s, const accord_batch *b, accord_deps *out)

@@ -67,6 +67,7 @@ enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_F
              EV_OP_START, EV_OP_END, EV_COUNT_ALL };
 
 struct ShardComm;   // RCCL communicator + exchange buffers (shard.cpp)
+namespace accord_impl { struct PinnedBlock; void pinned_arena_destroy(accord_store *s); }
 
 struct accord_store {
     accord_store_cfg cfg{};
@@ -137,6 +138,7 @@ struct accord_store {
     float ops_ms = 0;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
+    accord_impl::PinnedBlock *dl_arena = nullptr;   // page-locked host arena of accord_deps_download
     hipEvent_t ev[EV_COUNT_ALL] = {};
     bool events = false;
     accord_timing timing{};

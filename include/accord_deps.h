@@ -179,6 +179,17 @@ int32_t accord_store_reset(accord_store *store);               /* back to an emp
 int32_t accord_deps_batch(accord_store *store, const accord_batch *batch, accord_deps *out);
 void    accord_deps_release(accord_deps *deps);
 
+/* SafeCommandStore.mapReduceActive for ONE txn of a host deps set (accord_deps_download /
+ * accord_deps_batch output): replays the visitor in the contract order of
+ * local/SafeCommandStore.java:269-273 -- keys first, then ranges, both ascending; within each, the
+ * txnIds ascending -- as fn(ctx, is_range, key or range start, range end, txn value).  The
+ * reference's CommandFunction.apply(p1, keyOrRange, txnId, executeAt, in) (:58-61) feeding
+ * Deps.AbstractBuilder.add rebuilds exactly this txn's PartialDeps.  A nonzero return from fn stops
+ * the visit and is returned.  Host-only (no device work). */
+typedef int32_t (*accord_visit_fn)(void *ctx, uint32_t is_range, uint32_t key_or_start, uint32_t range_end,
+                                   uint32_t txn_value);
+int32_t accord_deps_visit(const accord_deps *deps, uint32_t txn, accord_visit_fn fn, void *ctx);
+
 /* ---- device-resident pipeline (inputs already in HBM; used by the bench) ---- */
 int32_t accord_batch_upload(accord_store *store, const accord_batch *host_batch);  /* H2D, sync */
 int32_t accord_deps_compute(accord_store *store);          /* enqueue + run the whole pipeline */

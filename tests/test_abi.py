@@ -124,3 +124,40 @@ def test_txn_id_string_format():
     lsb = (1_000_000 << 16) | (1 << 1)
     assert A.txn_id_str(msb, lsb, 3) == "[1,1000000,2(KW),3]"
     assert A.txn_id_str(msb, (5 << 16) | 1, 1) == "[1,5,1(RR),1]"
+
+
+def test_deps_visit_replays_mapreduceactive_order():
+    """accord_deps_visit (host-only) over oracle deps: keys ascending then ranges ascending, txnIds
+    ascending within each (local/SafeCommandStore.java:269-273); feeding the visits to
+    KeyDeps/RangeDeps builders (the oracle's RelationMultiMap builder) rebuilds the same deps."""
+    import oracle_lib as O
+    s = A.generate_stream(3000, 4, 500, 0.99, 0.5, range_frac=0.2, range_len_max=40, seed=11)
+    d = O.deps_fast(s, 64)
+    for i in (0, 5, 777, 1500, 2999):
+        seen = d.visit(i)
+        keys = [(a, v) for r, a, b, v in seen if r == 0]
+        rngs = [((a, b), v) for r, a, b, v in seen if r == 1]
+        assert all(r == 0 for r, *_ in seen[:len(keys)])                  # keys first
+        assert [k for k, _ in keys] == sorted(k for k, _ in keys)         # ascending keys
+        assert [r for r, _ in rngs] == sorted(r for r, _ in rngs)         # ascending ranges
+        rebuilt = O.keydeps_build([k for k, _ in keys], [v for _, v in keys], s.msb, s.lsb, s.node)
+        kk, vv, xx = d.key_deps(i)
+        if len(keys):
+            assert np.array_equal(rebuilt[0], kk) and np.array_equal(rebuilt[1], vv) and np.array_equal(rebuilt[2], xx)
+        else:
+            assert len(kk) == 0
+        rs, re_, rv, rx = d.range_deps(i)
+        want = [((int(rs[r]), int(re_[r])), int(rv[rx[b]])) for r in range(len(rs))
+                for b in range(len(rs) if r == 0 else rx[r - 1], rx[r])]
+        assert rngs == want
+
+
+def test_deps_visit_stops_on_nonzero():
+    import oracle_lib as O
+    s = A.generate_stream(500, 4, 50, 0.0, 0.5, seed=12)
+    d = O.deps_fast(s, 64)
+    i = int(np.argmax(np.diff(d.kd_val_off)))
+    dd, keep = d.to_c()
+    calls = []
+    f = A.VISIT_FN(lambda ctx, r, a, b, v: (calls.append(v), 7)[1])
+    assert A.lib().accord_deps_visit(C.byref(dd), i, f, None) == 7 and len(calls) == 1
