@@ -31,7 +31,7 @@ __all__ = [
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG_ROOT = os.path.dirname(_HERE)
-lib_path = os.path.join(_PKG_ROOT, "libaccord_deps.so")
+lib_path = os.environ.get("ACCORD_LIB") or os.path.join(_PKG_ROOT, "libaccord_deps.so")   # ACCORD_LIB: measurement builds
 
 ACCORD_OK = 0
 ERR = {

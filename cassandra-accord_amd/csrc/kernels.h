@@ -61,6 +61,7 @@ struct alignas(16) PairSlice {
 
 struct KeyDepsParams {
     uint32_t n;
+    uint32_t P;                        // (txn, key) pairs of the batch (key_off[n])
     const uint64_t *msb, *lsb;
     const int32_t *node;
     const uint32_t *key_off, *key_ord;

@@ -21,6 +21,8 @@
 // recomputes and writes.
 #include "device_common.h"
 #include "kernels.h"
+
+#include <cstdlib>
 #include "../../include/accord_deps.h"
 
 namespace accord {
@@ -405,6 +407,115 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
         if (p < end && q[j] != 0xFFFFFFFFu) slice[q[j]] = PairSlice{l[j], hi[j], cnt[j], 0u};
+    }
+}
+
+// The same for windows W <= H2_HALO, with the window bound found by a fixed-step binary search run
+// in lockstep over the thread's items (every step issues all items' LDS reads before any is
+// consumed).  Each txn holds a key at most once, so the entries of the pair's key with txn >= i - W
+// number at most W + 1 and the bound lies in [p - W, p]: the predicate "same key and txn >= i - W"
+// is monotone over that range of the key-major history, and the search needs neither the segment
+// start nor a global fallback.
+__global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
+    uint32_t P, uint32_t window, uint32_t steps, const uint32_t *__restrict__ sorted_key,
+    const uint32_t *__restrict__ sorted_pair, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ seg_start,
+    const uint32_t *__restrict__ pw_local, const uint32_t *__restrict__ carry, const uint64_t *__restrict__ c_local,
+    const ClassCarry *__restrict__ ccarry, const uint32_t *__restrict__ seg_end, const uint32_t *__restrict__ pair_bound,
+    PairSlice *__restrict__ slice, uint32_t ncarry)
+{
+    __shared__ uint32_t tx[H2_HALO + H2_TILE];
+    __shared__ uint32_t tk[H2_HALO + H2_TILE];
+    const uint32_t base = blockIdx.x * H2_TILE;
+    const uint32_t lds_lo = base > H2_HALO ? base - H2_HALO : 0u;
+    const uint32_t end = min(P, base + H2_TILE);
+    uint32_t key[H2_ITEMS], q[H2_ITEMS], a[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        key[j] = p < end ? sorted_key[p] : 0u;
+        const uint32_t v = p < end ? sorted_pair[p] : 0u;
+        q[j] = v >= ncarry ? v - ncarry : 0xFFFFFFFFu;       // carried entries get no slice
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) a[j] = seg_start[key[j]];   // issued early, used late
+    for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) {
+        tx[x - lds_lo] = hist[x];
+        tk[x - lds_lo] = sorted_key[x];
+    }
+    __syncthreads();
+    uint32_t ent[H2_ITEMS], lo[H2_ITEMS], len[H2_ITEMS], thr[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        ent[j] = p < end ? tx[p - lds_lo] : 0u;
+        const uint32_t i = ent[j] & ENT_TXN_MASK;
+        thr[j] = i > window ? i - window : 0u;
+        const uint32_t lb = p > window ? max(p - window, lds_lo) : lds_lo;
+        lo[j] = lb;
+        len[j] = p < end ? p - lb : 0u;               // search [lb, p): p itself always qualifies
+    }
+    for (uint32_t st = 0; st < steps; ++st) {
+        uint32_t probe[H2_ITEMS];
+#pragma unroll
+        for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+            const uint32_t half = len[j] >> 1;
+            const uint32_t m = lo[j] + half;
+            probe[j] = len[j] ? (tk[m - lds_lo] == key[j] && (tx[m - lds_lo] & ENT_TXN_MASK) >= thr[j] ? 1u : 0u) : 1u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+            const uint32_t half = len[j] >> 1;
+            if (!probe[j]) { lo[j] += half + 1; len[j] -= half + 1; }
+            else len[j] = half;
+        }
+    }
+    // lo = the window bound l; then the last Write before l inside the segment, else the segment start
+    uint32_t pw[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        if (thr[j] == 0) lo[j] = a[j];                // txn <= W: nothing has left the window
+        pw[j] = 0;
+        if (lo[j] > a[j]) {
+            const uint32_t x = lo[j] - 1;
+            pw[j] = max(pw_local[x], carry[x / HS_TILE]);   // (last Write <= x) + 1
+        }
+    }
+    uint32_t hi[H2_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        hi[j] = p;
+        if (pair_bound && p < end && q[j] != 0xFFFFFFFFu) {
+            const uint32_t b = pair_bound[q[j]], c = seg_end[key[j]];
+            uint32_t x = p + 1, step = 1;
+            while (x < c && (hist[x] & ENT_TXN_MASK) < b) {   // gallop, then bisect
+                const uint32_t probe = x + step;
+                if (probe >= c || (hist[probe] & ENT_TXN_MASK) >= b) {
+                    uint32_t l2 = x + 1, h2 = min(probe, c);
+                    while (l2 < h2) {
+                        const uint32_t m = (l2 + h2) >> 1;
+                        if ((hist[m] & ENT_TXN_MASK) < b) l2 = m + 1; else h2 = m;
+                    }
+                    x = l2;
+                    break;
+                }
+                x = probe + 1;
+                step <<= 1;
+            }
+            hi[j] = (b > (ent[j] & ENT_TXN_MASK)) ? x : p;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+        const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+        const uint32_t l = pw[j] > a[j] ? pw[j] - 1 : a[j];
+        uint32_t cnt = 0;
+        if (p < end && hi[j] > l) {
+            const uint32_t kind = ent[j] >> ENT_KIND_SHIFT, wmask = witness_mask(kind);
+            cnt = witnessed_upto(c_local, ccarry, hi[j] - 1, wmask) - (l ? witnessed_upto(c_local, ccarry, l - 1, wmask) : 0u);
+            if (hi[j] > p) cnt -= (wmask >> kind) & 1u;   // p1: the txn itself
+        }
+        if (p < end && q[j] != 0xFFFFFFFFu) slice[q[j]] = PairSlice{l, hi[j], cnt, 0u};
     }
 }
 
@@ -852,16 +963,29 @@ __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn
     return rt;
 }
 
+struct alignas(16) BmWord {
+    unsigned long long bits;          // 64 bits of the near bitmap
+    uint32_t pre;                     // distinct deps before this word (far deps included)
+    uint32_t pad;
+};
+
+// OR the near bits of one candidate batch into the bitmap (LDS atomics; measured: combining equal
+// words across lanes first costs more VALU than the same-address atomics it saves -- the kernel is
+// VALU-issue bound)
+__device__ __forceinline__ void near_bits_or(BmWord *bw, bool nr, uint32_t bit, uint32_t)
+{
+    if (nr) atomicOr(&bw[bit >> 6].bits, 1ull << (bit & 63));
+}
+
 template <int WPL>
 __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void keydeps_fast_kernel(
     KeyDepsParams p, const TxnRec *__restrict__ recs)
 {
-    __shared__ unsigned long long bm_all[KD_WAVES][64 * WPL];
-    __shared__ uint32_t wp_all[KD_WAVES][64 * WPL];
+    __shared__ BmWord bw_all[KD_WAVES][64 * WPL];   // near bitmap words + rank prefix (one b128 read)
     __shared__ uint32_t fr_all[KD_WAVES][64];       // far deps: value, then its rank
     const uint32_t w = wave_id(), lane = lane_id();
-    unsigned long long *bm = bm_all[w];
-    uint32_t *wp = wp_all[w], *fr = fr_all[w];
+    BmWord *bw = bw_all[w];
+    uint32_t *fr = fr_all[w];
     const uint64_t lt = lanemask_lt();
     constexpr uint32_t SPAN = 64u * 64u * WPL;
     const uint32_t S = gridDim.x * KD_WAVES, n = p.n;
@@ -898,7 +1022,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             uint32_t fidx[FK_CB];
             if (!fallback) {
 #pragma unroll
-                for (int q = 0; q < WPL; ++q) bm[lane * WPL + q] = 0ull;
+                for (int q = 0; q < WPL; ++q) bw[lane * WPL + q].bits = 0ull;
                 wave_lds_sync();
 #pragma unroll
                 for (int cc = 0; cc < FK_CB; ++cc) {
@@ -909,7 +1033,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                     const bool wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;   // p1
                     const uint32_t bit = j + nb;
                     const bool nr = wit && bit < SPAN;
-                    if (nr) atomicOr(&bm[bit >> 6], 1ull << (bit & 63));
+                    near_bits_or(bw, nr, bit, lane);
                     const uint64_t fb = __ballot(wit && !nr);
                     if (fb) {                             // wave-uniform
                         const uint32_t f = F + (uint32_t)__popcll(fb & lt);
@@ -948,12 +1072,12 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             // union: popcounts -> per-word rank prefix (after the far deps); |txnIds|
             uint32_t pc[WPL], mysum = 0;
 #pragma unroll
-            for (int q = 0; q < WPL; ++q) { pc[q] = (uint32_t)__popcll(bm[lane * WPL + q]); mysum += pc[q]; }
+            for (int q = 0; q < WPL; ++q) { pc[q] = (uint32_t)__popcll(bw[lane * WPL + q].bits); mysum += pc[q]; }
             const uint32_t incl = wave_incl_scan(mysum);
             {
                 uint32_t ex = incl - mysum + far_u;
 #pragma unroll
-                for (int q = 0; q < WPL; ++q) { wp[lane * WPL + q] = ex; ex += pc[q]; }
+                for (int q = 0; q < WPL; ++q) { bw[lane * WPL + q].pre = ex; ex += pc[q]; }
             }
             if (lane == 0) stg(p.cnt_vals, t, readlane(incl, 63) + far_u);
             // keys and keysToTxnIds header from the witnessed counts
@@ -978,7 +1102,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 const bool wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;   // p1
                 const bool nr = wit && j + nb < SPAN;
                 const uint32_t bit = nr ? j + nb : 0u;
-                uint32_t rank = wp[bit >> 6] + (uint32_t)__popcll(bm[bit >> 6] & ((1ull << (bit & 63)) - 1ull));
+                const BmWord bwd = bw[bit >> 6];
+                uint32_t rank = bwd.pre + (uint32_t)__popcll(bwd.bits & ((1ull << (bit & 63)) - 1ull));
                 if (F && wit && !nr) rank = fr[fidx[cc]];
                 const uint64_t wb = __ballot(wit);
                 if (wit) {
@@ -1177,6 +1302,14 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
     ClassCarry *ccarry = (ClassCarry *)((char *)temp + off);
     hipLaunchKernelGGL(history1_kernel, dim3(tiles), dim3(HS_THREADS), 0, s, P, sorted_key, hist, seg_start, seg_end, pw_local, tile_max, c_local, tile_cnt);
     hipLaunchKernelGGL(history_carry_kernel, dim3(1), dim3(256), 0, s, tile_max, tile_cnt, ccarry, tiles);
+    if (window <= H2_HALO) {
+        uint32_t steps = 0;
+        while ((1u << steps) <= window) ++steps;     // ceil(log2(window + 1)) halvings of a <= window range
+        hipLaunchKernelGGL(history2_lockstep_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P,
+                           window, steps, sorted_key, sorted_pair, hist, seg_start, pw_local, tile_max, c_local, ccarry,
+                           seg_end, pair_bound, slice, carry);
+        return;
+    }
     hipLaunchKernelGGL(history2_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P, window,
                        sorted_key, sorted_pair, hist,
                        seg_start, pw_local, tile_max, c_local, ccarry, seg_end, pair_bound, slice, carry);

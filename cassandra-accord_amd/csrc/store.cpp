@@ -353,7 +353,7 @@ int32_t accord_deps_compute(accord_store *s)
     record(s, EV_SEGMENT);
 
     accord::KeyDepsParams kp{};
-    kp.n = n;
+    kp.n = n; kp.P = P;
     kp.msb = s->msb.as<uint64_t>(); kp.lsb = s->lsb.as<uint64_t>(); kp.node = s->node.as<int32_t>();
     kp.key_off = s->key_off.as<uint32_t>(); kp.key_ord = s->key_ord.as<uint32_t>();
     kp.txn_index = s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr;
