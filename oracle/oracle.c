@@ -1105,6 +1105,169 @@ int or_waiting_on_events(const or_deps *d, uint32_t n, uint32_t *round_out)
     return done == n ? 0 : -7;   /* -7: a txn never became ready (cycle / missing dep) */
 }
 
+/* Execution readiness restated from the CommandsForKey side, independent of
+ * the deps values of managed txns: each key keeps a CFK of the managed txns on it (key domain and
+ * Kind.isGloballyVisible, SafeCommandStore.java:219-233), all STABLE with executeAt = txnId.
+ *  - managed txn t clears its key-k WaitingOn bit when CommandsForKey.notify (:1512-1635) finds
+ *    expectMissingCount == |missing| at t: the unapplied committed txns before t in executeAt order,
+ *    counted per kind (Write: reads + writes; Read: writes; SyncPoints: all three), against its
+ *    missing[] -- empty here, because every txn is registered STABLE in TxnId order and update()
+ *    elides committed txns from missing (:1103-1109).  notify runs over [next, nextWrite] of the key
+ *    (:1199-1203) whenever a txn on it applies, and once at registration (:1176-1186);
+ *  - unmanaged txns (range domain, EphemeralRead) go through registerUnmanaged (:1406-1498): key k
+ *    is pending until every committed txn on k executing at or before waitingUntil (the max
+ *    executeAt of its deps on k) has applied, released by notifyUnmanaged(APPLY, next.executeAt)
+ *    (:1211-1212);
+ *  - a range-dep bit clears when that dep applies (Commands.updateWaitingOn, Commands.java:755-830).
+ * Synchronous rounds as or_waiting_on_events.  0 ok, -7 stuck, -8 deps name a txn the CFK lacks. */
+int or_levels_cfk(const or_stream *s, const or_deps *d, uint32_t *round_out)
+{
+    const uint32_t n = s->n;
+    int rc = 0;
+    uint32_t nkeys = 0;
+    for (uint32_t x = 0; x < s->key_off[n]; ++x) if (s->key_ord[x] + 1 > nkeys) nkeys = s->key_ord[x] + 1;
+    for (uint32_t x = 0; x < d->kd_key_off[n]; ++x) if (d->kd_keys[x] + 1 > nkeys) nkeys = d->kd_keys[x] + 1;
+    uint8_t *managed = (uint8_t *)calloc(n ? n : 1, 1), *applied = (uint8_t *)calloc(n ? n : 1, 1);
+    uint8_t *dirty = (uint8_t *)calloc(nkeys ? nkeys : 1, 1);
+    uint32_t *cfk_off = (uint32_t *)calloc((size_t)nkeys + 1, sizeof(uint32_t));
+    uint32_t *nextp = (uint32_t *)calloc(nkeys ? nkeys : 1, sizeof(uint32_t));
+    uint32_t *dlist = (uint32_t *)calloc(nkeys ? nkeys : 1, sizeof(uint32_t));
+    uint32_t *pend_off = (uint32_t *)calloc((size_t)nkeys + 1, sizeof(uint32_t));
+    uint32_t *bits_left = (uint32_t *)calloc(n ? n : 1, sizeof(uint32_t));
+    uint32_t *radj_off = (uint32_t *)calloc((size_t)n + 1, sizeof(uint32_t));
+    uint32_t *frontier = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    uint32_t nslot = d->kd_key_off[n];
+    uint8_t *slot_clear = (uint8_t *)calloc(nslot ? nslot : 1, 1);
+    uint32_t *cfk = NULL, *fill = NULL, *pend_slot = NULL, *pend_txn = NULL, *pend_until = NULL, *pend_head = NULL,
+             *rw = NULL;
+    if (!managed || !applied || !dirty || !cfk_off || !nextp || !dlist || !pend_off || !bits_left || !radj_off || !frontier ||
+        !slot_clear) { rc = -1; goto out; }
+    for (uint32_t i = 0; i < n; ++i) {
+        managed[i] = domain_of(s->lsb[i]) == 0 && is_globally_visible(kind_of(s->lsb[i])) == 1;
+        if (managed[i])
+            for (uint32_t x = s->key_off[i]; x < s->key_off[i + 1]; ++x) cfk_off[s->key_ord[x] + 1]++;
+        else
+            for (uint32_t x = d->kd_key_off[i]; x < d->kd_key_off[i + 1]; ++x) pend_off[d->kd_keys[x] + 1]++;
+        for (uint32_t v = d->rd_val_off[i]; v < d->rd_val_off[i + 1]; ++v) radj_off[d->rd_vals[v] + 1]++;
+        bits_left[i] = (d->kd_key_off[i + 1] - d->kd_key_off[i]) + (d->rd_val_off[i + 1] - d->rd_val_off[i]);
+    }
+    for (uint32_t k = 0; k < nkeys; ++k) { cfk_off[k + 1] += cfk_off[k]; pend_off[k + 1] += pend_off[k]; }
+    for (uint32_t j = 0; j < n; ++j) radj_off[j + 1] += radj_off[j];
+    cfk = (uint32_t *)malloc(((size_t)cfk_off[nkeys] + 1) * sizeof(uint32_t));
+    fill = (uint32_t *)malloc(((size_t)(nkeys > n ? nkeys : n) + 1) * sizeof(uint32_t));
+    pend_slot = (uint32_t *)malloc(((size_t)pend_off[nkeys] + 1) * sizeof(uint32_t));
+    pend_until = (uint32_t *)malloc(((size_t)pend_off[nkeys] + 1) * sizeof(uint32_t));
+    pend_txn = (uint32_t *)malloc(((size_t)pend_off[nkeys] + 1) * sizeof(uint32_t));
+    pend_head = (uint32_t *)calloc(nkeys ? nkeys : 1, sizeof(uint32_t));
+    rw = (uint32_t *)malloc(((size_t)radj_off[n] + 1) * sizeof(uint32_t));
+    if (!cfk || !fill || !pend_slot || !pend_txn || !pend_until || !pend_head || !rw) { rc = -1; goto out; }
+    /* CFK txns[] per key in TxnId (= executeAt) order */
+    memcpy(fill, cfk_off, (size_t)nkeys * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n; ++i)
+        if (managed[i])
+            for (uint32_t x = s->key_off[i]; x < s->key_off[i + 1]; ++x) cfk[fill[s->key_ord[x]]++] = i;
+    /* registerUnmanaged: one pending APPLY record per (txn, key of its keyDeps), waitingUntil = the
+     * max executeAt of its deps on the key (all committed, all before it: :1427-1449) */
+    memcpy(fill, pend_off, (size_t)nkeys * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (managed[i]) continue;
+        const int32_t *k2v = d->kd_k2v + d->kd_k2v_off[i];
+        uint32_t kc = d->kd_key_off[i + 1] - d->kd_key_off[i];
+        for (uint32_t q = 0; q < kc; ++q) {
+            uint32_t b = q == 0 ? kc : (uint32_t)k2v[q - 1], e = (uint32_t)k2v[q], until = 0;
+            for (uint32_t x = b; x < e; ++x) {
+                uint32_t j = d->kd_vals[d->kd_val_off[i] + (uint32_t)k2v[x]];
+                if (j > until) until = j;
+            }
+            uint32_t k = d->kd_keys[d->kd_key_off[i] + q];
+            pend_slot[fill[k]] = d->kd_key_off[i] + q;
+            pend_txn[fill[k]] = i;
+            pend_until[fill[k]++] = until;
+        }
+    }
+    /* pending records of a key in waitingUntil order (released as a prefix) */
+    for (uint32_t k = 0; k < nkeys; ++k)
+        for (uint32_t a = pend_off[k] + 1; a < pend_off[k + 1]; ++a)
+            for (uint32_t b = a; b > pend_off[k] && pend_until[b - 1] > pend_until[b]; --b) {
+                uint32_t t = pend_until[b]; pend_until[b] = pend_until[b - 1]; pend_until[b - 1] = t;
+                t = pend_slot[b]; pend_slot[b] = pend_slot[b - 1]; pend_slot[b - 1] = t;
+                t = pend_txn[b]; pend_txn[b] = pend_txn[b - 1]; pend_txn[b - 1] = t;
+            }
+    memcpy(fill, radj_off, (size_t)n * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n; ++i)
+        for (uint32_t v = d->rd_val_off[i]; v < d->rd_val_off[i + 1]; ++v) rw[fill[d->rd_vals[v]]++] = i;
+    for (uint32_t k = 0; k < nkeys; ++k) { nextp[k] = cfk_off[k]; pend_head[k] = pend_off[k]; dirty[k] = 1; }
+
+    uint32_t done = 0, r = 0, nf = 0, ndirty = nkeys;
+    for (uint32_t k = 0; k < nkeys; ++k) dlist[k] = k;
+    for (;;) {
+        /* CFK side: notify + notifyUnmanaged on every key whose state changed */
+        for (uint32_t dk = 0; dk < ndirty; ++dk) {
+            const uint32_t k = dlist[dk];
+            dirty[k] = 0;
+            while (nextp[k] < cfk_off[k + 1] && applied[cfk[nextp[k]]]) nextp[k]++;
+            uint32_t ur = 0, uw = 0, usp = 0;
+            for (uint32_t p = nextp[k]; p < cfk_off[k + 1]; ++p) {
+                uint32_t t = cfk[p];
+                if (applied[t]) continue;
+                int kind = kind_of(s->lsb[t]);
+                uint32_t expect = kind == K_READ ? uw : kind == K_WRITE ? uw + ur : uw + ur + usp;
+                if (expect == 0) {           /* |missing| == 0: removeWaitingOn(t, key) */
+                    const uint32_t *ks = d->kd_keys + d->kd_key_off[t];
+                    uint32_t lo = 0, hi = d->kd_key_off[t + 1] - d->kd_key_off[t];
+                    while (lo < hi) { uint32_t m = (lo + hi) / 2; if (ks[m] < k) lo = m + 1; else hi = m; }
+                    uint32_t slot = d->kd_key_off[t] + lo;
+                    if (lo < d->kd_key_off[t + 1] - d->kd_key_off[t] && ks[lo] == k && !slot_clear[slot]) {
+                        slot_clear[slot] = 1;
+                        if (--bits_left[t] == 0) frontier[nf++] = t;
+                    }
+                }
+                if (kind == K_WRITE) { ++uw; break; }          /* notify stops at nextWrite */
+                if (kind == K_READ) ++ur; else ++usp;
+            }
+            uint32_t next = nextp[k] < cfk_off[k + 1] ? cfk[nextp[k]] : UINT32_MAX;
+            while (pend_head[k] < pend_off[k + 1] && pend_until[pend_head[k]] < next) {
+                uint32_t slot = pend_slot[pend_head[k]], t = pend_txn[pend_head[k]++];
+                if (!slot_clear[slot]) {
+                    slot_clear[slot] = 1;
+                    if (--bits_left[t] == 0) frontier[nf++] = t;
+                }
+            }
+        }
+        ndirty = 0;
+        if (r == 0)
+            for (uint32_t i = 0; i < n; ++i)
+                if (d->kd_key_off[i + 1] == d->kd_key_off[i] && d->rd_val_off[i + 1] == d->rd_val_off[i]) frontier[nf++] = i;
+        if (!nf) break;
+        /* execute + apply this round's frontier */
+        uint32_t cur = nf;
+        for (uint32_t f = 0; f < cur; ++f) {
+            uint32_t j = frontier[f];
+            round_out[j] = r;
+            applied[j] = 1;
+            if (managed[j])
+                for (uint32_t x = s->key_off[j]; x < s->key_off[j + 1]; ++x)
+                    if (!dirty[s->key_ord[x]]) { dirty[s->key_ord[x]] = 1; dlist[ndirty++] = s->key_ord[x]; }
+        }
+        done += cur;
+        nf = 0;
+        /* range-dep bits (frontier is reused for the next round: copy out this round's first) */
+        memcpy(fill, frontier, (size_t)cur * sizeof(uint32_t));
+        for (uint32_t f = 0; f < cur; ++f) {
+            uint32_t j = fill[f];
+            for (uint32_t x = radj_off[j]; x < radj_off[j + 1]; ++x)
+                if (--bits_left[rw[x]] == 0) frontier[nf++] = rw[x];
+        }
+        ++r;
+    }
+    rc = done == n ? 0 : -7;
+out:
+    free(managed); free(applied); free(dirty); free(cfk_off); free(nextp); free(dlist); free(pend_off); free(bits_left);
+    free(radj_off); free(frontier); free(slot_clear); free(cfk); free(fill); free(pend_slot); free(pend_txn);
+    free(pend_until); free(pend_head); free(rw);
+    return rc;
+}
+
 /* ==========================================================================================
  * Deps-set operations over every txn of an or_deps set.
  * Values are indices into one TxnId table sorted ascending (the stream the deps were computed

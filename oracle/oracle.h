@@ -128,6 +128,11 @@ int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level,
 /* Event-driven readiness simulation (bits cleared by applies, CFK notify per key); round[i] is the
  * synchronous round in which txn i executes.  Must equal or_waiting_on's level.  0 ok, -7 stuck. */
 int or_waiting_on_events(const or_deps *d, uint32_t n, uint32_t *round_out);
+/* The same rounds restated from the CommandsForKey side: per-key CFK notify with the missing[]
+ * counts for managed txns, registerUnmanaged/notifyUnmanaged for range and EphemeralRead txns, and
+ * range-dep bits cleared on apply.  Uses the stream's keys/kinds; deps only for the WaitingOn bits,
+ * the unmanaged waitingUntil bounds and range deps.  0 ok, -7 stuck. */
+int or_levels_cfk(const or_stream *s, const or_deps *d, uint32_t *round_out);
 
 /* ---- deps-set operations over every txn of a set; values index one
  * TxnId table sorted ascending (index order == Timestamp order) ---- */

@@ -65,6 +65,7 @@ def lib():
         L.or_stab_key.restype = C.c_uint32
         L.or_waiting_on.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p, _u32p, C.POINTER(_u64p)]
         L.or_waiting_on_events.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p]
+        L.or_levels_cfk.argtypes = [C.POINTER(_OrStream), C.POINTER(_OrDeps), _u32p]
         L.or_deps_union.argtypes = [C.c_uint32, C.POINTER(_OrDeps), C.POINTER(_OrDeps)]
         L.or_deps_slice.argtypes = [C.POINTER(_OrDeps), _u32p, _u32p, _u32p, C.c_uint32, C.POINTER(_OrDeps)]
         L.or_deps_invert.argtypes = [C.POINTER(_OrDeps), C.c_int, _u32p, C.POINTER(_i32p)]
@@ -259,6 +260,18 @@ def waiting_on_events(p: PartialDeps):
     if rc != 0:
         raise OracleError(rc)
     return rounds[:n].copy()
+
+
+def levels_cfk(s: Stream, p: PartialDeps):
+    """Readiness rounds restated from the CommandsForKey side (notify + missing[] counts,
+    registerUnmanaged / notifyUnmanaged, range-dep bits): or_levels_cfk."""
+    o, keep = _or_stream(s, 0)
+    d, keep2 = _c_deps(p)
+    rounds = np.zeros(max(1, s.n), dtype=np.uint32)
+    rc = lib().or_levels_cfk(C.byref(o), C.byref(d), rounds.ctypes.data_as(_u32p))
+    if rc != 0:
+        raise OracleError(rc)
+    return rounds[:s.n].copy()
 
 
 def deps_union(parts):

@@ -1,6 +1,6 @@
 """WaitingOn bitsets and execution levelling on the GPU vs the
-oracle (or_waiting_on, itself pinned against the event-driven readiness simulation in
-test_oracle_stream.py).  Bit-exact: levels and every bitset word."""
+oracle (or_waiting_on) and, for streams without SyncPoint kinds, the CommandsForKey-side readiness
+simulation or_levels_cfk (notify with missing[] counts, registerUnmanaged; test_oracle_stream.py).  Bit-exact: levels and every bitset word."""
 import numpy as np
 import pytest
 
@@ -23,7 +23,7 @@ CASES = [
 ]
 
 
-def _check(s, ks, W):
+def _check(s, ks, W, cfk=False):
     with CommandStore(device=0, key_lo=0, key_hi=ks, window=W) as st:
         st.upload(s)
         st.compute()
@@ -35,6 +35,9 @@ def _check(s, ks, W):
     bad = np.nonzero(wo.level != level)[0]
     assert bad.size == 0, (bad[:5], wo.level[bad[:5]], level[bad[:5]])
     assert wo.max_level == int(level.max(initial=0))
+    if cfk:
+        # readiness restated from CommandsForKey notify / registerUnmanaged (or_levels_cfk)
+        assert np.array_equal(wo.level, O.levels_cfk(s, d))
     return wo
 
 
@@ -44,7 +47,7 @@ def test_waiting_on_matches_oracle(gpu_device, case):
     s = generate_stream(n, k, ks, z, wf, seed=seed, range_frac=rf, range_len_max=rl)
     if kinds:
         s = with_random_kinds(s, seed)
-    wo = _check(s, ks, W)
+    wo = _check(s, ks, W, cfk=not kinds)
     if ks == 1:
         assert np.array_equal(wo.level, np.arange(n, dtype=np.uint32))
 
@@ -93,3 +96,4 @@ def test_config5_full_size(gpu_device):
     bad = np.nonzero(wo.level != level)[0]
     assert bad.size == 0, (bad[:5], wo.level[bad[:5]], level[bad[:5]])
     assert wo.max_level == int(level.max(initial=0))
+    assert np.array_equal(wo.level, O.levels_cfk(s, d))

@@ -149,8 +149,59 @@ def test_levels_equal_event_simulation(cfg):
     s = generate_stream(n, k, ks, z, wf, seed=seed, range_frac=rf, range_len_max=rl)
     if kinds:
         s = with_random_kinds(s, seed)
+    if kinds:
+        # SyncPoints witness SyncPoints but Writes do not, so a window-pruned SyncPoint before the
+        # last Write is not covered transitively: the "none applied" levelling input is only
+        # consistent with deps computed without pruning (status-at-time W >= n)
+        W = n
     d = O.deps_fast(s, W)
     level, _, _ = O.waiting_on(d)
     rounds = O.waiting_on_events(d)
     assert np.array_equal(level, rounds)
+    # independent of the deps-only loop: CommandsForKey.notify counts / registerUnmanaged
+    cfk = O.levels_cfk(s, d)
+    assert np.all(cfk >= level)
+    # unmanaged txns (range domain, EphemeralRead) are released by notifyUnmanaged(APPLY,
+    # next.executeAt) (CommandsForKey.java:1298-1314): every committed txn on the key up to the
+    # max dep must have applied, which also waits on SyncPoints the deps do not witness
+    assert np.array_equal(cfk, levels_unmanaged_prefix(s, d))
+    if not kinds:
+        assert np.array_equal(level, cfk)
     assert level.max() > 10
+
+
+def managed_mask(s):
+    lsb = s.lsb.astype(np.uint64)
+    kind = (lsb >> np.uint64(1)) & np.uint64(7)
+    return ((lsb & np.uint64(1)) == 0) & (kind != 2) & (kind != 5)
+
+
+def levels_unmanaged_prefix(s, d):
+    """level recurrence with the CFK release rule for unmanaged txns: level(i) = 1 + max over its
+    deps and, for each keyDeps key k of an unmanaged i, over every managed txn on k at or before
+    its max dep on k; 0 if there is nothing to wait for."""
+    managed = managed_mask(s)
+    on_key = {}
+    lv = np.zeros(s.n, dtype=np.int64)
+    for i in range(s.n):
+        best = -1
+        for v in d.kd_vals[d.kd_val_off[i]:d.kd_val_off[i + 1]]:
+            best = max(best, lv[v])
+        for v in d.rd_vals[d.rd_val_off[i]:d.rd_val_off[i + 1]]:
+            best = max(best, lv[v])
+        if not managed[i]:
+            kc = int(d.kd_key_off[i + 1] - d.kd_key_off[i])
+            k2v = d.kd_k2v[d.kd_k2v_off[i]:d.kd_k2v_off[i + 1]]
+            vals = d.kd_vals[d.kd_val_off[i]:d.kd_val_off[i + 1]]
+            for q in range(kc):
+                b = kc if q == 0 else int(k2v[q - 1])
+                wu = max(int(vals[int(x)]) for x in k2v[b:int(k2v[q])])
+                for j in on_key.get(int(d.kd_keys[d.kd_key_off[i] + q]), ()):
+                    if j > wu:
+                        break
+                    best = max(best, lv[j])
+        lv[i] = best + 1
+        if managed[i]:
+            for k in s.key_ord[s.key_off[i]:s.key_off[i + 1]]:
+                on_key.setdefault(int(k), []).append(i)
+    return lv.astype(np.uint32)
