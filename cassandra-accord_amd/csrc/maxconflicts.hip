@@ -64,33 +64,84 @@ __device__ __forceinline__ void record_error(accord::DevStatus *st, uint32_t i, 
     atomicMin(&st->first, v);
 }
 
-// txn-major over txns [first, last): validate (key domain, kind, keys sorted-unique inside the
-// store) and pack (key, txn, pair) for the sort; pair indices relative to key_off[first].
-// ExclusiveSyncPoint in the key domain is rejected: CommandStore.preaccept hands its keys to
-// markExclusiveSyncPoint as Ranges (local/CommandStore.java:335-339), so it has no key-domain
-// MaxConflicts reading.
+// Store keys a txn reads and writes: its keys (key domain) or the keys its ranges (s, e] cover,
+// clipped to the store [key_lo, key_hi) -- MaxConflicts is a ReducingRangeMap over routing keys and
+// an IntKey range has no points between keys, so a range is exactly the keys it covers
+// (local/MaxConflicts.java:46-80; keys sliced to the store, local/CommandStore.java:318).
+__device__ __forceinline__ uint32_t mc_range_keys(uint32_t rs, uint32_t re, uint32_t key_lo, uint32_t key_hi,
+                                                  uint32_t &a)
+{
+    const uint64_t lo = max((uint64_t)rs + 1, (uint64_t)key_lo), hi = min((uint64_t)re + 1, (uint64_t)key_hi);
+    a = (uint32_t)lo;
+    return hi > lo ? (uint32_t)(hi - lo) : 0u;
+}
+
+// Per-txn pair counts over [first, last) (cnt[last - first] = 0 so the exclusive scan ends with the total).
+__global__ void __launch_bounds__(256) mc_count_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ lsb,
+                                                       const uint32_t *__restrict__ key_off,
+                                                       const uint32_t *__restrict__ rng_off,
+                                                       const uint32_t *__restrict__ rng_start,
+                                                       const uint32_t *__restrict__ rng_end, uint32_t key_lo,
+                                                       uint32_t key_hi, uint32_t *__restrict__ cnt)
+{
+    const uint32_t t = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > last) return;
+    uint32_t c = 0;
+    if (t < last) {
+        if (lsb[t] & 1) {
+            for (uint32_t r = rng_off[t]; r < rng_off[t + 1]; ++r) {
+                uint32_t a;
+                c += mc_range_keys(rng_start[r], rng_end[r], key_lo, key_hi, a);
+            }
+        } else {
+            c = key_off[t + 1] - key_off[t];
+        }
+    }
+    cnt[t - first] = c;
+}
+
+// txn-major over txns [first, last): validate and pack (key, txn, pair) for the sort at the txn's
+// pair offset po[t - first].  Key txns: keys sorted-unique inside the store.  Range txns: ranges
+// non-empty, sorted, non-overlapping.  ExclusiveSyncPoint in the key domain is rejected:
+// CommandStore.preaccept hands its keys to markExclusiveSyncPoint as Ranges (:335-339).
 __global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ lsb,
                                                       const uint32_t *__restrict__ key_off,
-                                                      const uint32_t *__restrict__ key_ord, uint32_t key_lo,
-                                                      uint32_t key_hi, uint32_t *__restrict__ pk,
-                                                      uint32_t *__restrict__ pv, uint32_t *__restrict__ pe,
-                                                      accord::DevStatus *st)
+                                                      const uint32_t *__restrict__ key_ord,
+                                                      const uint32_t *__restrict__ rng_off,
+                                                      const uint32_t *__restrict__ rng_start,
+                                                      const uint32_t *__restrict__ rng_end, uint32_t key_lo,
+                                                      uint32_t key_hi, const uint32_t *__restrict__ po,
+                                                      uint32_t *__restrict__ pk, uint32_t *__restrict__ pv,
+                                                      uint32_t *__restrict__ pe, accord::DevStatus *st)
 {
     const uint32_t t = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= last) return;
     const uint64_t l = lsb[t];
     const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
-    if (domain != 0) record_error(st, t, ACCORD_ERR_DOMAIN);
-    if (kind >= 4) record_error(st, t, ACCORD_ERR_KIND);
-    const uint32_t pbase = key_off[first];
+    if (kind >= 5 || (domain == 0 && kind == 4)) record_error(st, t, ACCORD_ERR_KIND);
+    uint32_t o = po[t - first];
+    if (domain) {
+        for (uint32_t r = rng_off[t]; r < rng_off[t + 1]; ++r) {
+            const uint32_t rs = rng_start[r], re = rng_end[r];
+            if (rs >= re || (r > rng_off[t] && rs < rng_end[r - 1])) record_error(st, t, ACCORD_ERR_KEYS);
+            uint32_t a;
+            const uint32_t c = mc_range_keys(rs, re, key_lo, key_hi, a);
+            for (uint32_t j = 0; j < c; ++j, ++o) {
+                pk[o] = a + j - key_lo;
+                pv[o] = t;
+                pe[o] = o;
+            }
+        }
+        return;
+    }
     const uint32_t b = key_off[t], e = key_off[t + 1];
     uint32_t prev = 0;
-    for (uint32_t p = b; p < e; ++p) {
+    for (uint32_t p = b; p < e; ++p, ++o) {
         const uint32_t k = key_ord[p];
         if (k < key_lo || k >= key_hi || (p > b && k <= prev)) record_error(st, t, ACCORD_ERR_KEYS);
-        pk[p - pbase] = (k >= key_lo && k < key_hi) ? k - key_lo : 0;
-        pv[p - pbase] = t;
-        pe[p - pbase] = p - pbase;
+        pk[o] = (k >= key_lo && k < key_hi) ? k - key_lo : 0;
+        pv[o] = t;
+        pe[o] = o;
         prev = k;
     }
 }
@@ -207,10 +258,11 @@ __global__ void __launch_bounds__(MC_CARRY_THREADS) mc_carry_kernel(uint32_t nti
 // txn-major fold of the pairs' prefixes in key order: foldl(keys, Timestamp::max(value, acc), NONE).
 // *stop = the first globally visible txn that takes the slow path with no executeAt known here: its
 // executeAt is time.uniqueNow(minNonConflicting) (local/CommandStore.java:348), chosen by the caller,
-// so neither it nor any later txn of the batch may be merged before the caller supplies it.
+// so neither it nor any later txn of the batch may be merged before the caller supplies it.  A
+// range-domain ExclusiveSyncPoint returns txnId without reading the map (:335-339): NONE, fast.
 __global__ void __launch_bounds__(256) mc_fold_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ msb,
                                                       const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
-                                                      const uint32_t *__restrict__ key_off, const TsV *__restrict__ prefix,
+                                                      const uint32_t *__restrict__ po, const TsV *__restrict__ prefix,
                                                       uint64_t *__restrict__ om, uint64_t *__restrict__ ol,
                                                       int32_t *__restrict__ on, uint8_t *__restrict__ ohas,
                                                       uint8_t *__restrict__ ofast, uint32_t known_exec, uint32_t ov_t,
@@ -218,17 +270,18 @@ __global__ void __launch_bounds__(256) mc_fold_kernel(uint32_t first, uint32_t l
 {
     const uint32_t t = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= last) return;
-    const uint32_t pbase = key_off[first];
+    const uint32_t kind = (uint32_t)(lsb[t] >> 1) & 7;
+    const bool xsp = (lsb[t] & 1) && kind == 4;
     TsV acc;
     acc.has = 0; acc.msb = 0; acc.lsb = 0; acc.node = 0;
-    for (uint32_t p = key_off[t]; p < key_off[t + 1]; ++p) {
-        const TsV x = prefix[p - pbase];
-        if (x.has && (!acc.has || tcmp(x, acc) >= 0)) acc = x;
-    }
+    if (!xsp)
+        for (uint32_t p = po[t - first]; p < po[t - first + 1]; ++p) {
+            const TsV x = prefix[p];
+            if (x.has && (!acc.has || tcmp(x, acc) >= 0)) acc = x;
+        }
     om[t] = acc.msb; ol[t] = acc.lsb; on[t] = acc.node; ohas[t] = (uint8_t)acc.has;
-    const bool fast = ts_cmp(msb[t], lsb[t], node[t], acc.msb, acc.lsb, acc.node) >= 0;
+    const bool fast = xsp || ts_cmp(msb[t], lsb[t], node[t], acc.msb, acc.lsb, acc.node) >= 0;
     ofast[t] = (uint8_t)fast;
-    const uint32_t kind = (uint32_t)(lsb[t] >> 1) & 7;
     if (!fast && !known_exec && t != ov_t && kind != 2u) atomicMin(stop, t);
 }
 
@@ -266,6 +319,23 @@ extern "C" int32_t accord_max_conflicts_reset(accord_store *s)
 
 namespace {
 
+// Device buffers for a pass over P (txn, key) pairs.
+int32_t mc_buffers(accord_store *s, uint32_t P)
+{
+    DevBuf *T = s->op_tmp;   // pk, pv(txn), sk, sv, tk, tv, pe(pair), prefix, tile comps, carry, radix temp, se, te, sorted values
+    for (int b = 0; b < 7; ++b) HIPCHECK(s, T[b].ensure((size_t)P * 4 + 4));
+    HIPCHECK(s, T[7].ensure((size_t)P * sizeof(TsV) + 32));
+    const uint32_t ntiles = (P + MC_TILE - 1) / MC_TILE;
+    HIPCHECK(s, T[8].ensure((size_t)ntiles * sizeof(Comp) + 64));
+    HIPCHECK(s, T[9].ensure((size_t)ntiles * sizeof(TsV) + 32));
+    HIPCHECK(s, T[10].ensure(accord::radix_sort_temp_bytes(P)));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max(P, accord::radix_sort_scan_len(P))), s->stream));
+    HIPCHECK(s, T[11].ensure((size_t)P * 4 + 4));                 // sorted pair index
+    HIPCHECK(s, T[12].ensure((size_t)P * 4 + 4));                 // its ping-pong buffer
+    HIPCHECK(s, T[13].ensure((size_t)P * sizeof(TsV) + 32));      // values in sorted order
+    return ACCORD_OK;
+}
+
 // One fold pass over txns [first, last): pack, stable sort by key, segmented scan seeded by the
 // store's map (written into mc_state2), and -- with outputs -- the per-txn fold and the stop index.
 int32_t mc_pass(accord_store *s, uint32_t first, uint32_t last, const McValues &mv, bool outputs, uint32_t *stop_dev)
@@ -277,20 +347,30 @@ int32_t mc_pass(accord_store *s, uint32_t first, uint32_t last, const McValues &
     uint64_t *om = s->mc_out.as<uint64_t>(), *ol = om + s->n;
     int32_t *on = (int32_t *)(ol + s->n);
     uint8_t *ohas = (uint8_t *)(on + s->n), *ofast = ohas + s->n;
-    std::vector<uint32_t> ko(2);
-    // pair range of [first, last): key_off is on the device; the host copy of the batch offsets
-    // is not kept, so read the two bounds
-    HIPCHECK(s, hipMemcpyAsync(&ko[0], s->key_off.as<uint32_t>() + first, 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(s, hipMemcpyAsync(&ko[1], s->key_off.as<uint32_t>() + last, 4, hipMemcpyDeviceToHost, st));
+    const uint32_t nt = last - first;
+    // pair offsets of [first, last): counts, exclusive scan (po[nt] = total), read the total
+    uint32_t *po = s->mc_po.as<uint32_t>();
+    mc_count_kernel<<<(nt + 1 + 255) / 256, 256, 0, st>>>(first, last, s->lsb.as<uint64_t>(), s->key_off.as<uint32_t>(),
+                                                         s->rng_off.as<uint32_t>(), s->rng_start.as<uint32_t>(),
+                                                         s->rng_end.as<uint32_t>(), s->cfg.key_lo, s->cfg.key_hi,
+                                                         s->mc_cnt.as<uint32_t>());
+    unsigned long long *tot = (unsigned long long *)&dev->totals[6];
+    accord::exclusive_scan_u32(s->mc_cnt.as<uint32_t>(), po, nt + 1, tot, s->scan_tmp.p, st);
+    unsigned long long Pt = 0;
+    HIPCHECK(s, hipMemcpyAsync(&Pt, tot, 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
-    const uint32_t P = ko[1] - ko[0], nt = last - first;
+    if (Pt >= (1ull << 31)) return fail(s, ACCORD_ERR_CAPACITY, "MaxConflicts fold: %llu (txn, key) pairs", Pt);
+    const uint32_t P = (uint32_t)Pt;
+    int32_t rc = mc_buffers(s, P);
+    if (rc) return rc;
     const uint32_t ntiles = (P + MC_TILE - 1) / MC_TILE;
     HIPCHECK(s, hipMemcpyAsync(s->mc_state2.p, s->mc_state.p, (size_t)nkeys * sizeof(TsV), hipMemcpyDeviceToDevice, st));
     if (nt)
         mc_pack_kernel<<<(nt + 255) / 256, 256, 0, st>>>(first, last, s->lsb.as<uint64_t>(), s->key_off.as<uint32_t>(),
-                                                         s->key_ord.as<uint32_t>(), s->cfg.key_lo, s->cfg.key_hi,
-                                                         T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[6].as<uint32_t>(),
-                                                         &dev->status);
+                                                         s->key_ord.as<uint32_t>(), s->rng_off.as<uint32_t>(),
+                                                         s->rng_start.as<uint32_t>(), s->rng_end.as<uint32_t>(),
+                                                         s->cfg.key_lo, s->cfg.key_hi, po, T[0].as<uint32_t>(),
+                                                         T[1].as<uint32_t>(), T[6].as<uint32_t>(), &dev->status);
     if (P) {
         accord::radix_sort_pairs(T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[2].as<uint32_t>(), T[3].as<uint32_t>(),
                                  T[4].as<uint32_t>(), T[5].as<uint32_t>(), T[6].as<uint32_t>(), T[11].as<uint32_t>(),
@@ -305,7 +385,7 @@ int32_t mc_pass(accord_store *s, uint32_t first, uint32_t last, const McValues &
     }
     if (outputs && nt)
         mc_fold_kernel<<<(nt + 255) / 256, 256, 0, st>>>(first, last, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(),
-                                                         s->node.as<int32_t>(), s->key_off.as<uint32_t>(), T[7].as<TsV>(),
+                                                         s->node.as<int32_t>(), po, T[7].as<TsV>(),
                                                          om, ol, on, ohas, ofast, s->has_exec ? 1u : 0u, mv.ov_t, stop_dev);
     HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;
@@ -316,25 +396,16 @@ int32_t mc_fold(accord_store *s, uint32_t first, bool override, uint64_t ov_msb,
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     if (!s->has_batch) return fail(s, ACCORD_ERR_STATE, "accord_max_conflicts_fold before accord_batch_upload");
-    if (s->R) return fail(s, ACCORD_ERR_DOMAIN, "accord_max_conflicts_fold: range txns are not supported yet");
     if (first != s->mc_next || first >= s->n + (s->n == 0 ? 1u : 0u))
         return fail(s, ACCORD_ERR_STATE, "MaxConflicts fold of this batch must continue at txn %u (asked: %u)", s->mc_next, first);
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     int32_t rc = mc_ensure_state(s);
     if (rc) return rc;
-    const uint32_t n = s->n, P = s->P;
+    const uint32_t n = s->n;
     hipStream_t st = s->stream;
-    DevBuf *T = s->op_tmp;   // pk, pv(txn), sk, sv, tk, tv, pe(pair), prefix, tile comps, carry, radix temp, se, te, sorted values
-    for (int b = 0; b < 7; ++b) HIPCHECK(s, T[b].ensure((size_t)P * 4 + 4));
-    HIPCHECK(s, T[7].ensure((size_t)P * sizeof(TsV) + 32));
-    const uint32_t ntiles = (P + MC_TILE - 1) / MC_TILE;
-    HIPCHECK(s, T[8].ensure((size_t)ntiles * sizeof(Comp) + 64));
-    HIPCHECK(s, T[9].ensure((size_t)ntiles * sizeof(TsV) + 32));
-    HIPCHECK(s, T[10].ensure(accord::radix_sort_temp_bytes(P)));
-    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max(P, accord::radix_sort_scan_len(P))), s->stream));
-    HIPCHECK(s, T[11].ensure((size_t)P * 4 + 4));                 // sorted pair index
-    HIPCHECK(s, T[12].ensure((size_t)P * 4 + 4));                 // its ping-pong buffer
-    HIPCHECK(s, T[13].ensure((size_t)P * sizeof(TsV) + 32));      // values in sorted order
+    HIPCHECK(s, s->mc_cnt.ensure(((size_t)n + 2) * 4));
+    HIPCHECK(s, s->mc_po.ensure(((size_t)n + 2) * 4));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n + 1), s->stream));
     HIPCHECK(s, s->mc_out.ensure((size_t)n * 22 + 64));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     HostTotals *dev = s->status_totals.as<HostTotals>();

@@ -101,7 +101,7 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
                       &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->tmp_ent, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list, &s->cv_tmp,
-                      &s->seg_start, &s->seg_end, &s->mc_state, &s->mc_state2, &s->mc_out, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
+                      &s->seg_start, &s->seg_end, &s->mc_state, &s->mc_state2, &s->mc_out, &s->mc_cnt, &s->mc_po, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
                       &s->rng_owner, &s->is_range, &s->rt_excl, &s->range_txns, &s->cnt_rngs, &s->cnt_rvals,

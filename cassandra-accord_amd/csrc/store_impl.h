@@ -133,7 +133,7 @@ struct accord_store {
     int ds_cur = -1;
     DevBuf op_tmp[24];
     // MaxConflicts (maxconflicts.hip): per-key map (double-buffered) and the last fold's outputs
-    DevBuf mc_state, mc_state2, mc_out;
+    DevBuf mc_state, mc_state2, mc_out, mc_cnt, mc_po;   // + per-txn pair counts / offsets of a pass
     uint32_t mc_next = 0;          // next txn of the uploaded batch the fold continues at
     float ops_ms = 0;
     ShardComm *comm = nullptr;

@@ -260,7 +260,7 @@ void    accord_deps_inverse_release(accord_deps_inverse *inv);
 int32_t accord_ops_timing(accord_store *store, float *ms);
 
 /* ---- MaxConflicts fold ----
- * Replaces, for the uploaded batch of key txns in stream order, the per-PreAccept
+ * Replaces, for the uploaded batch of key and range txns in stream order, the per-PreAccept
  *   Timestamp minNonConflicting = maxConflicts.get(keys)          (local/CommandStore.java:344,
  *                                                                  local/MaxConflicts.java:46-49)
  *   permitFastPath && txnId.compareTo(minNonConflicting) >= 0     (local/CommandStore.java:345)
@@ -279,8 +279,11 @@ int32_t accord_ops_timing(accord_store *store, float *ms);
  * [first, f] are final (f's own reading does not depend on f's executeAt).  The caller picks f's
  * executeAt and continues with accord_max_conflicts_fold_from(store, f, executeAt, out), which
  * merges it and folds on from there.  Folding a batch again from an earlier txn is ACCORD_ERR_STATE.
- * ExclusiveSyncPoint in the key domain: ACCORD_ERR_KIND (preaccept casts its keys to Ranges, :335-339).
- * Range txns: ACCORD_ERR_DOMAIN (not supported yet). */
+ * Range txns read and write the store keys their ranges (s, e] cover, clipped to [key_lo, key_hi)
+ * (an IntKey ReducingRangeMap has no points between keys); ranges must be non-empty, sorted and
+ * non-overlapping (ACCORD_ERR_KEYS).  A range-domain ExclusiveSyncPoint returns txnId without reading
+ * the map (markExclusiveSyncPoint, :335-339: present = 0, fast = 1; rejectBefore stays in Java) and
+ * merges its executeAt; in the key domain it is ACCORD_ERR_KIND (preaccept casts its keys to Ranges). */
 typedef struct {
     uint64_t *msb, *lsb;        /* [n] minNonConflicting (host arrays, caller-owned; NULL = skip) */
     int32_t  *node;

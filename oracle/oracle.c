@@ -1674,6 +1674,146 @@ int or_max_conflicts(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const
     return 0;
 }
 
+/* MaxConflicts over key and range txns with the map held as a ReducingRangeMap-style list of
+ * disjoint intervals (utils/ReducingIntervalMap.java, utils/ReducingRangeMap.java) rather than one
+ * entry per key: a key k is the interval [k, k+1), a range (s, e] (Range.EndInclusive) the interval
+ * [s+1, e+1), clipped to the store's keys [key_lo, key_lo + nkeys) ("keys sliced to those owned",
+ * local/CommandStore.java:318).  get = foldl over the intersecting intervals in order with
+ * Timestamp.max(value, acc) (MaxConflicts.java:46-54); update = merge with Timestamp.max(old, new)
+ * (:68-80), which splits intervals at the new bounds.  ExclusiveSyncPoint in the range domain
+ * returns txnId before reading the map (CommandStore.java:335-339: present = 0, fast = 1) and is
+ * merged like any globally visible txn; in the key domain it is -3.  The per-key state arrays are
+ * the map's point values on entry and exit.  Returns 0, -3 kind, -4 key outside the store, -6
+ * ranges not sorted / overlapping / empty. */
+typedef struct { uint32_t a, b; ts_t v; } mc_ivl;
+typedef struct { mc_ivl *p; size_t n, cap; } mc_map;
+
+static int mcm_push(mc_map *m, uint32_t a, uint32_t b, ts_t v)
+{
+    if (a >= b) return 0;
+    if (m->n == m->cap) {
+        size_t nc = m->cap ? m->cap * 2 : 64;
+        mc_ivl *np = (mc_ivl *)realloc(m->p, nc * sizeof(mc_ivl));
+        if (!np) return -1;
+        m->p = np; m->cap = nc;
+    }
+    m->p[m->n].a = a; m->p[m->n].b = b; m->p[m->n].v = v;
+    m->n++;
+    return 0;
+}
+
+/* foldl(Timestamp::max(value, acc)) over the intervals intersecting [a, b) */
+static void mcm_get(const mc_map *m, uint32_t a, uint32_t b, int *has, ts_t *acc)
+{
+    for (size_t i = 0; i < m->n; ++i) {
+        const mc_ivl *x = &m->p[i];
+        if (x->b <= a || x->a >= b) continue;
+        if (!*has || ts_cmp(&x->v, acc) >= 0) *acc = x->v;
+        *has = 1;
+    }
+}
+
+/* merge(this, create([a, b), v)) with Timestamp::max(old, new): old kept unless new is greater */
+static int mcm_update(mc_map *m, uint32_t a, uint32_t b, const ts_t *v)
+{
+    mc_map o = {0, 0, 0};
+    uint32_t cur = a;            /* next uncovered point of [a, b) */
+    for (size_t i = 0; i < m->n; ++i) {
+        const mc_ivl x = m->p[i];
+        if (x.b <= a || x.a >= b) {
+            if (x.a >= b && cur < b) { if (mcm_push(&o, cur, b, *v)) goto oom; cur = b; }
+            if (mcm_push(&o, x.a, x.b, x.v)) goto oom;
+            continue;
+        }
+        if (x.a < a && mcm_push(&o, x.a, a, x.v)) goto oom;
+        const uint32_t lo = x.a > a ? x.a : a, hi = x.b < b ? x.b : b;
+        if (cur < lo && mcm_push(&o, cur, lo, *v)) goto oom;
+        if (mcm_push(&o, lo, hi, ts_cmp(v, &x.v) > 0 ? *v : x.v)) goto oom;
+        cur = hi;
+        if (x.b > b && mcm_push(&o, b, x.b, x.v)) goto oom;
+    }
+    if (cur < b && mcm_push(&o, cur, b, *v)) goto oom;
+    free(m->p);
+    *m = o;
+    return 0;
+oom:
+    free(o.p);
+    return -1;
+}
+
+int or_max_conflicts_rm(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
+                        const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,
+                        const uint32_t *rng_start, const uint32_t *rng_end, const uint64_t *exec_msb,
+                        const uint64_t *exec_lsb, const int32_t *exec_node, uint32_t key_lo, uint32_t nkeys,
+                        uint64_t *st_msb, uint64_t *st_lsb, int32_t *st_node, uint8_t *st_has,
+                        uint64_t *o_msb, uint64_t *o_lsb, int32_t *o_node, uint8_t *o_has, uint8_t *o_fast,
+                        uint32_t first, int has_override, uint64_t ov_msb, uint64_t ov_lsb, int32_t ov_node,
+                        uint32_t *folded)
+{
+    mc_map m = {0, 0, 0};
+    int rc = 0;
+    *folded = n;
+    for (uint32_t k = 0; k < nkeys; ++k)
+        if (st_has[k]) {
+            ts_t v = {st_msb[k], st_lsb[k], st_node[k]};
+            if (mcm_push(&m, k, k + 1, v)) { rc = -1; goto out; }
+        }
+    for (uint32_t i = first; i < n; ++i) {
+        const int kind = kind_of(lsb[i]), range = (int)(lsb[i] & 1);
+        if (kind >= 5 || (!range && kind == K_EXCL_SYNC_POINT)) { rc = -3; goto out; }
+        /* the txn's intervals, clipped to the store */
+        uint32_t na = range ? rng_off[i + 1] - rng_off[i] : key_off[i + 1] - key_off[i];
+        uint32_t *ia = (uint32_t *)malloc(((size_t)na + 1) * 2 * sizeof(uint32_t));
+        if (!ia) { rc = -1; goto out; }
+        uint32_t ni = 0;
+        for (uint32_t q = 0; q < na; ++q) {
+            uint64_t a, b;
+            if (range) {
+                const uint32_t r = rng_off[i] + q;
+                if (rng_start[r] >= rng_end[r] || (q > 0 && rng_start[r] < rng_end[r - 1])) { free(ia); rc = -6; goto out; }
+                a = (uint64_t)rng_start[r] + 1; b = (uint64_t)rng_end[r] + 1;
+                if (a < key_lo) a = key_lo;
+                if (b > (uint64_t)key_lo + nkeys) b = (uint64_t)key_lo + nkeys;
+                if (a >= b) continue;
+            } else {
+                const uint32_t k = key_ord[key_off[i] + q];
+                if (k < key_lo || k - key_lo >= nkeys) { free(ia); rc = -4; goto out; }
+                a = k; b = (uint64_t)k + 1;
+            }
+            ia[2 * ni] = (uint32_t)(a - key_lo); ia[2 * ni + 1] = (uint32_t)(b - key_lo); ++ni;
+        }
+        int has = 0, fast;
+        ts_t acc = {0, 0, 0};
+        if (range && kind == K_EXCL_SYNC_POINT) fast = 1;     /* markExclusiveSyncPoint; return txnId */
+        else {
+            for (uint32_t q = 0; q < ni; ++q) mcm_get(&m, ia[2 * q], ia[2 * q + 1], &has, &acc);
+            fast = or_ts_compare(msb[i], lsb[i], node[i], acc.msb, acc.lsb, acc.node) >= 0;
+        }
+        o_msb[i] = acc.msb; o_lsb[i] = acc.lsb; o_node[i] = acc.node; o_has[i] = (uint8_t)has;
+        o_fast[i] = (uint8_t)fast;
+        if (is_globally_visible(kind) == 1) {
+            ts_t e;
+            if (i == first && has_override) { e.msb = ov_msb; e.lsb = ov_lsb; e.node = ov_node; }
+            else if (exec_msb) { e.msb = exec_msb[i]; e.lsb = exec_lsb[i]; e.node = exec_node[i]; }
+            else if (fast) { e.msb = msb[i]; e.lsb = lsb[i]; e.node = node[i]; }
+            else { free(ia); *folded = i; goto out; }
+            for (uint32_t q = 0; q < ni; ++q)
+                if (mcm_update(&m, ia[2 * q], ia[2 * q + 1], &e)) { free(ia); rc = -1; goto out; }
+        }
+        free(ia);
+    }
+out:
+    if (rc == 0) {
+        memset(st_has, 0, nkeys);
+        for (size_t j = 0; j < m.n; ++j)
+            for (uint32_t k = m.p[j].a; k < m.p[j].b; ++k) {
+                st_msb[k] = m.p[j].v.msb; st_lsb[k] = m.p[j].v.lsb; st_node[k] = m.p[j].v.node; st_has[k] = 1;
+            }
+    }
+    free(m.p);
+    return rc;
+}
+
 /* ==========================================================================================
  * Stateful literal CommandStore (test infrastructure): a resident store fed batch by batch,
  * with real status events in between.  Key txns only.  Every txn a batch carries is inserted

@@ -318,11 +318,14 @@ def deps_invert(p: PartialDeps, range_side: bool = False):
     return off, a
 
 
-def max_conflicts(s, key_lo: int, nkeys: int, state=None, first: int = 0, exec_at=None, out=None):
+def max_conflicts(s, key_lo: int, nkeys: int, state=None, first: int = 0, exec_at=None, out=None,
+                  intervals=None):
     """or_max_conflicts: per-txn (msb, lsb, node, present, fast), the updated per-key map and the
     number of txns merged (`folded`: the fold stops at a slow-path txn whose executeAt is unknown).
     `state` = (msb, lsb, node, present) arrays of nkeys entries (None = MaxConflicts.EMPTY);
-    first/exec_at continue a stopped fold with the caller's executeAt for txn `first`."""
+    first/exec_at continue a stopped fold with the caller's executeAt for txn `first`.
+    intervals: use or_max_conflicts_rm (the map as disjoint intervals; key and range txns);
+    None = only when the stream has range txns."""
     n = len(s.msb)
     if state is None:
         state = (np.zeros(nkeys, np.uint64), np.zeros(nkeys, np.uint64), np.zeros(nkeys, np.int32),
@@ -344,6 +347,29 @@ def max_conflicts(s, key_lo: int, nkeys: int, state=None, first: int = 0, exec_a
     folded = C.c_uint32(0)
     ov = exec_at if exec_at is not None else (0, 0, 0)
     p = lambda a, t: None if a is None else a.ctypes.data_as(t)
+    if intervals is None:
+        intervals = bool(np.any(lsb & np.uint64(1)))
+    if intervals:
+        L = lib()
+        if not getattr(L, "_mcrm_typed", False):
+            L.or_max_conflicts_rm.argtypes = ([C.c_uint32, _u64p, _u64p, _i32p, _u32p, _u32p, _u32p, _u32p, _u32p,
+                                               _u64p, _u64p, _i32p, C.c_uint32, C.c_uint32, _u64p, _u64p, _i32p, _u8p]
+                                              + [_u64p, _u64p, _i32p, _u8p, _u8p]
+                                              + [C.c_uint32, C.c_int, C.c_uint64, C.c_uint64, C.c_int32, _u32p])
+            L._mcrm_typed = True
+        ro = np.ascontiguousarray(s.rng_off if s.rng_off is not None else np.zeros(n + 1), np.uint32)
+        rs = np.ascontiguousarray(s.rng_start if s.rng_start is not None else np.zeros(1), np.uint32)
+        re = np.ascontiguousarray(s.rng_end if s.rng_end is not None else np.zeros(1), np.uint32)
+        rc = L.or_max_conflicts_rm(n, p(msb, _u64p), p(lsb, _u64p), p(node, _i32p), p(ko, _u32p), p(kk, _u32p),
+                                   p(ro, _u32p), p(rs, _u32p), p(re, _u32p),
+                                   p(em, _u64p), p(el, _u64p), p(en, _i32p), key_lo, nkeys,
+                                   p(st[0], _u64p), p(st[1], _u64p), p(st[2], _i32p), p(st[3], _u8p),
+                                   p(out[0], _u64p), p(out[1], _u64p), p(out[2], _i32p), p(out[3], _u8p),
+                                   p(out[4], _u8p), first, 1 if exec_at is not None else 0, int(ov[0]), int(ov[1]),
+                                   int(ov[2]), C.byref(folded))
+        if rc != 0:
+            raise OracleError(rc)
+        return out, st, int(folded.value)
     rc = lib().or_max_conflicts(n, p(msb, _u64p), p(lsb, _u64p), p(node, _i32p), p(ko, _u32p), p(kk, _u32p),
                                 p(em, _u64p), p(el, _u64p), p(en, _i32p), key_lo, nkeys,
                                 p(st[0], _u64p), p(st[1], _u64p), p(st[2], _i32p), p(st[3], _u8p),
