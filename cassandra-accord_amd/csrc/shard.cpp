@@ -13,6 +13,8 @@
 
 #include <rccl/rccl.h>
 
+#include <array>
+#include <cstdint>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -29,7 +31,7 @@ struct Part {
 struct ShardComm {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    DevBuf ind, cscan, exp[3], bnd, counts, allcounts, recv;
+    DevBuf ind, cscan, exp[6], bnd, counts, allcounts, recv;
     unsigned long long *total = nullptr;
     DevBuf total_buf, flag;
 };
@@ -41,8 +43,8 @@ void shard_comm_destroy(accord_store *s)
     if (!s || !s->comm) return;
     ShardComm *c = s->comm;
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    DevBuf *bufs[] = {&c->ind, &c->cscan, &c->exp[0], &c->exp[1], &c->exp[2], &c->bnd, &c->counts, &c->allcounts,
-                      &c->recv, &c->total_buf, &c->flag};
+    DevBuf *bufs[] = {&c->ind, &c->cscan, &c->exp[0], &c->exp[1], &c->exp[2], &c->exp[3], &c->exp[4], &c->exp[5],
+                      &c->bnd, &c->counts, &c->allcounts, &c->recv, &c->total_buf, &c->flag};
     for (DevBuf *b : bufs) b->release();
     delete c;
     s->comm = nullptr;
@@ -122,6 +124,18 @@ int32_t merge_parts(accord_store *s, const std::vector<Part> &parts, uint32_t n,
     return ACCORD_OK;
 }
 
+// Parts with RangeDeps: the stores' RangeDeps share range keys (a range txn intersecting several
+// stores' key blocks appears in each), so their union is RelationMultiMap.linearUnion, not the
+// concatenation the key-disjoint merge relies on.  Both sides go through accord_deps_union; the
+// result becomes the store's current deps.
+int32_t union_general(accord_store *s, uint32_t nparts, const accord_deps *parts)
+{
+    const int32_t rc = accord_deps_union(s, nparts, parts);
+    if (rc) return rc;
+    s->merged = true;
+    return ACCORD_OK;
+}
+
 #define NCCLGROUPCHECK(s, expr)                                                                  \
     do {                                                                                         \
         ncclResult_t r_ = (expr);                                                                \
@@ -147,13 +161,14 @@ int32_t accord_deps_merge(accord_store *s, uint32_t nparts, const accord_deps *p
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     const uint32_t n = parts[0].n;
     std::vector<Part> ps(nparts);
+    bool ranges = false;
     for (uint32_t g = 0; g < nparts; ++g) {
         if (parts[g].n != n) return fail(s, ACCORD_ERR_ARG, "merge parts cover different txn counts");
-        if (parts[g].rd_rngs_total || parts[g].rd_vals_total)
-            return fail(s, ACCORD_ERR_STATE, "merge of RangeDeps is not supported by this build");
+        ranges = ranges || parts[g].rd_rngs_total || parts[g].rd_vals_total;
         ps[g] = Part{parts[g].kd_key_off, parts[g].kd_keys, parts[g].kd_val_off, parts[g].kd_vals,
                      parts[g].kd_k2v_off, parts[g].kd_k2v};
     }
+    if (ranges) return union_general(s, nparts, parts);
     return merge_parts(s, ps, n, txn_lo);
 }
 
@@ -200,24 +215,27 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
     ShardComm *c = s->comm;
     const uint32_t G = (uint32_t)c->nranks, me = (uint32_t)c->rank, n = s->n;
     hipStream_t st = s->stream;
+    // Offset arrays (KeyDeps keys / values / keysToTxnIds, RangeDeps ranges / values /
+    // rangesToTxnIds) and the data arrays each indexes (ranges: starts and ends).
+    constexpr int NA = 6, ND = 7;
+    static const int grp[ND] = {0, 1, 2, 3, 3, 4, 5};
 
     // Every rank must reach the same collectives: the local checks and allocations run first, then
     // one all-reduce (max) of their status agrees whether every rank goes ahead; a rank that failed
     // keeps its own message, the others report that a peer failed.
-    std::vector<uint32_t> bnd(3 * (G + 1));
-    uint32_t *exp_off[3] = {nullptr, nullptr, nullptr};
+    std::vector<uint32_t> bnd(NA * (G + 1));
+    uint32_t *exp_off[NA] = {};
     auto prepare = [&]() -> int32_t {
         if (!s->computed || s->merged) return fail(s, ACCORD_ERR_STATE, "exchange needs a freshly computed partial");
-        if (s->tot_rngs || s->tot_rvals) return fail(s, ACCORD_ERR_STATE, "exchange of RangeDeps is not supported by this build");
         if (!s->has_txn_index && s->n != n_total) return fail(s, ACCORD_ERR_ARG, "batch without txn_index must be the whole stream");
         // 1. partial offsets expanded to every global txn position
         HIPCHECK(s, c->ind.ensure((size_t)n_total * 4 + 4));
         HIPCHECK(s, c->cscan.ensure(((size_t)n_total + 1) * 4));
-        for (int a = 0; a < 3; ++a) HIPCHECK(s, c->exp[a].ensure(((size_t)n_total + 1) * 4));
-        HIPCHECK(s, c->bnd.ensure((size_t)3 * (G + 1) * 4));
+        for (int a = 0; a < NA; ++a) HIPCHECK(s, c->exp[a].ensure(((size_t)n_total + 1) * 4));
+        HIPCHECK(s, c->bnd.ensure((size_t)NA * (G + 1) * 4));
         HIPCHECK(s, c->total_buf.ensure(16));
-        HIPCHECK(s, c->counts.ensure(3 * (size_t)G * 8));
-        HIPCHECK(s, c->allcounts.ensure(3 * (size_t)G * 8 * G));
+        HIPCHECK(s, c->counts.ensure(2 * NA * (size_t)G * 8));
+        HIPCHECK(s, c->allcounts.ensure(2 * NA * (size_t)G * 8 * G));
         HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n_total), s->stream));
         return ACCORD_OK;
     };
@@ -240,38 +258,49 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
         if (rc) return rc;
     }
     if (s->events) (void)hipEventRecord(s->ev[EV_XCHG_START], st);
-    const uint32_t *off[3] = {s->kd_key_off.as<uint32_t>(), s->kd_val_off.as<uint32_t>(), s->kd_k2v_off.as<uint32_t>()};
-    for (int a = 0; a < 3; ++a) exp_off[a] = c->exp[a].as<uint32_t>();
-    if (s->has_txn_index) {
-        accord::launch_expand_offsets(n, n_total, s->txn_index.as<uint32_t>(), c->ind.as<uint32_t>(),
-                                      c->cscan.as<uint32_t>(), off, exp_off, s->scan_tmp.p,
-                                      c->total_buf.as<unsigned long long>(), st);
-    } else {
-        for (int a = 0; a < 3; ++a)
-            HIPCHECK(s, hipMemcpyAsync(exp_off[a], off[a], ((size_t)n_total + 1) * 4, hipMemcpyDeviceToDevice, st));
+    const uint32_t *off[NA] = {s->kd_key_off.as<uint32_t>(), s->kd_val_off.as<uint32_t>(), s->kd_k2v_off.as<uint32_t>(),
+                               s->rd_rng_off.as<uint32_t>(), s->rd_val_off.as<uint32_t>(), s->rd_r2v_off.as<uint32_t>()};
+    for (int a = 0; a < NA; ++a) exp_off[a] = c->exp[a].as<uint32_t>();
+    for (int h = 0; h < 2; ++h) {          // KeyDeps side, RangeDeps side
+        if (s->has_txn_index) {
+            accord::launch_expand_offsets(n, n_total, s->txn_index.as<uint32_t>(), c->ind.as<uint32_t>(),
+                                          c->cscan.as<uint32_t>(), off + 3 * h, exp_off + 3 * h, s->scan_tmp.p,
+                                          c->total_buf.as<unsigned long long>(), st);
+        } else {
+            for (int a = 3 * h; a < 3 * h + 3; ++a)
+                HIPCHECK(s, hipMemcpyAsync(exp_off[a], off[a], ((size_t)n_total + 1) * 4, hipMemcpyDeviceToDevice, st));
+        }
+        accord::launch_boundaries(G, n_total, exp_off + 3 * h, c->bnd.as<uint32_t>() + 3 * h * (G + 1), st);
     }
-    accord::launch_boundaries(G, n_total, exp_off, c->bnd.as<uint32_t>(), st);
     HIPCHECK(s, hipMemcpyAsync(bnd.data(), c->bnd.p, bnd.size() * 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
 
-    // 2. element counts I send to every rank; all-gather the G x G x 3 matrix
+    // 2. per destination: element counts and start offsets of what I send; all-gather the G x G matrix
     auto home_lo = [&](uint32_t d) { return (uint32_t)(((unsigned long long)d * n_total) / G); };
-    std::vector<unsigned long long> mine(3 * (size_t)G);
+    const size_t W = 2 * NA;
+    std::vector<unsigned long long> mine(W * (size_t)G);
     for (uint32_t d = 0; d < G; ++d)
-        for (int a = 0; a < 3; ++a) mine[3 * d + a] = bnd[a * (G + 1) + d + 1] - bnd[a * (G + 1) + d];
+        for (int a = 0; a < NA; ++a) {
+            mine[W * d + a] = bnd[a * (G + 1) + d + 1] - bnd[a * (G + 1) + d];
+            mine[W * d + NA + a] = bnd[a * (G + 1) + d];
+        }
     HIPCHECK(s, hipMemcpyAsync(c->counts.p, mine.data(), mine.size() * 8, hipMemcpyHostToDevice, st));
     NCCLCHECK(s, ncclAllGather(c->counts.p, c->allcounts.p, mine.size(), ncclUint64, c->comm, st));
     std::vector<unsigned long long> all(mine.size() * G);
     HIPCHECK(s, hipMemcpyAsync(all.data(), c->allcounts.p, all.size() * 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
 
-    // 3. receive layout: per source [off_key|off_val|off_k2v (nh+1 each)][keys][vals][k2v]
+    // 3. receive layout: per source [NA offset arrays (nh+1 each)][ND data arrays]
     const uint32_t my_lo = home_lo(me), nh = home_lo(me + 1) - my_lo;
     std::vector<size_t> rbase(G + 1);
     rbase[0] = 0;
+    bool ranges = false;
     for (uint32_t src = 0; src < G; ++src) {
-        const unsigned long long *cnt = &all[(size_t)src * 3 * G + 3 * me];
-        rbase[src + 1] = rbase[src] + 3 * ((size_t)nh + 1) + cnt[0] + cnt[1] + cnt[2];
+        const unsigned long long *cnt = &all[(size_t)src * W * G + W * me];
+        size_t sz = NA * ((size_t)nh + 1);
+        for (int k = 0; k < ND; ++k) sz += cnt[grp[k]];
+        rbase[src + 1] = rbase[src] + sz;
+        ranges = ranges || cnt[3] || cnt[4];
     }
     {
         const hipError_t e = c->recv.ensure(rbase[G] * 4 + 16);
@@ -280,51 +309,87 @@ int32_t accord_deps_exchange_merge(accord_store *s, uint32_t n_total)
         if (rc) return rc;
     }
     uint32_t *R = c->recv.as<uint32_t>();
-    std::vector<Part> parts(G);
+    std::vector<std::array<uint32_t *, NA>> roff(G);
+    std::vector<std::array<uint32_t *, ND>> rdat(G);
     for (uint32_t src = 0; src < G; ++src) {
-        const unsigned long long *cnt = &all[(size_t)src * 3 * G + 3 * me];
+        const unsigned long long *cnt = &all[(size_t)src * W * G + W * me];
         uint32_t *b = R + rbase[src];
-        Part &p = parts[src];
-        p.key_off = b; p.val_off = b + (nh + 1); p.k2v_off = b + 2 * (nh + 1);
-        p.keys = b + 3 * (nh + 1); p.vals = p.keys + cnt[0]; p.k2v = (const int32_t *)(p.vals + cnt[1]);
+        for (int a = 0; a < NA; ++a) roff[src][a] = b + (size_t)a * (nh + 1);
+        uint32_t *p = b + (size_t)NA * (nh + 1);
+        for (int k = 0; k < ND; ++k) { rdat[src][k] = p; p += cnt[grp[k]]; }
     }
-    const uint32_t *data[3] = {s->kd_keys.as<uint32_t>(), s->kd_vals.as<uint32_t>(), (const uint32_t *)s->kd_k2v.p};
+    const uint32_t *data[ND] = {s->kd_keys.as<uint32_t>(), s->kd_vals.as<uint32_t>(), (const uint32_t *)s->kd_k2v.p,
+                                s->rd_rng_start.as<uint32_t>(), s->rd_rng_end.as<uint32_t>(), s->rd_vals.as<uint32_t>(),
+                                (const uint32_t *)s->rd_r2v.p};
     NCCLCHECK(s, ncclGroupStart());
     for (uint32_t d = 0; d < G; ++d) {
         const uint32_t lo = home_lo(d), nd = home_lo(d + 1) - lo;
-        for (int a = 0; a < 3; ++a) {
+        for (int a = 0; a < NA; ++a) {
             const uint32_t *so = exp_off[a] + lo;
-            const uint32_t *sd = data[a] + bnd[a * (G + 1) + d];
-            const size_t dc = mine[3 * d + a];
             if (d == me) {
-                uint32_t *ro = (uint32_t *)(a == 0 ? parts[me].key_off : a == 1 ? parts[me].val_off : parts[me].k2v_off);
-                uint32_t *rd = (uint32_t *)(a == 0 ? parts[me].keys : a == 1 ? parts[me].vals : (const uint32_t *)parts[me].k2v);
-                if (hipMemcpyAsync(ro, so, ((size_t)nd + 1) * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-                    (dc && hipMemcpyAsync(rd, sd, dc * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)) {
+                if (hipMemcpyAsync(roff[me][a], so, ((size_t)nd + 1) * 4, hipMemcpyDeviceToDevice, st) != hipSuccess) {
                     (void)ncclGroupEnd();
                     return fail(s, ACCORD_ERR_HIP, "local exchange copy failed");
                 }
             } else {
                 NCCLGROUPCHECK(s, ncclSend(so, (size_t)nd + 1, ncclUint32, (int)d, c->comm, st));
-                if (dc) NCCLGROUPCHECK(s, ncclSend(sd, dc, ncclUint32, (int)d, c->comm, st));
+            }
+        }
+        for (int k = 0; k < ND; ++k) {
+            const int a = grp[k];
+            const size_t dc = mine[W * d + a];
+            if (!dc) continue;
+            const uint32_t *sd = data[k] + bnd[a * (G + 1) + d];
+            if (d == me) {
+                if (hipMemcpyAsync(rdat[me][k], sd, dc * 4, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+                    (void)ncclGroupEnd();
+                    return fail(s, ACCORD_ERR_HIP, "local exchange copy failed");
+                }
+            } else {
+                NCCLGROUPCHECK(s, ncclSend(sd, dc, ncclUint32, (int)d, c->comm, st));
             }
         }
     }
     for (uint32_t src = 0; src < G; ++src) {
         if (src == me) continue;
-        const unsigned long long *cnt = &all[(size_t)src * 3 * G + 3 * me];
-        for (int a = 0; a < 3; ++a) {
-            uint32_t *ro = (uint32_t *)(a == 0 ? parts[src].key_off : a == 1 ? parts[src].val_off : parts[src].k2v_off);
-            uint32_t *rd = (uint32_t *)(a == 0 ? parts[src].keys : a == 1 ? parts[src].vals : (const uint32_t *)parts[src].k2v);
-            NCCLGROUPCHECK(s, ncclRecv(ro, (size_t)nh + 1, ncclUint32, (int)src, c->comm, st));
-            if (cnt[a]) NCCLGROUPCHECK(s, ncclRecv(rd, cnt[a], ncclUint32, (int)src, c->comm, st));
-        }
+        const unsigned long long *cnt = &all[(size_t)src * W * G + W * me];
+        for (int a = 0; a < NA; ++a) NCCLGROUPCHECK(s, ncclRecv(roff[src][a], (size_t)nh + 1, ncclUint32, (int)src, c->comm, st));
+        for (int k = 0; k < ND; ++k)
+            if (cnt[grp[k]]) NCCLGROUPCHECK(s, ncclRecv(rdat[src][k], cnt[grp[k]], ncclUint32, (int)src, c->comm, st));
     }
     NCCLCHECK(s, ncclGroupEnd());
     if (s->events) (void)hipEventRecord(s->ev[EV_XCHG_END], st);
 
-    // 4. union of the G parts of my txns
-    int32_t rc = merge_parts(s, parts, nh, my_lo);
+    // 4. union of the G parts of my txns.  Received offsets are the sender's (not rebased): the
+    // key-disjoint merge reads them relative to their first entry; the general union gets data
+    // pointers shifted back by the sender's start offset so the offsets index them directly.
+    int32_t rc;
+    if (!ranges) {
+        std::vector<Part> parts(G);
+        for (uint32_t src = 0; src < G; ++src)
+            parts[src] = Part{roff[src][0], rdat[src][0], roff[src][1], rdat[src][1], roff[src][2],
+                              (const int32_t *)rdat[src][2]};
+        rc = merge_parts(s, parts, nh, my_lo);
+    } else {
+        std::vector<accord_deps> views(G);
+        for (uint32_t src = 0; src < G; ++src) {
+            const unsigned long long *cnt = &all[(size_t)src * W * G + W * me];
+            const unsigned long long *start = cnt + NA;
+            auto back = [&](uint32_t *p, int a) { return (uint32_t *)((uintptr_t)p - (uintptr_t)(start[a] * 4)); };
+            accord_deps &v = views[src];
+            std::memset(&v, 0, sizeof(v));
+            v.n = nh;
+            v.kd_keys_total = cnt[0]; v.kd_vals_total = cnt[1]; v.kd_k2v_total = cnt[2];
+            v.rd_rngs_total = cnt[3]; v.rd_vals_total = cnt[4]; v.rd_r2v_total = cnt[5];
+            v.kd_key_off = roff[src][0]; v.kd_keys = back(rdat[src][0], 0);
+            v.kd_val_off = roff[src][1]; v.kd_vals = back(rdat[src][1], 1);
+            v.kd_k2v_off = roff[src][2]; v.kd_k2v = (int32_t *)back(rdat[src][2], 2);
+            v.rd_rng_off = roff[src][3]; v.rd_rng_start = back(rdat[src][3], 3); v.rd_rng_end = back(rdat[src][4], 3);
+            v.rd_val_off = roff[src][4]; v.rd_vals = back(rdat[src][5], 4);
+            v.rd_r2v_off = roff[src][5]; v.rd_r2v = (int32_t *)back(rdat[src][6], 5);
+        }
+        rc = union_general(s, G, views.data());
+    }
     if (rc) return rc;
     if (s->events) {
         (void)hipEventRecord(s->ev[EV_MERGE_END], st);

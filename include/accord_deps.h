@@ -201,14 +201,18 @@ int32_t accord_store_timing(accord_store *store, accord_timing *t);
  * parts: G device views (accord_deps_device_view of stores on this GPU, or received buffers) of
  * the same n txns, with key-disjoint parts ordered by key (CommandStores partition the keyspace).
  * The union becomes this store's current deps (read with device_view / download); txnIds are
- * global stream positions and txn_lo is the global position of txn 0 of the parts. */
+ * global stream positions and txn_lo is the global position of txn 0 of the parts.  Parts with
+ * RangeDeps (a range txn spanning several stores is in each store's RangeDeps under the same range
+ * key) are unioned with RelationMultiMap.linearUnion on both sides (accord_deps_union). */
 int32_t accord_deps_merge(accord_store *store, uint32_t nparts, const accord_deps *parts, uint32_t txn_lo);
 
 /* ---- multi-GPU: one store per rank over RCCL (xGMI) ----
  * Rank r holds the partial deps of its key block for the txns intersecting it (batch txn_index =
  * global stream positions).  accord_deps_exchange_merge sends every partial to the rank owning
  * the txn (txn g -> rank floor(g*G/n_total)) with one grouped RCCL send/recv and unions the G parts
- * there; afterwards the store's current deps are the full (node-level) deps of its own txns. */
+ * there; afterwards the store's current deps are the full (node-level) deps of its own txns.  Both
+ * KeyDeps and RangeDeps travel (6 offset + 7 data arrays per destination); when any received part
+ * holds RangeDeps the owner unions with accord_deps_union, else with the key-disjoint merge. */
 int32_t accord_comm_unique_id(void *id128);                  /* ncclGetUniqueId, 128 bytes */
 int32_t accord_comm_init(accord_store *store, int32_t nranks, int32_t rank, const void *id128);
 int32_t accord_deps_exchange_merge(accord_store *store, uint32_t n_total);

@@ -37,6 +37,42 @@ def test_local_stores_union_equals_single_store(gpu_device, nstores):
     assert got.first_difference(want) is None, got.first_difference(want)
 
 
+@pytest.mark.parametrize("nstores,rl", [(2, 40), (3, 400), (8, 2000)])
+def test_local_stores_union_with_ranges(gpu_device, nstores, rl):
+    # range txns span store blocks: every store reports them (their KeyDeps cut to its keys, the
+    # same range keys in RangeDeps), so the union is RelationMultiMap.linearUnion, not concatenation
+    ks, W = 5000, 64
+    s = generate_stream(12000, 6, ks, 0.99, 0.5, seed=35, range_frac=0.1, range_len_max=rl)
+    stores = []
+    try:
+        for lo, hi in even_split(ks, nstores):
+            st = CommandStore(device=0, key_lo=lo, key_hi=hi, window=W)
+            st.upload(s.restrict_keys(lo, hi))
+            st.compute()
+            stores.append(st)
+        with CommandStore(device=0, key_lo=0, key_hi=ks, window=W) as merger:
+            merger.merge(stores, txn_lo=0)
+            got = merger.download()
+    finally:
+        for st in stores:
+            st.close()
+    want = O.deps_fast(s, W)
+    assert got.first_difference(want) is None, got.first_difference(want)
+
+
+def test_exchange_merge_single_rank_ranges(gpu_device):
+    ks, W = 4000, 128
+    s = generate_stream(20000, 6, ks, 0.99, 0.5, seed=36, range_frac=0.1, range_len_max=300)
+    with CommandStore(device=0, key_lo=0, key_hi=ks, window=W) as st:
+        st.comm_init(1, 0, CommandStore.comm_unique_id())
+        st.upload(s)
+        st.compute()
+        st.exchange_merge(s.n)
+        got = st.download()
+    want = O.deps_fast(s, W)
+    assert got.first_difference(want) is None, got.first_difference(want)
+
+
 def test_store_subset_with_txn_index(gpu_device):
     # a store that only receives the txns intersecting its keys keeps global coordinates
     ks, W = 3000, 64

@@ -64,12 +64,44 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e), 0))
 
 
-def test_two_rank_shard_union_equals_full_deps():
+def _worker_ranges(rank, world, port, q):
+    """Range txns: each rank's partial is a whole PartialDeps (KeyDeps + RangeDeps); the owner
+    unions the parts it receives with Deps.merge (or_deps_union) -- what the device does through
+    accord_deps_union once the exchange carries both sides."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        s = generate_stream(N, 4, KS, 0.99, 0.5, seed=42, range_frac=0.15, range_len_max=120)
+        lo, hi = rank * KS // world, (rank + 1) * KS // world
+        part = O.deps_fast(s.restrict_keys(lo, hi), W)
+        parts = [None] * world
+        for src in range(world):
+            obj = [part] if src == rank else [None]
+            dist.broadcast_object_list(obj, src=src)
+            parts[src] = obj[0]
+        merged = O.deps_union(parts)
+        full = O.deps_fast(s, W)
+        a, b = rank * N // world, (rank + 1) * N // world
+        bad = 0
+        for t in range(a, b):
+            x, y = merged.key_deps(t), full.key_deps(t)
+            u, v = merged.range_deps(t), full.range_deps(t)
+            if not all(np.array_equal(np.asarray(i), np.asarray(j)) for i, j in zip(tuple(x) + tuple(u), tuple(y) + tuple(v))):
+                bad += 1
+        dist.destroy_process_group()
+        q.put((rank, bad, b - a))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), 0))
+
+
+@pytest.mark.parametrize("worker", [_worker, _worker_ranges], ids=["keys", "ranges"])
+def test_two_rank_shard_union_equals_full_deps(worker):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in range(world)]
