@@ -53,7 +53,7 @@ EXPORTED_SYMBOLS = [
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
     "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset", "accord_txn_register",
-    "accord_deps_visit",
+    "accord_deps_visit", "accord_deps_range_stab", "accord_range_stab_release",
 ]
 VISIT_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32)
 
@@ -117,6 +117,11 @@ class _WaitingOn(C.Structure):
     _fields_ = [("n", C.c_uint32), ("max_level", C.c_uint32), ("words_total", C.c_uint64),
                 ("preds_total", C.c_uint64), ("level", _u32p), ("wo_off", _u32p), ("words", _u64p),
                 ("owner", C.c_void_p)]
+
+
+class _RangeStab(C.Structure):
+    _fields_ = [("nq", C.c_uint32), ("reserved", C.c_uint32), ("total", C.c_uint64), ("off", _u32p),
+                ("txn", _u32p), ("owner", C.c_void_p)]
 
 
 class _Inverse(C.Structure):
@@ -198,6 +203,9 @@ def lib() -> C.CDLL:
         L.accord_deps_visit.argtypes = [C.POINTER(_Deps), C.c_uint32, VISIT_FN, C.c_void_p]
         L.accord_txn_register.argtypes = [C.c_void_p, C.c_uint32, _u64p, _u64p, _i32p, _u8p, _u64p, _u64p, _i32p]
         L.accord_max_conflicts_state.argtypes = [C.c_void_p, _u64p, _u64p, _i32p, _u8p]
+        L.accord_deps_range_stab.argtypes = [C.c_void_p, C.POINTER(_Deps), _u32p, _u32p, _u32p, C.POINTER(_RangeStab)]
+        L.accord_range_stab_release.argtypes = [C.POINTER(_RangeStab)]
+        L.accord_range_stab_release.restype = None
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
             if f.restype is C.c_int:  # default
@@ -722,6 +730,23 @@ class CommandStore:
                     _arr(w.rd_t2r_off, w.n + 1, np.uint32), _arr(w.rd_t2r, w.rd_total, np.int32))
         finally:
             lib().accord_deps_inverse_release(C.byref(w))
+
+    def range_stab(self, src: "CommandStore", q_off, q_start, q_end):
+        """SearchableRangeList stabbing of src's RangeDeps, built on the device: for each query
+        (q_start, q_end] of txn i (queries [q_off[i], q_off[i+1])), the txnIds of txn i's RangeDeps
+        ranges intersecting it, ascending (RangeDeps.forEach / computeTxnIds).  Returns
+        (off[nq+1], txns)."""
+        v = src._device_view_c()
+        qo = np.ascontiguousarray(q_off, dtype=np.uint32)
+        qs = np.ascontiguousarray(q_start, dtype=np.uint32)
+        qe = np.ascontiguousarray(q_end, dtype=np.uint32)
+        r = _RangeStab()
+        self._check(lib().accord_deps_range_stab(self._h, C.byref(v), qo.ctypes.data_as(_u32p),
+                                                 qs.ctypes.data_as(_u32p), qe.ctypes.data_as(_u32p), C.byref(r)))
+        try:
+            return _arr(r.off, r.nq + 1, np.uint32), _arr(r.txn, r.total, np.uint32)
+        finally:
+            lib().accord_range_stab_release(C.byref(r))
 
     def upload_deps(self, p: "PartialDeps"):
         """A host PartialDeps set becomes this store's current deps (e.g. replica replies)."""

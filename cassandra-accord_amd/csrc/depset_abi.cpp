@@ -368,6 +368,110 @@ int32_t accord_deps_upload(accord_store *s, const accord_deps *h)
     return ACCORD_OK;
 }
 
+struct StabOwner {
+    std::vector<uint32_t> off, v;
+};
+
+int32_t accord_deps_range_stab(accord_store *s, const accord_deps *src, const uint32_t *q_off, const uint32_t *q_start,
+                               const uint32_t *q_end, accord_range_stab *out)
+{
+    RC(check_views(s, 1, src));
+    if (!out || !q_off) return fail(s, ACCORD_ERR_ARG, "accord_deps_range_stab: null argument");
+    if (!src->rd_rng_off || !src->rd_val_off || !src->rd_r2v_off)
+        return fail(s, ACCORD_ERR_ARG, "accord_deps_range_stab: deps view without RangeDeps offsets");
+    const uint32_t n = src->n;
+    if (q_off[0] != 0) return fail(s, ACCORD_ERR_ARG, "query offsets must start at 0");
+    for (uint32_t i = 0; i < n; ++i)
+        if (q_off[i + 1] < q_off[i]) return fail(s, ACCORD_ERR_ARG, "query offsets decrease at txn %u", i);
+    const uint32_t nq = q_off[n];
+    if (nq && (!q_start || !q_end)) return fail(s, ACCORD_ERR_ARG, "queries without bounds");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    StabOwner *own = new (std::nothrow) StabOwner();
+    if (!own) return fail(s, ACCORD_ERR_OOM, "out of host memory");
+    struct Guard { StabOwner *&o; ~Guard() { delete o; } } guard{own};
+    op_begin(s);
+    hipStream_t st = s->stream;
+    DevBuf *T = s->op_tmp;
+    const size_t n1 = (size_t)n + 1, q1 = (size_t)nq + 1;
+    HIPCHECK(s, T[T_VLEN].ensure(n1 * 4)); HIPCHECK(s, T[T_KLEN].ensure(q1 * 4)); HIPCHECK(s, T[T_BLEN].ensure(q1 * 4));
+    HIPCHECK(s, T[T_VEOFF].ensure(q1 * 4)); HIPCHECK(s, T[T_KEOFF].ensure(n1 * 4)); HIPCHECK(s, T[T_BEOFF].ensure(n1 * 4));
+    HIPCHECK(s, T[T_KLST].ensure(q1 * 4)); HIPCHECK(s, T[T_CNTV].ensure(q1 * 4));
+    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    HIPCHECK(s, hipMemsetAsync(dev, 0xFF, sizeof(HostTotals), st));
+    HIPCHECK(s, hipMemsetAsync(&dev->status.overflow, 0, sizeof(uint32_t), st));
+    HIPCHECK(s, hipMemcpyAsync(T[T_VLEN].p, q_off, n1 * 4, hipMemcpyHostToDevice, st));
+    if (nq) {
+        HIPCHECK(s, hipMemcpyAsync(T[T_KLEN].p, q_start, (size_t)nq * 4, hipMemcpyHostToDevice, st));
+        HIPCHECK(s, hipMemcpyAsync(T[T_BLEN].p, q_end, (size_t)nq * 4, hipMemcpyHostToDevice, st));
+    }
+    accord::RangeIndexParams p{};
+    p.n = n;
+    p.rng_off = src->rd_rng_off; p.rs = src->rd_rng_start; p.re = src->rd_rng_end;
+    p.val_off = src->rd_val_off; p.vals = src->rd_vals; p.r2v_off = src->rd_r2v_off; p.r2v = src->rd_r2v;
+    p.status = &dev->status;
+    // 1. checkpoints per txn, their offsets
+    HIPCHECK(s, hipMemsetAsync(T[T_KEOFF].p, 0, n1 * 4, st));
+    p.chk_cnt = T[T_KEOFF].as<uint32_t>();
+    accord::launch_ri_chk_count(p, st);
+    Scans sc;
+    RC(scans_init(s, sc));
+    RC(sc.add(p.chk_cnt, T[T_BEOFF].as<uint32_t>(), n + 1));
+    unsigned long long tot[1];
+    RC(sc.read(tot));
+    const uint64_t nchk = tot[0];
+    if (nchk >= (1ull << 31)) return fail(s, ACCORD_ERR_CAPACITY, "range index: %llu checkpoints", (unsigned long long)nchk);
+    p.chk_off = T[T_BEOFF].as<uint32_t>();
+    // 2. checkpoint lists: sizes, offsets, contents
+    HIPCHECK(s, T[T_VOWN].ensure((nchk + 1) * 4)); HIPCHECK(s, T[T_VLST].ensure((nchk + 1) * 4));
+    HIPCHECK(s, hipMemsetAsync(T[T_VOWN].p, 0, (nchk + 1) * 4, st));
+    p.list_cnt = T[T_VOWN].as<uint32_t>();
+    accord::launch_ri_lists(p, (uint32_t)nchk, false, st);
+    RC(sc.add(p.list_cnt, T[T_VLST].as<uint32_t>(), (uint32_t)nchk + 1));
+    RC(sc.read(tot));
+    const uint64_t L = tot[0];
+    if (L >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "range index: %llu checkpoint entries", (unsigned long long)L);
+    HIPCHECK(s, T[T_KOWN].ensure(L * 4 + 4));
+    p.list_off = T[T_VLST].as<uint32_t>(); p.lists = T[T_KOWN].as<uint32_t>();
+    accord::launch_ri_lists(p, (uint32_t)nchk, true, st);
+    // 3. stab: per query |txnIds|, offsets, the txnIds
+    accord::launch_ri_qtxn(n, T[T_VLEN].as<uint32_t>(), T[T_VEOFF].as<uint32_t>(), st);
+    HIPCHECK(s, hipMemsetAsync(T[T_KLST].p, 0, q1 * 4, st));
+    p.nq = nq; p.q_txn = T[T_VEOFF].as<uint32_t>(); p.q_s = T[T_KLEN].as<uint32_t>(); p.q_e = T[T_BLEN].as<uint32_t>();
+    p.out_cnt = T[T_KLST].as<uint32_t>();
+    accord::launch_ri_stab(p, false, st);
+    RC(sc.add(p.out_cnt, T[T_CNTV].as<uint32_t>(), nq + 1));
+    RC(sc.read(tot));
+    const uint64_t total = tot[0];
+    HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    if (s->pinned->status.overflow)
+        return fail(s, ACCORD_ERR_CAPACITY, "range stab: txn %u has more than %u RangeDeps ranges or %u txnIds",
+                    s->pinned->status.overflow_first, accord::RI_MAX_RANGES, accord::RI_UMAX);
+    HIPCHECK(s, T[T_CNTK].ensure(total * 4 + 4));
+    p.out_off = T[T_CNTV].as<uint32_t>(); p.out = T[T_CNTK].as<uint32_t>();
+    accord::launch_ri_stab(p, true, st);
+    HIPCHECK(s, hipGetLastError());
+    try { own->off.resize(q1); own->v.resize(total + 1); } catch (...) { return fail(s, ACCORD_ERR_OOM, "out of host memory"); }
+    HIPCHECK(s, hipMemcpyAsync(own->off.data(), p.out_off, q1 * 4, hipMemcpyDeviceToHost, st));
+    if (total) HIPCHECK(s, hipMemcpyAsync(own->v.data(), p.out, total * 4, hipMemcpyDeviceToHost, st));
+    RC(op_end(s));
+    out->nq = nq;
+    out->total = total;
+    out->off = own->off.data();
+    out->txn = own->v.data();
+    out->owner = own;
+    own = nullptr;          // released by accord_range_stab_release
+    return ACCORD_OK;
+}
+
+void accord_range_stab_release(accord_range_stab *r)
+{
+    if (!r) return;
+    delete (StabOwner *)r->owner;
+    std::memset(r, 0, sizeof(*r));
+}
+
 void accord_deps_inverse_release(accord_deps_inverse *inv)
 {
     if (!inv) return;

@@ -219,6 +219,31 @@ void launch_expand_offsets(uint32_t n, uint32_t n_total, const uint32_t *txn_ind
 void launch_boundaries(uint32_t G, uint32_t n_total, uint32_t *const exp_off[3], uint32_t *bnd, hipStream_t s);
 void launch_merge_fill(const MergeParams &p, hipStream_t s);
 
+// ---- SearchableRangeList stabbing of RangeDeps (rangeindex.hip) ----
+constexpr uint32_t RI_C = 16;                  // ranges per checkpoint block
+constexpr uint32_t RI_UMAX = 32768;            // RangeDeps txnIds of one txn the LDS bitmap holds
+constexpr uint32_t RI_MAX_RANGES = 1u << 16;   // RangeDeps ranges of one txn the index covers
+struct RangeIndexParams {
+    uint32_t n;
+    const uint32_t *rng_off, *rs, *re, *val_off, *vals, *r2v_off;
+    const int32_t *r2v;
+    uint32_t *chk_cnt;                         // [n] checkpoints per txn (scanned into chk_off)
+    const uint32_t *chk_off;                   // [n + 1]
+    uint32_t *list_cnt;                        // [nchk] list sizes (scanned into list_off)
+    const uint32_t *list_off;                  // [nchk + 1]
+    uint32_t *lists;
+    uint32_t nq;
+    const uint32_t *q_txn, *q_s, *q_e;         // queries (qs, qe] of txn q_txn
+    uint32_t *out_cnt;
+    const uint32_t *out_off;
+    uint32_t *out;
+    DevStatus *status;
+};
+void launch_ri_chk_count(const RangeIndexParams &p, hipStream_t s);
+void launch_ri_lists(const RangeIndexParams &p, uint32_t nchk, bool fill, hipStream_t s);
+void launch_ri_qtxn(uint32_t n, const uint32_t *q_off, uint32_t *q_txn, hipStream_t s);
+void launch_ri_stab(const RangeIndexParams &p, bool fill, hipStream_t s);
+
 // ---- deps-set operations: union / slice / invert (depset.hip) ----
 // One side (KeyDeps: lo = key ordinals, hi unused; RangeDeps: ranges (lo, hi]) of G device deps
 // sets, as device pointer tables indexed by part.  Offsets may start anywhere (element g of a

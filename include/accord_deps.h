@@ -260,6 +260,27 @@ typedef struct {
 
 int32_t accord_deps_invert(accord_store *store, const accord_deps *src, accord_deps_inverse *out);
 void    accord_deps_inverse_release(accord_deps_inverse *inv);
+/* accord_deps_range_stab: SearchableRangeList over every txn's RangeDeps (RangeDeps.ensureSearchable,
+ *   primitives/RangeDeps.java:709-720; SearchableRangeList.build, utils/SearchableRangeList.java:79-133)
+ *   built on the device, then for each query of txn i -- queries [q_off[i], q_off[i+1]), each
+ *   (q_start, q_end] (a key k is (k-1, k]), host arrays -- the txnIds of txn i's RangeDeps ranges
+ *   intersecting it, ascending unique (RangeDeps.forEach(range) / computeTxnIds(key),
+ *   primitives/RangeDeps.java:158-189; CheckpointIntervalArray.forEach, utils/CheckpointIntervalArray.java:
+ *   100-221).  txn values are src's rd_vals entries (stream positions).  A txn with more than 65536
+ *   RangeDeps ranges or 32768 RangeDeps txnIds is ACCORD_ERR_CAPACITY.  Result in library-owned
+ *   host memory: off[nq+1], txn[total]. */
+typedef struct {
+    uint32_t  nq;
+    uint32_t  reserved;
+    uint64_t  total;
+    uint32_t *off;
+    uint32_t *txn;
+    void     *owner;            /* library-private */
+} accord_range_stab;
+int32_t accord_deps_range_stab(accord_store *store, const accord_deps *src, const uint32_t *q_off,
+                               const uint32_t *q_start, const uint32_t *q_end, accord_range_stab *out);
+void    accord_range_stab_release(accord_range_stab *r);
+
 /* device ms of the last union / slice / invert (ACCORD_STORE_PROFILE stores, else 0) */
 int32_t accord_ops_timing(accord_store *store, float *ms);
 
