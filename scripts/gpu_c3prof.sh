@@ -5,7 +5,7 @@ TAG=${TAG:-c3}; O="$R/gpurun_out/$TAG"; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --config 3 --steps 3 --warmup 1 --no-cpu > "$O/prof.log" 2>&1
 rc=$?
-python3 - "$O/prof/run_kernel_stats.csv" <<'PY'
+python3 - "$(find "$O/prof" -name '*kernel_stats.csv' | head -n 1)" <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 for r in rows[:25]:
