@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--write-frac", type=float, default=None)
     ap.add_argument("--cpu-sample", type=int, default=None, help="txns of the CPU-baseline prefix sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--resident", action="store_true",
+                    help="also time the stream fed as 8 batches to one resident store (resident_batches); "
+                         "off by default so a kernel trace of the default run holds one batch size only")
     args = ap.parse_args()
     preset = PRESETS[args.config]
     for k, v in preset.items():
@@ -197,7 +200,7 @@ def main():
     resident = None
     if world == 1 and not args.waiting_on:
         boundary = boundary_rate(store, s)
-        if s.rng_off[-1] == 0:
+        if s.rng_off[-1] == 0 and args.resident:
             resident = resident_split(s, args, stage["total"])
 
     if rank != 0:

@@ -8,6 +8,7 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > "$O/bench.json" 2> "$O/bench.err" && \
 timeout -k 10 300 python bench.py --config 5 --steps 3 --warmup 1 > "$O/bench_c5.json" 2> "$O/bench_c5.err" && \
 timeout -k 10 300 python bench.py --config 3 --steps 5 --warmup 2 --no-cpu > "$O/bench_c3.json" 2> "$O/bench_c3.err" && \
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --resident > "$O/bench_resident.json" 2> "$O/bench_resident.err" && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu > "$O/prof_trace.log" 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_trace_c5" -o run --output-format csv -- python3 "$R/bench.py" --config 5 --steps 2 --warmup 1 --no-cpu > "$O/prof_trace_c5.log" 2>&1 && \
