@@ -167,6 +167,11 @@ struct RangeDepsParams {
     uint32_t n_range_txns;
     const uint32_t *range_txns;
     const uint32_t *bound_l;            // Accept batch: txns started before executeAt (nullptr = i)
+    // resident stores: txn i of the batch is stream position g0 + i; the range commands carried
+    // from earlier batches (owner positions ascending, all before g0) precede the batch's own in
+    // the candidate order; checkpoints cover txn blocks [cp_base, cp_base + ncp)
+    uint32_t g0, ncr, cp_base;
+    const uint32_t *rc_owner, *rc_start, *rc_end, *rc_kind;
     // RangeDeps counts / outputs
     uint32_t *cnt_rngs, *cnt_vals, *cnt_r2v;
     const uint32_t *rd_rng_off, *rd_val_off, *rd_r2v_off;
@@ -185,8 +190,13 @@ void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s);
 // filled with dep txn indices, then per txn the sorted unique txnIds (into kd_vals at the txnIds
 // upper-bound offsets) and the body rewritten to ranks.
 constexpr uint32_t RK_CP_SHIFT = 12;
-size_t rangekeys_cp_bytes(uint32_t n, uint32_t nkeys);
-void launch_rangekeys_checkpoints(uint32_t P, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s);
+size_t rangekeys_cp_bytes(uint32_t ncp, uint32_t nkeys);
+void launch_rangekeys_checkpoints(uint32_t PH, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s);
+// resident stores: the range commands a later batch can still see (owner >= thr), carried and this
+// batch's, into the out arrays (a suffix of the candidate order); *kept = their number
+void launch_range_carry(const RangeDepsParams &p, uint32_t R, uint32_t thr, uint32_t *out_owner, uint32_t *out_start,
+                        uint32_t *out_end, uint32_t *out_kind, uint32_t *first_tmp, unsigned long long *kept,
+                        hipStream_t s);
 // keys of every range txn's ranges (clipped to the store), for the stored-slice offsets
 void launch_rangekeys_nkeys(const RangeDepsParams &p, uint32_t *cnt, hipStream_t s);
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s);

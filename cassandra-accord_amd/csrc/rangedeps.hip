@@ -75,9 +75,22 @@ __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p
         const bool key_query = (lsb_i & 1) == 0;
         const uint32_t q0 = key_query ? p.key_off[i] : p.rng_off[i];
         const uint32_t q1 = key_query ? p.key_off[i + 1] : p.rng_off[i + 1];
-        // live range commands: started in the window and before the bound (i; Accept: executeAt)
-        const uint32_t r_lo = p.rng_off[i > p.window ? i - p.window : 0];
-        const uint32_t r_hi = p.rng_off[p.bound_l ? p.bound_l[i] : i];
+        // live range commands: started in the window and before the bound (i; Accept: executeAt).
+        // Candidate index space: the ncr carried commands (resident stores), then the batch's.
+        const uint32_t g = p.g0 + i;
+        const uint32_t lo_g = g > p.window ? g - p.window : 0u;
+        uint32_t r_lo;
+        if (lo_g >= p.g0) {
+            r_lo = p.ncr + p.rng_off[lo_g - p.g0];
+        } else {
+            uint32_t l = 0, h = p.ncr;                   // first carried command with owner >= lo_g
+            while (l < h) {
+                const uint32_t m = (l + h) >> 1;
+                if (p.rc_owner[m] < lo_g) l = m + 1; else h = m;
+            }
+            r_lo = l;
+        }
+        const uint32_t r_hi = p.ncr + p.rng_off[p.bound_l ? p.bound_l[i] : i];
         uint32_t H = 0;
         // up to 8 query keys / ranges: held wave-uniform, every candidate tested by compares
         const uint32_t nq = q1 - q0;
@@ -97,10 +110,15 @@ __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p
                 const uint32_t r = r0 + lane;
                 bool hit = false;
                 uint32_t j = 0, s = 0, e = 0;
+                uint32_t jkind = 0;
                 if (r < r_hi) {
-                    j = p.rng_owner[r];
-                    s = p.rng_start[r];
-                    e = p.rng_end[r];
+                    if (r < p.ncr) {
+                        j = p.rc_owner[r]; s = p.rc_start[r]; e = p.rc_end[r]; jkind = p.rc_kind[r];
+                    } else {
+                        const uint32_t rb = r - p.ncr, jl = p.rng_owner[rb];
+                        j = p.g0 + jl; s = p.rng_start[rb]; e = p.rng_end[rb];
+                        jkind = (uint32_t)(p.lsb[jl] >> 1) & 7;
+                    }
                     bool inter = false;
                     if (few) {
 #pragma unroll
@@ -110,7 +128,7 @@ __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p
                     } else {
                         inter = rd_hits(p, s, e, key_query, q0, q1);
                     }
-                    hit = inter && j != i && ((wmask >> ((uint32_t)(p.lsb[j] >> 1) & 7)) & 1u);   // p1
+                    hit = inter && j != g && ((wmask >> jkind) & 1u);   // p1
                 }
                 const uint64_t bal = __ballot(hit);
                 const uint32_t h = H + (uint32_t)__popcll(bal & lt);
@@ -214,15 +232,18 @@ __global__ __launch_bounds__(256) void rk_checkpoint_kernel(uint32_t P, const ui
         const uint32_t k = sorted_key[x];
         const uint32_t a = p.seg_start[k], c = p.seg_end[k];
         const uint32_t t = p.hist[x] & ENT_TXN_MASK;
-        const uint32_t b_lo = x == a ? 0u : ((p.hist[x - 1] & ENT_TXN_MASK) >> RK_CP_SHIFT) + 1u;
-        const uint32_t b_hi = min(t >> RK_CP_SHIFT, p.ncp - 1u);
+        // absolute txn blocks [cp_base, cp_base + ncp) live in the table
+        const uint32_t b_end = p.cp_base + p.ncp;
+        const uint32_t b_lo = max(p.cp_base, x == a ? 0u : ((p.hist[x - 1] & ENT_TXN_MASK) >> RK_CP_SHIFT) + 1u);
+        const uint32_t b_hi = min(t >> RK_CP_SHIFT, b_end - 1u);
         if (b_lo <= b_hi) {
             const uint4 v = make_uint4(x, t, rk_pw_before(p, x), 0u);
-            for (uint32_t b = b_lo; b <= b_hi; ++b) p.cp[(size_t)b * p.nkeys + k] = v;
+            for (uint32_t b = b_lo; b <= b_hi; ++b) p.cp[(size_t)(b - p.cp_base) * p.nkeys + k] = v;
         }
-        if (x + 1 == c && (t >> RK_CP_SHIFT) + 1u < p.ncp) {
+        if (x + 1 == c && (t >> RK_CP_SHIFT) + 1u < b_end) {
             const uint4 v = make_uint4(c, 0xFFFFFFFFu, rk_pw_before(p, c), 0u);
-            for (uint32_t b = (t >> RK_CP_SHIFT) + 1u; b < p.ncp; ++b) p.cp[(size_t)b * p.nkeys + k] = v;
+            for (uint32_t b = max(p.cp_base, (t >> RK_CP_SHIFT) + 1u); b < b_end; ++b)
+                p.cp[(size_t)(b - p.cp_base) * p.nkeys + k] = v;
         }
     }
 }
@@ -262,12 +283,14 @@ template <int U>
 __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, const uint32_t (&kk)[U],
                                           const bool (&valid)[U], uint32_t wmask, RkSlice (&out)[U])
 {
-    const bool windowed = i > p.window;
-    const uint32_t thr = windowed ? i - p.window : 0u;
-    // slices end at the first entry with txn >= eb (i; Accept: the txns started before executeAt)
-    const uint32_t eb = p.bound_l ? p.bound_l[i] : i;
-    const bool past = (eb >> RK_CP_SHIFT) >= p.ncp;     // eb == n on a block boundary: whole segment
-    const size_t row1 = (size_t)(past ? 0u : eb >> RK_CP_SHIFT) * p.nkeys, row2 = (size_t)(thr >> RK_CP_SHIFT) * p.nkeys;
+    const uint32_t g = p.g0 + i;                    // stream position (history entries hold them)
+    const bool windowed = g > p.window;
+    const uint32_t thr = windowed ? g - p.window : 0u;
+    // slices end at the first entry with txn >= eb (g; Accept: the txns started before executeAt)
+    const uint32_t eb = p.bound_l ? p.g0 + p.bound_l[i] : g;
+    const bool past = (eb >> RK_CP_SHIFT) >= p.cp_base + p.ncp;   // eb on the last block boundary: whole segment
+    const size_t row1 = (size_t)(past ? 0u : (eb >> RK_CP_SHIFT) - p.cp_base) * p.nkeys,
+                 row2 = (size_t)((thr >> RK_CP_SHIFT) - p.cp_base) * p.nkeys;
     uint32_t a[U], c[U];
     uint4 e1[U], e2[U];
 #pragma unroll
@@ -594,18 +617,62 @@ void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s)
     hipLaunchKernelGGL((rangedeps_kernel<true, RD_HCAP_BIG, 1, true>), dim3(256), dim3(64), 0, s, p);
 }
 
-size_t rangekeys_cp_bytes(uint32_t n, uint32_t nkeys)
+size_t rangekeys_cp_bytes(uint32_t ncp, uint32_t nkeys)
 {
-    const size_t ncp = n ? ((size_t)(n - 1) >> RK_CP_SHIFT) + 1 : 1;
-    return ncp * nkeys * sizeof(uint4) + 64;
+    return (size_t)ncp * nkeys * sizeof(uint4) + 64;
 }
 
-void launch_rangekeys_checkpoints(uint32_t P, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s)
+void launch_rangekeys_checkpoints(uint32_t PH, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s)
 {
-    if (p.n_range_txns == 0 || P == 0) return;
-    uint32_t blocks = (P + 255) / 256;
+    if (p.n_range_txns == 0 || PH == 0) return;
+    uint32_t blocks = (PH + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(rk_checkpoint_kernel, dim3(blocks), dim3(256), 0, s, P, sorted_key, p);
+    hipLaunchKernelGGL(rk_checkpoint_kernel, dim3(blocks), dim3(256), 0, s, PH, sorted_key, p);
+}
+
+namespace {
+
+// first candidate (carried, then the batch's) whose owner >= thr: owners ascend along the order
+__global__ void rc_first_kernel(RangeDepsParams p, uint32_t R, uint32_t thr, uint32_t *first,
+                                unsigned long long *kept)
+{
+    uint32_t l = 0, h = p.ncr + R;
+    while (l < h) {
+        const uint32_t m = (l + h) >> 1;
+        const uint32_t o = m < p.ncr ? p.rc_owner[m] : p.g0 + p.rng_owner[m - p.ncr];
+        if (o < thr) l = m + 1; else h = m;
+    }
+    first[0] = l;
+    *kept = p.ncr + R - l;
+}
+
+__global__ __launch_bounds__(256) void rc_copy_kernel(RangeDepsParams p, uint32_t R, const uint32_t *__restrict__ first,
+                                                      uint32_t *__restrict__ oo, uint32_t *__restrict__ os,
+                                                      uint32_t *__restrict__ oe, uint32_t *__restrict__ ok)
+{
+    const uint32_t f = first[0], tot = p.ncr + R;
+    for (uint32_t e = f + blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
+        uint32_t o, s, en, k;
+        if (e < p.ncr) { o = p.rc_owner[e]; s = p.rc_start[e]; en = p.rc_end[e]; k = p.rc_kind[e]; }
+        else {
+            const uint32_t r = e - p.ncr, jl = p.rng_owner[r];
+            o = p.g0 + jl; s = p.rng_start[r]; en = p.rng_end[r]; k = (uint32_t)(p.lsb[jl] >> 1) & 7;
+        }
+        oo[e - f] = o; os[e - f] = s; oe[e - f] = en; ok[e - f] = k;
+    }
+}
+
+} // namespace
+
+void launch_range_carry(const RangeDepsParams &p, uint32_t R, uint32_t thr, uint32_t *out_owner, uint32_t *out_start,
+                        uint32_t *out_end, uint32_t *out_kind, uint32_t *first_tmp, unsigned long long *kept,
+                        hipStream_t s)
+{
+    hipLaunchKernelGGL(rc_first_kernel, dim3(1), dim3(1), 0, s, p, R, thr, first_tmp, kept);
+    uint32_t blocks = (p.ncr + R + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(rc_copy_kernel, dim3(blocks), dim3(256), 0, s, p, R, first_tmp, out_owner, out_start, out_end, out_kind);
 }
 
 static uint32_t rk_blocks(uint32_t nrt)

@@ -111,7 +111,9 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
                       &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
-                      &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2};
+                      &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2,
+                      &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
+                      &s->rc_end2, &s->rc_kind2, &s->rc_first};
     accord_impl::shard_comm_destroy(s);
     accord_impl::pinned_arena_destroy(s);
     for (DevBuf *b : bufs) b->release();
@@ -152,8 +154,8 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     for (uint32_t i = 0; i < n; ++i) nrt += (uint32_t)(b->lsb[i] & 1);
     if (b->txn_index && nrt)
         return fail(s, ACCORD_ERR_ARG, "txn_index (store subset of a stream) is supported for key txns only");
-    if (s->resident && nrt)
-        return fail(s, ACCORD_ERR_STATE, "range txns in a resident store are not supported by this build");
+    if (nrt && accord_impl::registered_mode(s))
+        return fail(s, ACCORD_ERR_STATE, "range txns in a registered-status store (ACCORD_WINDOW_NONE) are not supported by this build");
     s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt;
     s->rk_keys_total = 0;                // sizes the range txns' stored key slices
     if (nrt && b->rng_off)
@@ -286,7 +288,10 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->range_txns.ensure((size_t)nrt * 4 + 4));
 
     HIPCHECK(s, s->fk_list.ensure((size_t)n * 4 + 64));
-    if (R) HIPCHECK(s, s->rd_big.ensure((size_t)n * 4 + 64));
+    // RangeDeps for the batch: its own range commands and, in a resident store, the carried ones
+    const uint32_t ncr = s->resident ? s->rc_n : 0u;
+    const bool rdeps = R || ncr;
+    if (rdeps) HIPCHECK(s, s->rd_big.ensure((size_t)n * 4 + 64));
 
     HostTotals *dev = s->status_totals.as<HostTotals>();
     record(s, EV_START);
@@ -298,7 +303,7 @@ int32_t accord_deps_compute(accord_store *s)
         fl.add(s->seg_start.p, (size_t)nkeys * 4, 0u);
         fl.add(s->seg_end.p, (size_t)nkeys * 4, 0u);
         fl.add(s->fk_list.p, 4, 0u);                                   // fallback list count
-        if (R) {
+        if (rdeps) {
             fl.add(s->rd_big.p, 4, 0u);                                 // big range-hit list count
         } else {
             fl.add(s->rd_rng_off.p, n1 * 4, 0u);
@@ -384,10 +389,16 @@ int32_t accord_deps_compute(accord_store *s)
         rp.c_local = hv.c_local; rp.ccarry = hv.ccarry;
     }
     rp.nkeys = nkeys;
-    rp.ncp = n ? ((n - 1) >> accord::RK_CP_SHIFT) + 1 : 1;
+    // resident stores: txn i is stream position g0 + i; the checkpoint blocks span every window
+    rp.g0 = s->resident ? s->next_global : 0u;
+    rp.ncr = ncr;
+    rp.rc_owner = s->rc_owner.as<uint32_t>(); rp.rc_start = s->rc_start.as<uint32_t>();
+    rp.rc_end = s->rc_end.as<uint32_t>(); rp.rc_kind = s->rc_kind.as<uint32_t>();
+    rp.cp_base = (rp.g0 > s->cfg.window ? rp.g0 - s->cfg.window : 0u) >> accord::RK_CP_SHIFT;
+    rp.ncp = n ? ((rp.g0 + n - 1) >> accord::RK_CP_SHIFT) - rp.cp_base + 1 : 1;
     rp.cnt_vals_exact = s->cnt_vals.as<uint32_t>();
     if (nrt) {
-        HIPCHECK(s, s->rk_cp.ensure(accord::rangekeys_cp_bytes(n, nkeys)));
+        HIPCHECK(s, s->rk_cp.ensure(accord::rangekeys_cp_bytes(rp.ncp, nkeys)));
         HIPCHECK(s, s->rk_cnt.ensure((size_t)nrt * 4 + 4));
         HIPCHECK(s, s->rk_off.ensure(((size_t)nrt + 1) * 4));
         HIPCHECK(s, s->rk_slices.ensure(s->rk_keys_total * 8 + 8));
@@ -403,7 +414,7 @@ int32_t accord_deps_compute(accord_store *s)
 
     // sizes: key txns from the per-pair witnessed counts, range txns by their own count pass
     if (nrt) {
-        accord::launch_rangekeys_checkpoints(P, s->sort_key.as<uint32_t>(), rp, st);
+        accord::launch_rangekeys_checkpoints(PH, s->sort_key.as<uint32_t>(), rp, st);
         accord::launch_rangekeys_nkeys(rp, s->rk_cnt.as<uint32_t>(), st);
         accord::exclusive_scan_u32(s->rk_cnt.as<uint32_t>(), s->rk_off.as<uint32_t>(), nrt, &dev->totals[6],
                                    s->scan_tmp.p, st);
@@ -411,7 +422,7 @@ int32_t accord_deps_compute(accord_store *s)
     accord::launch_keydeps_sizes(n, kp.key_off, kp.slice, rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
                                  rp.cnt_k2v, &dev->status, st);
     if (nrt) accord::launch_rangekeys_count(rp, st);
-    if (R) {
+    if (rdeps) {
         rp.rd_big_count = s->rd_big.as<uint32_t>();
         rp.rd_big_list = rp.rd_big_count + 16;
         accord::launch_rangedeps_count(rp, st);
@@ -423,7 +434,7 @@ int32_t accord_deps_compute(accord_store *s)
         unsigned long long *tot[3] = {&dev->totals[0], &dev->totals[1], &dev->totals[2]};
         accord::exclusive_scan_multi(3, in, out, tot, n, s->scan_tmp.p, st);
     }
-    if (R) {
+    if (rdeps) {
         const uint32_t *in[3] = {rp.cnt_rngs, rp.cnt_vals, rp.cnt_r2v};
         uint32_t *out[3] = {s->rd_rng_off.as<uint32_t>(), s->rd_val_off.as<uint32_t>(), s->rd_r2v_off.as<uint32_t>()};
         unsigned long long *tot[3] = {&dev->totals[3], &dev->totals[4], &dev->totals[5]};
@@ -481,7 +492,7 @@ int32_t accord_deps_compute(accord_store *s)
         accord::launch_rangekeys_fill(rp, st);
         accord::launch_rangekeys_union(rp, st);
     }
-    if (R) accord::launch_rangedeps_fill(rp, st);
+    if (rdeps) accord::launch_rangedeps_fill(rp, st);
     record(s, EV_RANGE);
     accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[7], s->scan_tmp.p, st);
     HIPCHECK(s, s->cv_tmp.ensure(accord::compact_temp_bytes(vub_total)));
@@ -499,6 +510,15 @@ int32_t accord_deps_compute(accord_store *s)
                              s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(),
                              accord::history_views(s->hist_tmp.p, PH), s->carry_tmp.p, s->scan_tmp.p, s->cy_key2.as<uint32_t>(),
                              s->cy_ent2.as<uint32_t>(), &dev->totals[8], reg, st);
+        if (rdeps) {    // the range commands the next batch's window can still reach
+            const size_t cap = (size_t)ncr + R + 1;
+            HIPCHECK(s, s->rc_owner2.ensure(cap * 4)); HIPCHECK(s, s->rc_start2.ensure(cap * 4));
+            HIPCHECK(s, s->rc_end2.ensure(cap * 4)); HIPCHECK(s, s->rc_kind2.ensure(cap * 4));
+            HIPCHECK(s, s->rc_first.ensure(16));
+            accord::launch_range_carry(rp, R, thr, s->rc_owner2.as<uint32_t>(), s->rc_start2.as<uint32_t>(),
+                                       s->rc_end2.as<uint32_t>(), s->rc_kind2.as<uint32_t>(),
+                                       s->rc_first.as<uint32_t>(), &dev->totals[9], st);
+        }
     }
     record(s, EV_COMPACT);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
@@ -517,6 +537,11 @@ int32_t accord_deps_compute(accord_store *s)
         std::swap(s->cy_key, s->cy_key2);
         std::swap(s->cy_ent, s->cy_ent2);
         s->carry_n = (uint32_t)s->pinned->totals[8];
+        if (rdeps) {
+            std::swap(s->rc_owner, s->rc_owner2); std::swap(s->rc_start, s->rc_start2);
+            std::swap(s->rc_end, s->rc_end2); std::swap(s->rc_kind, s->rc_kind2);
+            s->rc_n = (uint32_t)s->pinned->totals[9];
+        }
         s->next_global = s->b_end;
         if (n) {
             s->has_prev = true;
@@ -561,7 +586,7 @@ int32_t accord_store_state(accord_store *s, accord_store_state_info *info)
 int32_t accord_store_reset(accord_store *s)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
-    s->next_global = 0; s->carry_n = 0; s->has_prev = false;
+    s->next_global = 0; s->carry_n = 0; s->rc_n = 0; s->has_prev = false;
     s->rg_tx_n = 0; s->rg_known = 0;
     s->prev_msb = s->prev_lsb = 0; s->prev_node = 0;
     s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->wo_done = false;

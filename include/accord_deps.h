@@ -136,7 +136,10 @@ void       *accord_store_stream(accord_store *store);        /* the store's hipS
  * entries a later txn can reach (CommandsForKey.txns from the last Write before the window on;
  * older entries are pruned for good, as committed entries below maxCommittedBefore are,
  * local/CommandsForKey.java:620-645,1654-1684).  A rejected batch leaves the state unchanged.
- * Key txns only in this build (a range txn in a resident store: ACCORD_ERR_STATE). */
+ * Range txns: the store also keeps the range commands a later txn's window can reach (owner
+ * position >= next_global - W; the range-command scan of impl/InMemoryCommandStore.java:883-1016
+ * over the commands still live), so RangeDeps and the range txns' KeyDeps continue across batches
+ * too.  A registered-status store (ACCORD_WINDOW_NONE) rejects range txns (ACCORD_ERR_STATE). */
 /* Real status events (SURVEY.md §8b accord_txn_register): a resident store created with window
  * ACCORD_WINDOW_NONE has no status-at-time model -- every txn enters its keys' CommandsForKey
  * PREACCEPTED when its batch is computed (CommandsForKey.insert, local/CommandsForKey.java:880-944)

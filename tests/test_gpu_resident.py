@@ -112,3 +112,73 @@ def test_config2_full_in_8_batches(gpu_device):
     assert got.first_difference(one) is None
     assert got.first_difference(O.deps_fast(s, W)) is None
     assert state["carry_entries"] < n                           # far less than the 8.4 M history pairs
+
+
+# range txns in a resident store: the range commands a later batch's window can still reach travel
+# with the key history (owner positions >= next_global - W), so RangeDeps and the range txns'
+# KeyDeps of every batch equal the single-batch run over the whole stream
+RANGE_CASES = [
+    # n, k, keyspace, zipf, write_frac, range_frac, range_len_max, W, seed, parts
+    (6000, 4, 2000, 0.99, 0.5, 0.2, 200, 256, 31, 8),
+    (8000, 3, 500, 0.0, 0.3, 0.1, 60, 64, 32, 23),
+    (5000, 2, 3000, 0.99, 0.5, 0.05, 1500, 3000, 33, 11),     # window spans most batches
+    (6000, 4, 1000, 0.99, 0.5, 0.3, 100, 0, 34, 6),           # W = 0: nothing carries
+    (4000, 4, 800, 0.99, 0.5, 0.02, 300, 512, 35, 80),        # short batches, most without ranges
+    (9000, 4, 20000, 0.99, 0.5, 0.15, 400, 4500, 36, 5),      # windows span checkpoint blocks
+]
+
+
+@pytest.mark.parametrize("case", RANGE_CASES, ids=[f"r{i}" for i in range(len(RANGE_CASES))])
+def test_range_batches_equal_single(gpu_device, case):
+    n, k, ks, z, wf, rf, rl, W, seed, parts = case
+    s = generate_stream(n, k, ks, z, wf, range_frac=rf, range_len_max=rl, seed=seed)
+    assert int(s.rng_off[-1]) > 0
+    pts = split_points(n, parts, seed)
+    got, state = run_batches(s, ks, W, pts)
+    assert state["next_global"] == n
+    one = single(s, ks, W)
+    assert got.first_difference(one) is None
+    assert got.first_difference(O.deps_fast(s, W)) is None
+
+
+def test_range_accept_batches(gpu_device):
+    n, ks, W = 6000, 600, 128
+    s = generate_stream(n, 4, ks, 0.99, 0.5, range_frac=0.15, range_len_max=80, seed=37)
+    s = s.accept(frac=0.5, max_delay=200, seed=37)
+    pts = split_points(n, 7, 37)
+    got, _ = run_batches(s, ks, W, pts)
+    ends = O.batch_ends(np.diff(pts))
+    assert got.first_difference(O.deps_fast(s, W, batch_end=ends)) is None
+
+
+def test_range_carry_resets(gpu_device):
+    s = generate_stream(4000, 4, 500, 0.99, 0.5, range_frac=0.2, range_len_max=100, seed=38)
+    with CommandStore(device=0, key_lo=0, key_hi=500, window=300, resident=True) as st:
+        a = st.calculate_deps_batch(s.slice(0, 2000))
+        b = st.calculate_deps_batch(s.slice(2000, 4000))
+        st.reset()
+        again = PartialDeps.concat([st.calculate_deps_batch(s.slice(0, 2000)),
+                                    st.calculate_deps_batch(s.slice(2000, 4000))])
+    assert PartialDeps.concat([a, b]).first_difference(again) is None
+    assert again.first_difference(single(s, 500, 300)) is None
+
+
+def test_registered_store_rejects_ranges(gpu_device):
+    from accord_amd import WINDOW_NONE
+    s = generate_stream(200, 2, 100, 0.0, 0.5, range_frac=0.3, range_len_max=10, seed=39)
+    with CommandStore(device=0, key_lo=0, key_hi=100, window=WINDOW_NONE, resident=True) as st:
+        with pytest.raises(IllegalStateException):
+            st.calculate_deps_batch(s)
+
+
+@pytest.mark.timeout(600)
+def test_config3_full_in_8_batches(gpu_device):
+    """BASELINE configs[2] (config 2 with 20% range txns of up to 1000 keys) fed as 8 consecutive
+    batches to one resident store == the single-batch run == the fast oracle."""
+    n, ks, W = 1 << 20, 100_000, 256
+    s = generate_stream(n, 8, ks, 0.99, 0.5, range_frac=0.2, range_len_max=1000, seed=3)
+    pts = [i * n // 8 for i in range(9)]
+    got, _ = run_batches(s, ks, W, pts)
+    one = single(s, ks, W)
+    assert got.first_difference(one) is None
+    assert got.first_difference(O.deps_fast(s, W)) is None
