@@ -166,6 +166,8 @@ struct RangeDepsParams {
     uint2 *rk_slices;                   // (lo, raw | wcnt << 16) per key of every range txn's ranges
     uint32_t n_range_txns;
     const uint32_t *range_txns;
+    uint32_t *rk_cls;                   // union size classes: counts [0, 8), then per class n_range_txns
+                                        //   records {txn, D, body base, txnIds base} (uint4)
     const uint32_t *bound_l;            // Accept batch: txns started before executeAt (nullptr = i)
     // resident stores: txn i of the batch is stream position g0 + i; the range commands carried
     // from earlier batches (owner positions ascending, all before g0) precede the batch's own in
@@ -201,6 +203,8 @@ void launch_range_carry(const RangeDepsParams &p, uint32_t R, uint32_t thr, uint
 void launch_rangekeys_nkeys(const RangeDepsParams &p, uint32_t *cnt, hipStream_t s);
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s);
 void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s);
+constexpr uint32_t RK_CLASSES = 5;
+inline size_t rangekeys_class_bytes(uint32_t nrt) { return ((size_t)RK_CLASSES * nrt * 4 + 8) * 4; }
 void launch_rangekeys_union(const RangeDepsParams &p, hipStream_t s);
 
 // ---- K6 merge (merge.hip) ----

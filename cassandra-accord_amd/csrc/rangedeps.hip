@@ -472,75 +472,180 @@ __global__ __launch_bounds__(256) void rk_nkeys_kernel(RangeDepsParams p, uint32
     }
 }
 
-// Bitonic sort of 64*E keys held in registers, blocked layout (element g = lane*E + r): strides
-// >= E exchange between lanes (shuffle), strides < E swap registers of the same lane.
-template <int E> __device__ __forceinline__ void wave_bitonic(uint32_t (&v)[E], uint32_t lane)
+// ---- union sort: a bitonic network over n = 64*E keys held in registers ----
+// Two register layouts: striped (element g = r*64 + lane, register bits = g bits 6..) and blocked
+// (g = lane*E + r, register bits = g bits 0..e-1).  A stage on bit jb runs in-lane, as plain
+// min/max on register pairs, in the layout whose register bits hold jb; the layout switches by a
+// transposition through the wave's LDS (E stores + E loads per lane, conflict-free padding), and
+// only bits in neither layout (E < 64: bits e..5) exchange through lane shuffles.  Every stage is
+// resolved at compile time (template recursion over the stage index).
+constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+constexpr int us_stages(int logn) { return logn * (logn + 1) / 2; }
+constexpr int us_kb(int s) { int kb = 1; while (s >= kb) { s -= kb; ++kb; } return kb; }
+constexpr int us_jb(int s) { int kb = 1; while (s >= kb) { s -= kb; ++kb; } return kb - 1 - s; }
+// layout a stage on bit jb runs in (1 striped, 0 blocked), given the current one
+constexpr int us_need(int e, int jb, int cur) { return jb >= 6 ? 1 : jb < e ? 0 : cur; }
+constexpr int us_layout_before(int e, int s)
 {
-    for (uint32_t k = 2; k <= 64u * E; k <<= 1) {
-        for (uint32_t j = k >> 1; j >= (uint32_t)E; j >>= 1) {          // cross-lane
-            const uint32_t m = j / E;
-            const bool keep_min = ((lane & m) == 0) == (((lane * E) & k) == 0);
+    int cur = 1;                                     // loaded striped (coalesced)
+    for (int t = 0; t < s; ++t) cur = us_need(e, us_jb(t), cur);
+    return cur;
+}
+// LDS words of one wave's sort buffer: element g at g + g/32 + g/1024
+constexpr uint32_t us_lds_words(int E) { return 64u * E + 2u * E + (uint32_t)E / 16u + 1u; }
+
+// lane base / per-register offset of element (lane, r) in the padded buffer (exact for powers of 2)
+template <int E> __device__ __forceinline__ uint32_t us_base(int layout, uint32_t lane)
+{
+    return layout ? lane + (lane >> 5) : lane * E + ((lane * E) >> 5) + ((lane * E) >> 10);
+}
+template <int E> __host__ __device__ constexpr uint32_t us_off(int layout, int r)
+{
+    return layout ? (uint32_t)r * 66u + ((uint32_t)r >> 4) : (uint32_t)r + ((uint32_t)r >> 5);
+}
+
+template <int E, int FROM>
+__device__ __forceinline__ void us_transpose(uint32_t (&v)[E], uint32_t *lds, uint32_t lane)
+{
+    const uint32_t bw = us_base<E>(FROM, lane), br = us_base<E>(1 - FROM, lane);
 #pragma unroll
-            for (int r = 0; r < E; ++r) {
-                const uint32_t o = (uint32_t)__shfl_xor((int)v[r], (int)m, 64);
-                v[r] = keep_min ? min(v[r], o) : max(v[r], o);
-            }
+    for (int r = 0; r < E; ++r) lds[bw + us_off<E>(FROM, r)] = v[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < E; ++r) v[r] = lds[br + us_off<E>(1 - FROM, r)];
+    wave_lds_sync();
+}
+
+template <int E, int S>
+__device__ __forceinline__ void us_stage(uint32_t (&v)[E], uint32_t *lds, uint32_t lane)
+{
+    constexpr int e = ilog2c(E), logn = e + 6;
+    constexpr int kb = us_kb(S), jb = us_jb(S);
+    constexpr int cur = us_layout_before(e, S), lay = us_need(e, jb, cur);
+    if constexpr (lay != cur) us_transpose<E, cur>(v, lds, lane);
+    // ascending iff bit kb of g is 0 (kb == logn: the last merge, all ascending)
+    constexpr bool k_all = kb >= logn;
+    constexpr bool k_reg = !k_all && (lay ? kb >= 6 : kb < e);
+    constexpr int krb = k_reg ? (lay ? kb - 6 : kb) : 0;
+    constexpr int klb = (!k_all && !k_reg) ? (lay ? kb : kb - e) : 0;
+    const bool asc_lane = (k_all || k_reg) ? true : ((lane >> klb) & 1u) == 0;
+    constexpr bool j_reg = lay ? jb >= 6 : jb < e;
+    if constexpr (j_reg) {
+        constexpr int rb = lay ? jb - 6 : jb;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            if ((r >> rb) & 1) continue;
+            const int r2 = r | (1 << rb);
+            const bool asc = k_reg ? ((r >> krb) & 1) == 0 : asc_lane;
+            const uint32_t a = v[r], b = v[r2];
+            const uint32_t lo = min(a, b), hi = max(a, b);
+            v[r] = asc ? lo : hi;
+            v[r2] = asc ? hi : lo;
         }
+    } else {
+        constexpr int lb = lay ? jb : jb - e;
+        const bool lower = ((lane >> lb) & 1u) == 0;
 #pragma unroll
-        for (int j = E / 2; j >= 1; j >>= 1) {                          // in-lane
-            if ((uint32_t)j < k) {
-#pragma unroll
-                for (int r = 0; r < E; ++r) {
-                    if ((r & j) == 0) {
-                        const bool asc = ((lane * E + (uint32_t)r) & k) == 0;
-                        const uint32_t a = v[r], b = v[r | j];
-                        const uint32_t lo = min(a, b), hi = max(a, b);
-                        v[r] = asc ? lo : hi;
-                        v[r | j] = asc ? hi : lo;
-                    }
-                }
-            }
+        for (int r = 0; r < E; ++r) {
+            const bool asc = k_reg ? ((r >> krb) & 1) == 0 : asc_lane;
+            const uint32_t o = (uint32_t)__shfl_xor((int)v[r], 1 << lb, 64);
+            v[r] = (lower == asc) ? min(v[r], o) : max(v[r], o);
         }
     }
 }
 
-// One range txn's union with E keys per lane (D <= 64*E): sort the body's dep txn indices, write
-// the unique ones (txnIds, ascending = TxnId order) and replace every body entry by its rank.
-template <int E>
-__device__ __forceinline__ void rk_union(const RangeDepsParams &p, uint32_t i, uint32_t D, uint32_t k2v_base, uint32_t *ubuf,
-                                         uint32_t lane)
+// all stages from S on; ends in the blocked layout
+template <int E, int S>
+__device__ __forceinline__ void us_run(uint32_t (&v)[E], uint32_t *lds, uint32_t lane)
 {
+    constexpr int e = ilog2c(E);
+    if constexpr (S < us_stages(e + 6)) {
+        us_stage<E, S>(v, lds, lane);
+        us_run<E, S + 1>(v, lds, lane);
+    } else if constexpr (us_layout_before(e, S) != 0) {
+        us_transpose<E, 1>(v, lds, lane);
+    }
+}
+
+// One range txn's union with E keys per lane (D <= 64*E): sort the body, write the unique dep txn
+// indices (txnIds, ascending = TxnId order) and replace every body entry by its rank.  When the
+// body's values span less than 2^(32 - log2 n) the sort runs on packed (value - min, position)
+// keys, so each entry's rank comes out of the sorted order directly; otherwise it sorts the values
+// and finds the ranks by binary search over the unique values in LDS.
+template <int E>
+__device__ __forceinline__ void rk_union(const RangeDepsParams &p, uint32_t i, uint32_t D, uint32_t k2v_base,
+                                         uint32_t vb, uint32_t *lds, uint32_t lane)
+{
+    constexpr int IB = ilog2c(E) + 6;
+    constexpr uint32_t IMASK = (1u << IB) - 1u;
     uint32_t v[E];
+    uint32_t vmin = 0xFFFFFFFFu, vmax = 0;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-        const uint32_t g = lane * E + (uint32_t)r;
+        const uint32_t g = (uint32_t)r * 64 + lane;
         v[r] = g < D ? (uint32_t)p.kd_k2v[k2v_base + g] : 0xFFFFFFFFu;
+        if (g < D) { vmin = min(vmin, v[r]); vmax = max(vmax, v[r]); }
     }
-    wave_bitonic<E>(v, lane);
+    vmin = ~readlane(wave_incl_max(~vmin), 63);
+    vmax = readlane(wave_incl_max(vmax), 63);
+    const bool packed = vmax - vmin < (1u << (32 - IB)) - 1u;
+    if (packed) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const uint32_t g = (uint32_t)r * 64 + lane;
+            if (g < D) v[r] = ((v[r] - vmin) << IB) | g;
+        }
+    }
+    us_run<E, 0>(v, lds, lane);                       // blocked: element g = lane*E + r, ascending
+    const uint32_t sh = packed ? (uint32_t)IB : 0u;
     const uint32_t prev_last = (uint32_t)__shfl_up((int)v[E - 1], 1, 64);
     uint32_t cnt = 0;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const uint32_t g = lane * E + (uint32_t)r;
         const uint32_t prev = r ? v[r - 1] : prev_last;
-        cnt += (g < D && (g == 0 || v[r] != prev)) ? 1u : 0u;
+        cnt += (g < D && (g == 0 || (v[r] >> sh) != (prev >> sh))) ? 1u : 0u;
     }
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t U = readlane(incl, 63);
-    const uint32_t vb = p.kd_val_off[i];                  // txnIds upper-bound offsets
     uint32_t idx = incl - cnt;
+    if (lane == 0) p.cnt_vals_exact[i] = U;
+    // outputs leave through the LDS buffer (free after the sort), so the stores coalesce
+    if (packed) {
+        // ranks by body position
+        uint32_t run = idx;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const uint32_t g = lane * E + (uint32_t)r;
+            const uint32_t prev = r ? v[r - 1] : prev_last;
+            if (g < D) {
+                run += (g == 0 || (v[r] >> IB) != (prev >> IB)) ? 1u : 0u;
+                lds[v[r] & IMASK] = run - 1u;
+            }
+        }
+        wave_lds_sync();
+        for (uint32_t x = lane; x < D; x += 64) p.kd_k2v[k2v_base + x] = (int32_t)lds[x];
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const uint32_t g = lane * E + (uint32_t)r;
+            const uint32_t prev = r ? v[r - 1] : prev_last;
+            if (g < D && (g == 0 || (v[r] >> IB) != (prev >> IB))) lds[idx++] = (v[r] >> IB) + vmin;
+        }
+        wave_lds_sync();
+        for (uint32_t x = lane; x < U; x += 64) p.kd_vals[vb + x] = lds[x];
+        wave_lds_sync();
+        return;
+    }
+    uint32_t *ubuf = lds;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const uint32_t g = lane * E + (uint32_t)r;
         const uint32_t prev = r ? v[r - 1] : prev_last;
-        if (g < D && (g == 0 || v[r] != prev)) {
-            ubuf[idx] = v[r];
-            p.kd_vals[vb + idx] = v[r];
-            ++idx;
-        }
+        if (g < D && (g == 0 || v[r] != prev)) ubuf[idx++] = v[r];
     }
-    if (lane == 0) p.cnt_vals_exact[i] = U;
     wave_lds_sync();
+    for (uint32_t x = lane; x < U; x += 64) p.kd_vals[vb + x] = ubuf[x];
     // ranks: four lower-bound searches per lane in lockstep (one LDS round trip per step)
     for (uint32_t x0 = 0; x0 < D; x0 += 256) {
         uint32_t j[4], l[4], h[4];
@@ -574,26 +679,54 @@ __device__ __forceinline__ void rk_union(const RangeDepsParams &p, uint32_t i, u
     wave_lds_sync();
 }
 
-// Union pass: one wave per range txn whose body size D lies in (DLO, 64*E]; one launch per size
-// class, so each runs with the registers and LDS (64*E words per wave) of its own class.
-template <int E, uint32_t DLO>
-__global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_union_kernel(RangeDepsParams p)
+// Size classes of the range txns' bodies: D in (0, 256], (256, 1024], (1024, 2048], (2048, 4096],
+// (4096, 8192] -> lists (wave-aggregated appends); D = 0 is finished here, larger overflows.
+__global__ __launch_bounds__(256) void rk_classes_kernel(RangeDepsParams p)
 {
-    __shared__ uint32_t buf_all[RK_WAVES][64 * E];
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t nrt = p.n_range_txns;
+    for (uint32_t b = blockIdx.x * blockDim.x; b < nrt; b += gridDim.x * blockDim.x) {
+        const uint32_t li = b + threadIdx.x;
+        int c = -1;
+        uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+        if (li < nrt) {
+            const uint32_t i = p.range_txns[li];
+            const uint32_t kc = p.kd_key_off[i + 1] - p.kd_key_off[i];
+            const uint32_t D = p.kd_k2v_off[i + 1] - p.kd_k2v_off[i] - kc;
+            if (D == 0) p.cnt_vals_exact[i] = 0;
+            else if (D > 8192u) rd_overflow(p.status, i);
+            else c = D <= 256u ? 0 : D <= 1024u ? 1 : D <= 2048u ? 2 : D <= 4096u ? 3 : 4;
+            rec = make_uint4(i, D, p.kd_k2v_off[i] + kc, p.kd_val_off[i]);
+        }
+        for (int k = 0; k < (int)RK_CLASSES; ++k) {
+            const uint64_t m = __ballot(c == k);
+            if (!m) continue;
+            const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&p.rk_cls[k], (uint32_t)__popcll(m));
+            base = readlane(base, (int)leader);
+            if (c == k) reinterpret_cast<uint4 *>(p.rk_cls + 8)[(size_t)k * nrt + base + (uint32_t)__popcll(m & lt)] = rec;
+        }
+    }
+}
+
+// Union pass of one size class: one wave per listed range txn, the registers and LDS of its class.
+template <int E>
+__global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_union_kernel(RangeDepsParams p, uint32_t cls)
+{
+    __shared__ uint32_t buf_all[RK_WAVES][us_lds_words(E)];
     const uint32_t w = wave_id(), lane = lane_id();
     uint32_t *buf = buf_all[w];
-    for (uint32_t li = blockIdx.x * RK_WAVES + w; li < p.n_range_txns; li += gridDim.x * RK_WAVES) {
-        const uint32_t i = p.range_txns[li];
-        const uint32_t key_base = p.kd_key_off[i], kc = p.kd_key_off[i + 1] - key_base;
-        const uint32_t k2v_base = p.kd_k2v_off[i] + kc;
-        const uint32_t D = p.kd_k2v_off[i + 1] - p.kd_k2v_off[i] - kc;
-        if (DLO == 0 && D == 0) { if (lane == 0) p.cnt_vals_exact[i] = 0; continue; }
-        if (D <= DLO) continue;
-        if (D > 64u * E) {
-            if (E == RK_EMAX && lane == 0) rd_overflow(p.status, i);   // beyond the largest class
-            continue;
-        }
-        rk_union<E>(p, i, D, k2v_base, buf, lane);
+    const uint32_t count = p.rk_cls[cls];
+    const uint4 *list = reinterpret_cast<const uint4 *>(p.rk_cls + 8) + (size_t)cls * p.n_range_txns;
+    const uint32_t stride = gridDim.x * RK_WAVES;
+    uint32_t it = blockIdx.x * RK_WAVES + w;
+    uint4 rec = it < count ? list[it] : make_uint4(0u, 0u, 0u, 0u);
+    for (; it < count; it += stride) {
+        const uint4 cur = rec;                          // {txn, D, body base, txnIds base}
+        if (it + stride < count) rec = list[it + stride];   // the next record, in flight meanwhile
+        rk_union<E>(p, cur.x, cur.y, cur.z, cur.w, buf, lane);
     }
 }
 
@@ -704,12 +837,14 @@ void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s)
 void launch_rangekeys_union(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n_range_txns == 0) return;
+    uint32_t cb = (p.n_range_txns + 255) / 256;
+    hipLaunchKernelGGL(rk_classes_kernel, dim3(cb > 2048 ? 2048 : cb), dim3(256), 0, s, p);
     const dim3 g(rk_blocks(p.n_range_txns)), b(RK_WAVES * 64);
-    hipLaunchKernelGGL((rangekeys_union_kernel<4, 0>), g, b, 0, s, p);
-    hipLaunchKernelGGL((rangekeys_union_kernel<16, 256>), g, b, 0, s, p);
-    hipLaunchKernelGGL((rangekeys_union_kernel<32, 1024>), g, b, 0, s, p);
-    hipLaunchKernelGGL((rangekeys_union_kernel<64, 2048>), g, b, 0, s, p);
-    hipLaunchKernelGGL((rangekeys_union_kernel<RK_EMAX, 4096>), g, b, 0, s, p);
+    hipLaunchKernelGGL((rangekeys_union_kernel<4>), g, b, 0, s, p, 0u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<16>), g, b, 0, s, p, 1u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<32>), g, b, 0, s, p, 2u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<64>), g, b, 0, s, p, 3u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<RK_EMAX>), g, b, 0, s, p, 4u);
 }
 
 } // namespace accord

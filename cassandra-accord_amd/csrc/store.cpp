@@ -106,7 +106,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
                       &s->rng_owner, &s->is_range, &s->rt_excl, &s->range_txns, &s->cnt_rngs, &s->cnt_rvals,
                       &s->cnt_r2v, &s->rd_rng_off, &s->rd_val_off, &s->rd_r2v_off, &s->rd_rng_start, &s->rd_rng_end,
-                      &s->rd_vals, &s->rd_r2v, &s->rd_big, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
+                      &s->rd_vals, &s->rd_r2v, &s->rd_big, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->rk_cls, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
@@ -286,6 +286,7 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->is_range.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->rt_excl.ensure(n1 * 4));
     HIPCHECK(s, s->range_txns.ensure((size_t)nrt * 4 + 4));
+    if (nrt) HIPCHECK(s, s->rk_cls.ensure(accord::rangekeys_class_bytes(nrt)));
 
     HIPCHECK(s, s->fk_list.ensure((size_t)n * 4 + 64));
     // RangeDeps for the batch: its own range commands and, in a resident store, the carried ones
@@ -303,6 +304,7 @@ int32_t accord_deps_compute(accord_store *s)
         fl.add(s->seg_start.p, (size_t)nkeys * 4, 0u);
         fl.add(s->seg_end.p, (size_t)nkeys * 4, 0u);
         fl.add(s->fk_list.p, 4, 0u);                                   // fallback list count
+        if (nrt) fl.add(s->rk_cls.p, 8 * 4, 0u);                        // union class list counts
         if (rdeps) {
             fl.add(s->rd_big.p, 4, 0u);                                 // big range-hit list count
         } else {
@@ -407,6 +409,7 @@ int32_t accord_deps_compute(accord_store *s)
         rp.rk_slices = s->rk_slices.as<uint2>();
     }
     rp.n_range_txns = nrt; rp.range_txns = s->range_txns.as<uint32_t>();
+    rp.rk_cls = s->rk_cls.as<uint32_t>();
     rp.cnt_rngs = s->cnt_rngs.as<uint32_t>(); rp.cnt_vals = s->cnt_rvals.as<uint32_t>(); rp.cnt_r2v = s->cnt_r2v.as<uint32_t>();
     // range txns' KeyDeps: exact txnIds count into the upper-bound array (their bound is exact)
     rp.cnt_keys = s->cnt_keys.as<uint32_t>(); rp.cnt_vals_k = s->cnt_vub.as<uint32_t>(); rp.cnt_k2v = s->cnt_k2v.as<uint32_t>();

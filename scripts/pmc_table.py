@@ -1,21 +1,15 @@
-"""Per-kernel averages of every counter in rocprofv3 --pmc pass directories (dev helper)."""
-import csv
-import collections
-import sys
-
-
-def kname(s):
-    s = s.replace("(anonymous namespace)::", "").replace("accord::", "")
-    return s.split("(")[0].replace("void ", "")
-
-
-agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for d in [a.rstrip("/") for a in sys.argv[1:]]:
-    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, cs in agg.items():
-    if k.startswith("__amd") or k.startswith("sc_"):
+"""Per-kernel table of a rocprofv3 counter-collection csv: python3 pmc_table.py <csv> [name-filter]."""
+import csv, sys
+from collections import defaultdict
+rows = csv.DictReader(open(sys.argv[1]))
+filt = sys.argv[2] if len(sys.argv) > 2 else ""
+acc = defaultdict(lambda: defaultdict(float))
+for r in rows:
+    n = r["Kernel_Name"]
+    if filt not in n:
         continue
+    key = n.replace("(anonymous namespace)::", "").split("(")[0][-60:]
+    acc[key][r["Counter_Name"]] += float(r["Counter_Value"])
+for k, d in acc.items():
     print(k)
-    for c, v in sorted(cs.items()):
-        print(f"    {c:24s} {sum(v) / len(v):16.0f}")
+    print("   " + "  ".join(f"{c}={v:.4g}" for c, v in sorted(d.items())))
