@@ -155,6 +155,7 @@ struct RangeDepsParams {
     // history (for range txns' KeyDeps)
     const uint32_t *hist, *seg_start, *seg_end, *pw_local, *pw_carry;
     uint32_t pw_tile;
+    uint32_t kinds_present;             // entry kinds in the history (bit per kind; SP and XSP together)
     const uint64_t *c_local;            // witnessed counts (HistoryViews)
     const ClassCarry *ccarry;
     uint4 *cp;                          // checkpoints: first history position with txn >= b << RK_CP_SHIFT

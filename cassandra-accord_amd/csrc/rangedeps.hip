@@ -325,7 +325,9 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
         const uint32_t raw = out[u].raw;
         if (raw == 0) continue;
         uint32_t wc = 0;
-        if (raw <= RK_SHORT) {
+        if ((p.kinds_present & ~wmask) == 0) {
+            wc = raw;                                   // every kind in the history is witnessed
+        } else if (raw <= RK_SHORT) {
             for (uint32_t r = 0; r < raw; ++r) wc += (wmask >> (p.hist[out[u].lo + r] >> ENT_KIND_SHIFT)) & 1u;
         } else {
             const uint32_t lo = out[u].lo, pos = lo + raw;
@@ -343,10 +345,9 @@ constexpr uint32_t RK_SLICE_WIDE = 0xFFFFFFFFu;
 // Per range txn (one wave): count pass computes and stores every key's slice (keys of its ranges
 // in ascending order, clipped to the store) and the KeyDeps sizes; the fill pass writes keys, the
 // keysToTxnIds header and the body holding the dep txn indices (key order).
-template <bool FILL>
+template <bool FILL, int U>                          // U keys per lane per step
 __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParams p)
 {
-    constexpr int U = 2;                             // keys per lane per step
     __shared__ uint32_t rex_all[RK_WAVES][64], rlo_all[RK_WAVES][64];
     const uint32_t w = wave_id(), lane = lane_id();
     uint32_t *rex = rex_all[w], *rlo = rlo_all[w];
@@ -683,6 +684,7 @@ __device__ __forceinline__ void rk_union(const RangeDepsParams &p, uint32_t i, u
 // (4096, 8192] -> lists (wave-aggregated appends); D = 0 is finished here, larger overflows.
 __global__ __launch_bounds__(256) void rk_classes_kernel(RangeDepsParams p)
 {
+    __shared__ uint32_t cnt_s[RK_CLASSES], base_s[RK_CLASSES];
     const uint32_t lane = lane_id();
     const uint64_t lt = lanemask_lt();
     const uint32_t nrt = p.n_range_txns;
@@ -699,15 +701,24 @@ __global__ __launch_bounds__(256) void rk_classes_kernel(RangeDepsParams p)
             else c = D <= 256u ? 0 : D <= 1024u ? 1 : D <= 2048u ? 2 : D <= 4096u ? 3 : 4;
             rec = make_uint4(i, D, p.kd_k2v_off[i] + kc, p.kd_val_off[i]);
         }
+        // block-level appends: wave offsets in LDS, one global atomic per class per block
+        uint32_t mine = 0;
+        __syncthreads();
+        if (threadIdx.x < RK_CLASSES) cnt_s[threadIdx.x] = 0;
+        __syncthreads();
         for (int k = 0; k < (int)RK_CLASSES; ++k) {
             const uint64_t m = __ballot(c == k);
             if (!m) continue;
             const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&p.rk_cls[k], (uint32_t)__popcll(m));
-            base = readlane(base, (int)leader);
-            if (c == k) reinterpret_cast<uint4 *>(p.rk_cls + 8)[(size_t)k * nrt + base + (uint32_t)__popcll(m & lt)] = rec;
+            uint32_t wb = 0;
+            if (lane == leader) wb = atomicAdd(&cnt_s[k], (uint32_t)__popcll(m));
+            wb = readlane(wb, (int)leader);
+            if (c == k) mine = wb + (uint32_t)__popcll(m & lt);
         }
+        __syncthreads();
+        if (threadIdx.x < RK_CLASSES) base_s[threadIdx.x] = cnt_s[threadIdx.x] ? atomicAdd(&p.rk_cls[threadIdx.x], cnt_s[threadIdx.x]) : 0u;
+        __syncthreads();
+        if (c >= 0) reinterpret_cast<uint4 *>(p.rk_cls + 8)[(size_t)c * nrt + base_s[c] + mine] = rec;
     }
 }
 
@@ -825,13 +836,13 @@ void launch_rangekeys_nkeys(const RangeDepsParams &p, uint32_t *cnt, hipStream_t
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n_range_txns == 0) return;
-    hipLaunchKernelGGL(rangekeys_kernel<false>, dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangekeys_kernel<false, 8>), dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
 }
 
 void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n_range_txns == 0) return;
-    hipLaunchKernelGGL(rangekeys_kernel<true>, dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangekeys_kernel<true, 4>), dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
 }
 
 void launch_rangekeys_union(const RangeDepsParams &p, hipStream_t s)

@@ -150,13 +150,16 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     const uint32_t P = b->key_off[n];
     const uint32_t R = b->rng_off ? b->rng_off[n] : 0;
     if (R && (!b->rng_start || !b->rng_end)) return fail(s, ACCORD_ERR_ARG, "range CSR without range bounds");
-    uint32_t nrt = 0;
-    for (uint32_t i = 0; i < n; ++i) nrt += (uint32_t)(b->lsb[i] & 1);
+    uint32_t nrt = 0, kinds = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        nrt += (uint32_t)(b->lsb[i] & 1);
+        if (b->key_off[i + 1] > b->key_off[i]) kinds |= 1u << ((b->lsb[i] >> 1) & 7);   // history entry kinds
+    }
     if (b->txn_index && nrt)
         return fail(s, ACCORD_ERR_ARG, "txn_index (store subset of a stream) is supported for key txns only");
     if (nrt && accord_impl::registered_mode(s))
         return fail(s, ACCORD_ERR_STATE, "range txns in a registered-status store (ACCORD_WINDOW_NONE) are not supported by this build");
-    s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt;
+    s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt; s->b_kinds = kinds;
     s->rk_keys_total = 0;                // sizes the range txns' stored key slices
     if (nrt && b->rng_off)
         for (uint32_t i = 0; i < n; ++i)
@@ -391,6 +394,7 @@ int32_t accord_deps_compute(accord_store *s)
         rp.c_local = hv.c_local; rp.ccarry = hv.ccarry;
     }
     rp.nkeys = nkeys;
+    rp.kinds_present = (s->resident ? s->hist_kinds : 0u) | s->b_kinds;
     // resident stores: txn i is stream position g0 + i; the checkpoint blocks span every window
     rp.g0 = s->resident ? s->next_global : 0u;
     rp.ncr = ncr;
@@ -540,6 +544,7 @@ int32_t accord_deps_compute(accord_store *s)
         std::swap(s->cy_key, s->cy_key2);
         std::swap(s->cy_ent, s->cy_ent2);
         s->carry_n = (uint32_t)s->pinned->totals[8];
+        s->hist_kinds |= s->b_kinds;
         if (rdeps) {
             std::swap(s->rc_owner, s->rc_owner2); std::swap(s->rc_start, s->rc_start2);
             std::swap(s->rc_end, s->rc_end2); std::swap(s->rc_kind, s->rc_kind2);
@@ -589,7 +594,7 @@ int32_t accord_store_state(accord_store *s, accord_store_state_info *info)
 int32_t accord_store_reset(accord_store *s)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
-    s->next_global = 0; s->carry_n = 0; s->rc_n = 0; s->has_prev = false;
+    s->next_global = 0; s->carry_n = 0; s->rc_n = 0; s->hist_kinds = 0; s->has_prev = false;
     s->rg_tx_n = 0; s->rg_known = 0;
     s->prev_msb = s->prev_lsb = 0; s->prev_node = 0;
     s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->wo_done = false;

@@ -97,6 +97,7 @@ struct accord_store {
     // key-major history entries (cy_key relative key ordinal, cy_ent kind<<29 | global txn)
     bool resident = false, has_prev = false;
     uint32_t next_global = 0, carry_n = 0;
+    uint32_t hist_kinds = 0, b_kinds = 0;   // entry kinds (bit per kind) carried / of the uploaded batch
     uint64_t prev_msb = 0, prev_lsb = 0;
     int32_t prev_node = 0;
     DevBuf cy_key, cy_ent, cy_key2, cy_ent2, carry_tmp;

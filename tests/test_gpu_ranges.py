@@ -66,3 +66,21 @@ def test_range_batch_rejects_overlapping_ranges(gpu_device):
     bad = Stream(s.msb, s.lsb, s.node, s.key_off, s.key_ord, s.rng_off, st, en)
     with pytest.raises(IllegalArgumentException):
         run_gpu(bad, 8, 100)
+
+
+@pytest.mark.parametrize("seed,kinds_p", [
+    (14, [0.35, 0.35, 0.1, 0.1, 0.1]),     # every kind: range Writes must still skip SyncPoints/EphemeralReads
+    (15, [0.0, 1.0, 0.0, 0.0, 0.0]),       # Writes only: every entry witnessed by every range txn
+    (16, [0.5, 0.5, 0.0, 0.0, 0.0]),       # R/W: range Writes witness all, range Reads only Writes
+    (17, [0.3, 0.3, 0.0, 0.4, 0.0]),       # SyncPoints in the histories
+])
+def test_mixed_kinds_vs_literal(gpu_device, seed, kinds_p):
+    from accord_amd import Stream
+    s = generate_stream(2500, 4, 400, 0.99, 0.5, range_frac=0.25, range_len_max=120, seed=seed)
+    rng = np.random.default_rng(seed)
+    kinds = rng.choice([0, 1, 2, 3, 4], size=s.n, p=kinds_p).astype(np.uint64)
+    lsb = (s.lsb & ~np.uint64(0xE)) | (kinds << np.uint64(1))
+    s2 = Stream(s.msb, lsb, s.node, s.key_off, s.key_ord, s.rng_off, s.rng_start, s.rng_end)
+    got = run_gpu(s2, 64, 400)
+    want = O.deps_literal(s2, 64)
+    assert got.first_difference(want) is None, got.first_difference(want)
