@@ -162,7 +162,8 @@ struct RangeDepsParams {
                                         //   {position, its txn, (last Write before it) + 1, 0}
     uint32_t nkeys, ncp;                //   per key (cp[b * nkeys + k]), ncp blocks
     uint32_t *cnt_vals_exact;           // exact txnIds count per txn (range txns: written by the union pass)
-    uint32_t *rd_big_list, *rd_big_count;   // txns with more range hits than the main pass holds
+    uint32_t *rd_big_list, *rd_big_count;   // txns with more range hits than the per-txn pass holds
+    uint32_t *rd_fb_list, *rd_fb_count;     // txns the tile pass hands to the per-txn pass
     const uint32_t *rk_off;             // per range txn: first of its stored key slices
     uint2 *rk_slices;                   // (lo, raw | wcnt << 16) per key of every range txn's ranges
     uint32_t n_range_txns;

@@ -57,9 +57,9 @@ __device__ __forceinline__ bool rd_hits(const RangeDepsParams &p, uint32_t s, ui
     return lo < q1 && p.rng_start[lo] < e;
 }
 
-// Main pass (LIST = false): every txn, hits up to HCAP; a txn with more is appended to a list in
-// the count pass and skipped (by both passes).  Big pass (LIST = true): the listed txns with
-// RD_HCAP_BIG hits of LDS; more than that is reported as overflow.
+// Per-txn pass (LIST = false): the txns the tile pass handed on, hits up to HCAP; a txn with more
+// is appended to a list in the count pass and skipped (by both passes).  Big pass (LIST = true):
+// the listed txns with RD_HCAP_BIG hits of LDS; more than that is reported as overflow.
 template <bool FILL, uint32_t HCAP, int WAVES, bool LIST>
 __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p)
 {
@@ -67,9 +67,10 @@ __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p
     const uint32_t w = wave_id(), lane = lane_id();
     RdLds<HCAP> &L = lds_all[w];
     const uint64_t lt = lanemask_lt();
-    const uint32_t limit = LIST ? *p.rd_big_count : p.n;
+    // main pass: the txns the tile pass handed on (rd_fb_list); big pass: those with more hits
+    const uint32_t limit = LIST ? *p.rd_big_count : *p.rd_fb_count;
     for (uint32_t it = blockIdx.x * WAVES + w; it < limit; it += gridDim.x * WAVES) {
-        const uint32_t i = LIST ? p.rd_big_list[it] : it;
+        const uint32_t i = LIST ? p.rd_big_list[it] : p.rd_fb_list[it];
         const uint64_t lsb_i = p.lsb[i];
         const uint32_t wmask = witness_mask((uint32_t)(lsb_i >> 1) & 7);
         const bool key_query = (lsb_i & 1) == 0;
@@ -199,6 +200,159 @@ __global__ __launch_bounds__(WAVES * 64) void rangedeps_kernel(RangeDepsParams p
                 p.rd_r2v[xb + first_before] = (int32_t)(ur + le_code);
             }
         }
+    }
+}
+
+// Tile pass: one wave per 64 consecutive txns, a lane per txn.  Consecutive txns see nearly the
+// same live range commands, so the wave stages the union of its lanes' candidate windows in LDS
+// once and every lane scans its own window there (the per-txn pass reloads ~W live commands per
+// txn).  A lane keeps up to RT_HL hits (candidate indices); a txn with more hits, more than 8 query
+// keys/ranges, or a tile whose window exceeds RT_CAND goes to the per-txn pass (count: appended to
+// rd_fb_list; fill: skipped, the per-txn pass fills it).  Same outputs as rangedeps_kernel.
+constexpr uint32_t RT_CAND = 512, RT_HL = 16, RT_WAVES = 2;
+struct RtLds {
+    uint32_t s[RT_CAND], e[RT_CAND], jk[RT_CAND];     // jk = owner position | witness kind << 29
+    uint32_t hit[64 * RT_HL];
+};
+
+__device__ __forceinline__ void rd_fb_push(const RangeDepsParams &p, uint32_t i)
+{
+    p.rd_fb_list[atomicAdd(p.rd_fb_count, 1u)] = i;
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(RT_WAVES * 64) void rangedeps_tile_kernel(RangeDepsParams p)
+{
+    __shared__ RtLds lds_all[RT_WAVES];
+    const uint32_t w = wave_id(), lane = lane_id();
+    RtLds &L = lds_all[w];
+    const uint32_t ntiles = (p.n + 63) / 64;
+    for (uint32_t tile = blockIdx.x * RT_WAVES + w; tile < ntiles; tile += gridDim.x * RT_WAVES) {
+        const uint32_t i = tile * 64 + lane;
+        const bool valid = i < p.n;
+        const uint32_t g = p.g0 + i;
+        uint32_t r_lo = 0, r_hi = 0;
+        if (valid) {
+            const uint32_t lo_g = g > p.window ? g - p.window : 0u;
+            if (lo_g >= p.g0) {
+                r_lo = p.ncr + p.rng_off[lo_g - p.g0];
+            } else {
+                uint32_t l = 0, h = p.ncr;
+                while (l < h) {
+                    const uint32_t m = (l + h) >> 1;
+                    if (p.rc_owner[m] < lo_g) l = m + 1; else h = m;
+                }
+                r_lo = l;
+            }
+            r_hi = p.ncr + p.rng_off[p.bound_l ? p.bound_l[i] : i];
+        }
+        const uint32_t R_lo = ~readlane(wave_incl_max(valid ? ~r_lo : 0u), 63);
+        const uint32_t R_hi = readlane(wave_incl_max(valid ? r_hi : 0u), 63);
+        if (R_hi > R_lo && R_hi - R_lo > RT_CAND) {           // window too large: per-txn pass
+            if (!FILL && valid) rd_fb_push(p, i);
+            continue;
+        }
+        for (uint32_t c = lane; R_lo + c < R_hi; c += 64) {
+            const uint32_t r = R_lo + c;
+            uint32_t j, s, e, kind;
+            if (r < p.ncr) {
+                j = p.rc_owner[r]; s = p.rc_start[r]; e = p.rc_end[r]; kind = p.rc_kind[r];
+            } else {
+                const uint32_t rb = r - p.ncr, jl = p.rng_owner[rb];
+                j = p.g0 + jl; s = p.rng_start[rb]; e = p.rng_end[rb];
+                kind = (uint32_t)(p.lsb[jl] >> 1) & 7;
+            }
+            L.s[c] = s; L.e[c] = e; L.jk[c] = j | (kind << 29);
+        }
+        wave_lds_sync();
+        bool fb = false;
+        uint32_t H = 0;
+        if (valid) {
+            const uint64_t lsb_i = p.lsb[i];
+            const uint32_t wmask = witness_mask((uint32_t)(lsb_i >> 1) & 7);
+            const bool key_query = (lsb_i & 1) == 0;
+            const uint32_t q0 = key_query ? p.key_off[i] : p.rng_off[i];
+            const uint32_t q1 = key_query ? p.key_off[i + 1] : p.rng_off[i + 1];
+            const uint32_t nq = q1 - q0;
+            if (nq > 8) {
+                fb = true;
+            } else if (nq > 0) {
+                uint32_t qa[8], qb[8];
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) {
+                    qa[q] = q < nq ? (key_query ? p.key_ord[q0 + q] : p.rng_start[q0 + q]) : 0u;
+                    qb[q] = q < nq ? (key_query ? qa[q] : p.rng_end[q0 + q]) : 0u;
+                }
+                for (uint32_t c = r_lo - R_lo; c < r_hi - R_lo; ++c) {
+                    const uint32_t s = L.s[c], e = L.e[c], jk = L.jk[c];
+                    bool inter = false;
+#pragma unroll
+                    for (uint32_t q = 0; q < 8; ++q)
+                        inter = inter || (q < nq && (key_query ? (qa[q] > s && qa[q] <= e) : (s < qb[q] && qa[q] < e)));
+                    if (inter && (jk & ENT_TXN_MASK) != g && ((wmask >> (jk >> 29)) & 1u)) {
+                        if (H < RT_HL) L.hit[lane * RT_HL + H] = c;
+                        ++H;
+                    }
+                }
+            }
+            if (H > RT_HL) fb = true;
+        }
+        if (fb) {
+            if (!FILL) rd_fb_push(p, i);
+        } else if (valid) {
+            // hits in candidate order = ascending owner: distinct owners are the transitions; distinct
+            // ranges (Range.compare order) by an O(H^2) pass over the few hits
+            const uint32_t *hs = L.hit + lane * RT_HL;
+            uint32_t ur = 0, uj = 0, prevj = 0xFFFFFFFFu;
+            for (uint32_t h = 0; h < H; ++h) {
+                const uint32_t c = hs[h], j = L.jk[c] & ENT_TXN_MASK;
+                uj += j != prevj ? 1u : 0u;
+                prevj = j;
+                bool first = true;
+                for (uint32_t x = 0; x < h; ++x) {
+                    const uint32_t cx = hs[x];
+                    if (L.s[cx] == L.s[c] && L.e[cx] == L.e[c]) { first = false; break; }
+                }
+                ur += first ? 1u : 0u;
+            }
+            if (!FILL) {
+                p.cnt_rngs[i] = ur; p.cnt_vals[i] = uj; p.cnt_r2v[i] = ur + H;
+            } else {
+                const uint32_t rb = p.rd_rng_off[i], vb = p.rd_val_off[i], xb = p.rd_r2v_off[i];
+                uint32_t jrank = 0xFFFFFFFFu;
+                prevj = 0xFFFFFFFFu;
+                for (uint32_t h = 0; h < H; ++h) {
+                    const uint32_t c = hs[h], jh = L.jk[c] & ENT_TXN_MASK;
+                    const unsigned long long code = ((unsigned long long)L.s[c] << 32) | L.e[c];
+                    if (jh != prevj) { ++jrank; prevj = jh; p.rd_vals[vb + jrank] = jh; }
+                    uint32_t le_code = 0, before = 0, first_before = 0;
+                    bool first = true;
+                    for (uint32_t x = 0; x < H; ++x) {
+                        const uint32_t cx = hs[x];
+                        const unsigned long long cg = ((unsigned long long)L.s[cx] << 32) | L.e[cx];
+                        le_code += cg <= code ? 1u : 0u;
+                        before += (cg < code || (cg == code && x < h)) ? 1u : 0u;
+                        if (cg == code && x < h) first = false;
+                        // distinct ranges below code: count each code at its first hit
+                        if (cg < code) {
+                            bool fx = true;
+                            for (uint32_t y = 0; y < x; ++y) {
+                                const uint32_t cy = hs[y];
+                                if (L.s[cy] == L.s[cx] && L.e[cy] == L.e[cx]) { fx = false; break; }
+                            }
+                            first_before += fx ? 1u : 0u;
+                        }
+                    }
+                    p.rd_r2v[xb + ur + before] = (int32_t)jrank;
+                    if (first) {
+                        p.rd_rng_start[rb + first_before] = (uint32_t)(code >> 32);
+                        p.rd_rng_end[rb + first_before] = (uint32_t)code;
+                        p.rd_r2v[xb + first_before] = (int32_t)(ur + le_code);
+                    }
+                }
+            }
+        }
+        wave_lds_sync();
     }
 }
 
@@ -743,21 +897,26 @@ __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_union_kernel(RangeDep
 
 } // namespace
 
+static uint32_t rt_blocks(uint32_t n)
+{
+    const uint32_t tiles = (n + 63) / 64;
+    uint32_t b = (tiles + RT_WAVES - 1) / RT_WAVES;
+    return b > 8192u ? 8192u : b;
+}
+
 void launch_rangedeps_count(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n == 0) return;
-    uint32_t blocks = (p.n + RD_WAVES - 1) / RD_WAVES;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL((rangedeps_kernel<false, RD_HCAP, RD_WAVES, false>), dim3(blocks), dim3(RD_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL(rangedeps_tile_kernel<false>, dim3(rt_blocks(p.n)), dim3(RT_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangedeps_kernel<false, RD_HCAP, RD_WAVES, false>), dim3(1024), dim3(RD_WAVES * 64), 0, s, p);
     hipLaunchKernelGGL((rangedeps_kernel<false, RD_HCAP_BIG, 1, true>), dim3(256), dim3(64), 0, s, p);
 }
 
 void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n == 0) return;
-    uint32_t blocks = (p.n + RD_WAVES - 1) / RD_WAVES;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL((rangedeps_kernel<true, RD_HCAP, RD_WAVES, false>), dim3(blocks), dim3(RD_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL(rangedeps_tile_kernel<true>, dim3(rt_blocks(p.n)), dim3(RT_WAVES * 64), 0, s, p);
+    hipLaunchKernelGGL((rangedeps_kernel<true, RD_HCAP, RD_WAVES, false>), dim3(1024), dim3(RD_WAVES * 64), 0, s, p);
     hipLaunchKernelGGL((rangedeps_kernel<true, RD_HCAP_BIG, 1, true>), dim3(256), dim3(64), 0, s, p);
 }
 

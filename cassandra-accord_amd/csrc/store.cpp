@@ -295,7 +295,7 @@ int32_t accord_deps_compute(accord_store *s)
     // RangeDeps for the batch: its own range commands and, in a resident store, the carried ones
     const uint32_t ncr = s->resident ? s->rc_n : 0u;
     const bool rdeps = R || ncr;
-    if (rdeps) HIPCHECK(s, s->rd_big.ensure((size_t)n * 4 + 64));
+    if (rdeps) HIPCHECK(s, s->rd_big.ensure(((size_t)2 * n + 64) * 4));   // big list | tile fallback list
 
     HostTotals *dev = s->status_totals.as<HostTotals>();
     record(s, EV_START);
@@ -310,6 +310,7 @@ int32_t accord_deps_compute(accord_store *s)
         if (nrt) fl.add(s->rk_cls.p, 8 * 4, 0u);                        // union class list counts
         if (rdeps) {
             fl.add(s->rd_big.p, 4, 0u);                                 // big range-hit list count
+            fl.add(s->rd_big.as<uint32_t>() + 32 + n, 4, 0u);           // tile fallback list count
         } else {
             fl.add(s->rd_rng_off.p, n1 * 4, 0u);
             fl.add(s->rd_val_off.p, n1 * 4, 0u);
@@ -432,6 +433,8 @@ int32_t accord_deps_compute(accord_store *s)
     if (rdeps) {
         rp.rd_big_count = s->rd_big.as<uint32_t>();
         rp.rd_big_list = rp.rd_big_count + 16;
+        rp.rd_fb_count = rp.rd_big_count + 32 + n;
+        rp.rd_fb_list = rp.rd_fb_count + 16;
         accord::launch_rangedeps_count(rp, st);
     }
     record(s, EV_COUNT);
