@@ -368,6 +368,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void rangedeps_tile_kernel(RangeDeps
 //           offsets, compacted with the key txns' later) and the body rewritten to ranks
 // ---------------------------------------------------------------------------------------------
 constexpr int RK_WAVES = 4;
+constexpr int RK_FB = 4;                       // fill: groups of 64 history loads in flight
 constexpr int RK_EMAX = 128;                   // largest union class: 8192 deps per range txn
 
 // cp[b * K + k] = {x, txn(x), pw(x), 0}: x = first position of key k's segment [a, c) with
@@ -502,7 +503,7 @@ constexpr uint32_t RK_SLICE_WIDE = 0xFFFFFFFFu;
 template <bool FILL, int U>                          // U keys per lane per step
 __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParams p)
 {
-    __shared__ uint32_t rex_all[RK_WAVES][64], rlo_all[RK_WAVES][64];
+    __shared__ uint32_t rex_all[RK_WAVES][64 * U], rlo_all[RK_WAVES][64 * U];
     const uint32_t w = wave_id(), lane = lane_id();
     uint32_t *rex = rex_all[w], *rlo = rlo_all[w];
     const uint64_t lt = lanemask_lt();
@@ -562,6 +563,10 @@ __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParam
                     for (int u = 0; u < U; ++u)
                         if (re[u].raw >= 65536u) sl[u] = re[u];
                 }
+                // headers of the chunk's U*64 keys, their raw entries' prefix in LDS, then the body of
+                // the whole chunk with RK_FB groups of 64 history loads in flight
+                const uint32_t body0 = body;
+                uint32_t rbase = 0;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t key = c0 + 64 * u + lane;
@@ -575,33 +580,39 @@ __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParam
                         p.kd_k2v[k2v_base + ns] = (int32_t)(kc_total + body + wincl);
                     }
                     const uint32_t rincl = wave_incl_scan(raw);
-                    const uint32_t rtot = readlane(rincl, 63);
-                    rex[lane] = rincl - raw;
-                    rlo[lane] = sl[u].lo;
-                    wave_lds_sync();
-                    // candidates of these 64 keys in key order; body position = running witnessed count
-                    uint32_t run = body;
-                    for (uint32_t w0 = 0; w0 < rtot; w0 += 64) {
-                        const uint32_t rr = w0 + lane;
-                        bool wit = false;
-                        uint32_t j = 0;
-                        if (rr < rtot) {
-                            uint32_t sidx = 0;       // last slot with rex <= rr (rex[0] = 0)
-#pragma unroll
-                            for (uint32_t step = 32; step >= 1; step >>= 1)
-                                if (sidx + step <= 63 && rex[sidx + step] <= rr) sidx += step;
-                            const uint32_t e = p.hist[rlo[sidx] + (rr - rex[sidx])];
-                            j = e & ENT_TXN_MASK;
-                            wit = (wmask >> (e >> ENT_KIND_SHIFT)) & 1u;
-                        }
-                        const uint64_t wb = __ballot(wit);
-                        if (wit) p.kd_k2v[k2v_base + kc_total + run + (uint32_t)__popcll(wb & lt)] = (int32_t)j;
-                        run += (uint32_t)__popcll(wb);
-                    }
-                    wave_lds_sync();
+                    rex[u * 64 + lane] = rbase + rincl - raw;
+                    rlo[u * 64 + lane] = sl[u].lo;
+                    rbase += readlane(rincl, 63);
                     kc += (uint32_t)__popcll(hb);
                     body += readlane(wincl, 63);
                 }
+                wave_lds_sync();
+                // candidates in key order; body position = running witnessed count
+                uint32_t run = body0;
+                for (uint32_t w0 = 0; w0 < rbase; w0 += 64 * RK_FB) {
+                    uint32_t e[RK_FB];
+#pragma unroll
+                    for (int b = 0; b < RK_FB; ++b) {
+                        const uint32_t rr = w0 + 64 * b + lane;
+                        e[b] = 0;
+                        if (rr < rbase) {
+                            uint32_t sidx = 0;       // last slot with rex <= rr (rex[0] = 0)
+#pragma unroll
+                            for (uint32_t step = 32 * U; step >= 1; step >>= 1)
+                                if (sidx + step < 64u * U && rex[sidx + step] <= rr) sidx += step;
+                            e[b] = p.hist[rlo[sidx] + (rr - rex[sidx])];
+                        }
+                    }
+#pragma unroll
+                    for (int b = 0; b < RK_FB; ++b) {
+                        const uint32_t rr = w0 + 64 * b + lane;
+                        const bool wit = rr < rbase && ((wmask >> (e[b] >> ENT_KIND_SHIFT)) & 1u);
+                        const uint64_t wb = __ballot(wit);
+                        if (wit) p.kd_k2v[k2v_base + kc_total + run + (uint32_t)__popcll(wb & lt)] = (int32_t)(e[b] & ENT_TXN_MASK);
+                        run += (uint32_t)__popcll(wb);
+                    }
+                }
+                wave_lds_sync();
             }
             kidx += ke - ks + 1;
         }
@@ -877,8 +888,9 @@ __global__ __launch_bounds__(256) void rk_classes_kernel(RangeDepsParams p)
 }
 
 // Union pass of one size class: one wave per listed range txn, the registers and LDS of its class.
-template <int E>
-__global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_union_kernel(RangeDepsParams p, uint32_t cls)
+template <int E, int WPE>
+__global__ __launch_bounds__(RK_WAVES * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void rangekeys_union_kernel(RangeDepsParams p, uint32_t cls)
 {
     __shared__ uint32_t buf_all[RK_WAVES][us_lds_words(E)];
     const uint32_t w = wave_id(), lane = lane_id();
@@ -1010,11 +1022,11 @@ void launch_rangekeys_union(const RangeDepsParams &p, hipStream_t s)
     uint32_t cb = (p.n_range_txns + 255) / 256;
     hipLaunchKernelGGL(rk_classes_kernel, dim3(cb > 2048 ? 2048 : cb), dim3(256), 0, s, p);
     const dim3 g(rk_blocks(p.n_range_txns)), b(RK_WAVES * 64);
-    hipLaunchKernelGGL((rangekeys_union_kernel<4>), g, b, 0, s, p, 0u);
-    hipLaunchKernelGGL((rangekeys_union_kernel<16>), g, b, 0, s, p, 1u);
-    hipLaunchKernelGGL((rangekeys_union_kernel<32>), g, b, 0, s, p, 2u);
-    hipLaunchKernelGGL((rangekeys_union_kernel<64>), g, b, 0, s, p, 3u);
-    hipLaunchKernelGGL((rangekeys_union_kernel<RK_EMAX>), g, b, 0, s, p, 4u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<4, 1>), g, b, 0, s, p, 0u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<16, 1>), g, b, 0, s, p, 1u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<32, 1>), g, b, 0, s, p, 2u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<64, 2>), g, b, 0, s, p, 3u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<RK_EMAX, 1>), g, b, 0, s, p, 4u);
 }
 
 } // namespace accord
