@@ -426,6 +426,7 @@ __device__ __forceinline__ uint32_t rk_first_ge(const uint32_t *__restrict__ his
 
 struct RkSlice {
     uint32_t lo, raw, wcnt;
+    uint32_t l, pre;        // first entry inside the window; 1 if lo is the last Write before it
 };
 
 // The deps slices of range txn i on U keys per lane (store-relative kk[u], valid[u]): raw entries
@@ -463,17 +464,22 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
         if (!(valid[u] && a[u] < c[u])) continue;
         const uint32_t pos = past ? c[u] : e1[u].y >= eb ? e1[u].x : rk_first_ge(p.hist, e1[u].x + 1, c[u], eb);
         if (pos == a[u]) continue;
-        uint32_t pw = 0;
+        uint32_t pw = 0, l = a[u];
         if (windowed) {
             if (e2[u].y >= thr || e2[u].x >= pos) {
-                pw = min(e2[u].x, pos) == e2[u].x ? e2[u].z : rk_pw_before(p, pos);
+                l = min(e2[u].x, pos);
+                pw = l == e2[u].x ? e2[u].z : rk_pw_before(p, pos);
             } else {
-                pw = rk_pw_before(p, rk_first_ge(p.hist, e2[u].x + 1, pos, thr));
+                l = rk_first_ge(p.hist, e2[u].x + 1, pos, thr);
+                pw = rk_pw_before(p, l);
             }
         }
-        const uint32_t lo = windowed && pw > a[u] ? pw - 1 : a[u];
+        const bool pre = windowed && pw > a[u];
+        const uint32_t lo = pre ? pw - 1 : a[u];
         out[u].lo = lo;
         out[u].raw = pos - lo;
+        out[u].l = l;
+        out[u].pre = pre ? 1u : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -482,6 +488,17 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
         uint32_t wc = 0;
         if ((p.kinds_present & ~wmask) == 0) {
             wc = raw;                                   // every kind in the history is witnessed
+        } else if ((p.kinds_present & ~3u) == 0 && wmask == 2u) {
+            // Reads and Writes only, the txn witnesses Writes: before the window just the last Write
+            // (lo; the entries after it there are Reads), inside it the Writes of [l, pos)
+            const uint32_t l = out[u].l, pos = out[u].lo + raw;
+            wc = out[u].pre;
+            if (pos - l <= RK_SHORT) {
+                for (uint32_t x = l; x < pos; ++x) wc += (p.hist[x] >> ENT_KIND_SHIFT) == 1u ? 1u : 0u;
+            } else {
+                wc += witnessed_upto(p.c_local, p.ccarry, pos - 1, wmask, p.pw_tile) -
+                      (l ? witnessed_upto(p.c_local, p.ccarry, l - 1, wmask, p.pw_tile) : 0u);
+            }
         } else if (raw <= RK_SHORT) {
             for (uint32_t r = 0; r < raw; ++r) wc += (wmask >> (p.hist[out[u].lo + r] >> ENT_KIND_SHIFT)) & 1u;
         } else {
