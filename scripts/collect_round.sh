@@ -11,8 +11,8 @@ cp "$O/prof_trace/run_kernel_stats.csv" "$P/kernel_stats_config2.csv"
 cp "$O/prof_trace_c5/run_kernel_stats.csv" "$P/kernel_stats_config5.csv"
 cp "$O/pytest_gpu.log" "$P/pytest_gpu.log"
 { echo "rocprofv3 --pmc, one counter group per pass (FETCH_SIZE / WRITE_SIZE separately), config 2;"
-  echo "per-dispatch averages. gfx950 FETCH_SIZE reports ~1/2 of wide coalesced reads (MI355X_MICROARCH.md)"
-  python3 scripts/pmc_table.py "$O"/pmc1 "$O"/pmc2 "$O"/pmc3 "$O"/pmc4 "$O"/pmc5; } > "$P/pmc_config2.txt"
+  echo "sums over all dispatches of the run. gfx950 FETCH_SIZE reports ~1/2 of wide coalesced reads (MI355X_MICROARCH.md)"
+  for d in "$O"/pmc[0-9]*/; do echo "== $d"; python3 scripts/pmc_table.py "$d/run_counter_collection.csv"; done; } > "$P/pmc_config2.txt"
 cp "$O/traffic_config2.json" profiles/traffic_config2.json
 python3 - "$P" <<'PY'
 import json, sys
