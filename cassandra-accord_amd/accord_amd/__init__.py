@@ -54,7 +54,9 @@ EXPORTED_SYMBOLS = [
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
     "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset", "accord_txn_register",
     "accord_deps_visit", "accord_deps_range_stab", "accord_range_stab_release",
+    "accord_redundant_before_set",
 ]
+NO_TXN = 0xFFFFFFFF          # RedundantBefore bound Timestamp.NONE
 VISIT_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32)
 
 
@@ -198,6 +200,8 @@ def lib() -> C.CDLL:
         L.accord_max_conflicts_fold_from.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_int32,
                                                      C.POINTER(_MaxConflictsOut)]
         L.accord_max_conflicts_reset.argtypes = [C.c_void_p]
+        L.accord_redundant_before_set.argtypes = [C.c_void_p, C.c_uint32, _u32p, _u32p, _u64p, _u64p, _u32p,
+                                                  C.c_uint64]
         L.accord_store_state.argtypes = [C.c_void_p, C.POINTER(_StoreState)]
         L.accord_store_reset.argtypes = [C.c_void_p]
         L.accord_deps_visit.argtypes = [C.POINTER(_Deps), C.c_uint32, VISIT_FN, C.c_void_p]
@@ -649,6 +653,21 @@ class CommandStore:
             em, el, en = exec_at
             self._check(lib().accord_max_conflicts_fold_from(self._h, first, int(em), int(el), int(en), C.byref(o)))
         return msb, lsb, node, present, fast, int(o.folded)
+
+    def redundant_before(self, start=(), end=(), start_epoch=(), end_epoch=(), bound=(), min_epoch: int = 0):
+        """RedundantBefore of this store (local/RedundantBefore.java): its non-null entries (start, end]
+        ascending and disjoint, with [start_epoch, end_epoch) and shardAppliedOrInvalidatedBefore as a
+        stream position (NO_TXN = NONE); min_epoch = minUnsyncedEpoch.  Every later calculation returns
+        builder.build().with(RedundantBefore.collectDeps(...)) (messages/PreAccept.java:260-263).  No
+        entries = RedundantBefore.EMPTY."""
+        a = [np.ascontiguousarray(start, np.uint32), np.ascontiguousarray(end, np.uint32),
+             np.ascontiguousarray(start_epoch, np.uint64), np.ascontiguousarray(end_epoch, np.uint64),
+             np.ascontiguousarray(bound, np.uint32)]
+        if len({len(x) for x in a}) != 1:
+            raise IllegalArgumentException(-1, "RedundantBefore arrays differ in length")
+        self._check(lib().accord_redundant_before_set(
+            self._h, len(a[0]), a[0].ctypes.data_as(_u32p), a[1].ctypes.data_as(_u32p), a[2].ctypes.data_as(_u64p),
+            a[3].ctypes.data_as(_u64p), a[4].ctypes.data_as(_u32p), int(min_epoch)))
 
     def max_conflicts_reset(self):
         self._check(lib().accord_max_conflicts_reset(self._h))

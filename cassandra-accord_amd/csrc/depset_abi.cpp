@@ -231,7 +231,115 @@ struct InverseOwner {
 
 } // namespace
 
+namespace accord_impl {
+
+// The redundant RangeDeps of every txn of the computed batch (RedundantBefore.collectDeps,
+// redundant.hip), then PartialDeps.with of the computed deps and it (linearUnion on both sides,
+// as accord_deps_union): messages/PreAccept.java:262-263.
+int32_t redundant_apply(accord_store *s)
+{
+    const uint32_t n = s->n;
+    const size_t n1 = (size_t)n + 1;
+    hipStream_t st = s->stream;
+    DepSet &r = s->rb_set;
+    HIPCHECK(s, s->rb_cnt.ensure(3 * n1 * 4));
+    HIPCHECK(s, s->rb_zero.ensure(n1 * 4));
+    HIPCHECK(s, hipMemsetAsync(s->rb_zero.p, 0, n1 * 4, st));
+    HIPCHECK(s, r.rng_off.ensure(n1 * 4)); HIPCHECK(s, r.rval_off.ensure(n1 * 4)); HIPCHECK(s, r.r_off.ensure(n1 * 4));
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    {
+        accord::FillList fl;
+        fl.add(&dev->status.first, sizeof(dev->status.first), 0xFFFFFFFFu);
+        fl.add(&dev->status.overflow, 4, 0u);
+        fl.add(&dev->status.overflow_first, 4, 0xFFFFFFFFu);
+        accord::launch_fill_words(fl, st);
+    }
+    accord::RbParams p{};
+    p.n = n;
+    p.msb = s->msb.as<uint64_t>();
+    p.exec_msb = s->has_exec ? s->exec_msb.as<uint64_t>() : nullptr;
+    p.key_off = s->key_off.as<uint32_t>(); p.key_ord = s->key_ord.as<uint32_t>();
+    p.rng_off = s->R ? s->rng_off.as<uint32_t>() : nullptr;
+    p.rng_start = s->R ? s->rng_start.as<uint32_t>() : nullptr;
+    p.rng_end = s->R ? s->rng_end.as<uint32_t>() : nullptr;
+    p.m = s->rb_m;
+    p.e_start = s->rb_start.as<uint32_t>(); p.e_end = s->rb_end.as<uint32_t>(); p.e_bound = s->rb_bound.as<uint32_t>();
+    p.e_start_epoch = s->rb_sep.as<uint64_t>(); p.e_end_epoch = s->rb_eep.as<uint64_t>();
+    p.min_epoch = s->rb_min_epoch;
+    uint32_t *cnt = s->rb_cnt.as<uint32_t>();
+    p.cnt_rngs = cnt; p.cnt_vals = cnt + n1; p.cnt_r2v = cnt + 2 * n1;
+    p.status = &dev->status;
+    accord::launch_rb_count(p, st);
+    Scans sc;
+    RC(scans_init(s, sc));
+    RC(sc.add(p.cnt_rngs, r.rng_off.as<uint32_t>(), n));
+    RC(sc.add(p.cnt_vals, r.rval_off.as<uint32_t>(), n));
+    RC(sc.add(p.cnt_r2v, r.r_off.as<uint32_t>(), n));
+    unsigned long long tot[3];
+    RC(sc.read(tot));
+    {
+        HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(accord::DevStatus), hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+        if (s->pinned->status.overflow)
+            return fail(s, ACCORD_ERR_CAPACITY, "%u txns touch more than %u RedundantBefore entries (first: txn %u)",
+                        s->pinned->status.overflow, accord::RB_MAX, s->pinned->status.overflow_first);
+    }
+    HIPCHECK(s, r.rng_start.ensure(tot[0] * 4 + 4)); HIPCHECK(s, r.rng_end.ensure(tot[0] * 4 + 4));
+    HIPCHECK(s, r.rvals.ensure(tot[1] * 4 + 4)); HIPCHECK(s, r.r.ensure(tot[2] * 4 + 4));
+    p.rng_off_out = r.rng_off.as<uint32_t>(); p.val_off_out = r.rval_off.as<uint32_t>(); p.r2v_off_out = r.r_off.as<uint32_t>();
+    p.out_start = r.rng_start.as<uint32_t>(); p.out_end = r.rng_end.as<uint32_t>();
+    p.out_vals = r.rvals.as<uint32_t>(); p.out_r2v = r.r.as<int32_t>();
+    accord::launch_rb_fill(p, st);
+    HIPCHECK(s, hipGetLastError());
+    accord_deps parts[2];
+    RC(accord_deps_device_view(s, &parts[0]));
+    std::memset(&parts[1], 0, sizeof(parts[1]));
+    parts[1].n = n;
+    parts[1].kd_key_off = parts[1].kd_val_off = parts[1].kd_k2v_off = s->rb_zero.as<uint32_t>();
+    parts[1].rd_rngs_total = tot[0]; parts[1].rd_vals_total = tot[1]; parts[1].rd_r2v_total = tot[2];
+    parts[1].rd_rng_off = r.rng_off.as<uint32_t>(); parts[1].rd_rng_start = r.rng_start.as<uint32_t>();
+    parts[1].rd_rng_end = r.rng_end.as<uint32_t>(); parts[1].rd_val_off = r.rval_off.as<uint32_t>();
+    parts[1].rd_vals = r.rvals.as<uint32_t>(); parts[1].rd_r2v_off = r.r_off.as<uint32_t>();
+    parts[1].rd_r2v = r.r.as<int32_t>();
+    DepSet &o = next_set(s);
+    RC(union_side(s, parts, 2, false, o));
+    RC(union_side(s, parts, 2, true, o));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    publish(s, o, n);
+    return ACCORD_OK;
+}
+
+} // namespace accord_impl
+
 extern "C" {
+
+int32_t accord_redundant_before_set(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
+                                    const uint64_t *start_epoch, const uint64_t *end_epoch, const uint32_t *bound,
+                                    uint64_t min_epoch)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (m && (!start || !end || !start_epoch || !end_epoch || !bound)) return fail(s, ACCORD_ERR_ARG, "null argument");
+    for (uint32_t i = 0; i < m; ++i) {
+        if (!(start[i] < end[i])) return fail(s, ACCORD_ERR_RANGES, "RedundantBefore entry %u is empty", i);
+        if (i && end[i - 1] > start[i])
+            return fail(s, ACCORD_ERR_RANGES, "RedundantBefore entries %u, %u not ascending and disjoint", i - 1, i);
+    }
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    if (m) {
+        HIPCHECK(s, s->rb_start.ensure((size_t)m * 4)); HIPCHECK(s, s->rb_end.ensure((size_t)m * 4));
+        HIPCHECK(s, s->rb_bound.ensure((size_t)m * 4));
+        HIPCHECK(s, s->rb_sep.ensure((size_t)m * 8)); HIPCHECK(s, s->rb_eep.ensure((size_t)m * 8));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_start.p, start, (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_end.p, end, (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_bound.p, bound, (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_sep.p, start_epoch, (size_t)m * 8, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_eep.p, end_epoch, (size_t)m * 8, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+    }
+    s->rb_m = m;
+    s->rb_min_epoch = min_epoch;
+    return ACCORD_OK;
+}
 
 int32_t accord_deps_union(accord_store *s, uint32_t nparts, const accord_deps *parts)
 {

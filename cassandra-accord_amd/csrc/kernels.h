@@ -338,4 +338,24 @@ size_t levels_temp_bytes(uint32_t n);
 void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level, uint32_t *info,
                    void *temp, hipStream_t s);
 
+// ---- RedundantBefore.collectDeps (redundant.hip) ----
+constexpr uint32_t RB_NONE = 0xFFFFFFFFu;   // shardAppliedOrInvalidatedBefore == Timestamp.NONE
+constexpr uint32_t RB_MAX = 64;             // map entries one txn may touch
+struct RbParams {
+    uint32_t n;
+    const uint64_t *msb, *exec_msb;                    // executeAt epoch (exec_msb null: txnId)
+    const uint32_t *key_off, *key_ord, *rng_off, *rng_start, *rng_end;
+    uint32_t m;                                        // map entries, (e_start, e_end] ascending, disjoint
+    const uint32_t *e_start, *e_end, *e_bound;
+    const uint64_t *e_start_epoch, *e_end_epoch;
+    uint64_t min_epoch;
+    uint32_t *cnt_rngs, *cnt_vals, *cnt_r2v;           // count pass
+    const uint32_t *rng_off_out, *val_off_out, *r2v_off_out;
+    uint32_t *out_start, *out_end, *out_vals;
+    int32_t *out_r2v;
+    DevStatus *status;
+};
+void launch_rb_count(const RbParams &p, hipStream_t s);
+void launch_rb_fill(const RbParams &p, hipStream_t s);
+
 } // namespace accord

@@ -113,11 +113,13 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
                       &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2,
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
-                      &s->rc_end2, &s->rc_kind2, &s->rc_first};
+                      &s->rc_end2, &s->rc_kind2, &s->rc_first,
+                      &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero};
     accord_impl::shard_comm_destroy(s);
     accord_impl::pinned_arena_destroy(s);
     for (DevBuf *b : bufs) b->release();
     for (DepSet &d : s->ds) d.release();
+    s->rb_set.release();
     for (DevBuf &b : s->op_tmp) b.release();
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventDestroy(ev);
@@ -581,6 +583,7 @@ int32_t accord_deps_compute(accord_store *s)
     s->timing.pairs = P;
     s->timing.hist_entries = PH;
     s->computed = true;
+    if (s->rb_m) return accord_impl::redundant_apply(s);   // builder.build().with(redundant)
     return ACCORD_OK;
 }
 

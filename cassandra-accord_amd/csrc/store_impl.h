@@ -141,6 +141,12 @@ struct accord_store {
     DevBuf mc_state, mc_state2, mc_out, mc_cnt, mc_po;   // + per-txn pair counts / offsets of a pass
     uint32_t mc_next = 0;          // next txn of the uploaded batch the fold continues at
     float ops_ms = 0;
+    // RedundantBefore map (accord_redundant_before_set): rb_m non-null entries, and the redundant
+    // RangeDeps of the last computed batch before their union into the result
+    uint32_t rb_m = 0;
+    uint64_t rb_min_epoch = 0;
+    DevBuf rb_start, rb_end, rb_bound, rb_sep, rb_eep, rb_cnt, rb_zero;
+    DepSet rb_set;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
     accord_impl::PinnedBlock *dl_arena = nullptr;   // page-locked host arena of accord_deps_download
@@ -159,6 +165,8 @@ bool registered_mode(const accord_store *s);
 int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill);
 int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
 int32_t status_join_batch(accord_store *s);
+// RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp)
+int32_t redundant_apply(accord_store *s);
 }
 using accord_impl::fail;
 

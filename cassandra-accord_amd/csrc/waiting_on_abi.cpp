@@ -28,6 +28,8 @@ int32_t accord_waiting_on_compute(accord_store *s)
     if (!s->computed) return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_compute before accord_deps_compute");
     if (s->merged || s->has_txn_index)
         return fail(s, ACCORD_ERR_STATE, "WaitingOn levelling runs on a full stream's deps (gather to one store first)");
+    if (s->ds_cur >= 0)   // a union / slice / RedundantBefore result: the model's deps are the pipeline's own
+        return fail(s, ACCORD_ERR_STATE, "WaitingOn levelling runs on the computed deps, not a deps-set result");
     if (s->has_exec)   // the levelling model is defined on PreAccept deps
         return fail(s, ACCORD_ERR_STATE, "WaitingOn levelling runs on a PreAccept batch's deps, not an Accept batch");
     HIPCHECK(s, hipSetDevice(s->cfg.device));

@@ -174,6 +174,25 @@ typedef struct {
 int32_t accord_store_state(accord_store *store, accord_store_state_info *info);
 int32_t accord_store_reset(accord_store *store);               /* back to an empty CommandStore */
 
+/* ---- RedundantBefore.collectDeps (local/RedundantBefore.java:181-190, 418-421) ----
+ * PreAccept.calculatePartialDeps returns builder.build().with(redundant) (messages/PreAccept.java:
+ * 260-263), where `redundant` holds (entry.range, shardAppliedOrInvalidatedBefore) for every entry of
+ * the store's RedundantBefore map the txn's keys / ranges touch (ReducingRangeMap.foldl,
+ * utils/ReducingRangeMap.java:111-194: each entry once) unless Entry.outOfBounds(minEpoch, executeAt)
+ * (executeAt.epoch() < startEpoch || minEpoch >= endEpoch, :260-263) or the bound is NONE.
+ * The map is given as its m non-null entries: (start, end] ascending and disjoint, [start_epoch,
+ * end_epoch), and shardAppliedOrInvalidatedBefore as the GLOBAL STREAM POSITION of that TxnId in
+ * this store (ACCORD_NO_TXN = Timestamp.NONE).  The bound TxnIds are sync points the store has
+ * processed itself, so TxnId order is position order and deps values keep one value space.
+ * min_epoch = the message's minUnsyncedEpoch (EpochSupplier.constant, messages/PreAccept.java:103).
+ * Every later accord_deps_compute / accord_deps_batch returns the union; m = 0 clears the map
+ * (RedundantBefore.EMPTY).  A txn touching more than 64 entries is ACCORD_ERR_CAPACITY; entries
+ * not ascending / disjoint or empty are ACCORD_ERR_RANGES. */
+#define ACCORD_NO_TXN 0xFFFFFFFFu
+int32_t accord_redundant_before_set(accord_store *store, uint32_t m, const uint32_t *start, const uint32_t *end,
+                                    const uint64_t *start_epoch, const uint64_t *end_epoch, const uint32_t *bound,
+                                    uint64_t min_epoch);
+
 /* ---- synchronous batch entry: host in, host out ----
  * CommandStore.calculateDepsBatch(TxnId[], Seekables[], Timestamp[] executeAt, ...) ->
  * PartialDeps[]: identical to calling PreAccept.calculatePartialDeps (messages/PreAccept.java:

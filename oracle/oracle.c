@@ -1989,3 +1989,159 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
 }
 
 uint32_t or_lstore_size(const or_lstore *s) { return s->n; }
+
+
+/* ------------------------------------------------------------------------------------------
+ * RedundantBefore.collectDeps (local/RedundantBefore.java:418-421) = ReducingRangeMap.foldl
+ * (utils/ReducingRangeMap.java:111-194) of Entry.collectDep (:181-190) over the txn's keys or
+ * ranges, into a fresh PartialDeps builder (messages/PreAccept.java:251,260-262).  The map is the
+ * reference's (starts[], values[]) form with inclusiveEnds = true (intervals (starts[i],
+ * starts[i+1]], matching Range.EndInclusive); it is rebuilt here from the entry list the C ABI takes
+ * (a gap between two entries is a null value).  Bounds are stream positions (ACCORD_NO_TXN = NONE).
+ * ------------------------------------------------------------------------------------------ */
+/* SortedArrays.exponentialSearch over u32 (found: index, else -1 - insertion point) */
+static long rb_exp_search(const uint32_t *a, long from, long to, uint32_t key)
+{
+    long lo = from, hi = to;
+    while (lo < hi) {
+        long m = (lo + hi) >> 1;
+        if (a[m] < key) lo = m + 1; else if (a[m] > key) hi = m; else return m;
+    }
+    return -1 - lo;
+}
+/* AbstractRanges.findNext(from, key): the range containing key (start < key <= end), else
+ * -1 - the first range after it */
+static long rb_ranges_find(const uint32_t *rs, const uint32_t *re, long from, long to, uint32_t key)
+{
+    long lo = from, hi = to;
+    while (lo < hi) {
+        long m = (lo + hi) >> 1;
+        if (re[m] < key) lo = m + 1; else if (rs[m] >= key) hi = m; else return m;
+    }
+    return -1 - lo;
+}
+
+typedef struct {
+    uint32_t nstarts;           /* values: nstarts - 1 */
+    uint32_t *starts;
+    long *value;                /* entry index or -1 (null) */
+} rb_map;
+
+static int rb_map_build(rb_map *M, uint32_t m, const uint32_t *es, const uint32_t *ee)
+{
+    M->starts = (uint32_t *)malloc((2 * (size_t)m + 1) * sizeof(uint32_t));
+    M->value = (long *)malloc((2 * (size_t)m + 1) * sizeof(long));
+    M->nstarts = 0;
+    if (!M->starts || !M->value) return -1;
+    for (uint32_t i = 0; i < m; ++i) {
+        if (M->nstarts && M->starts[M->nstarts - 1] == es[i]) {
+            M->value[M->nstarts - 1] = i;                   /* adjacent: this interval opens here */
+        } else {
+            if (M->nstarts) M->value[M->nstarts - 1] = -1;  /* gap between entries: null */
+            M->starts[M->nstarts] = es[i];
+            M->value[M->nstarts] = i;
+            ++M->nstarts;
+        }
+        M->starts[M->nstarts] = ee[i];
+        M->value[M->nstarts] = -1;
+        ++M->nstarts;
+    }
+    return 0;
+}
+
+typedef struct {
+    const uint64_t *sep, *eep;
+    const uint32_t *bound;
+    uint64_t min_epoch, exec_epoch;
+    const uint32_t *es, *ee;
+    mm_builder *b;
+    int err;
+} rb_fold_ctx;
+
+static void rb_collect_dep(rb_fold_ctx *c, long e)      /* Entry.collectDep (:181-190) */
+{
+    if (e < 0 || c->err) return;
+    /* outOfBounds(lb = minEpoch, ub = executeAt): ub.epoch() < startEpoch || lb.epoch() >= endEpoch */
+    if (c->exec_epoch < c->sep[e] || c->min_epoch >= c->eep[e]) return;
+    if (c->bound[e] == 0xFFFFFFFFu) return;            /* shardAppliedOrInvalidatedBefore == NONE */
+    if (mmb_add(c->b, ((uint64_t)c->es[e] << 32) | c->ee[e], c->bound[e])) c->err = 1;
+}
+
+static void rb_foldl_keys(const rb_map *M, const uint32_t *keys, long nk, rb_fold_ctx *c)   /* :138-168 */
+{
+    const long nv = (long)M->nstarts - 1;
+    if (nv <= 0) return;
+    long i = 0, j = rb_exp_search(keys, 0, nk, M->starts[0]);
+    if (j < 0) j = -1 - j; else ++j;                       /* inclusiveEnds */
+    while (j < nk) {
+        i = rb_exp_search(M->starts, i, M->nstarts, keys[j]);
+        if (i < 0) i = -2 - i; else --i;                   /* inclusiveEnds */
+        if (i >= nv) return;
+        long nextj = rb_exp_search(keys, j, nk, M->starts[i + 1]);
+        if (nextj < 0) nextj = -1 - nextj; else ++nextj;   /* inclusiveEnds */
+        if (j != nextj && i >= 0) rb_collect_dep(c, M->value[i]);
+        ++i;
+        j = nextj;
+    }
+}
+
+static void rb_foldl_ranges(const rb_map *M, const uint32_t *rs, const uint32_t *re, long nr, rb_fold_ctx *c)   /* :170-208 */
+{
+    const long nv = (long)M->nstarts - 1;
+    if (nv <= 0) return;
+    long j = rb_ranges_find(rs, re, 0, nr, M->starts[0]);
+    if (j < 0) j = -1 - j; else if (re[j] == M->starts[0]) ++j;
+    long i = 0;
+    while (j < nr) {
+        const uint32_t start = rs[j];
+        long nexti = rb_exp_search(M->starts, i, M->nstarts, start);
+        if (nexti < 0) i = i > -2 - nexti ? i : -2 - nexti;
+        else if (nexti > i) i = nexti - 1;                 /* !inclusiveStarts() */
+        else i = nexti;
+        if (i >= nv) return;
+        long toj, nextj = rb_ranges_find(rs, re, j, nr, M->starts[i + 1]);
+        if (nextj < 0) toj = nextj = -1 - nextj;
+        else {
+            toj = nextj + 1;
+            if (re[nextj] == M->starts[i + 1]) ++nextj;
+        }
+        if (toj > j && i >= 0) rb_collect_dep(c, M->value[i]);
+        ++i;
+        j = nextj;
+    }
+}
+
+int or_redundant_collect(const or_stream *s, uint32_t m, const uint32_t *es, const uint32_t *ee, const uint64_t *sep,
+                         const uint64_t *eep, const uint32_t *bound, uint64_t min_epoch, or_deps *out)
+{
+    const uint32_t n = s->n;
+    ts_t *tbl = (ts_t *)malloc((size_t)(n ? n : 1) * sizeof(ts_t));
+    rb_map M = {0, NULL, NULL};
+    mm_builder kb, rb;
+    mm_out kd, rd;
+    int rc = -1;
+    if (!tbl) return -1;
+    for (uint32_t i = 0; i < n; ++i) { tbl[i].msb = s->msb[i]; tbl[i].lsb = s->lsb[i]; tbl[i].node = s->node[i]; }
+    for (uint32_t e = 0; e < m; ++e)
+        if (bound[e] != 0xFFFFFFFFu && bound[e] >= n) { free(tbl); return -2; }
+    mmb_init(&kb, tbl); mmb_init(&rb, tbl);
+    if (mmo_init(&kd) || mmo_init(&rd) || rb_map_build(&M, m, es, ee)) goto done;
+    for (uint32_t t = 0; t < n; ++t) {
+        const uint64_t em = s->exec_msb ? s->exec_msb[t] : s->msb[t];
+        rb_fold_ctx c = {sep, eep, bound, min_epoch, em >> 15, es, ee, &rb, 0};   /* Timestamp.epoch: msb >>> 15 */
+        const uint32_t r0 = s->rng_off ? s->rng_off[t] : 0, r1 = s->rng_off ? s->rng_off[t + 1] : 0;
+        if (r1 > r0) rb_foldl_ranges(&M, s->rng_start + r0, s->rng_end + r0, (long)(r1 - r0), &c);
+        else rb_foldl_keys(&M, s->key_ord + s->key_off[t], (long)(s->key_off[t + 1] - s->key_off[t]), &c);
+        if (c.err) goto done;
+        if (mmb_build(&kb, &kd, 0) || mmb_build(&rb, &rd, 1)) goto done;
+        mmb_reset(&kb); mmb_reset(&rb);
+    }
+    if (alloc_out(out, &kd, &rd, n)) goto done;
+    rc = 0;
+done:
+    free(M.starts); free(M.value);
+    mmb_free(&kb); mmb_free(&rb);
+    mmo_free(&kd); mmo_free(&rd);
+    free(tbl);
+    return rc;
+}

@@ -138,6 +138,12 @@ int or_levels_cfk(const or_stream *s, const or_deps *d, uint32_t *round_out);
  * TxnId table sorted ascending (index order == Timestamp order) ---- */
 /* Deps.merge / linearUnion of G sets of the same n txns (KeyDeps + RangeDeps; keys may overlap) */
 int or_deps_union(uint32_t G, const or_deps *parts, or_deps *out);
+/* RedundantBefore.collectDeps of every txn of the stream (local/RedundantBefore.java:181-190,
+ * 418-421; ReducingRangeMap.foldl, inclusiveEnds): m entries (es, ee] ascending and disjoint with
+ * [sep, eep) epochs and bound stream positions (0xFFFFFFFF = NONE); min_epoch = minUnsyncedEpoch.
+ * The redundant PartialDeps (RangeDeps only); PreAccept returns or_deps_union(deps, it). */
+int or_redundant_collect(const or_stream *s, uint32_t m, const uint32_t *es, const uint32_t *ee, const uint64_t *sep,
+                         const uint64_t *eep, const uint32_t *bound, uint64_t min_epoch, or_deps *out);
 /* KeyDeps.slice + RangeDeps.slice (+ trimUnusedValues) to select ranges (s,e]: per txn
  * sel_off[n+1] CSR, or sel_off NULL = the same nsel ranges for every txn */
 int or_deps_slice(const or_deps *d, const uint32_t *sel_off, const uint32_t *sel_start, const uint32_t *sel_end,

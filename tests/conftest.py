@@ -19,6 +19,10 @@ def pytest_configure(config):
         subprocess.run(["make", "-C", PKG, "-j8"], check=True, capture_output=True)
     if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    # a session that runs GPU tests brings torch's HIP runtime up before any test loads the library:
+    # a CPU test loading libaccord_deps.so first leaves the later device probe without a device
+    if "not gpu" not in (config.getoption("markexpr", "") or ""):
+        import torch  # noqa: F401
 
 
 @pytest.fixture(scope="session")

@@ -69,6 +69,8 @@ def lib():
         L.or_deps_union.argtypes = [C.c_uint32, C.POINTER(_OrDeps), C.POINTER(_OrDeps)]
         L.or_deps_slice.argtypes = [C.POINTER(_OrDeps), _u32p, _u32p, _u32p, C.c_uint32, C.POINTER(_OrDeps)]
         L.or_deps_invert.argtypes = [C.POINTER(_OrDeps), C.c_int, _u32p, C.POINTER(_i32p)]
+        L.or_redundant_collect.argtypes = [C.POINTER(_OrStream), C.c_uint32, _u32p, _u32p, _u64p, _u64p, _u32p,
+                                           C.c_uint64, C.POINTER(_OrDeps)]
         _LIB = L
     return _LIB
 
@@ -157,6 +159,25 @@ def deps_fast(s: Stream, window: int, batch_end=None) -> PartialDeps:
     o, keep = _or_stream(s, window, batch_end)
     d = _OrDeps()
     rc = lib().or_stream_deps_fast(C.byref(o), C.byref(d))
+    if rc != 0:
+        raise OracleError(rc)
+    try:
+        return _to_partial(d)
+    finally:
+        lib().or_deps_free(C.byref(d))
+
+
+def redundant_collect(s: Stream, start, end, start_epoch, end_epoch, bound, min_epoch: int) -> PartialDeps:
+    """RedundantBefore.collectDeps of every txn (the redundant PartialDeps of
+    PreAccept.calculatePartialDeps, messages/PreAccept.java:260-262); bound 0xFFFFFFFF = NONE."""
+    o, keep = _or_stream(s, 0)
+    a = [np.ascontiguousarray(start, np.uint32), np.ascontiguousarray(end, np.uint32),
+         np.ascontiguousarray(start_epoch, np.uint64), np.ascontiguousarray(end_epoch, np.uint64),
+         np.ascontiguousarray(bound, np.uint32)]
+    d = _OrDeps()
+    rc = lib().or_redundant_collect(C.byref(o), len(a[0]), a[0].ctypes.data_as(_u32p), a[1].ctypes.data_as(_u32p),
+                                    a[2].ctypes.data_as(_u64p), a[3].ctypes.data_as(_u64p), a[4].ctypes.data_as(_u32p),
+                                    min_epoch, C.byref(d))
     if rc != 0:
         raise OracleError(rc)
     try:
