@@ -81,6 +81,9 @@ struct KeyDepsParams {
     // Accept batch: per txn the global position bounding its candidates (txns started before its
     // executeAt); nullptr = PreAccept (bound = own position).  The txn itself is never a dep (p1).
     const uint32_t *bound_g;
+    // big txns (more keys than a wave has lanes, or more distinct far deps than the general kernel's
+    // far list): listed by the general kernel, built by a workgroup each (big_wex: scratch per pair)
+    uint32_t *big_list, *big_count, *big_wex;
 };
 
 // Where a batch sits in the store's stream: global positions start at min_gi, and (has_prev) the
@@ -128,6 +131,7 @@ void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *
 // kernel over the txns it hands back (p.fb_list / p.fb_count, count zeroed before the launch)
 size_t keydeps_fast_temp_bytes(uint32_t n);
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, void *recs, hipStream_t s);
+void launch_keydeps_big(const KeyDepsParams &p, hipStream_t s);
 // vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
 size_t compact_temp_bytes(uint64_t max_total);
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,

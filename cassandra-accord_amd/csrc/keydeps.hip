@@ -531,15 +531,10 @@ __global__ __launch_bounds__(256) void keydeps_sizes_kernel(uint32_t n, const ui
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t k0 = key_off[i], k1 = key_off[i + 1];
         uint32_t kc = 0, body = 0;
-        if (k1 - k0 > KD_KCAP) {
-            atomicAdd(&status->overflow, 1u);
-            atomicMin(&status->overflow_first, i);
-        } else {
-            for (uint32_t q = k0; q < k1; ++q) {
-                const uint32_t c = slice[q].wcnt;
-                kc += c ? 1u : 0u;
-                body += c;
-            }
+        for (uint32_t q = k0; q < k1; ++q) {
+            const uint32_t c = slice[q].wcnt;
+            kc += c ? 1u : 0u;
+            body += c;
         }
         cnt_keys[i] = kc;
         cnt_vub[i] = body;
@@ -718,8 +713,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
         lo0 = lo1; pos0 = pos1; wc0 = wc1; lo1 = lo2; pos1 = pos2; wc1 = wc2;
         incl0 = incl1; delta0 = delta1; raw_total0 = raw_total1;
 
-        if (k > KD_KCAP) {                              // reported by the sizes pass
-            if (lane == 0) stg(p.cnt_vals, i, 0u);
+        if (k > KD_KCAP) {                              // more keys than lanes: the big-txn kernel
+            if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = i;
             continue;
         }
         if (k == 0) {                                   // range txn (sized by rangekeys) / no key here
@@ -775,12 +770,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW
         }
         wave_lds_sync();
         const uint32_t F = L.far_count;
-        if (F > KD_FARCAP) {
-            if (lane == 0) {
-                atomicAdd(&p.status->overflow, 1u);
-                atomicMin(&p.status->overflow_first, i);
-                stg(p.cnt_vals, i, 0u);
-            }
+        if (F > KD_FARCAP) {                            // more far deps than the list holds: big-txn kernel
+            if (lane == 0) p.big_list[atomicAdd(p.big_count, 1u)] = i;
             continue;
         }
 
@@ -1122,6 +1113,168 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Big txns: more keys than a wave has lanes (k > KD_KCAP) or more distinct deps older than the
+// near span than the general kernel's far list holds (> KD_FARCAP) -- no size limit besides the
+// output arrays.  One workgroup per listed txn (the general kernel lists them):
+//   keys / keysToTxnIds header : block scans over the pairs in chunks of 256 (same values as the
+//                                other kernels: keys with >= 1 witnessed entry, end offsets)
+//   union                      : windows of BK_SPAN txns, from the smallest witnessed dep up; per
+//                                window an LDS bitmap (OR of the window's witnessed entries), word
+//                                popcount prefixes, then every witnessed entry of the window writes
+//                                its rank at its body position and the bitmap expands into txnIds
+// A wave walks one pair's slice at a time (64 entries per step, ballot-counted body positions from
+// the pair's witnessed prefix), so long slices and many keys both spread over the block.
+// ---------------------------------------------------------------------------------------------
+constexpr int BK_THREADS = 256;
+constexpr uint32_t BK_WORDS = 8192;                 // 64 KiB of bitmap
+constexpr uint32_t BK_SPAN = BK_WORDS * 64;         // txns per window
+constexpr uint32_t BK_WPT = BK_WORDS / BK_THREADS;  // bitmap words per thread
+
+// exclusive block scan of v (all threads of the block call it); total of the block in `tot`
+__device__ __forceinline__ uint32_t bk_excl_scan(uint32_t v, uint32_t &tot, uint32_t *sh)
+{
+    const uint32_t incl = wave_incl_scan(v), w = wave_id();
+    if (lane_id() == 63) sh[w] = incl;
+    __syncthreads();
+    uint32_t off = 0, t = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < BK_THREADS / 64; ++q) { off += q < w ? sh[q] : 0u; t += sh[q]; }
+    __syncthreads();
+    tot = t;
+    return off + incl - v;
+}
+
+__device__ __forceinline__ uint32_t bk_min(uint32_t v, uint32_t *sh)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    if (lane_id() == 0) sh[wave_id()] = v;
+    __syncthreads();
+    uint32_t m = sh[0];
+#pragma unroll
+    for (uint32_t q = 1; q < BK_THREADS / 64; ++q) m = min(m, sh[q]);
+    __syncthreads();
+    return m;
+}
+
+__global__ __launch_bounds__(BK_THREADS) void keydeps_big_kernel(KeyDepsParams p)
+{
+    __shared__ unsigned long long bm[BK_WORDS];
+    __shared__ uint32_t pre[BK_WORDS];
+    __shared__ uint32_t sh[BK_THREADS / 64];
+    const uint32_t tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t count = *p.big_count;
+    for (uint32_t b = blockIdx.x; b < count; b += gridDim.x) {
+        const uint32_t i = p.big_list[b];
+        const uint32_t k0 = p.key_off[i], k = p.key_off[i + 1] - k0;
+        const uint32_t kind = (uint32_t)(p.lsb[i] >> 1) & 7, wmask = witness_mask(kind);
+        const uint32_t gi = p.txn_index ? p.txn_index[i] : i;
+        const uint32_t key_base = p.kd_key_off[i], val_base = p.vub_off[i], k2v_base = p.kd_k2v_off[i];
+        // ---- keys, header, each pair's witnessed prefix ----
+        uint32_t kc = 0;
+        for (uint32_t c = 0; c < k; c += BK_THREADS) {
+            const uint32_t q = c + tid;
+            uint32_t t;
+            (void)bk_excl_scan(q < k && p.slice[k0 + q].wcnt ? 1u : 0u, t, sh);
+            kc += t;
+        }
+        uint32_t run_kc = 0, run_wc = 0;
+        for (uint32_t c = 0; c < k; c += BK_THREADS) {
+            const uint32_t q = c + tid;
+            const uint32_t wc = q < k ? p.slice[k0 + q].wcnt : 0u;
+            uint32_t tk, tw;
+            const uint32_t xk = bk_excl_scan(wc ? 1u : 0u, tk, sh) + run_kc;
+            const uint32_t xw = bk_excl_scan(wc, tw, sh) + run_wc;
+            if (q < k) {
+                p.big_wex[k0 + q] = xw;
+                if (wc) {
+                    p.kd_keys[key_base + xk] = p.key_ord[k0 + q];
+                    p.kd_k2v[k2v_base + xk] = (int32_t)(kc + xw + wc);
+                }
+            }
+            run_kc += tk;
+            run_wc += tw;
+        }
+        __syncthreads();
+        // ---- the smallest witnessed dep ----
+        uint32_t mn = 0xFFFFFFFFu;
+        for (uint32_t q = w; q < k; q += BK_THREADS / 64) {
+            const PairSlice ps = p.slice[k0 + q];
+            for (uint32_t x = ps.lo + lane; x < ps.pos; x += 64) {
+                const uint32_t ev = p.hist[x], j = ev & ENT_TXN_MASK;
+                if (((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi) mn = min(mn, j);
+            }
+        }
+        uint32_t wlo = bk_min(mn, sh);
+        uint32_t base = 0;                                  // distinct deps below the window
+        while (wlo != 0xFFFFFFFFu) {
+            // window [wlo, wlo + BK_SPAN)
+            for (uint32_t x = tid; x < BK_WORDS; x += BK_THREADS) bm[x] = 0ull;
+            __syncthreads();
+            uint32_t nx = 0xFFFFFFFFu;                      // smallest witnessed dep past the window
+            for (uint32_t q = w; q < k; q += BK_THREADS / 64) {
+                const PairSlice ps = p.slice[k0 + q];
+                for (uint32_t x = ps.lo + lane; x < ps.pos; x += 64) {
+                    const uint32_t ev = p.hist[x], j = ev & ENT_TXN_MASK;
+                    if (!(((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi)) continue;
+                    if (j >= wlo && j - wlo < BK_SPAN) atomicOr(&bm[(j - wlo) >> 6], 1ull << ((j - wlo) & 63));
+                    else if (j >= wlo) nx = min(nx, j);     // past the window (earlier ones are done)
+                }
+            }
+            __syncthreads();
+            uint32_t pc[BK_WPT], mine = 0;
+#pragma unroll
+            for (uint32_t y = 0; y < BK_WPT; ++y) { pc[y] = (uint32_t)__popcll(bm[tid * BK_WPT + y]); mine += pc[y]; }
+            uint32_t wtot;
+            uint32_t ex = bk_excl_scan(mine, wtot, sh) + base;
+#pragma unroll
+            for (uint32_t y = 0; y < BK_WPT; ++y) {
+                const uint32_t x = tid * BK_WPT + y;
+                pre[x] = ex;
+                unsigned long long bits = bm[x];
+                uint32_t o = ex;
+                while (bits) {                              // the window's txnIds, ascending
+                    const uint32_t bit = (uint32_t)__builtin_ctzll(bits);
+                    bits &= bits - 1ull;
+                    stg(p.vgap, val_base + o++, wlo + x * 64 + bit);
+                }
+                ex += pc[y];
+            }
+            __syncthreads();
+            // ranks of the window's witnessed entries at their body positions
+            for (uint32_t q = w; q < k; q += BK_THREADS / 64) {
+                const PairSlice ps = p.slice[k0 + q];
+                uint32_t run = p.big_wex[k0 + q];
+                for (uint32_t x0 = ps.lo; x0 < ps.pos; x0 += 64) {
+                    const uint32_t x = x0 + lane;
+                    uint32_t ev = 0, j = 0;
+                    bool wit = false;
+                    if (x < ps.pos) {
+                        ev = p.hist[x];
+                        j = ev & ENT_TXN_MASK;
+                        wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;
+                    }
+                    const uint64_t bal = __ballot(wit);
+                    if (wit && j >= wlo && j - wlo < BK_SPAN) {
+                        const uint32_t d = j - wlo;
+                        const uint32_t rank = pre[d >> 6] + (uint32_t)__popcll(bm[d >> 6] & ((1ull << (d & 63)) - 1ull));
+                        stg(p.kd_k2v, k2v_base + kc + run + (uint32_t)__popcll(bal & lt), (int32_t)rank);
+                    }
+                    run += (uint32_t)__popcll(bal);
+                }
+            }
+            base += wtot;
+            wlo = bk_min(nx, sh);
+            __syncthreads();
+        }
+        if (tid == 0) p.cnt_vals[i] = base;
+        __syncthreads();
+    }
+}
+
 void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_t s)
 {
     if (p.n == 0) return;
@@ -1327,6 +1480,13 @@ void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *
 
 size_t keydeps_fast_temp_bytes(uint32_t n) { return fk_temp_bytes(n); }
 
+// one workgroup per listed big txn (the list is short: a fixed grid that loops over it)
+void launch_keydeps_big(const KeyDepsParams &p, hipStream_t s)
+{
+    if (p.n == 0) return;
+    hipLaunchKernelGGL(keydeps_big_kernel, dim3(512), dim3(BK_THREADS), 0, s, p);
+}
+
 void launch_keydeps_fill(const KeyDepsParams &p, int wpl, void *recs, hipStream_t s)
 {
     // fast path over every txn; the general kernel over the fallback list (fb_count zeroed by the
@@ -1336,10 +1496,12 @@ void launch_keydeps_fill(const KeyDepsParams &p, int wpl, void *recs, hipStream_
         q.fb_list = nullptr;
         q.fb_count = nullptr;
         launch_keydeps(q, wpl, s);
+        launch_keydeps_big(p, s);
         return;
     }
     launch_keydeps_fast(p, wpl, recs, s);
     launch_keydeps(p, wpl, s);
+    launch_keydeps_big(p, s);
 }
 
 size_t compact_temp_bytes(uint64_t max_total) { return ((max_total + CV_OUT - 1) / CV_OUT + 1) * 4 + 64; }

@@ -114,7 +114,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2,
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
                       &s->rc_end2, &s->rc_kind2, &s->rc_first,
-                      &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero};
+                      &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero};
     accord_impl::shard_comm_destroy(s);
     accord_impl::pinned_arena_destroy(s);
     for (DevBuf *b : bufs) b->release();
@@ -294,6 +294,8 @@ int32_t accord_deps_compute(accord_store *s)
     if (nrt) HIPCHECK(s, s->rk_cls.ensure(accord::rangekeys_class_bytes(nrt)));
 
     HIPCHECK(s, s->fk_list.ensure((size_t)n * 4 + 64));
+    HIPCHECK(s, s->bk_list.ensure((size_t)n * 4 + 64));
+    HIPCHECK(s, s->bk_wex.ensure((size_t)P * 4 + 4));
     // RangeDeps for the batch: its own range commands and, in a resident store, the carried ones
     const uint32_t ncr = s->resident ? s->rc_n : 0u;
     const bool rdeps = R || ncr;
@@ -309,6 +311,7 @@ int32_t accord_deps_compute(accord_store *s)
         fl.add(s->seg_start.p, (size_t)nkeys * 4, 0u);
         fl.add(s->seg_end.p, (size_t)nkeys * 4, 0u);
         fl.add(s->fk_list.p, 4, 0u);                                   // fallback list count
+        fl.add(s->bk_list.p, 4, 0u);                                   // big-txn list count
         if (nrt) fl.add(s->rk_cls.p, 8 * 4, 0u);                        // union class list counts
         if (rdeps) {
             fl.add(s->rd_big.p, 4, 0u);                                 // big range-hit list count
@@ -498,6 +501,9 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->fk_recs.ensure(accord::keydeps_fast_temp_bytes(n)));
     kp.fb_count = s->fk_list.as<uint32_t>();
     kp.fb_list = kp.fb_count + 16;
+    kp.big_count = s->bk_list.as<uint32_t>();
+    kp.big_list = kp.big_count + 16;
+    kp.big_wex = s->bk_wex.as<uint32_t>();
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {

@@ -80,6 +80,7 @@ struct accord_store {
     // work
     DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, tmp_ent, seg_start, seg_end, radix_tmp;
     DevBuf hist, slice, hist_tmp, cnt_vub, vub_off, vgap, fk_recs, fk_list, cv_tmp;
+    DevBuf bk_list, bk_wex;        // big txns (keydeps_big_kernel): count | list, per-pair scratch
     DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
     DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v, rd_big, rk_cp, rk_cnt, rk_off, rk_slices, rk_cls;
     uint64_t rk_keys_total = 0;      // keys of all range txns' ranges clipped to the store (upload)
