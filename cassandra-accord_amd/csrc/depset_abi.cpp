@@ -3,6 +3,7 @@
 // stream, with one host read of the sizes between count and fill passes.
 #include "store_impl.h"
 
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -344,14 +345,33 @@ int32_t accord_redundant_before_set(accord_store *s, uint32_t m, const uint32_t 
 int32_t accord_deps_union(accord_store *s, uint32_t nparts, const accord_deps *parts)
 {
     RC(check_views(s, nparts, parts));
-    if (nparts > 64) return fail(s, ACCORD_ERR_CAPACITY, "union of %u sets (1..64 supported)", nparts);
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     op_begin(s);
-    DepSet &o = next_set(s);
-    RC(union_side(s, parts, nparts, false, o));
-    RC(union_side(s, parts, nparts, true, o));
+    // up to 64 parts per pass; more fold into the running result (linearUnion is associative).  A
+    // later pass writes the buffer the store's current deps sat in, so those must come first.
+    for (uint32_t g = 64; g < nparts; ++g)
+        for (const DepSet &d : s->ds)
+            if (d.key_off.p && parts[g].kd_key_off == d.key_off.as<uint32_t>())
+                return fail(s, ACCORD_ERR_ARG, "union part %u is this store's own deps set: pass it among the first 64", g);
+    const uint32_t n = parts[0].n;
+    uint32_t done = 0;
+    std::vector<accord_deps> grp;
+    while (done < nparts) {
+        grp.clear();
+        if (done) {
+            grp.emplace_back();
+            RC(accord_deps_device_view(s, &grp.back()));   // the union so far
+        }
+        const uint32_t take = std::min<uint32_t>(nparts - done, 64u - (uint32_t)grp.size());
+        grp.insert(grp.end(), parts + done, parts + done + take);
+        done += take;
+        DepSet &o = next_set(s);
+        RC(union_side(s, grp.data(), (uint32_t)grp.size(), false, o));
+        RC(union_side(s, grp.data(), (uint32_t)grp.size(), true, o));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+        publish(s, o, n);
+    }
     RC(op_end(s));
-    publish(s, o, parts[0].n);
     return ACCORD_OK;
 }
 

@@ -168,8 +168,12 @@ int32_t accord_deps_merge(accord_store *s, uint32_t nparts, const accord_deps *p
         ps[g] = Part{parts[g].kd_key_off, parts[g].kd_keys, parts[g].kd_val_off, parts[g].kd_vals,
                      parts[g].kd_k2v_off, parts[g].kd_k2v};
     }
-    if (ranges) return union_general(s, nparts, parts);
-    return merge_parts(s, ps, n, txn_lo);
+    // RangeDeps, more parts than the merge kernel's lanes, or a txn past its union capacity: the
+    // general union (linearUnion on both sides gives the same sets for key-disjoint parts)
+    if (ranges || nparts > 64) return union_general(s, nparts, parts);
+    const int32_t rc = merge_parts(s, ps, n, txn_lo);
+    if (rc == ACCORD_ERR_CAPACITY) return union_general(s, nparts, parts);
+    return rc;
 }
 
 int32_t accord_comm_unique_id(void *id128)

@@ -246,7 +246,7 @@ int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merg
  * is index order.  union and slice make their result this store's current deps (read it with
  * accord_deps_device_view / accord_deps_download; a source may be this store's own current deps).
  *
- * accord_deps_union: Deps.merge / PartialDeps.with of nparts (1..64) sets of the same n txns, KeyDeps
+ * accord_deps_union: Deps.merge / PartialDeps.with of nparts (>= 1; 64 per pass) sets of the same n txns, KeyDeps
  *   and RangeDeps, keys may overlap -- RelationMultiMap.linearUnion (utils/RelationMultiMap.java:
  *   561-816) via KeyDeps.merge (primitives/KeyDeps.java:115-140) / RangeDeps.merge
  *   (primitives/RangeDeps.java:101-126): the coordinator-side merge of replica replies

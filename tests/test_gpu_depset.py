@@ -54,6 +54,23 @@ def test_union_with_empty_txns_and_long_lists():
         _eq(out.download(), O.deps_union([pa, pb]))
 
 
+def test_union_of_more_than_64_sets():
+    # 130 parts (10 distinct sets, repeated): three passes of at most 64 parts each
+    rng = np.random.default_rng(17)
+    n = 200
+    parts = [from_canon(random_depset(rng, n, 3000, 100, 8, 3, 30, shared_keys=np.arange(30))) for _ in range(10)]
+    stores = [_uploaded(p) for p in parts]
+    try:
+        with _store() as out:
+            out.union([stores[g % 10] for g in range(130)])
+            _eq(out.download(), O.deps_union(parts))
+            with pytest.raises(IllegalArgumentException):    # own deps past the first 64 parts
+                out.union([stores[g % 10] for g in range(70)] + [out])
+    finally:
+        for s in stores:
+            s.close()
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_slice_random_shared_and_per_txn(seed):
     rng = np.random.default_rng(40 + seed)

@@ -118,3 +118,24 @@ def test_merge_rejects_overlapping_parts(gpu_device):
             st.compute()
         with pytest.raises(IllegalArgumentException):
             m.merge([a, b])
+
+
+def test_merge_of_more_than_64_stores(gpu_device):
+    # 80 key-disjoint stores: past the merge kernel's 64 lanes the general union folds 64 parts per pass
+    ks, W = 4000, 64
+    s = generate_stream(6000, 6, ks, 0.99, 0.5, seed=37)
+    stores = []
+    try:
+        for lo, hi in even_split(ks, 80):
+            st = CommandStore(device=0, key_lo=lo, key_hi=hi, window=W)
+            st.upload(s.restrict_keys(lo, hi))
+            st.compute()
+            stores.append(st)
+        with CommandStore(device=0, key_lo=0, key_hi=ks, window=W) as merger:
+            merger.merge(stores, txn_lo=0)
+            got = merger.download()
+    finally:
+        for st in stores:
+            st.close()
+    want = O.deps_fast(s, W)
+    assert got.first_difference(want) is None, got.first_difference(want)
