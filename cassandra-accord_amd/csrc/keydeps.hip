@@ -416,6 +416,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
 // number at most W + 1 and the bound lies in [p - W, p]: the predicate "same key and txn >= i - W"
 // is monotone over that range of the key-major history, and the search needs neither the segment
 // start nor a global fallback.
+template <uint32_t HALO>
 __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     uint32_t P, uint32_t window, uint32_t steps, const uint32_t *__restrict__ sorted_key,
     const uint32_t *__restrict__ sorted_pair, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ seg_start,
@@ -423,10 +424,10 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     const ClassCarry *__restrict__ ccarry, const uint32_t *__restrict__ seg_end, const uint32_t *__restrict__ pair_bound,
     PairSlice *__restrict__ slice, uint32_t ncarry)
 {
-    __shared__ uint32_t tx[H2_HALO + H2_TILE];
-    __shared__ uint32_t tk[H2_HALO + H2_TILE];
+    __shared__ uint32_t tx[HALO + H2_TILE];
+    __shared__ uint32_t tk[HALO + H2_TILE];
     const uint32_t base = blockIdx.x * H2_TILE;
-    const uint32_t lds_lo = base > H2_HALO ? base - H2_HALO : 0u;
+    const uint32_t lds_lo = base > HALO ? base - HALO : 0u;
     const uint32_t end = min(P, base + H2_TILE);
     uint32_t key[H2_ITEMS], q[H2_ITEMS], a[H2_ITEMS];
 #pragma unroll
@@ -890,6 +891,9 @@ __global__ __launch_bounds__(256) void txnrec_kernel(KeyDepsParams p, TxnRec *__
     }
 }
 
+#ifndef ACCORD_FK_MASK
+#define ACCORD_FK_MASK 0
+#endif
 constexpr int FK_CB = 6;                      // candidate batches of 64 a fast-path txn may use
 constexpr uint32_t FK_RAW = 64u * FK_CB;      // raw candidates the fast path takes
 
@@ -935,6 +939,43 @@ __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn
     const uint32_t excl = incl - raw;
     const int32_t delta = (int32_t)x.lo - (int32_t)excl;
     const uint32_t rt = readlane(incl, 7);
+#if ACCORD_FK_MASK
+    // non-empty slots compacted to lanes 0..: their starts are distinct, so a candidate's slot is the
+    // number of starts at or below it, read off a 64-bit boundary mask per batch (SALU) by mbcnt
+    const uint64_t ne = __ballot(lane < 8 && raw != 0) & 0xFFull;
+    const uint32_t ci = (uint32_t)__popcll(ne & lanemask_lt());
+    const bool mine = lane < 8 && raw != 0;
+    const int32_t dc = __builtin_amdgcn_ds_permute((int)((mine ? ci : 63u) << 2), delta);
+    const uint32_t xc = (uint32_t)__builtin_amdgcn_ds_permute((int)((mine ? ci : 63u) << 2), (int)excl);
+    const uint32_t nslots = (uint32_t)__popcll(ne);
+    uint32_t bq[8];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) bq[q] = (uint32_t)q < nslots ? readlane(xc, q) : 0xFFFFFFFFu;
+    const bool take = k <= 8 && rt <= FK_RAW;
+#pragma unroll
+    for (int c = 0; c < FK_CB; ++c) e[c] = KD_NONE;
+    uint32_t below = 0;                                   // starts before the batch (uniform)
+#pragma unroll
+    for (int c = 0; c < FK_CB; ++c) {
+        if (!take || (uint32_t)c * 64u >= rt) break;      // wave-uniform
+        const uint32_t b0 = c * 64;
+        uint64_t m = 0;
+        uint32_t nb = 0;
+#pragma unroll
+        for (int q = 1; q < 8; ++q) {
+            const uint32_t o = bq[q] - b0;                // wraps for starts before the batch
+            m |= o < 64u ? (1ull << o) : 0ull;
+            nb += bq[q] < b0 ? 1u : 0u;
+        }
+        below = nb;
+        const uint32_t slot = below + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) + (uint32_t)((m >> lane) & 1ull);
+        const int32_t d = __builtin_amdgcn_ds_bpermute((int)(slot << 2), dc);
+        const uint32_t r = b0 + lane;
+        if (r < rt) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
+    }
+    return rt;
+#else
     uint32_t eq[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) eq[q] = readlane(excl, q + 1);
@@ -952,6 +993,7 @@ __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn
         if (r < rt) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
     }
     return rt;
+#endif
 }
 
 struct alignas(16) BmWord {
@@ -1458,7 +1500,10 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
     if (window <= H2_HALO) {
         uint32_t steps = 0;
         while ((1u << steps) <= window) ++steps;     // ceil(log2(window + 1)) halvings of a <= window range
-        hipLaunchKernelGGL(history2_lockstep_kernel, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P,
+        // the halo only has to reach back W positions: the smallest that does keeps the block's LDS small
+        auto h2 = window <= 256 ? history2_lockstep_kernel<256> : window <= 512 ? history2_lockstep_kernel<512>
+                : window <= 1024 ? history2_lockstep_kernel<1024> : history2_lockstep_kernel<H2_HALO>;
+        hipLaunchKernelGGL(h2, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P,
                            window, steps, sorted_key, sorted_pair, hist, seg_start, pw_local, tile_max, c_local, ccarry,
                            seg_end, pair_bound, slice, carry);
         return;
