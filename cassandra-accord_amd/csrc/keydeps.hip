@@ -891,9 +891,6 @@ __global__ __launch_bounds__(256) void txnrec_kernel(KeyDepsParams p, TxnRec *__
     }
 }
 
-#ifndef ACCORD_FK_MASK
-#define ACCORD_FK_MASK 0
-#endif
 constexpr int FK_CB = 6;                      // candidate batches of 64 a fast-path txn may use
 constexpr uint32_t FK_RAW = 64u * FK_CB;      // raw candidates the fast path takes
 
@@ -939,43 +936,6 @@ __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn
     const uint32_t excl = incl - raw;
     const int32_t delta = (int32_t)x.lo - (int32_t)excl;
     const uint32_t rt = readlane(incl, 7);
-#if ACCORD_FK_MASK
-    // non-empty slots compacted to lanes 0..: their starts are distinct, so a candidate's slot is the
-    // number of starts at or below it, read off a 64-bit boundary mask per batch (SALU) by mbcnt
-    const uint64_t ne = __ballot(lane < 8 && raw != 0) & 0xFFull;
-    const uint32_t ci = (uint32_t)__popcll(ne & lanemask_lt());
-    const bool mine = lane < 8 && raw != 0;
-    const int32_t dc = __builtin_amdgcn_ds_permute((int)((mine ? ci : 63u) << 2), delta);
-    const uint32_t xc = (uint32_t)__builtin_amdgcn_ds_permute((int)((mine ? ci : 63u) << 2), (int)excl);
-    const uint32_t nslots = (uint32_t)__popcll(ne);
-    uint32_t bq[8];
-#pragma unroll
-    for (int q = 1; q < 8; ++q) bq[q] = (uint32_t)q < nslots ? readlane(xc, q) : 0xFFFFFFFFu;
-    const bool take = k <= 8 && rt <= FK_RAW;
-#pragma unroll
-    for (int c = 0; c < FK_CB; ++c) e[c] = KD_NONE;
-    uint32_t below = 0;                                   // starts before the batch (uniform)
-#pragma unroll
-    for (int c = 0; c < FK_CB; ++c) {
-        if (!take || (uint32_t)c * 64u >= rt) break;      // wave-uniform
-        const uint32_t b0 = c * 64;
-        uint64_t m = 0;
-        uint32_t nb = 0;
-#pragma unroll
-        for (int q = 1; q < 8; ++q) {
-            const uint32_t o = bq[q] - b0;                // wraps for starts before the batch
-            m |= o < 64u ? (1ull << o) : 0ull;
-            nb += bq[q] < b0 ? 1u : 0u;
-        }
-        below = nb;
-        const uint32_t slot = below + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) + (uint32_t)((m >> lane) & 1ull);
-        const int32_t d = __builtin_amdgcn_ds_bpermute((int)(slot << 2), dc);
-        const uint32_t r = b0 + lane;
-        if (r < rt) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
-    }
-    return rt;
-#else
     uint32_t eq[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) eq[q] = readlane(excl, q + 1);
@@ -993,7 +953,6 @@ __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn
         if (r < rt) e[c] = ldg(p.hist, (uint32_t)((int32_t)r + d));
     }
     return rt;
-#endif
 }
 
 struct alignas(16) BmWord {
