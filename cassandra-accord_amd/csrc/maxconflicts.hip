@@ -285,6 +285,155 @@ __global__ void __launch_bounds__(256) mc_fold_kernel(uint32_t first, uint32_t l
     if (!fast && !known_exec && t != ov_t && kind != 2u) atomicMin(stop, t);
 }
 
+// ---- PreAccept batches: monotone values ----
+// Without exec_* every merged value is the txn's TxnId (the batch is strictly ascending) except the
+// pass's first txn when the caller supplied its executeAt (accord_max_conflicts_fold_from): that txn
+// is the head of every key segment it touches (stable sort, first in stream order).  The fold over a
+// segment prefix [seed, v_f?, v_1 < v_2 < ...] is then max_keep_old(max_keep_old(seed, v_f), v_last):
+// only the LAST visible txn before the pair matters, which a plain u32 max-scan of sorted positions
+// finds.  Each pair gets a 4-byte code -- that txn (or none) and whether the override txn precedes it
+// -- and the fold gathers the timestamps, instead of the general path's 24-byte prefix per pair.
+constexpr uint32_t MM_THREADS = 256, MM_ITEMS = 4, MM_TILE = MM_THREADS * MM_ITEMS;
+constexpr uint32_t MM_NONE = 0x7FFFFFFFu, MM_F = 0x80000000u;
+
+__device__ __forceinline__ bool mm_visible(uint32_t t, const uint64_t *lsb) { return ((uint32_t)(lsb[t] >> 1) & 7) != 2u; }
+
+// segment starts + per tile the largest (sorted position + 1) of a visible non-override pair
+__global__ void __launch_bounds__(MM_THREADS) mm_tile_kernel(uint32_t P, const uint32_t *__restrict__ sk,
+                                                             const uint32_t *__restrict__ sv,
+                                                             const uint64_t *__restrict__ lsb, uint32_t ov_t,
+                                                             uint32_t *__restrict__ segstart,
+                                                             uint32_t *__restrict__ tile_max)
+{
+    __shared__ uint32_t wm[MM_THREADS / 64];
+    const uint32_t q0 = blockIdx.x * MM_TILE + threadIdx.x * MM_ITEMS;
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < MM_ITEMS; ++j) {
+        const uint32_t q = q0 + j;
+        if (q >= P) break;
+        const uint32_t k = sk[q], t = sv[q];
+        if (q == 0 || sk[q - 1] != k) segstart[k] = q;
+        if (t != ov_t && mm_visible(t, lsb)) m = q + 1;
+    }
+    m = wave_incl_max(m);
+    if (lane_id() == 63) wm[wave_id()] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x = 0;
+        for (uint32_t w = 0; w < MM_THREADS / 64; ++w) x = max(x, wm[w]);
+        tile_max[blockIdx.x] = x;
+    }
+}
+
+// exclusive max-scan of the tile maxima (one block)
+__global__ void __launch_bounds__(256) mm_carry_kernel(uint32_t ntiles, uint32_t *__restrict__ tile_max)
+{
+    __shared__ uint32_t wm[4];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < ntiles; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < ntiles ? tile_max[i] : 0u;
+        const uint32_t incl = wave_incl_max(v);
+        if (lane_id() == 63) wm[wave_id()] = incl;
+        __syncthreads();
+        uint32_t ex = __shfl_up(incl, 1, 64);
+        if (lane_id() == 0) ex = 0;
+        uint32_t blk = 0;
+        for (uint32_t w = 0; w < 4; ++w) {
+            if (w < wave_id()) ex = max(ex, wm[w]);
+            blk = max(blk, wm[w]);
+        }
+        if (i < ntiles) tile_max[i] = max(carry, ex);
+        carry = max(carry, blk);
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ TsV mm_value(uint32_t t, const uint64_t *lsb, const McValues &mv)
+{
+    return elem_value(t, lsb, mv);
+}
+
+// per pair (sorted order): its code at its pair index; per segment end: the key's new map value
+__global__ void __launch_bounds__(MM_THREADS) mm_apply_kernel(uint32_t P, const uint32_t *__restrict__ sk,
+                                                              const uint32_t *__restrict__ sv,
+                                                              const uint32_t *__restrict__ se,
+                                                              const uint64_t *__restrict__ lsb, McValues mv,
+                                                              const uint32_t *__restrict__ segstart,
+                                                              const uint32_t *__restrict__ carry,
+                                                              const TsV *__restrict__ state,
+                                                              uint32_t *__restrict__ code, TsV *__restrict__ state_out)
+{
+    __shared__ uint32_t wm[MM_THREADS / 64];
+    const uint32_t q0 = blockIdx.x * MM_TILE + threadIdx.x * MM_ITEMS;
+    uint32_t v[MM_ITEMS], k[MM_ITEMS], t[MM_ITEMS];
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < MM_ITEMS; ++j) {
+        const uint32_t q = q0 + j;
+        v[j] = 0; k[j] = 0; t[j] = 0;
+        if (q < P) {
+            k[j] = sk[q]; t[j] = sv[q];
+            if (t[j] != mv.ov_t && mm_visible(t[j], lsb)) v[j] = q + 1;
+        }
+        m = max(m, v[j]);
+    }
+    const uint32_t incl = wave_incl_max(m);
+    if (lane_id() == 63) wm[wave_id()] = incl;
+    __syncthreads();
+    uint32_t run = __shfl_up(incl, 1, 64);
+    if (lane_id() == 0) run = 0;
+    for (uint32_t w = 0; w < wave_id(); ++w) run = max(run, wm[w]);
+    run = max(run, carry[blockIdx.x]);
+#pragma unroll
+    for (uint32_t j = 0; j < MM_ITEMS; ++j) {
+        const uint32_t q = q0 + j;
+        if (q >= P) break;
+        const uint32_t ss = segstart[k[j]];
+        const bool f_head = sv[ss] == mv.ov_t;                  // the override txn opens the segment
+        const uint32_t last = run > ss ? sv[run - 1] : MM_NONE;   // last visible pair before q in the segment
+        code[se[q]] = last | ((f_head && q != ss) ? MM_F : 0u);
+        run = max(run, v[j]);
+        if (q + 1 == P || sk[q + 1] != k[j]) {                 // segment end: the key's map value
+            TsV x = state[k[j]];
+            if (f_head) x = max_keep_old(x, mm_value(mv.ov_t, lsb, mv));
+            if (run > ss) x = max_keep_old(x, mm_value(sv[run - 1], lsb, mv));
+            state_out[k[j]] = x;
+        }
+    }
+}
+
+// txn-major fold: each pair's prefix value rebuilt from its code, then foldl(keys, max(value, acc))
+__global__ void __launch_bounds__(256) mm_fold_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ msb,
+                                                      const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
+                                                      McValues mv, const uint32_t *__restrict__ po,
+                                                      const uint32_t *__restrict__ pk, const uint32_t *__restrict__ code,
+                                                      const TsV *__restrict__ state, uint64_t *__restrict__ om,
+                                                      uint64_t *__restrict__ ol, int32_t *__restrict__ on,
+                                                      uint8_t *__restrict__ ohas, uint8_t *__restrict__ ofast,
+                                                      uint32_t *__restrict__ stop)
+{
+    const uint32_t t = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= last) return;
+    const uint32_t kind = (uint32_t)(lsb[t] >> 1) & 7;
+    const bool xsp = (lsb[t] & 1) && kind == 4;
+    TsV acc;
+    acc.has = 0; acc.msb = 0; acc.lsb = 0; acc.node = 0;
+    if (!xsp)
+        for (uint32_t p = po[t - first]; p < po[t - first + 1]; ++p) {
+            const uint32_t c = code[p];
+            TsV x = state[pk[p]];
+            if (c & MM_F) x = max_keep_old(x, mm_value(mv.ov_t, lsb, mv));
+            if ((c & MM_NONE) != MM_NONE) x = max_keep_old(x, mm_value(c & MM_NONE, lsb, mv));
+            if (x.has && (!acc.has || tcmp(x, acc) >= 0)) acc = x;
+        }
+    om[t] = acc.msb; ol[t] = acc.lsb; on[t] = acc.node; ohas[t] = (uint8_t)acc.has;
+    const bool fast = xsp || ts_cmp(msb[t], lsb[t], node[t], acc.msb, acc.lsb, acc.node) >= 0;
+    ofast[t] = (uint8_t)fast;
+    if (!fast && t != mv.ov_t && kind != 2u) atomicMin(stop, t);
+}
+
 inline uint32_t bits_for_mc(uint32_t v)
 {
     uint32_t b = 1;
@@ -375,6 +524,25 @@ int32_t mc_pass(accord_store *s, uint32_t first, uint32_t last, const McValues &
         accord::radix_sort_pairs(T[0].as<uint32_t>(), T[1].as<uint32_t>(), T[2].as<uint32_t>(), T[3].as<uint32_t>(),
                                  T[4].as<uint32_t>(), T[5].as<uint32_t>(), T[6].as<uint32_t>(), T[11].as<uint32_t>(),
                                  T[12].as<uint32_t>(), P, (int)bits_for_mc(nkeys ? nkeys - 1 : 0), T[10].p, s->scan_tmp.p, st);
+        if (!s->has_exec) {          // PreAccept: monotone values, 4-byte codes (see mm_tile_kernel)
+            const uint32_t mt = (P + MM_TILE - 1) / MM_TILE;
+            HIPCHECK(s, T[14].ensure((size_t)nkeys * 4 + 4));
+            HIPCHECK(s, T[15].ensure((size_t)mt * 4 + 4));
+            uint32_t *segstart = T[14].as<uint32_t>(), *tmax = T[15].as<uint32_t>();
+            uint32_t *code = T[12].as<uint32_t>();            // the sort's ping-pong pair index: free now
+            mm_tile_kernel<<<mt, MM_THREADS, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), s->lsb.as<uint64_t>(),
+                                                      mv.ov_t, segstart, tmax);
+            mm_carry_kernel<<<1, 256, 0, st>>>(mt, tmax);
+            mm_apply_kernel<<<mt, MM_THREADS, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(),
+                                                       s->lsb.as<uint64_t>(), mv, segstart, tmax, s->mc_state.as<TsV>(),
+                                                       code, s->mc_state2.as<TsV>());
+            if (outputs && nt)
+                mm_fold_kernel<<<(nt + 255) / 256, 256, 0, st>>>(first, last, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(),
+                                                                 s->node.as<int32_t>(), mv, po, T[0].as<uint32_t>(), code,
+                                                                 s->mc_state.as<TsV>(), om, ol, on, ohas, ofast, stop_dev);
+            HIPCHECK(s, hipGetLastError());
+            return ACCORD_OK;
+        }
         mc_scan_kernel<0><<<ntiles, MC_TILE, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(),
                                                       T[13].as<TsV>(), s->lsb.as<uint64_t>(), mv, s->mc_state.as<TsV>(),
                                                       T[8].as<Comp>(), nullptr, nullptr, nullptr);

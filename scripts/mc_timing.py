@@ -6,9 +6,9 @@ from accord_amd import CommandStore, generate_stream, lib
 
 s = generate_stream(1 << 20, 8, 100_000, 0.99, 0.5, seed=2)
 with CommandStore(device=0, key_lo=0, key_hi=100_000, window=256, profile=True) as st:
-    st.upload(s)
     ms = []
     for i in range(8):
+        st.upload(s)                       # a batch folds once: a new upload starts it again
         st.max_conflicts_reset()
         st.max_conflicts_fold(download=False)
         f = C.c_float()
