@@ -31,6 +31,8 @@ struct TsV {                 // one MaxConflicts value: Timestamp bits + "entry 
 };
 
 constexpr uint32_t MC_TILE = 1024;   // one element per thread, 16 waves
+constexpr uint32_t MC_INVISIBLE = 0x80000000u;   // sorted txn value: the txn is not globally visible
+constexpr uint32_t MC_TXN = 0x7FFFFFFFu;
 constexpr uint32_t MC_CARRY_THREADS = 1024;
 
 __device__ __forceinline__ int tcmp(const TsV &a, const TsV &b)
@@ -120,6 +122,7 @@ __global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t first, uint32_t l
     const uint32_t kind = (uint32_t)(l >> 1) & 7, domain = (uint32_t)l & 1;
     if (kind >= 5 || (domain == 0 && kind == 4)) record_error(st, t, ACCORD_ERR_KIND);
     uint32_t o = po[t - first];
+    const uint32_t inv = kind == 2u ? MC_INVISIBLE : 0u;   // EphemeralRead: merges nothing (elem_value)
     if (domain) {
         for (uint32_t r = rng_off[t]; r < rng_off[t + 1]; ++r) {
             const uint32_t rs = rng_start[r], re = rng_end[r];
@@ -128,7 +131,7 @@ __global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t first, uint32_t l
             const uint32_t c = mc_range_keys(rs, re, key_lo, key_hi, a);
             for (uint32_t j = 0; j < c; ++j, ++o) {
                 pk[o] = a + j - key_lo;
-                pv[o] = t;
+                pv[o] = t | inv;
                 pe[o] = o;
             }
         }
@@ -140,7 +143,7 @@ __global__ void __launch_bounds__(256) mc_pack_kernel(uint32_t first, uint32_t l
         const uint32_t k = key_ord[p];
         if (k < key_lo || k >= key_hi || (p > b && k <= prev)) record_error(st, t, ACCORD_ERR_KEYS);
         pk[o] = (k >= key_lo && k < key_hi) ? k - key_lo : 0;
-        pv[o] = t;
+        pv[o] = t | inv;
         pe[o] = o;
         prev = k;
     }
@@ -188,7 +191,7 @@ __global__ void __launch_bounds__(MC_TILE) mc_scan_kernel(
         key = sk[q];
         // mode 0 gathers the txn's value once and leaves it in sorted order for mode 1
         TsV v;
-        if (MODE == 0) { v = elem_value(sv[q], lsb, mv); svals[q] = v; }
+        if (MODE == 0) { v = elem_value(sv[q] & MC_TXN, lsb, mv); svals[q] = v; }
         else v = svals[q];
         c.head = (q == 0 || sk[q - 1] != key) ? 1u : 0u;
         if (c.head) {
@@ -296,12 +299,21 @@ __global__ void __launch_bounds__(256) mc_fold_kernel(uint32_t first, uint32_t l
 constexpr uint32_t MM_THREADS = 256, MM_ITEMS = 4, MM_TILE = MM_THREADS * MM_ITEMS;
 constexpr uint32_t MM_NONE = 0x7FFFFFFFu, MM_F = 0x80000000u;
 
-__device__ __forceinline__ bool mm_visible(uint32_t t, const uint64_t *lsb) { return ((uint32_t)(lsb[t] >> 1) & 7) != 2u; }
+// every txn's merged value once, 32-byte aligned: one sector per gather in the apply / fold passes
+struct alignas(32) TsV32 {
+    TsV v;
+    uint64_t pad;
+};
+__global__ void __launch_bounds__(256) mm_values_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ lsb,
+                                                        McValues mv, TsV32 *__restrict__ vt)
+{
+    const uint32_t t = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < last) vt[t].v = elem_value(t, lsb, mv);
+}
 
 // segment starts + per tile the largest (sorted position + 1) of a visible non-override pair
 __global__ void __launch_bounds__(MM_THREADS) mm_tile_kernel(uint32_t P, const uint32_t *__restrict__ sk,
-                                                             const uint32_t *__restrict__ sv,
-                                                             const uint64_t *__restrict__ lsb, uint32_t ov_t,
+                                                             const uint32_t *__restrict__ sv, uint32_t ov_t,
                                                              uint32_t *__restrict__ segstart,
                                                              uint32_t *__restrict__ tile_max)
 {
@@ -314,7 +326,7 @@ __global__ void __launch_bounds__(MM_THREADS) mm_tile_kernel(uint32_t P, const u
         if (q >= P) break;
         const uint32_t k = sk[q], t = sv[q];
         if (q == 0 || sk[q - 1] != k) segstart[k] = q;
-        if (t != ov_t && mm_visible(t, lsb)) m = q + 1;
+        if (t != ov_t && !(t & MC_INVISIBLE)) m = q + 1;
     }
     m = wave_incl_max(m);
     if (lane_id() == 63) wm[wave_id()] = m;
@@ -350,16 +362,12 @@ __global__ void __launch_bounds__(256) mm_carry_kernel(uint32_t ntiles, uint32_t
     }
 }
 
-__device__ __forceinline__ TsV mm_value(uint32_t t, const uint64_t *lsb, const McValues &mv)
-{
-    return elem_value(t, lsb, mv);
-}
 
 // per pair (sorted order): its code at its pair index; per segment end: the key's new map value
 __global__ void __launch_bounds__(MM_THREADS) mm_apply_kernel(uint32_t P, const uint32_t *__restrict__ sk,
                                                               const uint32_t *__restrict__ sv,
                                                               const uint32_t *__restrict__ se,
-                                                              const uint64_t *__restrict__ lsb, McValues mv,
+                                                              const TsV32 *__restrict__ vt, uint32_t ov_t,
                                                               const uint32_t *__restrict__ segstart,
                                                               const uint32_t *__restrict__ carry,
                                                               const TsV *__restrict__ state,
@@ -375,7 +383,7 @@ __global__ void __launch_bounds__(MM_THREADS) mm_apply_kernel(uint32_t P, const 
         v[j] = 0; k[j] = 0; t[j] = 0;
         if (q < P) {
             k[j] = sk[q]; t[j] = sv[q];
-            if (t[j] != mv.ov_t && mm_visible(t[j], lsb)) v[j] = q + 1;
+            if (t[j] != ov_t && !(t[j] & MC_INVISIBLE)) v[j] = q + 1;
         }
         m = max(m, v[j]);
     }
@@ -391,14 +399,14 @@ __global__ void __launch_bounds__(MM_THREADS) mm_apply_kernel(uint32_t P, const 
         const uint32_t q = q0 + j;
         if (q >= P) break;
         const uint32_t ss = segstart[k[j]];
-        const bool f_head = sv[ss] == mv.ov_t;                  // the override txn opens the segment
-        const uint32_t last = run > ss ? sv[run - 1] : MM_NONE;   // last visible pair before q in the segment
+        const bool f_head = ov_t != MC_TXN && (sv[ss] & MC_TXN) == ov_t;   // the override txn opens the segment
+        const uint32_t last = run > ss ? sv[run - 1] & MC_TXN : MM_NONE;   // last visible pair before q in the segment
         code[se[q]] = last | ((f_head && q != ss) ? MM_F : 0u);
         run = max(run, v[j]);
         if (q + 1 == P || sk[q + 1] != k[j]) {                 // segment end: the key's map value
             TsV x = state[k[j]];
-            if (f_head) x = max_keep_old(x, mm_value(mv.ov_t, lsb, mv));
-            if (run > ss) x = max_keep_old(x, mm_value(sv[run - 1], lsb, mv));
+            if (f_head) x = max_keep_old(x, vt[ov_t].v);
+            if (run > ss) x = max_keep_old(x, vt[sv[run - 1] & MC_TXN].v);
             state_out[k[j]] = x;
         }
     }
@@ -407,7 +415,8 @@ __global__ void __launch_bounds__(MM_THREADS) mm_apply_kernel(uint32_t P, const 
 // txn-major fold: each pair's prefix value rebuilt from its code, then foldl(keys, max(value, acc))
 __global__ void __launch_bounds__(256) mm_fold_kernel(uint32_t first, uint32_t last, const uint64_t *__restrict__ msb,
                                                       const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
-                                                      McValues mv, const uint32_t *__restrict__ po,
+                                                      const TsV32 *__restrict__ vt, uint32_t ov_t,
+                                                      const uint32_t *__restrict__ po,
                                                       const uint32_t *__restrict__ pk, const uint32_t *__restrict__ code,
                                                       const TsV *__restrict__ state, uint64_t *__restrict__ om,
                                                       uint64_t *__restrict__ ol, int32_t *__restrict__ on,
@@ -420,18 +429,44 @@ __global__ void __launch_bounds__(256) mm_fold_kernel(uint32_t first, uint32_t l
     const bool xsp = (lsb[t] & 1) && kind == 4;
     TsV acc;
     acc.has = 0; acc.msb = 0; acc.lsb = 0; acc.node = 0;
-    if (!xsp)
-        for (uint32_t p = po[t - first]; p < po[t - first + 1]; ++p) {
+    if (!xsp) {
+        // A pair's value is max_keep_old(y, v_c): y = the key's map value merged with the override
+        // txn's, v_c = the TxnId of its last visible predecessor c.  TxnIds ascend with c, so the
+        // largest v_c is that of the largest c: fold the y's (small, L2-resident map), take the max c,
+        // and gather one TxnId per txn.  Only a y comparing equal to that TxnId needs the exact
+        // per-pair order of the fold (ties keep the later key's value).
+        const uint32_t p0 = po[t - first], p1 = po[t - first + 1];
+        TsV Y;
+        Y.has = 0; Y.msb = 0; Y.lsb = 0; Y.node = 0;
+        uint32_t cmax = 0;                                  // 1 + largest c
+        for (uint32_t p = p0; p < p1; ++p) {
             const uint32_t c = code[p];
-            TsV x = state[pk[p]];
-            if (c & MM_F) x = max_keep_old(x, mm_value(mv.ov_t, lsb, mv));
-            if ((c & MM_NONE) != MM_NONE) x = max_keep_old(x, mm_value(c & MM_NONE, lsb, mv));
-            if (x.has && (!acc.has || tcmp(x, acc) >= 0)) acc = x;
+            TsV y = state[pk[p]];
+            if (c & MM_F) y = max_keep_old(y, vt[ov_t].v);
+            if (y.has && (!Y.has || tcmp(y, Y) >= 0)) Y = y;
+            if ((c & MM_NONE) != MM_NONE) cmax = max(cmax, (c & MM_NONE) + 1u);
         }
+        acc = Y;
+        if (cmax) {
+            const TsV V = vt[cmax - 1].v;
+            const int r = Y.has ? tcmp(V, Y) : 1;
+            if (r > 0) acc = V;
+            else if (r == 0) {                              // rare: replay the exact fold
+                acc.has = 0;
+                for (uint32_t p = p0; p < p1; ++p) {
+                    const uint32_t c = code[p];
+                    TsV x = state[pk[p]];
+                    if (c & MM_F) x = max_keep_old(x, vt[ov_t].v);
+                    if ((c & MM_NONE) != MM_NONE) x = max_keep_old(x, vt[c & MM_NONE].v);
+                    if (x.has && (!acc.has || tcmp(x, acc) >= 0)) acc = x;
+                }
+            }
+        }
+    }
     om[t] = acc.msb; ol[t] = acc.lsb; on[t] = acc.node; ohas[t] = (uint8_t)acc.has;
     const bool fast = xsp || ts_cmp(msb[t], lsb[t], node[t], acc.msb, acc.lsb, acc.node) >= 0;
     ofast[t] = (uint8_t)fast;
-    if (!fast && t != mv.ov_t && kind != 2u) atomicMin(stop, t);
+    if (!fast && t != ov_t && kind != 2u) atomicMin(stop, t);
 }
 
 inline uint32_t bits_for_mc(uint32_t v)
@@ -528,17 +563,20 @@ int32_t mc_pass(accord_store *s, uint32_t first, uint32_t last, const McValues &
             const uint32_t mt = (P + MM_TILE - 1) / MM_TILE;
             HIPCHECK(s, T[14].ensure((size_t)nkeys * 4 + 4));
             HIPCHECK(s, T[15].ensure((size_t)mt * 4 + 4));
+            HIPCHECK(s, T[16].ensure((size_t)s->n * sizeof(TsV32) + 64));
+            TsV32 *vt = T[16].as<TsV32>();
+            const uint32_t ovt = mv.ov_t == 0xFFFFFFFFu ? MC_TXN : mv.ov_t;
+            mm_values_kernel<<<(nt + 255) / 256, 256, 0, st>>>(first, last, s->lsb.as<uint64_t>(), mv, vt);
             uint32_t *segstart = T[14].as<uint32_t>(), *tmax = T[15].as<uint32_t>();
             uint32_t *code = T[12].as<uint32_t>();            // the sort's ping-pong pair index: free now
-            mm_tile_kernel<<<mt, MM_THREADS, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), s->lsb.as<uint64_t>(),
-                                                      mv.ov_t, segstart, tmax);
+            mm_tile_kernel<<<mt, MM_THREADS, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), ovt, segstart, tmax);
             mm_carry_kernel<<<1, 256, 0, st>>>(mt, tmax);
             mm_apply_kernel<<<mt, MM_THREADS, 0, st>>>(P, T[2].as<uint32_t>(), T[3].as<uint32_t>(), T[11].as<uint32_t>(),
-                                                       s->lsb.as<uint64_t>(), mv, segstart, tmax, s->mc_state.as<TsV>(),
+                                                       vt, ovt, segstart, tmax, s->mc_state.as<TsV>(),
                                                        code, s->mc_state2.as<TsV>());
             if (outputs && nt)
                 mm_fold_kernel<<<(nt + 255) / 256, 256, 0, st>>>(first, last, s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(),
-                                                                 s->node.as<int32_t>(), mv, po, T[0].as<uint32_t>(), code,
+                                                                 s->node.as<int32_t>(), vt, ovt, po, T[0].as<uint32_t>(), code,
                                                                  s->mc_state.as<TsV>(), om, ol, on, ohas, ofast, stop_dev);
             HIPCHECK(s, hipGetLastError());
             return ACCORD_OK;
