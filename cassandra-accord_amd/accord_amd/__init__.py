@@ -41,6 +41,7 @@ ERR = {
 STORE_PROFILE = 1
 STORE_RESIDENT = 2
 WINDOW_NONE = 0xFFFFFFFF     # no status-at-time model: statuses from CommandStore.register
+ST_ERASED = 8                # register(): SaveStatus Erased / Invalidated (range commands leave the range scan)
 
 EXPORTED_SYMBOLS = [
     "accord_store_create", "accord_store_destroy", "accord_last_error", "accord_store_stream",
@@ -555,7 +556,8 @@ class CommandStore:
     def register(self, msb, lsb, node, status, exec_msb=None, exec_lsb=None, exec_node=None):
         """InternalStatus events (CommandsForKey.update) for txns this resident store holds, named by
         TxnId (strictly ascending); window must be WINDOW_NONE.  status: 0 TRANSITIVELY_KNOWN ..
-        7 INVALID_OR_TRUNCATED; executeAt for ACCEPTED..APPLIED."""
+        7 INVALID_OR_TRUNCATED, 8 ST_ERASED (SaveStatus Erased / Invalidated); executeAt for
+        ACCEPTED..APPLIED."""
         a = [np.ascontiguousarray(msb, np.uint64), np.ascontiguousarray(lsb, np.uint64),
              np.ascontiguousarray(node, np.int32), np.ascontiguousarray(status, np.uint8)]
         e = None if exec_msb is None else [np.ascontiguousarray(exec_msb, np.uint64),

@@ -25,7 +25,9 @@
 
 namespace {
 
-constexpr uint8_t ST_TK = 0, ST_PREACCEPTED = 2, ST_ACCEPTED = 3, ST_COMMITTED = 4, ST_APPLIED = 6, ST_INVALID = 7;
+constexpr uint8_t ST_TK = 0, ST_PREACCEPTED = 2, ST_ACCEPTED = 3, ST_COMMITTED = 4, ST_APPLIED = 6, ST_INVALID = 7,
+                  ST_ERASED = 8;   // SaveStatus Erased / Invalidated: as INVALID for CFK, and off the range scan
+constexpr uint32_t RC_KIND_ERASED = 7;  // carried range command kind no txn witnesses (masks use kinds 0..4)
 
 __device__ __forceinline__ bool committed(uint32_t st) { return st >= ST_COMMITTED && st <= ST_APPLIED; }
 
@@ -117,7 +119,7 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q)
         if (!((wmask >> (e >> ENT_KIND_SHIFT)) & 1u)) continue;
         if (p1 && g == self) continue;
         const uint32_t st = status_of(p.v, g);
-        if (st == ST_TK || st == ST_INVALID) continue;
+        if (st == ST_TK || st >= ST_INVALID) continue;
         if (committed(st) && has_mcb && tcmp(exec_of(p.v, g), mcb) < 0) continue;
         if (FILL) p.hist2[out + c] = e;
         ++c;
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256) void prune_mark_kernel(uint32_t P, const uint3
                                                          uint32_t *__restrict__ keep_flag)
 {
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x)
-        keep_flag[x] = status_of(v, hist[x] & ENT_TXN_MASK) != ST_INVALID ? 1u : 0u;
+        keep_flag[x] = status_of(v, hist[x] & ENT_TXN_MASK) < ST_INVALID ? 1u : 0u;
 }
 
 // ---- registration ----
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(256) void reg_check_kernel(RegParams p)
         if (r > 0 && ts_cmp(p.msb[r - 1], p.lsb[r - 1], p.node[r - 1], id.msb, id.lsb, id.node) >= 0)
             record_error(p.err, r, ACCORD_ERR_UNSORTED);
         const uint32_t nw = p.status[r];
-        if (nw > ST_INVALID) { record_error(p.err, r, ACCORD_ERR_ARG); continue; }
+        if (nw > ST_ERASED) { record_error(p.err, r, ACCORD_ERR_ARG); continue; }
         uint32_t lo = 0, hi = p.tx_n;
         while (lo < hi) {
             const uint32_t m = (lo + hi) >> 1;
@@ -191,6 +193,24 @@ __global__ __launch_bounds__(256) void reg_check_kernel(RegParams p)
             if (committed(cur) && (ex.msb != p.xmsb[g] || ex.lsb != p.xlsb[g] || ex.node != p.xnode[g]))
                 record_error(p.err, r, ACCORD_ERR_STATE);  // a committed executeAt never changes
         }
+    }
+}
+
+// An Erased / Invalidated range command leaves the range scan (impl/InMemoryCommandStore.java:891,
+// SaveStatus >= Erased): its carried entries (owners ascending, one per range) get a kind no txn
+// witnesses.
+__global__ __launch_bounds__(256) void reg_erase_ranges_kernel(RegParams p, uint32_t rc_n, const uint32_t *__restrict__ rc_owner,
+                                                               uint32_t *__restrict__ rc_kind)
+{
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += gridDim.x * blockDim.x) {
+        if (p.status[r] < ST_ERASED || !(p.lsb[r] & 1ull)) continue;
+        const uint32_t g = p.pos[r];
+        uint32_t lo = 0, hi = rc_n;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (rc_owner[m] < g) lo = m + 1; else hi = m;
+        }
+        for (; lo < rc_n && rc_owner[lo] == g; ++lo) rc_kind[lo] = RC_KIND_ERASED;
     }
 }
 
@@ -254,6 +274,103 @@ StatusView view_of(accord_store *s)
     return v;
 }
 
+// ---- range txns in a registered-status store ----
+// KeyDeps of a range txn (mapReduceForKey over every CFK key of its ranges, impl/InMemoryCommandStore.
+// java:274-289) without a window: per key the entries before the bound (first entry >= the txn /
+// its executeAt's registered prefix), through the full mapReduceActive filter on keys that hold a
+// registered status (maxCommittedBefore, committed pruning, TK / INVALID skipped) and the witness
+// filter elsewhere.  One wave per range txn, a lane per key; count (FILL = false) or fill the
+// keys, header and body (dep txn positions; the union pass turns them into ranks).
+struct RkGenParams {
+    accord::RangeDepsParams p;
+    StatusView v;
+    const uint32_t *flag;              // keys holding a registered status (nullptr: none)
+    const uint64_t *msb, *xmsb, *xlsb;
+    const int32_t *node, *xnode;
+};
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void rk_general_kernel(RkGenParams q)
+{
+    const accord::RangeDepsParams &p = q.p;
+    const uint32_t lane = lane_id();
+    const uint64_t lt = lanemask_lt();
+    const uint32_t waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t li = blockIdx.x * (blockDim.x / 64) + wave_id(); li < p.n_range_txns; li += waves) {
+        const uint32_t i = p.range_txns[li];
+        const uint64_t l = p.lsb[i];
+        const uint32_t wmask = witness_mask((uint32_t)(l >> 1) & 7);
+        const Ts sb = q.xmsb ? Ts{q.xmsb[i], q.xlsb[i], q.xnode[i]} : Ts{q.msb[i], l, q.node[i]};
+        const uint32_t eb = p.g0 + (p.bound_l ? p.bound_l[i] : i);   // entries before it are registered
+        uint32_t key_base = 0, kc_total = 0, k2v_base = 0;
+        if (FILL) {
+            key_base = p.kd_key_off[i];
+            kc_total = p.kd_key_off[i + 1] - key_base;
+            k2v_base = p.kd_k2v_off[i];
+        }
+        uint32_t kc = 0, body = 0;
+        for (uint32_t r = p.rng_off[i]; r < p.rng_off[i + 1]; ++r) {
+            const uint32_t ks = max(p.rng_start[r] + 1, p.key_lo), ke = min(p.rng_end[r], p.key_hi - 1);
+            if (ks > ke) continue;
+            for (uint32_t c0 = ks; c0 <= ke && c0 >= ks; c0 += 64) {
+                const uint32_t key = c0 + lane;
+                const bool valid = key <= ke && key >= ks;
+                uint32_t a = 0, pos = 0, cnt = 0;
+                bool flagged = false, has_mcb = false;
+                Ts mcb{0, 0, 0};
+                if (valid) {
+                    const uint32_t kk = key - p.key_lo;
+                    a = p.seg_start[kk];
+                    const uint32_t c = p.seg_end[kk];
+                    uint32_t lo = a, hi = c;                // first entry with txn >= eb
+                    while (lo < hi) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if ((p.hist[m] & ENT_TXN_MASK) < eb) lo = m + 1; else hi = m;
+                    }
+                    pos = a < c ? lo : a;
+                    flagged = q.flag && q.flag[kk];
+                    if (flagged)
+                        for (uint32_t x = a; x < pos; ++x) {  // maxCommittedBefore (:620-624)
+                            const uint32_t e = p.hist[x], gg = e & ENT_TXN_MASK;
+                            if ((e >> ENT_KIND_SHIFT) != 1u || !committed(status_of(q.v, gg))) continue;
+                            const Ts ex = exec_of(q.v, gg);
+                            if (tcmp(ex, sb) >= 0) continue;
+                            if (!has_mcb || tcmp(ex, mcb) > 0) { mcb = ex; has_mcb = true; }
+                        }
+                }
+                // emitted entries of [a, pos): counted, then (fill) written at the key's body offset
+                auto emitted = [&](uint32_t e) -> bool {
+                    if (!((wmask >> (e >> ENT_KIND_SHIFT)) & 1u)) return false;
+                    if (!flagged) return true;
+                    const uint32_t gg = e & ENT_TXN_MASK, st = status_of(q.v, gg);
+                    if (st == ST_TK || st >= ST_INVALID) return false;
+                    return !(committed(st) && has_mcb && tcmp(exec_of(q.v, gg), mcb) < 0);
+                };
+                for (uint32_t x = a; x < pos; ++x) cnt += emitted(p.hist[x]) ? 1u : 0u;
+                const uint64_t hb = __ballot(cnt > 0);
+                const uint32_t wincl = wave_incl_scan(cnt);
+                if (FILL && cnt) {
+                    const uint32_t ns = kc + (uint32_t)__popcll(hb & lt);
+                    p.kd_keys[key_base + ns] = key;
+                    p.kd_k2v[k2v_base + ns] = (int32_t)(kc_total + body + wincl);
+                    uint32_t o = k2v_base + kc_total + body + wincl - cnt;
+                    for (uint32_t x = a; x < pos; ++x) {
+                        const uint32_t e = p.hist[x];
+                        if (emitted(e)) p.kd_k2v[o++] = (int32_t)(e & ENT_TXN_MASK);
+                    }
+                }
+                kc += (uint32_t)__popcll(hb);
+                body += readlane(wincl, 63);
+            }
+        }
+        if (!FILL && lane == 0) {
+            p.cnt_keys[i] = kc;
+            p.cnt_vals_k[i] = body;          // txnIds upper bound (exact count: the union pass)
+            p.cnt_k2v[i] = kc + body;
+        }
+    }
+}
+
 } // namespace
 
 namespace accord_impl {
@@ -267,6 +384,7 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     const uint32_t n = s->n, P = s->P, nkeys = s->cfg.key_hi - s->cfg.key_lo;
     hipStream_t st = s->stream;
     *hist_for_fill = s->hist.as<uint32_t>();
+    s->rg_flag_ok = false;
     if (C == 0 || s->next_global == 0) return ACCORD_OK;       // nothing registered can be on a key yet
     HIPCHECK(s, s->rg_flag.ensure((size_t)nkeys * 4 + 4));
     HIPCHECK(s, s->rg_gcnt.ensure((size_t)P * 4 + 4));
@@ -275,6 +393,7 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     const StatusView v = view_of(s);
     hipLaunchKernelGGL(flag_keys_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->pair_key.as<uint32_t>(),
                        s->pair_ent.as<uint32_t>(), v, s->rg_flag.as<uint32_t>());
+    s->rg_flag_ok = true;
     GenParams g{};
     g.n = n; g.key_lo = s->cfg.key_lo;
     g.msb = s->msb.as<uint64_t>(); g.lsb = s->lsb.as<uint64_t>(); g.node = s->node.as<int32_t>();
@@ -298,6 +417,24 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     g.ext_base = PH;
     if (n) hipLaunchKernelGGL(general_kernel<true>, dim3(grid_for(n)), dim3(256), 0, st, g);
     *hist_for_fill = s->rg_hist2.as<uint32_t>();
+    return ACCORD_OK;
+}
+
+// KeyDeps of the batch's range txns in a registered-status store (count or fill pass); the flags of
+// status_general_pairs (keys holding a registered status) must be current.
+int32_t status_range_keys(accord_store *s, const accord::RangeDepsParams &rp, bool fill)
+{
+    if (rp.n_range_txns == 0) return ACCORD_OK;
+    RkGenParams q{};
+    q.p = rp;
+    q.v = view_of(s);
+    q.flag = s->rg_flag_ok ? s->rg_flag.as<uint32_t>() : nullptr;
+    q.msb = s->msb.as<uint64_t>(); q.node = s->node.as<int32_t>();
+    if (s->has_exec) { q.xmsb = s->exec_msb.as<uint64_t>(); q.xlsb = s->exec_lsb.as<uint64_t>(); q.xnode = s->exec_node.as<int32_t>(); }
+    const uint32_t blocks = std::min<uint32_t>((rp.n_range_txns + 3) / 4, 4096u);
+    if (fill) hipLaunchKernelGGL(rk_general_kernel<true>, dim3(blocks), dim3(256), 0, s->stream, q);
+    else hipLaunchKernelGGL(rk_general_kernel<false>, dim3(blocks), dim3(256), 0, s->stream, q);
+    HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;
 }
 
@@ -352,7 +489,7 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     if (!msb || !lsb || !node || !status) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: null argument");
     bool need_exec = false;
     for (uint32_t r = 0; r < n; ++r) {
-        if (status[r] > ST_INVALID) return fail(s, ACCORD_ERR_ARG, "event %u: InternalStatus ordinal %u", r, status[r]);
+        if (status[r] > ST_ERASED) return fail(s, ACCORD_ERR_ARG, "event %u: status ordinal %u", r, status[r]);
         need_exec |= status[r] >= ST_ACCEPTED && status[r] <= ST_APPLIED;
     }
     if (need_exec && (!exec_msb || !exec_lsb || !exec_node))
@@ -399,6 +536,9 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
         return fail(s, code, "accord_txn_register: event %u rejected (%s); nothing applied", r, why);
     }
     hipLaunchKernelGGL(reg_apply_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
+    if (s->rc_n)
+        hipLaunchKernelGGL(reg_erase_ranges_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, s->rc_n,
+                           s->rc_owner.as<uint32_t>(), s->rc_kind.as<uint32_t>());
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;

@@ -159,8 +159,6 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     }
     if (b->txn_index && nrt)
         return fail(s, ACCORD_ERR_ARG, "txn_index (store subset of a stream) is supported for key txns only");
-    if (nrt && accord_impl::registered_mode(s))
-        return fail(s, ACCORD_ERR_STATE, "range txns in a registered-status store (ACCORD_WINDOW_NONE) are not supported by this build");
     s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt; s->b_kinds = kinds;
     s->rk_keys_total = 0;                // sizes the range txns' stored key slices
     if (nrt && b->rng_off)
@@ -409,7 +407,8 @@ int32_t accord_deps_compute(accord_store *s)
     rp.cp_base = (rp.g0 > s->cfg.window ? rp.g0 - s->cfg.window : 0u) >> accord::RK_CP_SHIFT;
     rp.ncp = n ? ((rp.g0 + n - 1) >> accord::RK_CP_SHIFT) - rp.cp_base + 1 : 1;
     rp.cnt_vals_exact = s->cnt_vals.as<uint32_t>();
-    if (nrt) {
+    const bool reg_ranges = nrt && accord_impl::registered_mode(s);   // no window: the general range-key pass
+    if (nrt && !reg_ranges) {
         HIPCHECK(s, s->rk_cp.ensure(accord::rangekeys_cp_bytes(rp.ncp, nkeys)));
         HIPCHECK(s, s->rk_cnt.ensure((size_t)nrt * 4 + 4));
         HIPCHECK(s, s->rk_off.ensure(((size_t)nrt + 1) * 4));
@@ -426,7 +425,7 @@ int32_t accord_deps_compute(accord_store *s)
     rp.status = &dev->status;
 
     // sizes: key txns from the per-pair witnessed counts, range txns by their own count pass
-    if (nrt) {
+    if (nrt && !reg_ranges) {
         accord::launch_rangekeys_checkpoints(PH, s->sort_key.as<uint32_t>(), rp, st);
         accord::launch_rangekeys_nkeys(rp, s->rk_cnt.as<uint32_t>(), st);
         accord::exclusive_scan_u32(s->rk_cnt.as<uint32_t>(), s->rk_off.as<uint32_t>(), nrt, &dev->totals[6],
@@ -434,7 +433,12 @@ int32_t accord_deps_compute(accord_store *s)
     }
     accord::launch_keydeps_sizes(n, kp.key_off, kp.slice, rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
                                  rp.cnt_k2v, &dev->status, st);
-    if (nrt) accord::launch_rangekeys_count(rp, st);
+    if (reg_ranges) {
+        int32_t rc = accord_impl::status_range_keys(s, rp, false);
+        if (rc) return rc;
+    } else if (nrt) {
+        accord::launch_rangekeys_count(rp, st);
+    }
     if (rdeps) {
         rp.rd_big_count = s->rd_big.as<uint32_t>();
         rp.rd_big_list = rp.rd_big_count + 16;
@@ -507,7 +511,12 @@ int32_t accord_deps_compute(accord_store *s)
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {
-        accord::launch_rangekeys_fill(rp, st);
+        if (reg_ranges) {
+            int32_t rc = accord_impl::status_range_keys(s, rp, true);
+            if (rc) return rc;
+        } else {
+            accord::launch_rangekeys_fill(rp, st);
+        }
         accord::launch_rangekeys_union(rp, st);
     }
     if (rdeps) accord::launch_rangedeps_fill(rp, st);

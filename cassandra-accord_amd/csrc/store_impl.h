@@ -112,6 +112,7 @@ struct accord_store {
     DevBuf rg_tmsb, rg_tlsb, rg_tnode, rg_tg, rg_status, rg_emsb, rg_elsb, rg_enode;
     DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2;
     uint32_t rg_tx_n = 0, rg_known = 0;
+    bool rg_flag_ok = false;       // rg_flag holds this batch's keys-with-registered-status flags
     // the uploaded batch: its carried-entry prefix, where it ends (global) and its last TxnId
     uint32_t b_end = 0;
     bool b_registered = false;     // the uploaded batch was computed into the resident stream
@@ -166,6 +167,7 @@ bool registered_mode(const accord_store *s);
 int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill);
 int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
 int32_t status_join_batch(accord_store *s);
+int32_t status_range_keys(accord_store *s, const accord::RangeDepsParams &rp, bool fill);
 // RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp)
 int32_t redundant_apply(accord_store *s);
 }

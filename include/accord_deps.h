@@ -139,7 +139,9 @@ void       *accord_store_stream(accord_store *store);        /* the store's hipS
  * Range txns: the store also keeps the range commands a later txn's window can reach (owner
  * position >= next_global - W; the range-command scan of impl/InMemoryCommandStore.java:883-1016
  * over the commands still live), so RangeDeps and the range txns' KeyDeps continue across batches
- * too.  A registered-status store (ACCORD_WINDOW_NONE) rejects range txns (ACCORD_ERR_STATE). */
+ * too.  In a registered-status store (ACCORD_WINDOW_NONE) every range command stays until an event
+ * gives it ACCORD_ST_ERASED, and a range txn's KeyDeps run the full mapReduceActive filter on the
+ * keys of its ranges. */
 /* Real status events (SURVEY.md §8b accord_txn_register): a resident store created with window
  * ACCORD_WINDOW_NONE has no status-at-time model -- every txn enters its keys' CommandsForKey
  * PREACCEPTED when its batch is computed (CommandsForKey.insert, local/CommandsForKey.java:880-944)
@@ -161,6 +163,11 @@ void       *accord_store_stream(accord_store *store);        /* the store's hipS
 #define ACCORD_ST_STABLE             5
 #define ACCORD_ST_APPLIED            6
 #define ACCORD_ST_INVALID_OR_TRUNCATED 7
+/* SaveStatus Erased / Invalidated (local/SaveStatus.java:86-87): INVALID_OR_TRUNCATED for
+ * CommandsForKey, and a range command with it leaves the range-command scan (SaveStatus >= Erased,
+ * impl/InMemoryCommandStore.java:891).  A range command at INVALID_OR_TRUNCATED (ErasedOrInvalidated,
+ * Truncated*: before Erased in SaveStatus order, :80-85) is still visited. */
+#define ACCORD_ST_ERASED             8
 int32_t accord_txn_register(accord_store *store, uint32_t n, const uint64_t *msb, const uint64_t *lsb,
                             const int32_t *node, const uint8_t *status, const uint64_t *exec_msb,
                             const uint64_t *exec_lsb, const int32_t *exec_node);

@@ -1830,8 +1830,12 @@ struct or_lstore {
     ts_t *tbl;                 /* TxnIds by global position */
     uint32_t *koff, *kord;     /* keys of every registered txn (CSR by global position) */
     uint32_t n, cap, nk, kcap;
-    uint8_t *status;           /* current InternalStatus of every txn */
+    uint8_t *status;           /* current InternalStatus of every txn (8: SaveStatus Erased/Invalidated) */
     ts_t *exec;
+    /* range txns: InMemoryCommandStore.rangeCommands (impl/InMemoryCommandStore.java:739-762) --
+     * the command's ranges (CSR by global position) and whether its SaveStatus reached Erased */
+    uint32_t *roff, *rst, *ren;
+    uint32_t nr, rcap;
 };
 
 or_lstore *or_lstore_create(uint32_t nkeys)
@@ -1841,7 +1845,8 @@ or_lstore *or_lstore_create(uint32_t nkeys)
     s->nkeys = nkeys;
     s->cfks = (cfk_t *)calloc(nkeys ? nkeys : 1, sizeof(cfk_t));
     s->koff = (uint32_t *)calloc(1, sizeof(uint32_t));
-    if (!s->cfks || !s->koff) { or_lstore_free(s); return NULL; }
+    s->roff = (uint32_t *)calloc(1, sizeof(uint32_t));
+    if (!s->cfks || !s->koff || !s->roff) { or_lstore_free(s); return NULL; }
     return s;
 }
 
@@ -1850,6 +1855,7 @@ void or_lstore_free(or_lstore *s)
     if (!s) return;
     if (s->cfks) for (uint32_t k = 0; k < s->nkeys; ++k) { free(s->cfks[k].txns); free(s->cfks[k].committed); }
     free(s->cfks); free(s->tbl); free(s->koff); free(s->kord); free(s->status); free(s->exec);
+    free(s->roff); free(s->rst); free(s->ren);
     free(s);
 }
 
@@ -1870,6 +1876,9 @@ static int lstore_reserve(or_lstore *s, uint32_t n, uint32_t nk)
         ts_t *ex = (ts_t *)realloc(s->exec, (size_t)c * sizeof(ts_t));
         if (!ex) return -1;
         s->exec = ex;
+        uint32_t *ro = (uint32_t *)realloc(s->roff, ((size_t)c + 1) * sizeof(uint32_t));
+        if (!ro) return -1;
+        s->roff = ro;
         s->cap = c;
     }
     if (nk > s->kcap) {
@@ -1883,6 +1892,76 @@ static int lstore_reserve(or_lstore *s, uint32_t n, uint32_t nk)
     return 0;
 }
 
+static int lstore_reserve_ranges(or_lstore *s, uint32_t nr)
+{
+    if (nr <= s->rcap) return 0;
+    uint32_t c = s->rcap ? s->rcap : 1024;
+    while (c < nr) c *= 2;
+    uint32_t *a = (uint32_t *)realloc(s->rst, (size_t)c * sizeof(uint32_t));
+    if (!a) return -1;
+    s->rst = a;
+    uint32_t *b = (uint32_t *)realloc(s->ren, (size_t)c * sizeof(uint32_t));
+    if (!b) return -1;
+    s->ren = b;
+    s->rcap = c;
+    return 0;
+}
+
+#define S_ERASED 8             /* SaveStatus >= Erased (Erased, Invalidated): local/SaveStatus.java:83-87 */
+
+/* mapReduceRangesInternal (impl/InMemoryCommandStore.java:883-1016) over the store's range commands
+ * [0, reg): skip SaveStatus >= Erased (:891; ErasedOrInvalidated is before Erased and still visited),
+ * txnId < startedBefore (:901-902), the p1 txn, unwitnessed kinds (:927); every range of the command
+ * intersecting the query -> (range, txnId) collected in a TreeMap by Range.compare and replayed. */
+static int lstore_range_scan(const or_lstore *s, const or_stream *b, uint32_t i, uint32_t reg, const ts_t *sb,
+                             long p1, int test_kinds, mm_builder *rb)
+{
+    typedef struct { uint64_t code; uint32_t txn; } hit_t;
+    hit_t *h = NULL;
+    size_t nh = 0, ch = 0;
+    int rc = -1;
+    for (uint32_t g = 0; g < reg; ++g) {
+        if (s->roff[g + 1] == s->roff[g]) continue;                          /* not a range command */
+        if (s->status[g] >= S_ERASED) continue;
+        if (ts_cmp(&s->tbl[g], sb) >= 0) continue;
+        if (p1 >= 0 && (uint32_t)p1 == g) continue;
+        if (!kinds_test(test_kinds, kind_of(s->tbl[g].lsb))) continue;
+        for (uint32_t a = s->roff[g]; a < s->roff[g + 1]; ++a) {
+            const uint32_t rs = s->rst[a], re = s->ren[a];
+            int hit = 0;
+            if (domain_of(b->lsb[i]) == 0) {
+                for (uint32_t p = b->key_off[i]; p < b->key_off[i + 1] && !hit; ++p)
+                    hit = range_intersects_key(rs, re, b->key_ord[p]);
+            } else {
+                for (uint32_t r = b->rng_off[i]; r < b->rng_off[i + 1] && !hit; ++r)
+                    hit = range_intersects_range(rs, re, b->rng_start[r], b->rng_end[r]);
+            }
+            if (!hit) continue;
+            if (nh == ch) {
+                ch = ch ? ch * 2 : 64;
+                hit_t *nhp = (hit_t *)realloc(h, ch * sizeof(hit_t));
+                if (!nhp) goto done;
+                h = nhp;
+            }
+            h[nh].code = ((uint64_t)rs << 32) | re;
+            h[nh].txn = g;
+            ++nh;
+        }
+    }
+    /* TreeMap by Range.compare, each list in scan (TxnId) order: a stable insertion sort by range */
+    for (size_t a = 1; a < nh; ++a) {
+        hit_t x = h[a]; size_t c = a;
+        while (c > 0 && h[c - 1].code > x.code) { h[c] = h[c - 1]; --c; }
+        h[c] = x;
+    }
+    for (size_t a = 0; a < nh; ++a)
+        if (mmb_add(rb, h[a].code, h[a].txn)) goto done;
+    rc = 0;
+done:
+    free(h);
+    return rc;
+}
+
 int or_lstore_batch(or_lstore *s, const or_stream *b, or_deps *out)
 {
     const uint32_t n = b->n;
@@ -1890,24 +1969,33 @@ int or_lstore_batch(or_lstore *s, const or_stream *b, or_deps *out)
     if (!rc) rc = validate_exec(b, n);
     if (rc) return rc;
     for (uint32_t i = 0; i < n; ++i) {
-        if (domain_of(b->lsb[i]) != 0) return -5;                                   /* key txns only */
+        if (domain_of(b->lsb[i]) != 0 && !b->rng_off) return -5;
         for (uint32_t p = b->key_off[i]; p < b->key_off[i + 1]; ++p) if (b->key_ord[p] >= s->nkeys) return -4;
     }
     if (n && s->n && or_ts_compare(s->tbl[s->n - 1].msb, s->tbl[s->n - 1].lsb, s->tbl[s->n - 1].node,
                                    b->msb[0], b->lsb[0], b->node[0]) >= 0) return -2;
     const uint32_t base = s->n;
+    const uint32_t nbr = b->rng_off ? b->rng_off[n] - b->rng_off[0] : 0;
     if (lstore_reserve(s, base + n, s->koff[base] + b->key_off[n])) return -1;
-    for (uint32_t i = 0; i < n; ++i) {                 /* the batch's TxnIds and keys (not registered yet) */
+    if (lstore_reserve_ranges(s, s->roff[base] + nbr)) return -1;
+    for (uint32_t i = 0; i < n; ++i) {                 /* the batch's TxnIds, keys and ranges (not registered yet) */
         ts_t t = {b->msb[i], b->lsb[i], b->node[i]};
         s->tbl[base + i] = t;
         s->koff[base + i + 1] = s->koff[base + i] + (b->key_off[i + 1] - b->key_off[i]);
         memcpy(s->kord + s->koff[base + i], b->key_ord + b->key_off[i], (b->key_off[i + 1] - b->key_off[i]) * 4);
+        const uint32_t r0 = b->rng_off ? b->rng_off[i] : 0, r1 = b->rng_off ? b->rng_off[i + 1] : 0;
+        s->roff[base + i + 1] = s->roff[base + i] + (r1 - r0);
+        if (r1 > r0) {
+            memcpy(s->rst + s->roff[base + i], b->rng_start + r0, (r1 - r0) * 4);
+            memcpy(s->ren + s->roff[base + i], b->rng_end + r0, (r1 - r0) * 4);
+        }
         s->status[base + i] = S_PREACCEPTED;
         s->exec[base + i] = t;
     }
-    mm_builder kb;
+    mm_builder kb, rb;
     mm_out kd, rd;
     mmb_init(&kb, s->tbl);
+    mmb_init(&rb, s->tbl);
     if (mmo_init(&kd) || mmo_init(&rd)) return -1;
     rc = -1;
     uint32_t reg = 0;                                  /* batch txns [0, reg) are inserted */
@@ -1918,25 +2006,36 @@ int or_lstore_batch(or_lstore *s, const or_stream *b, or_deps *out)
         if (reg_to < i + 1) reg_to = i + 1;
         for (; reg < reg_to; ++reg) {
             const uint32_t g = base + reg;
-            if (is_globally_visible(kind_of(b->lsb[reg])) == 1)
+            if (domain_of(b->lsb[reg]) == 0 && is_globally_visible(kind_of(b->lsb[reg])) == 1)
                 for (uint32_t p = b->key_off[reg]; p < b->key_off[reg + 1]; ++p)
                     if (cfk_insert(&s->cfks[b->key_ord[p]], s->tbl, g, S_PREACCEPTED)) goto done;
+            /* a range txn joins rangeCommands (its ranges above), not any CommandsForKey */
         }
         const int test_kinds = witnesses_of(kind_of(b->lsb[i]));
-        mmb_reset(&kb);
-        for (uint32_t p = b->key_off[i]; p < b->key_off[i + 1]; ++p) {
-            const uint32_t key = b->key_ord[p];
-            if (cfk_map_reduce_active(&s->cfks[key], s->tbl, &sb, test_kinds, key, &kb, p1)) goto done;
+        mmb_reset(&kb); mmb_reset(&rb);
+        if (domain_of(b->lsb[i]) == 0) {
+            for (uint32_t p = b->key_off[i]; p < b->key_off[i + 1]; ++p) {
+                const uint32_t key = b->key_ord[p];
+                if (cfk_map_reduce_active(&s->cfks[key], s->tbl, &sb, test_kinds, key, &kb, p1)) goto done;
+            }
+        } else {
+            /* mapReduceForKey Range case (impl/InMemoryCommandStore.java:274-289): every CFK key in
+             * each (start, end], ascending */
+            for (uint32_t r = b->rng_off[i]; r < b->rng_off[i + 1]; ++r)
+                for (uint32_t key = b->rng_start[r] + 1; key <= b->rng_end[r] && key < s->nkeys; ++key)
+                    if (s->cfks[key].n && cfk_map_reduce_active(&s->cfks[key], s->tbl, &sb, test_kinds, key, &kb, p1))
+                        goto done;
         }
+        if (lstore_range_scan(s, b, i, base + reg, &sb, p1, test_kinds, &rb)) goto done;
         if (mmb_build(&kb, &kd, 0)) goto done;
-        if (mmo_close_txn(&rd)) goto done;             /* no RangeDeps */
+        if (mmb_build(&rb, &rd, 1)) goto done;
     }
     s->n = base + n;
     if (alloc_out(out, &kd, &rd, n)) goto done;
     rc = 0;
 done:
     if (rc) s->n = base;
-    mmb_free(&kb);
+    mmb_free(&kb); mmb_free(&rb);
     mmo_free(&kd); mmo_free(&rd);
     return rc;
 }
@@ -1951,7 +2050,7 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
     if (!pos) return -1;
     for (uint32_t r = 0; r < n; ++r) {                 /* validate everything before changing anything */
         if (r && or_ts_compare(msb[r - 1], lsb[r - 1], node[r - 1], msb[r], lsb[r], node[r]) >= 0) { free(pos); return -2; }
-        if (status[r] > S_INVALID_OR_TRUNCATED) { free(pos); return -1; }
+        if (status[r] > S_ERASED) { free(pos); return -1; }
         uint32_t lo = 0, hi = s->n;
         while (lo < hi) {
             uint32_t m = (lo + hi) / 2;
@@ -1981,8 +2080,11 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
         s->status[g] = nw;
         s->exec[g] = ex;
         if (is_globally_visible(kind_of(s->tbl[g].lsb)) != 1) continue;   /* never inserted into CFK */
+        if (domain_of(s->tbl[g].lsb) != 0) continue;                       /* range command: status only */
+        /* Erased / Invalidated leave CommandsForKey as INVALID_OR_TRUNCATED does */
+        const uint8_t cs = nw >= S_ERASED ? (uint8_t)S_INVALID_OR_TRUNCATED : nw;
         for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p)
-            if (cfk_update_status(&s->cfks[s->kord[p]], s->tbl, g, nw, &ex)) { free(pos); return -1; }
+            if (cfk_update_status(&s->cfks[s->kord[p]], s->tbl, g, cs, &ex)) { free(pos); return -1; }
     }
     free(pos);
     return 0;

@@ -404,8 +404,9 @@ def max_conflicts(s, key_lo: int, nkeys: int, state=None, first: int = 0, exec_a
 
 class LStore:
     """Stateful literal CommandStore (or_lstore_*): batches fed in order, InternalStatus events in
-    between; deps values are global positions.  Key txns only."""
-    TK, HISTORICAL, PREACCEPTED, ACCEPTED, COMMITTED, STABLE, APPLIED, INVALID = range(8)
+    between; deps values are global positions.  Range txns join rangeCommands; status 8 (ERASED) is
+    SaveStatus Erased / Invalidated: off the range scan, INVALID_OR_TRUNCATED for CommandsForKey."""
+    TK, HISTORICAL, PREACCEPTED, ACCEPTED, COMMITTED, STABLE, APPLIED, INVALID, ERASED = range(9)
 
     def __init__(self, nkeys: int):
         L = lib()

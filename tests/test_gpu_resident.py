@@ -163,12 +163,13 @@ def test_range_carry_resets(gpu_device):
     assert again.first_difference(single(s, 500, 300)) is None
 
 
-def test_registered_store_rejects_ranges(gpu_device):
+def test_registered_store_takes_ranges(gpu_device):
+    # no events yet: every txn PREACCEPTED, no window -- the stateful literal oracle's result
     from accord_amd import WINDOW_NONE
     s = generate_stream(200, 2, 100, 0.0, 0.5, range_frac=0.3, range_len_max=10, seed=39)
     with CommandStore(device=0, key_lo=0, key_hi=100, window=WINDOW_NONE, resident=True) as st:
-        with pytest.raises(IllegalStateException):
-            st.calculate_deps_batch(s)
+        got = st.calculate_deps_batch(s)
+    assert got.first_difference(O.LStore(100).batch(s)) is None
 
 
 @pytest.mark.timeout(600)

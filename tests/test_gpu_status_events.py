@@ -9,12 +9,12 @@ import pytest
 
 from accord_amd import CommandStore, IllegalArgumentException, IllegalStateException, WINDOW_NONE, generate_stream
 import oracle_lib as O
-from status_events import APPLIED, COMMITTED, INVALID, PREACCEPTED, events_for
+from status_events import APPLIED, COMMITTED, ERASED, INVALID, PREACCEPTED, events_for
 
 pytestmark = pytest.mark.gpu
 
 
-def run(s, ks, pts, seed, frac=0.5, delay=40, accept=None):
+def run(s, ks, pts, seed, frac=0.5, delay=40, accept=None, erased=False):
     rng = np.random.default_rng(seed)
     status = np.full(s.n, PREACCEPTED, np.uint8)
     execs = [None] * s.n
@@ -26,7 +26,7 @@ def run(s, ks, pts, seed, frac=0.5, delay=40, accept=None):
             want = ora.batch(part)
             diff = got.first_difference(want)
             assert diff is None, (b, diff)
-            idx, stt, em, el, en = events_for(s, 0, c, status, execs, rng, frac=frac, delay=delay)
+            idx, stt, em, el, en = events_for(s, 0, c, status, execs, rng, frac=frac, delay=delay, erased=erased)
             st.register(s.msb[idx], s.lsb[idx], s.node[idx], stt, em, el, en)
             ora.register(s.msb[idx], s.lsb[idx], s.node[idx], stt, em, el, en)
         return st.state()
@@ -82,3 +82,41 @@ def test_register_errors_apply_nothing(gpu_device):
             st.register(s.msb[[3, 2]], s.lsb[[3, 2]], s.node[[3, 2]], [PREACCEPTED, PREACCEPTED])
         # a rejected call applied nothing: t1 can still be committed at its TxnId
         st.register(s.msb[1:2], s.lsb[1:2], s.node[1:2], [APPLIED], s.msb[1:2], s.lsb[1:2], s.node[1:2])
+
+
+@pytest.mark.parametrize("n,k,ks,rf,rl,parts,seed", [
+    (3000, 4, 300, 0.2, 40, 6, 11),
+    (2000, 2, 60, 0.3, 10, 8, 12),          # hot keys, short ranges
+    (2500, 6, 1000, 0.1, 300, 5, 13),
+])
+def test_range_txns_with_events(gpu_device, n, k, ks, rf, rl, parts, seed):
+    # range commands stay until ERASED (SaveStatus >= Erased); INVALID_OR_TRUNCATED ones are still
+    # visited (SURVEY.md §8c KAT 5); range txns' KeyDeps run the CFK filter on their ranges' keys
+    s = generate_stream(n, k, ks, 0.99, 0.5, range_frac=rf, range_len_max=rl, seed=seed)
+    pts = [i * n // parts for i in range(parts + 1)]
+    run(s, ks, pts, seed, erased=True)
+
+
+def test_range_txns_with_events_accept(gpu_device):
+    s = generate_stream(2500, 4, 300, 0.99, 0.5, range_frac=0.2, range_len_max=50, seed=14)
+    acc = s.accept(frac=0.5, max_delay=30, seed=14)
+    run(s, 300, [0, 600, 1300, 1900, 2500], 14, accept=acc, erased=True)
+
+
+def test_kat5_erased_or_invalidated_on_gpu(gpu_device):
+    # SURVEY.md §8c KAT 5 through the C ABI (the oracle KAT: test_oracle_events.py): a range command
+    # at INVALID_OR_TRUNCATED (ErasedOrInvalidated) is still a dependency, at ERASED it is not
+    from test_oracle_events import mk_mixed, range_deps_of, reg
+    s = mk_mixed([(10, "W", 1, None, [(0, 5)]), (11, "W", 1, None, [(3, 9)]), (12, "W", 1, [4], None),
+                  (13, "W", 1, [4], None), (14, "W", 1, [4], None)])
+    ora = O.LStore(16)
+    with CommandStore(device=0, key_lo=0, key_hi=16, window=WINDOW_NONE, resident=True) as st:
+        def both(a, b):
+            got, want = st.calculate_deps_batch(s.slice(a, b)), ora.batch(s.slice(a, b))
+            assert got.first_difference(want) is None
+            return got
+        assert range_deps_of(both(0, 3), 2) == {(0, 5): [0], (3, 9): [1]}
+        reg(st, s, [0], [INVALID]); reg(ora, s, [0], [INVALID])
+        assert range_deps_of(both(3, 4), 0) == {(0, 5): [0], (3, 9): [1]}
+        reg(st, s, [0, 1], [ERASED, INVALID]); reg(ora, s, [0, 1], [ERASED, INVALID])
+        assert range_deps_of(both(4, 5), 0) == {(3, 9): [1]}

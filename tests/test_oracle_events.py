@@ -6,7 +6,7 @@ import pytest
 
 from accord_amd import PartialDeps, Stream
 import oracle_lib as O
-from status_events import COMMITTED, STABLE, APPLIED, INVALID, TK, ACCEPTED, events_for
+from status_events import COMMITTED, STABLE, APPLIED, INVALID, ERASED, TK, ACCEPTED, events_for
 
 KIND = {"R": 0, "W": 1, "ER": 2, "SP": 3}
 
@@ -99,3 +99,60 @@ def test_schedules_are_batch_split_invariant_without_events():
     parts = [b.batch(s.slice(x, y)) for x, y in ((0, 700), (700, 701), (701, 2500), (2500, 3000))]
     assert PartialDeps.concat(parts).first_difference(one) is None
     assert one.first_difference(O.deps_literal(s, 0xFFFFFFFF)) is None
+
+
+def mk_mixed(txns):
+    """txns: [(hlc, kind, node, keys or None, ranges or None)]: a key txn (domain 0) carries keys, a
+    range txn (domain 1) (start, end] ranges."""
+    n = len(txns)
+    msb = np.full(n, 1 << 15, np.uint64)
+    lsb = np.array([(h << 16) | (KIND[k] << 1) | (1 if rs is not None else 0) for h, k, _, _, rs in txns], np.uint64)
+    node = np.array([t[2] for t in txns], np.int32)
+    key_off = np.zeros(n + 1, np.uint32)
+    key_off[1:] = np.cumsum([len(t[3] or []) for t in txns])
+    key_ord = np.array([k for t in txns for k in (t[3] or [])], np.uint32)
+    rng_off = np.zeros(n + 1, np.uint32)
+    rng_off[1:] = np.cumsum([len(t[4] or []) for t in txns])
+    rs = np.array([a for t in txns for a, _ in (t[4] or [])], np.uint32)
+    re = np.array([b for t in txns for _, b in (t[4] or [])], np.uint32)
+    return Stream(msb, lsb, node, key_off, key_ord, rng_off, rs, re)
+
+
+def range_deps_of(d: PartialDeps, i):
+    rs, re, rv, r2v = d.range_deps(i)
+    out, t = {}, len(rs)
+    for k in range(len(rs)):
+        out[(int(rs[k]), int(re[k]))] = [int(rv[r2v[x]]) for x in range(t, r2v[k])]
+        t = r2v[k]
+    return out
+
+
+def test_kat5_erased_or_invalidated_range_command_still_visited():
+    # SURVEY.md §8c KAT 5: mapReduceRangesInternal skips saveStatus >= Erased (impl/InMemoryCommandStore.
+    # java:891); ErasedOrInvalidated precedes Erased in SaveStatus order (local/SaveStatus.java:83-86),
+    # so a range command there is still a dependency.  Here INVALID_OR_TRUNCATED (the InternalStatus of
+    # ErasedOrInvalidated / Truncated*) keeps the range command, ERASED removes it.
+    s = mk_mixed([(10, "W", 1, None, [(0, 5)]), (11, "W", 1, None, [(3, 9)]), (12, "W", 1, [4], None),
+                  (13, "W", 1, [4], None), (14, "W", 1, [4], None)])
+    st = O.LStore(16)
+    d = st.batch(s.slice(0, 3))
+    assert range_deps_of(d, 2) == {(0, 5): [0], (3, 9): [1]}
+    assert range_deps_of(d, 1) == {(0, 5): [0]}                       # ranges (0,5] and (3,9] meet
+    reg(st, s, [0], [INVALID])                                         # ErasedOrInvalidated: still visited
+    d = st.batch(s.slice(3, 4))
+    assert range_deps_of(d, 0) == {(0, 5): [0], (3, 9): [1]}
+    reg(st, s, [0, 1], [ERASED, INVALID])                              # Erased: off the scan
+    d = st.batch(s.slice(4, 5))
+    assert range_deps_of(d, 0) == {(3, 9): [1]}
+
+
+def test_kat_range_txn_keydeps_use_cfk_filter():
+    # a range txn's KeyDeps are mapReduceActive on every CFK key of its ranges
+    # (impl/InMemoryCommandStore.java:274-289): committed pruning applies to them as to key txns
+    s = mk_mixed([(10, "W", 1, [2], None), (11, "W", 1, [2], None), (12, "R", 1, [3], None),
+                  (13, "W", 1, None, [(1, 3)])])
+    st = O.LStore(8)
+    st.batch(s.slice(0, 3))
+    reg(st, s, [0, 1], [APPLIED, APPLIED])
+    d = st.batch(s.slice(3, 4))
+    assert deps_of(d, 0) == {2: [1], 3: [2]}                         # t0 pruned below executeAt(t1)
