@@ -84,6 +84,7 @@ struct KeyDepsParams {
     // big txns (more keys than a wave has lanes, or more distinct far deps than the general kernel's
     // far list): listed by the general kernel, built by a workgroup each (big_wex: scratch per pair)
     uint32_t *big_list, *big_count, *big_wex;
+    uint32_t tiny;                     // thread-per-txn pass for tiny txns (batches of few keys per txn)
 };
 
 // Where a batch sits in the store's stream: global positions start at min_gi, and (has_prev) the

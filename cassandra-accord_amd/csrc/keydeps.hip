@@ -891,6 +891,12 @@ __global__ __launch_bounds__(256) void txnrec_kernel(KeyDepsParams p, TxnRec *__
     }
 }
 
+// tiny txns (keydeps_tiny_kernel below): k <= TN_K keys and <= TN_RAW raw candidates
+constexpr uint32_t TN_K = 4, TN_RAW = 16;
+constexpr uint32_t TN_END = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool tn_take(uint32_t k, uint32_t raw) { return k > 0 && k <= TN_K && raw <= TN_RAW; }
+
 constexpr int FK_CB = 6;                      // candidate batches of 64 a fast-path txn may use
 constexpr uint32_t FK_RAW = 64u * FK_CB;      // raw candidates the fast path takes
 
@@ -939,7 +945,7 @@ __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn
     uint32_t eq[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) eq[q] = readlane(excl, q + 1);
-    const bool take = k <= 8 && rt <= FK_RAW;
+    const bool take = k <= 8 && rt <= FK_RAW && !(p.tiny && tn_take(k, rt));   // tiny txns: not this kernel's
 #pragma unroll
     for (int c = 0; c < FK_CB; ++c) e[c] = KD_NONE;
 #pragma unroll
@@ -1006,6 +1012,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 if (lane == 0) stg(p.cnt_vals, t, 0u);
                 break;
             }
+            if (p.tiny && tn_take(k, rta)) break;     // a tiny txn: keydeps_tiny_kernel builds it
             bool fallback = k > 8 || rta > FK_RAW;
             const uint32_t kind = readlane(a.rec, 2), gi = readlane(a.rec, 3);
             const uint32_t wmask = witness_mask(kind);
@@ -1276,6 +1283,87 @@ __global__ __launch_bounds__(BK_THREADS) void keydeps_big_kernel(KeyDepsParams p
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tiny txns: k <= TN_K keys and <= TN_RAW raw candidates -- most txns of a store that owns a slice
+// of the keyspace (a rank of the multi-GPU bench sees ~1.5 keys per txn).  One THREAD per txn
+// instead of a wave: its <= TN_RAW candidates (slot-major, as the fast kernel orders them) are
+// loaded at once into registers, the union is ranked by pairwise compares (a value's rank =
+// first occurrences below it), and txnIds / body are written from the registers.  The fast kernel
+// skips exactly these txns.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void keydeps_tiny_kernel(KeyDepsParams p)
+{
+    // launched (and skipped by the fast kernel) only for batches of few keys per txn: with the
+    // fast kernel's per-txn pipeline running over every txn anyway, a thread-per-txn pass pays off
+    // only when tiny txns are the bulk (measured: config 5, 4 keys/txn, +0.26 ms; an 8-rank store
+    // block, 1.5 keys/txn, -0.5 ms)
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < p.n; t += gridDim.x * blockDim.x) {
+        const uint32_t k0 = p.key_off[t], k = p.key_off[t + 1] - k0;
+        if (k == 0 || k > TN_K) continue;
+        uint32_t lo[TN_K], ex[TN_K], wc[TN_K], raw = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < TN_K; ++q) {
+            lo[q] = wc[q] = 0;
+            ex[q] = raw;
+            if (q < k) {
+                const PairSlice ps = p.slice[k0 + q];
+                lo[q] = ps.lo; wc[q] = ps.wcnt;
+                raw += ps.pos - ps.lo;
+            }
+        }
+        if (!tn_take(k, raw)) continue;
+        const uint32_t wmask = witness_mask((uint32_t)(p.lsb[t] >> 1) & 7);
+        const uint32_t gi = p.txn_index ? p.txn_index[t] : t;
+        // candidate r of slot q sits at hist[lo_q + r - ex_q]; later slots win the select chain
+        uint32_t v[TN_RAW];
+#pragma unroll
+        for (uint32_t r = 0; r < TN_RAW; ++r) {
+            uint32_t a = lo[0] + r;
+#pragma unroll
+            for (uint32_t q = 1; q < TN_K; ++q) a = (q < k && r >= ex[q]) ? lo[q] + (r - ex[q]) : a;
+            v[r] = TN_END;
+            if (r < raw) {
+                const uint32_t e = p.hist[a], j = e & ENT_TXN_MASK;
+                if (((wmask >> (e >> ENT_KIND_SHIFT)) & 1u) && j != gi) v[r] = j;
+            }
+        }
+        bool first[TN_RAW];
+        uint32_t U = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < TN_RAW; ++r) {
+            bool f = v[r] != TN_END;
+#pragma unroll
+            for (uint32_t x = 0; x < r; ++x) f = f && v[x] != v[r];
+            first[r] = f;
+            U += f ? 1u : 0u;
+        }
+        const uint32_t key_base = p.kd_key_off[t], val_base = p.vub_off[t], k2v_base = p.kd_k2v_off[t];
+        uint32_t kc = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < TN_K; ++q) kc += wc[q] ? 1u : 0u;
+        uint32_t run = 0, ns = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < TN_K; ++q)
+            if (wc[q]) {
+                run += wc[q];
+                p.kd_keys[key_base + ns] = p.key_ord[k0 + q];
+                p.kd_k2v[k2v_base + ns] = (int32_t)(kc + run);
+                ++ns;
+            }
+        uint32_t pos = k2v_base + kc;                   // body: witnessed candidates in slot order
+#pragma unroll
+        for (uint32_t r = 0; r < TN_RAW; ++r) {
+            if (v[r] == TN_END) continue;
+            uint32_t rank = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < TN_RAW; ++x) rank += (first[x] && v[x] < v[r]) ? 1u : 0u;
+            p.kd_k2v[pos++] = (int32_t)rank;
+            if (first[r]) p.vgap[val_base + rank] = v[r];
+        }
+        p.cnt_vals[t] = U;
+    }
+}
+
 void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_t s)
 {
     if (p.n == 0) return;
@@ -1504,6 +1592,11 @@ void launch_keydeps_fill(const KeyDepsParams &p, int wpl, void *recs, hipStream_
         return;
     }
     launch_keydeps_fast(p, wpl, recs, s);
+    if (p.tiny) {
+        uint32_t b = (p.n + 255) / 256;
+        if (b > 8192) b = 8192;
+        hipLaunchKernelGGL(keydeps_tiny_kernel, dim3(b), dim3(256), 0, s, p);
+    }
     launch_keydeps(p, wpl, s);
     launch_keydeps_big(p, s);
 }
