@@ -509,6 +509,7 @@ int32_t accord_deps_compute(accord_store *s)
     kp.big_list = kp.big_count + 16;
     kp.big_wex = s->bk_wex.as<uint32_t>();
     kp.tiny = (uint64_t)P <= 2ull * n ? 1u : 0u;      // <= 2 keys per txn on average: a store's key block
+    if (const char *e = getenv("ACCORD_TINY")) kp.tiny = e[0] == '1' ? 1u : 0u;   // dev aid: force on / off
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {
