@@ -275,17 +275,20 @@ __device__ __forceinline__ void lv_expand(const uint32_t (&bq)[16], int32_t (&d)
 __device__ __forceinline__ int32_t lv_matvec(int32_t acc, const int32_t (&d)[64], uint32_t bv, uint32_t lo,
                                              uint32_t hi)
 {
+    int32_t acc2 = acc;                     // two max chains: half the dependent-latency depth
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
         if ((uint32_t)(8 * g) < hi && (uint32_t)(8 * g + 8) > lo) {      // wave-uniform
 #pragma unroll
-            for (int m = 8 * g; m < 8 * g + 8; m += 2) {
+            for (int m = 8 * g; m < 8 * g + 8; m += 4) {
                 const int32_t s0 = (int32_t)readlane(bv, m), s1 = (int32_t)readlane(bv, m + 1);
+                const int32_t s2 = (int32_t)readlane(bv, m + 2), s3 = (int32_t)readlane(bv, m + 3);
                 acc = max(acc, max(s0 + d[m], s1 + d[m + 1]));
+                acc2 = max(acc2, max(s2 + d[m + 2], s3 + d[m + 3]));
             }
         }
     }
-    return acc;
+    return max(acc, acc2);
 }
 
 struct LvShared {
