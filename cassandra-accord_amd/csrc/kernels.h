@@ -163,7 +163,7 @@ struct RangeDepsParams {
     uint32_t kinds_present;             // entry kinds in the history (bit per kind; SP and XSP together)
     const uint64_t *c_local;            // witnessed counts (HistoryViews)
     const ClassCarry *ccarry;
-    uint4 *cp;                          // checkpoints: first history position with txn >= b << RK_CP_SHIFT
+    uint2 *cp;                          // checkpoints: first history position with txn >= b << RK_CP_SHIFT
                                         //   {position, its txn, (last Write before it) + 1, 0}
     uint32_t nkeys, ncp;                //   per key (cp[b * nkeys + k]), ncp blocks
     uint32_t *cnt_vals_exact;           // exact txnIds count per txn (range txns: written by the union pass)

@@ -371,10 +371,19 @@ constexpr int RK_WAVES = 4;
 constexpr int RK_FB = 4;                       // fill: groups of 64 history loads in flight
 constexpr int RK_EMAX = 128;                   // largest union class: 8192 deps per range txn
 
-// cp[b * K + k] = {x, txn(x), pw(x), 0}: x = first position of key k's segment [a, c) with
-// txn(x) >= b << RK_CP_SHIFT (c if none; txn then ~0), pw(x) = (last Write at or before x - 1) + 1
-// (global history positions, 0 if none).  Thread per history position: it owns the blocks
-// between its predecessor and itself.
+// cp[b * K + k] = {x, yo | d << 12} (8 bytes): x = first position of key k's segment [a, c) with
+// txn(x) >= b << RK_CP_SHIFT (c if none); yo = txn(x) - (b << RK_CP_SHIFT) saturated at 4095 (4095
+// if none) -- enough to compare txn(x) with any query txn of block b; d = x - pw(x), pw(x) =
+// (last Write at or before x - 1) + 1 (global history positions, 0 if none), RK_CP_DFAR when it
+// does not fit 20 bits (the reader recomputes pw).  Thread per history position: it owns the
+// blocks between its predecessor and itself.
+constexpr uint32_t RK_CP_YMAX = (1u << RK_CP_SHIFT) - 1u, RK_CP_DFAR = (1u << (32 - RK_CP_SHIFT)) - 1u;
+static_assert(RK_CP_SHIFT == 12, "checkpoint word: 12 bits of txn offset, 20 of Write distance");
+__device__ __forceinline__ uint2 rk_cp_make(uint32_t x, uint32_t yo, uint32_t pw)
+{
+    const uint32_t d = x - pw;
+    return make_uint2(x, yo | (d < RK_CP_DFAR ? d : RK_CP_DFAR) << RK_CP_SHIFT);
+}
 __device__ __forceinline__ uint32_t rk_pw_before(const RangeDepsParams &p, uint32_t x)
 {
     return x ? max(p.pw_local[x - 1], p.pw_carry[(x - 1) / p.pw_tile]) : 0u;
@@ -392,11 +401,13 @@ __global__ __launch_bounds__(256) void rk_checkpoint_kernel(uint32_t P, const ui
         const uint32_t b_lo = max(p.cp_base, x == a ? 0u : ((p.hist[x - 1] & ENT_TXN_MASK) >> RK_CP_SHIFT) + 1u);
         const uint32_t b_hi = min(t >> RK_CP_SHIFT, b_end - 1u);
         if (b_lo <= b_hi) {
-            const uint4 v = make_uint4(x, t, rk_pw_before(p, x), 0u);
-            for (uint32_t b = b_lo; b <= b_hi; ++b) p.cp[(size_t)(b - p.cp_base) * p.nkeys + k] = v;
+            const uint2 v = rk_cp_make(x, RK_CP_YMAX, rk_pw_before(p, x));     // blocks before t's
+            for (uint32_t b = b_lo; b < b_hi; ++b) p.cp[(size_t)(b - p.cp_base) * p.nkeys + k] = v;
+            p.cp[(size_t)(b_hi - p.cp_base) * p.nkeys + k] =
+                b_hi == t >> RK_CP_SHIFT ? rk_cp_make(x, t & RK_CP_YMAX, rk_pw_before(p, x)) : v;
         }
         if (x + 1 == c && (t >> RK_CP_SHIFT) + 1u < b_end) {
-            const uint4 v = make_uint4(c, 0xFFFFFFFFu, rk_pw_before(p, c), 0u);
+            const uint2 v = rk_cp_make(c, RK_CP_YMAX, rk_pw_before(p, c));
             for (uint32_t b = max(p.cp_base, (t >> RK_CP_SHIFT) + 1u); b < b_end; ++b)
                 p.cp[(size_t)(b - p.cp_base) * p.nkeys + k] = v;
         }
@@ -448,11 +459,11 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
     const size_t row1 = (size_t)(past ? 0u : (eb >> RK_CP_SHIFT) - p.cp_base) * p.nkeys,
                  row2 = (size_t)((thr >> RK_CP_SHIFT) - p.cp_base) * p.nkeys;
     uint32_t a[U], c[U];
-    uint4 e1[U], e2[U];
+    uint2 e1[U], e2[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         a[u] = c[u] = 0;
-        e1[u] = e2[u] = make_uint4(0u, 0u, 0u, 0u);
+        e1[u] = e2[u] = make_uint2(0u, 0u);
         if (valid[u]) {
             a[u] = p.seg_start[kk[u]]; c[u] = p.seg_end[kk[u]];
             e1[u] = p.cp[row1 + kk[u]]; e2[u] = p.cp[row2 + kk[u]];
@@ -462,13 +473,16 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
     for (int u = 0; u < U; ++u) {
         out[u] = RkSlice{0u, 0u, 0u};
         if (!(valid[u] && a[u] < c[u])) continue;
-        const uint32_t pos = past ? c[u] : e1[u].y >= eb ? e1[u].x : rk_first_ge(p.hist, e1[u].x + 1, c[u], eb);
+        const uint32_t pos = past ? c[u]
+                           : (e1[u].y & RK_CP_YMAX) >= (eb & RK_CP_YMAX) ? e1[u].x
+                                                                         : rk_first_ge(p.hist, e1[u].x + 1, c[u], eb);
         if (pos == a[u]) continue;
         uint32_t pw = 0, l = a[u];
         if (windowed) {
-            if (e2[u].y >= thr || e2[u].x >= pos) {
+            if ((e2[u].y & RK_CP_YMAX) >= (thr & RK_CP_YMAX) || e2[u].x >= pos) {
                 l = min(e2[u].x, pos);
-                pw = l == e2[u].x ? e2[u].z : rk_pw_before(p, pos);
+                const uint32_t d = e2[u].y >> RK_CP_SHIFT;
+                pw = l == e2[u].x && d != RK_CP_DFAR ? e2[u].x - d : rk_pw_before(p, l);
             } else {
                 l = rk_first_ge(p.hist, e2[u].x + 1, pos, thr);
                 pw = rk_pw_before(p, l);
@@ -951,7 +965,7 @@ void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s)
 
 size_t rangekeys_cp_bytes(uint32_t ncp, uint32_t nkeys)
 {
-    return (size_t)ncp * nkeys * sizeof(uint4) + 64;
+    return (size_t)ncp * nkeys * sizeof(uint2) + 64;
 }
 
 void launch_rangekeys_checkpoints(uint32_t PH, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s)

@@ -413,7 +413,7 @@ int32_t accord_deps_compute(accord_store *s)
         HIPCHECK(s, s->rk_cnt.ensure((size_t)nrt * 4 + 4));
         HIPCHECK(s, s->rk_off.ensure(((size_t)nrt + 1) * 4));
         HIPCHECK(s, s->rk_slices.ensure(s->rk_keys_total * 8 + 8));
-        rp.cp = s->rk_cp.as<uint4>();
+        rp.cp = s->rk_cp.as<uint2>();
         rp.rk_off = s->rk_off.as<uint32_t>();
         rp.rk_slices = s->rk_slices.as<uint2>();
     }
