@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = [
     "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
     "accord_comm_init", "accord_deps_exchange_merge", "accord_shard_timing",
-    "accord_waiting_on_compute", "accord_waiting_on_download", "accord_waiting_on_release",
+    "accord_waiting_on_compute", "accord_waiting_on_initialise", "accord_waiting_on_download", "accord_waiting_on_release",
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
@@ -119,7 +119,7 @@ class _Deps(C.Structure):
 class _WaitingOn(C.Structure):
     _fields_ = [("n", C.c_uint32), ("max_level", C.c_uint32), ("words_total", C.c_uint64),
                 ("preds_total", C.c_uint64), ("level", _u32p), ("wo_off", _u32p), ("words", _u64p),
-                ("owner", C.c_void_p)]
+                ("owner", C.c_void_p), ("applied_or_invalidated", _u64p)]
 
 
 class _RangeStab(C.Structure):
@@ -186,6 +186,7 @@ def lib() -> C.CDLL:
         L.accord_deps_exchange_merge.argtypes = [C.c_void_p, C.c_uint32]
         L.accord_shard_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.accord_waiting_on_compute.argtypes = [C.c_void_p]
+        L.accord_waiting_on_initialise.argtypes = [C.c_void_p]
         L.accord_waiting_on_download.argtypes = [C.c_void_p, C.POINTER(_WaitingOn)]
         L.accord_waiting_on_release.argtypes = [C.POINTER(_WaitingOn)]
         L.accord_waiting_on_release.restype = None
@@ -509,6 +510,7 @@ class WaitingOn:
     words: np.ndarray
     max_level: int
     preds_total: int
+    applied_or_invalidated: "np.ndarray | None" = None   # accord_waiting_on_initialise only
 
     def bits(self, i: int) -> np.ndarray:
         return self.words[self.wo_off[i]:self.wo_off[i + 1]]
@@ -797,12 +799,20 @@ class CommandStore:
             return WaitingOn(level=_arr(w.level, w.n, np.uint32).copy(),
                              wo_off=_arr(w.wo_off, w.n + 1, np.uint32).copy(),
                              words=_arr(w.words, w.words_total, np.uint64).copy(),
-                             max_level=int(w.max_level), preds_total=int(w.preds_total))
+                             max_level=int(w.max_level), preds_total=int(w.preds_total),
+                             applied_or_invalidated=(_arr(w.applied_or_invalidated, w.words_total, np.uint64).copy()
+                                                     if w.applied_or_invalidated else None))
         finally:
             lib().accord_waiting_on_release(C.byref(w))
 
     def waiting_on(self) -> "WaitingOn":
         self.waiting_on_compute()
+        return self.waiting_on_download()
+
+    def waiting_on_initialise(self) -> "WaitingOn":
+        """Commands.initialiseWaitingOn + updateWaitingOn of the last batch against the registered
+        statuses (registered-status stores; include/accord_deps.h accord_waiting_on_initialise)."""
+        self._check(lib().accord_waiting_on_initialise(self._h))
         return self.waiting_on_download()
 
     def waiting_on_timing(self):

@@ -373,9 +373,77 @@ __global__ __launch_bounds__(256) void rk_general_kernel(RkGenParams q)
 
 } // namespace
 
+namespace {
+
+// ---- WaitingOn of a registered-status store's batch ----
+// Commands.initialiseWaitingOn (local/Commands.java:735-753) and its initial updateWaitingOn
+// (:755-830; WaitingOn.Update, local/Command.java:1403-1600) against the registered statuses: the
+// RangeDeps txnId bits start set and each dep that hasBeen(PreCommitted) is resolved -- truncated /
+// invalidated: setAppliedOrInvalidated; executing after us (own kind not awaitsOnlyDeps):
+// removeWaitingOn; APPLIED: setAppliedAndPropagate (the dep's own appliedOrInvalidated taken as
+// empty) -- the KeyDeps key bits stay set (CommandsForKey.notify clears them later).  The
+// appliedOrInvalidated set exists for Range-domain txns only (Update(TxnId, Keys, ...) :1431-1437).
+// A thread per txn builds its words one at a time.
+__global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t *__restrict__ msb,
+                                                      const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
+                                                      const uint32_t *__restrict__ txn_index,
+                                                      const uint32_t *__restrict__ kd_key_off,
+                                                      const uint32_t *__restrict__ rd_val_off,
+                                                      const uint32_t *__restrict__ rd_vals,
+                                                      const uint32_t *__restrict__ wo_off, StatusView v,
+                                                      unsigned long long *__restrict__ words,
+                                                      unsigned long long *__restrict__ aoi)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const uint32_t g = txn_index[t], ost = status_of(v, g);
+        const uint64_t l = lsb[t];
+        // own executeAt: the registered one once it has one, else the TxnId
+        const Ts own = ost >= ST_ACCEPTED && ost <= ST_APPLIED ? exec_of(v, g) : Ts{msb[t], l, node[t]};
+        const uint32_t kind = (uint32_t)(l >> 1) & 7u;
+        const bool only_deps = kind == 4u || kind == 2u;      // Txn.Kind.awaitsOnlyDeps (Txn.java:211-214)
+        const bool range_domain = (l & 1u) != 0;
+        const uint32_t r0 = rd_val_off[t], R = rd_val_off[t + 1] - r0;
+        const uint32_t bits = R + (kd_key_off[t + 1] - kd_key_off[t]);
+        const uint32_t w0 = wo_off[t], nw = wo_off[t + 1] - w0;
+        for (uint32_t q = 0; q < nw; ++q) {
+            unsigned long long wv = 0, av = 0;
+            const uint32_t b0 = q * 64u, b1 = min(bits, b0 + 64u);
+            for (uint32_t b = b0; b < b1; ++b) {
+                const unsigned long long bit = 1ull << (b & 63u);
+                if (b >= R) { wv |= bit; continue; }            // key bits
+                const uint32_t d = rd_vals[r0 + b], st = status_of(v, d);
+                bool wait = true, applied = false;
+                if (st >= ST_COMMITTED) {                       // hasBeen(PreCommitted)
+                    if (st >= ST_INVALID) { wait = false; applied = true; }                 // truncated / invalidated
+                    else if (!only_deps && tcmp(exec_of(v, d), own) > 0) wait = false;     // executes after us
+                    else if (st == ST_APPLIED) { wait = false; applied = true; }
+                }
+                if (wait) wv |= bit;
+                if (applied && range_domain) av |= bit;
+            }
+            words[w0 + q] = wv;
+            aoi[w0 + q] = av;
+        }
+    }
+}
+
+} // namespace
+
 namespace accord_impl {
 
 bool registered_mode(const accord_store *s) { return s->resident && s->cfg.window == ACCORD_WINDOW_NONE; }
+
+// WaitingOn words + appliedOrInvalidated of the last computed batch (wo_off already scanned)
+int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned long long *words,
+                               unsigned long long *aoi)
+{
+    if (s->n)
+        hipLaunchKernelGGL(wo_init_kernel, dim3(grid_for(s->n)), dim3(256), 0, s->stream, s->n, s->msb.as<uint64_t>(),
+                           s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
+                           s->kd_key_off.as<uint32_t>(), s->rd_val_off.as<uint32_t>(), s->rd_vals.as<uint32_t>(), wo_off,
+                           view_of(s), words, aoi);
+    return ACCORD_OK;
+}
 
 // After the segment stage of a registered-status store: pairs on keys with registered entries get
 // their emitted entries materialised; returns the history array the fill must read.

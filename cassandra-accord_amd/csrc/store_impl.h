@@ -130,7 +130,8 @@ struct accord_store {
     float xchg_ms = 0, merge_ms = 0;
     // WaitingOn + levelling (waiting_on_abi.cpp)
     bool wo_done = false;
-    DevBuf wo_cnt, wo_off, wo_words, pred_cnt, pred_off, preds, level, wo_info, lv_tmp;
+    DevBuf wo_cnt, wo_off, wo_words, wo_aoi, pred_cnt, pred_off, preds, level, wo_info, lv_tmp;
+    bool wo_has_aoi = false;       // accord_waiting_on_initialise: appliedOrInvalidated words in wo_aoi
     uint64_t wo_words_total = 0, preds_total = 0;
     uint32_t max_level = 0;
     float wo_ms[3] = {0, 0, 0};
@@ -168,6 +169,8 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
 int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
 int32_t status_join_batch(accord_store *s);
 int32_t status_range_keys(accord_store *s, const accord::RangeDepsParams &rp, bool fill);
+int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned long long *words,
+                               unsigned long long *aoi);
 // RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp)
 int32_t redundant_apply(accord_store *s);
 }

@@ -15,7 +15,7 @@ void record(accord_store *s, int stage)
 
 struct HostWaitingOnOwner {
     std::vector<uint32_t> level, wo_off;
-    std::vector<uint64_t> words;
+    std::vector<uint64_t> words, aoi;
 };
 
 } // namespace
@@ -37,6 +37,7 @@ int32_t accord_waiting_on_compute(accord_store *s)
     const size_t n1 = (size_t)n + 1;
     hipStream_t st = s->stream;
     s->wo_done = false;
+    s->wo_has_aoi = false;
     HIPCHECK(s, s->wo_cnt.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->wo_off.ensure(n1 * 4));
     HIPCHECK(s, s->pred_cnt.ensure((size_t)n * 4 + 4));
@@ -101,6 +102,46 @@ int32_t accord_waiting_on_compute(accord_store *s)
     return ACCORD_OK;
 }
 
+int32_t accord_waiting_on_initialise(accord_store *s)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (!accord_impl::registered_mode(s))
+        return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise needs a registered-status store "
+                                         "(resident, window ACCORD_WINDOW_NONE)");
+    if (!s->computed) return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise before accord_deps_compute");
+    if (s->merged || s->ds_cur >= 0)
+        return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise runs on the batch's computed deps");
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    const uint32_t n = s->n;
+    hipStream_t st = s->stream;
+    s->wo_done = false;
+    HIPCHECK(s, s->wo_cnt.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->wo_off.ensure(((size_t)n + 1) * 4));
+    HIPCHECK(s, s->level.ensure((size_t)n * 4 + 4));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n), s->stream));
+    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    accord::launch_wo_words_count(n, s->kd_key_off.as<uint32_t>(), s->rd_val_off.as<uint32_t>(),
+                                  s->wo_cnt.as<uint32_t>(), st);
+    accord::exclusive_scan_u32(s->wo_cnt.as<uint32_t>(), s->wo_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
+    HIPCHECK(s, hipMemcpyAsync(s->pinned->totals, dev->totals, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    s->wo_words_total = s->pinned->totals[0];
+    HIPCHECK(s, s->wo_words.ensure(s->wo_words_total * 8 + 8));
+    HIPCHECK(s, s->wo_aoi.ensure(s->wo_words_total * 8 + 8));
+    int32_t rc = accord_impl::status_waiting_on_init(s, s->wo_off.as<uint32_t>(), s->wo_words.as<unsigned long long>(),
+                                                     s->wo_aoi.as<unsigned long long>());
+    if (rc != ACCORD_OK) return rc;
+    if (n) HIPCHECK(s, hipMemsetAsync(s->level.p, 0, (size_t)n * 4, st));   // no levelling here
+    HIPCHECK(s, hipStreamSynchronize(st));
+    HIPCHECK(s, hipGetLastError());
+    s->preds_total = 0;
+    s->max_level = 0;
+    s->wo_has_aoi = true;
+    s->wo_done = true;
+    return ACCORD_OK;
+}
+
 int32_t accord_waiting_on_download(accord_store *s, accord_waiting_on *out)
 {
     if (!s || !out) return fail(s, ACCORD_ERR_ARG, "null argument");
@@ -113,6 +154,7 @@ int32_t accord_waiting_on_download(accord_store *s, accord_waiting_on *out)
         o->level.resize(n + 1);
         o->wo_off.resize(n + 1);
         o->words.resize(s->wo_words_total + 1);
+        if (s->wo_has_aoi) o->aoi.resize(s->wo_words_total + 1);
     } catch (...) {
         delete o;
         return fail(s, ACCORD_ERR_OOM, "out of host memory");
@@ -122,6 +164,8 @@ int32_t accord_waiting_on_download(accord_store *s, accord_waiting_on *out)
     if (e == hipSuccess) e = hipMemcpyAsync(o->wo_off.data(), s->wo_off.p, (n + 1) * 4, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess && s->wo_words_total)
         e = hipMemcpyAsync(o->words.data(), s->wo_words.p, s->wo_words_total * 8, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess && s->wo_has_aoi && s->wo_words_total)
+        e = hipMemcpyAsync(o->aoi.data(), s->wo_aoi.p, s->wo_words_total * 8, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
         delete o;
@@ -135,6 +179,7 @@ int32_t accord_waiting_on_download(accord_store *s, accord_waiting_on *out)
     out->level = o->level.data();
     out->wo_off = o->wo_off.data();
     out->words = o->words.data();
+    out->applied_or_invalidated = s->wo_has_aoi ? o->aoi.data() : nullptr;
     out->owner = o;
     return ACCORD_OK;
 }

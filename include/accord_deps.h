@@ -371,9 +371,26 @@ typedef struct {
     uint32_t *wo_off;           /* [n+1] word offsets */
     uint64_t *words;            /* [words_total] */
     void     *owner;            /* library-private */
+    /* accord_waiting_on_initialise only (else NULL): WaitingOn.appliedOrInvalidated in the words'
+     * layout -- bits [0, R_i) of Range-domain txns; all zero for Key-domain txns (null there) */
+    uint64_t *applied_or_invalidated;
 } accord_waiting_on;
 
 int32_t accord_waiting_on_compute(accord_store *store);                 /* device-resident */
+/* Commands.initialiseWaitingOn (local/Commands.java:735-753) with its initial updateWaitingOn
+ * (:755-830; WaitingOn.Update, local/Command.java:1403-1600) for every txn of the last computed batch
+ * of a registered-status store (resident, ACCORD_WINDOW_NONE), against the statuses registered at
+ * the time of the call (register the batch's txns COMMITTED/STABLE with their executeAt first; a txn
+ * without an executeAt is taken at its TxnId).  words: bits [0, R_i) = RangeDeps txnIds, set unless
+ * the dep hasBeen(PreCommitted) and is truncated / invalidated (INVALID_OR_TRUNCATED, ERASED:
+ * setAppliedOrInvalidated), executes after the txn (dep executeAt > own executeAt, own kind not
+ * awaitsOnlyDeps: removeWaitingOn) or is APPLIED (setAppliedAndPropagate); bits [R_i, R_i + K_i) =
+ * KeyDeps keys, set (CommandsForKey.notify clears them as the keys' predecessors apply).  The
+ * propagation of an applied dep's own appliedOrInvalidated set is not modelled (taken as empty), nor
+ * are pre-bootstrap / stale ranges (removeRedundantDependencies) or executeAtLeast.  level = 0,
+ * max_level = 0, preds_total = 0 (levelling is accord_waiting_on_compute's model).  Download with
+ * accord_waiting_on_download (applied_or_invalidated set). */
+int32_t accord_waiting_on_initialise(accord_store *store);
 int32_t accord_waiting_on_download(accord_store *store, accord_waiting_on *out);
 void    accord_waiting_on_release(accord_waiting_on *wo);
 /* device ms of the last accord_waiting_on_compute: bitsets, reduced predecessors, levelling */

@@ -1026,6 +1026,54 @@ int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level, uint32_t *wo_of
     return 0;
 }
 
+/* Commands.initialiseWaitingOn + the initial updateWaitingOn (see oracle.h).  Txn.Kind.awaitsOnlyDeps
+ * (primitives/Txn.java:211-214): ExclusiveSyncPoint, EphemeralRead. */
+int or_initialise_waiting_on(const or_deps *d, uint32_t n, const uint64_t *lsb, const uint64_t *own_msb,
+                             const uint64_t *own_lsb, const int32_t *own_node, const uint8_t *status,
+                             const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                             uint32_t *wo_off, uint64_t **wo_words, uint64_t **aoi_words)
+{
+    enum { COMMITTED = 4, APPLIED = 6, INVALID_OR_TRUNCATED = 7 };
+    size_t total = 0;
+    wo_off[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t bits = (d->rd_val_off[i + 1] - d->rd_val_off[i]) + (d->kd_key_off[i + 1] - d->kd_key_off[i]);
+        total += (bits + 63) / 64;
+        wo_off[i + 1] = (uint32_t)total;
+    }
+    uint64_t *w = (uint64_t *)calloc(total ? total : 1, sizeof(uint64_t));
+    uint64_t *a = (uint64_t *)calloc(total ? total : 1, sizeof(uint64_t));
+    if (!w || !a) { free(w); free(a); return -1; }
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t kind = (uint32_t)(lsb[i] >> 1) & 7u;
+        const int awaits_only_deps = kind == 4u || kind == 2u;      /* ExclusiveSyncPoint, EphemeralRead */
+        const int range_domain = (int)(lsb[i] & 1u);                 /* Routable.Domain.Range */
+        const uint32_t r0 = d->rd_val_off[i], R = d->rd_val_off[i + 1] - r0;
+        const uint32_t K = d->kd_key_off[i + 1] - d->kd_key_off[i];
+        uint64_t *wi = w + wo_off[i], *ai = a + wo_off[i];
+        /* WaitingOn.Update(txnId, deps): the waiting set starts with every txnId and key */
+        for (uint32_t b = 0; b < R + K; ++b) wi[b / 64] |= 1ULL << (b & 63);
+        /* forEachWaitingOnId: txnId bits in reverse order */
+        for (uint32_t j = R; j-- > 0;) {
+            const uint32_t g = d->rd_vals[r0 + j];
+            const uint32_t st = status[g];
+            if (st < COMMITTED) continue;                            /* !hasBeen(PreCommitted) */
+            const uint64_t bit = 1ULL << (j & 63);
+            if (st >= INVALID_OR_TRUNCATED) {                        /* hasBeen(Truncated): setAppliedOrInvalidated */
+                if (wi[j / 64] & bit) { wi[j / 64] &= ~bit; if (range_domain) ai[j / 64] |= bit; }
+            } else if (!awaits_only_deps &&
+                       or_ts_compare(emsb[g], elsb[g], enode[g], own_msb[i], own_lsb[i], own_node[i]) > 0) {
+                wi[j / 64] &= ~bit;                                  /* executes after us: removeWaitingOn */
+            } else if (st == APPLIED) {                              /* setAppliedAndPropagate */
+                if (wi[j / 64] & bit) { wi[j / 64] &= ~bit; if (range_domain) ai[j / 64] |= bit; }
+            }
+        }
+    }
+    *wo_words = w;
+    *aoi_words = a;
+    return 0;
+}
+
 /* Event-driven restatement of execution readiness (validates the levelling abstraction, SURVEY.md
  * §8a a13): every txn starts with its WaitingOn bits (Commands.initialiseWaitingOn,
  * local/Commands.java:735-753).  A range-dep bit clears when that dep applies

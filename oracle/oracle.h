@@ -125,6 +125,24 @@ uint32_t or_stab_key(uint32_t nr, const uint32_t *rs, const uint32_t *re, uint32
 int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level,
                   uint32_t *wo_off /* [n+1] */, uint64_t **wo_words /* malloc'd */);
 
+/* Commands.initialiseWaitingOn (local/Commands.java:735-753) with its initial updateWaitingOn
+ * (:755-830; WaitingOn.Update, local/Command.java:1403-1600) for the n txns of one batch of a
+ * registered-status store: deps d hold global positions; status/emsb/elsb/enode give every
+ * position's InternalStatus ordinal (CommandsForKey.java:194-203; 8 = SaveStatus Erased) and
+ * executeAt at the moment the WaitingOn is built; own_* is each txn's own executeAt.
+ *   bits [0, R)     RangeDeps txnIds, set; then each dep that hasBeen(PreCommitted) (>= COMMITTED):
+ *                   truncated / invalidated (>= INVALID_OR_TRUNCATED) -> setAppliedOrInvalidated;
+ *                   else executeAt > own executeAt (own kind not awaitsOnlyDeps) -> removeWaitingOn;
+ *                   else APPLIED -> setAppliedAndPropagate (the dep's own appliedOrInvalidated
+ *                   taken as empty); else still waiting
+ *   bits [R, R+K)   KeyDeps keys, set (initialiseWaiting; CommandsForKey.notify clears them later)
+ *   aoi_words       appliedOrInvalidated (same word layout; Range-domain txns only, null for keys)
+ * Words and aoi are malloc'd.  0 ok. */
+int or_initialise_waiting_on(const or_deps *d, uint32_t n, const uint64_t *lsb, const uint64_t *own_msb,
+                             const uint64_t *own_lsb, const int32_t *own_node, const uint8_t *status,
+                             const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode,
+                             uint32_t *wo_off /* [n+1] */, uint64_t **wo_words, uint64_t **aoi_words);
+
 /* Event-driven readiness simulation (bits cleared by applies, CFK notify per key); round[i] is the
  * synchronous round in which txn i executes.  Must equal or_waiting_on's level.  0 ok, -7 stuck. */
 int or_waiting_on_events(const or_deps *d, uint32_t n, uint32_t *round_out);

@@ -65,6 +65,8 @@ def lib():
         L.or_stab_key.restype = C.c_uint32
         L.or_waiting_on.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p, _u32p, C.POINTER(_u64p)]
         L.or_waiting_on_events.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u32p]
+        L.or_initialise_waiting_on.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u64p, _u64p, _u64p, _i32p, _u8p,
+                                               _u64p, _u64p, _i32p, _u32p, C.POINTER(_u64p), C.POINTER(_u64p)]
         L.or_levels_cfk.argtypes = [C.POINTER(_OrStream), C.POINTER(_OrDeps), _u32p]
         L.or_deps_union.argtypes = [C.c_uint32, C.POINTER(_OrDeps), C.POINTER(_OrDeps)]
         L.or_deps_slice.argtypes = [C.POINTER(_OrDeps), _u32p, _u32p, _u32p, C.c_uint32, C.POINTER(_OrDeps)]
@@ -270,6 +272,39 @@ def waiting_on(p: PartialDeps):
     w = _arr(words, int(wo_off[-1]), np.uint64)
     C.CDLL(None).free(words)
     return level[:n].copy(), wo_off, w
+
+
+def initialise_waiting_on(p: PartialDeps, s: Stream, g0: int, status, execs):
+    """Commands.initialiseWaitingOn + the initial updateWaitingOn (or_initialise_waiting_on) of
+    batch s (txn t at global position g0 + t, deps p with global positions) against status[g] /
+    execs[g] (None or (msb, lsb, node)) of every position.  Returns (wo_off, words, aoi)."""
+    n = s.n
+    G = len(status)
+    st = np.ascontiguousarray(status, dtype=np.uint8)
+    em = np.zeros(max(1, G), np.uint64); el = np.zeros(max(1, G), np.uint64); en = np.zeros(max(1, G), np.int32)
+    for g, x in enumerate(execs):
+        if x is not None:
+            em[g], el[g], en[g] = x
+    om = s.msb.astype(np.uint64).copy(); ol = s.lsb.astype(np.uint64).copy(); on = s.node.astype(np.int32).copy()
+    for t in range(n):
+        g = g0 + t
+        if 3 <= int(st[g]) <= 6 and execs[g] is not None:      # ACCEPTED..APPLIED carry an executeAt
+            om[t], ol[t], on[t] = execs[g]
+    d, keep = _c_deps(p)
+    wo_off = np.zeros(n + 1, dtype=np.uint32)
+    words, aoi = _u64p(), _u64p()
+    lsb = np.ascontiguousarray(s.lsb, dtype=np.uint64)
+    rc = lib().or_initialise_waiting_on(C.byref(d), n, lsb.ctypes.data_as(_u64p), om.ctypes.data_as(_u64p),
+                                        ol.ctypes.data_as(_u64p), on.ctypes.data_as(_i32p), st.ctypes.data_as(_u8p),
+                                        em.ctypes.data_as(_u64p), el.ctypes.data_as(_u64p), en.ctypes.data_as(_i32p),
+                                        wo_off.ctypes.data_as(_u32p), C.byref(words), C.byref(aoi))
+    if rc != 0:
+        raise OracleError(rc)
+    w = _arr(words, int(wo_off[-1]), np.uint64)
+    a = _arr(aoi, int(wo_off[-1]), np.uint64)
+    C.CDLL(None).free(words)
+    C.CDLL(None).free(aoi)
+    return wo_off, w, a
 
 
 def waiting_on_events(p: PartialDeps):
