@@ -370,6 +370,9 @@ __global__ __launch_bounds__(RT_WAVES * 64) void rangedeps_tile_kernel(RangeDeps
 constexpr int RK_WAVES = 4;
 constexpr int RK_FB = 4;                       // fill: groups of 64 history loads in flight
 constexpr int RK_EMAX = 128;                   // largest union class: 8192 deps per range txn
+// fill: a chunk whose raw candidates fit RK_CM (and no slice is longer than RK_CMRAW) maps every
+// candidate to its history position through an LDS table, one read instead of a binary search
+constexpr uint32_t RK_CM = 640, RK_CMRAW = 32;
 
 // cp[b * K + k] = {x, yo | d << 12} (8 bytes): x = first position of key k's segment [a, c) with
 // txn(x) >= b << RK_CP_SHIFT (c if none); yo = txn(x) - (b << RK_CP_SHIFT) saturated at 4095 (4095
@@ -535,8 +538,10 @@ template <bool FILL, int U>                          // U keys per lane per step
 __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParams p)
 {
     __shared__ uint32_t rex_all[RK_WAVES][64 * U], rlo_all[RK_WAVES][64 * U];
+    __shared__ uint32_t cmap_all[FILL ? RK_WAVES : 1][FILL ? RK_CM : 1];
     const uint32_t w = wave_id(), lane = lane_id();
     uint32_t *rex = rex_all[w], *rlo = rlo_all[w];
+    uint32_t *cmap = cmap_all[FILL ? w : 0];
     const uint64_t lt = lanemask_lt();
     for (uint32_t li = blockIdx.x * RK_WAVES + w; li < p.n_range_txns; li += gridDim.x * RK_WAVES) {
         const uint32_t i = p.range_txns[li];
@@ -597,7 +602,7 @@ __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParam
                 // headers of the chunk's U*64 keys, their raw entries' prefix in LDS, then the body of
                 // the whole chunk with RK_FB groups of 64 history loads in flight
                 const uint32_t body0 = body;
-                uint32_t rbase = 0;
+                uint32_t rbase = 0, rexu[U], rawu[U], mraw = 0;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t key = c0 + 64 * u + lane;
@@ -611,15 +616,41 @@ __global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParam
                         p.kd_k2v[k2v_base + ns] = (int32_t)(kc_total + body + wincl);
                     }
                     const uint32_t rincl = wave_incl_scan(raw);
-                    rex[u * 64 + lane] = rbase + rincl - raw;
+                    rex[u * 64 + lane] = rexu[u] = rbase + rincl - raw;
                     rlo[u * 64 + lane] = sl[u].lo;
+                    rawu[u] = raw;
+                    mraw = max(mraw, raw);
                     rbase += readlane(rincl, 63);
                     kc += (uint32_t)__popcll(hb);
                     body += readlane(wincl, 63);
                 }
-                wave_lds_sync();
                 // candidates in key order; body position = running witnessed count
                 uint32_t run = body0;
+                if (rbase <= RK_CM && readlane(wave_incl_max(mraw), 63) <= RK_CMRAW) {   // wave-uniform
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        for (uint32_t j = 0; j < rawu[u]; ++j) cmap[rexu[u] + j] = sl[u].lo + j;
+                    wave_lds_sync();
+                    for (uint32_t w0 = 0; w0 < rbase; w0 += 64 * RK_FB) {
+                        uint32_t e[RK_FB];
+#pragma unroll
+                        for (int b = 0; b < RK_FB; ++b) {
+                            const uint32_t rr = w0 + 64 * b + lane;
+                            e[b] = rr < rbase ? p.hist[cmap[rr]] : 0u;
+                        }
+#pragma unroll
+                        for (int b = 0; b < RK_FB; ++b) {
+                            const uint32_t rr = w0 + 64 * b + lane;
+                            const bool wit = rr < rbase && ((wmask >> (e[b] >> ENT_KIND_SHIFT)) & 1u);
+                            const uint64_t wb = __ballot(wit);
+                            if (wit) p.kd_k2v[k2v_base + kc_total + run + (uint32_t)__popcll(wb & lt)] = (int32_t)(e[b] & ENT_TXN_MASK);
+                            run += (uint32_t)__popcll(wb);
+                        }
+                    }
+                    wave_lds_sync();
+                    continue;
+                }
+                wave_lds_sync();
                 for (uint32_t w0 = 0; w0 < rbase; w0 += 64 * RK_FB) {
                     uint32_t e[RK_FB];
 #pragma unroll
