@@ -174,3 +174,21 @@ def test_gpu_equals_oracle_accept_batches(gpu_device):
     s = generate_stream(2000, 4, 200, 0.99, 0.5, range_frac=0.2, range_len_max=30, seed=43)
     acc = s.accept(frac=0.5, max_delay=30, seed=43)
     run_schedule(s, 200, [0, 500, 1100, 1600, 2000], 43, accept=acc)
+
+
+@pytest.mark.gpu
+def test_initialise_needs_registered_store(gpu_device):
+    from accord_amd import IllegalStateException
+    s = generate_stream(300, 2, 50, 0.0, 0.5, seed=44)
+    with CommandStore(device=0, key_lo=0, key_hi=50, window=256) as st:          # status-at-time model
+        st.calculate_deps_batch(s)
+        with pytest.raises(IllegalStateException):
+            st.waiting_on_initialise()
+    with CommandStore(device=0, key_lo=0, key_hi=50, window=WINDOW_NONE, resident=True) as st:
+        with pytest.raises(IllegalStateException):                              # nothing computed yet
+            st.waiting_on_initialise()
+        d = st.calculate_deps_batch(s)
+        w = st.waiting_on_initialise()                                           # nothing registered: all set
+        assert np.array_equal(w.words, O.waiting_on(d)[2])
+        assert w.max_level == 0 and not w.level.any() and not w.applied_or_invalidated.any()
+
