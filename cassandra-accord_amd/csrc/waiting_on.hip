@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void wo_words_count_kernel(uint32_t n, const u
 // The reduction needs witnesses(i) ⊆ witnesses(Write) = {R, W}; SyncPoints (which also witness
 // SyncPoints, that a Write does not) and range txns (whose KeyDeps come from rangekeys, not from
 // key histories) keep their full dependency lists.
+constexpr uint32_t WO_KB = 4;      // keys per txn walked with batched loads (larger txns: one key at a time)
 template <bool FILL>
 __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
 {
@@ -67,7 +68,42 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
         const bool reduce = (l & 1) == 0 && (wmask & ~0x3u) == 0;
         uint32_t cnt = 0;
         uint32_t o = FILL ? p.pred_off[i] : 0;
-        if (reduce) {
+        const uint32_t q0 = p.key_off[i], k = p.key_off[i + 1] - q0;
+        if (reduce && k <= WO_KB) {
+            // the same walk with each dependent round (slices, Write bounds, last Writes) issued for
+            // all keys at once
+            PairSlice ps[WO_KB];
+            uint32_t pw[WO_KB], lw[WO_KB];
+#pragma unroll
+            for (uint32_t j = 0; j < WO_KB; ++j) ps[j] = j < k ? p.slice[q0 + j] : PairSlice{0u, 0u, 0u, 0u};
+#pragma unroll
+            for (uint32_t j = 0; j < WO_KB; ++j) {
+                const uint32_t x = ps[j].pos - 1;
+                pw[j] = ps[j].pos != ps[j].lo ? max(p.pw_local[x], p.pw_carry[x / p.pw_tile]) : 0u;   // (last Write <= x) + 1
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < WO_KB; ++j) lw[j] = pw[j] > ps[j].lo ? p.hist[pw[j] - 1] : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < WO_KB; ++j) {
+                const uint32_t pos = ps[j].pos, lo = ps[j].lo;
+                if (pos == lo) continue;
+                uint32_t from = lo;
+                if (pw[j] > lo) {                                                   // lw inside the slice
+                    ++cnt;
+                    if (FILL) p.preds[o++] = lw[j] & ENT_TXN_MASK;
+                    from = pw[j];
+                }
+                if (wmask & 1u) {                                                   // Reads after lw
+                    for (uint32_t e = from; e < pos; ++e) {
+                        const uint32_t ev = p.hist[e];
+                        if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {
+                            ++cnt;
+                            if (FILL) p.preds[o++] = ev & ENT_TXN_MASK;
+                        }
+                    }
+                }
+            }
+        } else if (reduce) {
             for (uint32_t q = p.key_off[i]; q < p.key_off[i + 1]; ++q) {
                 const PairSlice ps = p.slice[q];
                 const uint32_t pos = ps.pos, lo = ps.lo;
