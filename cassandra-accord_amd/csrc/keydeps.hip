@@ -532,10 +532,18 @@ __global__ __launch_bounds__(256) void keydeps_sizes_kernel(uint32_t n, const ui
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t k0 = key_off[i], k1 = key_off[i + 1];
         uint32_t kc = 0, body = 0;
-        for (uint32_t q = k0; q < k1; ++q) {
-            const uint32_t c = slice[q].wcnt;
-            kc += c ? 1u : 0u;
-            body += c;
+        if (k1 - k0 <= 8) {                   // all loads issued before any is consumed
+            uint32_t c[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) c[j] = k0 + j < k1 ? slice[k0 + j].wcnt : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) { kc += c[j] ? 1u : 0u; body += c[j]; }
+        } else {
+            for (uint32_t q = k0; q < k1; ++q) {
+                const uint32_t c = slice[q].wcnt;
+                kc += c ? 1u : 0u;
+                body += c;
+            }
         }
         cnt_keys[i] = kc;
         cnt_vub[i] = body;
