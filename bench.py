@@ -138,6 +138,7 @@ def main():
     t0 = time.perf_counter()
     stage = {"validate": 0.0, "sort": 0.0, "segment": 0.0, "count": 0.0, "scan": 0.0, "fill": 0.0, "range_fill": 0.0,
              "compact": 0.0, "total": 0.0, "exchange": 0.0, "merge": 0.0, "wo_bits": 0.0, "wo_preds": 0.0, "wo_level": 0.0}
+    count_detail, scan_spins, scan_fallbacks = {}, 0, 0
     for _ in range(args.steps):
         step()
         t = store.timing()
@@ -150,6 +151,10 @@ def main():
         stage["range_fill"] += t.range_ms
         stage["compact"] += t.compact_ms
         stage["total"] += t.total_ms
+        for k, v in t.count_detail.items():
+            count_detail[k] = count_detail.get(k, 0.0) + v
+        scan_spins += t.scan_spins
+        scan_fallbacks += t.scan_fallbacks
         if world > 1:
             xms, mms = store.shard_timing()
             stage["exchange"] += xms
@@ -169,6 +174,8 @@ def main():
         elapsed = float(tt.item())
     for k in stage:
         stage[k] /= max(1, args.steps)
+    for k in count_detail:
+        count_detail[k] /= max(1, args.steps)
 
     # sizes for the byte model: the rank's own computed partial (before the exchange)
     store.compute()
@@ -242,6 +249,9 @@ def main():
         "deps_per_s": D * world * args.steps / elapsed,
         "sizes": {"N": n, "P": P, "keys_out": kc, "U": U, "D": D},
         "stage_ms": stage,
+        "count_stage_ms": count_detail,
+        "scan_lookback": {"spins_per_step": scan_spins / max(1, args.steps),
+                          "fallbacks_total": scan_fallbacks},
         "roofline": {"kernel": "fill stage: txnrec_kernel + keydeps_fast_kernel<1> + keydeps_kernel<1,8>",
                      "bound": "hbm",
                      "achieved": fill_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",

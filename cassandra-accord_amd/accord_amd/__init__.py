@@ -48,7 +48,7 @@ EXPORTED_SYMBOLS = [
     "accord_deps_batch", "accord_deps_release", "accord_batch_upload", "accord_deps_compute",
     "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
-    "accord_comm_init", "accord_deps_exchange_merge", "accord_shard_timing",
+    "accord_comm_init", "accord_deps_exchange_merge", "accord_deps_exchange_local", "accord_shard_timing",
     "accord_waiting_on_compute", "accord_waiting_on_initialise", "accord_waiting_on_download", "accord_waiting_on_release",
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
@@ -143,7 +143,10 @@ class _Timing(C.Structure):
                 ("count_ms", C.c_float), ("scan_ms", C.c_float), ("fill_ms", C.c_float),
                 ("range_ms", C.c_float), ("total_ms", C.c_float),
                 ("compact_ms", C.c_float), ("reserved_ms", C.c_float),
-                ("pairs", C.c_uint64), ("hist_entries", C.c_uint64)]
+                ("pairs", C.c_uint64), ("hist_entries", C.c_uint64),
+                ("count_rk_cp_ms", C.c_float), ("count_rk_nkeys_ms", C.c_float), ("count_kd_sizes_ms", C.c_float),
+                ("count_rk_ms", C.c_float), ("count_rd_ms", C.c_float), ("reserved2_ms", C.c_float),
+                ("scan_spins", C.c_uint64), ("scan_fallbacks", C.c_uint64)]
 
 
 class _WorkloadCfg(C.Structure):
@@ -184,6 +187,7 @@ def lib() -> C.CDLL:
         L.accord_comm_unique_id.argtypes = [C.c_void_p]
         L.accord_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
         L.accord_deps_exchange_merge.argtypes = [C.c_void_p, C.c_uint32]
+        L.accord_deps_exchange_local.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32]
         L.accord_shard_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.accord_waiting_on_compute.argtypes = [C.c_void_p]
         L.accord_waiting_on_initialise.argtypes = [C.c_void_p]
@@ -419,6 +423,19 @@ class PartialDeps:
                 self.rd_vals[self.rd_val_off[i]:self.rd_val_off[i + 1]],
                 self.rd_r2v[self.rd_r2v_off[i]:self.rd_r2v_off[i + 1]])
 
+    def txns(self, a: int, b: int) -> "PartialDeps":
+        """The deps of txns [a, b) as a set of their own (offset arrays rebased)."""
+        kw = {}
+        for off, datas in (("kd_key_off", ("kd_keys",)), ("kd_val_off", ("kd_vals",)), ("kd_k2v_off", ("kd_k2v",)),
+                           ("rd_rng_off", ("rd_rng_start", "rd_rng_end")), ("rd_val_off", ("rd_vals",)),
+                           ("rd_r2v_off", ("rd_r2v",))):
+            o = getattr(self, off)
+            lo, hi = int(o[a]), int(o[b])
+            kw[off] = (o[a:b + 1].astype(np.int64) - lo).astype(np.uint32)
+            for dname in datas:
+                kw[dname] = getattr(self, dname)[lo:hi].copy()
+        return PartialDeps(**kw)
+
     def totals(self):
         return dict(keys=int(self.kd_key_off[-1]), vals=int(self.kd_val_off[-1]), k2v=int(self.kd_k2v_off[-1]),
                     body=int(self.kd_k2v_off[-1] - self.kd_key_off[-1]), rd_vals=int(self.rd_val_off[-1]))
@@ -529,6 +546,9 @@ class Timing:
     pairs: int
     hist_entries: int
     compact_ms: float = 0.0
+    count_detail: dict = dataclasses.field(default_factory=dict)   # count stage by kernel (ms)
+    scan_spins: int = 0          # look-back spin iterations of the compute's scans
+    scan_fallbacks: int = 0      # look-backs that summed their inputs instead of waiting
 
 
 class CommandStore:
@@ -719,6 +739,18 @@ class CommandStore:
     def exchange_merge(self, n_total: int):
         self._check(lib().accord_deps_exchange_merge(self._h, n_total))
 
+    @staticmethod
+    def exchange_local(stores, n_total: int):
+        """accord_deps_exchange_merge for len(stores) simulated ranks on one device: stores[r] acts
+        as rank r (each holding its key block's partial of the stream), the plan and the union are
+        the RCCL path's, the transport is device copies.  Afterwards stores[r] holds the node-level
+        deps of its own txns [r*n_total/G, (r+1)*n_total/G)."""
+        arr = (C.c_void_p * len(stores))(*[st._h for st in stores])
+        rc = lib().accord_deps_exchange_local(arr, len(stores), n_total)
+        if rc != ACCORD_OK:
+            msgs = [lib().accord_last_error(st._h).decode() for st in stores]
+            _raise(rc, "; ".join(m for m in msgs if m) or lib().accord_last_error(None).decode())
+
     def shard_timing(self):
         a, b = C.c_float(), C.c_float()
         self._check(lib().accord_shard_timing(self._h, C.byref(a), C.byref(b)))
@@ -824,7 +856,10 @@ class CommandStore:
         t = _Timing()
         self._check(lib().accord_store_timing(self._h, C.byref(t)))
         return Timing(t.validate_ms, t.sort_ms, t.segment_ms, t.count_ms, t.scan_ms, t.fill_ms, t.range_ms,
-                      t.total_ms, t.pairs, t.hist_entries, t.compact_ms)
+                      t.total_ms, t.pairs, t.hist_entries, t.compact_ms,
+                      {"rk_checkpoints": t.count_rk_cp_ms, "rk_nkeys": t.count_rk_nkeys_ms,
+                       "kd_sizes": t.count_kd_sizes_ms, "rk_count": t.count_rk_ms, "rd_count": t.count_rd_ms},
+                      int(t.scan_spins), int(t.scan_fallbacks))
 
 
 # ---------------------------------------------------------------- string forms

@@ -44,6 +44,13 @@ void launch_fill_words(const FillList &L, hipStream_t s);
 // (DevBuf::ensure_zeroed) and used for nothing else, starting at the same address for every scan
 // that shares it (the store's scan_tmp); scans sharing it must run in stream order (it resets itself).
 size_t scan_temp_bytes(uint32_t n);
+// cumulative counters at the start of a scan-state buffer (since it was allocated): look-back spin
+// iterations, and look-backs that stopped waiting and summed the predecessors' inputs
+struct ScanCounters {
+    unsigned long long spins;
+    unsigned long long fallbacks;
+};
+inline const void *scan_counters(const void *temp) { return (const char *)temp + 16; }
 // out[i] = sum(in[0..i)), i in [0, n]; out has n+1 entries; total also written to *total_dev (u64).
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, unsigned long long *total_dev, void *temp,
                         hipStream_t s);
@@ -232,13 +239,23 @@ struct MergeParams {
     DevStatus *status;
 };
 void launch_merge_count(const MergeParams &p, hipStream_t s);
-// exp_off[a][t] = off[a][#subset txns with global position < t], t in [0, n_total]
-void launch_expand_offsets(uint32_t n, uint32_t n_total, const uint32_t *txn_index, uint32_t *ind, uint32_t *c,
-                           const uint32_t *const off[3], uint32_t *const exp_off[3], void *scan_tmp,
-                           unsigned long long *total, hipStream_t s);
-// bnd[a*(G+1) + d] = exp_off[a][d * n_total / G]
-void launch_boundaries(uint32_t G, uint32_t n_total, uint32_t *const exp_off[3], uint32_t *bnd, hipStream_t s);
 void launch_merge_fill(const MergeParams &p, hipStream_t s);
+// ---- exchange plan (merge.hip): the 6 CSR offset arrays of a partial (KeyDeps keys / txnIds /
+// keysToTxnIds, RangeDeps ranges / txnIds / rangesToTxnIds) ----
+constexpr int XCHG_NA = 6;
+struct XchgOffsets {
+    uint32_t *p[XCHG_NA];
+};
+// c[t] = #subset txns with global position < t (t in [0, n_total]) of a store holding a subset of
+// the stream (txn_index); ind is scratch of n_total + 1 words
+void launch_expand_index(uint32_t n, uint32_t n_total, const uint32_t *txn_index, uint32_t *ind, uint32_t *c,
+                         void *scan_tmp, unsigned long long *total, hipStream_t s);
+// out.p[a][t] = in.p[a][c[t]], t in [0, n_total]
+void launch_expand_offsets(uint32_t n_total, const uint32_t *c, const XchgOffsets &in, const XchgOffsets &out,
+                           hipStream_t s);
+// counts[2*XCHG_NA*d + a] / [.. + XCHG_NA + a] = element count / first element of offset array a
+// for destination d (txns [d*n_total/G, (d+1)*n_total/G)); counts[2*XCHG_NA*G] = 0 (status)
+void launch_xchg_counts(uint32_t G, uint32_t n_total, const XchgOffsets &e, unsigned long long *counts, hipStream_t s);
 
 // ---- SearchableRangeList stabbing of RangeDeps (rangeindex.hip) ----
 constexpr uint32_t RI_C = 16;                  // ranges per checkpoint block

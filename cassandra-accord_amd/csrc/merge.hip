@@ -199,47 +199,55 @@ __global__ void scatter_ones_kernel(uint32_t n, const uint32_t *__restrict__ idx
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ind[idx[i]] = 1u;
 }
 
-__global__ void expand_offsets_kernel(uint32_t n_total, const uint32_t *__restrict__ c, const uint32_t *__restrict__ a0,
-                                      const uint32_t *__restrict__ a1, const uint32_t *__restrict__ a2,
-                                      uint32_t *__restrict__ e0, uint32_t *__restrict__ e1, uint32_t *__restrict__ e2)
+__global__ void expand_offsets_kernel(uint32_t n_total, const uint32_t *__restrict__ c, XchgOffsets in, XchgOffsets out)
 {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t <= n_total; t += gridDim.x * blockDim.x) {
         const uint32_t q = c[t];
-        e0[t] = a0[q]; e1[t] = a1[q]; e2[t] = a2[q];
+#pragma unroll
+        for (int a = 0; a < XCHG_NA; ++a) out.p[a][t] = in.p[a][q];
     }
 }
 
-__global__ void boundaries_kernel(uint32_t G, uint32_t n_total, const uint32_t *__restrict__ e0,
-                                  const uint32_t *__restrict__ e1, const uint32_t *__restrict__ e2,
-                                  uint32_t *__restrict__ bnd)
+// Per destination rank d (its txns [d*n_total/G, (d+1)*n_total/G)) and offset array a: the element
+// count and first element of what this rank sends, read off the (expanded) offset arrays, plus a
+// status word (0 = this rank goes ahead).
+__global__ void xchg_counts_kernel(uint32_t G, uint32_t n_total, XchgOffsets e, unsigned long long *__restrict__ counts)
 {
-    const uint32_t d = threadIdx.x;
-    if (d <= G) {
-        const uint32_t t = (uint32_t)(((unsigned long long)d * n_total) / G);
-        bnd[d] = e0[t]; bnd[(G + 1) + d] = e1[t]; bnd[2 * (G + 1) + d] = e2[t];
+    constexpr uint32_t W = 2 * XCHG_NA;
+    for (uint32_t x = threadIdx.x; x < G * XCHG_NA; x += blockDim.x) {
+        const uint32_t d = x / XCHG_NA, a = x % XCHG_NA;
+        const uint32_t t0 = (uint32_t)(((unsigned long long)d * n_total) / G);
+        const uint32_t t1 = (uint32_t)(((unsigned long long)(d + 1) * n_total) / G);
+        const uint32_t b0 = e.p[a][t0], b1 = e.p[a][t1];
+        counts[W * d + a] = b1 - b0;
+        counts[W * d + XCHG_NA + a] = b0;
     }
+    if (threadIdx.x == 0) counts[W * G] = 0ull;
 }
 
 } // namespace
 
-void launch_expand_offsets(uint32_t n, uint32_t n_total, const uint32_t *txn_index, uint32_t *ind, uint32_t *c,
-                           const uint32_t *const off[3], uint32_t *const exp_off[3], void *scan_tmp,
-                           unsigned long long *total, hipStream_t s)
+void launch_expand_index(uint32_t n, uint32_t n_total, const uint32_t *txn_index, uint32_t *ind, uint32_t *c,
+                         void *scan_tmp, unsigned long long *total, hipStream_t s)
 {
     (void)hipMemsetAsync(ind, 0, (size_t)n_total * 4 + 4, s);
     uint32_t blocks = (n + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     if (n) hipLaunchKernelGGL(scatter_ones_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, s, n, txn_index, ind);
     exclusive_scan_u32(ind, c, n_total, total, scan_tmp, s);
-    uint32_t b2 = (n_total + 256) / 256;
-    if (b2 > 4096) b2 = 4096;
-    hipLaunchKernelGGL(expand_offsets_kernel, dim3(b2), dim3(256), 0, s, n_total, c, off[0], off[1], off[2],
-                       exp_off[0], exp_off[1], exp_off[2]);
 }
 
-void launch_boundaries(uint32_t G, uint32_t n_total, uint32_t *const exp_off[3], uint32_t *bnd, hipStream_t s)
+void launch_expand_offsets(uint32_t n_total, const uint32_t *c, const XchgOffsets &in, const XchgOffsets &out,
+                           hipStream_t s)
 {
-    hipLaunchKernelGGL(boundaries_kernel, dim3(1), dim3(128), 0, s, G, n_total, exp_off[0], exp_off[1], exp_off[2], bnd);
+    uint32_t b2 = (n_total + 256) / 256;
+    if (b2 > 4096) b2 = 4096;
+    hipLaunchKernelGGL(expand_offsets_kernel, dim3(b2), dim3(256), 0, s, n_total, c, in, out);
+}
+
+void launch_xchg_counts(uint32_t G, uint32_t n_total, const XchgOffsets &e, unsigned long long *counts, hipStream_t s)
+{
+    hipLaunchKernelGGL(xchg_counts_kernel, dim3(1), dim3(256), 0, s, G, n_total, e, counts);
 }
 
 void launch_merge_count(const MergeParams &p, hipStream_t s)

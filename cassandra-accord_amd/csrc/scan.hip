@@ -9,12 +9,18 @@
 //     block writes its tile of offsets;
 //   * a status word is one 8-byte agent-scope atomic (flag | epoch | value), so no payload has to be
 //     ordered behind it (MI355X_MICROARCH.md, inter-workgroup visibility: the 8-B granule);
-//   * the state buffer is self-resetting: it must be zero when allocated (DevBuf::ensure_zeroed),
-//     the epoch in its header tells this launch's statuses from stale ones, and the block that
-//     draws the last tile id -- every other block has drawn its id and published by the time its
-//     look-back completes -- rewinds the counter and advances the epoch for the next launch;
+//   * the state buffer is self-resetting: it must be zero when allocated (DevBuf::ensure_zeroed).
+//     The tile counter and the epoch share one 64-bit word, so a block draws its id and learns the
+//     launch's epoch in one atomic; the block that draws the last id (every other block has drawn
+//     one already) rewinds the counter and advances the epoch for the next launch.  Status words
+//     of an older epoch read as unpublished.  30-bit epochs: the store re-zeroes the buffer long
+//     before they wrap (accord_deps_compute);
+//   * values are 32 bits: a prefix that reaches 2^32 is published with the overflow flag, which
+//     propagates, and the total reports >= 2^32 (every caller checks its totals);
 //   * a look-back that spins for too long falls back to summing the predecessors' inputs itself,
-//     so termination does not depend on dispatch order.
+//     so termination does not depend on dispatch order;
+//   * counters after the header (ScanCounters) accumulate the look-back spins and fallbacks of
+//     every launch, for the store's profile.
 // Totals are carried in u64 so an overflow of the u32 offset space is detectable on the host.
 #include "device_common.h"
 #include "kernels.h"
@@ -27,19 +33,20 @@ constexpr int SC_ITEMS = 16;
 constexpr uint32_t SC_TILE = SC_THREADS * SC_ITEMS;
 constexpr int SC_MAX_ARRAYS = 4;
 
-// status word: flag (2 bits: 0 none, 1 aggregate, 2 inclusive prefix) | epoch (22 bits) | value (40)
-constexpr uint64_t ST_VALUE_MASK = (1ull << 40) - 1;
-constexpr uint32_t ST_EPOCH_MASK = (1u << 22) - 1;
-__device__ __forceinline__ uint64_t st_make(uint32_t flag, uint32_t epoch, uint64_t v)
+// status word: flag (2 bits: 0 none, 1 aggregate, 2 inclusive prefix, 3 inclusive prefix that
+// reached 2^32) | epoch (30 bits) | value (32 bits)
+constexpr uint32_t ST_EPOCH_MASK = (1u << 30) - 1;
+__device__ __forceinline__ uint64_t st_make(uint32_t flag, uint32_t epoch, uint32_t v)
 {
-    return ((uint64_t)flag << 62) | ((uint64_t)(epoch & ST_EPOCH_MASK) << 40) | (v & ST_VALUE_MASK);
+    return ((uint64_t)flag << 62) | ((uint64_t)(epoch & ST_EPOCH_MASK) << 32) | v;
 }
 
 struct ScanHeader {
-    uint32_t counter;    // next tile id (0 between launches)
-    uint32_t epoch;      // epoch of the previous launch
-    uint32_t pad[2];
+    unsigned long long ctl;      // next tile id (low 32 bits, 0 between launches) | epoch of the previous launch
+    unsigned long long pad;
+    ScanCounters counters;       // at scan_counters(temp)
 };
+static_assert(sizeof(ScanHeader) == 32, "scan header");
 
 struct ScanArgs {
     const uint32_t *in[SC_MAX_ARRAYS];
@@ -56,6 +63,8 @@ __device__ __forceinline__ void st_status(uint64_t *p, uint64_t v)
     (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+constexpr uint64_t OVF = 1ull << 32;
+
 template <int NA>
 __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_t n, uint32_t tiles,
                                                              ScanHeader *__restrict__ hdr, uint64_t *__restrict__ status)
@@ -66,8 +75,9 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
     __shared__ uint32_t tile[NA][SC_TILE];
     const uint32_t tid = threadIdx.x, w = wave_id(), lane = lane_id();
     if (tid == 0) {
-        s_id = atomicAdd(&hdr->counter, 1u);
-        s_epoch = (__hip_atomic_load(&hdr->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & ST_EPOCH_MASK;
+        const unsigned long long old = atomicAdd(&hdr->ctl, 1ull);
+        s_id = (uint32_t)old;
+        s_epoch = ((uint32_t)(old >> 32) + 1u) & ST_EPOCH_MASK;
     }
     __syncthreads();
     const uint32_t b = s_id, e = s_epoch;
@@ -120,38 +130,45 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
         if (b == 0) {
 #pragma unroll
             for (int k = 0; k < NA; ++k)
-                if (lane == 0) st_status(&status[(size_t)k * tiles + 0], st_make(2, e, agg[k]));
+                if (lane == 0) st_status(&status[(size_t)k * tiles + 0], st_make(agg[k] >= OVF ? 3 : 2, e, (uint32_t)agg[k]));
         } else {
+            // an aggregate that alone reaches 2^32 makes every later prefix overflow: publish it as such
 #pragma unroll
             for (int k = 0; k < NA; ++k)
-                if (lane == 0) st_status(&status[(size_t)k * tiles + b], st_make(1, e, agg[k]));
+                if (lane == 0) st_status(&status[(size_t)k * tiles + b], st_make(agg[k] >= OVF ? 3 : 1, e, (uint32_t)agg[k]));
             int32_t j = (int32_t)b - 1;       // walk back from here
-            uint32_t spins = 0;
+            uint32_t spins = 0, spins_all = 0;
             bool done = false;
             while (!done) {
                 const int32_t t = j - (int32_t)lane;
                 // a tile counts once all its arrays carry the same flag of this epoch (an
-                // aggregate, or the inclusive prefix); tiles before 0 are an empty prefix
-                uint32_t fmin = 2, fmax = 2;
+                // aggregate, or an inclusive prefix, overflowed or not); tiles before 0 are an
+                // empty prefix
+                uint32_t gmin = 2, gmax = 2;
                 uint64_t val[NA];
+                bool ovf[NA];
 #pragma unroll
                 for (int k = 0; k < NA; ++k) {
                     val[k] = 0;
+                    ovf[k] = false;
                     if (t >= 0) {
                         const uint64_t sw = ld_status(&status[(size_t)k * tiles + t]);
-                        const bool cur = (uint32_t)((sw >> 40) & ST_EPOCH_MASK) == e;
+                        const bool cur = (uint32_t)((sw >> 32) & ST_EPOCH_MASK) == e;
                         const uint32_t f = cur ? (uint32_t)(sw >> 62) : 0u;
-                        fmin = min(fmin, f);
-                        fmax = k == 0 ? f : max(fmax, f);
-                        val[k] = sw & ST_VALUE_MASK;
+                        const uint32_t g = f > 2 ? 2u : f;
+                        gmin = min(gmin, g);
+                        gmax = k == 0 ? g : max(gmax, g);
+                        val[k] = (uint32_t)sw;
+                        ovf[k] = f == 3;
                     }
                 }
-                const uint32_t flag = fmin == fmax ? fmin : 0u;
+                const uint32_t flag = gmin == gmax ? gmin : 0u;
                 const uint64_t pm = __ballot(flag == 2);          // lanes holding an inclusive prefix
                 const uint64_t nm = __ballot(flag == 0);          // lanes not published yet
                 const uint32_t first_p = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
                 const uint64_t below = first_p >= 64 ? ~0ull : ((1ull << first_p) - 1);
                 if (nm & below) {                                  // a predecessor is still working
+                    ++spins_all;
                     if (++spins > (1u << 20)) break;               // defensive: fall back below
                     __builtin_amdgcn_s_sleep(1);
                     continue;
@@ -159,7 +176,9 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
                 spins = 0;
 #pragma unroll
                 for (int k = 0; k < NA; ++k) {
-                    uint64_t v = lane <= first_p ? val[k] : 0ull;
+                    const bool mine = lane <= first_p;
+                    uint64_t v = mine ? val[k] : 0ull;
+                    if (__any(mine && ovf[k])) v = lane == 0 ? OVF : 0ull;   // the prefix reached 2^32
 #pragma unroll
                     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
                     excl[k] += v;
@@ -178,8 +197,14 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
                 }
             }
 #pragma unroll
-            for (int k = 0; k < NA; ++k)
-                if (lane == 0) st_status(&status[(size_t)k * tiles + b], st_make(2, e, excl[k] + agg[k]));
+            for (int k = 0; k < NA; ++k) {
+                const uint64_t inc = excl[k] + agg[k];
+                if (lane == 0) st_status(&status[(size_t)k * tiles + b], st_make(inc >= OVF ? 3 : 2, e, (uint32_t)inc));
+            }
+            if (lane == 0 && (spins_all || !done)) {
+                if (spins_all) atomicAdd(&hdr->counters.spins, (unsigned long long)spins_all);
+                if (!done) atomicAdd(&hdr->counters.fallbacks, 1ull);
+            }
         }
         if (lane == 0) {
 #pragma unroll
@@ -213,9 +238,8 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
             a.out[k][n] = (uint32_t)tot;
             if (a.total[k]) *a.total[k] = tot;
         }
-        // every block has drawn its id and published: rewind for the next launch
-        hdr->counter = 0u;
-        __hip_atomic_store(&hdr->epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // every block has drawn its id (this one drew the last): rewind for the next launch
+        __hip_atomic_store(&hdr->ctl, (unsigned long long)e << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 __global__ __launch_bounds__(256) void fill_words_kernel(FillList L)

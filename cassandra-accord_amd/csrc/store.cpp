@@ -172,7 +172,7 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     if (s->rk_keys_total >= (1ull << 32))
         return fail(s, ACCORD_ERR_CAPACITY, "range txns cover %llu (txn, key) pairs, over 2^32",
                     (unsigned long long)s->rk_keys_total);
-    s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->mc_next = 0;
+    s->has_batch = false; s->computed = false; s->merged = false; s->m_pending = false; s->ds_cur = -1; s->mc_next = 0;
     s->b_registered = false;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
@@ -242,6 +242,7 @@ int32_t accord_deps_compute(accord_store *s)
     hipStream_t st = s->stream;
     s->computed = false;
     s->merged = false;
+    s->m_pending = false;
     s->ds_cur = -1;
     s->wo_done = false;
 
@@ -284,6 +285,12 @@ int32_t accord_deps_compute(accord_store *s)
     // the store's scan state, shared by every scan of the pipeline (radix digit offsets, CSR offsets,
     // carry compaction): sized for the longest
     HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max({n, PH, accord::radix_sort_scan_len(PH)})), s->stream));
+    // the scan state's 30-bit epochs advance once per scan (a few dozen per compute): re-zeroed long
+    // before they could wrap onto a status word still in the buffer
+    if (++s->computes_since_zero >= (1u << 22)) {
+        HIPCHECK(s, hipMemsetAsync(s->scan_tmp.p, 0, s->scan_tmp.cap, st));
+        s->computes_since_zero = 0;
+    }
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     HIPCHECK(s, s->rng_owner.ensure((size_t)R * 4));
     HIPCHECK(s, s->is_range.ensure((size_t)n * 4 + 4));
@@ -425,20 +432,24 @@ int32_t accord_deps_compute(accord_store *s)
     rp.status = &dev->status;
 
     // sizes: key txns from the per-pair witnessed counts, range txns by their own count pass
+    if (nrt && !reg_ranges) accord::launch_rangekeys_checkpoints(PH, s->sort_key.as<uint32_t>(), rp, st);
+    record(s, EV_C_RKCP);
     if (nrt && !reg_ranges) {
-        accord::launch_rangekeys_checkpoints(PH, s->sort_key.as<uint32_t>(), rp, st);
         accord::launch_rangekeys_nkeys(rp, s->rk_cnt.as<uint32_t>(), st);
         accord::exclusive_scan_u32(s->rk_cnt.as<uint32_t>(), s->rk_off.as<uint32_t>(), nrt, &dev->totals[6],
                                    s->scan_tmp.p, st);
     }
+    record(s, EV_C_RKN);
     accord::launch_keydeps_sizes(n, kp.key_off, kp.slice, rp.cnt_keys, s->cnt_vub.as<uint32_t>(),
                                  rp.cnt_k2v, &dev->status, st);
+    record(s, EV_C_KDS);
     if (reg_ranges) {
         int32_t rc = accord_impl::status_range_keys(s, rp, false);
         if (rc) return rc;
     } else if (nrt) {
         accord::launch_rangekeys_count(rp, st);
     }
+    record(s, EV_C_RK);
     if (rdeps) {
         rp.rd_big_count = s->rd_big.as<uint32_t>();
         rp.rd_big_list = rp.rd_big_count + 16;
@@ -551,6 +562,9 @@ int32_t accord_deps_compute(accord_store *s)
     }
     record(s, EV_COMPACT);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
+    if (s->events)
+        HIPCHECK(s, hipMemcpyAsync(&s->pinned->scan, accord::scan_counters(s->scan_tmp.p), sizeof(accord::ScanCounters),
+                                   hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
     {
@@ -596,6 +610,17 @@ int32_t accord_deps_compute(accord_store *s)
         s->timing.range_ms = el(EV_FILL, EV_RANGE);
         s->timing.compact_ms = el(EV_RANGE, EV_COMPACT);
         s->timing.total_ms = el(EV_START, EV_COMPACT);
+        s->timing.count_rk_cp_ms = el(EV_SEGMENT, EV_C_RKCP);
+        s->timing.count_rk_nkeys_ms = el(EV_C_RKCP, EV_C_RKN);
+        s->timing.count_kd_sizes_ms = el(EV_C_RKN, EV_C_KDS);
+        s->timing.count_rk_ms = el(EV_C_KDS, EV_C_RK);
+        s->timing.count_rd_ms = el(EV_C_RK, EV_COUNT);
+        // the store's scan counters are cumulative since the state was (re)zeroed
+        const accord::ScanCounters now = s->pinned->scan;
+        const bool fresh = now.spins < s->scan_seen.spins || now.fallbacks < s->scan_seen.fallbacks;
+        s->timing.scan_spins = fresh ? now.spins : now.spins - s->scan_seen.spins;
+        s->timing.scan_fallbacks = fresh ? now.fallbacks : now.fallbacks - s->scan_seen.fallbacks;
+        s->scan_seen = now;
     }
     s->timing.pairs = P;
     s->timing.hist_entries = PH;
@@ -618,9 +643,17 @@ int32_t accord_store_reset(accord_store *s)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     s->next_global = 0; s->carry_n = 0; s->rc_n = 0; s->hist_kinds = 0; s->has_prev = false;
-    s->rg_tx_n = 0; s->rg_known = 0;
+    s->rg_tx_n = 0; s->rg_known = 0; s->rg_flag_ok = false;
     s->prev_msb = s->prev_lsb = 0; s->prev_node = 0;
-    s->has_batch = false; s->computed = false; s->merged = false; s->ds_cur = -1; s->wo_done = false;
+    s->has_batch = false; s->b_registered = false; s->computed = false; s->merged = false; s->m_pending = false;
+    s->ds_cur = -1; s->wo_done = false; s->mc_next = 0;
+    // RedundantBefore.EMPTY (its bounds are positions of the old stream) and MaxConflicts.EMPTY
+    s->rb_m = 0; s->rb_min_epoch = 0;
+    if (s->mc_state.p) {
+        HIPCHECK(s, hipSetDevice(s->cfg.device));
+        HIPCHECK(s, hipMemsetAsync(s->mc_state.p, 0, s->mc_state.cap, s->stream));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+    }
     return ACCORD_OK;
 }
 
@@ -650,6 +683,10 @@ int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
         return ACCORD_OK;
     }
     if (s->merged) {
+        if (s->m_pending) {
+            const int32_t rc = accord_impl::merge_finalize(s);
+            if (rc) return rc;
+        }
         d->n = s->m_n;
         d->kd_keys_total = s->m_tot_keys; d->kd_vals_total = s->m_tot_vals; d->kd_k2v_total = s->m_tot_k2v;
         d->kd_key_off = s->m_key_off.as<uint32_t>(); d->kd_keys = s->m_keys.as<uint32_t>();

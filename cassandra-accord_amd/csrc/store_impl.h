@@ -42,6 +42,7 @@ struct HostTotals {
     accord::DevStatus status;
     unsigned long long totals[10];  // kd keys, kd vals bound, kd k2v, rd ranges, rd vals, rd r2v, range txns,
                                     // kd vals, resident carry entries, spare
+    accord::ScanCounters scan;      // the store's scan-state counters (profiled stores read them)
 };
 
 // A device-resident PartialDeps set (result of accord_deps_union / accord_deps_slice).
@@ -64,7 +65,7 @@ using accord_impl::HostTotals;
 
 enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_FILL, EV_RANGE, EV_COMPACT,
              EV_XCHG_START, EV_XCHG_END, EV_MERGE_END, EV_WO_START, EV_WO_BITS, EV_WO_PREDS, EV_WO_LEVEL,
-             EV_OP_START, EV_OP_END, EV_COUNT_ALL };
+             EV_OP_START, EV_OP_END, EV_C_RKCP, EV_C_RKN, EV_C_KDS, EV_C_RK, EV_COUNT_ALL };
 
 struct ShardComm;   // RCCL communicator + exchange buffers (shard.cpp)
 namespace accord_impl { struct PinnedBlock; void pinned_arena_destroy(accord_store *s); }
@@ -127,6 +128,7 @@ struct accord_store {
     uint32_t m_n = 0, m_txn_lo = 0;
     DevBuf m_key_off, m_val_off, m_k2v_off, m_keys, m_vals, m_k2v, m_cnt_keys, m_cnt_vals, m_cnt_k2v, m_ptrs, m_zero;
     uint64_t m_tot_keys = 0, m_tot_vals = 0, m_tot_k2v = 0;
+    bool m_pending = false;        // merged totals / error word in flight to `pinned` (merge_finalize)
     float xchg_ms = 0, merge_ms = 0;
     // WaitingOn + levelling (waiting_on_abi.cpp)
     bool wo_done = false;
@@ -156,6 +158,8 @@ struct accord_store {
     hipEvent_t ev[EV_COUNT_ALL] = {};
     bool events = false;
     accord_timing timing{};
+    accord::ScanCounters scan_seen{};   // scan counters at the end of the previous profiled compute
+    uint32_t computes_since_zero = 0;   // computes since the scan state was last zeroed
     int wpl = 1;
 };
 
@@ -163,6 +167,7 @@ struct accord_store {
 namespace accord_impl {
 int32_t fail(accord_store *s, int32_t code, const char *fmt, ...);
 void shard_comm_destroy(accord_store *s);
+int32_t merge_finalize(accord_store *s);   // read a bounded merge's totals (shard.cpp)
 // registered statuses (status.hip)
 bool registered_mode(const accord_store *s);
 int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill);

@@ -119,6 +119,12 @@ typedef struct {
     float validate_ms, sort_ms, segment_ms, count_ms, scan_ms, fill_ms, range_ms, total_ms;
     float compact_ms, reserved_ms;   /* txnIds compaction (gapped -> dense CSR) */
     uint64_t pairs, hist_entries;
+    /* the count stage by kernel: range txns' key checkpoints, their key counts (+ offsets scan),
+     * key txns' sizes, range txns' KeyDeps counts, RangeDeps counts */
+    float count_rk_cp_ms, count_rk_nkeys_ms, count_kd_sizes_ms, count_rk_ms, count_rd_ms, reserved2_ms;
+    /* every decoupled look-back scan of the compute: spin iterations spent waiting on a predecessor
+     * tile's status, and look-backs that gave up waiting and summed the inputs themselves */
+    uint64_t scan_spins, scan_fallbacks;
 } accord_timing;
 
 /* ---- store lifecycle (CommandStore; impl/InMemoryCommandStore.java:89) ---- */
@@ -241,10 +247,19 @@ int32_t accord_deps_merge(accord_store *store, uint32_t nparts, const accord_dep
  * the txn (txn g -> rank floor(g*G/n_total)) with one grouped RCCL send/recv and unions the G parts
  * there; afterwards the store's current deps are the full (node-level) deps of its own txns.  Both
  * KeyDeps and RangeDeps travel (6 offset + 7 data arrays per destination); when any received part
- * holds RangeDeps the owner unions with accord_deps_union, else with the key-disjoint merge. */
+ * holds RangeDeps the owner unions with accord_deps_union, else with the key-disjoint merge.
+ * The exchange is plan (device offsets + one all-gather of the G x G count table, the only host
+ * read) -> transport -> union (sized by the received counts; its totals are read, and a merge
+ * error reported, when the result is first used: accord_deps_device_view / _download).
+ *
+ * accord_deps_exchange_local: the same plan and union for G stores of ONE device acting as ranks
+ * 0..G-1 (stores[r] = rank r, no communicator), with the transport replaced by device copies of the
+ * identical segment lists -- the multi-rank exchange exercised on one GPU (tests, rank simulation).
+ * Each store afterwards holds the node-level deps of its own txns, as after accord_deps_exchange_merge. */
 int32_t accord_comm_unique_id(void *id128);                  /* ncclGetUniqueId, 128 bytes */
 int32_t accord_comm_init(accord_store *store, int32_t nranks, int32_t rank, const void *id128);
 int32_t accord_deps_exchange_merge(accord_store *store, uint32_t n_total);
+int32_t accord_deps_exchange_local(accord_store *const *stores, uint32_t nranks, uint32_t n_total);
 int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merge_ms);
 
 /* ---- deps-set operations on device ----

@@ -173,3 +173,25 @@ def test_gpu_redundant_before_accept_epochs(gpu_device):
         st.redundant_before(es, ee, sep, eep, bound, min_epoch=0)
         got = st.calculate_deps_batch(s)
     assert got.first_difference(want) is None
+
+
+@pytest.mark.gpu
+def test_gpu_reset_clears_redundant_before_and_max_conflicts(gpu_device):
+    # accord_store_reset = an empty CommandStore: RedundantBefore.EMPTY and MaxConflicts.EMPTY too
+    rng = np.random.default_rng(41)
+    s = with_epochs(generate_stream(2000, 4, 500, 0.99, 0.5, seed=41), rng)
+    es, ee, sep, eep, bound = random_map(rng, 500, 40, s.n)
+    with CommandStore(device=0, key_lo=0, key_hi=500, window=64) as st, \
+            CommandStore(device=0, key_lo=0, key_hi=500, window=64) as fresh:
+        st.redundant_before(es, ee, sep, eep, bound, min_epoch=1)
+        st.calculate_deps_batch(s)
+        st.max_conflicts_fold(s)
+        st.reset()
+        got = st.calculate_deps_batch(s)
+        assert got.first_difference(fresh.calculate_deps_batch(s)) is None
+        assert got.first_difference(O.deps_fast(s, 64)) is None
+        a = st.max_conflicts_fold(s)
+        b = fresh.max_conflicts_fold(s)
+        for x, y in zip(a[:5], b[:5]):
+            assert np.array_equal(x, y)
+        assert a[5] == b[5]
