@@ -59,11 +59,12 @@ void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *ou
                           uint32_t n, void *temp, hipStream_t s);
 
 // ---- key deps pipeline (keydeps.hip) ----
-// Per (txn, key) pair, txn-major: the deps slice [lo, pos) of the key's history and the number of
-// its entries the txn's kind witnesses.  One 16-byte record so the key-major -> txn-major scatter
-// is a single store per pair.
+// Per (txn, key) pair, txn-major: the deps slice [lo, pos) of the key's history, the number of
+// its entries the txn's kind witnesses, and the pair's store-relative key ordinal.  One 16-byte
+// record so the key-major -> txn-major scatter is a single store per pair (and the fill reads the
+// key with the slice).
 struct alignas(16) PairSlice {
-    uint32_t lo, pos, wcnt, pad;
+    uint32_t lo, pos, wcnt, key;
 };
 
 struct KeyDepsParams {

@@ -406,7 +406,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
-        if (p < end && q[j] != 0xFFFFFFFFu) slice[q[j]] = PairSlice{l[j], hi[j], cnt[j], 0u};
+        if (p < end && q[j] != 0xFFFFFFFFu) slice[q[j]] = PairSlice{l[j], hi[j], cnt[j], key[j]};
     }
 }
 
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
             cnt = witnessed_upto(c_local, ccarry, hi[j] - 1, wmask) - (l ? witnessed_upto(c_local, ccarry, l - 1, wmask) : 0u);
             if (hi[j] > p) cnt -= (wmask >> kind) & 1u;   // p1: the txn itself
         }
-        if (p < end && q[j] != 0xFFFFFFFFu) slice[q[j]] = PairSlice{l, hi[j], cnt, 0u};
+        if (p < end && q[j] != 0xFFFFFFFFu) slice[q[j]] = PairSlice{l, hi[j], cnt, key[j]};
     }
 }
 
@@ -934,7 +934,7 @@ __device__ __forceinline__ void fk_slices(const KeyDepsParams &p, FkTxn &x, uint
     if (k <= 8 && lane < k) {
         const PairSlice ps = ldg(p.slice, k0 + lane);
         x.lo = ps.lo; x.pos = ps.pos; x.wc = ps.wcnt;
-        x.key = ldg(p.key_ord, k0 + lane);
+        x.key = ps.key + p.key_lo;                    // the slice carries its (store-relative) key
     }
 }
 
@@ -969,35 +969,69 @@ __device__ __forceinline__ uint32_t fk_cands(const KeyDepsParams &p, const FkTxn
     return rt;
 }
 
-struct alignas(16) BmWord {
-    unsigned long long bits;          // 64 bits of the near bitmap
-    uint32_t pre;                     // distinct deps before this word (far deps included)
-    uint32_t pad;
-};
+// Near map: one byte per txn of the near span [bound - SPAN, bound), set by plain byte stores
+// (measured, scripts/micro/lds_patterns.hip: lanes storing to one word cost nothing extra, while
+// same-word LDS atomics serialize -- 8 lanes on a word = 8x), then packed into bits: lane L owns
+// the BPL bytes [L*BPL, (L+1)*BPL) of the map, packs them into its bit word and zeroes them for the
+// next txn.  A candidate's rank comes from its word owner by one lane permute (no LDS traffic).
+// 4 map bytes (0 / 1 each) -> 4 bits, byte b at bit b: the bytes land on bits 24..27 of the product
+// (M = 2^24 + 2^17 + 2^10 + 2^3; the cross terms stay below bit 20 or above bit 31)
+__device__ __forceinline__ uint32_t pack4(uint32_t x) { return ((x & 0x01010101u) * 0x01020408u) >> 24; }
 
-// OR the near bits of one candidate batch into the bitmap (LDS atomics; measured: combining equal
-// words across lanes first costs more VALU than the same-address atomics it saves -- the kernel is
-// VALU-issue bound)
-__device__ __forceinline__ void near_bits_or(BmWord *bw, bool nr, uint32_t bit, uint32_t)
+template <int BPL>
+__device__ __forceinline__ uint32_t near_take(uint8_t *map, uint32_t lane)
 {
-    if (nr) atomicOr(&bw[bit >> 6].bits, 1ull << (bit & 63));
+    uint32_t bits = 0;
+#pragma unroll
+    for (int h = 0; h < BPL / 16; ++h) {
+        uint4 *q = (uint4 *)(map + lane * BPL + h * 16);
+        const uint4 v = *q;
+        *q = make_uint4(0u, 0u, 0u, 0u);               // cleared for the next txn (in-order LDS)
+        bits |= (pack4(v.x) | pack4(v.y) << 4 | pack4(v.z) << 8 | pack4(v.w) << 12) << (16 * h);
+    }
+    return bits;
 }
 
-template <int WPL>
+// Diagnostic build only (-DACCORD_FK_STAMPS, scripts/fk_stamps.py): s_memtime stamps at the
+// segment boundaries of the fast kernel's txn loop, summed per segment over every wave.  Read the
+// SHARES, not the run time: each stamp drains the wave's LDS traffic.
+#ifdef ACCORD_FK_STAMPS
+__device__ unsigned long long g_fk_stamps[16];
+#define FK_STAMP(seg)                                                                          \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        unsigned long long t_;                                                                 \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        fk_sum[seg] += t_ - fk_last;                                                           \
+        fk_last = t_;                                                                          \
+    } while (0)
+#else
+#define FK_STAMP(seg) do {} while (0)
+#endif
+
+template <int BPL>
 __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void keydeps_fast_kernel(
     KeyDepsParams p, const TxnRec *__restrict__ recs)
 {
-    __shared__ BmWord bw_all[KD_WAVES][64 * WPL];   // near bitmap words + rank prefix (one b128 read)
+    constexpr uint32_t SPAN = 64u * BPL;
+    __shared__ __attribute__((aligned(16))) uint8_t map_all[KD_WAVES][SPAN];   // near map (bytes)
     __shared__ uint32_t fr_all[KD_WAVES][64];       // far deps: value, then its rank
     const uint32_t w = wave_id(), lane = lane_id();
-    BmWord *bw = bw_all[w];
+    uint8_t *map = map_all[w];
     uint32_t *fr = fr_all[w];
     const uint64_t lt = lanemask_lt();
-    constexpr uint32_t SPAN = 64u * 64u * WPL;
-    const uint32_t S = gridDim.x * KD_WAVES, n = p.n;
+#pragma unroll
+    for (int h = 0; h < BPL / 16; ++h) *(uint4 *)(map + lane * BPL + h * 16) = make_uint4(0u, 0u, 0u, 0u);
+    // XCD-aware order: blocks b and b + 8 share an XCD (round-robin placement, MI355X_MICROARCH.md),
+    // so the 8 block classes take contiguous eighths of the batch and each XCD's waves sweep theirs
+    // in step: consecutive txns read the same hot keys' history slices, which then stay in that
+    // XCD's L2 instead of being fetched into all eight
+    const uint32_t xg = blockIdx.x & 7u, B = gridDim.x >> 3;
+    const uint32_t n = (uint32_t)(((uint64_t)p.n * (xg + 1)) >> 3), S = B * KD_WAVES;
+    uint32_t t = (uint32_t)(((uint64_t)p.n * xg) >> 3) + (blockIdx.x >> 3) * KD_WAVES + w;
 
     // software pipeline: records three txns ahead, slices two ahead, candidates one ahead
-    uint32_t t = blockIdx.x * KD_WAVES + w;
     FkTxn a, b, c;
     a.rec = fk_rec(recs, t, n, lane);
     b.rec = fk_rec(recs, t + S, n, lane);
@@ -1007,12 +1041,20 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     uint32_t ea[FK_CB];
     uint32_t rta = fk_cands(p, a, lane, ea);
 
+#ifdef ACCORD_FK_STAMPS
+    unsigned long long fk_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fk_last = 0, fk_n = 0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fk_last)::"memory");
+#endif
     for (; t < n; t += S) {
         FkTxn d;
         d.rec = fk_rec(recs, t + 3 * S, n, lane);
         fk_slices(p, c, lane);
         uint32_t eb[FK_CB];
         const uint32_t rtb = fk_cands(p, b, lane, eb);
+        FK_STAMP(0);                                  // prefetch issue (waits for c's record, b's slices)
+#ifdef ACCORD_FK_STAMPS
+        ++fk_n;
+#endif
 
         do {   // ---- txn t (break = done with it) ----
             const uint32_t k = readlane(a.rec, 1);
@@ -1024,13 +1066,10 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             bool fallback = k > 8 || rta > FK_RAW;
             const uint32_t kind = readlane(a.rec, 2), gi = readlane(a.rec, 3);
             const uint32_t wmask = witness_mask(kind);
-            const uint32_t nb = SPAN - readlane(a.rec, 7);   // near bit of txn j: j + nb (< SPAN iff near)
+            const uint32_t nb = SPAN - readlane(a.rec, 7);   // map byte of txn j: j + nb (< SPAN iff near)
             uint32_t F = 0;                           // far deps (older than the near span)
             uint32_t fidx[FK_CB];
             if (!fallback) {
-#pragma unroll
-                for (int q = 0; q < WPL; ++q) bw[lane * WPL + q].bits = 0ull;
-                wave_lds_sync();
 #pragma unroll
                 for (int cc = 0; cc < FK_CB; ++cc) {
                     fidx[cc] = 0;
@@ -1038,9 +1077,9 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                     const uint32_t ev = ea[cc];
                     const uint32_t j = ev & ENT_TXN_MASK;
                     const bool wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;   // p1
-                    const uint32_t bit = j + nb;
-                    const bool nr = wit && bit < SPAN;
-                    near_bits_or(bw, nr, bit, lane);
+                    const uint32_t off = j + nb;
+                    const bool nr = wit && off < SPAN;
+                    if (nr) map[off] = 1;
                     const uint64_t fb = __ballot(wit && !nr);
                     if (fb) {                             // wave-uniform
                         const uint32_t f = F + (uint32_t)__popcll(fb & lt);
@@ -1053,9 +1092,14 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             }
             if (fallback) {
                 if (lane == 0) p.fb_list[atomicAdd(p.fb_count, 1u)] = t;
+                if (rta <= FK_RAW && k <= 8) {        // its bytes went into the map: clear them
+                    wave_lds_sync();
+                    (void)near_take<BPL>(map, lane);
+                }
                 break;
             }
             wave_lds_sync();
+            FK_STAMP(1);                              // phase 1 (waits for this txn's candidates)
             // far deps: de-duplicated ranks (all of them precede the near span in TxnId order)
             uint32_t far_u = 0;
             if (F) {                                      // wave-uniform
@@ -1076,17 +1120,14 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 if (lane < F) fr[lane] = rk;
                 if ((om >> lane) & 1ull) stg(p.vgap, readlane(a.rec, 5) + rk, x);
             }
-            // union: popcounts -> per-word rank prefix (after the far deps); |txnIds|
-            uint32_t pc[WPL], mysum = 0;
-#pragma unroll
-            for (int q = 0; q < WPL; ++q) { pc[q] = (uint32_t)__popcll(bw[lane * WPL + q].bits); mysum += pc[q]; }
-            const uint32_t incl = wave_incl_scan(mysum);
-            {
-                uint32_t ex = incl - mysum + far_u;
-#pragma unroll
-                for (int q = 0; q < WPL; ++q) { bw[lane * WPL + q].pre = ex; ex += pc[q]; }
-            }
+            FK_STAMP(2);                              // far deps
+            // union: the lane's map bytes -> bit word, popcount prefix (after the far deps); |txnIds|
+            const uint32_t bits = near_take<BPL>(map, lane);
+            const uint32_t pc = (uint32_t)__popc(bits);
+            const uint32_t incl = wave_incl_scan(pc);
+            const uint32_t pre = incl - pc + far_u;
             if (lane == 0) stg(p.cnt_vals, t, readlane(incl, 63) + far_u);
+            FK_STAMP(3);                              // union
             // keys and keysToTxnIds header from the witnessed counts
             const uint32_t key_base = readlane(a.rec, 4), val_base = readlane(a.rec, 5), k2v_base = readlane(a.rec, 6);
             const bool ne = lane < k && a.wc != 0;
@@ -1098,7 +1139,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 stg(p.kd_keys, key_base + ns, a.key);
                 stg(p.kd_k2v, k2v_base + ns, (int32_t)(kc + wincl));
             }
-            wave_lds_sync();
+            if (F) wave_lds_sync();                      // far ranks in fr[]
+            FK_STAMP(4);                              // keys + header
             // body: rank of every witnessed entry; txnIds at their ranks
             uint32_t run = 0;
 #pragma unroll
@@ -1107,10 +1149,19 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 const uint32_t ev = ea[cc];
                 const uint32_t j = ev & ENT_TXN_MASK;
                 const bool wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;   // p1
-                const bool nr = wit && j + nb < SPAN;
-                const uint32_t bit = nr ? j + nb : 0u;
-                const BmWord bwd = bw[bit >> 6];
-                uint32_t rank = bwd.pre + (uint32_t)__popcll(bwd.bits & ((1ull << (bit & 63)) - 1ull));
+                const uint32_t off = j + nb;
+                const bool nr = wit && off < SPAN;
+                const uint32_t src = (nr ? off : 0u) / BPL;            // the word owner of the byte
+                const uint32_t ob = (nr ? off : 0u) % BPL;
+                uint32_t rank;
+                if (BPL == 16) {                           // 16 bits + a prefix below 2^16: one permute
+                    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(pre << 16 | bits));
+                    rank = (v >> 16) + (uint32_t)__popc(v & ((1u << ob) - 1u));
+                } else {
+                    const uint32_t wbits = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)bits);
+                    const uint32_t wpre = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)pre);
+                    rank = wpre + (uint32_t)__popc(wbits & ((1u << ob) - 1u));
+                }
                 if (F && wit && !nr) rank = fr[fidx[cc]];
                 const uint64_t wb = __ballot(wit);
                 if (wit) {
@@ -1119,6 +1170,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 }
                 run += (uint32_t)__popcll(wb);
             }
+            FK_STAMP(5);                              // phase 2 (body + txnIds stores)
         } while (0);
 
         // rotate the pipeline (after the txn: a register copy waits for the loads it copies)
@@ -1126,7 +1178,15 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         rta = rtb;
 #pragma unroll
         for (int cc = 0; cc < FK_CB; ++cc) ea[cc] = eb[cc];
+        FK_STAMP(6);                                  // rotation (+ skipped / fallback txns)
     }
+#ifdef ACCORD_FK_STAMPS
+    if (lane == 0) {
+        for (int q = 0; q < 7; ++q) atomicAdd(&g_fk_stamps[q], fk_sum[q]);
+        atomicAdd(&g_fk_stamps[7], fk_n);
+        atomicAdd(&g_fk_stamps[8], 1ull);
+    }
+#endif
 }
 
 
@@ -1380,10 +1440,14 @@ void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_
     hipLaunchKernelGGL(txnrec_kernel, dim3(rb), dim3(256), 0, s, p, (TxnRec *)recs);
     uint32_t blocks = (p.n + KD_WAVES - 1) / KD_WAVES;
     if (blocks > 256u * 16u) blocks = 256u * 16u;
-    switch (wpl) {
-    case 1: hipLaunchKernelGGL((keydeps_fast_kernel<1>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs); break;
-    case 2: hipLaunchKernelGGL((keydeps_fast_kernel<2>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs); break;
-    default: hipLaunchKernelGGL((keydeps_fast_kernel<4>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs); break;
+    blocks = (blocks + 7u) & ~7u;                       // a multiple of 8: one block class per XCD
+    (void)wpl;
+    // near span: 1024 txns below the bound for windows up to 384 (config 2: 94 % of the distinct
+    // deps, p99 16 far ones per txn), else 2048
+    if (p.window <= 384u) {
+        hipLaunchKernelGGL((keydeps_fast_kernel<16>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs);
+    } else {
+        hipLaunchKernelGGL((keydeps_fast_kernel<32>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs);
     }
 }
 
@@ -1637,3 +1701,12 @@ void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *va
 }
 
 } // namespace accord
+
+#ifdef ACCORD_FK_STAMPS
+extern "C" int accord_dbg_fk_stamps(unsigned long long *out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(accord::g_fk_stamps), 16 * 8) != hipSuccess) return -1;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(accord::g_fk_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

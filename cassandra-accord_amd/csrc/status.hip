@@ -124,7 +124,7 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q)
         if (FILL) p.hist2[out + c] = e;
         ++c;
     }
-    if (FILL) p.slice[q] = accord::PairSlice{out, out + c, c, 0u};
+    if (FILL) p.slice[q] = accord::PairSlice{out, out + c, c, sl.key};
     else p.gcnt[q] = c;
 }
 

@@ -9,7 +9,7 @@ for spec in "$@"; do
   obj=${obj:-keydeps}; src=${src:-csrc/$obj.hip}
   mkdir -p build/var_$name
   [ "$src" != csrc/$obj.hip ] && cp "$src" csrc/.var_$name.hip && src=csrc/.var_$name.hip
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function $flags -c $src -o build/var_$name/$obj.o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Wall -Wno-unused-function $flags -c $src -o build/var_$name/$obj.o &
 done
 wait
 rm -f csrc/.var_*.hip
