@@ -339,6 +339,7 @@ int32_t accord_redundant_before_set(accord_store *s, uint32_t m, const uint32_t 
     }
     s->rb_m = m;
     s->rb_min_epoch = min_epoch;
+    if (accord_impl::registered_mode(s)) RC(accord_impl::status_truncate_carry(s, m, start, end, bound));
     return ACCORD_OK;
 }
 

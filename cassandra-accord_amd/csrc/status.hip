@@ -84,9 +84,28 @@ struct GenParams {
     StatusView v;
 };
 
-// One pair: maxCommittedBefore, then count (FILL = false) or write (FILL = true) the emitted entries.
+// wave-wide max of a Timestamp (lanes without one hold has = false)
+__device__ __forceinline__ void wave_ts_max(Ts &m, bool &has)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const Ts o{(uint64_t)__shfl_xor((long long)m.msb, d, 64), (uint64_t)__shfl_xor((long long)m.lsb, d, 64),
+                   __shfl_xor(m.node, d, 64)};
+        const bool oh = __shfl_xor(has ? 1 : 0, d, 64) != 0;
+        if (oh && (!has || tcmp(o, m) > 0)) { m = o; has = true; }
+    }
+}
+
+// One pair, one wave (lanes stride over the pair's slice [lo, pos) of the key's history):
+//   maxCommittedBefore = max executeAt over committed Writes with executeAt < startedBefore (:620-624)
+//   emitted            = witnessed entries, not TRANSITIVELY_KNOWN / INVALID_OR_TRUNCATED, committed
+//                        ones only with executeAt >= maxCommittedBefore (:634-645); p1 excluded
+// Count pass: when the emitted entries are exactly the witnessed entries of [first emitted, pos) --
+// the common case once the carried history is pruned -- the pair's slice is narrowed to that range of
+// the history itself (the fill kernels filter by kind and drop the txn itself); otherwise its count
+// reserves an extension run that the fill pass writes.
 template <bool FILL>
-__device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q)
+__device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q, uint32_t lane)
 {
     const accord::PairSlice sl = p.slice[q];
     const uint64_t l = p.lsb[t];
@@ -99,11 +118,10 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q)
         sb = x;
     }
     const uint32_t self = p.txn_index[t];
-    // segment start: the slice of a W = infinity history starts at the key's first entry
     const uint32_t lo = sl.lo, hi = sl.pos;
     bool has_mcb = false;
     Ts mcb{0, 0, 0};
-    for (uint32_t x = lo; x < hi; ++x) {
+    for (uint32_t x = lo + lane; x < hi; x += 64) {
         const uint32_t e = p.hist[x], g = e & ENT_TXN_MASK;
         if ((e >> ENT_KIND_SHIFT) != 1u) continue;    // Writes only
         const uint32_t st = status_of(p.v, g);
@@ -112,40 +130,89 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q)
         if (tcmp(ex, sb) >= 0) continue;
         if (!has_mcb || tcmp(ex, mcb) > 0) { mcb = ex; has_mcb = true; }
     }
-    uint32_t c = 0;
-    const uint32_t out = FILL ? p.ext_base + p.goff[q] : 0u;
-    for (uint32_t x = lo; x < hi; ++x) {
-        const uint32_t e = p.hist[x], g = e & ENT_TXN_MASK;
-        if (!((wmask >> (e >> ENT_KIND_SHIFT)) & 1u)) continue;
-        if (p1 && g == self) continue;
+    wave_ts_max(mcb, has_mcb);
+    // what the fill kernels keep of a history entry (kind witnessed, not the txn itself)
+    auto witnessed = [&](uint32_t e) { return ((wmask >> (e >> ENT_KIND_SHIFT)) & 1u) && (e & ENT_TXN_MASK) != self; };
+    auto emitted = [&](uint32_t e) -> bool {
+        if (!((wmask >> (e >> ENT_KIND_SHIFT)) & 1u)) return false;
+        const uint32_t g = e & ENT_TXN_MASK;
+        if (p1 && g == self) return false;
         const uint32_t st = status_of(p.v, g);
-        if (st == ST_TK || st >= ST_INVALID) continue;
-        if (committed(st) && has_mcb && tcmp(exec_of(p.v, g), mcb) < 0) continue;
-        if (FILL) p.hist2[out + c] = e;
-        ++c;
+        if (st == ST_TK || st >= ST_INVALID) return false;
+        return !(committed(st) && has_mcb && tcmp(exec_of(p.v, g), mcb) < 0);
+    };
+    if (!FILL) {
+        // emitted count, first emitted position, last witnessed-but-not-emitted position
+        uint32_t c = 0, first = hi, last_rej = 0;
+        bool any_rej = false;
+        for (uint32_t x = lo + lane; x < hi; x += 64) {
+            const uint32_t e = p.hist[x];
+            if (emitted(e)) { ++c; first = min(first, x); }
+            else if (witnessed(e)) { any_rej = true; last_rej = max(last_rej, x); }
+        }
+        c = wave_sum(c);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, d, 64));
+        const bool rej = __any(any_rej && last_rej > first);      // first is wave-uniform here
+        if (lane == 0) {
+            if (!rej) {   // contiguous: the fill reads the history range itself
+                p.slice[q] = accord::PairSlice{c ? first : hi, hi, c, sl.key};
+                p.gcnt[q] = 0;
+            } else {
+                p.gcnt[q] = c;
+            }
+        }
+        return;
     }
-    if (FILL) p.slice[q] = accord::PairSlice{out, out + c, c, sl.key};
-    else p.gcnt[q] = c;
+    // fill (pairs with an extension run only): the emitted entries, in order
+    const uint64_t lt = lanemask_lt();
+    const uint32_t out = p.ext_base + p.goff[q];
+    uint32_t c = 0;
+    for (uint32_t x0 = lo; x0 < hi; x0 += 64) {
+        const uint32_t x = x0 + lane;
+        const bool em = x < hi && emitted(p.hist[x]);
+        const uint64_t b = __ballot(em);
+        if (em) p.hist2[out + c + (uint32_t)__popcll(b & lt)] = p.hist[x];
+        c += (uint32_t)__popcll(b);
+    }
+    if (lane == 0) p.slice[q] = accord::PairSlice{out, out + c, c, sl.key};
 }
 
+// A wave per txn over its keys that hold a registered status: the count pass narrows contiguous
+// pairs' slices itself and counts the others, the fill pass writes the counted ones.
 template <bool FILL>
 __global__ __launch_bounds__(256) void general_kernel(GenParams p)
 {
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < p.n; t += gridDim.x * blockDim.x)
+    const uint32_t lane = lane_id();
+    const uint32_t waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t t = blockIdx.x * (blockDim.x / 64) + wave_id(); t < p.n; t += waves)
         for (uint32_t q = p.key_off[t]; q < p.key_off[t + 1]; ++q) {
-            if (!p.flag[p.key_ord[q] - p.key_lo]) { if (!FILL) p.gcnt[q] = 0; continue; }
-            general_pair<FILL>(p, t, q);
+            if (!p.flag[p.key_ord[q] - p.key_lo]) { if (!FILL && lane == 0) p.gcnt[q] = 0; continue; }
+            if (FILL && p.gcnt[q] == 0) continue;          // contiguous pair: slice already set
+            general_pair<FILL>(p, t, q, lane);
         }
 }
 
 // carry flags of a registered-status store: an entry stays until its txn is INVALID_OR_TRUNCATED
-// (CommandsForKey drops truncated txns, local/CommandsForKey.java:1654-1684; every other entry can
-// still be emitted or bound maxCommittedBefore after later events)
+// (CommandsForKey skips those for good, local/CommandsForKey.java:436,643) or the store's
+// RedundantBefore truncates it (status_truncate_carry); every other entry can still be emitted, or
+// bound maxCommittedBefore, after later events
 __global__ __launch_bounds__(256) void prune_mark_kernel(uint32_t P, const uint32_t *__restrict__ hist, StatusView v,
                                                          uint32_t *__restrict__ keep_flag)
 {
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x)
         keep_flag[x] = status_of(v, hist[x] & ENT_TXN_MASK) < ST_INVALID ? 1u : 0u;
+}
+
+// CommandsForKey.withRedundantBefore (:1654-1684) on the carried history: entries below their key's
+// shardRedundantBefore leave
+__global__ __launch_bounds__(256) void truncate_mark_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
+                                                            const uint32_t *__restrict__ cent,
+                                                            const uint32_t *__restrict__ key_bound,
+                                                            uint32_t *__restrict__ keep_flag)
+{
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x)
+        keep_flag[c] = (cent[c] & ENT_TXN_MASK) >= key_bound[ckey[c]] ? 1u : 0u;
 }
 
 // ---- registration ----
@@ -471,7 +538,8 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     g.slice = s->slice.as<accord::PairSlice>();
     g.gcnt = s->rg_gcnt.as<uint32_t>(); g.goff = s->rg_goff.as<uint32_t>();
     g.v = v;
-    if (n) hipLaunchKernelGGL(general_kernel<false>, dim3(grid_for(n)), dim3(256), 0, st, g);
+    const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);     // a wave per txn
+    if (n) hipLaunchKernelGGL(general_kernel<false>, dim3(gw), dim3(256), 0, st, g);
     HostTotals *dev = s->status_totals.as<HostTotals>();
     accord::exclusive_scan_u32(g.gcnt, s->rg_goff.as<uint32_t>(), P, &dev->totals[9], s->scan_tmp.p, st);
     unsigned long long X = 0;
@@ -483,7 +551,7 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     HIPCHECK(s, hipMemcpyAsync(s->rg_hist2.p, s->hist.p, (size_t)PH * 4, hipMemcpyDeviceToDevice, st));
     g.hist2 = s->rg_hist2.as<uint32_t>();
     g.ext_base = PH;
-    if (n) hipLaunchKernelGGL(general_kernel<true>, dim3(grid_for(n)), dim3(256), 0, st, g);
+    if (n) hipLaunchKernelGGL(general_kernel<true>, dim3(gw), dim3(256), 0, st, g);
     *hist_for_fill = s->rg_hist2.as<uint32_t>();
     return ACCORD_OK;
 }
@@ -512,6 +580,51 @@ int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag)
     if (PH)
         hipLaunchKernelGGL(prune_mark_kernel, dim3(grid_for(PH)), dim3(256), 0, s->stream, PH, s->hist.as<uint32_t>(),
                            view_of(s), keep_flag);
+    return ACCORD_OK;
+}
+
+// CommandsForKey.withRedundantBefore (local/CommandsForKey.java:1654-1684) on a registered-status
+// store's carried history, for a new RedundantBefore map (m entries (start, end], bound =
+// shardAppliedOrInvalidatedBefore as a position, ACCORD_NO_TXN = none): every key's entries below its
+// entry's bound leave the resident state, so the next batches no longer see them.  A bound never
+// goes back in the reference (:1656); a lower one here truncates nothing more.
+int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
+                              const uint32_t *bound)
+{
+    const uint32_t C = s->carry_n, key_lo = s->cfg.key_lo, nkeys = s->cfg.key_hi - key_lo;
+    if (C == 0 || m == 0) return ACCORD_OK;
+    std::vector<uint32_t> kb(nkeys, 0u);
+    bool any = false;
+    uint32_t e = 0;
+    for (uint32_t r = 0; r < nkeys; ++r) {         // key r + key_lo in (start, end]
+        const uint32_t k = key_lo + r;
+        while (e < m && end[e] < k) ++e;
+        if (e == m) break;
+        if (start[e] < k && bound[e] != ACCORD_NO_TXN && bound[e] > 0) { kb[r] = bound[e]; any = true; }
+    }
+    if (!any) return ACCORD_OK;
+    hipStream_t st = s->stream;
+    HIPCHECK(s, s->rg_kbound.ensure((size_t)nkeys * 4));
+    HIPCHECK(s, s->carry_tmp.ensure(accord::carry_temp_bytes(C, nkeys)));
+    HIPCHECK(s, s->cy_key2.ensure((size_t)C * 4 + 4));
+    HIPCHECK(s, s->cy_ent2.ensure((size_t)C * 4 + 4));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(C), st));
+    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
+    HIPCHECK(s, hipMemcpyAsync(s->rg_kbound.p, kb.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
+    uint32_t *flag = accord::carry_flags(s->carry_tmp.p, nkeys);
+    hipLaunchKernelGGL(truncate_mark_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->cy_key.as<uint32_t>(),
+                       s->cy_ent.as<uint32_t>(), s->rg_kbound.as<uint32_t>(), flag);
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    accord::launch_carry(C, nkeys, 0u, s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), nullptr, nullptr,
+                         accord::HistoryViews{}, s->carry_tmp.p, s->scan_tmp.p, s->cy_key2.as<uint32_t>(),
+                         s->cy_ent2.as<uint32_t>(), &dev->totals[8], true, st);
+    unsigned long long kept = 0;
+    HIPCHECK(s, hipMemcpyAsync(&kept, &dev->totals[8], 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    HIPCHECK(s, hipGetLastError());
+    std::swap(s->cy_key, s->cy_key2);
+    std::swap(s->cy_ent, s->cy_ent2);
+    s->carry_n = (uint32_t)kept;
     return ACCORD_OK;
 }
 

@@ -111,7 +111,7 @@ struct accord_store {
     // (rg_t*, rg_tx_n entries, rg_tg = global position), InternalStatus + executeAt by global
     // position (rg_known positions), per-batch work
     DevBuf rg_tmsb, rg_tlsb, rg_tnode, rg_tg, rg_status, rg_emsb, rg_elsb, rg_enode;
-    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2;
+    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound;
     uint32_t rg_tx_n = 0, rg_known = 0;
     bool rg_flag_ok = false;       // rg_flag holds this batch's keys-with-registered-status flags
     // the uploaded batch: its carried-entry prefix, where it ends (global) and its last TxnId
@@ -172,6 +172,8 @@ int32_t merge_finalize(accord_store *s);   // read a bounded merge's totals (sha
 bool registered_mode(const accord_store *s);
 int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill);
 int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
+int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
+                              const uint32_t *bound);
 int32_t status_join_batch(accord_store *s);
 int32_t status_range_keys(accord_store *s, const accord::RangeDepsParams &rp, bool fill);
 int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned long long *words,

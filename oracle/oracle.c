@@ -350,6 +350,7 @@ typedef struct {
 typedef struct {
     txninfo_t *txns;   uint32_t n;     /* sorted by TxnId, :415 */
     uint32_t *committed; uint32_t nc;  /* indices into txns, sorted by executeAt, :419 */
+    uint32_t redundant_before;         /* shardRedundantBefore as a position (0: none), :413 */
 } cfk_t;
 
 static __thread const ts_t *g_sort_tbl;   /* qsort context (thread-local: one thread per store) */
@@ -379,8 +380,15 @@ static int cfk_rebuild(cfk_t *c, txninfo_t *new_txns, uint32_t new_n)
     c->nc = 0;
     for (uint32_t i = 0; i < new_n; ++i)
         if (new_txns[i].status >= S_COMMITTED && new_txns[i].status != S_INVALID_OR_TRUNCATED) c->committed[c->nc++] = i;
+    /* stable sort by executeAt (Arrays.sort of objects is stable); committed entries arrive in TxnId
+     * order and executeAt >= TxnId, so the array is nearly sorted: insertion sort, O(n + inversions) */
     g_sort_txns = new_txns;
-    qsort(c->committed, c->nc, sizeof(uint32_t), cmp_committed);
+    for (uint32_t a = 1; a < c->nc; ++a) {
+        const uint32_t x = c->committed[a];
+        uint32_t b = a;
+        while (b > 0 && cmp_committed(&c->committed[b - 1], &x) > 0) { c->committed[b] = c->committed[b - 1]; --b; }
+        c->committed[b] = x;
+    }
     return 0;
 }
 
@@ -771,7 +779,8 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
 
     for (uint32_t i = 0; i < n; ++i) {
         int tk = witnesses_of(kind_of(s->lsb[i]));
-        int64_t applied_before = (int64_t)i - (int64_t)s->window;    /* j < i-W are applied */
+        int64_t applied_before = s->applied_before ? (int64_t)s->applied_before[i]
+                                                   : (int64_t)i - (int64_t)s->window;    /* j < i-W are applied */
         const ts_t sb_i = started_before(s, i);
         const uint32_t bound = bound_of(s, n, &sb_i, i);     /* candidates j < bound (= i: PreAccept) */
         const long p1 = p1_of(s, i);                       /* excluded (Accept: the txn itself) */
@@ -799,6 +808,11 @@ int or_stream_deps_fast(const or_stream *s, or_deps *out)
                 long w = (long)l2 - 1;
                 while (w >= (long)a && kind_of(s->lsb[hist[w]]) != K_WRITE) --w;
                 if (w >= (long)a) start = (uint32_t)w;
+            }
+            if (s->floor && key > 0) {                    /* withRedundantBefore: entries < floor gone */
+                uint32_t l2 = a, h2 = p;
+                while (l2 < h2) { uint32_t m = (l2 + h2) / 2; if (hist[m] < s->floor[i]) l2 = m + 1; else h2 = m; }
+                if (l2 > start) start = l2;
             }
             uint32_t before = (uint32_t)lists.n;
             for (uint32_t e = start; e < p; ++e)
@@ -2131,14 +2145,39 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
         if (domain_of(s->tbl[g].lsb) != 0) continue;                       /* range command: status only */
         /* Erased / Invalidated leave CommandsForKey as INVALID_OR_TRUNCATED does */
         const uint8_t cs = nw >= S_ERASED ? (uint8_t)S_INVALID_OR_TRUNCATED : nw;
-        for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p)
-            if (cfk_update_status(&s->cfks[s->kord[p]], s->tbl, g, cs, &ex)) { free(pos); return -1; }
+        for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p) {
+            cfk_t *c = &s->cfks[s->kord[p]];
+            if (g < c->redundant_before) continue;       /* truncated from this key */
+            if (cfk_update_status(c, s->tbl, g, cs, &ex)) { free(pos); return -1; }
+        }
     }
     free(pos);
     return 0;
 }
 
 uint32_t or_lstore_size(const or_lstore *s) { return s->n; }
+
+int or_lstore_truncate(or_lstore *s, uint32_t m, const uint32_t *start, const uint32_t *end, const uint32_t *bound)
+{
+    for (uint32_t e = 0; e < m; ++e) if (start[e] >= end[e] || (e && end[e - 1] > start[e])) return -1;
+    uint32_t e = 0;
+    for (uint32_t k = 0; k < s->nkeys; ++k) {
+        while (e < m && end[e] < k) ++e;                 /* first entry with end >= k */
+        if (e == m || !(start[e] < k)) continue;         /* k in (start, end] */
+        if (bound[e] == 0xFFFFFFFFu) continue;           /* Timestamp.NONE */
+        cfk_t *c = &s->cfks[k];
+        if (bound[e] < c->redundant_before) return -1;    /* checkArgument: never goes back (:1656) */
+        c->redundant_before = bound[e];
+        uint32_t pos = 0;                                /* insertPos(0, bound) (:1664) */
+        while (pos < c->n && c->txns[pos].txn < bound[e]) ++pos;
+        if (pos == 0) continue;
+        txninfo_t *nt = (txninfo_t *)malloc(((size_t)(c->n - pos) + 1) * sizeof(txninfo_t));
+        if (!nt) return -1;
+        memcpy(nt, c->txns + pos, (size_t)(c->n - pos) * sizeof(txninfo_t));
+        if (cfk_rebuild(c, nt, c->n - pos)) return -1;
+    }
+    return 0;
+}
 
 
 /* ------------------------------------------------------------------------------------------

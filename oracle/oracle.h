@@ -59,6 +59,18 @@ typedef struct {
      * txn i only sees txns registered when its batch is computed, i.e. positions < batch_end[i].
      * Matters for Accept batches whose executeAt lies past their batch.  NULL = one batch. */
     const uint32_t *batch_end;
+    /* fast restatement only: per txn the position below which txns are committed at executeAt =
+     * txnId (replaces i - W; NULL = the window model).  A resident registered-status store whose
+     * batches are COMMITTED (executeAt = TxnId) right after they are computed -- the schedule of
+     * bench.py --registered -- has applied_before[i] = the first position of i's batch (COMMITTED
+     * and APPLIED prune alike in mapReduceActive, local/CommandsForKey.java:634-645). */
+    const uint32_t *applied_before;
+    /* fast restatement only: per txn the shardRedundantBefore in force when its batch is computed,
+     * as a position: CommandsForKey.withRedundantBefore (local/CommandsForKey.java:1654-1684) has
+     * dropped every key entry below it (one bound for every key but key 0, which lies in no
+     * (start, end] entry; range commands are not affected).
+     * NULL = no truncation. */
+    const uint32_t *floor;
 } or_stream;
 
 /* Per-txn PartialDeps in the exact reference layout (KeyDeps.java:150-187,
@@ -91,6 +103,12 @@ int        or_lstore_batch(or_lstore *s, const or_stream *b, or_deps *out);
 int        or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                               const uint8_t *status, const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode);
 uint32_t   or_lstore_size(const or_lstore *s);
+/* CommandsForKey.withRedundantBefore (local/CommandsForKey.java:1654-1684) on every key: the map's
+ * m entries (start, end] ascending and disjoint, bound = shardRedundantBefore as a position
+ * (0xFFFFFFFF = NONE); each key's txns below its entry's bound leave its CommandsForKey.  Later
+ * status events for a dropped txn no longer reach that key. */
+int        or_lstore_truncate(or_lstore *s, uint32_t m, const uint32_t *start, const uint32_t *end,
+                              const uint32_t *bound);
 
 /* ---- primitives restated for the reference's own property tests ---- */
 

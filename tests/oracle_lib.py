@@ -26,7 +26,8 @@ class _OrStream(C.Structure):
     _fields_ = [("n", C.c_uint32), ("msb", _u64p), ("lsb", _u64p), ("node", _i32p),
                 ("key_off", _u32p), ("key_ord", _u32p), ("rng_off", _u32p), ("rng_start", _u32p),
                 ("rng_end", _u32p), ("window", C.c_uint32),
-                ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p), ("batch_end", _u32p)]
+                ("exec_msb", _u64p), ("exec_lsb", _u64p), ("exec_node", _i32p), ("batch_end", _u32p),
+                ("applied_before", _u32p), ("floor", _u32p)]
 
 
 class _OrDeps(C.Structure):
@@ -99,7 +100,7 @@ def _to_partial(d: _OrDeps) -> PartialDeps:
     return PartialDeps(**kw)
 
 
-def _or_stream(s: Stream, window: int, batch_end=None):
+def _or_stream(s: Stream, window: int, batch_end=None, applied_before=None, floor=None):
     keep = [np.ascontiguousarray(a) for a in (s.msb, s.lsb, s.node, s.key_off, s.key_ord, s.rng_off,
                                               s.rng_start, s.rng_end)]
     msb, lsb, node, ko, kord, ro, rs, re = keep
@@ -125,6 +126,14 @@ def _or_stream(s: Stream, window: int, batch_end=None):
         be = np.ascontiguousarray(batch_end, dtype=np.uint32)
         keep.append(be)
         o.batch_end = be.ctypes.data_as(_u32p)
+    if applied_before is not None:
+        ab = np.ascontiguousarray(applied_before, dtype=np.uint32)
+        keep.append(ab)
+        o.applied_before = ab.ctypes.data_as(_u32p)
+    if floor is not None:
+        fl = np.ascontiguousarray(floor, dtype=np.uint32)
+        keep.append(fl)
+        o.floor = fl.ctypes.data_as(_u32p)
     return o, keep
 
 
@@ -132,6 +141,12 @@ class OracleError(RuntimeError):
     def __init__(self, rc):
         super().__init__(f"oracle rc={rc}")
         self.rc = rc
+
+
+def batch_starts(sizes):
+    """applied_before[i] of the committed-per-batch schedule: the first position of i's batch."""
+    starts = np.cumsum(np.asarray(sizes, np.int64)) - np.asarray(sizes, np.int64)
+    return np.repeat(starts, sizes).astype(np.uint32)
 
 
 def batch_ends(sizes):
@@ -157,8 +172,11 @@ def deps_literal(s: Stream, window: int, limit: int | None = None, batch_end=Non
         lib().or_deps_free(C.byref(d))
 
 
-def deps_fast(s: Stream, window: int, batch_end=None) -> PartialDeps:
-    o, keep = _or_stream(s, window, batch_end)
+def deps_fast(s: Stream, window: int, batch_end=None, applied_before=None, floor=None) -> PartialDeps:
+    """Fast restatement; applied_before[i] (optional) replaces i - W as the position below which
+    txns are committed at executeAt = txnId, floor[i] (optional) is the shardRedundantBefore below
+    which key entries were truncated (see oracle.h)."""
+    o, keep = _or_stream(s, window, batch_end, applied_before, floor)
     d = _OrDeps()
     rc = lib().or_stream_deps_fast(C.byref(o), C.byref(d))
     if rc != 0:
@@ -454,6 +472,7 @@ class LStore:
             L.or_lstore_register.argtypes = [C.c_void_p, C.c_uint32, _u64p, _u64p, _i32p, _u8p, _u64p, _u64p, _i32p]
             L.or_lstore_size.argtypes = [C.c_void_p]
             L.or_lstore_size.restype = C.c_uint32
+            L.or_lstore_truncate.argtypes = [C.c_void_p, C.c_uint32, _u32p, _u32p, _u32p]
             L._lstore_typed = True
         self._h = L.or_lstore_create(nkeys)
 
@@ -478,6 +497,13 @@ class LStore:
             return _to_partial(d)
         finally:
             lib().or_deps_free(C.byref(d))
+
+    def truncate(self, start, end, bound):
+        """CommandsForKey.withRedundantBefore on every key of the map's entries (oracle.h)."""
+        a = [np.ascontiguousarray(x, np.uint32) for x in (start, end, bound)]
+        rc = lib().or_lstore_truncate(self._h, len(a[0]), *[x.ctypes.data_as(_u32p) for x in a])
+        if rc != 0:
+            raise OracleError(rc)
 
     def register(self, msb, lsb, node, status, exec_msb=None, exec_lsb=None, exec_node=None):
         a = [np.ascontiguousarray(msb, np.uint64), np.ascontiguousarray(lsb, np.uint64),
