@@ -70,19 +70,26 @@ def main():
     ap.add_argument("--range-frac", type=float, default=None)
     ap.add_argument("--range-len", type=int, default=1000)
     ap.add_argument("--write-frac", type=float, default=None)
-    ap.add_argument("--cpu-sample", type=int, default=None, help="txns of the CPU-baseline prefix sample")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="first txns of the CPU-baseline prefix sample (default: grown by doubling within --cpu-budget)")
+    ap.add_argument("--cpu-budget", type=float, default=25.0,
+                    help="seconds of CPU-baseline work: the prefix doubles while the next run fits (600 = the "
+                         "largest prefix within 10 minutes)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--resident", action="store_true",
                     help="also time the stream fed as 8 batches to one resident store (resident_batches); "
                          "off by default so a kernel trace of the default run holds one batch size only")
+    ap.add_argument("--registered", action="store_true",
+                    help="also time the registered-status store (real status events, no status-at-time model) "
+                         "on the config-2 stream fed in batches (registered_batches)")
+    ap.add_argument("--reg-batch", type=int, default=1024, help="txns per batch of the --registered leg")
+    ap.add_argument("--reg-batches", type=int, default=64, help="batches of the --registered leg")
     args = ap.parse_args()
     preset = PRESETS[args.config]
     for k, v in preset.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
     args.waiting_on = args.config == 5
-    if args.cpu_sample is None:
-        args.cpu_sample = 24_000
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -205,10 +212,13 @@ def main():
 
     boundary = None
     resident = None
+    registered = None
     if world == 1 and not args.waiting_on:
         boundary = boundary_rate(store, s)
         if s.rng_off[-1] == 0 and args.resident:
             resident = resident_split(s, args, stage["total"])
+        if s.rng_off[-1] == 0 and args.registered:
+            registered = registered_batches(s, args)
 
     if rank != 0:
         store.close()
@@ -244,7 +254,8 @@ def main():
         "config": {"workload": workload_name(args),
                    "n_txns_per_gpu": args.n, "keys_per_txn": args.keys_per_txn, "keyspace": args.keyspace,
                    "zipf": args.zipf, "window": args.window, "seed": args.seed,
-                   "n_txns_total": n_total, "stores": stores_total,
+                   "n_txns_total": n_total,
+                   "gpu_stores": world, "evensplit_stores": stores_total if world > 1 else None,
                    "parallelism": f"keyspace-sharded x{world}" + (" + RCCL exchange/union" if world > 1 else "")},
         "deps_per_s": D * world * args.steps / elapsed,
         "sizes": {"N": n, "P": P, "keys_out": kc, "U": U, "D": D},
@@ -270,6 +281,8 @@ def main():
         line["boundary_inclusive"] = boundary
     if resident is not None:
         line["resident_batches"] = resident
+    if registered is not None:
+        line["registered_batches"] = registered
     print(json.dumps(line))
     store.close()
     if dist is not None:
@@ -307,31 +320,127 @@ def boundary_rate(store, s):
     return {"ms": ms, "txns_per_s": s.n / (ms * 1e-3), "path": "accord_deps_batch, host buffers in and out"}
 
 
-def resident_split(s, args, single_ms, batches=8, reps=3):
-    """The same stream fed as `batches` consecutive batches to one resident store (CommandsForKey
-    state kept in HBM across batches, deps identical to the single batch): device time of the
-    computes (HIP events) and host wall time around them (uploads excluded), per full stream,
-    against the single-batch device time."""
+def resident_split(s, args, single_ms, batch_counts=(8, 64, 512), reps=3):
+    """The same stream fed as B consecutive batches to one resident store (CommandsForKey state kept
+    in HBM across batches, deps identical to the single batch), for each B of batch_counts: device
+    time of the computes (HIP events, with the per-stage split) and host wall time around them
+    (uploads excluded), per full stream, against the single-batch device time."""
     from accord_amd import CommandStore
-    pts = [i * s.n // batches for i in range(batches + 1)]
-    parts = [s.slice(a, b) for a, b in zip(pts[:-1], pts[1:])]
-    dev, wall = [], []
+    out = []
     with CommandStore(device=0, key_lo=0, key_hi=args.keyspace, window=args.window, profile=True,
                       resident=True) as st:
-        for _ in range(reps + 1):
-            st.reset()
-            d = w = 0.0
-            for p in parts:
-                st.upload(p)
-                t0 = time.perf_counter()
-                st.compute()
-                w += time.perf_counter() - t0
-                d += st.timing().total_ms
-            dev.append(d)
-            wall.append(w * 1e3)
-    dev, wall = min(dev[1:]), min(wall[1:])
-    return {"batches": batches, "device_ms": dev, "compute_wall_ms": wall, "single_batch_device_ms": single_ms,
-            "device_ratio": dev / single_ms if single_ms else None}
+        for batches in batch_counts:
+            pts = [i * s.n // batches for i in range(batches + 1)]
+            parts = [s.slice(a, b) for a, b in zip(pts[:-1], pts[1:])]
+            best = None
+            for _ in range(reps + 1):
+                st.reset()
+                acc = {"device_ms": 0.0, "compute_wall_ms": 0.0, "validate_ms": 0.0, "sort_ms": 0.0,
+                       "segment_ms": 0.0, "count_ms": 0.0, "scan_ms": 0.0, "fill_ms": 0.0, "compact_ms": 0.0}
+                for p in parts:
+                    st.upload(p)
+                    t0 = time.perf_counter()
+                    st.compute()
+                    acc["compute_wall_ms"] += (time.perf_counter() - t0) * 1e3
+                    t = st.timing()
+                    acc["device_ms"] += t.total_ms
+                    for k in ("validate_ms", "sort_ms", "segment_ms", "count_ms", "scan_ms", "fill_ms", "compact_ms"):
+                        acc[k] += getattr(t, k)
+                if best is None or acc["device_ms"] < best["device_ms"]:
+                    best = acc
+            best["batches"] = batches
+            best["single_batch_device_ms"] = single_ms
+            best["device_ratio"] = best["device_ms"] / single_ms if single_ms else None
+            best["wall_ratio"] = best["compute_wall_ms"] / single_ms if single_ms else None
+            out.append(best)
+    return out
+
+
+ST_COMMITTED, ST_APPLIED = 4, 6
+
+
+def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
+    """The real drop-in mode: a resident store with no status-at-time model (window
+    ACCORD_WINDOW_NONE) fed the first reg_batches x reg_batch txns of the stream, with the event
+    schedule of tests/status_events.py committed_schedule -- right after batch b is computed its txns
+    are registered COMMITTED at executeAt = TxnId and those of batch b - 4 APPLIED
+    (accord_txn_register), and the store's RedundantBefore moves to the first txn of batch b - 8
+    (accord_redundant_before_set: CommandsForKey.withRedundantBefore truncates the resident history,
+    RedundantBefore.collectDeps adds the bound to every later txn's deps).  Per batch: the compute's
+    device time (HIP events) and stages, and the host wall time of compute, register and
+    RedundantBefore calls (uploads excluded).  Beside it: the status-at-time resident store (window
+    W) fed the same batches, for the fill-stage comparison."""
+    from accord_amd import CommandStore, WINDOW_NONE
+    bsz, nb = args.reg_batch, args.reg_batches
+    nb = min(nb, s.n // bsz)
+    parts = [s.slice(b * bsz, (b + 1) * bsz) for b in range(nb)]
+    starts = [b * bsz for b in range(nb + 1)]
+    ks = args.keyspace
+
+    def events(b):
+        idx = np.arange(starts[b], starts[b + 1])
+        st = np.full(idx.size, ST_COMMITTED, np.uint8)
+        if b >= lag_applied:
+            a = np.arange(starts[b - lag_applied], starts[b - lag_applied + 1])
+            idx = np.concatenate([a, idx])
+            st = np.concatenate([np.full(a.size, ST_APPLIED, np.uint8), st])
+        return (s.msb[idx], s.lsb[idx], s.node[idx], st, s.msb[idx], s.lsb[idx], s.node[idx])
+
+    evs = [events(b) for b in range(nb)]
+
+    def run(window, with_events):
+        best = None
+        with CommandStore(device=0, key_lo=0, key_hi=ks, window=window, profile=True, resident=True) as st:
+            for _ in range(reps + 1):
+                st.reset()
+                st.redundant_before()
+                acc = {"device_ms": 0.0, "fill_ms": 0.0, "count_ms": 0.0, "sort_ms": 0.0, "segment_ms": 0.0,
+                       "compact_ms": 0.0, "compute_wall_ms": 0.0, "register_wall_ms": 0.0, "rb_wall_ms": 0.0}
+                for b, p in enumerate(parts):
+                    st.upload(p)
+                    t0 = time.perf_counter()
+                    st.compute()
+                    t1 = time.perf_counter()
+                    t = st.timing()
+                    acc["device_ms"] += t.total_ms
+                    acc["fill_ms"] += t.fill_ms
+                    acc["count_ms"] += t.count_ms
+                    acc["sort_ms"] += t.sort_ms
+                    acc["segment_ms"] += t.segment_ms
+                    acc["compact_ms"] += t.compact_ms
+                    acc["compute_wall_ms"] += (t1 - t0) * 1e3
+                    if with_events:
+                        t2 = time.perf_counter()
+                        st.register(*evs[b])
+                        t3 = time.perf_counter()
+                        acc["register_wall_ms"] += (t3 - t2) * 1e3
+                        if b >= lag_rb and starts[b - lag_rb] > 0:
+                            st.redundant_before(start=[0], end=[ks - 1], start_epoch=[0], end_epoch=[1 << 62],
+                                                bound=[starts[b - lag_rb]], min_epoch=0)
+                            acc["rb_wall_ms"] += (time.perf_counter() - t3) * 1e3
+                carry = st.state()["carry_entries"]
+                if best is None or acc["compute_wall_ms"] < best[0]["compute_wall_ms"]:
+                    best = (acc, carry)
+        acc, carry = best
+        per = {k.replace("_ms", "_ms_per_batch"): v / nb for k, v in acc.items()}
+        per["carry_entries_end"] = carry
+        return per, acc
+
+    reg, racc = run(WINDOW_NONE, True)
+    sat, _ = run(args.window, False)
+    wall = racc["compute_wall_ms"] + racc["register_wall_ms"] + racc["rb_wall_ms"]
+    return {"schedule": f"{nb} batches x {bsz} txns of the config-2 stream; after batch b: COMMITTED "
+                        f"(executeAt = TxnId) for b, APPLIED for b-{lag_applied}, RedundantBefore = first txn "
+                        f"of b-{lag_rb}",
+            "txns": nb * bsz,
+            "txns_per_s_wall": nb * bsz / (wall * 1e-3),
+            "txns_per_s_device": nb * bsz / (racc["device_ms"] * 1e-3),
+            "registered": reg,
+            "status_at_time_W": sat,
+            "fill_ratio_vs_status_at_time": (reg["fill_ms_per_batch"] / sat["fill_ms_per_batch"])
+            if sat["fill_ms_per_batch"] else None,
+            "device_ratio_vs_status_at_time": (reg["device_ms_per_batch"] / sat["device_ms_per_batch"])
+            if sat["device_ms_per_batch"] else None}
 
 
 def measured_traffic(config):
@@ -360,34 +469,60 @@ def _cpu_model():
 def cpu_baseline(s, args):
     """The oracle's literal restatement of the reference algorithm (sorted-array CommandsForKey
     copied/re-sorted on every status change, linear mapReduceActive scan, RelationMultiMap
-    builder) on the first --cpu-sample txns of the same stream.  Key-only streams run the
-    reference's threading model: S = 8 CommandStores (EvenSplit of the keyspace), one thread per
-    store (impl/InMemoryCommandStore.java:1131-1148); ctypes releases the GIL for each store's
-    call.  The per-store partials are not unioned (the coordinator's job), which favours the CPU."""
+    builder) on a prefix of the same stream.  Key-only streams run the reference's node-level
+    shape: S = 8 CommandStores (EvenSplit of the keyspace), one thread per store
+    (impl/InMemoryCommandStore.java:1131-1148; ctypes releases the GIL for each store's call), then
+    the coordinator's union of the 8 partials (PreAccept.reduce / Deps.merge) -- the same deps the
+    GPU's single store produces.  The prefix starts at --cpu-sample (8192) and doubles while the
+    next run is expected to fit --cpu-budget seconds; the largest completed run is reported.  Beside
+    it, config 1 (64k txns x 4 keys, uniform 100k keys, one store) at full size."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
         from concurrent.futures import ThreadPoolExecutor
-        m = min(args.cpu_sample, s.n)
-        pre = s.prefix(m)
-        multi = int(pre.rng_off[-1]) == 0 and not args.waiting_on
-        threads = min(8, os.cpu_count() or 1) if multi else 1
-        t0 = time.perf_counter()
-        if multi:
-            stores = [pre.restrict_keys(b * args.keyspace // 8, (b + 1) * args.keyspace // 8) for b in range(8)]
-            with ThreadPoolExecutor(threads) as ex:
-                list(ex.map(lambda st: oracle_lib.deps_literal(st, args.window), stores))
-        else:
-            d = oracle_lib.deps_literal(pre, args.window)
-            if args.waiting_on:
-                oracle_lib.waiting_on(d)
-        dt = time.perf_counter() - t0
-        how = (f"8 stores on {threads} threads" if multi else "1 store, 1 thread") + \
+        key_only = int(s.rng_off[-1]) == 0 and not args.waiting_on
+        threads = min(8, os.cpu_count() or 1) if key_only else 1
+
+        def run(m):
+            pre = s.prefix(m)
+            t0 = time.perf_counter()
+            if key_only:
+                stores = [pre.restrict_keys(b * args.keyspace // 8, (b + 1) * args.keyspace // 8) for b in range(8)]
+                with ThreadPoolExecutor(threads) as ex:
+                    parts = list(ex.map(lambda st: oracle_lib.deps_literal(st, args.window), stores))
+                oracle_lib.deps_union(parts)
+            else:
+                d = oracle_lib.deps_literal(pre, args.window)
+                if args.waiting_on:
+                    oracle_lib.waiting_on(d)
+            return time.perf_counter() - t0
+
+        m = min(args.cpu_sample or 8192, s.n)
+        spent = 0.0
+        while True:
+            dt = run(m)
+            spent += dt
+            done = (m, dt)
+            # a doubled prefix costs >= 2x (CommandsForKey histories grow with it): stop unless it fits
+            if m >= s.n or spent + 2.5 * dt > args.cpu_budget:
+                break
+            m = min(2 * m, s.n)
+        m, dt = done
+        how = (f"8 stores on {threads} threads + union of the partials" if key_only else "1 store, 1 thread") + \
               (" + levelling" if args.waiting_on else "")
-        return {"value": m / dt, "unit": "txns/s", "cores": threads, "kind": "port",
-                "sample": f"first {m} txns of the config-{args.config} stream, literal reference algorithm, "
-                          f"{how}, {dt:.1f} s; CFK histories grow with the prefix so the full run would be slower",
-                "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
+        out = {"value": m / dt, "unit": "txns/s", "cores": threads, "kind": "port",
+               "sample": f"first {m} txns of the config-{args.config} stream, literal reference algorithm, "
+                         f"{how}, {dt:.1f} s; CFK histories grow with the prefix so the full run would be slower",
+               "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
+        from accord_amd import generate_stream
+        c1 = generate_stream(65536, 4, 100_000, 0.0, 0.5, seed=1)
+        t0 = time.perf_counter()
+        oracle_lib.deps_literal(c1, args.window)
+        t1 = time.perf_counter() - t0
+        out["config1_full"] = {"value": c1.n / t1, "unit": "txns/s", "seconds": t1, "cores": 1,
+                               "sample": f"config 1 at full size: 65536 txns x 4 keys, uniform over 100000 keys, "
+                                         f"50% writes, W={args.window}, one store, literal reference algorithm"}
+        return out
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "txns/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
 
