@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = [
     "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
     "accord_comm_init", "accord_deps_exchange_merge", "accord_deps_exchange_local", "accord_shard_timing",
+    "accord_ready_update",
     "accord_waiting_on_compute", "accord_waiting_on_initialise", "accord_waiting_on_download", "accord_waiting_on_release",
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
@@ -114,6 +115,10 @@ class _Deps(C.Structure):
                 ("rd_rng_off", _u32p), ("rd_rng_start", _u32p), ("rd_rng_end", _u32p),
                 ("rd_val_off", _u32p), ("rd_vals", _u32p), ("rd_r2v_off", _u32p), ("rd_r2v", _i32p),
                 ("owner", C.c_void_p)]
+
+
+class _Ready(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("waiting", C.c_uint64), ("txn", C.POINTER(C.c_uint32))]
 
 
 class _WaitingOn(C.Structure):
@@ -191,6 +196,7 @@ def lib() -> C.CDLL:
         L.accord_shard_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.accord_waiting_on_compute.argtypes = [C.c_void_p]
         L.accord_waiting_on_initialise.argtypes = [C.c_void_p]
+        L.accord_ready_update.argtypes = [C.c_void_p, C.POINTER(_Ready)]
         L.accord_waiting_on_download.argtypes = [C.c_void_p, C.POINTER(_WaitingOn)]
         L.accord_waiting_on_release.argtypes = [C.POINTER(_WaitingOn)]
         L.accord_waiting_on_release.restype = None
@@ -846,6 +852,17 @@ class CommandStore:
         statuses (registered-status stores; include/accord_deps.h accord_waiting_on_initialise)."""
         self._check(lib().accord_waiting_on_initialise(self._h))
         return self.waiting_on_download()
+
+    def ready_update(self):
+        """Execution readiness (include/accord_deps.h accord_ready_update): re-evaluates every txn of
+        the waiting set (batches whose WaitingOn was initialised) against the registered statuses --
+        Commands.updateWaitingOn for range deps, CommandsForKey.notify / notifyUnmanaged for keys --
+        and returns the global positions (ascending) of the txns now ReadyToExecute, and how many
+        txns still wait."""
+        r = _Ready()
+        self._check(lib().accord_ready_update(self._h, C.byref(r)))
+        got = np.ctypeslib.as_array(r.txn, shape=(r.n,)).copy() if r.n else np.zeros(0, np.uint32)
+        return got, int(r.waiting)
 
     def waiting_on_timing(self):
         a, b, c = C.c_float(), C.c_float(), C.c_float()

@@ -1,0 +1,418 @@
+// Execution readiness of a registered-status store (CommandsForKey.notify /
+// notifyUnmanaged and Commands.updateWaitingOn on the device).
+//
+// accord_waiting_on_initialise puts the last computed batch's txns into the store's waiting set: a
+// generation holding a copy of their deps (KeyDeps + RangeDeps txnIds, global positions), their
+// WaitingOn words and appliedOrInvalidated words, and per (txn, key) the unmanaged pending record.
+// accord_ready_update then, against the statuses registered so far:
+//   1. summarises every key's CommandsForKey from the resident history (a wave per key): the
+//      earliest executeAt among the unapplied committed (COMMITTED / STABLE) txns per kind class
+//      (Read, Write, SyncPoints), `next` (the earliest of all of them, nulled when minUncommitted
+//      precedes it, local/CommandsForKey.java:432-461) and minUncommitted;
+//   2. re-evaluates every waiting txn (a wave per txn, a lane per WaitingOn bit):
+//      - range-dep bit: Commands.updateWaitingOn (local/Commands.java:769-830) once the dep
+//        hasBeen(PreCommitted): truncated / invalidated -> setAppliedOrInvalidated, executes after
+//        us (not awaitsOnlyDeps) -> removeWaitingOn, applied -> setAppliedAndPropagate;
+//      - key bit of a managed txn (key domain, globally visible; STABLE): notify's count test
+//        (:1512-1635) expectMissingCount == |missing|, which holds iff no unapplied committed txn
+//        of a kind it witnesses executes before it (the class minima) and no dep of the key in its
+//        deps is still uncommitted (uncommitted non-deps are exactly its missing[] set,
+//        computeInfoAndAdditions :1071-1140, committed ones elided :1103-1109);
+//      - key bit of an unmanaged txn (range domain, EphemeralRead; hasBeen Stable):
+//        registerUnmanaged (:1406-1498) on the first evaluation, a COMMIT record whose waitingUntil
+//        precedes minUncommitted re-evaluated as updatePending (:1315-1360), an APPLY record
+//        released by notifyUnmanaged(APPLY, next.executeAt) (:1264-1283);
+//      - no bit left and STABLE: ReadyToExecute (Commands.maybeExecute, :656-733), reported once.
+// The reference evaluates these tests when an event reaches the key (notifyAndUpdatePending,
+// :1163-1215); here every waiting txn is evaluated at every call, so a txn is released at the first
+// call at which its test holds.  oracle/oracle.c (or_lstore_ready) restates the same evaluation over
+// literal CommandsForKey objects.
+#include "store_impl.h"
+#include "status_view.h"
+
+#include <algorithm>
+#include <vector>
+
+using namespace accord_status;
+
+namespace {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+struct KeySummary {
+    uint32_t min_cls[3];              // unapplied committed txn with the earliest executeAt: Read, Write, SyncPoints
+    uint32_t next;                    // earliest of them (any kind)
+    uint32_t min_unc;                 // first uncommitted txn (TxnId order)
+    uint32_t pad[3];
+};
+
+__device__ __forceinline__ uint32_t kind_class(uint32_t kind) { return kind == 0u ? 0u : kind == 1u ? 1u : 2u; }
+
+// segment bounds of the carried history (key-major): kseg0[k] .. kseg1[k]
+__global__ __launch_bounds__(256) void rd_seg_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
+                                                     uint32_t *__restrict__ kseg0, uint32_t *__restrict__ kseg1)
+{
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+        const uint32_t k = ckey[c];
+        if (c == 0 || ckey[c - 1] != k) kseg0[k] = c;
+        if (c + 1 == C || ckey[c + 1] != k) kseg1[k] = c + 1;
+    }
+}
+
+// the earlier of two candidate txns by executeAt (NONE = no candidate)
+__device__ __forceinline__ uint32_t earlier(const StatusView &v, uint32_t a, uint32_t b)
+{
+    if (a == NONE) return b;
+    if (b == NONE) return a;
+    return tcmp(exec_of(v, b), exec_of(v, a)) < 0 ? b : a;
+}
+
+__device__ __forceinline__ uint32_t wave_earlier(const StatusView &v, uint32_t x)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x = earlier(v, x, (uint32_t)__shfl_xor((int)x, d, 64));
+    return x;
+}
+
+// a wave per key: the summary of its CommandsForKey (managed txns: EphemeralReads are not inserted)
+__global__ __launch_bounds__(256) void rd_summary_kernel(uint32_t nkeys, const uint32_t *__restrict__ kseg0,
+                                                         const uint32_t *__restrict__ kseg1,
+                                                         const uint32_t *__restrict__ cent, StatusView v,
+                                                         KeySummary *__restrict__ sum)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t k = blockIdx.x * (blockDim.x / 64) + wave_id(); k < nkeys; k += waves) {
+        const uint32_t a = kseg0[k], b = kseg1[k];
+        uint32_t mc[3] = {NONE, NONE, NONE}, mu = NONE;
+        for (uint32_t x = a + lane; x < b; x += 64) {
+            const uint32_t e = cent[x], g = e & ENT_TXN_MASK, kind = e >> ENT_KIND_SHIFT;
+            if (kind == 2u) continue;
+            const uint32_t st = status_of(v, g);
+            if (st >= ST_INVALID) continue;
+            if (st >= ST_COMMITTED) {
+                if (st < ST_APPLIED) {
+                    const uint32_t c = kind_class(kind);
+                    mc[c] = earlier(v, mc[c], g);
+                }
+            } else {
+                mu = min(mu, g);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) mc[c] = wave_earlier(v, mc[c]);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) mu = min(mu, (uint32_t)__shfl_xor((int)mu, d, 64));
+        if (lane == 0) {
+            KeySummary s{};
+            for (int c = 0; c < 3; ++c) s.min_cls[c] = mc[c];
+            s.next = earlier(v, earlier(v, mc[0], mc[1]), mc[2]);   // nulled by the evaluation (TxnId order)
+            s.min_unc = mu;
+            sum[k] = s;
+        }
+    }
+}
+
+struct ReadyParams {
+    uint32_t n, key_lo;
+    const uint32_t *g;                // [n] global positions
+    const uint64_t *lsb;              // [n] TxnId lsb (kind, domain)
+    const uint64_t *tmsb, *tlsb;      // the store's TxnIds, ascending, and their global positions (ascending)
+    const int32_t *tnode;
+    const uint32_t *tg;
+    uint32_t tx_n;
+    const uint32_t *rd_off, *rd_vals;
+    const uint32_t *key_off, *keys, *val_off, *vals, *k2v_off;
+    const int32_t *k2v;
+    const uint32_t *wo_off;
+    unsigned long long *words, *aoi;
+    uint8_t *pend;                    // per key slot: 0 unregistered, 1 COMMIT, 2 APPLY, 3 released
+    uint32_t *until;
+    uint8_t *done;
+    uint32_t *out, *out_cnt;          // txns that became ready (positions)
+    const KeySummary *sum;
+    const uint32_t *kb;               // per key: shardRedundantBefore as a position (0: none)
+    StatusView v;
+};
+
+// the TxnId of global position g (the store's TxnId table is in stream order)
+__device__ __forceinline__ Ts tid_of(const ReadyParams &p, uint32_t g)
+{
+    uint32_t lo = 0, hi = p.tx_n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (p.tg[m] < g) lo = m + 1; else hi = m;
+    }
+    return Ts{p.tmsb[lo], p.tlsb[lo], p.tnode[lo]};
+}
+
+// registerUnmanaged (reg) / updatePending over the deps [d0, d1) of one key: 1 = ready, 0 = APPLY
+// pending (*until = the relevant dep executing last), -1 = COMMIT pending (*until = the last dep)
+__device__ int unmanaged_eval(const ReadyParams &p, uint32_t t, uint32_t d0, uint32_t d1, uint32_t kbound,
+                              const Ts &ex, bool only_deps, bool reg, uint32_t &until)
+{
+    const uint32_t vb = p.val_off[t], kb0 = p.k2v_off[t];
+    uint32_t x = d0;
+    while (x < d1 && p.vals[vb + p.k2v[kb0 + x]] < kbound) ++x;    // txnIds.find(shardRedundantBefore)
+    if (x >= d1) return 1;
+    bool ready = true, to_apply = true;
+    uint32_t best = NONE;
+    for (; x < d1; ++x) {
+        const uint32_t u = p.vals[vb + p.k2v[kb0 + x]], st = status_of(p.v, u);
+        if (reg && st < ST_COMMITTED) { ready = to_apply = false; continue; }
+        const Ts ue = exec_of(p.v, u);
+        if (only_deps || tcmp(ue, ex) < 0) {
+            ready &= st >= ST_APPLIED;
+            if (best == NONE || tcmp(exec_of(p.v, best), ue) < 0) best = u;
+        }
+    }
+    if (ready) return 1;
+    const uint32_t last = p.vals[vb + p.k2v[kb0 + d1 - 1]];
+    if (to_apply) { until = best == NONE ? last : best; return 0; }
+    until = last;
+    return -1;
+}
+
+// a wave per waiting txn, a lane per WaitingOn bit (64 per word)
+__global__ __launch_bounds__(256) void rd_eval_kernel(ReadyParams p)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t t = blockIdx.x * (blockDim.x / 64) + wave_id(); t < p.n; t += waves) {
+        if (p.done[t]) continue;
+        const uint32_t g = p.g[t], st = status_of(p.v, g);
+        const uint64_t l = p.lsb[t];
+        const uint32_t kind = (uint32_t)(l >> 1) & 7u;
+        const bool rdom = (l & 1u) != 0;
+        const bool only_deps = kind == 4u || kind == 2u;                 // Txn.Kind.awaitsOnlyDeps
+        const bool managed = !rdom && kind != 2u;                        // key domain, globally visible
+        const Ts ex = exec_of(p.v, g);
+        const uint32_t wmask = witness_mask(kind);
+        const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], K = p.key_off[t + 1] - p.key_off[t];
+        const uint32_t w0 = p.wo_off[t], nw = p.wo_off[t + 1] - w0;
+        bool waiting = false;
+        for (uint32_t q = 0; q < nw; ++q) {
+            const unsigned long long old = p.words[w0 + q];
+            const uint32_t b = q * 64u + lane;
+            bool clear = false, applied = false;
+            if (b < R + K && ((old >> lane) & 1ull)) {
+                if (b < R) {                                             // range-dep bit
+                    const uint32_t d = p.rd_vals[p.rd_off[t] + b], ds = status_of(p.v, d);
+                    if (ds >= ST_COMMITTED) {                            // hasBeen(PreCommitted)
+                        if (ds >= ST_INVALID) clear = applied = true;
+                        else if (!only_deps && tcmp(exec_of(p.v, d), ex) > 0) clear = true;
+                        else if (ds == ST_APPLIED) clear = applied = true;
+                    }
+                } else {                                                 // key bit
+                    const uint32_t qs = b - R, slot = p.key_off[t] + qs;
+                    const uint32_t kk = p.keys[slot] - p.key_lo;
+                    const KeySummary s = p.sum[kk];
+                    const uint32_t kbound = p.kb ? p.kb[kk] : 0u;
+                    const uint32_t hb = p.k2v_off[t];
+                    const uint32_t d0 = qs == 0 ? K : (uint32_t)p.k2v[hb + qs - 1], d1 = (uint32_t)p.k2v[hb + qs];
+                    if (managed) {
+                        if (st == ST_STABLE) {
+                            bool blocked = false;                        // an unapplied committed predecessor
+                            if (((wmask >> 0) & 1u) && s.min_cls[0] != NONE && tcmp(exec_of(p.v, s.min_cls[0]), ex) < 0) blocked = true;
+                            if (((wmask >> 1) & 1u) && s.min_cls[1] != NONE && tcmp(exec_of(p.v, s.min_cls[1]), ex) < 0) blocked = true;
+                            if (((wmask >> 3) & 1u) && s.min_cls[2] != NONE && tcmp(exec_of(p.v, s.min_cls[2]), ex) < 0) blocked = true;
+                            for (uint32_t x = d0; x < d1 && !blocked; ++x) {   // a dep still uncommitted
+                                const uint32_t u = p.vals[p.val_off[t] + p.k2v[hb + x]];
+                                if (u >= kbound && status_of(p.v, u) < ST_COMMITTED) blocked = true;
+                            }
+                            clear = !blocked;
+                        }
+                    } else if (st >= ST_STABLE && st < ST_INVALID) {     // hasBeen(Stable), not truncated
+                        uint32_t pd = p.pend[slot], un = p.until[slot];
+                        if (pd == 0) {                                   // registerUnmanaged
+                            const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, true, un);
+                            pd = r == 1 ? 3u : r == 0 ? 2u : 1u;
+                        }
+                        uint32_t nx = s.next;
+                        if (nx != NONE && s.min_unc != NONE && tcmp(tid_of(p, s.min_unc), exec_of(p.v, nx)) < 0)
+                            nx = NONE;                                   // nulled by minUncommitted (:454-455)
+                        if (pd == 1 && (s.min_unc == NONE || s.min_unc > un)) {   // COMMIT -> updatePending
+                            const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, false, un);
+                            pd = r == 1 ? 3u : 2u;
+                        }
+                        if (pd == 2 && (s.min_unc == NONE || nx != NONE)) {       // notifyUnmanaged(APPLY, next)
+                            if (nx == NONE || tcmp(exec_of(p.v, un), exec_of(p.v, nx)) < 0) pd = 3;
+                        }
+                        p.pend[slot] = (uint8_t)pd;
+                        p.until[slot] = un;
+                        clear = pd == 3;
+                    }
+                }
+            }
+            const unsigned long long cm = __ballot(clear);
+            const unsigned long long am = __ballot(applied && rdom);   // appliedOrInvalidated: Range-domain txns
+            const unsigned long long nwv = old & ~cm;
+            if (lane == 0) {
+                if (cm) p.words[w0 + q] = nwv;
+                if (am) p.aoi[w0 + q] |= am;
+            }
+            waiting |= nwv != 0ull;
+        }
+        if (!waiting && st == ST_STABLE && lane == 0) {
+            p.done[t] = 1;
+            p.out[atomicAdd(p.out_cnt, 1u)] = g;
+        }
+    }
+}
+
+inline uint32_t grid_for_waves(uint64_t waves)
+{
+    uint64_t b = (waves + 3) / 4;
+    return (uint32_t)(b < 1 ? 1 : b > 8192 ? 8192 : b);
+}
+
+} // namespace
+
+namespace accord_impl {
+
+struct ReadyGen {
+    uint32_t n = 0, left = 0, glo = 0, ghi = 0;   // txns, not yet ready, first / last global position
+    uint64_t words = 0;
+    DevBuf g, lsb, rd_off, rd_vals, key_off, keys, val_off, vals, k2v_off, k2v, wo_off, wo, aoi, pend, until, done;
+    void release()
+    {
+        DevBuf *b[] = {&g, &lsb, &rd_off, &rd_vals, &key_off, &keys, &val_off, &vals, &k2v_off, &k2v, &wo_off, &wo, &aoi,
+                       &pend, &until, &done};
+        for (DevBuf *x : b) x->release();
+    }
+};
+
+void ready_destroy(accord_store *s)
+{
+    for (ReadyGen *r : s->rdy_gens) { r->release(); delete r; }
+    s->rdy_gens.clear();
+    s->rdy_waiting = 0;
+}
+
+// the last computed batch (its WaitingOn just initialised) joins the waiting set
+int32_t ready_track_batch(accord_store *s)
+{
+    const uint32_t n = s->n;
+    if (n == 0) return ACCORD_OK;
+    hipStream_t st = s->stream;
+    ReadyGen *r = new (std::nothrow) ReadyGen();
+    if (!r) return fail(s, ACCORD_ERR_OOM, "out of host memory");
+    s->rdy_gens.push_back(r);
+    r->n = r->left = n;
+    r->words = s->wo_words_total;
+    const size_t n1 = (size_t)n + 1;
+    auto copy = [&](DevBuf &dst, const DevBuf &src, size_t bytes) -> hipError_t {
+        hipError_t e = dst.ensure(bytes + 8);
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst.p, src.p, bytes, hipMemcpyDeviceToDevice, st);
+        return e;
+    };
+    HIPCHECK(s, copy(r->g, s->txn_index, (size_t)n * 4));    // resident stores: global positions
+    HIPCHECK(s, hipMemcpyAsync(&r->glo, s->txn_index.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipMemcpyAsync(&r->ghi, s->txn_index.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, copy(r->lsb, s->lsb, (size_t)n * 8));
+    HIPCHECK(s, copy(r->rd_off, s->rd_val_off, n1 * 4));
+    HIPCHECK(s, copy(r->rd_vals, s->rd_vals, s->tot_rvals * 4));
+    HIPCHECK(s, copy(r->key_off, s->kd_key_off, n1 * 4));
+    HIPCHECK(s, copy(r->keys, s->kd_keys, s->tot_keys * 4));
+    HIPCHECK(s, copy(r->val_off, s->kd_val_off, n1 * 4));
+    HIPCHECK(s, copy(r->vals, s->kd_vals, s->tot_vals * 4));
+    HIPCHECK(s, copy(r->k2v_off, s->kd_k2v_off, n1 * 4));
+    HIPCHECK(s, copy(r->k2v, s->kd_k2v, s->tot_k2v * 4));
+    HIPCHECK(s, copy(r->wo_off, s->wo_off, n1 * 4));
+    HIPCHECK(s, copy(r->wo, s->wo_words, s->wo_words_total * 8));
+    HIPCHECK(s, copy(r->aoi, s->wo_aoi, s->wo_words_total * 8));
+    HIPCHECK(s, r->pend.ensure(s->tot_keys + 8));
+    HIPCHECK(s, r->until.ensure(s->tot_keys * 4 + 8));
+    HIPCHECK(s, r->done.ensure((size_t)n + 8));
+    HIPCHECK(s, hipMemsetAsync(r->pend.p, 0, s->tot_keys + 8, st));
+    HIPCHECK(s, hipMemsetAsync(r->done.p, 0, (size_t)n + 8, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    s->rdy_waiting += n;
+    return ACCORD_OK;
+}
+
+} // namespace accord_impl
+
+extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
+{
+    if (!s || !out) return fail(s, ACCORD_ERR_ARG, "null argument");
+    if (!accord_impl::registered_mode(s))
+        return fail(s, ACCORD_ERR_STATE, "accord_ready_update needs a registered-status store (resident, ACCORD_WINDOW_NONE)");
+    out->n = 0;
+    out->txn = nullptr;
+    out->waiting = s->rdy_waiting;
+    HIPCHECK(s, hipSetDevice(s->cfg.device));
+    hipStream_t st = s->stream;
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo, C = s->carry_n;
+    uint64_t cap = 0;
+    for (accord_impl::ReadyGen *r : s->rdy_gens) cap += r->n;
+    s->rdy_list.clear();
+    if (cap == 0) return ACCORD_OK;
+    HIPCHECK(s, s->rdy_kseg0.ensure((size_t)nkeys * 4 + 4));
+    HIPCHECK(s, s->rdy_kseg1.ensure((size_t)nkeys * 4 + 4));
+    HIPCHECK(s, s->rdy_sum.ensure((size_t)nkeys * sizeof(KeySummary) + 64));
+    HIPCHECK(s, s->rdy_out.ensure(cap * 4 + 64));
+    HIPCHECK(s, hipMemsetAsync(s->rdy_kseg0.p, 0, (size_t)nkeys * 4, st));
+    HIPCHECK(s, hipMemsetAsync(s->rdy_kseg1.p, 0, (size_t)nkeys * 4, st));
+    HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, 64, st));
+    if (s->rdy_kb_dirty) {
+        HIPCHECK(s, s->rdy_kb.ensure((size_t)nkeys * 4 + 4));
+        HIPCHECK(s, hipMemcpyAsync(s->rdy_kb.p, s->rdy_kb_host.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
+        s->rdy_kb_dirty = false;
+    }
+    StatusView v;
+    v.status = s->rg_status.as<uint8_t>();
+    v.emsb = s->rg_emsb.as<uint64_t>(); v.elsb = s->rg_elsb.as<uint64_t>(); v.enode = s->rg_enode.as<int32_t>();
+    v.known = s->rg_known;
+    if (C) hipLaunchKernelGGL(rd_seg_kernel, dim3(std::min<uint32_t>((C + 255) / 256, 8192u)), dim3(256), 0, st, C,
+                              s->cy_key.as<uint32_t>(), s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>());
+    if (nkeys) hipLaunchKernelGGL(rd_summary_kernel, dim3(grid_for_waves(nkeys)), dim3(256), 0, st, nkeys,
+                                  s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>(), s->cy_ent.as<uint32_t>(), v,
+                                  s->rdy_sum.as<KeySummary>());
+    uint32_t *cnt = s->rdy_out.as<uint32_t>(), *list = cnt + 16;
+    for (accord_impl::ReadyGen *r : s->rdy_gens) {
+        if (r->left == 0) continue;
+        ReadyParams p{};
+        p.n = r->n; p.key_lo = s->cfg.key_lo;
+        p.g = r->g.as<uint32_t>(); p.lsb = r->lsb.as<uint64_t>();
+        p.tmsb = s->rg_tmsb.as<uint64_t>(); p.tlsb = s->rg_tlsb.as<uint64_t>(); p.tnode = s->rg_tnode.as<int32_t>();
+        p.tg = s->rg_tg.as<uint32_t>(); p.tx_n = s->rg_tx_n;
+        p.rd_off = r->rd_off.as<uint32_t>(); p.rd_vals = r->rd_vals.as<uint32_t>();
+        p.key_off = r->key_off.as<uint32_t>(); p.keys = r->keys.as<uint32_t>();
+        p.val_off = r->val_off.as<uint32_t>(); p.vals = r->vals.as<uint32_t>();
+        p.k2v_off = r->k2v_off.as<uint32_t>(); p.k2v = r->k2v.as<int32_t>();
+        p.wo_off = r->wo_off.as<uint32_t>(); p.words = r->wo.as<unsigned long long>(); p.aoi = r->aoi.as<unsigned long long>();
+        p.pend = r->pend.as<uint8_t>(); p.until = r->until.as<uint32_t>(); p.done = r->done.as<uint8_t>();
+        p.out = list; p.out_cnt = cnt;
+        p.sum = s->rdy_sum.as<KeySummary>();
+        p.kb = s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
+        p.v = v;
+        hipLaunchKernelGGL(rd_eval_kernel, dim3(grid_for_waves(r->n)), dim3(256), 0, st, p);
+    }
+    HIPCHECK(s, hipGetLastError());
+    uint32_t nr = 0;
+    HIPCHECK(s, hipMemcpyAsync(&nr, cnt, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    s->rdy_list.resize(nr);
+    if (nr) {
+        HIPCHECK(s, hipMemcpyAsync(s->rdy_list.data(), list, (size_t)nr * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+        std::sort(s->rdy_list.begin(), s->rdy_list.end());
+    }
+    // generations drain in stream order: count each one's released txns, free the empty ones
+    size_t a = 0;
+    for (accord_impl::ReadyGen *r : s->rdy_gens) {
+        uint32_t c = 0;
+        while (a < s->rdy_list.size() && s->rdy_list[a] <= r->ghi) { c += s->rdy_list[a] >= r->glo; ++a; }
+        r->left -= c;
+    }
+    std::vector<accord_impl::ReadyGen *> keep;
+    for (accord_impl::ReadyGen *r : s->rdy_gens) {
+        if (r->left == 0) { r->release(); delete r; }
+        else keep.push_back(r);
+    }
+    s->rdy_gens.swap(keep);
+    s->rdy_waiting -= nr;
+    out->n = nr;
+    out->txn = s->rdy_list.data();
+    out->waiting = s->rdy_waiting;
+    return ACCORD_OK;
+}

@@ -19,40 +19,16 @@
 // truncated committed Write no longer bounds maxCommittedBefore, so nothing else can be dropped
 // without knowing the future events).
 #include "store_impl.h"
+#include "status_view.h"
 
 #include <algorithm>
 #include <vector>
 
 namespace {
 
-constexpr uint8_t ST_TK = 0, ST_PREACCEPTED = 2, ST_ACCEPTED = 3, ST_COMMITTED = 4, ST_APPLIED = 6, ST_INVALID = 7,
-                  ST_ERASED = 8;   // SaveStatus Erased / Invalidated: as INVALID for CFK, and off the range scan
+using namespace accord_status;
+
 constexpr uint32_t RC_KIND_ERASED = 7;  // carried range command kind no txn witnesses (masks use kinds 0..4)
-
-__device__ __forceinline__ bool committed(uint32_t st) { return st >= ST_COMMITTED && st <= ST_APPLIED; }
-
-struct Ts {
-    uint64_t msb, lsb;
-    int32_t node;
-};
-
-__device__ __forceinline__ int tcmp(const Ts &a, const Ts &b) { return ts_cmp(a.msb, a.lsb, a.node, b.msb, b.lsb, b.node); }
-
-struct StatusView {
-    const uint8_t *status;            // [next_global] InternalStatus by global position
-    const uint64_t *emsb, *elsb;      // executeAt by global position
-    const int32_t *enode;
-    uint32_t known;                   // positions >= known are this batch's txns: PREACCEPTED
-};
-
-__device__ __forceinline__ uint32_t status_of(const StatusView &v, uint32_t g)
-{
-    return g < v.known ? v.status[g] : ST_PREACCEPTED;
-}
-__device__ __forceinline__ Ts exec_of(const StatusView &v, uint32_t g)
-{
-    return Ts{v.emsb[g], v.elsb[g], v.enode[g]};
-}
 
 __device__ __forceinline__ void record_error(accord::DevStatus *st, uint32_t i, int32_t code)
 {
@@ -603,6 +579,10 @@ int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start
         if (start[e] < k && bound[e] != ACCORD_NO_TXN && bound[e] > 0) { kb[r] = bound[e]; any = true; }
     }
     if (!any) return ACCORD_OK;
+    // the readiness evaluation skips deps below each key's bound (ready.hip): a cumulative max
+    if (s->rdy_kb_host.size() != nkeys) s->rdy_kb_host.assign(nkeys, 0u);
+    for (uint32_t r = 0; r < nkeys; ++r) s->rdy_kb_host[r] = std::max(s->rdy_kb_host[r], kb[r]);
+    s->rdy_kb_dirty = true;
     hipStream_t st = s->stream;
     HIPCHECK(s, s->rg_kbound.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->carry_tmp.ensure(accord::carry_temp_bytes(C, nkeys)));

@@ -116,6 +116,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rc_end2, &s->rc_kind2, &s->rc_first,
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero};
     accord_impl::shard_comm_destroy(s);
+    accord_impl::ready_destroy(s);
     accord_impl::pinned_arena_destroy(s);
     for (DevBuf *b : bufs) b->release();
     for (DepSet &d : s->ds) d.release();
@@ -649,6 +650,8 @@ int32_t accord_store_reset(accord_store *s)
     s->ds_cur = -1; s->wo_done = false; s->mc_next = 0;
     // RedundantBefore.EMPTY (its bounds are positions of the old stream) and MaxConflicts.EMPTY
     s->rb_m = 0; s->rb_min_epoch = 0;
+    accord_impl::ready_destroy(s);
+    s->rdy_kb_host.clear(); s->rdy_kb_dirty = false; s->rdy_kb.release();
     if (s->mc_state.p) {
         HIPCHECK(s, hipSetDevice(s->cfg.device));
         HIPCHECK(s, hipMemsetAsync(s->mc_state.p, 0, s->mc_state.cap, s->stream));

@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 namespace accord_impl {
 
@@ -68,7 +69,7 @@ enum Stage { EV_START, EV_VALIDATE, EV_SORT, EV_SEGMENT, EV_COUNT, EV_SCAN, EV_F
              EV_OP_START, EV_OP_END, EV_C_RKCP, EV_C_RKN, EV_C_KDS, EV_C_RK, EV_COUNT_ALL };
 
 struct ShardComm;   // RCCL communicator + exchange buffers (shard.cpp)
-namespace accord_impl { struct PinnedBlock; void pinned_arena_destroy(accord_store *s); }
+namespace accord_impl { struct PinnedBlock; void pinned_arena_destroy(accord_store *s); struct ReadyGen; }
 
 struct accord_store {
     accord_store_cfg cfg{};
@@ -152,6 +153,13 @@ struct accord_store {
     uint64_t rb_min_epoch = 0;
     DevBuf rb_start, rb_end, rb_bound, rb_sep, rb_eep, rb_cnt, rb_zero;
     DepSet rb_set;
+    // execution readiness (ready.hip): the waiting set, one generation per initialised batch
+    std::vector<accord_impl::ReadyGen *> rdy_gens;
+    uint64_t rdy_waiting = 0;
+    DevBuf rdy_kseg0, rdy_kseg1, rdy_sum, rdy_out, rdy_kb;
+    std::vector<uint32_t> rdy_kb_host;       // per key: shardRedundantBefore as a position (cumulative max)
+    bool rdy_kb_dirty = false;
+    std::vector<uint32_t> rdy_list;          // the last accord_ready_update's ready txns
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
     accord_impl::PinnedBlock *dl_arena = nullptr;   // page-locked host arena of accord_deps_download
@@ -178,6 +186,9 @@ int32_t status_join_batch(accord_store *s);
 int32_t status_range_keys(accord_store *s, const accord::RangeDepsParams &rp, bool fill);
 int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned long long *words,
                                unsigned long long *aoi);
+// execution readiness (ready.hip)
+int32_t ready_track_batch(accord_store *s);
+void ready_destroy(accord_store *s);
 // RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp)
 int32_t redundant_apply(accord_store *s);
 }

@@ -139,7 +139,7 @@ int32_t accord_waiting_on_initialise(accord_store *s)
     s->max_level = 0;
     s->wo_has_aoi = true;
     s->wo_done = true;
-    return ACCORD_OK;
+    return accord_impl::ready_track_batch(s);      // the batch joins the waiting set (ready.hip)
 }
 
 int32_t accord_waiting_on_download(accord_store *s, accord_waiting_on *out)

@@ -406,6 +406,37 @@ int32_t accord_waiting_on_compute(accord_store *store);                 /* devic
  * max_level = 0, preds_total = 0 (levelling is accord_waiting_on_compute's model).  Download with
  * accord_waiting_on_download (applied_or_invalidated set). */
 int32_t accord_waiting_on_initialise(accord_store *store);
+
+/* ---- execution readiness: CommandsForKey.notify / notifyUnmanaged and
+ * Commands.updateWaitingOn on the device ----
+ * accord_waiting_on_initialise also puts the batch's txns into the store's waiting set (with a copy
+ * of their deps).  accord_ready_update re-evaluates every waiting txn against the statuses registered
+ * so far (accord_txn_register) and returns the txns that became ReadyToExecute (Commands.maybeExecute,
+ * local/Commands.java:656-733: no WaitingOn bit left and status STABLE), ascending global positions;
+ * they leave the set (the caller executes them and registers them APPLIED, which in turn releases
+ * their dependents at a later call).  Per waiting txn:
+ *   range-dep bits   Commands.updateWaitingOn (:769-830) as in accord_waiting_on_initialise;
+ *   key bits, managed txns (key domain, globally visible; STABLE): CommandsForKey.notify's test
+ *                    (local/CommandsForKey.java:1512-1635) expectMissingCount == |missing|: no
+ *                    unapplied committed txn of a kind it witnesses executes before it on the key and
+ *                    none of its deps on the key is uncommitted;
+ *   key bits, unmanaged txns (range domain, EphemeralRead; hasBeen Stable): registerUnmanaged
+ *                    (:1406-1498), COMMIT records re-evaluated by updatePending once minUncommitted
+ *                    passes them (:1315-1360), APPLY records released by notifyUnmanaged(APPLY,
+ *                    next.executeAt) (:1264-1283).
+ * The reference evaluates these tests when an event reaches the key (notifyAndUpdatePending,
+ * :1163-1215); every call here evaluates them for every waiting txn, so a txn is reported at the first
+ * call at which its test holds.  Not modelled: removeRedundantDependencies (bootstrap / stale ranges,
+ * local/CommandStore.java:601-678) and executeAtLeast; setAppliedAndPropagate's propagation is implied
+ * by the store-wide statuses (a propagated txn is APPLIED / invalidated here already).
+ * `txn` stays valid until the next call on the store; `waiting` = txns still in the set. */
+typedef struct {
+    uint32_t  n;
+    uint32_t  reserved;
+    uint64_t  waiting;
+    const uint32_t *txn;        /* [n] ascending global positions */
+} accord_ready;
+int32_t accord_ready_update(accord_store *store, accord_ready *out);
 int32_t accord_waiting_on_download(accord_store *store, accord_waiting_on *out);
 void    accord_waiting_on_release(accord_waiting_on *wo);
 /* device ms of the last accord_waiting_on_compute: bitsets, reduced predecessors, levelling */

@@ -1898,7 +1898,12 @@ struct or_lstore {
      * the command's ranges (CSR by global position) and whether its SaveStatus reached Erased */
     uint32_t *roff, *rst, *ren;
     uint32_t nr, rcap;
+    /* execution readiness: the txns whose WaitingOn was initialised and that are not ready yet */
+    struct or_waiter *wt;
+    uint32_t nwt, cwt;
 };
+
+static void or_lstore_waiters_free(or_lstore *s);
 
 or_lstore *or_lstore_create(uint32_t nkeys)
 {
@@ -1918,6 +1923,7 @@ void or_lstore_free(or_lstore *s)
     if (s->cfks) for (uint32_t k = 0; k < s->nkeys; ++k) { free(s->cfks[k].txns); free(s->cfks[k].committed); }
     free(s->cfks); free(s->tbl); free(s->koff); free(s->kord); free(s->status); free(s->exec);
     free(s->roff); free(s->rst); free(s->ren);
+    or_lstore_waiters_free(s);
     free(s);
 }
 
@@ -2179,6 +2185,230 @@ int or_lstore_truncate(or_lstore *s, uint32_t m, const uint32_t *start, const ui
     return 0;
 }
 
+
+/* ------------------------------------------------------------------------------------------
+ * Execution readiness of a registered-status store: the WaitingOn of every
+ * txn whose WaitingOn was initialised (Commands.initialiseWaitingOn, local/Commands.java:735-753),
+ * cleared as the store's statuses change, until the txn is ReadyToExecute (maybeExecute, :656-733).
+ * Each or_lstore_ready call evaluates, against the current CommandsForKey state, the tests the
+ * reference evaluates when an event reaches a key:
+ *  - range-dep bits: Commands.updateWaitingOn (:769-830) for every dep that hasBeen(PreCommitted);
+ *  - key bits of managed txns (key domain, globally visible; STABLE): CommandsForKey.notify's count
+ *    test (local/CommandsForKey.java:1512-1635): expectMissingCount (unapplied committed txns before
+ *    the txn's executeAt in committed[] plus uncommitted txns with a lower TxnId, by the kinds it
+ *    witnesses) == |missing| (the uncommitted txns it witnesses with TxnId < executeAt that its
+ *    deps lack: computeInfoAndAdditions :1071-1140, committed ones elided :1103-1109);
+ *  - key bits of unmanaged txns (range domain, EphemeralRead; hasBeen Stable):
+ *    registerUnmanaged (:1406-1498) once, then updatePending on a COMMIT record whose waitingUntil
+ *    precedes minUncommitted (:1243-1262, :1315-1360) and the APPLY release of notifyUnmanaged
+ *    (:1264-1283) with next / minUncommitted as the constructor derives them (:422-470).
+ * The reference evaluates these tests when an event reaches the key (notifyAndUpdatePending,
+ * :1163-1215); here they are evaluated for every waiting txn at every call (a txn is released at
+ * the first call at which its test holds).  Ready = no bit left and status STABLE.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct or_waiter {
+    uint32_t g, nr, nk;
+    uint32_t *rdeps;             /* [nr] RangeDeps txnIds (positions) */
+    uint32_t *keys;              /* [nk] KeyDeps keys */
+    uint32_t *kdoff, *kdeps;     /* per key its KeyDeps txnIds (positions, ascending) */
+    uint64_t *words, *aoi;       /* WaitingOn bits: [0, nr) txnIds, [nr, nr + nk) keys */
+    uint8_t *pend;               /* per key (unmanaged): 0 unregistered, 1 COMMIT, 2 APPLY, 3 released */
+    uint32_t *until;             /* per key: the waitingUntil txn (position) */
+} or_waiter;
+
+static void or_lstore_waiters_free(or_lstore *s)
+{
+    for (uint32_t w = 0; w < s->nwt; ++w) {
+        or_waiter *x = &s->wt[w];
+        free(x->rdeps); free(x->keys); free(x->kdoff); free(x->kdeps); free(x->words); free(x->aoi);
+        free(x->pend); free(x->until);
+    }
+    free(s->wt);
+    s->wt = NULL; s->nwt = s->cwt = 0;
+}
+
+int or_lstore_waiting_add(or_lstore *s, uint32_t base, const or_deps *d, uint32_t n)
+{
+    if (s->nwt + n > s->cwt) {
+        uint32_t c = s->cwt ? s->cwt : 1024;
+        while (c < s->nwt + n) c *= 2;
+        or_waiter *nw = (or_waiter *)realloc(s->wt, (size_t)c * sizeof(or_waiter));
+        if (!nw) return -1;
+        s->wt = nw; s->cwt = c;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        or_waiter *x = &s->wt[s->nwt];
+        memset(x, 0, sizeof(*x));
+        x->g = base + i;
+        x->nr = d->rd_val_off[i + 1] - d->rd_val_off[i];
+        x->nk = d->kd_key_off[i + 1] - d->kd_key_off[i];
+        const uint32_t nw = (x->nr + x->nk + 63) / 64;
+        const int32_t *k2v = d->kd_k2v + d->kd_k2v_off[i];
+        const uint32_t body = d->kd_k2v_off[i + 1] - d->kd_k2v_off[i] - x->nk;
+        x->rdeps = (uint32_t *)malloc(((size_t)x->nr + 1) * 4);
+        x->keys = (uint32_t *)malloc(((size_t)x->nk + 1) * 4);
+        x->kdoff = (uint32_t *)malloc(((size_t)x->nk + 1) * 4);
+        x->kdeps = (uint32_t *)malloc(((size_t)body + 1) * 4);
+        x->words = (uint64_t *)calloc(nw + 1, 8);
+        x->aoi = (uint64_t *)calloc(nw + 1, 8);
+        x->pend = (uint8_t *)calloc((size_t)x->nk + 1, 1);
+        x->until = (uint32_t *)calloc((size_t)x->nk + 1, 4);
+        if (!x->rdeps || !x->keys || !x->kdoff || !x->kdeps || !x->words || !x->aoi || !x->pend || !x->until) return -1;
+        for (uint32_t j = 0; j < x->nr; ++j) x->rdeps[j] = d->rd_vals[d->rd_val_off[i] + j];
+        x->kdoff[0] = 0;
+        for (uint32_t q = 0; q < x->nk; ++q) {
+            x->keys[q] = d->kd_keys[d->kd_key_off[i] + q];
+            const uint32_t b = q == 0 ? x->nk : (uint32_t)k2v[q - 1], e = (uint32_t)k2v[q];
+            for (uint32_t y = b; y < e; ++y) x->kdeps[x->kdoff[q] + (y - b)] = d->kd_vals[d->kd_val_off[i] + (uint32_t)k2v[y]];
+            x->kdoff[q + 1] = x->kdoff[q] + (e - b);
+        }
+        for (uint32_t b = 0; b < x->nr + x->nk; ++b) x->words[b / 64] |= 1ULL << (b & 63);
+        ++s->nwt;
+    }
+    return 0;
+}
+
+uint32_t or_lstore_waiting(const or_lstore *s) { return s->nwt; }
+
+static inline int w_test(const uint64_t *w, uint32_t b) { return (int)((w[b / 64] >> (b & 63)) & 1u); }
+static inline void w_clear(uint64_t *w, uint32_t b) { w[b / 64] &= ~(1ULL << (b & 63)); }
+
+/* the CommandsForKey constructor's minUncommitted and next (local/CommandsForKey.java:432-461):
+ * positions, or -1 */
+static void cfk_next(const cfk_t *c, long *min_unc, long *next)
+{
+    *min_unc = -1; *next = -1;
+    const txninfo_t *best = NULL;
+    for (uint32_t i = 0; i < c->n; ++i) {
+        const txninfo_t *t = &c->txns[i];
+        if (t->status == S_INVALID_OR_TRUNCATED) continue;
+        if (t->status >= S_COMMITTED) {
+            if (t->status < S_APPLIED && (!best || ts_cmp(&best->execute_at, &t->execute_at) > 0)) best = t;
+        } else if (*min_unc < 0) *min_unc = t->txn;
+    }
+    if (best) *next = best->txn;
+    /* next is nulled when minUncommitted precedes its executeAt (:454-455) */
+    (void)0;
+}
+
+/* registerUnmanaged (:1406-1498) / updatePending (:1315-1360) over the deps of one key: returns 1 =
+ * ready, 0 = pending APPLY (*until = the relevant dep executing last), -1 = pending COMMIT (*until =
+ * the last dep), for a waiter at executeAt ex; `reg` = registration (uncommitted deps -> COMMIT) */
+static int unmanaged_eval(const or_lstore *s, const cfk_t *c, const or_waiter *x, uint32_t q, const ts_t *ex,
+                          int only_deps, int reg, uint32_t *until)
+{
+    const uint32_t *dl = x->kdeps + x->kdoff[q];
+    const uint32_t nd = x->kdoff[q + 1] - x->kdoff[q];
+    uint32_t i = 0;
+    while (i < nd && dl[i] < c->redundant_before) ++i;          /* txnIds.find(shardRedundantBefore) */
+    if (i >= nd) return 1;
+    int ready = 1, to_apply = 1;
+    long best = -1;
+    for (; i < nd; ++i) {
+        const long j = cfk_search(c, s->tbl, &s->tbl[dl[i]]);
+        if (j < 0) { ready = to_apply = 0; continue; }          /* missing from this CFK */
+        const txninfo_t *t = &c->txns[j];
+        if (reg && t->status < S_COMMITTED) { ready = to_apply = 0; continue; }
+        if (only_deps || ts_cmp(&t->execute_at, ex) < 0) {
+            ready &= t->status >= S_APPLIED;
+            if (best < 0 || ts_cmp(&s->exec[best], &t->execute_at) < 0) best = t->txn;
+        }
+    }
+    if (ready) return 1;
+    if (to_apply) { *until = best < 0 ? dl[nd - 1] : (uint32_t)best; return 0; }
+    *until = dl[nd - 1];
+    return -1;
+}
+
+int or_lstore_ready(or_lstore *s, uint32_t *ready_out, uint32_t *nready)
+{
+    uint32_t nout = 0, keep = 0;
+    for (uint32_t w = 0; w < s->nwt; ++w) {
+        or_waiter *x = &s->wt[w];
+        const uint32_t g = x->g;
+        const uint8_t st = s->status[g];
+        const int kind = kind_of(s->tbl[g].lsb), rdom = domain_of(s->tbl[g].lsb);
+        const int only_deps = kind == K_EXCL_SYNC_POINT || kind == K_EPHEMERAL_READ;   /* awaitsOnlyDeps */
+        const ts_t *ex = &s->exec[g];
+        /* range-dep bits: Commands.updateWaitingOn (forEachWaitingOnId: reverse order) */
+        for (uint32_t j = x->nr; j-- > 0;) {
+            if (!w_test(x->words, j)) continue;
+            const uint32_t dg = x->rdeps[j];
+            const uint8_t ds = s->status[dg];
+            if (ds < S_COMMITTED) continue;                     /* !hasBeen(PreCommitted) */
+            if (ds >= S_INVALID_OR_TRUNCATED) { w_clear(x->words, j); if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63); }
+            else if (!only_deps && ts_cmp(&s->exec[dg], ex) > 0) w_clear(x->words, j);
+            else if (ds == S_APPLIED) { w_clear(x->words, j); if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63); }
+        }
+        const int managed = rdom == 0 && is_globally_visible(kind) == 1;
+        for (uint32_t q = 0; q < x->nk; ++q) {
+            const uint32_t b = x->nr + q;
+            if (!w_test(x->words, b)) continue;
+            const cfk_t *c = &s->cfks[x->keys[q]];
+            if (managed) {
+                if (st != S_STABLE) continue;
+                /* CommandsForKey.notify's test for this txn on this key */
+                const int wk = witnesses_of(kind);
+                uint32_t expect = 0, missing = 0;
+                for (uint32_t a = 0; a < c->nc; ++a) {              /* committed[], executeAt order */
+                    const txninfo_t *t = &c->txns[c->committed[a]];
+                    if (ts_cmp(&t->execute_at, ex) >= 0) break;
+                    if (t->status == S_APPLIED) continue;
+                    if (kinds_test(wk, kind_of(s->tbl[t->txn].lsb))) ++expect;
+                }
+                const uint32_t *dl = x->kdeps + x->kdoff[q];
+                const uint32_t nd = x->kdoff[q + 1] - x->kdoff[q];
+                for (uint32_t a = 0; a < c->n; ++a) {               /* backfill: uncommitted, TxnId order */
+                    const txninfo_t *t = &c->txns[a];
+                    if (ts_cmp(&s->tbl[t->txn], ex) >= 0) break;
+                    if (t->status >= S_COMMITTED || t->txn == g) continue;
+                    if (!kinds_test(wk, kind_of(s->tbl[t->txn].lsb))) continue;
+                    ++expect;
+                    uint32_t lo = 0, hi = nd;                        /* in its deps? */
+                    while (lo < hi) { uint32_t m = (lo + hi) / 2; if (dl[m] < t->txn) lo = m + 1; else hi = m; }
+                    if (!(lo < nd && dl[lo] == t->txn)) ++missing;
+                }
+                if (expect == missing) w_clear(x->words, b);
+                continue;
+            }
+            if (st < S_STABLE || st >= S_INVALID_OR_TRUNCATED) continue;   /* hasBeen(Stable), not truncated */
+            if (x->pend[q] == 0) {                                   /* registerUnmanaged */
+                const int r = unmanaged_eval(s, c, x, q, ex, only_deps, 1, &x->until[q]);
+                if (r == 1) { x->pend[q] = 3; w_clear(x->words, b); continue; }
+                x->pend[q] = r == 0 ? 2 : 1;
+            }
+            long min_unc, next;
+            cfk_next(c, &min_unc, &next);
+            if (next >= 0 && min_unc >= 0 && ts_cmp(&s->tbl[min_unc], &s->exec[next]) < 0) next = -1;
+            if (x->pend[q] == 1 && (min_unc < 0 || (uint32_t)min_unc > x->until[q])) {   /* COMMIT -> updatePending */
+                const int r = unmanaged_eval(s, c, x, q, ex, only_deps, 0, &x->until[q]);
+                if (r == 1) { x->pend[q] = 3; w_clear(x->words, b); continue; }
+                x->pend[q] = 2;
+            }
+            if (x->pend[q] == 2 && (min_unc < 0 || next >= 0)) {      /* notifyUnmanaged(APPLY, next) */
+                if (next < 0 || ts_cmp(&s->exec[x->until[q]], &s->exec[next]) < 0) { x->pend[q] = 3; w_clear(x->words, b); }
+            }
+        }
+        int waiting = 0;
+        for (uint32_t a = 0; a < (x->nr + x->nk + 63) / 64; ++a) waiting |= x->words[a] != 0;
+        if (!waiting && st == S_STABLE) {
+            ready_out[nout++] = g;
+            free(x->rdeps); free(x->keys); free(x->kdoff); free(x->kdeps); free(x->words); free(x->aoi);
+            free(x->pend); free(x->until);
+            continue;
+        }
+        s->wt[keep++] = *x;
+    }
+    s->nwt = keep;
+    /* ascending positions */
+    for (uint32_t a = 1; a < nout; ++a) {
+        uint32_t v = ready_out[a], b = a;
+        while (b > 0 && ready_out[b - 1] > v) { ready_out[b] = ready_out[b - 1]; --b; }
+        ready_out[b] = v;
+    }
+    *nready = nout;
+    return 0;
+}
 
 /* ------------------------------------------------------------------------------------------
  * RedundantBefore.collectDeps (local/RedundantBefore.java:418-421) = ReducingRangeMap.foldl

@@ -109,6 +109,14 @@ uint32_t   or_lstore_size(const or_lstore *s);
  * status events for a dropped txn no longer reach that key. */
 int        or_lstore_truncate(or_lstore *s, uint32_t m, const uint32_t *start, const uint32_t *end,
                               const uint32_t *bound);
+/* Execution readiness (see oracle.c): the n txns at positions base.. join the
+ * waiting set with their deps d (values = positions, as or_lstore_batch returns them) and every
+ * WaitingOn bit set; or_lstore_ready re-evaluates every waiting txn against the current state and
+ * returns (ascending) the txns that became ReadyToExecute -- no bit left, status STABLE -- which
+ * leave the set. */
+int        or_lstore_waiting_add(or_lstore *s, uint32_t base, const or_deps *d, uint32_t n);
+int        or_lstore_ready(or_lstore *s, uint32_t *ready_out, uint32_t *nready);
+uint32_t   or_lstore_waiting(const or_lstore *s);
 
 /* ---- primitives restated for the reference's own property tests ---- */
 

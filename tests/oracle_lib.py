@@ -473,6 +473,10 @@ class LStore:
             L.or_lstore_size.argtypes = [C.c_void_p]
             L.or_lstore_size.restype = C.c_uint32
             L.or_lstore_truncate.argtypes = [C.c_void_p, C.c_uint32, _u32p, _u32p, _u32p]
+            L.or_lstore_waiting_add.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_OrDeps), C.c_uint32]
+            L.or_lstore_ready.argtypes = [C.c_void_p, _u32p, _u32p]
+            L.or_lstore_waiting.argtypes = [C.c_void_p]
+            L.or_lstore_waiting.restype = C.c_uint32
             L._lstore_typed = True
         self._h = L.or_lstore_create(nkeys)
 
@@ -497,6 +501,29 @@ class LStore:
             return _to_partial(d)
         finally:
             lib().or_deps_free(C.byref(d))
+
+    def waiting_add(self, base: int, p: PartialDeps):
+        """The txns at positions base.. (deps p, positions as values) join the waiting set with every
+        WaitingOn bit set (or_lstore_waiting_add)."""
+        d, keep = _c_deps(p)
+        rc = lib().or_lstore_waiting_add(self._h, base, C.byref(d), p.n)
+        if rc != 0:
+            raise OracleError(rc)
+
+    def ready(self):
+        """Execution readiness (or_lstore_ready): the waiting txns that became ReadyToExecute,
+        ascending positions; they leave the set."""
+        w = lib().or_lstore_waiting(self._h)
+        out = np.zeros(max(1, w), np.uint32)
+        cnt = np.zeros(1, np.uint32)
+        rc = lib().or_lstore_ready(self._h, out.ctypes.data_as(_u32p), cnt.ctypes.data_as(_u32p))
+        if rc != 0:
+            raise OracleError(rc)
+        return out[:int(cnt[0])].copy()
+
+    @property
+    def waiting(self) -> int:
+        return lib().or_lstore_waiting(self._h)
 
     def truncate(self, start, end, bound):
         """CommandsForKey.withRedundantBefore on every key of the map's entries (oracle.h)."""
