@@ -82,6 +82,11 @@ def main():
     ap.add_argument("--registered", action="store_true",
                     help="also time the registered-status store (real status events, no status-at-time model) "
                          "on the config-2 stream fed in batches (registered_batches)")
+    ap.add_argument("--ready", action="store_true",
+                    help="also time execution readiness (accord_ready_update) over a registered-status "
+                         "schedule: batches registered STABLE, ready txns registered APPLIED round by round")
+    ap.add_argument("--ready-batch", type=int, default=4096, help="txns per batch of the --ready leg")
+    ap.add_argument("--ready-batches", type=int, default=16, help="batches of the --ready leg")
     ap.add_argument("--reg-batch", type=int, default=1024, help="txns per batch of the --registered leg")
     ap.add_argument("--reg-batches", type=int, default=64, help="batches of the --registered leg")
     args = ap.parse_args()
@@ -213,12 +218,15 @@ def main():
     boundary = None
     resident = None
     registered = None
+    ready = None
     if world == 1 and not args.waiting_on:
         boundary = boundary_rate(store, s)
         if s.rng_off[-1] == 0 and args.resident:
             resident = resident_split(s, args, stage["total"])
         if s.rng_off[-1] == 0 and args.registered:
             registered = registered_batches(s, args)
+        if s.rng_off[-1] == 0 and args.ready:
+            ready = ready_schedule(s, args)
 
     if rank != 0:
         store.close()
@@ -283,6 +291,8 @@ def main():
         line["resident_batches"] = resident
     if registered is not None:
         line["registered_batches"] = registered
+    if ready is not None:
+        line["readiness"] = ready
     print(json.dumps(line))
     store.close()
     if dist is not None:
@@ -441,6 +451,62 @@ def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
             if sat["fill_ms_per_batch"] else None,
             "device_ratio_vs_status_at_time": (reg["device_ms_per_batch"] / sat["device_ms_per_batch"])
             if sat["device_ms_per_batch"] else None}
+
+
+ST_STABLE = 5
+
+
+def ready_schedule(s, args, rounds_per_batch=4):
+    """Execution readiness (include/accord_deps.h accord_ready_update) over the
+    first ready_batches x ready_batch txns of the stream in a registered-status store: per batch the
+    deps are computed, the batch is registered STABLE at executeAt = TxnId and its WaitingOn
+    initialised (the txns join the waiting set), then up to rounds_per_batch rounds of
+    accord_ready_update -> the ready txns registered APPLIED; finally the set is drained.  Reports the
+    wall time of the ready_update calls (device summaries + evaluation + one host read) against the
+    txns they released."""
+    from accord_amd import CommandStore, WINDOW_NONE
+    bsz, nb = args.ready_batch, min(args.ready_batches, s.n // args.ready_batch)
+    upd_ms, app_ms, calls, released, rounds = 0.0, 0.0, 0, 0, 0
+
+    def rnd(st):
+        nonlocal upd_ms, app_ms, calls, released, rounds
+        t0 = time.perf_counter()
+        ready, waiting = st.ready_update()
+        upd_ms += (time.perf_counter() - t0) * 1e3
+        calls += 1
+        if ready.size:
+            released += ready.size
+            rounds += 1
+            t1 = time.perf_counter()
+            st.register(s.msb[ready], s.lsb[ready], s.node[ready], np.full(ready.size, ST_APPLIED, np.uint8),
+                        s.msb[ready], s.lsb[ready], s.node[ready])
+            app_ms += (time.perf_counter() - t1) * 1e3
+        return ready.size, waiting
+
+    with CommandStore(device=0, key_lo=0, key_hi=args.keyspace, window=WINDOW_NONE, resident=True) as st:
+        for b in range(nb):
+            lo, hi = b * bsz, (b + 1) * bsz
+            st.upload(s.slice(lo, hi))
+            st.compute()
+            idx = np.arange(lo, hi)
+            st.register(s.msb[idx], s.lsb[idx], s.node[idx], np.full(bsz, ST_STABLE, np.uint8),
+                        s.msb[idx], s.lsb[idx], s.node[idx])
+            st.waiting_on_initialise()
+            for _ in range(rounds_per_batch):
+                if rnd(st)[0] == 0:
+                    break
+        waiting = 1
+        for _ in range(100000):
+            r, waiting = rnd(st)
+            if r == 0:
+                break
+    return {"schedule": f"{nb} batches x {bsz} txns of the config-2 stream, registered-status store: each batch "
+                        f"STABLE (executeAt = TxnId) and initialised, <= {rounds_per_batch} ready -> APPLIED rounds "
+                        f"per batch, then drained",
+            "txns": nb * bsz, "released": released, "left_waiting": waiting, "update_calls": calls,
+            "release_rounds": rounds, "update_ms_per_call": upd_ms / max(1, calls),
+            "released_txns_per_s_update_wall": released / (upd_ms * 1e-3) if upd_ms else None,
+            "apply_register_ms_total": app_ms}
 
 
 def measured_traffic(config):

@@ -58,19 +58,11 @@ struct GenParams {
     uint32_t *hist2;
     uint32_t ext_base;                // first extension position of hist2
     StatusView v;
+    // committed[] index of the Writes (cw_*): cw_off[x] = committed Writes before history position x,
+    // cw_pos[j] = the j-th one's position, cw_pm[j] = the one with the latest executeAt among its key's
+    // up to j (CommandsForKey.committed, local/CommandsForKey.java:462-469)
+    const uint32_t *cw_off, *cw_pos, *cw_pm;
 };
-
-// wave-wide max of a Timestamp (lanes without one hold has = false)
-__device__ __forceinline__ void wave_ts_max(Ts &m, bool &has)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const Ts o{(uint64_t)__shfl_xor((long long)m.msb, d, 64), (uint64_t)__shfl_xor((long long)m.lsb, d, 64),
-                   __shfl_xor(m.node, d, 64)};
-        const bool oh = __shfl_xor(has ? 1 : 0, d, 64) != 0;
-        if (oh && (!has || tcmp(o, m) > 0)) { m = o; has = true; }
-    }
-}
 
 // One pair, one wave (lanes stride over the pair's slice [lo, pos) of the key's history):
 //   maxCommittedBefore = max executeAt over committed Writes with executeAt < startedBefore (:620-624)
@@ -95,18 +87,19 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q, uint32_
     }
     const uint32_t self = p.txn_index[t];
     const uint32_t lo = sl.lo, hi = sl.pos;
+    // maxCommittedBefore (:620-624): the latest executeAt before startedBefore among the key's committed
+    // Writes before the bound, walked back from the last one; the running argmax (cw_pm) ends the walk
+    // as soon as no earlier Write can beat the best found (usually the first step: executeAts follow
+    // TxnId order but for the few still executing after startedBefore)
     bool has_mcb = false;
     Ts mcb{0, 0, 0};
-    for (uint32_t x = lo + lane; x < hi; x += 64) {
-        const uint32_t e = p.hist[x], g = e & ENT_TXN_MASK;
-        if ((e >> ENT_KIND_SHIFT) != 1u) continue;    // Writes only
-        const uint32_t st = status_of(p.v, g);
-        if (!committed(st)) continue;
-        const Ts ex = exec_of(p.v, g);
-        if (tcmp(ex, sb) >= 0) continue;
-        if (!has_mcb || tcmp(ex, mcb) > 0) { mcb = ex; has_mcb = true; }
+    for (uint32_t j = p.cw_off[hi], j0 = p.cw_off[lo]; j > j0; --j) {   // wave-uniform
+        const Ts best = exec_of(p.v, p.hist[p.cw_pos[p.cw_pm[j - 1]]] & ENT_TXN_MASK);
+        if (has_mcb && tcmp(best, mcb) <= 0) break;
+        if (tcmp(best, sb) < 0) { mcb = best; has_mcb = true; break; }
+        const Ts ex = exec_of(p.v, p.hist[p.cw_pos[j - 1]] & ENT_TXN_MASK);
+        if (tcmp(ex, sb) < 0 && (!has_mcb || tcmp(ex, mcb) > 0)) { mcb = ex; has_mcb = true; }
     }
-    wave_ts_max(mcb, has_mcb);
     // what the fill kernels keep of a history entry (kind witnessed, not the txn itself)
     auto witnessed = [&](uint32_t e) { return ((wmask >> (e >> ENT_KIND_SHIFT)) & 1u) && (e & ENT_TXN_MASK) != self; };
     auto emitted = [&](uint32_t e) -> bool {
@@ -152,6 +145,57 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q, uint32_
         c += (uint32_t)__popcll(b);
     }
     if (lane == 0) p.slice[q] = accord::PairSlice{out, out + c, c, sl.key};
+}
+
+// committed[] index of the Writes (see GenParams): flags, positions, running argmax by executeAt
+__global__ __launch_bounds__(256) void cw_flag_kernel(uint32_t P, const uint32_t *__restrict__ hist, StatusView v,
+                                                      uint32_t *__restrict__ flag)
+{
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x) {
+        const uint32_t e = hist[x];
+        flag[x] = (e >> ENT_KIND_SHIFT) == 1u && committed(status_of(v, e & ENT_TXN_MASK)) ? 1u : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void cw_scatter_kernel(uint32_t P, const uint32_t *__restrict__ flag,
+                                                         const uint32_t *__restrict__ off, uint32_t *__restrict__ pos)
+{
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x)
+        if (flag[x]) pos[off[x]] = x;
+}
+
+// a wave per key: cw_pm over the key's committed Writes, 64 at a time (wave max-scan by executeAt,
+// carrying the previous chunk's maximum)
+__global__ __launch_bounds__(256) void cw_pm_kernel(uint32_t nkeys, const uint32_t *__restrict__ seg_start,
+                                                    const uint32_t *__restrict__ seg_end, const uint32_t *__restrict__ off,
+                                                    const uint32_t *__restrict__ pos, const uint32_t *__restrict__ hist,
+                                                    StatusView v, uint32_t *__restrict__ pm)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t k = blockIdx.x * (blockDim.x / 64) + wave_id(); k < nkeys; k += waves) {
+        const uint32_t a = seg_start[k], c = seg_end[k];
+        if (c <= a) continue;
+        const uint32_t j0 = off[a], j1 = off[c];
+        uint32_t carry = 0xFFFFFFFFu;
+        Ts cex{0, 0, 0};
+        for (uint32_t b = j0; b < j1; b += 64) {
+            const uint32_t j = b + lane;
+            uint32_t m = j < j1 ? j : 0xFFFFFFFFu;
+            Ts ex = j < j1 ? exec_of(v, hist[pos[j]] & ENT_TXN_MASK) : Ts{0, 0, 0};
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t om = (uint32_t)__shfl_up((int)m, d, 64);
+                const Ts oe{(uint64_t)__shfl_up((long long)ex.msb, d, 64), (uint64_t)__shfl_up((long long)ex.lsb, d, 64),
+                            __shfl_up(ex.node, d, 64)};
+                if (lane >= (uint32_t)d && om != 0xFFFFFFFFu && (m == 0xFFFFFFFFu || tcmp(oe, ex) > 0)) { m = om; ex = oe; }
+            }
+            if (carry != 0xFFFFFFFFu && (m == 0xFFFFFFFFu || tcmp(cex, ex) > 0)) { m = carry; ex = cex; }
+            if (j < j1) pm[j] = m;
+            carry = readlane(m, 63);
+            cex = Ts{(uint64_t)__shfl((long long)ex.msb, 63, 64), (uint64_t)__shfl((long long)ex.lsb, 63, 64),
+                     __shfl(ex.node, 63, 64)};
+        }
+    }
 }
 
 // A wave per txn over its keys that hold a registered status: the count pass narrows contiguous
@@ -514,6 +558,21 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     g.slice = s->slice.as<accord::PairSlice>();
     g.gcnt = s->rg_gcnt.as<uint32_t>(); g.goff = s->rg_goff.as<uint32_t>();
     g.v = v;
+    {   // the committed[] index of the Writes over the combined history
+        HIPCHECK(s, s->rg_cwflag.ensure(((size_t)PH + 1) * 4));
+        HIPCHECK(s, s->rg_cwoff.ensure(((size_t)PH + 1) * 4));
+        HIPCHECK(s, s->rg_cwpos.ensure((size_t)PH * 4 + 4));
+        HIPCHECK(s, s->rg_cwpm.ensure((size_t)PH * 4 + 4));
+        uint32_t *flag = s->rg_cwflag.as<uint32_t>(), *off = s->rg_cwoff.as<uint32_t>();
+        hipLaunchKernelGGL(cw_flag_kernel, dim3(grid_for(PH)), dim3(256), 0, st, PH, s->hist.as<uint32_t>(), v, flag);
+        HostTotals *dv = s->status_totals.as<HostTotals>();
+        accord::exclusive_scan_u32(flag, off, PH, &dv->totals[9], s->scan_tmp.p, st);
+        hipLaunchKernelGGL(cw_scatter_kernel, dim3(grid_for(PH)), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>());
+        hipLaunchKernelGGL(cw_pm_kernel, dim3(std::min<uint32_t>((nkeys + 3) / 4, 8192u)), dim3(256), 0, st, nkeys,
+                           s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(), off, s->rg_cwpos.as<uint32_t>(),
+                           s->hist.as<uint32_t>(), v, s->rg_cwpm.as<uint32_t>());
+        g.cw_off = off; g.cw_pos = s->rg_cwpos.as<uint32_t>(); g.cw_pm = s->rg_cwpm.as<uint32_t>();
+    }
     const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);     // a wave per txn
     if (n) hipLaunchKernelGGL(general_kernel<false>, dim3(gw), dim3(256), 0, st, g);
     HostTotals *dev = s->status_totals.as<HostTotals>();

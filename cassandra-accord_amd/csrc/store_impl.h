@@ -112,7 +112,7 @@ struct accord_store {
     // (rg_t*, rg_tx_n entries, rg_tg = global position), InternalStatus + executeAt by global
     // position (rg_known positions), per-batch work
     DevBuf rg_tmsb, rg_tlsb, rg_tnode, rg_tg, rg_status, rg_emsb, rg_elsb, rg_enode;
-    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound;
+    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound, rg_cwflag, rg_cwoff, rg_cwpos, rg_cwpm;
     uint32_t rg_tx_n = 0, rg_known = 0;
     bool rg_flag_ok = false;       // rg_flag holds this batch's keys-with-registered-status flags
     // the uploaded batch: its carried-entry prefix, where it ends (global) and its last TxnId

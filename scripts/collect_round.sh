@@ -7,6 +7,8 @@ cp "$O/bench.json" "$P/bench_config2.json"
 cp "$O/bench_c5.json" "$P/bench_config5.json"
 cp "$O/bench_c3.json" "$P/bench_config3.json"
 [ -f "$O/bench_resident.json" ] && cp "$O/bench_resident.json" "$P/bench_config2_resident.json"
+[ -f "$O/bench_registered.json" ] && cp "$O/bench_registered.json" "$P/bench_config2_registered.json"
+[ -f "$O/prof_trace_c3/run_kernel_stats.csv" ] && cp "$O/prof_trace_c3/run_kernel_stats.csv" "$P/kernel_stats_config3.csv"
 cp "$O/prof_trace/run_kernel_stats.csv" "$P/kernel_stats_config2.csv"
 cp "$O/prof_trace_c5/run_kernel_stats.csv" "$P/kernel_stats_config5.csv"
 cp "$O/pytest_gpu.log" "$P/pytest_gpu.log"

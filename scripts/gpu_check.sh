@@ -7,5 +7,5 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 ${CPU:---no-cpu} > "$O/bench.json" 2> "$O/bench.err" && \
 { [ -z "$AB" ] || TAG=$TAG bash scripts/ab_libs.sh; } && \
 { [ -z "$LEGS" ] || { timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --resident > "$O/bench_resident.json" 2> "$O/bench_resident.err" && \
-  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --registered > "$O/bench_registered.json" 2> "$O/bench_registered.err"; }; }
+  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --registered --ready > "$O/bench_registered.json" 2> "$O/bench_registered.err"; }; }
 rc=$?; echo "rc=$rc"; tail -3 "$O/pytest_gpu.log"; exit $rc

@@ -9,9 +9,11 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 > "$O/bench.json" 2> "$O
 timeout -k 10 300 python bench.py --config 5 --steps 3 --warmup 1 > "$O/bench_c5.json" 2> "$O/bench_c5.err" && \
 timeout -k 10 300 python bench.py --config 3 --steps 5 --warmup 2 --no-cpu > "$O/bench_c3.json" 2> "$O/bench_c3.err" && \
 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --resident > "$O/bench_resident.json" 2> "$O/bench_resident.err" && \
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --registered --ready > "$O/bench_registered.json" 2> "$O/bench_registered.err" && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu > "$O/prof_trace.log" 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_trace_c5" -o run --output-format csv -- python3 "$R/bench.py" --config 5 --steps 2 --warmup 1 --no-cpu > "$O/prof_trace_c5.log" 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_trace_c3" -o run --output-format csv -- python3 "$R/bench.py" --config 3 --steps 3 --warmup 1 --no-cpu > "$O/prof_trace_c3.log" 2>&1 && \
 i=0 && \
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS" "SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS_ATOMIC"; do
   i=$((i+1))
