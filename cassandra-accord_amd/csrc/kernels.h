@@ -209,11 +209,14 @@ void launch_rangedeps_fill(const RangeDepsParams &p, hipStream_t s);
 constexpr uint32_t RK_CP_SHIFT = 12;
 size_t rangekeys_cp_bytes(uint32_t ncp, uint32_t nkeys);
 void launch_rangekeys_checkpoints(uint32_t PH, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s);
+// carried range command kind no txn witnesses (witness masks use kinds 0..4): an ACCORD_ST_ERASED one
+constexpr uint32_t RC_KIND_ERASED = 7;
 // resident stores: the range commands a later batch can still see (owner >= thr), carried and this
-// batch's, into the out arrays (a suffix of the candidate order); *kept = their number
+// batch's, into the out arrays (a suffix of the candidate order); *kept = their number.  flags /
+// offs (ncr + R + 1 words each, registered-status stores): also drop the erased ones (a flag scan).
 void launch_range_carry(const RangeDepsParams &p, uint32_t R, uint32_t thr, uint32_t *out_owner, uint32_t *out_start,
                         uint32_t *out_end, uint32_t *out_kind, uint32_t *first_tmp, unsigned long long *kept,
-                        hipStream_t s);
+                        uint32_t *flags, uint32_t *offs, void *scan_state, hipStream_t s);
 // keys of every range txn's ranges (clipped to the store), for the stored-slice offsets
 void launch_rangekeys_nkeys(const RangeDepsParams &p, uint32_t *cnt, hipStream_t s);
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s);

@@ -17,14 +17,19 @@ namespace accord {
 namespace {
 constexpr int RS_THREADS = 256;
 constexpr int RS_WAVES = RS_THREADS / 64;
-constexpr int RS_ITEMS = 16;
-constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
+// items per thread: 16 for large sorts; a sort too small to give every CU several tiles of 4096
+// (a resident store's batch) takes tiles of 1024 instead, so the grid still fills the chip
+constexpr int RS_ITEMS_MAX = 16;
+constexpr uint32_t RS_SMALL_N = 1u << 22;
+__host__ __device__ constexpr int rs_tile(int items) { return RS_THREADS * items; }
 constexpr int RS_MAX_BITS = 9;
 constexpr int RS_MAX_BINS = 1 << RS_MAX_BITS;
 
+template <int RS_ITEMS>
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint32_t *__restrict__ keys, uint32_t n, int shift,
                                                          uint32_t mask, uint32_t *__restrict__ hist, uint32_t tiles)
 {
+    constexpr int RS_TILE = rs_tile(RS_ITEMS);
     __shared__ uint32_t h[RS_MAX_BINS];
     const uint32_t tid = threadIdx.x, bins = mask + 1;
     for (uint32_t b = tid; b < bins; b += RS_THREADS) h[b] = 0;
@@ -43,7 +48,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep(const uint32_t *__restr
 // wave ballots against a wave-private running digit count in LDS -- no block barrier per round --
 // then one block scan of the digit totals places each wave's runs, the tile is re-ordered by digit
 // in LDS and written out as contiguous per-digit runs.
-template <int BITS>
+template <int BITS, int RS_ITEMS>
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                            const uint32_t *__restrict__ ein, uint32_t *__restrict__ eout,
@@ -51,6 +56,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
                                                            const uint32_t *__restrict__ offs, uint32_t tiles)
 {
     constexpr uint32_t BINS = 1u << BITS;       // LDS sizing; digits use the runtime mask (<= BINS-1)
+    constexpr int RS_TILE = rs_tile(RS_ITEMS);
     const uint32_t MASK = mask;
     __shared__ uint32_t s_keys[RS_TILE];
     __shared__ uint32_t s_vals[RS_TILE];
@@ -159,9 +165,12 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
 }
 } // namespace
 
+inline int rs_items(uint32_t n) { return n < RS_SMALL_N ? 4 : RS_ITEMS_MAX; }
+inline uint32_t rs_tiles(uint32_t n) { return (n + rs_tile(rs_items(n)) - 1) / rs_tile(rs_items(n)); }
+
 size_t radix_sort_temp_bytes(uint32_t n)
 {
-    uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
+    uint32_t tiles = rs_tiles(n);
     size_t hist = (size_t)RS_MAX_BINS * (tiles ? tiles : 1);
     size_t a = ((hist * 4 + (hist + 1) * 4) + 15) & ~(size_t)15;
     return a + 16;
@@ -169,7 +178,7 @@ size_t radix_sort_temp_bytes(uint32_t n)
 
 uint32_t radix_sort_scan_len(uint32_t n)
 {
-    uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
+    uint32_t tiles = rs_tiles(n);
     return (uint32_t)RS_MAX_BINS * (tiles ? tiles : 1);
 }
 
@@ -178,7 +187,8 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
                       uint32_t *ents_tmp, uint32_t n, int bits, void *temp, void *scan_state, hipStream_t s)
 {
     if (n == 0) return;
-    const uint32_t tiles = (n + RS_TILE - 1) / RS_TILE;
+    const uint32_t tiles = rs_tiles(n);
+    const bool small = rs_items(n) != RS_ITEMS_MAX;
     const size_t hist_cap = (size_t)RS_MAX_BINS * tiles;
     uint32_t *hist = (uint32_t *)temp;
     uint32_t *offs = hist + hist_cap;
@@ -197,12 +207,20 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
         uint32_t *vo = to_out ? vals_out : vals_tmp;
         uint32_t *eo = ents_in ? (to_out ? ents_out : ents_tmp) : nullptr;
         const size_t hist_n = (size_t)(mask + 1) * tiles;
-        hipLaunchKernelGGL(rs_upsweep, dim3(tiles), dim3(RS_THREADS), 0, s, ki, n, shift, mask, hist, tiles);
+        if (small) hipLaunchKernelGGL(rs_upsweep<4>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, n, shift, mask, hist, tiles);
+        else hipLaunchKernelGGL(rs_upsweep<RS_ITEMS_MAX>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, n, shift, mask, hist, tiles);
         exclusive_scan_u32(hist, offs, (uint32_t)hist_n, total, scan_state, s);
-        if (pb > 8)
-            hipLaunchKernelGGL(rs_downsweep<9>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
-        else
-            hipLaunchKernelGGL(rs_downsweep<8>, dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
+        if (pb > 8) {
+            if (small)
+                hipLaunchKernelGGL((rs_downsweep<9, 4>), dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
+            else
+                hipLaunchKernelGGL((rs_downsweep<9, RS_ITEMS_MAX>), dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
+        } else {
+            if (small)
+                hipLaunchKernelGGL((rs_downsweep<8, 4>), dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
+            else
+                hipLaunchKernelGGL((rs_downsweep<8, RS_ITEMS_MAX>), dim3(tiles), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, ei, eo, n, shift, mask, offs, tiles);
+        }
         ki = ko; vi = vo; ei = eo;
         shift += pb;
     }

@@ -1039,16 +1039,58 @@ __global__ __launch_bounds__(256) void rc_copy_kernel(RangeDepsParams p, uint32_
     }
 }
 
+// registered-status stores: keep the commands not erased (ACCORD_ST_ERASED: off the range scan for
+// good, impl/InMemoryCommandStore.java:891), owners stay ascending
+__device__ __forceinline__ void rc_entry(const RangeDepsParams &p, uint32_t e, uint32_t &o, uint32_t &s, uint32_t &en,
+                                         uint32_t &k)
+{
+    if (e < p.ncr) { o = p.rc_owner[e]; s = p.rc_start[e]; en = p.rc_end[e]; k = p.rc_kind[e]; }
+    else {
+        const uint32_t r = e - p.ncr, jl = p.rng_owner[r];
+        o = p.g0 + jl; s = p.rng_start[r]; en = p.rng_end[r]; k = (uint32_t)(p.lsb[jl] >> 1) & 7;
+    }
+}
+
+__global__ __launch_bounds__(256) void rc_flag_kernel(RangeDepsParams p, uint32_t R, uint32_t thr, uint32_t *__restrict__ flag)
+{
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < p.ncr + R; e += gridDim.x * blockDim.x) {
+        uint32_t o, s, en, k;
+        rc_entry(p, e, o, s, en, k);
+        flag[e] = o >= thr && k != RC_KIND_ERASED ? 1u : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void rc_scatter_kernel(RangeDepsParams p, uint32_t R, const uint32_t *__restrict__ flag,
+                                                         const uint32_t *__restrict__ off, uint32_t *__restrict__ oo,
+                                                         uint32_t *__restrict__ os, uint32_t *__restrict__ oe,
+                                                         uint32_t *__restrict__ ok)
+{
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < p.ncr + R; e += gridDim.x * blockDim.x) {
+        if (!flag[e]) continue;
+        uint32_t o, s, en, k;
+        rc_entry(p, e, o, s, en, k);
+        const uint32_t d = off[e];
+        oo[d] = o; os[d] = s; oe[d] = en; ok[d] = k;
+    }
+}
+
 } // namespace
 
 void launch_range_carry(const RangeDepsParams &p, uint32_t R, uint32_t thr, uint32_t *out_owner, uint32_t *out_start,
                         uint32_t *out_end, uint32_t *out_kind, uint32_t *first_tmp, unsigned long long *kept,
-                        hipStream_t s)
+                        uint32_t *flags, uint32_t *offs, void *scan_state, hipStream_t s)
 {
-    hipLaunchKernelGGL(rc_first_kernel, dim3(1), dim3(1), 0, s, p, R, thr, first_tmp, kept);
     uint32_t blocks = (p.ncr + R + 255) / 256;
     if (blocks < 1) blocks = 1;
     if (blocks > 4096) blocks = 4096;
+    if (flags) {
+        hipLaunchKernelGGL(rc_flag_kernel, dim3(blocks), dim3(256), 0, s, p, R, thr, flags);
+        exclusive_scan_u32(flags, offs, p.ncr + R, kept, scan_state, s);
+        hipLaunchKernelGGL(rc_scatter_kernel, dim3(blocks), dim3(256), 0, s, p, R, flags, offs, out_owner, out_start,
+                           out_end, out_kind);
+        return;
+    }
+    hipLaunchKernelGGL(rc_first_kernel, dim3(1), dim3(1), 0, s, p, R, thr, first_tmp, kept);
     hipLaunchKernelGGL(rc_copy_kernel, dim3(blocks), dim3(256), 0, s, p, R, first_tmp, out_owner, out_start, out_end, out_kind);
 }
 

@@ -28,7 +28,7 @@ namespace {
 
 using namespace accord_status;
 
-constexpr uint32_t RC_KIND_ERASED = 7;  // carried range command kind no txn witnesses (masks use kinds 0..4)
+using accord::RC_KIND_ERASED;
 
 __device__ __forceinline__ void record_error(accord::DevStatus *st, uint32_t i, int32_t code)
 {

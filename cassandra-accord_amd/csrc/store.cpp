@@ -113,7 +113,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
                       &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2, &s->rg_kbound, &s->rg_cwflag, &s->rg_cwoff, &s->rg_cwpos, &s->rg_cwpm,
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
-                      &s->rc_end2, &s->rc_kind2, &s->rc_first,
+                      &s->rc_end2, &s->rc_kind2, &s->rc_first, &s->rc_flag, &s->rc_offs,
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero};
     accord_impl::shard_comm_destroy(s);
     accord_impl::ready_destroy(s);
@@ -285,7 +285,9 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->rd_r2v_off.ensure(n1 * 4));
     // the store's scan state, shared by every scan of the pipeline (radix digit offsets, CSR offsets,
     // carry compaction): sized for the longest
-    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max({n, PH, accord::radix_sort_scan_len(PH)})), s->stream));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(
+                    accord::scan_temp_bytes(std::max({n, PH, accord::radix_sort_scan_len(PH), (s->resident ? s->rc_n : 0u) + R})),
+                    s->stream));
     // the scan state's 30-bit epochs advance once per scan (a few dozen per compute): re-zeroed long
     // before they could wrap onto a status word still in the buffer
     if (++s->computes_since_zero >= (1u << 22)) {
@@ -556,9 +558,15 @@ int32_t accord_deps_compute(accord_store *s)
             HIPCHECK(s, s->rc_owner2.ensure(cap * 4)); HIPCHECK(s, s->rc_start2.ensure(cap * 4));
             HIPCHECK(s, s->rc_end2.ensure(cap * 4)); HIPCHECK(s, s->rc_kind2.ensure(cap * 4));
             HIPCHECK(s, s->rc_first.ensure(16));
+            uint32_t *flags = nullptr, *offs = nullptr;
+            if (reg) {    // registered-status store: erased range commands leave the carry
+                HIPCHECK(s, s->rc_flag.ensure(cap * 4));
+                HIPCHECK(s, s->rc_offs.ensure(cap * 4));
+                flags = s->rc_flag.as<uint32_t>(); offs = s->rc_offs.as<uint32_t>();
+            }
             accord::launch_range_carry(rp, R, thr, s->rc_owner2.as<uint32_t>(), s->rc_start2.as<uint32_t>(),
                                        s->rc_end2.as<uint32_t>(), s->rc_kind2.as<uint32_t>(),
-                                       s->rc_first.as<uint32_t>(), &dev->totals[9], st);
+                                       s->rc_first.as<uint32_t>(), &dev->totals[9], flags, offs, s->scan_tmp.p, st);
         }
     }
     record(s, EV_COMPACT);

@@ -106,7 +106,7 @@ struct accord_store {
     DevBuf cy_key, cy_ent, cy_key2, cy_ent2, carry_tmp;
     // range commands a later batch may still see (owner global position >= next_global - W,
     // ascending; rc_n of them), double-buffered like the key history carry
-    DevBuf rc_owner, rc_start, rc_end, rc_kind, rc_owner2, rc_start2, rc_end2, rc_kind2, rc_first;
+    DevBuf rc_owner, rc_start, rc_end, rc_kind, rc_owner2, rc_start2, rc_end2, rc_kind2, rc_first, rc_flag, rc_offs;
     uint32_t rc_n = 0;
     // registered statuses (status.hip; resident + ACCORD_WINDOW_NONE): TxnId table sorted
     // (rg_t*, rg_tx_n entries, rg_tg = global position), InternalStatus + executeAt by global

@@ -27,7 +27,7 @@ def _uploaded(p):
 
 
 @pytest.mark.parametrize("G", [1, 2, 3, 5])
-def test_union_random_overlapping(G):
+def test_union_random_overlapping(gpu_device, G):
     rng = np.random.default_rng(10 + G)
     n = 300
     parts = [from_canon(random_depset(rng, n, 2000, 200, 10, 4, 40, shared_keys=np.arange(40))) for _ in range(G)]
@@ -39,7 +39,7 @@ def test_union_random_overlapping(G):
         s.close()
 
 
-def test_union_with_empty_txns_and_long_lists():
+def test_union_with_empty_txns_and_long_lists(gpu_device):
     rng = np.random.default_rng(3)
     n = 64
     a = random_depset(rng, n, 20000, 50, 4, 2, 3000, shared_keys=np.arange(6))
@@ -54,7 +54,7 @@ def test_union_with_empty_txns_and_long_lists():
         _eq(out.download(), O.deps_union([pa, pb]))
 
 
-def test_union_of_more_than_64_sets():
+def test_union_of_more_than_64_sets(gpu_device):
     # 130 parts (10 distinct sets, repeated): three passes of at most 64 parts each
     rng = np.random.default_rng(17)
     n = 200
@@ -72,7 +72,7 @@ def test_union_of_more_than_64_sets():
 
 
 @pytest.mark.parametrize("seed", range(3))
-def test_slice_random_shared_and_per_txn(seed):
+def test_slice_random_shared_and_per_txn(gpu_device, seed):
     rng = np.random.default_rng(40 + seed)
     n, ks = 400, 300
     p = from_canon(random_depset(rng, n, 3000, ks, 12, 6, 30))
@@ -94,7 +94,7 @@ def test_slice_random_shared_and_per_txn(seed):
         _eq(out.download(), O.deps_slice(want, ss, se))
 
 
-def test_rangedeps_slice_kats_on_gpu():
+def test_rangedeps_slice_kats_on_gpu(gpu_device):
     p = from_canon([({}, {(0, 100): [0], (50, 60): [1]})] * 3)
     cases = [([70], [80]), ([55], [80]), ([70, 90], [80, 95]), ([5, 55], [10, 80]), ([0], [40])]
     with _uploaded(p) as src, _store() as out:
@@ -103,7 +103,7 @@ def test_rangedeps_slice_kats_on_gpu():
             _eq(out.download(), O.deps_slice(p, ss, se))
 
 
-def test_invert_random():
+def test_invert_random(gpu_device):
     rng = np.random.default_rng(77)
     p = from_canon(random_depset(rng, 500, 5000, 400, 16, 8, 200))
     with _uploaded(p) as src, _store() as out:
@@ -114,7 +114,7 @@ def test_invert_random():
     assert np.array_equal(ro, wro) and np.array_equal(rv, wrv)
 
 
-def test_ops_on_computed_mixed_stream():
+def test_ops_on_computed_mixed_stream(gpu_device):
     """Ops over the deps the GPU pipeline computed for a mixed key/range stream: slice per
     destination shard, re-union of the slices == the original, invert == oracle."""
     s = generate_stream(20000, 4, 3000, 0.99, 0.5, range_frac=0.2, range_len_max=200, seed=21)
@@ -138,7 +138,7 @@ def test_ops_on_computed_mixed_stream():
         assert np.array_equal(ro, wro) and np.array_equal(rv, wrv)
 
 
-def test_config2_sized_union_of_shard_slices():
+def test_config2_sized_union_of_shard_slices(gpu_device):
     """Size-independent property at config-2 scale (1 Mi txns, Zipf 0.99): the union of the
     slices to a 4-way split of the keyspace is the original deps, and the slices' sizes add up."""
     s = generate_stream(1 << 20, 8, 100_000, 0.99, 0.5, seed=2)
@@ -165,7 +165,7 @@ def test_config2_sized_union_of_shard_slices():
             x.close()
 
 
-def test_slice_rejects_bad_ranges():
+def test_slice_rejects_bad_ranges(gpu_device):
     p = from_canon([({1: [0]}, {})])
     with _uploaded(p) as src, _store() as out:
         with pytest.raises(IllegalArgumentException):
