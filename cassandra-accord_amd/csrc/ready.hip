@@ -24,13 +24,21 @@
 //        released by notifyUnmanaged(APPLY, next.executeAt) (:1264-1283);
 //      - no bit left and STABLE: ReadyToExecute (Commands.maybeExecute, :656-733), reported once.
 // The reference evaluates these tests when an event reaches the key (notifyAndUpdatePending,
-// :1163-1215); here every waiting txn is evaluated at every call, so a txn is released at the first
-// call at which its test holds.  oracle/oracle.c (or_lstore_ready) restates the same evaluation over
+// :1163-1215); here a txn is re-evaluated at every call at which something its tests read changed,
+// so it is released at the first call at which its test holds.  What changed since the last call is
+// found from a per-position change epoch (rg_chg, stamped by accord_txn_register and the batch join):
+// a key is dirty when a carried entry of it changed (every input of its tests -- the key's summary,
+// its deps' statuses and executeAts -- is a carried entry of the key, or a txn the carry dropped for
+// good: INVALID / ERASED, whose later events change nothing the tests read, or below the key's
+// RedundantBefore bound, which the tests skip); a txn is re-evaluated when it changed itself, a key
+// of a set bit is dirty or a range dep of a set bit changed.  A new batch or a truncation (a new carry)
+// and a txn's first evaluation evaluate everything.  oracle/oracle.c (or_lstore_ready) restates the same evaluation over
 // literal CommandsForKey objects.
 #include "store_impl.h"
 #include "status_view.h"
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 using namespace accord_status;
@@ -48,7 +56,8 @@ struct KeySummary {
 
 __device__ __forceinline__ uint32_t kind_class(uint32_t kind) { return kind == 0u ? 0u : kind == 1u ? 1u : 2u; }
 
-// segment bounds of the carried history (key-major): kseg0[k] .. kseg1[k]
+// segment bounds of the carried history (key-major): kseg0[k] .. kseg1[k] (zeroed first); computed
+// once per version of the carry (it changes only when a batch is computed or truncated)
 __global__ __launch_bounds__(256) void rd_seg_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
                                                      uint32_t *__restrict__ kseg0, uint32_t *__restrict__ kseg1)
 {
@@ -59,53 +68,123 @@ __global__ __launch_bounds__(256) void rd_seg_kernel(uint32_t C, const uint32_t 
     }
 }
 
-// the earlier of two candidate txns by executeAt (NONE = no candidate)
-__device__ __forceinline__ uint32_t earlier(const StatusView &v, uint32_t a, uint32_t b)
+// A candidate txn with its executeAt in registers (g = NONE: none)
+struct Cand {
+    uint32_t g;
+    Ts ex;
+};
+
+__device__ __forceinline__ Cand cand_shfl_down(const Cand &c, uint32_t d)
 {
-    if (a == NONE) return b;
-    if (b == NONE) return a;
-    return tcmp(exec_of(v, b), exec_of(v, a)) < 0 ? b : a;
+    return Cand{(uint32_t)__shfl_down((int)c.g, d, 64),
+                Ts{(uint64_t)__shfl_down((long long)c.ex.msb, d, 64), (uint64_t)__shfl_down((long long)c.ex.lsb, d, 64),
+                   __shfl_down(c.ex.node, d, 64)}};
 }
 
-__device__ __forceinline__ uint32_t wave_earlier(const StatusView &v, uint32_t x)
+__device__ __forceinline__ void cand_min(Cand &a, const Cand &b)
 {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x = earlier(v, x, (uint32_t)__shfl_xor((int)x, d, 64));
-    return x;
+    if (b.g != NONE && (a.g == NONE || tcmp(b.ex, a.ex) < 0)) a = b;
 }
 
-// a wave per key: the summary of its CommandsForKey (managed txns: EphemeralReads are not inserted)
-__global__ __launch_bounds__(256) void rd_summary_kernel(uint32_t nkeys, const uint32_t *__restrict__ kseg0,
-                                                         const uint32_t *__restrict__ kseg1,
-                                                         const uint32_t *__restrict__ cent, StatusView v,
-                                                         KeySummary *__restrict__ sum)
+// Per-key summaries in two passes, so a hot key's long history spreads over many waves:
+// rd_part_kernel -- a wave per 64 consecutive carried entries (key-major): every key run inside the
+//   64 reduced by segmented shuffles (earliest executeAt per kind class among the unapplied
+//   committed, first uncommitted), the result stored at the run's first entry (part[]);
+// rd_summary_kernel -- a wave per key: its runs' partials (its first entry and every 64-entry
+//   boundary inside its history) reduced into the key's summary.
+// Managed txns only: EphemeralReads are not inserted into CommandsForKey.
+struct KeyPart {
+    uint32_t cls[3];
+    uint32_t unc;
+};
+
+// Dirty keys (dirty != nullptr): a carried entry whose txn changed since epoch `seen` marks its key
+// with this call's id and appends it to list[] once.
+struct DirtyMark {
+    const uint32_t *chg;
+    uint32_t seen, call;
+    uint32_t *dirty, *list, *cnt;
+};
+
+__global__ __launch_bounds__(256) void rd_part_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
+                                                      const uint32_t *__restrict__ cent, StatusView v,
+                                                      KeyPart *__restrict__ part, DirtyMark dm)
 {
     const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t k = blockIdx.x * (blockDim.x / 64) + wave_id(); k < nkeys; k += waves) {
-        const uint32_t a = kseg0[k], b = kseg1[k];
-        uint32_t mc[3] = {NONE, NONE, NONE}, mu = NONE;
-        for (uint32_t x = a + lane; x < b; x += 64) {
+    for (uint32_t c0 = (blockIdx.x * (blockDim.x / 64) + wave_id()) * 64u; c0 < C; c0 += waves * 64u) {
+        const uint32_t x = c0 + lane;
+        uint32_t key = NONE;
+        Cand cc[3] = {{NONE, {0, 0, 0}}, {NONE, {0, 0, 0}}, {NONE, {0, 0, 0}}};
+        uint32_t mu = NONE;
+        if (x < C) {
+            key = ckey[x];
             const uint32_t e = cent[x], g = e & ENT_TXN_MASK, kind = e >> ENT_KIND_SHIFT;
-            if (kind == 2u) continue;
-            const uint32_t st = status_of(v, g);
-            if (st >= ST_INVALID) continue;
-            if (st >= ST_COMMITTED) {
-                if (st < ST_APPLIED) {
-                    const uint32_t c = kind_class(kind);
-                    mc[c] = earlier(v, mc[c], g);
-                }
-            } else {
-                mu = min(mu, g);
+            const uint32_t st = kind == 2u ? ST_INVALID : status_of(v, g);
+            if (dm.dirty && dm.chg[g] > dm.seen && dm.dirty[key] != dm.call && atomicExch(&dm.dirty[key], dm.call) != dm.call)
+                dm.list[atomicAdd(dm.cnt, 1u)] = key;
+            if (st < ST_COMMITTED) mu = g;
+            else if (st < ST_APPLIED) cc[kind_class(kind)] = Cand{g, exec_of(v, g)};
+        }
+        // segmented suffix reduction over the run of equal keys (keys ascend inside the chunk)
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t ok = (uint32_t)__shfl_down((int)key, d, 64);
+            const bool take = lane + d < 64 && ok == key;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const Cand o = cand_shfl_down(cc[c], d);
+                if (take) cand_min(cc[c], o);
             }
+            const uint32_t om = (uint32_t)__shfl_down((int)mu, d, 64);
+            if (take) mu = min(mu, om);
+        }
+        const uint32_t pk = (uint32_t)__shfl_up((int)key, 1, 64);
+        if (x < C && (lane == 0 || pk != key)) part[x] = KeyPart{{cc[0].g, cc[1].g, cc[2].g}, mu};
+    }
+}
+
+// every key (list == nullptr), or the dirty keys list[0 .. *cnt)
+__global__ __launch_bounds__(256) void rd_summary_kernel(uint32_t nkeys, const uint32_t *__restrict__ kseg0,
+                                                         const uint32_t *__restrict__ kseg1,
+                                                         const KeyPart *__restrict__ part, StatusView v,
+                                                         KeySummary *__restrict__ sum, const uint32_t *__restrict__ list,
+                                                         const uint32_t *__restrict__ cnt)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    const uint32_t m = list ? *cnt : nkeys;
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + wave_id(); i < m; i += waves) {
+        const uint32_t k = list ? list[i] : i;
+        const uint32_t a = kseg0[k], b = kseg1[k];
+        Cand cc[3] = {{NONE, {0, 0, 0}}, {NONE, {0, 0, 0}}, {NONE, {0, 0, 0}}};
+        uint32_t mu = NONE;
+        // the runs: one starting at a, then one at every multiple of 64 inside (a, b)
+        const uint32_t nr = a < b ? 1u + ((b - 1) >> 6) - (a >> 6) : 0u;
+        for (uint32_t j = lane; j < nr; j += 64) {
+            const uint32_t x = j == 0 ? a : ((a >> 6) + j) << 6;
+            const KeyPart q = part[x];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                if (q.cls[c] != NONE) cand_min(cc[c], Cand{q.cls[c], exec_of(v, q.cls[c])});
+            mu = min(mu, q.unc);
         }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) mc[c] = wave_earlier(v, mc[c]);
+        for (uint32_t d = 32; d >= 1; d >>= 1) {
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) mu = min(mu, (uint32_t)__shfl_xor((int)mu, d, 64));
+            for (int c = 0; c < 3; ++c) {
+                const Cand o{(uint32_t)__shfl_xor((int)cc[c].g, d, 64),
+                             Ts{(uint64_t)__shfl_xor((long long)cc[c].ex.msb, d, 64),
+                                (uint64_t)__shfl_xor((long long)cc[c].ex.lsb, d, 64), __shfl_xor(cc[c].ex.node, d, 64)}};
+                cand_min(cc[c], o);
+            }
+            mu = min(mu, (uint32_t)__shfl_xor((int)mu, d, 64));
+        }
         if (lane == 0) {
             KeySummary s{};
-            for (int c = 0; c < 3; ++c) s.min_cls[c] = mc[c];
-            s.next = earlier(v, earlier(v, mc[0], mc[1]), mc[2]);   // nulled by the evaluation (TxnId order)
+            Cand nx = cc[0];
+            cand_min(nx, cc[1]);
+            cand_min(nx, cc[2]);
+            for (int c = 0; c < 3; ++c) s.min_cls[c] = cc[c].g;
+            s.next = nx.g;                           // nulled by the evaluation (TxnId order)
             s.min_unc = mu;
             sum[k] = s;
         }
@@ -126,12 +205,15 @@ struct ReadyParams {
     const uint32_t *wo_off;
     unsigned long long *words, *aoi;
     uint8_t *pend;                    // per key slot: 0 unregistered, 1 COMMIT, 2 APPLY, 3 released
-    uint32_t *until;
+    uint32_t *until;                  // unmanaged: the pending record's txn; managed: the committed-deps cursor
     uint8_t *done;
     uint32_t *out, *out_cnt;          // txns that became ready (positions)
     const KeySummary *sum;
     const uint32_t *kb;               // per key: shardRedundantBefore as a position (0: none)
     StatusView v;
+    uint32_t full;                    // evaluate every txn (else: only those whose inputs changed)
+    uint32_t seen, call;              // change epoch of the last call; this call's id
+    const uint32_t *chg, *dirty;      // by position: change epoch; by key: id of the call it was dirty in
 };
 
 // the TxnId of global position g (the store's TxnId table is in stream order)
@@ -172,12 +254,73 @@ __device__ int unmanaged_eval(const ReadyParams &p, uint32_t t, uint32_t d0, uin
     return -1;
 }
 
-// a wave per waiting txn, a lane per WaitingOn bit (64 per word)
-__global__ __launch_bounds__(256) void rd_eval_kernel(ReadyParams p)
+// a wave per waiting txn, a lane per WaitingOn bit (64 per word); every generation in one launch
+// (the waves walk the concatenated txn index space, gbase[] = each generation's first index)
+constexpr uint32_t RD_GENS = 32;          // generations evaluated per launch
+struct ReadyLaunch {
+    uint32_t ngen, total;
+    uint32_t gbase[RD_GENS + 1];
+    uint32_t *work, *wcnt;            // incremental calls: the txns to evaluate (rd_filter_kernel)
+    ReadyParams g[RD_GENS];
+};
+
+__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane);
+
+// Incremental calls: a lane per waiting txn keeps those whose inputs changed since the last call
+// (the txn itself, the key of a set key bit dirty, the txn of a set range-dep bit changed) or that
+// were never evaluated; wave-aggregated appends to work[].
+__global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__restrict__ L)
+{
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id();
+    const uint32_t ngen = L->ngen, total = L->total;
+    bool need = false;
+    if (u < total) {
+        uint32_t gi = 0;
+        while (gi + 1 < ngen && L->gbase[gi + 1] <= u) ++gi;
+        const ReadyParams &p = L->g[gi];
+        const uint32_t t = u - L->gbase[gi];
+        if (!p.done[t]) {
+            need = p.full || p.chg[p.g[t]] > p.seen;
+            const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], RK = R + p.key_off[t + 1] - p.key_off[t];
+            const uint32_t w0 = p.wo_off[t], nw = p.wo_off[t + 1] - w0;
+            for (uint32_t q = 0; q < nw && !need; ++q) {
+                unsigned long long w = p.words[w0 + q];
+                while (w && !need) {
+                    const uint32_t b = q * 64u + (uint32_t)__ffsll((long long)w) - 1u;
+                    if (b >= RK) break;
+                    need = b < R ? p.chg[p.rd_vals[p.rd_off[t] + b]] > p.seen
+                                 : p.dirty[p.keys[p.key_off[t] + b - R] - p.key_lo] == p.call;
+                    w &= w - 1ull;
+                }
+            }
+        }
+    }
+    const unsigned long long m = __ballot(need);
+    if (m) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(L->wcnt, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        if (need) L->work[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = u;
+    }
+}
+
+// a wave per txn: every txn of the launch (work == nullptr) or the listed ones
+__global__ __launch_bounds__(256) void rd_eval_kernel(const ReadyLaunch *__restrict__ L, uint32_t listed)
 {
     const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t t = blockIdx.x * (blockDim.x / 64) + wave_id(); t < p.n; t += waves) {
-        if (p.done[t]) continue;
+    const uint32_t ngen = L->ngen, m = listed ? *L->wcnt : L->total;
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + wave_id(); i < m; i += waves) {
+        const uint32_t u = listed ? L->work[i] : i;
+        uint32_t gi = 0;
+        while (gi + 1 < ngen && L->gbase[gi + 1] <= u) ++gi;
+        rd_eval_txn(L->g[gi], u - L->gbase[gi], lane);
+    }
+}
+
+__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane)
+{
+    {
+        if (p.done[t]) return;
         const uint32_t g = p.g[t], st = status_of(p.v, g);
         const uint64_t l = p.lsb[t];
         const uint32_t kind = (uint32_t)(l >> 1) & 7u;
@@ -214,9 +357,18 @@ __global__ __launch_bounds__(256) void rd_eval_kernel(ReadyParams p)
                             if (((wmask >> 0) & 1u) && s.min_cls[0] != NONE && tcmp(exec_of(p.v, s.min_cls[0]), ex) < 0) blocked = true;
                             if (((wmask >> 1) & 1u) && s.min_cls[1] != NONE && tcmp(exec_of(p.v, s.min_cls[1]), ex) < 0) blocked = true;
                             if (((wmask >> 3) & 1u) && s.min_cls[2] != NONE && tcmp(exec_of(p.v, s.min_cls[2]), ex) < 0) blocked = true;
-                            for (uint32_t x = d0; x < d1 && !blocked; ++x) {   // a dep still uncommitted
-                                const uint32_t u = p.vals[p.val_off[t] + p.k2v[hb + x]];
-                                if (u >= kbound && status_of(p.v, u) < ST_COMMITTED) blocked = true;
+                            // a dep still uncommitted: committed (and below the bound) never reverts, so
+                            // the scan resumes where the last one stopped (until[] = its cursor here)
+                            // every uncommitted txn of the key is at or after min_unc (positions
+                            // ascend with TxnIds): none of the deps when the last one precedes it
+                            if (!blocked && d1 > d0 && s.min_unc != NONE &&
+                                s.min_unc <= p.vals[p.val_off[t] + p.k2v[hb + d1 - 1]]) {
+                                uint32_t x = max(d0, p.until[slot]);
+                                for (; x < d1; ++x) {
+                                    const uint32_t u = p.vals[p.val_off[t] + p.k2v[hb + x]];
+                                    if (u >= kbound && status_of(p.v, u) < ST_COMMITTED) { blocked = true; break; }
+                                }
+                                p.until[slot] = x;
                             }
                             clear = !blocked;
                         }
@@ -270,6 +422,7 @@ namespace accord_impl {
 
 struct ReadyGen {
     uint32_t n = 0, left = 0, glo = 0, ghi = 0;   // txns, not yet ready, first / last global position
+    bool fresh = true;                            // not evaluated yet
     uint64_t words = 0;
     DevBuf g, lsb, rd_off, rd_vals, key_off, keys, val_off, vals, k2v_off, k2v, wo_off, wo, aoi, pend, until, done;
     void release()
@@ -285,6 +438,8 @@ void ready_destroy(accord_store *s)
     for (ReadyGen *r : s->rdy_gens) { r->release(); delete r; }
     s->rdy_gens.clear();
     s->rdy_waiting = 0;
+    if (s->rdy_host) { (void)hipHostFree(s->rdy_host); s->rdy_host = nullptr; }
+    if (s->rdy_tab_host) { (void)hipHostFree(s->rdy_tab_host); s->rdy_tab_host = nullptr; s->rdy_tab_cap = 0; }
 }
 
 // the last computed batch (its WaitingOn just initialised) joins the waiting set
@@ -323,6 +478,7 @@ int32_t ready_track_batch(accord_store *s)
     HIPCHECK(s, r->until.ensure(s->tot_keys * 4 + 8));
     HIPCHECK(s, r->done.ensure((size_t)n + 8));
     HIPCHECK(s, hipMemsetAsync(r->pend.p, 0, s->tot_keys + 8, st));
+    HIPCHECK(s, hipMemsetAsync(r->until.p, 0, s->tot_keys * 4 + 8, st));
     HIPCHECK(s, hipMemsetAsync(r->done.p, 0, (size_t)n + 8, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     s->rdy_waiting += n;
@@ -343,16 +499,25 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     hipStream_t st = s->stream;
     const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo, C = s->carry_n;
     uint64_t cap = 0;
-    for (accord_impl::ReadyGen *r : s->rdy_gens) cap += r->n;
+    for (accord_impl::ReadyGen *r : s->rdy_gens) cap += r->left ? r->n : 0;
     s->rdy_list.clear();
     if (cap == 0) return ACCORD_OK;
-    HIPCHECK(s, s->rdy_kseg0.ensure((size_t)nkeys * 4 + 4));
-    HIPCHECK(s, s->rdy_kseg1.ensure((size_t)nkeys * 4 + 4));
+    constexpr uint32_t PEEK = 4096;            // ready txns read back with the count in one copy
     HIPCHECK(s, s->rdy_sum.ensure((size_t)nkeys * sizeof(KeySummary) + 64));
-    HIPCHECK(s, s->rdy_out.ensure(cap * 4 + 64));
-    HIPCHECK(s, hipMemsetAsync(s->rdy_kseg0.p, 0, (size_t)nkeys * 4, st));
-    HIPCHECK(s, hipMemsetAsync(s->rdy_kseg1.p, 0, (size_t)nkeys * 4, st));
-    HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, 64, st));
+    HIPCHECK(s, s->rdy_out.ensure(cap * 4 + 256));
+    const uint32_t ngens = (uint32_t)s->rdy_gens.size();
+    const uint32_t nl = (ngens + RD_GENS - 1) / RD_GENS;
+    HIPCHECK(s, s->rdy_launch.ensure((size_t)std::max(1u, nl) * sizeof(ReadyLaunch)));
+    if (!s->rdy_host) {
+        HIPCHECK(s, hipHostMalloc(&s->rdy_host, (PEEK + 64) * 4, hipHostMallocDefault));
+    }
+    constexpr uint32_t HDR = 64;               // rdy_out header words: ready count, dirty keys, work counts
+    HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, HDR * 4, st));
+    // everything is re-evaluated after a new carry (batch, truncation) or RedundantBefore bound
+    const bool full = s->rdy_kb_dirty || s->rdy_sum_version != s->carry_version;
+    const uint32_t seen = s->rdy_seen, call = ++s->rdy_call;
+    s->rdy_seen = s->rg_epoch;
+    s->rdy_sum_version = s->carry_version;
     if (s->rdy_kb_dirty) {
         HIPCHECK(s, s->rdy_kb.ensure((size_t)nkeys * 4 + 4));
         HIPCHECK(s, hipMemcpyAsync(s->rdy_kb.p, s->rdy_kb_host.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
@@ -362,15 +527,39 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     v.status = s->rg_status.as<uint8_t>();
     v.emsb = s->rg_emsb.as<uint64_t>(); v.elsb = s->rg_elsb.as<uint64_t>(); v.enode = s->rg_enode.as<int32_t>();
     v.known = s->rg_known;
-    if (C) hipLaunchKernelGGL(rd_seg_kernel, dim3(std::min<uint32_t>((C + 255) / 256, 8192u)), dim3(256), 0, st, C,
-                              s->cy_key.as<uint32_t>(), s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>());
-    if (nkeys) hipLaunchKernelGGL(rd_summary_kernel, dim3(grid_for_waves(nkeys)), dim3(256), 0, st, nkeys,
-                                  s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>(), s->cy_ent.as<uint32_t>(), v,
-                                  s->rdy_sum.as<KeySummary>());
-    uint32_t *cnt = s->rdy_out.as<uint32_t>(), *list = cnt + 16;
+    HIPCHECK(s, s->rdy_part.ensure((size_t)C * sizeof(KeyPart) + 64));
+    HIPCHECK(s, s->rdy_dirty.ensure_zeroed((size_t)nkeys * 4 + 4, st));
+    HIPCHECK(s, s->rdy_dlist.ensure((size_t)nkeys * 4 + 4));
+    uint32_t *cnt = s->rdy_out.as<uint32_t>(), *list = cnt + HDR;    // cnt[0]: ready txns, cnt[1]: dirty keys
+    DirtyMark dm{};
+    if (!full) {
+        dm.chg = s->rg_chg.as<uint32_t>(); dm.seen = seen; dm.call = call;
+        dm.dirty = s->rdy_dirty.as<uint32_t>(); dm.list = s->rdy_dlist.as<uint32_t>(); dm.cnt = cnt + 1;
+    }
+    if (C) hipLaunchKernelGGL(rd_part_kernel, dim3(grid_for_waves((C + 63) / 64)), dim3(256), 0, st, C,
+                              s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), v, s->rdy_part.as<KeyPart>(), dm);
+    if (s->rdy_kseg_version != s->carry_version || !s->rdy_kseg0.p) {
+        HIPCHECK(s, s->rdy_kseg0.ensure((size_t)nkeys * 4 + 4));
+        HIPCHECK(s, s->rdy_kseg1.ensure((size_t)nkeys * 4 + 4));
+        HIPCHECK(s, hipMemsetAsync(s->rdy_kseg0.p, 0, (size_t)nkeys * 4, st));
+        HIPCHECK(s, hipMemsetAsync(s->rdy_kseg1.p, 0, (size_t)nkeys * 4, st));
+        if (C) hipLaunchKernelGGL(rd_seg_kernel, dim3(std::min<uint32_t>((C + 255) / 256, 8192u)), dim3(256), 0, st, C,
+                                  s->cy_key.as<uint32_t>(), s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>());
+        s->rdy_kseg_version = s->carry_version;
+    }
+    if (nkeys) hipLaunchKernelGGL(rd_summary_kernel, dim3(full ? grid_for_waves(nkeys) : std::min(grid_for_waves(nkeys), 256u)),
+                                  dim3(256), 0, st, nkeys, s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>(),
+                                  s->rdy_part.as<KeyPart>(), v, s->rdy_sum.as<KeySummary>(),
+                                  full ? nullptr : s->rdy_dlist.as<uint32_t>(), cnt + 1);
+    // the generations with txns left, RD_GENS per launch (their parameter table copied to the device)
+    std::vector<ReadyLaunch> tabs;
+    bool any_inc = false;
     for (accord_impl::ReadyGen *r : s->rdy_gens) {
         if (r->left == 0) continue;
-        ReadyParams p{};
+        if (tabs.empty() || tabs.back().ngen == RD_GENS) { tabs.emplace_back(); tabs.back().ngen = 0; tabs.back().total = 0; }
+        ReadyLaunch &L = tabs.back();
+        ReadyParams &p = L.g[L.ngen];
+        p = ReadyParams{};
         p.n = r->n; p.key_lo = s->cfg.key_lo;
         p.g = r->g.as<uint32_t>(); p.lsb = r->lsb.as<uint64_t>();
         p.tmsb = s->rg_tmsb.as<uint64_t>(); p.tlsb = s->rg_tlsb.as<uint64_t>(); p.tnode = s->rg_tnode.as<int32_t>();
@@ -385,16 +574,62 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.sum = s->rdy_sum.as<KeySummary>();
         p.kb = s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
         p.v = v;
-        hipLaunchKernelGGL(rd_eval_kernel, dim3(grid_for_waves(r->n)), dim3(256), 0, st, p);
+        p.full = full || r->fresh;
+        any_inc |= !p.full;
+        p.seen = seen; p.call = call;
+        p.chg = s->rg_chg.as<uint32_t>(); p.dirty = s->rdy_dirty.as<uint32_t>();
+        r->fresh = false;
+        L.gbase[L.ngen] = L.total;
+        L.total += r->n;
+        L.gbase[++L.ngen] = L.total;
+    }
+    if (any_inc) {          // a work list per launch: cap entries, counts in rdy_wcnt
+        HIPCHECK(s, s->rdy_work.ensure(cap * 4 + 64));
+        uint32_t *wc = cnt + 2;                // in the header (cleared above) unless too many launches
+        if (tabs.size() > HDR - 2) {
+            HIPCHECK(s, s->rdy_wcnt.ensure(tabs.size() * 4 + 64));
+            HIPCHECK(s, hipMemsetAsync(s->rdy_wcnt.p, 0, tabs.size() * 4, st));
+            wc = s->rdy_wcnt.as<uint32_t>();
+        }
+        uint64_t off = 0;
+        for (size_t i = 0; i < tabs.size(); ++i) {
+            tabs[i].work = s->rdy_work.as<uint32_t>() + off;
+            tabs[i].wcnt = wc + i;
+            off += tabs[i].total;
+        }
+    }
+    HIPCHECK(s, s->rdy_launch.ensure(tabs.size() * sizeof(ReadyLaunch)));
+    const size_t tab_bytes = tabs.size() * sizeof(ReadyLaunch);
+    if (s->rdy_tab_cap < tab_bytes) {          // pinned staging for the tables (the call ends synchronised)
+        if (s->rdy_tab_host) (void)hipHostFree(s->rdy_tab_host);
+        s->rdy_tab_host = nullptr; s->rdy_tab_cap = 0;
+        HIPCHECK(s, hipHostMalloc(&s->rdy_tab_host, tab_bytes * 2, hipHostMallocDefault));
+        s->rdy_tab_cap = tab_bytes * 2;
+    }
+    std::memcpy(s->rdy_tab_host, tabs.data(), tab_bytes);
+    HIPCHECK(s, hipMemcpyAsync(s->rdy_launch.p, s->rdy_tab_host, tab_bytes, hipMemcpyHostToDevice, st));
+    for (size_t i = 0; i < tabs.size(); ++i) {
+        const ReadyLaunch *L = s->rdy_launch.as<ReadyLaunch>() + i;
+        if (any_inc) {
+            hipLaunchKernelGGL(rd_filter_kernel, dim3((tabs[i].total + 255) / 256), dim3(256), 0, st, L);
+            hipLaunchKernelGGL(rd_eval_kernel, dim3(std::min(grid_for_waves(tabs[i].total), 1024u)), dim3(256), 0, st, L, 1u);
+        } else {
+            hipLaunchKernelGGL(rd_eval_kernel, dim3(grid_for_waves(tabs[i].total)), dim3(256), 0, st, L, 0u);
+        }
     }
     HIPCHECK(s, hipGetLastError());
-    uint32_t nr = 0;
-    HIPCHECK(s, hipMemcpyAsync(&nr, cnt, 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(s, hipStreamSynchronize(st));
+    uint32_t *peek = (uint32_t *)s->rdy_host;
+    HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK)) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));       // also: the parameter tables were consumed
+    const uint32_t nr = peek[0];
     s->rdy_list.resize(nr);
     if (nr) {
-        HIPCHECK(s, hipMemcpyAsync(s->rdy_list.data(), list, (size_t)nr * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(s, hipStreamSynchronize(st));
+        if (nr <= PEEK) {
+            std::copy(peek + HDR, peek + HDR + nr, s->rdy_list.begin());
+        } else {
+            HIPCHECK(s, hipMemcpyAsync(s->rdy_list.data(), list, (size_t)nr * 4, hipMemcpyDeviceToHost, st));
+            HIPCHECK(s, hipStreamSynchronize(st));
+        }
         std::sort(s->rdy_list.begin(), s->rdy_list.end());
     }
     // generations drain in stream order: count each one's released txns, free the empty ones

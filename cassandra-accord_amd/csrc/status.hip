@@ -251,6 +251,8 @@ struct RegParams {
     int32_t *xnode;
     uint32_t *pos;                     // out: global position of every event
     accord::DevStatus *err;
+    uint32_t *chg;                     // by global position: the registration epoch of its last change
+    uint32_t epoch;
 };
 
 __global__ __launch_bounds__(256) void reg_check_kernel(RegParams p)
@@ -306,6 +308,7 @@ __global__ __launch_bounds__(256) void reg_apply_kernel(RegParams p)
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += gridDim.x * blockDim.x) {
         const uint32_t g = p.pos[r], nw = p.status[r];
         p.st[g] = (uint8_t)nw;
+        p.chg[g] = p.epoch;                 // readiness re-evaluates the keys of changed txns
         if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) { p.xmsb[g] = p.emsb[r]; p.xlsb[g] = p.elsb[r]; p.xnode[g] = p.enode[r]; }
     }
 }
@@ -317,10 +320,11 @@ __global__ __launch_bounds__(256) void join_kernel(uint32_t n, uint32_t tx_n, co
                                                    uint64_t *__restrict__ tlsb, int32_t *__restrict__ tnode,
                                                    uint32_t *__restrict__ tg, uint8_t *__restrict__ st,
                                                    uint64_t *__restrict__ xmsb, uint64_t *__restrict__ xlsb,
-                                                   int32_t *__restrict__ xnode)
+                                                   int32_t *__restrict__ xnode, uint32_t *__restrict__ chg, uint32_t epoch)
 {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t g = gidx[t];
+        chg[g] = epoch;
         tmsb[tx_n + t] = msb[t]; tlsb[tx_n + t] = lsb[t]; tnode[tx_n + t] = node[t]; tg[tx_n + t] = g;
         st[g] = ST_PREACCEPTED;
         xmsb[g] = msb[t]; xlsb[g] = lsb[t]; xnode[g] = node[t];
@@ -664,6 +668,7 @@ int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start
     std::swap(s->cy_key, s->cy_key2);
     std::swap(s->cy_ent, s->cy_ent2);
     s->carry_n = (uint32_t)kept;
+    ++s->carry_version;
     return ACCORD_OK;
 }
 
@@ -683,13 +688,16 @@ int32_t status_join_batch(accord_store *s)
     HIPCHECK(s, grow_keep(s->rg_emsb, G * 8, known * 8, st));
     HIPCHECK(s, grow_keep(s->rg_elsb, G * 8, known * 8, st));
     HIPCHECK(s, grow_keep(s->rg_enode, G * 4, known * 4, st));
+    HIPCHECK(s, grow_keep(s->rg_chg, G * 4, known * 4, st));
+    if (G > known) HIPCHECK(s, hipMemsetAsync(s->rg_chg.as<uint32_t>() + known, 0, (G - known) * 4, st));
+    ++s->rg_epoch;
     if (G > known)   // positions no txn of this store holds (txn_index gaps): never looked at
         HIPCHECK(s, hipMemsetAsync(s->rg_status.as<uint8_t>() + known, ST_PREACCEPTED, G - known, st));
     hipLaunchKernelGGL(join_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, (uint32_t)tx, s->msb.as<uint64_t>(),
                        s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
                        s->rg_tmsb.as<uint64_t>(), s->rg_tlsb.as<uint64_t>(), s->rg_tnode.as<int32_t>(),
                        s->rg_tg.as<uint32_t>(), s->rg_status.as<uint8_t>(), s->rg_emsb.as<uint64_t>(),
-                       s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>());
+                       s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>(), s->rg_chg.as<uint32_t>(), s->rg_epoch);
     HIPCHECK(s, hipStreamSynchronize(st));
     s->rg_tx_n = (uint32_t)(tx + n);
     s->rg_known = (uint32_t)G;
@@ -742,6 +750,8 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     p.xmsb = s->rg_emsb.as<uint64_t>(); p.xlsb = s->rg_elsb.as<uint64_t>(); p.xnode = s->rg_enode.as<int32_t>();
     p.pos = T[7].as<uint32_t>();
     p.err = &dev->status;
+    p.chg = s->rg_chg.as<uint32_t>();
+    p.epoch = s->rg_epoch + 1;
     if (p.tx_n == 0) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: the store holds no txn yet");
     hipLaunchKernelGGL(reg_check_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
     accord::DevStatus hs;
@@ -755,6 +765,7 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
                         : "unknown TxnId, or executeAt before TxnId";
         return fail(s, code, "accord_txn_register: event %u rejected (%s); nothing applied", r, why);
     }
+    ++s->rg_epoch;
     hipLaunchKernelGGL(reg_apply_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
     if (s->rc_n)
         hipLaunchKernelGGL(reg_erase_ranges_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, s->rc_n,

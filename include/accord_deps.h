@@ -402,7 +402,10 @@ int32_t accord_waiting_on_compute(accord_store *store);                 /* devic
  * awaitsOnlyDeps: removeWaitingOn) or is APPLIED (setAppliedAndPropagate); bits [R_i, R_i + K_i) =
  * KeyDeps keys, set (CommandsForKey.notify clears them as the keys' predecessors apply).  The
  * propagation of an applied dep's own appliedOrInvalidated set is not modelled (taken as empty), nor
- * are pre-bootstrap / stale ranges (removeRedundantDependencies) or executeAtLeast.  level = 0,
+ * are pre-bootstrap / stale ranges (removeRedundantDependencies) or executeAtLeast.  hasBeen(PreCommitted)
+ * is read from the InternalStatus (>= COMMITTED): a dep at SaveStatus PreCommitted* (InternalStatus
+ * PREACCEPTED / ACCEPTED, local/CommandsForKey.java:213-215) is treated as uncommitted -- the bit stays
+ * set until the dep commits (conservative: never released earlier than the reference).  level = 0,
  * max_level = 0, preds_total = 0 (levelling is accord_waiting_on_compute's model).  Download with
  * accord_waiting_on_download (applied_or_invalidated set). */
 int32_t accord_waiting_on_initialise(accord_store *store);
