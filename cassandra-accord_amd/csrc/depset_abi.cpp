@@ -221,6 +221,7 @@ void publish(accord_store *s, DepSet &o, uint32_t n)
 {
     o.n = n;
     s->ds_cur = (&o == &s->ds[0]) ? 0 : 1;
+    s->ds_rb = false;
     s->computed = true;
     s->wo_done = false;
 }
@@ -307,7 +308,28 @@ int32_t redundant_apply(accord_store *s)
     RC(union_side(s, parts, 2, true, o));
     HIPCHECK(s, hipStreamSynchronize(st));
     publish(s, o, n);
+    s->ds_rb = true;
     return ACCORD_OK;
+}
+
+CurDeps cur_deps(const accord_store *s)
+{
+    CurDeps c{};
+    if (s->ds_cur >= 0) {
+        const DepSet &x = s->ds[s->ds_cur];
+        c.kd_key_off = x.key_off.as<uint32_t>(); c.kd_keys = x.keys.as<uint32_t>();
+        c.kd_val_off = x.val_off.as<uint32_t>(); c.kd_vals = x.vals.as<uint32_t>();
+        c.kd_k2v_off = x.x_off.as<uint32_t>(); c.kd_k2v = x.x.as<uint32_t>();
+        c.rd_val_off = x.rval_off.as<uint32_t>(); c.rd_vals = x.rvals.as<uint32_t>();
+        c.tot_keys = x.tot_keys; c.tot_vals = x.tot_vals; c.tot_k2v = x.tot_x; c.tot_rvals = x.tot_rvals;
+    } else {
+        c.kd_key_off = s->kd_key_off.as<uint32_t>(); c.kd_keys = s->kd_keys.as<uint32_t>();
+        c.kd_val_off = s->kd_val_off.as<uint32_t>(); c.kd_vals = s->kd_vals.as<uint32_t>();
+        c.kd_k2v_off = s->kd_k2v_off.as<uint32_t>(); c.kd_k2v = s->kd_k2v.as<uint32_t>();
+        c.rd_val_off = s->rd_val_off.as<uint32_t>(); c.rd_vals = s->rd_vals.as<uint32_t>();
+        c.tot_keys = s->tot_keys; c.tot_vals = s->tot_vals; c.tot_k2v = s->tot_k2v; c.tot_rvals = s->tot_rvals;
+    }
+    return c;
 }
 
 } // namespace accord_impl

@@ -454,31 +454,32 @@ int32_t ready_track_batch(accord_store *s)
     r->n = r->left = n;
     r->words = s->wo_words_total;
     const size_t n1 = (size_t)n + 1;
-    auto copy = [&](DevBuf &dst, const DevBuf &src, size_t bytes) -> hipError_t {
+    auto copy = [&](DevBuf &dst, const void *src, size_t bytes) -> hipError_t {
         hipError_t e = dst.ensure(bytes + 8);
-        if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst.p, src.p, bytes, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst.p, src, bytes, hipMemcpyDeviceToDevice, st);
         return e;
     };
-    HIPCHECK(s, copy(r->g, s->txn_index, (size_t)n * 4));    // resident stores: global positions
+    const CurDeps cd = cur_deps(s);                           // the batch's deps (with RedundantBefore's)
+    HIPCHECK(s, copy(r->g, s->txn_index.p, (size_t)n * 4));  // resident stores: global positions
     HIPCHECK(s, hipMemcpyAsync(&r->glo, s->txn_index.p, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipMemcpyAsync(&r->ghi, s->txn_index.as<uint32_t>() + n - 1, 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(s, copy(r->lsb, s->lsb, (size_t)n * 8));
-    HIPCHECK(s, copy(r->rd_off, s->rd_val_off, n1 * 4));
-    HIPCHECK(s, copy(r->rd_vals, s->rd_vals, s->tot_rvals * 4));
-    HIPCHECK(s, copy(r->key_off, s->kd_key_off, n1 * 4));
-    HIPCHECK(s, copy(r->keys, s->kd_keys, s->tot_keys * 4));
-    HIPCHECK(s, copy(r->val_off, s->kd_val_off, n1 * 4));
-    HIPCHECK(s, copy(r->vals, s->kd_vals, s->tot_vals * 4));
-    HIPCHECK(s, copy(r->k2v_off, s->kd_k2v_off, n1 * 4));
-    HIPCHECK(s, copy(r->k2v, s->kd_k2v, s->tot_k2v * 4));
-    HIPCHECK(s, copy(r->wo_off, s->wo_off, n1 * 4));
-    HIPCHECK(s, copy(r->wo, s->wo_words, s->wo_words_total * 8));
-    HIPCHECK(s, copy(r->aoi, s->wo_aoi, s->wo_words_total * 8));
-    HIPCHECK(s, r->pend.ensure(s->tot_keys + 8));
-    HIPCHECK(s, r->until.ensure(s->tot_keys * 4 + 8));
+    HIPCHECK(s, copy(r->lsb, s->lsb.p, (size_t)n * 8));
+    HIPCHECK(s, copy(r->rd_off, cd.rd_val_off, n1 * 4));
+    HIPCHECK(s, copy(r->rd_vals, cd.rd_vals, cd.tot_rvals * 4));
+    HIPCHECK(s, copy(r->key_off, cd.kd_key_off, n1 * 4));
+    HIPCHECK(s, copy(r->keys, cd.kd_keys, cd.tot_keys * 4));
+    HIPCHECK(s, copy(r->val_off, cd.kd_val_off, n1 * 4));
+    HIPCHECK(s, copy(r->vals, cd.kd_vals, cd.tot_vals * 4));
+    HIPCHECK(s, copy(r->k2v_off, cd.kd_k2v_off, n1 * 4));
+    HIPCHECK(s, copy(r->k2v, cd.kd_k2v, cd.tot_k2v * 4));
+    HIPCHECK(s, copy(r->wo_off, s->wo_off.p, n1 * 4));
+    HIPCHECK(s, copy(r->wo, s->wo_words.p, s->wo_words_total * 8));
+    HIPCHECK(s, copy(r->aoi, s->wo_aoi.p, s->wo_words_total * 8));
+    HIPCHECK(s, r->pend.ensure(cd.tot_keys + 8));
+    HIPCHECK(s, r->until.ensure(cd.tot_keys * 4 + 8));
     HIPCHECK(s, r->done.ensure((size_t)n + 8));
-    HIPCHECK(s, hipMemsetAsync(r->pend.p, 0, s->tot_keys + 8, st));
-    HIPCHECK(s, hipMemsetAsync(r->until.p, 0, s->tot_keys * 4 + 8, st));
+    HIPCHECK(s, hipMemsetAsync(r->pend.p, 0, cd.tot_keys + 8, st));
+    HIPCHECK(s, hipMemsetAsync(r->until.p, 0, cd.tot_keys * 4 + 8, st));
     HIPCHECK(s, hipMemsetAsync(r->done.p, 0, (size_t)n + 8, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     s->rdy_waiting += n;

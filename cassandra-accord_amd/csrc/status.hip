@@ -528,11 +528,11 @@ bool registered_mode(const accord_store *s) { return s->resident && s->cfg.windo
 int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned long long *words,
                                unsigned long long *aoi)
 {
+    const CurDeps cd = cur_deps(s);
     if (s->n)
         hipLaunchKernelGGL(wo_init_kernel, dim3(grid_for(s->n)), dim3(256), 0, s->stream, s->n, s->msb.as<uint64_t>(),
                            s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
-                           s->kd_key_off.as<uint32_t>(), s->rd_val_off.as<uint32_t>(), s->rd_vals.as<uint32_t>(), wo_off,
-                           view_of(s), words, aoi);
+                           cd.kd_key_off, cd.rd_val_off, cd.rd_vals, wo_off, view_of(s), words, aoi);
     return ACCORD_OK;
 }
 

@@ -144,6 +144,7 @@ struct accord_store {
     // set; ds_cur >= 0 makes ds[ds_cur] the store's current deps
     DepSet ds[2];
     int ds_cur = -1;
+    bool ds_rb = false;            // ds[ds_cur] is this batch's deps united with RedundantBefore.collectDeps
     DevBuf op_tmp[24];
     // MaxConflicts (maxconflicts.hip): per-key map (double-buffered) and the last fold's outputs
     DevBuf mc_state, mc_state2, mc_out, mc_cnt, mc_po;   // + per-txn pair counts / offsets of a pass
@@ -200,6 +201,13 @@ int32_t ready_track_batch(accord_store *s);
 void ready_destroy(accord_store *s);
 // RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp)
 int32_t redundant_apply(accord_store *s);
+// The batch's current deps (device): the pipeline's own output, or its RedundantBefore union.
+struct CurDeps {
+    const uint32_t *kd_key_off, *kd_keys, *kd_val_off, *kd_vals, *kd_k2v_off, *kd_k2v;
+    const uint32_t *rd_val_off, *rd_vals;
+    uint64_t tot_keys, tot_vals, tot_k2v, tot_rvals;
+};
+CurDeps cur_deps(const accord_store *s);
 }
 using accord_impl::fail;
 

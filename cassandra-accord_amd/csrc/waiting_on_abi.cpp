@@ -109,8 +109,10 @@ int32_t accord_waiting_on_initialise(accord_store *s)
         return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise needs a registered-status store "
                                          "(resident, window ACCORD_WINDOW_NONE)");
     if (!s->computed) return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise before accord_deps_compute");
-    if (s->merged || s->ds_cur >= 0)
-        return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise runs on the batch's computed deps");
+    if (s->merged || (s->ds_cur >= 0 && !s->ds_rb))
+        return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise runs on the batch's computed deps "
+                                         "(or their RedundantBefore union), not a union / slice result");
+    const accord_impl::CurDeps cd = accord_impl::cur_deps(s);
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     const uint32_t n = s->n;
     hipStream_t st = s->stream;
@@ -121,8 +123,7 @@ int32_t accord_waiting_on_initialise(accord_store *s)
     HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n), s->stream));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     HostTotals *dev = s->status_totals.as<HostTotals>();
-    accord::launch_wo_words_count(n, s->kd_key_off.as<uint32_t>(), s->rd_val_off.as<uint32_t>(),
-                                  s->wo_cnt.as<uint32_t>(), st);
+    accord::launch_wo_words_count(n, cd.kd_key_off, cd.rd_val_off, s->wo_cnt.as<uint32_t>(), st);
     accord::exclusive_scan_u32(s->wo_cnt.as<uint32_t>(), s->wo_off.as<uint32_t>(), n, &dev->totals[0], s->scan_tmp.p, st);
     HIPCHECK(s, hipMemcpyAsync(s->pinned->totals, dev->totals, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));

@@ -407,14 +407,16 @@ int32_t accord_waiting_on_compute(accord_store *store);                 /* devic
  * PREACCEPTED / ACCEPTED, local/CommandsForKey.java:213-215) is treated as uncommitted -- the bit stays
  * set until the dep commits (conservative: never released earlier than the reference).  level = 0,
  * max_level = 0, preds_total = 0 (levelling is accord_waiting_on_compute's model).  Download with
- * accord_waiting_on_download (applied_or_invalidated set). */
+ * accord_waiting_on_download (applied_or_invalidated set).  The deps are the batch's computed deps,
+ * united with RedundantBefore.collectDeps when the store has a RedundantBefore map (the deps
+ * PreAccept returns, messages/PreAccept.java:262-263); a union / slice result is refused. */
 int32_t accord_waiting_on_initialise(accord_store *store);
 
 /* ---- execution readiness: CommandsForKey.notify / notifyUnmanaged and
  * Commands.updateWaitingOn on the device ----
  * accord_waiting_on_initialise also puts the batch's txns into the store's waiting set (with a copy
- * of their deps).  accord_ready_update re-evaluates every waiting txn against the statuses registered
- * so far (accord_txn_register) and returns the txns that became ReadyToExecute (Commands.maybeExecute,
+ * of their deps).  accord_ready_update re-evaluates the waiting txns whose inputs changed (all of
+ * them after a new batch or truncation) against the statuses registered so far (accord_txn_register) and returns the txns that became ReadyToExecute (Commands.maybeExecute,
  * local/Commands.java:656-733: no WaitingOn bit left and status STABLE), ascending global positions;
  * they leave the set (the caller executes them and registers them APPLIED, which in turn releases
  * their dependents at a later call).  Per waiting txn:

@@ -18,7 +18,7 @@ import pytest
 
 from accord_amd import CommandStore, Stream, WINDOW_NONE, generate_stream
 import oracle_lib as O
-from status_events import APPLIED, STABLE
+from status_events import APPLIED, INVALID, STABLE, rb_map
 
 KIND = {"R": 0, "W": 1, "ER": 2, "SP": 3, "XSP": 4}
 
@@ -255,3 +255,70 @@ def test_gpu_all_stable_levels(gpu_device):
     for r, txns in enumerate(rounds):
         got[txns] = r
     assert np.array_equal(got, O.levels_cfk(s, part).astype(np.int64))
+
+
+# ---- RedundantBefore truncation and invalidations under readiness ----
+
+def redundant(s, lo, hi, ks, bound):
+    """RedundantBefore.collectDeps of txns [lo, hi) under the one-entry map (as
+    tests/test_registered_schedule.py)."""
+    return O.redundant_collect(s.prefix(hi), **rb_map(ks, bound), min_epoch=0).txns(lo, hi)
+
+
+def schedule_rb(s, nkeys, bsz, seed, dev=None, inval_frac=0.05, rb_every=3, rounds_per_batch=3):
+    """Batches STABLE at executeAt = TxnId except a few txns INVALIDATED (they never become ready;
+    their dependents stop waiting for them), a few ready -> APPLIED rounds per batch, and every
+    rb_every batches the store's RedundantBefore moves to shardAppliedOrInvalidatedBefore (the
+    first txn not yet APPLIED / INVALID): CommandsForKey.withRedundantBefore truncates the keys'
+    histories (a new carry on the device: everything re-evaluated) and collectDeps adds the bound to
+    the next batches' deps.  Returns every round's ready list, the invalidated txns and the driver."""
+    rng = np.random.default_rng(seed)
+    d = Driver(s, nkeys, dev)
+    out, bound, inval = [], None, []
+    for b, lo in enumerate(range(0, s.n, bsz)):
+        hi = min(s.n, lo + bsz)
+        part = d.ora.batch(s.slice(lo, hi))
+        if bound is not None:
+            part = O.deps_union([part, redundant(s, lo, hi, nkeys, bound)])
+        if dev is not None:
+            got = dev.calculate_deps_batch(s.slice(lo, hi))
+            assert got.first_difference(part) is None, got.first_difference(part)
+        d.status[lo:hi] = 2
+        idx = np.arange(lo, hi)
+        bad = rng.random(hi - lo) < inval_frac
+        d.register(idx[~bad], STABLE)
+        d.register(idx[bad], INVALID)
+        inval.extend(idx[bad].tolist())
+        d.initialise(lo, part)
+        for _ in range(rounds_per_batch):
+            r = d.round()
+            out.append(r)
+            d.apply(r)
+        if b % rb_every == rb_every - 1:
+            done = (d.status[:hi] == APPLIED) | (d.status[:hi] == INVALID)
+            p = int(np.argmin(done)) if not done.all() else hi - 1
+            if p > 0 and (bound is None or p > bound):
+                m = rb_map(nkeys, p)
+                d.ora.truncate(m["start"], m["end"], m["bound"])
+                if dev is not None:
+                    dev.redundant_before(**m, min_epoch=0)
+                bound = p
+    out.extend(drain(d))
+    return out, np.array(sorted(inval), np.int64), d
+
+
+def test_schedule_rb_oracle_progress():
+    s = stable_stream(1800, 40, 10)
+    out, inval, d = schedule_rb(s, 40, 300, 10)
+    allr = np.concatenate(out)
+    assert np.array_equal(np.sort(np.concatenate([allr, inval])), np.arange(s.n))
+    assert d.ora.waiting == inval.size                   # invalidated txns never become ready
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ks,bsz,seed", [(3000, 60, 300, 11), (5000, 300, 500, 12)])
+def test_gpu_schedule_rb_equals_oracle(gpu_device, n, ks, bsz, seed):
+    s = stable_stream(n, ks, seed)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=ks, window=WINDOW_NONE, resident=True) as dev:
+        out, inval, d = schedule_rb(s, ks, bsz, seed, dev)
+    assert np.array_equal(np.sort(np.concatenate(out + [inval])), np.arange(n))
