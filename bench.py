@@ -22,6 +22,7 @@ import json
 import os
 import sys
 import time
+import types
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
@@ -87,6 +88,9 @@ def main():
                          "schedule: batches registered STABLE, ready txns registered APPLIED round by round")
     ap.add_argument("--ready-batch", type=int, default=4096, help="txns per batch of the --ready leg")
     ap.add_argument("--ready-batches", type=int, default=16, help="batches of the --ready leg")
+    ap.add_argument("--ready-cpu-batch", type=int, default=2048,
+                    help="--ready: one batch of this many txns drained by the oracle's readiness restatement "
+                         "(CPU) and by the device (0: skip)")
     ap.add_argument("--reg-batch", type=int, default=1024, help="txns per batch of the --registered leg")
     ap.add_argument("--reg-batches", type=int, default=64, help="batches of the --registered leg")
     args = ap.parse_args()
@@ -227,6 +231,9 @@ def main():
             registered = registered_batches(s, args)
         if s.rng_off[-1] == 0 and args.ready:
             ready = ready_schedule(s, args)
+            if args.ready_cpu_batch:
+                one = types.SimpleNamespace(ready_batch=args.ready_cpu_batch, ready_batches=1, keyspace=args.keyspace)
+                ready["same_sample"] = {"device": ready_schedule(s, one), "cpu_baseline": ready_cpu(s, args)}
 
     if rank != 0:
         store.close()
@@ -507,6 +514,40 @@ def ready_schedule(s, args, rounds_per_batch=4):
             "release_rounds": rounds, "update_ms_per_call": upd_ms / max(1, calls),
             "released_txns_per_s_update_wall": released / (upd_ms * 1e-3) if upd_ms else None,
             "apply_register_ms_total": app_ms}
+
+
+def ready_cpu(s, args):
+    """CPU baseline of the readiness leg: the oracle's restatement (or_lstore_ready over literal
+    CommandsForKey objects: the count test of every waiting txn at every call, one thread) draining
+    one batch of --ready-cpu-batch txns registered STABLE -- the same schedule the device runs beside
+    it ("device" in the same dict)."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        bsz = min(args.ready_cpu_batch, s.n)
+        L = oracle_lib.LStore(args.keyspace)
+        idx = np.arange(bsz)
+        part = L.batch(s.slice(0, bsz))
+        L.register(s.msb[idx], s.lsb[idx], s.node[idx], np.full(bsz, ST_STABLE, np.uint8), s.msb[idx], s.lsb[idx],
+                   s.node[idx])
+        L.waiting_add(0, part)
+        upd, calls, released = 0.0, 0, 0
+        for _ in range(100000):
+            t0 = time.perf_counter()
+            r = L.ready()
+            upd += time.perf_counter() - t0
+            calls += 1
+            if r.size == 0:
+                break
+            released += r.size
+            L.register(s.msb[r], s.lsb[r], s.node[r], np.full(r.size, ST_APPLIED, np.uint8), s.msb[r], s.lsb[r], s.node[r])
+        L.close()
+        return {"value": released / upd if upd else None, "unit": "released txns/s (ready calls)", "cores": 1,
+                "kind": "port", "update_calls": calls, "update_ms_per_call": upd * 1e3 / max(1, calls),
+                "sample": f"one batch of {bsz} config-2 txns STABLE at TxnId, drained ready -> APPLIED; literal "
+                          f"restatement, every waiting txn re-tested per call ({upd:.1f} s)"}
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "sample": f"failed: {e}"}
 
 
 def measured_traffic(config):
