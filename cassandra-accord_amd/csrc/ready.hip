@@ -38,6 +38,8 @@
 #include "status_view.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -99,11 +101,12 @@ struct KeyPart {
 };
 
 // Dirty keys (dirty != nullptr): a carried entry whose txn changed since epoch `seen` marks its key
-// with this call's id and appends it to list[] once.
+// with this call's id and appends it to list[] once (its summary is recomputed); one that became
+// committed (or invalid) marks it in eval[] (the "dep uncommitted" tests of its waiters may change).
 struct DirtyMark {
-    const uint32_t *chg;
+    const uint32_t *chg, *cchg;
     uint32_t seen, call;
-    uint32_t *dirty, *list, *cnt;
+    uint32_t *dirty, *list, *cnt, *eval;
 };
 
 __global__ __launch_bounds__(256) void rd_part_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
@@ -122,6 +125,7 @@ __global__ __launch_bounds__(256) void rd_part_kernel(uint32_t C, const uint32_t
             const uint32_t st = kind == 2u ? ST_INVALID : status_of(v, g);
             if (dm.dirty && dm.chg[g] > dm.seen && dm.dirty[key] != dm.call && atomicExch(&dm.dirty[key], dm.call) != dm.call)
                 dm.list[atomicAdd(dm.cnt, 1u)] = key;
+            if (dm.dirty && dm.cchg[g] > dm.seen) dm.eval[key] = dm.call;
             if (st < ST_COMMITTED) mu = g;
             else if (st < ST_APPLIED) cc[kind_class(kind)] = Cand{g, exec_of(v, g)};
         }
@@ -143,12 +147,14 @@ __global__ __launch_bounds__(256) void rd_part_kernel(uint32_t C, const uint32_t
     }
 }
 
-// every key (list == nullptr), or the dirty keys list[0 .. *cnt)
+// every key (list == nullptr), or the dirty keys list[0 .. *cnt): a key whose summary changed is
+// marked in eval[] with this call's id (its waiters' tests read the summary)
 __global__ __launch_bounds__(256) void rd_summary_kernel(uint32_t nkeys, const uint32_t *__restrict__ kseg0,
                                                          const uint32_t *__restrict__ kseg1,
                                                          const KeyPart *__restrict__ part, StatusView v,
                                                          KeySummary *__restrict__ sum, const uint32_t *__restrict__ list,
-                                                         const uint32_t *__restrict__ cnt)
+                                                         const uint32_t *__restrict__ cnt, uint32_t *__restrict__ eval,
+                                                         uint32_t call)
 {
     const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
     const uint32_t m = list ? *cnt : nkeys;
@@ -186,6 +192,12 @@ __global__ __launch_bounds__(256) void rd_summary_kernel(uint32_t nkeys, const u
             for (int c = 0; c < 3; ++c) s.min_cls[c] = cc[c].g;
             s.next = nx.g;                           // nulled by the evaluation (TxnId order)
             s.min_unc = mu;
+            if (list) {
+                const KeySummary o = sum[k];
+                if (o.min_cls[0] != s.min_cls[0] || o.min_cls[1] != s.min_cls[1] || o.min_cls[2] != s.min_cls[2] ||
+                    o.next != s.next || o.min_unc != s.min_unc)
+                    eval[k] = call;
+            }
             sum[k] = s;
         }
     }
@@ -435,6 +447,12 @@ struct ReadyGen {
 
 void ready_destroy(accord_store *s)
 {
+    if (s->rdy_stats && s->rdy_stats[0])
+        fprintf(stderr, "ready stats: calls %llu dirty keys %llu waiting-set scans %llu evaluated %llu\n",
+                (unsigned long long)s->rdy_stats[0], (unsigned long long)s->rdy_stats[1],
+                (unsigned long long)s->rdy_stats[2], (unsigned long long)s->rdy_stats[3]);
+    delete[] s->rdy_stats;
+    s->rdy_stats = nullptr;
     for (ReadyGen *r : s->rdy_gens) { r->release(); delete r; }
     s->rdy_gens.clear();
     s->rdy_waiting = 0;
@@ -530,12 +548,14 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     v.known = s->rg_known;
     HIPCHECK(s, s->rdy_part.ensure((size_t)C * sizeof(KeyPart) + 64));
     HIPCHECK(s, s->rdy_dirty.ensure_zeroed((size_t)nkeys * 4 + 4, st));
+    HIPCHECK(s, s->rdy_dirty2.ensure_zeroed((size_t)nkeys * 4 + 4, st));
     HIPCHECK(s, s->rdy_dlist.ensure((size_t)nkeys * 4 + 4));
     uint32_t *cnt = s->rdy_out.as<uint32_t>(), *list = cnt + HDR;    // cnt[0]: ready txns, cnt[1]: dirty keys
     DirtyMark dm{};
     if (!full) {
-        dm.chg = s->rg_chg.as<uint32_t>(); dm.seen = seen; dm.call = call;
+        dm.chg = s->rg_chg.as<uint32_t>(); dm.cchg = s->rg_cchg.as<uint32_t>(); dm.seen = seen; dm.call = call;
         dm.dirty = s->rdy_dirty.as<uint32_t>(); dm.list = s->rdy_dlist.as<uint32_t>(); dm.cnt = cnt + 1;
+        dm.eval = s->rdy_dirty2.as<uint32_t>();
     }
     if (C) hipLaunchKernelGGL(rd_part_kernel, dim3(grid_for_waves((C + 63) / 64)), dim3(256), 0, st, C,
                               s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), v, s->rdy_part.as<KeyPart>(), dm);
@@ -551,7 +571,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     if (nkeys) hipLaunchKernelGGL(rd_summary_kernel, dim3(full ? grid_for_waves(nkeys) : std::min(grid_for_waves(nkeys), 256u)),
                                   dim3(256), 0, st, nkeys, s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>(),
                                   s->rdy_part.as<KeyPart>(), v, s->rdy_sum.as<KeySummary>(),
-                                  full ? nullptr : s->rdy_dlist.as<uint32_t>(), cnt + 1);
+                                  full ? nullptr : s->rdy_dlist.as<uint32_t>(), cnt + 1, s->rdy_dirty2.as<uint32_t>(), call);
     // the generations with txns left, RD_GENS per launch (their parameter table copied to the device)
     std::vector<ReadyLaunch> tabs;
     bool any_inc = false;
@@ -578,7 +598,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.full = full || r->fresh;
         any_inc |= !p.full;
         p.seen = seen; p.call = call;
-        p.chg = s->rg_chg.as<uint32_t>(); p.dirty = s->rdy_dirty.as<uint32_t>();
+        p.chg = s->rg_chg.as<uint32_t>(); p.dirty = s->rdy_dirty2.as<uint32_t>();
         r->fresh = false;
         L.gbase[L.ngen] = L.total;
         L.total += r->n;
@@ -619,10 +639,17 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         }
     }
     HIPCHECK(s, hipGetLastError());
+    if (!s->rdy_stats && getenv("ACCORD_READY_STATS")) s->rdy_stats = new uint64_t[4]{0, 0, 0, 0};
     uint32_t *peek = (uint32_t *)s->rdy_host;
     HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK)) * 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));       // also: the parameter tables were consumed
     const uint32_t nr = peek[0];
+    if (s->rdy_stats) {                          // ACCORD_READY_STATS: diagnostic totals (ready_destroy prints)
+        s->rdy_stats[0] += 1; s->rdy_stats[1] += peek[1]; s->rdy_stats[2] += cap;
+        if (any_inc && tabs.size() <= HDR - 2)
+            for (size_t i = 0; i < tabs.size(); ++i) s->rdy_stats[3] += peek[2 + i];
+        else s->rdy_stats[3] += cap;
+    }
     s->rdy_list.resize(nr);
     if (nr) {
         if (nr <= PEEK) {

@@ -252,6 +252,7 @@ struct RegParams {
     uint32_t *pos;                     // out: global position of every event
     accord::DevStatus *err;
     uint32_t *chg;                     // by global position: the registration epoch of its last change
+    uint32_t *cchg;                    // ... of its last change from uncommitted to committed / invalid
     uint32_t epoch;
 };
 
@@ -306,9 +307,10 @@ __global__ __launch_bounds__(256) void reg_erase_ranges_kernel(RegParams p, uint
 __global__ __launch_bounds__(256) void reg_apply_kernel(RegParams p)
 {
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += gridDim.x * blockDim.x) {
-        const uint32_t g = p.pos[r], nw = p.status[r];
+        const uint32_t g = p.pos[r], nw = p.status[r], cur = p.st[g];
         p.st[g] = (uint8_t)nw;
         p.chg[g] = p.epoch;                 // readiness re-evaluates the keys of changed txns
+        if (cur < ST_COMMITTED && nw >= ST_COMMITTED) p.cchg[g] = p.epoch;
         if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) { p.xmsb[g] = p.emsb[r]; p.xlsb[g] = p.elsb[r]; p.xnode[g] = p.enode[r]; }
     }
 }
@@ -689,7 +691,9 @@ int32_t status_join_batch(accord_store *s)
     HIPCHECK(s, grow_keep(s->rg_elsb, G * 8, known * 8, st));
     HIPCHECK(s, grow_keep(s->rg_enode, G * 4, known * 4, st));
     HIPCHECK(s, grow_keep(s->rg_chg, G * 4, known * 4, st));
+    HIPCHECK(s, grow_keep(s->rg_cchg, G * 4, known * 4, st));
     if (G > known) HIPCHECK(s, hipMemsetAsync(s->rg_chg.as<uint32_t>() + known, 0, (G - known) * 4, st));
+    if (G > known) HIPCHECK(s, hipMemsetAsync(s->rg_cchg.as<uint32_t>() + known, 0, (G - known) * 4, st));
     ++s->rg_epoch;
     if (G > known)   // positions no txn of this store holds (txn_index gaps): never looked at
         HIPCHECK(s, hipMemsetAsync(s->rg_status.as<uint8_t>() + known, ST_PREACCEPTED, G - known, st));
@@ -751,6 +755,7 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     p.pos = T[7].as<uint32_t>();
     p.err = &dev->status;
     p.chg = s->rg_chg.as<uint32_t>();
+    p.cchg = s->rg_cchg.as<uint32_t>();
     p.epoch = s->rg_epoch + 1;
     if (p.tx_n == 0) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: the store holds no txn yet");
     hipLaunchKernelGGL(reg_check_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);

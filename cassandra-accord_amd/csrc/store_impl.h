@@ -114,6 +114,7 @@ struct accord_store {
     DevBuf rg_tmsb, rg_tlsb, rg_tnode, rg_tg, rg_status, rg_emsb, rg_elsb, rg_enode;
     DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound, rg_cwflag, rg_cwoff, rg_cwpos, rg_cwpm;
     DevBuf rg_chg;                 // per global position: the registration epoch of its last status change
+    DevBuf rg_cchg;                // ... of its last change from uncommitted to committed / invalid
     uint32_t rg_epoch = 1;
     uint32_t rg_tx_n = 0, rg_known = 0;
     bool rg_flag_ok = false;       // rg_flag holds this batch's keys-with-registered-status flags
@@ -159,7 +160,7 @@ struct accord_store {
     // execution readiness (ready.hip): the waiting set, one generation per initialised batch
     std::vector<accord_impl::ReadyGen *> rdy_gens;
     uint64_t rdy_waiting = 0;
-    DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dlist, rdy_work, rdy_wcnt;
+    DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dirty2, rdy_dlist, rdy_work, rdy_wcnt;
     uint32_t rdy_call = 0;                    // accord_ready_update calls (ids of the dirty marks)
     uint32_t rdy_seen = 0;                    // rg_epoch the last accord_ready_update saw
     uint64_t rdy_sum_version = ~0ull;         // carry version the key summaries belong to
@@ -167,6 +168,7 @@ struct accord_store {
     void *rdy_host = nullptr;                 // page-locked: the ready count + list readback
     void *rdy_tab_host = nullptr;             // pinned staging of the evaluation launch tables
     size_t rdy_tab_cap = 0;
+    uint64_t *rdy_stats = nullptr;            // ACCORD_READY_STATS diagnostics
     std::vector<uint32_t> rdy_kb_host;       // per key: shardRedundantBefore as a position (cumulative max)
     bool rdy_kb_dirty = false;
     std::vector<uint32_t> rdy_list;          // the last accord_ready_update's ready txns
