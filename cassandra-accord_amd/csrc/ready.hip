@@ -100,9 +100,11 @@ struct KeyPart {
     uint32_t unc;
 };
 
-// Dirty keys (dirty != nullptr): a carried entry whose txn changed since epoch `seen` marks its key
-// with this call's id and appends it to list[] once (its summary is recomputed); one that became
-// committed (or invalid) marks it in eval[] (the "dep uncommitted" tests of its waiters may change).
+// Incremental calls (dirty != nullptr): a carried entry whose txn changed since epoch `seen` marks
+// its key with this call's id and appends it to list[] once (its summary is recomputed); one that
+// became committed (or invalid) marks it in eval[] (the "dep uncommitted" tests of its waiters may
+// change); only the 64-entry chunks holding a changed entry recompute their partials (part[] keeps
+// the others' from earlier calls of the same carry).
 struct DirtyMark {
     const uint32_t *chg, *cchg;
     uint32_t seen, call;
@@ -119,15 +121,26 @@ __global__ __launch_bounds__(256) void rd_part_kernel(uint32_t C, const uint32_t
         uint32_t key = NONE;
         Cand cc[3] = {{NONE, {0, 0, 0}}, {NONE, {0, 0, 0}}, {NONE, {0, 0, 0}}};
         uint32_t mu = NONE;
-        if (x < C) {
-            key = ckey[x];
-            const uint32_t e = cent[x], g = e & ENT_TXN_MASK, kind = e >> ENT_KIND_SHIFT;
-            const uint32_t st = kind == 2u ? ST_INVALID : status_of(v, g);
-            if (dm.dirty && dm.chg[g] > dm.seen && dm.dirty[key] != dm.call && atomicExch(&dm.dirty[key], dm.call) != dm.call)
+        const uint32_t e = x < C ? cent[x] : 0u, g = e & ENT_TXN_MASK, kind = e >> ENT_KIND_SHIFT;
+        if (x < C) key = ckey[x];
+        if (dm.dirty) {
+            // incremental call: a chunk none of whose entries changed keeps its partials
+            const bool ch = x < C && dm.chg[g] > dm.seen;
+            if (__ballot(ch) == 0ull) continue;                  // wave-uniform
+            if (ch && dm.dirty[key] != dm.call && atomicExch(&dm.dirty[key], dm.call) != dm.call)
                 dm.list[atomicAdd(dm.cnt, 1u)] = key;
-            if (dm.dirty && dm.cchg[g] > dm.seen) dm.eval[key] = dm.call;
+            if (ch && dm.cchg[g] > dm.seen) dm.eval[key] = dm.call;
+        }
+        if (x < C) {
+            const uint32_t st = kind == 2u ? ST_INVALID : status_of(v, g);
             if (st < ST_COMMITTED) mu = g;
-            else if (st < ST_APPLIED) cc[kind_class(kind)] = Cand{g, exec_of(v, g)};
+            else if (st < ST_APPLIED) {
+                const Cand me{g, exec_of(v, g)};
+                const uint32_t kc = kind_class(kind);
+#pragma unroll
+                for (uint32_t c = 0; c < 3; ++c)      // static indices: the array stays in registers
+                    if (c == kc) cc[c] = me;
+            }
         }
         // segmented suffix reduction over the run of equal keys (keys ascend inside the chunk)
 #pragma unroll
@@ -165,13 +178,27 @@ __global__ __launch_bounds__(256) void rd_summary_kernel(uint32_t nkeys, const u
         uint32_t mu = NONE;
         // the runs: one starting at a, then one at every multiple of 64 inside (a, b)
         const uint32_t nr = a < b ? 1u + ((b - 1) >> 6) - (a >> 6) : 0u;
-        for (uint32_t j = lane; j < nr; j += 64) {
-            const uint32_t x = j == 0 ? a : ((a >> 6) + j) << 6;
-            const KeyPart q = part[x];
+        constexpr int SB = 4;                        // runs per lane per step: their loads in flight together
+        for (uint32_t j0 = lane; j0 < nr; j0 += 64u * SB) {
+            KeyPart q[SB];
 #pragma unroll
-            for (int c = 0; c < 3; ++c)
-                if (q.cls[c] != NONE) cand_min(cc[c], Cand{q.cls[c], exec_of(v, q.cls[c])});
-            mu = min(mu, q.unc);
+            for (int u = 0; u < SB; ++u) {
+                const uint32_t j = j0 + 64u * u;
+                const uint32_t x = j == 0 ? a : ((a >> 6) + j) << 6;
+                q[u] = j < nr ? part[x] : KeyPart{{NONE, NONE, NONE}, NONE};
+            }
+            Cand cq[SB][3];
+#pragma unroll
+            for (int u = 0; u < SB; ++u)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    cq[u][c] = q[u].cls[c] != NONE ? Cand{q[u].cls[c], exec_of(v, q[u].cls[c])} : Cand{NONE, {0, 0, 0}};
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) cand_min(cc[c], cq[u][c]);
+                mu = min(mu, q[u].unc);
+            }
         }
 #pragma unroll
         for (uint32_t d = 32; d >= 1; d >>= 1) {
@@ -279,8 +306,9 @@ struct ReadyLaunch {
 __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane);
 
 // Incremental calls: a lane per waiting txn keeps those whose inputs changed since the last call
-// (the txn itself, the key of a set key bit dirty, the txn of a set range-dep bit changed) or that
-// were never evaluated; wave-aggregated appends to work[].
+// (the txn itself, the key of a set key bit dirty -- for a managed txn: and no longer blocked by the
+// key's class minima --, the txn of a set range-dep bit changed) or that were never evaluated;
+// wave-aggregated appends to work[].
 __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__restrict__ L)
 {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id();
@@ -292,17 +320,36 @@ __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__res
         const ReadyParams &p = L->g[gi];
         const uint32_t t = u - L->gbase[gi];
         if (!p.done[t]) {
-            need = p.full || p.chg[p.g[t]] > p.seen;
+            const uint32_t g = p.g[t];
+            need = p.full || p.chg[g] > p.seen;
             const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], RK = R + p.key_off[t + 1] - p.key_off[t];
             const uint32_t w0 = p.wo_off[t], nw = p.wo_off[t + 1] - w0;
+            const uint64_t l = p.lsb[t];
+            const uint32_t kind = (uint32_t)(l >> 1) & 7u;
+            const bool managed = (l & 1u) == 0 && kind != 2u;
+            // a managed txn's key bit clears only when STABLE and no witnessed class minimum of the key
+            // executes before it: a dirty key whose minima still block it needs no evaluation
+            const bool stable = managed && !need && status_of(p.v, g) == ST_STABLE;
+            const uint32_t wmask = witness_mask(kind);
+            Ts ex{0, 0, 0};
+            if (stable) ex = exec_of(p.v, g);
             for (uint32_t q = 0; q < nw && !need; ++q) {
                 unsigned long long w = p.words[w0 + q];
                 while (w && !need) {
                     const uint32_t b = q * 64u + (uint32_t)__ffsll((long long)w) - 1u;
                     if (b >= RK) break;
-                    need = b < R ? p.chg[p.rd_vals[p.rd_off[t] + b]] > p.seen
-                                 : p.dirty[p.keys[p.key_off[t] + b - R] - p.key_lo] == p.call;
                     w &= w - 1ull;
+                    if (b < R) { need = p.chg[p.rd_vals[p.rd_off[t] + b]] > p.seen; continue; }
+                    const uint32_t kk = p.keys[p.key_off[t] + b - R] - p.key_lo;
+                    if (p.dirty[kk] != p.call) continue;
+                    if (!managed) { need = true; continue; }
+                    if (!stable) continue;                       // not STABLE: its key bits cannot clear
+                    const KeySummary sm = p.sum[kk];
+                    bool blocked = false;
+                    if (((wmask >> 0) & 1u) && sm.min_cls[0] != NONE && tcmp(exec_of(p.v, sm.min_cls[0]), ex) < 0) blocked = true;
+                    if (!blocked && ((wmask >> 1) & 1u) && sm.min_cls[1] != NONE && tcmp(exec_of(p.v, sm.min_cls[1]), ex) < 0) blocked = true;
+                    if (!blocked && ((wmask >> 3) & 1u) && sm.min_cls[2] != NONE && tcmp(exec_of(p.v, sm.min_cls[2]), ex) < 0) blocked = true;
+                    need = !blocked;
                 }
             }
         }
