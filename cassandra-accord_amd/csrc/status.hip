@@ -164,36 +164,93 @@ __global__ __launch_bounds__(256) void cw_scatter_kernel(uint32_t P, const uint3
         if (flag[x]) pos[off[x]] = x;
 }
 
-// a wave per key: cw_pm over the key's committed Writes, 64 at a time (wave max-scan by executeAt,
-// carrying the previous chunk's maximum)
-__global__ __launch_bounds__(256) void cw_pm_kernel(uint32_t nkeys, const uint32_t *__restrict__ seg_start,
-                                                    const uint32_t *__restrict__ seg_end, const uint32_t *__restrict__ off,
-                                                    const uint32_t *__restrict__ pos, const uint32_t *__restrict__ hist,
-                                                    StatusView v, uint32_t *__restrict__ pm)
+// cw_pm[j] = the argmax by executeAt over the key's committed Writes up to j (ties: the later one;
+// executeAts are unique), as a segmented scan over the index in two passes so a hot key's long run
+// spreads over many waves:
+// cw_local_kernel -- a wave per 64 index entries: the running argmax inside the chunk, restarting at
+//   key changes (keys ascend along the index); per chunk {first key, last key, argmax of its
+//   trailing run};
+// cw_carry_kernel -- a wave per chunk whose first run continues the previous chunk's last one: the
+//   argmax over the run's earlier chunks (their trailing-run argmaxes, 64 chunks per step) merged
+//   into the chunk's first run.
+__device__ __forceinline__ uint32_t cw_total(uint32_t PH, const uint32_t *flag, const uint32_t *off)
 {
+    return PH ? off[PH - 1] + flag[PH - 1] : 0u;
+}
+
+__device__ __forceinline__ bool cw_better(uint32_t a, const Ts &ea, uint32_t b, const Ts &eb)
+{
+    if (a == 0xFFFFFFFFu) return false;
+    if (b == 0xFFFFFFFFu) return true;
+    const int c = tcmp(ea, eb);
+    return c > 0 || (c == 0 && a > b);
+}
+
+__global__ __launch_bounds__(256) void cw_local_kernel(uint32_t PH, const uint32_t *__restrict__ flag,
+                                                       const uint32_t *__restrict__ off, const uint32_t *__restrict__ pos,
+                                                       const uint32_t *__restrict__ hist, const uint32_t *__restrict__ skey,
+                                                       StatusView v, uint32_t *__restrict__ pm, uint4 *__restrict__ chunk)
+{
+    const uint32_t J = cw_total(PH, flag, off);
     const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t k = blockIdx.x * (blockDim.x / 64) + wave_id(); k < nkeys; k += waves) {
-        const uint32_t a = seg_start[k], c = seg_end[k];
-        if (c <= a) continue;
-        const uint32_t j0 = off[a], j1 = off[c];
-        uint32_t carry = 0xFFFFFFFFu;
-        Ts cex{0, 0, 0};
-        for (uint32_t b = j0; b < j1; b += 64) {
-            const uint32_t j = b + lane;
-            uint32_t m = j < j1 ? j : 0xFFFFFFFFu;
-            Ts ex = j < j1 ? exec_of(v, hist[pos[j]] & ENT_TXN_MASK) : Ts{0, 0, 0};
+    for (uint32_t c0 = (blockIdx.x * (blockDim.x / 64) + wave_id()) * 64u; c0 < J; c0 += waves * 64u) {
+        const uint32_t j = c0 + lane;
+        const bool valid = j < J;
+        const uint32_t x = valid ? pos[j] : 0u;
+        const uint32_t key = valid ? skey[x] : 0xFFFFFFFFu;
+        uint32_t m = valid ? j : 0xFFFFFFFFu;
+        Ts ex = valid ? exec_of(v, hist[x] & ENT_TXN_MASK) : Ts{0, 0, 0};
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t om = (uint32_t)__shfl_up((int)m, d, 64);
-                const Ts oe{(uint64_t)__shfl_up((long long)ex.msb, d, 64), (uint64_t)__shfl_up((long long)ex.lsb, d, 64),
-                            __shfl_up(ex.node, d, 64)};
-                if (lane >= (uint32_t)d && om != 0xFFFFFFFFu && (m == 0xFFFFFFFFu || tcmp(oe, ex) > 0)) { m = om; ex = oe; }
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t om = (uint32_t)__shfl_up((int)m, d, 64), ok = (uint32_t)__shfl_up((int)key, d, 64);
+            const Ts oe{(uint64_t)__shfl_up((long long)ex.msb, d, 64), (uint64_t)__shfl_up((long long)ex.lsb, d, 64),
+                        __shfl_up(ex.node, d, 64)};
+            if (lane >= (uint32_t)d && ok == key && cw_better(om, oe, m, ex)) { m = om; ex = oe; }
+        }
+        if (valid) pm[j] = m;
+        const int last = (int)min(63u, J - 1u - c0);
+        const uint32_t kl = readlane(key, last), ml = readlane(m, last), kf = readlane(key, 0);
+        if (lane == 0) chunk[c0 >> 6] = make_uint4(kf, kl, ml, 0u);
+    }
+}
+
+__global__ __launch_bounds__(256) void cw_carry_kernel(uint32_t PH, const uint32_t *__restrict__ flag,
+                                                       const uint32_t *__restrict__ off, const uint32_t *__restrict__ pos,
+                                                       const uint32_t *__restrict__ hist, const uint32_t *__restrict__ skey,
+                                                       StatusView v, const uint4 *__restrict__ chunk,
+                                                       uint32_t *__restrict__ pm)
+{
+    const uint32_t J = cw_total(PH, flag, off), nch = (J + 63u) / 64u;
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t c = blockIdx.x * (blockDim.x / 64) + wave_id(); c < nch; c += waves) {
+        const uint32_t kf = chunk[c].x;
+        if (c == 0 || chunk[c - 1].y != kf) continue;             // wave-uniform: the run starts here
+        uint32_t best = 0xFFFFFFFFu;
+        Ts bex{0, 0, 0};
+        for (uint32_t top = c; top > 0; top = top > 64u ? top - 64u : 0u) {   // chunks top-1 .. top-64
+            const bool in = lane < top;
+            const uint4 q = in ? chunk[top - 1 - lane] : make_uint4(0u, 0u, 0u, 0u);
+            const bool same = in && q.y == kf;                       // its trailing run is this key's
+            const bool stop = !same || q.x != kf;                    // ... and the run starts inside it
+            const unsigned long long sm = __ballot(stop);
+            const uint32_t first = sm ? (uint32_t)__builtin_ctzll(sm) : 64u;
+            if ((lane < first || lane == first) && same) {
+                const Ts e = exec_of(v, hist[pos[q.z]] & ENT_TXN_MASK);
+                if (cw_better(q.z, e, best, bex)) { best = q.z; bex = e; }
             }
-            if (carry != 0xFFFFFFFFu && (m == 0xFFFFFFFFu || tcmp(cex, ex) > 0)) { m = carry; ex = cex; }
-            if (j < j1) pm[j] = m;
-            carry = readlane(m, 63);
-            cex = Ts{(uint64_t)__shfl((long long)ex.msb, 63, 64), (uint64_t)__shfl((long long)ex.lsb, 63, 64),
-                     __shfl(ex.node, 63, 64)};
+            if (sm) break;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t ob = (uint32_t)__shfl_xor((int)best, d, 64);
+            const Ts oe{(uint64_t)__shfl_xor((long long)bex.msb, d, 64), (uint64_t)__shfl_xor((long long)bex.lsb, d, 64),
+                        __shfl_xor(bex.node, d, 64)};
+            if (cw_better(ob, oe, best, bex)) { best = ob; bex = oe; }
+        }
+        const uint32_t j = c * 64u + lane;
+        if (best != 0xFFFFFFFFu && j < J && skey[pos[j]] == kf) {    // the chunk's first run
+            const uint32_t m = pm[j];
+            if (cw_better(best, bex, m, exec_of(v, hist[pos[m]] & ENT_TXN_MASK))) pm[j] = best;
         }
     }
 }
@@ -574,9 +631,14 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
         HostTotals *dv = s->status_totals.as<HostTotals>();
         accord::exclusive_scan_u32(flag, off, PH, &dv->totals[9], s->scan_tmp.p, st);
         hipLaunchKernelGGL(cw_scatter_kernel, dim3(grid_for(PH)), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>());
-        hipLaunchKernelGGL(cw_pm_kernel, dim3(std::min<uint32_t>((nkeys + 3) / 4, 8192u)), dim3(256), 0, st, nkeys,
-                           s->seg_start.as<uint32_t>(), s->seg_end.as<uint32_t>(), off, s->rg_cwpos.as<uint32_t>(),
-                           s->hist.as<uint32_t>(), v, s->rg_cwpm.as<uint32_t>());
+        HIPCHECK(s, s->rg_cwchunk.ensure(((size_t)PH / 64 + 2) * sizeof(uint4)));
+        const uint32_t cwb = std::min<uint32_t>((PH / 64 + 4) / 4, 8192u);
+        hipLaunchKernelGGL(cw_local_kernel, dim3(cwb), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>(),
+                           s->hist.as<uint32_t>(), s->sort_key.as<uint32_t>(), v, s->rg_cwpm.as<uint32_t>(),
+                           s->rg_cwchunk.as<uint4>());
+        hipLaunchKernelGGL(cw_carry_kernel, dim3(cwb), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>(),
+                           s->hist.as<uint32_t>(), s->sort_key.as<uint32_t>(), v, s->rg_cwchunk.as<uint4>(),
+                           s->rg_cwpm.as<uint32_t>());
         g.cw_off = off; g.cw_pos = s->rg_cwpos.as<uint32_t>(); g.cw_pm = s->rg_cwpm.as<uint32_t>();
     }
     const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);     // a wave per txn
