@@ -62,6 +62,9 @@ struct GenParams {
     // cw_pos[j] = the j-th one's position, cw_pm[j] = the one with the latest executeAt among its key's
     // up to j (CommandsForKey.committed, local/CommandsForKey.java:462-469)
     const uint32_t *cw_off, *cw_pos, *cw_pm;
+    // per history position (hx_*): hx = the committed entry of [key's first entry, x] executing last
+    // (NONE: none), hu = the uncommitted entries there; skey = each position's key
+    const uint32_t *hx, *hu, *skey;
 };
 
 // One pair, one wave (lanes stride over the pair's slice [lo, pos) of the key's history):
@@ -111,10 +114,39 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q, uint32_
         return !(committed(st) && has_mcb && tcmp(exec_of(p.v, g), mcb) < 0);
     };
     if (!FILL) {
+        // skip the prefix [lo, F) of the slice whose committed entries all execute before
+        // maxCommittedBefore and that holds no uncommitted entry: nothing in it is emitted.  F = the
+        // first position whose running latest-executing committed entry reaches maxCommittedBefore
+        // (monotone), found by a 64-way search.
+        uint32_t start = lo;
+        if (has_mcb && p.hx && hi > lo) {
+            uint32_t L = lo, H = hi;
+            while (L < H) {                                            // wave-uniform
+                const uint32_t step = (H - L + 63u) / 64u, y = L + lane * step;
+                bool reach = false;
+                if (y < H) {
+                    const uint32_t m = p.hx[y];
+                    reach = m != 0xFFFFFFFFu && tcmp(exec_of(p.v, p.hist[m] & ENT_TXN_MASK), mcb) >= 0;
+                }
+                const uint64_t bm = __ballot(reach);
+                if (bm == 0ull) {
+                    const uint64_t live = __ballot(y < H);
+                    L = L + (63u - (uint32_t)__builtin_clzll(live)) * step + 1u;
+                } else {
+                    const uint32_t f = (uint32_t)__builtin_ctzll(bm);
+                    H = L + f * step;
+                    if (f) L = L + (f - 1u) * step + 1u;
+                }
+            }
+            if (L > lo) {
+                const uint32_t u = p.hu[L - 1] - ((lo > 0 && p.skey[lo - 1] == p.skey[lo]) ? p.hu[lo - 1] : 0u);
+                if (u == 0) start = L;
+            }
+        }
         // emitted count, first emitted position, last witnessed-but-not-emitted position
         uint32_t c = 0, first = hi, last_rej = 0;
         bool any_rej = false;
-        for (uint32_t x = lo + lane; x < hi; x += 64) {
+        for (uint32_t x = start + lane; x < hi; x += 64) {
             const uint32_t e = p.hist[x];
             if (emitted(e)) { ++c; first = min(first, x); }
             else if (witnessed(e)) { any_rej = true; last_rej = max(last_rej, x); }
@@ -251,6 +283,87 @@ __global__ __launch_bounds__(256) void cw_carry_kernel(uint32_t PH, const uint32
         if (best != 0xFFFFFFFFu && j < J && skey[pos[j]] == kf) {    // the chunk's first run
             const uint32_t m = pm[j];
             if (cw_better(best, bex, m, exec_of(v, hist[pos[m]] & ENT_TXN_MASK))) pm[j] = best;
+        }
+    }
+}
+
+// hx / hu (GenParams) in the same two passes as cw_pm: chunk-local segmented scans, then the
+// carries of runs crossing chunks.  chunk = {first key, last key, hx of the trailing run, hu of it}.
+__global__ __launch_bounds__(256) void hx_local_kernel(uint32_t PH, const uint32_t *__restrict__ hist,
+                                                       const uint32_t *__restrict__ skey, StatusView v,
+                                                       uint32_t *__restrict__ hx, uint32_t *__restrict__ hu,
+                                                       uint4 *__restrict__ chunk)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t c0 = (blockIdx.x * (blockDim.x / 64) + wave_id()) * 64u; c0 < PH; c0 += waves * 64u) {
+        const uint32_t x = c0 + lane;
+        const bool valid = x < PH;
+        const uint32_t key = valid ? skey[x] : 0xFFFFFFFFu;
+        const uint32_t g = valid ? hist[x] & ENT_TXN_MASK : 0u, st = valid ? status_of(v, g) : ST_INVALID;
+        uint32_t m = valid && committed(st) ? x : 0xFFFFFFFFu;
+        uint32_t u = valid && st < ST_COMMITTED ? 1u : 0u;
+        Ts ex = m != 0xFFFFFFFFu ? exec_of(v, g) : Ts{0, 0, 0};
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t om = (uint32_t)__shfl_up((int)m, d, 64), ok = (uint32_t)__shfl_up((int)key, d, 64);
+            const uint32_t ou = (uint32_t)__shfl_up((int)u, d, 64);
+            const Ts oe{(uint64_t)__shfl_up((long long)ex.msb, d, 64), (uint64_t)__shfl_up((long long)ex.lsb, d, 64),
+                        __shfl_up(ex.node, d, 64)};
+            if (lane >= (uint32_t)d && ok == key) {
+                u += ou;
+                if (cw_better(om, oe, m, ex)) { m = om; ex = oe; }
+            }
+        }
+        if (valid) { hx[x] = m; hu[x] = u; }
+        const int last = (int)min(63u, PH - 1u - c0);
+        const uint32_t kl = readlane(key, last), ml = readlane(m, last), ul = readlane(u, last), kf = readlane(key, 0);
+        if (lane == 0) chunk[c0 >> 6] = make_uint4(kf, kl, ml, ul);
+    }
+}
+
+__global__ __launch_bounds__(256) void hx_carry_kernel(uint32_t PH, const uint32_t *__restrict__ hist,
+                                                       const uint32_t *__restrict__ skey, StatusView v,
+                                                       const uint4 *__restrict__ chunk, uint32_t *__restrict__ hx,
+                                                       uint32_t *__restrict__ hu)
+{
+    const uint32_t nch = (PH + 63u) / 64u;
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t c = blockIdx.x * (blockDim.x / 64) + wave_id(); c < nch; c += waves) {
+        const uint32_t kf = chunk[c].x;
+        if (c == 0 || chunk[c - 1].y != kf) continue;             // wave-uniform: the run starts here
+        uint32_t best = 0xFFFFFFFFu, cnt = 0;
+        Ts bex{0, 0, 0};
+        for (uint32_t top = c; top > 0; top = top > 64u ? top - 64u : 0u) {
+            const bool in = lane < top;
+            const uint4 q = in ? chunk[top - 1 - lane] : make_uint4(0u, 0u, 0u, 0u);
+            const bool same = in && q.y == kf;
+            const bool stop = !same || q.x != kf;
+            const unsigned long long sm = __ballot(stop);
+            const uint32_t first = sm ? (uint32_t)__builtin_ctzll(sm) : 64u;
+            if (lane <= first && same) {
+                cnt += q.w;
+                if (q.z != 0xFFFFFFFFu) {
+                    const Ts e = exec_of(v, hist[q.z] & ENT_TXN_MASK);
+                    if (cw_better(q.z, e, best, bex)) { best = q.z; bex = e; }
+                }
+            }
+            if (sm) break;
+        }
+        cnt = wave_sum(cnt);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t ob = (uint32_t)__shfl_xor((int)best, d, 64);
+            const Ts oe{(uint64_t)__shfl_xor((long long)bex.msb, d, 64), (uint64_t)__shfl_xor((long long)bex.lsb, d, 64),
+                        __shfl_xor(bex.node, d, 64)};
+            if (cw_better(ob, oe, best, bex)) { best = ob; bex = oe; }
+        }
+        const uint32_t x = c * 64u + lane;
+        if (x < PH && skey[x] == kf) {                                // the chunk's first run
+            hu[x] += cnt;
+            const uint32_t m = hx[x];
+            if (best != 0xFFFFFFFFu &&
+                cw_better(best, bex, m, m != 0xFFFFFFFFu ? exec_of(v, hist[m] & ENT_TXN_MASK) : Ts{0, 0, 0}))
+                hx[x] = best;
         }
     }
 }
@@ -640,6 +753,15 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
                            s->hist.as<uint32_t>(), s->sort_key.as<uint32_t>(), v, s->rg_cwchunk.as<uint4>(),
                            s->rg_cwpm.as<uint32_t>());
         g.cw_off = off; g.cw_pos = s->rg_cwpos.as<uint32_t>(); g.cw_pm = s->rg_cwpm.as<uint32_t>();
+        HIPCHECK(s, s->rg_hx.ensure((size_t)PH * 4 + 4));
+        HIPCHECK(s, s->rg_hu.ensure((size_t)PH * 4 + 4));
+        hipLaunchKernelGGL(hx_local_kernel, dim3(cwb), dim3(256), 0, st, PH, s->hist.as<uint32_t>(),
+                           s->sort_key.as<uint32_t>(), v, s->rg_hx.as<uint32_t>(), s->rg_hu.as<uint32_t>(),
+                           s->rg_cwchunk.as<uint4>());
+        hipLaunchKernelGGL(hx_carry_kernel, dim3(cwb), dim3(256), 0, st, PH, s->hist.as<uint32_t>(),
+                           s->sort_key.as<uint32_t>(), v, s->rg_cwchunk.as<uint4>(), s->rg_hx.as<uint32_t>(),
+                           s->rg_hu.as<uint32_t>());
+        g.hx = s->rg_hx.as<uint32_t>(); g.hu = s->rg_hu.as<uint32_t>(); g.skey = s->sort_key.as<uint32_t>();
     }
     const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);     // a wave per txn
     if (n) hipLaunchKernelGGL(general_kernel<false>, dim3(gw), dim3(256), 0, st, g);

@@ -111,7 +111,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->wo_aoi, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
                       &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
-                      &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2, &s->rg_kbound, &s->rg_cwflag, &s->rg_cwoff, &s->rg_cwpos, &s->rg_cwpm, &s->rg_cwchunk,
+                      &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2, &s->rg_kbound, &s->rg_cwflag, &s->rg_cwoff, &s->rg_cwpos, &s->rg_cwpm, &s->rg_cwchunk, &s->rg_hx, &s->rg_hu,
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
                       &s->rc_end2, &s->rc_kind2, &s->rc_first, &s->rc_flag, &s->rc_offs, &s->rdy_kseg0, &s->rdy_kseg1, &s->rdy_dirty, &s->rdy_dirty2, &s->rg_cchg, &s->rdy_dlist, &s->rdy_work, &s->rdy_wcnt, &s->rg_chg, &s->rdy_part, &s->rdy_sum, &s->rdy_out, &s->rdy_kb, &s->rdy_launch,
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero};

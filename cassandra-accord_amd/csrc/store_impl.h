@@ -112,7 +112,7 @@ struct accord_store {
     // (rg_t*, rg_tx_n entries, rg_tg = global position), InternalStatus + executeAt by global
     // position (rg_known positions), per-batch work
     DevBuf rg_tmsb, rg_tlsb, rg_tnode, rg_tg, rg_status, rg_emsb, rg_elsb, rg_enode;
-    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound, rg_cwflag, rg_cwoff, rg_cwpos, rg_cwpm, rg_cwchunk;
+    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound, rg_cwflag, rg_cwoff, rg_cwpos, rg_cwpm, rg_cwchunk, rg_hx, rg_hu;
     DevBuf rg_chg;                 // per global position: the registration epoch of its last status change
     DevBuf rg_cchg;                // ... of its last change from uncommitted to committed / invalid
     uint32_t rg_epoch = 1;
