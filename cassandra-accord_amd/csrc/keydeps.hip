@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void history_carry_kernel(uint32_t *__restrict
 // when a segment's window reaches past the halo: keys hotter than H2_HALO entries per W txns).
 // Each thread handles H2_ITEMS positions in stages (loads of every item issued before any is
 // consumed), so the dependent round trips are paid once per stage, not once per item.
-constexpr uint32_t H2_THREADS = 256, H2_TILE = 2048, H2_HALO = 2048, H2_ITEMS = H2_TILE / H2_THREADS;
+constexpr uint32_t H2_THREADS = 256, H2_TILE = 512, H2_HALO = 2048, H2_ITEMS = H2_TILE / H2_THREADS;
 
 __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32_t window, const uint32_t *__restrict__ sorted_key,
                                                               const uint32_t *__restrict__ sorted_pair,
