@@ -147,16 +147,17 @@ __global__ __launch_bounds__(256) void accept_bounds_kernel(
 }
 
 // ---- history annotation (key-major) ----
-constexpr int HS_THREADS = 256;
-constexpr int HS_ITEMS = 16;
+constexpr int HS_THREADS = 1024;
+constexpr int HS_ITEMS = 4;
 constexpr uint32_t HS_TILE = HS_THREADS * HS_ITEMS;
 static_assert(HS_TILE == HISTORY_TILE, "history tile");
 
 // Segment bounds per key; tile-local inclusive max-scan of (p+1 if entry p is a Write) -> the last
 // Write at or before p, and tile-local inclusive class counts; both completed by tile carries.
-// hist (key-major entries) comes out of the radix sort.  Every wave owns a contiguous quarter of
-// the tile and scans it in 16 coalesced rounds with wave scans and a running carry held in
-// registers; one block step adds the preceding waves' totals.
+// hist (key-major entries) comes out of the radix sort.  Every wave owns a contiguous sixteenth of
+// the tile and scans it in 4 coalesced rounds with wave scans and a running carry held in
+// registers; one block step adds the preceding waves' totals (16 waves of 4 rows: 50 VGPRs, 8 waves
+// per SIMD; 4 waves of 16 rows held 108 VGPRs, measured 6 us slower on config 2, r03_hs).
 __global__ __launch_bounds__(HS_THREADS) void history1_kernel(uint32_t P, const uint32_t *__restrict__ sorted_key,
                                                               const uint32_t *__restrict__ hist,
                                                               uint32_t *__restrict__ seg_start,
