@@ -7,7 +7,8 @@ history annotation -> per-txn conflict scan + KeyDeps linearisation, count and f
 batch already resident in HBM.  Default workload (BASELINE.json configs[1]): 1,048,576 key txns,
 8 keys each, Zipf(0.99) over 100,000 keys, 50% writes, window W=256, seed 2.
 
-Multi-GPU (`torchrun --nproc-per-node G`, config 4): one global stream of G x 1,048,576 txns
+Multi-GPU (`bench.py --gpus G`, which starts the G ranks itself, or `torchrun --nproc-per-node G`;
+config 4): one global stream of G x 1,048,576 txns
 (weak scaling: every GPU gets a config-2-sized share); the keyspace is split into 8G CommandStores
 by EvenSplit (local/ShardDistributor.java:46-157) and rank r owns the contiguous block of stores
 [8r, 8r+8).  A step is: compute the partial KeyDeps of the txns intersecting the rank's keys, one
@@ -54,6 +55,49 @@ PRESETS = {
 }
 
 
+def launch(gpus, argv, dry_run=False):
+    """`bench.py --gpus G` without a launcher: start G ranks of this script, one process per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = G, rendezvous on 127.0.0.1), before anything in this process
+    touches the GPU -- the parent imports no HIP / torch.cuda / accord_amd.  The parent relays rank
+    0's stdout (the JSON line; every rank's with --launch-dry-run) and exits with the first failing
+    rank's code; a rank that fails ends the others."""
+    import socket
+    import subprocess
+    import tempfile
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs, outs = [], []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        f = tempfile.TemporaryFile(mode="w+")
+        outs.append(f)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, stdout=f))
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            time.sleep(5)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+        if rc == 0 and p.returncode != 0:
+            rc = p.returncode
+    for r, f in enumerate(outs):
+        if r == 0 or dry_run:
+            f.seek(0)
+            sys.stdout.write(f.read())
+        f.close()
+    sys.stdout.flush()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,7 +137,20 @@ def main():
                          "(CPU) and by the device (0: skip)")
     ap.add_argument("--reg-batch", type=int, default=1024, help="txns per batch of the --registered leg")
     ap.add_argument("--reg-batches", type=int, default=64, help="batches of the --registered leg")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="--gpus G > 1: start the G ranks, each prints its rank / world and exits before any GPU work")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, sys.argv[1:], args.launch_dry_run))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}")
+    if args.launch_dry_run:
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "world": int(os.environ.get("WORLD_SIZE", "1")), "master": os.environ.get("MASTER_ADDR"),
+                          "port": os.environ.get("MASTER_PORT"), "gpus": args.gpus}))
+        if os.environ.get("ACCORD_DRY_FAIL_RANK") == os.environ.get("RANK"):
+            sys.exit(3)                 # the launcher's failure path (tests/test_bench_launch.py)
+        return
     preset = PRESETS[args.config]
     for k, v in preset.items():
         if getattr(args, k) is None:
@@ -120,15 +177,20 @@ def main():
     # EvenSplit over [0, keyspace): store b owns [b*ks/S, (b+1)*ks/S); rank r owns stores [8r, 8r+8)
     key_lo = (8 * rank) * args.keyspace // stores_total
     key_hi = (8 * rank + 8) * args.keyspace // stores_total
+    bounds = [b * args.keyspace // stores_total for b in range(stores_total)] + [0xFFFFFFFF]
     s = s_full if world == 1 else s_full.restrict_keys(key_lo, key_hi, drop_empty=True)
 
+    # one store handle per rank hosting its 8 CommandStores (one unbounded store at --gpus 1)
     store = CommandStore(device=0 if world == 1 else local_rank, key_lo=key_lo, key_hi=key_hi,
-                         window=args.window, profile=True)
+                         window=args.window, profile=True,
+                         store_bounds=bounds[8 * rank:8 * rank + 9] if world > 1 else None)
     store.upload(s)
+    rccl = None
     if world > 1:
         uid = [CommandStore.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         store.comm_init(world, rank, uid[0])
+        rccl = store.comm_size()
 
     if args.waiting_on and world > 1:
         raise SystemExit("config 5 levels one full stream per GPU (replicas only): run it with --gpus 1")
@@ -183,6 +245,7 @@ def main():
     hip.hipDeviceSynchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_local = elapsed
     if dist is not None:
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -192,6 +255,12 @@ def main():
         stage[k] /= max(1, args.steps)
     for k in count_detail:
         count_detail[k] /= max(1, args.steps)
+    per_rank = None
+    if dist is not None:
+        mine = {"rank": rank, "rccl": list(rccl), "txns": s.n, "pairs": s.pairs, "compute_ms": stage["total"],
+                "exchange_ms": stage["exchange"], "merge_ms": stage["merge"], "elapsed_s": elapsed_local}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
     # sizes for the byte model: the rank's own computed partial (before the exchange)
     store.compute()
@@ -266,12 +335,13 @@ def main():
         "vs_baseline": None,
         "dtype": "u32/u64 integer",
         "data": "synthetic (SURVEY.md §8d stream, splitmix64 + Zipf rejection-inversion)",
-        "config": {"workload": workload_name(args),
+        "config": {"workload": workload_name(args, world),
                    "n_txns_per_gpu": args.n, "keys_per_txn": args.keys_per_txn, "keyspace": args.keyspace,
                    "zipf": args.zipf, "window": args.window, "seed": args.seed,
                    "n_txns_total": n_total,
                    "gpu_stores": world, "evensplit_stores": stores_total if world > 1 else None,
                    "parallelism": f"keyspace-sharded x{world}" + (" + RCCL exchange/union" if world > 1 else "")},
+        "rccl_ranks": per_rank[0]["rccl"][0] if per_rank else None,
         "deps_per_s": D * world * args.steps / elapsed,
         "sizes": {"N": n, "P": P, "keys_out": kc, "U": U, "D": D},
         "stage_ms": stage,
@@ -290,6 +360,8 @@ def main():
                               "formula": "SURVEY.md §8d B / device time of the whole pipeline"},
         "cpu_baseline": cpu,
     }
+    if per_rank is not None:
+        line["ranks"] = per_rank
     if wo_info is not None:
         line["waiting_on"] = wo_info
     if boundary is not None:
@@ -306,7 +378,11 @@ def main():
         dist.destroy_process_group()
 
 
-def workload_name(args):
+def workload_name(args, world=1):
+    if world > 1:
+        return (f"config4: {world} x {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over "
+                f"{args.keyspace} keys, {8 * world} EvenSplit CommandStores (8 per GPU), W={args.window}; per-rank "
+                f"partial deps + one RCCL exchange + on-device union")
     if args.waiting_on:
         return (f"config5: {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over {args.keyspace} "
                 f"keys, {args.write_frac:.0%} writes, W={args.window}; deps + WaitingOn bitsets + levelling "

@@ -41,6 +41,7 @@ ERR = {
 STORE_PROFILE = 1
 STORE_RESIDENT = 2
 WINDOW_NONE = 0xFFFFFFFF     # no status-at-time model: statuses from CommandStore.register
+KEY_END = 0xFFFFFFFF         # an open upper store bound (accord_store_cfg.store_bounds)
 ST_ERASED = 8                # register(): SaveStatus Erased / Invalidated (range commands leave the range scan)
 
 EXPORTED_SYMBOLS = [
@@ -48,7 +49,7 @@ EXPORTED_SYMBOLS = [
     "accord_deps_batch", "accord_deps_release", "accord_batch_upload", "accord_deps_compute",
     "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
-    "accord_comm_init", "accord_deps_exchange_merge", "accord_deps_exchange_local", "accord_shard_timing",
+    "accord_comm_init", "accord_comm_size", "accord_deps_exchange_merge", "accord_deps_exchange_local", "accord_shard_timing",
     "accord_ready_update",
     "accord_waiting_on_compute", "accord_waiting_on_initialise", "accord_waiting_on_download", "accord_waiting_on_release",
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
@@ -96,7 +97,8 @@ class _MaxConflictsOut(C.Structure):
 
 class _StoreCfg(C.Structure):
     _fields_ = [("device", C.c_int32), ("key_lo", C.c_uint32), ("key_hi", C.c_uint32),
-                ("window", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+                ("window", C.c_uint32), ("flags", C.c_uint32), ("nstores", C.c_uint32),
+                ("store_bounds", _u32p)]
 
 
 class _Batch(C.Structure):
@@ -561,11 +563,18 @@ class CommandStore:
     """One CommandStore == one HIP stream on one device (impl/InMemoryCommandStore.java:89)."""
 
     def __init__(self, device: int = 0, key_lo: int = 0, key_hi: int = 100_000, window: int = 256,
-                 profile: bool = False, resident: bool = False):
+                 profile: bool = False, resident: bool = False, store_bounds=None):
         """resident=True: the store keeps its CommandsForKey state across batches (every batch
-        continues the store's stream; deps values are global stream positions)."""
+        continues the store's stream; deps values are global stream positions).
+        store_bounds: the CommandStores this handle hosts as S + 1 ascending key ordinals (store j
+        owns [b[j], b[j+1]); b[0] == 0 open below, b[S] == KEY_END open above); every range is
+        sliced Minimal to them (impl/InMemoryCommandStore.java:757-760).  None: one unbounded store."""
         flags = (STORE_PROFILE if profile else 0) | (STORE_RESIDENT if resident else 0)
-        cfg = _StoreCfg(device, key_lo, key_hi, window, flags, 0)
+        if store_bounds is None:
+            cfg = _StoreCfg(device, key_lo, key_hi, window, flags, 0, None)
+        else:
+            b = np.ascontiguousarray(store_bounds, np.uint32)
+            cfg = _StoreCfg(device, key_lo, key_hi, window, flags, len(b) - 1, b.ctypes.data_as(_u32p))
         h = C.c_void_p()
         rc = lib().accord_store_create(C.byref(cfg), C.byref(h))
         if rc != ACCORD_OK:
@@ -741,6 +750,12 @@ class CommandStore:
     def comm_init(self, nranks: int, rank: int, uid: bytes):
         buf = C.create_string_buffer(uid, 128)
         self._check(lib().accord_comm_init(self._h, nranks, rank, buf))
+
+    def comm_size(self):
+        """(ranks, rank) of the store's RCCL communicator as RCCL reports them (ncclCommCount)."""
+        a, b = C.c_int32(), C.c_int32()
+        self._check(lib().accord_comm_size(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def exchange_merge(self, n_total: int):
         self._check(lib().accord_deps_exchange_merge(self._h, n_total))

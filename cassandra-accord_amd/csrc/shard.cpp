@@ -475,6 +475,18 @@ int32_t accord_comm_unique_id(void *id128)
     return ACCORD_OK;
 }
 
+int32_t accord_comm_size(accord_store *s, int32_t *nranks, int32_t *rank)
+{
+    if (!s || !nranks || !rank) return fail(s, ACCORD_ERR_ARG, "accord_comm_size: null argument");
+    if (!s->comm || !s->comm->comm) return fail(s, ACCORD_ERR_STATE, "accord_comm_size before accord_comm_init");
+    int cnt = 0, me = 0;
+    ncclResult_t r = ncclCommCount(s->comm->comm, &cnt);
+    if (r == ncclSuccess) r = ncclCommUserRank(s->comm->comm, &me);
+    if (r != ncclSuccess) return fail(s, ACCORD_ERR_HIP, "ncclCommCount: %s", ncclGetErrorString(r));
+    *nranks = cnt; *rank = me;
+    return ACCORD_OK;
+}
+
 int32_t accord_comm_init(accord_store *s, int32_t nranks, int32_t rank, const void *id128)
 {
     if (!s || !id128 || nranks < 1 || rank < 0 || rank >= nranks) return fail(s, ACCORD_ERR_ARG, "accord_comm_init: bad arguments");

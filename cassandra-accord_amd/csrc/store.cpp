@@ -67,6 +67,15 @@ int32_t accord_store_create(const accord_store_cfg *cfg, accord_store **out)
     if (!cfg || !out) return fail(nullptr, ACCORD_ERR_ARG, "accord_store_create: null argument");
     *out = nullptr;
     if (cfg->key_hi <= cfg->key_lo) return fail(nullptr, ACCORD_ERR_ARG, "empty key range [%u,%u)", cfg->key_lo, cfg->key_hi);
+    if (cfg->nstores) {
+        const uint32_t *b = cfg->store_bounds;
+        if (!b) return fail(nullptr, ACCORD_ERR_ARG, "nstores = %u without store_bounds", cfg->nstores);
+        for (uint32_t j = 0; j < cfg->nstores; ++j)
+            if (b[j] >= b[j + 1]) return fail(nullptr, ACCORD_ERR_ARG, "store bounds not ascending at %u", j);
+        if (cfg->key_lo < b[0] || (b[cfg->nstores] != ACCORD_KEY_END && cfg->key_hi > b[cfg->nstores]))
+            return fail(nullptr, ACCORD_ERR_ARG, "key range [%u,%u) outside the stores [%u,%u)", cfg->key_lo,
+                        cfg->key_hi, b[0], b[cfg->nstores]);
+    }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0)
@@ -75,6 +84,8 @@ int32_t accord_store_create(const accord_store_cfg *cfg, accord_store **out)
     accord_store *s = new (std::nothrow) accord_store();
     if (!s) return fail(nullptr, ACCORD_ERR_OOM, "out of host memory");
     s->cfg = *cfg;
+    if (cfg->nstores) s->st_bounds.assign(cfg->store_bounds, cfg->store_bounds + cfg->nstores + 1);
+    s->cfg.store_bounds = nullptr;   // borrowed for the call only
     if ((e = hipSetDevice(cfg->device)) != hipSuccess || (e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete s;
         return fail(nullptr, ACCORD_ERR_HIP, "stream create: %s", hipGetErrorString(e));
@@ -151,8 +162,41 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     if (b->key_off[0] != 0 || (b->rng_off && b->rng_off[0] != 0))
         return fail(s, ACCORD_ERR_ARG, "CSR offsets must start at 0");
     const uint32_t P = b->key_off[n];
-    const uint32_t R = b->rng_off ? b->rng_off[n] : 0;
-    if (R && (!b->rng_start || !b->rng_end)) return fail(s, ACCORD_ERR_ARG, "range CSR without range bounds");
+    const uint32_t *ro = b->rng_off, *rs = b->rng_start, *re = b->rng_end;
+    uint32_t R = ro ? ro[n] : 0;
+    if (R && (!rs || !re)) return fail(s, ACCORD_ERR_ARG, "range CSR without range bounds");
+    if (R && !s->st_bounds.empty()) {
+        // slice every range Minimal to the handle's CommandStores (include/accord_deps.h
+        // accord_store_cfg.store_bounds; AbstractRanges.sliceMinimal, primitives/AbstractRanges.java:
+        // 339-377): the ranges are checked first, so a slice never hides a bad payload
+        for (uint32_t i = 0; i < n; ++i)
+            for (uint32_t r = ro[i]; r < ro[i + 1]; ++r)
+                if (rs[r] >= re[r] || (r > ro[i] && re[r - 1] > rs[r]))
+                    return fail(s, ACCORD_ERR_RANGES, "txn %u: %s", i, code_name(ACCORD_ERR_RANGES));
+        const std::vector<uint32_t> &B = s->st_bounds;
+        const uint32_t S = (uint32_t)B.size() - 1;
+        s->sl_off.resize((size_t)n + 1);
+        s->sl_start.clear(); s->sl_end.clear();
+        s->sl_off[0] = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            for (uint32_t r = ro[i]; r < ro[i + 1]; ++r) {
+                const int64_t a = rs[r], z = re[r];
+                // first store whose upper end (B[j+1] - 1, open at ACCORD_KEY_END) lies above a
+                uint32_t j = (uint32_t)(std::upper_bound(B.begin() + 1, B.end() - 1, (uint32_t)std::min<int64_t>(a + 1, UINT32_MAX)) - B.begin()) - 1;
+                for (; j < S; ++j) {
+                    const int64_t lo = (int64_t)B[j] - 1;
+                    const int64_t hi = B[j + 1] == ACCORD_KEY_END ? INT64_MAX : (int64_t)B[j + 1] - 1;
+                    if (lo >= z) break;
+                    if (!(a < hi && lo < z)) continue;
+                    s->sl_start.push_back((uint32_t)std::max(a, lo));
+                    s->sl_end.push_back((uint32_t)std::min(z, hi));
+                }
+            }
+            s->sl_off[i + 1] = (uint32_t)s->sl_start.size();
+        }
+        ro = s->sl_off.data(); rs = s->sl_start.data(); re = s->sl_end.data();
+        R = ro[n];
+    }
     uint32_t nrt = 0, kinds = 0;
     for (uint32_t i = 0; i < n; ++i) {
         nrt += (uint32_t)(b->lsb[i] & 1);
@@ -162,12 +206,12 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
         return fail(s, ACCORD_ERR_ARG, "txn_index (store subset of a stream) is supported for key txns only");
     s->n = n; s->P = P; s->R = R; s->n_range_txns = nrt; s->b_kinds = kinds;
     s->rk_keys_total = 0;                // sizes the range txns' stored key slices
-    if (nrt && b->rng_off)
+    if (nrt && ro)
         for (uint32_t i = 0; i < n; ++i)
             if (b->lsb[i] & 1)
-                for (uint32_t r = b->rng_off[i]; r < b->rng_off[i + 1]; ++r) {
-                    const uint64_t ks = std::max<uint64_t>((uint64_t)b->rng_start[r] + 1, s->cfg.key_lo);
-                    const uint64_t ke = std::min<uint64_t>(b->rng_end[r], (uint64_t)s->cfg.key_hi - 1);
+                for (uint32_t r = ro[i]; r < ro[i + 1]; ++r) {
+                    const uint64_t ks = std::max<uint64_t>((uint64_t)rs[r] + 1, s->cfg.key_lo);
+                    const uint64_t ke = std::min<uint64_t>(re[r], (uint64_t)s->cfg.key_hi - 1);
                     if (ks <= ke) s->rk_keys_total += ke - ks + 1;
                 }
     if (s->rk_keys_total >= (1ull << 32))
@@ -190,13 +234,13 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     }
     HIPCHECK(s, hipMemcpyAsync(s->key_off.p, b->key_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
     if (P) HIPCHECK(s, hipMemcpyAsync(s->key_ord.p, b->key_ord, (size_t)P * 4, hipMemcpyHostToDevice, s->stream));
-    if (b->rng_off)
-        HIPCHECK(s, hipMemcpyAsync(s->rng_off.p, b->rng_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
+    if (ro)
+        HIPCHECK(s, hipMemcpyAsync(s->rng_off.p, ro, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
     else
         HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
     if (R) {
-        HIPCHECK(s, hipMemcpyAsync(s->rng_start.p, b->rng_start, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rng_end.p, b->rng_end, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rng_start.p, rs, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rng_end.p, re, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
     }
     s->user_txn_index = b->txn_index != nullptr;
     s->has_txn_index = s->user_txn_index || s->resident;

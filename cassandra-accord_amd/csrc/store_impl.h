@@ -75,6 +75,9 @@ struct accord_store {
     accord_store_cfg cfg{};
     hipStream_t stream = nullptr;
     std::string err;
+    // the CommandStores this handle hosts (cfg.store_bounds, copied; empty = one unbounded store) and
+    // the uploaded batch's ranges sliced Minimal to them (host staging of accord_batch_upload)
+    std::vector<uint32_t> st_bounds, sl_off, sl_start, sl_end;
     // batch (device)
     uint32_t n = 0, P = 0, R = 0;
     bool has_batch = false, computed = false;

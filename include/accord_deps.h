@@ -62,8 +62,23 @@ typedef struct {
     uint32_t window;        /* W of the status-at-time model; ACCORD_WINDOW_NONE: none
                                (statuses from accord_txn_register, resident stores) */
     uint32_t flags;         /* ACCORD_STORE_PROFILE | ACCORD_STORE_RESIDENT */
-    uint32_t reserved;
+    /* The CommandStores this handle hosts, as nstores + 1 ascending key-ordinal bounds: store j owns
+     * ordinals [store_bounds[j], store_bounds[j+1]), i.e. the IntKey range
+     * (store_bounds[j] - 1, store_bounds[j+1] - 1]; store_bounds[0] == 0 is open below and
+     * store_bounds[nstores] == ACCORD_KEY_END open above.  Every range of an uploaded batch is
+     * sliced Minimal to these stores -- the range command each store registers
+     * (InMemoryCommandStore.update, impl/InMemoryCommandStore.java:757-760: ranges.slice(storeRanges,
+     * Minimal)) and the query it answers (mapReduceRangesInternal :886) -- so a range spanning
+     * stores yields one RangeDeps entry per store slice (primitives/RangeDeps.java:462-465) and the
+     * handle's result is the union of its stores' PartialDeps (PreAccept.reduce,
+     * messages/PreAccept.java:140-156); pieces outside every store are dropped.  [key_lo, key_hi)
+     * must lie inside the stores.  nstores = 0 (store_bounds NULL): one store over the whole key
+     * domain, ranges unsliced. */
+    uint32_t nstores;
+    const uint32_t *store_bounds;   /* [nstores + 1], borrowed for the call */
 } accord_store_cfg;
+
+#define ACCORD_KEY_END 0xFFFFFFFFu   /* an open upper store bound */
 
 /* A batch of transactions in TxnId order (the PreAccept stream of SURVEY.md §8d).  Key txns
  * (TxnId domain bit 0) carry sorted unique key ordinals; range txns (domain bit 1) carry sorted,
@@ -258,6 +273,8 @@ int32_t accord_deps_merge(accord_store *store, uint32_t nparts, const accord_dep
  * Each store afterwards holds the node-level deps of its own txns, as after accord_deps_exchange_merge. */
 int32_t accord_comm_unique_id(void *id128);                  /* ncclGetUniqueId, 128 bytes */
 int32_t accord_comm_init(accord_store *store, int32_t nranks, int32_t rank, const void *id128);
+/* the communicator's size and this store's rank as RCCL reports them (ncclCommCount / ncclCommUserRank) */
+int32_t accord_comm_size(accord_store *store, int32_t *nranks, int32_t *rank);
 int32_t accord_deps_exchange_merge(accord_store *store, uint32_t n_total);
 int32_t accord_deps_exchange_local(accord_store *const *stores, uint32_t nranks, uint32_t n_total);
 int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merge_ms);

@@ -1479,6 +1479,85 @@ fail:
     return rc;
 }
 
+/* ------------------------------------------------------------------------------------------
+ * The CommandStores of one node (SURVEY.md §7 "Hard parts" 5, §8e).  Store j owns the IntKey
+ * range (bounds[j]-1, bounds[j+1]-1] (bounds[0] == 0: open below; bounds[S] == 0xFFFFFFFF: open
+ * above).  Each store sees every txn of the stream restricted to itself -- its keys
+ * (Keys.slice) and its ranges sliced Minimal (AbstractRanges.sliceMinimal, primitives/
+ * AbstractRanges.java:339-377: one piece (max(s, lo), min(e, hi)] per intersecting range, in
+ * order) -- both as the registered range command (InMemoryCommandStore.update,
+ * impl/InMemoryCommandStore.java:757-760) and as the query (mapReduceRangesInternal :886).  Each
+ * computes its PartialDeps alone (literal or fast restatement, same global positions, same
+ * status-at-time model) and the node's result is their union (PreAccept.reduce ->
+ * PartialDeps.with, messages/PreAccept.java:140-156): a range command spanning stores stays one
+ * RangeDeps entry per store slice (primitives/RangeDeps.java:462-465).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct { uint32_t *key_off, *key_ord, *rng_off, *rng_start, *rng_end; } store_view;
+
+static void store_view_free(store_view *v)
+{
+    free(v->key_off); free(v->key_ord); free(v->rng_off); free(v->rng_start); free(v->rng_end);
+    memset(v, 0, sizeof(*v));
+}
+
+static int store_view_build(const or_stream *s, uint32_t blo, uint32_t bhi, store_view *v)
+{
+    const uint32_t n = s->n;
+    const int64_t lo = (int64_t)blo - 1;                                     /* (lo, hi] */
+    const int64_t hi = bhi == 0xFFFFFFFFu ? INT64_MAX : (int64_t)bhi - 1;
+    const uint32_t P = s->key_off[n], R = s->rng_off ? s->rng_off[n] : 0;
+    memset(v, 0, sizeof(*v));
+    v->key_off = (uint32_t *)malloc(((size_t)n + 1) * 4);
+    v->key_ord = (uint32_t *)malloc(((size_t)P + 1) * 4);
+    v->rng_off = (uint32_t *)malloc(((size_t)n + 1) * 4);
+    v->rng_start = (uint32_t *)malloc(((size_t)R + 1) * 4);
+    v->rng_end = (uint32_t *)malloc(((size_t)R + 1) * 4);
+    if (!v->key_off || !v->key_ord || !v->rng_off || !v->rng_start || !v->rng_end) { store_view_free(v); return -1; }
+    uint32_t np = 0, nr = 0;
+    v->key_off[0] = 0; v->rng_off[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) {
+            const int64_t k = s->key_ord[p];
+            if (lo < k && k <= hi) v->key_ord[np++] = s->key_ord[p];
+        }
+        v->key_off[i + 1] = np;
+        if (s->rng_off)
+            for (uint32_t r = s->rng_off[i]; r < s->rng_off[i + 1]; ++r) {
+                const int64_t rs = s->rng_start[r], re = s->rng_end[r];
+                if (!(rs < hi && lo < re)) continue;                            /* Range.compareIntersecting */
+                v->rng_start[nr] = (uint32_t)(rs >= lo ? rs : lo);              /* cs >= 0 ? rs : ls */
+                v->rng_end[nr] = (uint32_t)(re <= hi ? re : hi);                /* ce <= 0 ? re : le */
+                ++nr;
+            }
+        v->rng_off[i + 1] = nr;
+    }
+    return 0;
+}
+
+int or_stream_deps_stores(const or_stream *s, uint32_t nstores, const uint32_t *bounds, int literal, or_deps *out)
+{
+    if (nstores == 0) return -1;
+    for (uint32_t j = 0; j < nstores; ++j) if (bounds[j] >= bounds[j + 1]) return -1;
+    or_deps *parts = (or_deps *)calloc(nstores, sizeof(or_deps));
+    if (!parts) return -1;
+    int rc = 0;
+    uint32_t done = 0;
+    for (uint32_t j = 0; j < nstores && !rc; ++j) {
+        store_view v;
+        if ((rc = store_view_build(s, bounds[j], bounds[j + 1], &v))) break;
+        or_stream t = *s;
+        t.key_off = v.key_off; t.key_ord = v.key_ord;
+        t.rng_off = v.rng_off; t.rng_start = v.rng_start; t.rng_end = v.rng_end;
+        rc = literal ? stream_literal(&t, t.n, &parts[j]) : or_stream_deps_fast(&t, &parts[j]);
+        store_view_free(&v);
+        if (!rc) ++done;
+    }
+    if (!rc) rc = or_deps_union(nstores, parts, out);
+    for (uint32_t j = 0; j < done; ++j) or_deps_free(&parts[j]);
+    free(parts);
+    return rc;
+}
+
 /* trimUnusedValues (utils/RelationMultiMap.java:491-532): keep the values referenced by the body
  * in their order, rewrite the body to the kept positions. */
 static int trim_and_emit(mm_out *o, int range, const uint64_t *keys, uint32_t nk, const uint32_t *vals, uint32_t nv,

@@ -182,6 +182,13 @@ int or_levels_cfk(const or_stream *s, const or_deps *d, uint32_t *round_out);
  * TxnId table sorted ascending (index order == Timestamp order) ---- */
 /* Deps.merge / linearUnion of G sets of the same n txns (KeyDeps + RangeDeps; keys may overlap) */
 int or_deps_union(uint32_t G, const or_deps *parts, or_deps *out);
+/* The node-level deps of a stream over the S CommandStores of one node (SURVEY.md §7 "Hard parts"
+ * 5): store j owns the IntKey range (bounds[j]-1, bounds[j+1]-1] (bounds[0] == 0 open below,
+ * bounds[S] == 0xFFFFFFFF open above); each store computes the PartialDeps of every txn over its
+ * keys and its Minimal slices of every range (InMemoryCommandStore.java:757-760, 886;
+ * AbstractRanges.sliceMinimal :339-377) -- literal (1) or fast (0) restatement -- and the result
+ * is their union (PreAccept.reduce, messages/PreAccept.java:140-156). */
+int or_stream_deps_stores(const or_stream *s, uint32_t nstores, const uint32_t *bounds, int literal, or_deps *out);
 /* RedundantBefore.collectDeps of every txn of the stream (local/RedundantBefore.java:181-190,
  * 418-421; ReducingRangeMap.foldl, inclusiveEnds): m entries (es, ee] ascending and disjoint with
  * [sep, eep) epochs and bound stream positions (0xFFFFFFFF = NONE); min_epoch = minUnsyncedEpoch.

@@ -70,6 +70,7 @@ def lib():
                                                _u64p, _u64p, _i32p, _u32p, C.POINTER(_u64p), C.POINTER(_u64p)]
         L.or_levels_cfk.argtypes = [C.POINTER(_OrStream), C.POINTER(_OrDeps), _u32p]
         L.or_deps_union.argtypes = [C.c_uint32, C.POINTER(_OrDeps), C.POINTER(_OrDeps)]
+        L.or_stream_deps_stores.argtypes = [C.POINTER(_OrStream), C.c_uint32, _u32p, C.c_int, C.POINTER(_OrDeps)]
         L.or_deps_slice.argtypes = [C.POINTER(_OrDeps), _u32p, _u32p, _u32p, C.c_uint32, C.POINTER(_OrDeps)]
         L.or_deps_invert.argtypes = [C.POINTER(_OrDeps), C.c_int, _u32p, C.POINTER(_i32p)]
         L.or_redundant_collect.argtypes = [C.POINTER(_OrStream), C.c_uint32, _u32p, _u32p, _u64p, _u64p, _u32p,
@@ -179,6 +180,33 @@ def deps_fast(s: Stream, window: int, batch_end=None, applied_before=None, floor
     o, keep = _or_stream(s, window, batch_end, applied_before, floor)
     d = _OrDeps()
     rc = lib().or_stream_deps_fast(C.byref(o), C.byref(d))
+    if rc != 0:
+        raise OracleError(rc)
+    try:
+        return _to_partial(d)
+    finally:
+        lib().or_deps_free(C.byref(d))
+
+
+KEY_END = 0xFFFFFFFF     # an open upper store bound (include/accord_deps.h ACCORD_KEY_END)
+
+
+def store_bounds(keyspace: int, stores: int):
+    """EvenSplit boundaries of `stores` CommandStores over ordinals [0, keyspace)
+    (local/ShardDistributor.java:46-157): store b owns [bounds[b], bounds[b+1]); the outer stores
+    are open (the node owns the whole key domain)."""
+    b = [j * keyspace // stores for j in range(stores)] + [KEY_END]
+    b[0] = 0
+    return b
+
+
+def deps_stores(s: Stream, window: int, bounds, literal: bool = False, batch_end=None) -> PartialDeps:
+    """Node-level deps over the CommandStores with the given bounds (oracle.h or_stream_deps_stores):
+    every store slices the range commands and queries to its own range, the parts are unioned."""
+    o, keep = _or_stream(s, window, batch_end)
+    b = np.ascontiguousarray(bounds, np.uint32)
+    d = _OrDeps()
+    rc = lib().or_stream_deps_stores(C.byref(o), len(b) - 1, b.ctypes.data_as(_u32p), int(literal), C.byref(d))
     if rc != 0:
         raise OracleError(rc)
     try:

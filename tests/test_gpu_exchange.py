@@ -23,10 +23,12 @@ def rank_blocks(keyspace, G):
 
 
 def run_exchange(s, keyspace, G, W, subset):
+    b = O.store_bounds(keyspace, 8 * G)
     stores = []
     try:
-        for lo, hi in rank_blocks(keyspace, G):
-            st = CommandStore(device=0, key_lo=lo, key_hi=hi, window=W, profile=True)
+        for r, (lo, hi) in enumerate(rank_blocks(keyspace, G)):
+            # rank r hosts the 8 EvenSplit CommandStores [8r, 8r + 8): ranges sliced at their bounds
+            st = CommandStore(device=0, key_lo=lo, key_hi=hi, window=W, profile=True, store_bounds=b[8 * r:8 * r + 9])
             st.upload(s.restrict_keys(lo, hi, drop_empty=subset))
             st.compute()
             stores.append(st)
@@ -61,12 +63,13 @@ def test_exchange_key_txns_store_subsets(gpu_device, G):
 
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_exchange_with_range_txns(gpu_device, G):
-    # range txns span rank blocks: their RangeDeps reach several ranks under the same range keys, so
-    # the owner unions with RelationMultiMap.linearUnion (general union path)
+    # range txns span rank blocks: every rank's stores register and query their slices of the ranges,
+    # the parts reach the owner as store-sliced RangeDeps and it unions them with
+    # RelationMultiMap.linearUnion (general union path) -- equal to the 8G-store oracle
     ks, W, n = 8000, 128, 16000
     s = generate_stream(n, 6, ks, 0.99, 0.5, seed=50 + G, range_frac=0.15, range_len_max=1500)
     out, _ = run_exchange(s, ks, G, W, subset=False)
-    check_ranks(out, O.deps_fast(s, W), n, G)
+    check_ranks(out, O.deps_stores(s, W, O.store_bounds(ks, 8 * G)), n, G)
 
 
 def test_exchange_uneven_homes_and_empty_ranks(gpu_device):

@@ -65,23 +65,25 @@ def _worker(rank, world, port, q):
 
 
 def _worker_ranges(rank, world, port, q):
-    """Range txns: each rank's partial is a whole PartialDeps (KeyDeps + RangeDeps); the owner
-    unions the parts it receives with Deps.merge (or_deps_union) -- what the device does through
-    accord_deps_union once the exchange carries both sides."""
+    """Range txns: each rank's partial is a whole PartialDeps (KeyDeps + RangeDeps) of its stores;
+    the owner unions the parts it receives with Deps.merge (or_deps_union) -- what the device does
+    through accord_deps_union -- and the result is the node-level deps over all the stores."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         s = generate_stream(N, 4, KS, 0.99, 0.5, seed=42, range_frac=0.15, range_len_max=120)
-        lo, hi = rank * KS // world, (rank + 1) * KS // world
-        part = O.deps_fast(s.restrict_keys(lo, hi), W)
+        # 4 EvenSplit CommandStores per rank: every store slices the range commands and queries to
+        # its own range (InMemoryCommandStore.java:757-760), so a rank's part holds its stores' slices
+        bounds = O.store_bounds(KS, 4 * world)
+        part = O.deps_stores(s, W, bounds[4 * rank:4 * rank + 5])
         parts = [None] * world
         for src in range(world):
             obj = [part] if src == rank else [None]
             dist.broadcast_object_list(obj, src=src)
             parts[src] = obj[0]
         merged = O.deps_union(parts)
-        full = O.deps_fast(s, W)
+        full = O.deps_stores(s, W, bounds)
         a, b = rank * N // world, (rank + 1) * N // world
         bad = 0
         for t in range(a, b):
