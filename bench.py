@@ -39,7 +39,7 @@ def algorithmic_bytes(n, P, kc, U, D):
 
 
 def fill_kernel_bytes(n, P, kc, U, D):
-    """Algorithmic bytes of ONE pass of the fill stage (txnrec_kernel + keydeps_fast_kernel<1> +
+    """Algorithmic bytes of ONE pass of the fill stage (txnrec_kernel + keydeps_fast_kernel<16> +
     keydeps_kernel<1,8> over the fast kernel's fallback list; every txn is filled once): reads lsb (8N),
     key_off (4(N+1)), key_ord (4P), the pair slices poslo (8P), each raw candidate once (4D), the
     three offset arrays (12(N+1)); writes the txnIds count (4N), keys (4kc), txnIds (4U) and
@@ -348,7 +348,7 @@ def main():
         "count_stage_ms": count_detail,
         "scan_lookback": {"spins_per_step": scan_spins / max(1, args.steps),
                           "fallbacks_total": scan_fallbacks},
-        "roofline": {"kernel": "fill stage: txnrec_kernel + keydeps_fast_kernel<1> + keydeps_kernel<1,8>",
+        "roofline": {"kernel": "fill stage: txnrec_kernel + keydeps_fast_kernel<16> + keydeps_kernel<1,8>",
                      "bound": "hbm",
                      "achieved": fill_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": (fill_gbs / PEAK_HBM_GBS) if fill_gbs else None,

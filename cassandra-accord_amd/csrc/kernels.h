@@ -93,6 +93,12 @@ struct KeyDepsParams {
     // far list): listed by the general kernel, built by a workgroup each (big_wex: scratch per pair)
     uint32_t *big_list, *big_count, *big_wex;
     uint32_t tiny;                     // thread-per-txn pass for tiny txns (batches of few keys per txn)
+    // union records (emit mode, nullptr = off): the fast kernel leaves a txn's near union as its
+    // near-map bits, 16 per lane (ubits[t*64 + lane]), instead of scattering its near txnIds into
+    // vgap, and umode[t] = far deps + 1 (0: the txn's txnIds are in vgap, written by another kernel);
+    // launch_emit_vals then writes every txn's txnIds once at its exact offset
+    uint16_t *ubits;
+    uint8_t *umode;
 };
 
 // Where a batch sits in the store's stream: global positions start at min_gi, and (has_prev) the
@@ -143,6 +149,10 @@ void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, void *
 void launch_keydeps_big(const KeyDepsParams &p, hipStream_t s);
 // vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
 size_t compact_temp_bytes(uint64_t max_total);
+// txnIds at exact offsets from the fast kernel's union records (umode[t] > 0) or the gapped vgap
+// lists (umode[t] == 0): a wave per txn
+void launch_emit_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
+                      const uint16_t *ubits, const uint8_t *umode, const void *recs, uint32_t *vals, hipStream_t s);
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
                          uint32_t *vals, uint64_t max_total, void *temp, hipStream_t s);
 

@@ -247,6 +247,7 @@ struct ReadyParams {
     uint32_t *until;                  // unmanaged: the pending record's txn; managed: the committed-deps cursor
     uint8_t *done;
     uint32_t *out, *out_cnt;          // txns that became ready (positions)
+    uint32_t *drop, *drop_cnt;        // waiting txns invalidated / truncated: leave the set unreported
     const KeySummary *sum;
     const uint32_t *kb;               // per key: shardRedundantBefore as a position (0: none)
     StatusView v;
@@ -381,6 +382,13 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, ui
     {
         if (p.done[t]) return;
         const uint32_t g = p.g[t], st = status_of(p.v, g);
+        if (st >= ST_INVALID) {                  // never executes (maybeExecute needs Stable): leaves the set
+            if (lane == 0) {
+                p.done[t] = 1;
+                p.drop[atomicAdd(p.drop_cnt, 1u)] = g;
+            }
+            return;
+        }
         const uint64_t l = p.lsb[t];
         const uint32_t kind = (uint32_t)(l >> 1) & 7u;
         const bool rdom = (l & 1u) != 0;
@@ -502,20 +510,30 @@ void ready_destroy(accord_store *s)
     s->rdy_stats = nullptr;
     for (ReadyGen *r : s->rdy_gens) { r->release(); delete r; }
     s->rdy_gens.clear();
+    s->rdy_batch_gen = nullptr;
     s->rdy_waiting = 0;
     if (s->rdy_host) { (void)hipHostFree(s->rdy_host); s->rdy_host = nullptr; }
     if (s->rdy_tab_host) { (void)hipHostFree(s->rdy_tab_host); s->rdy_tab_host = nullptr; s->rdy_tab_cap = 0; }
 }
 
-// the last computed batch (its WaitingOn just initialised) joins the waiting set
-int32_t ready_track_batch(accord_store *s)
+// A batch's WaitingOn may be initialised again (a retry, or before and after its RedundantBefore
+// union) only while its generation has not been evaluated: the new generation then replaces it.
+// After an accord_ready_update has seen it, its released txns were reported and a second
+// generation would report them again -- refused.
+int32_t ready_batch_check(accord_store *s)
+{
+    if (s->rdy_batch_gen && !s->rdy_batch_gen->fresh)
+        return fail(s, ACCORD_ERR_STATE, "the batch's WaitingOn is already in the waiting set and was evaluated "
+                                         "by accord_ready_update; compute the next batch first");
+    return ACCORD_OK;
+}
+
+namespace {
+// the generation's device copies of the batch's deps and WaitingOn; no state of the store changes
+int32_t ready_gen_fill(accord_store *s, ReadyGen *r)
 {
     const uint32_t n = s->n;
-    if (n == 0) return ACCORD_OK;
     hipStream_t st = s->stream;
-    ReadyGen *r = new (std::nothrow) ReadyGen();
-    if (!r) return fail(s, ACCORD_ERR_OOM, "out of host memory");
-    s->rdy_gens.push_back(r);
     r->n = r->left = n;
     r->words = s->wo_words_total;
     const size_t n1 = (size_t)n + 1;
@@ -547,7 +565,36 @@ int32_t ready_track_batch(accord_store *s)
     HIPCHECK(s, hipMemsetAsync(r->until.p, 0, cd.tot_keys * 4 + 8, st));
     HIPCHECK(s, hipMemsetAsync(r->done.p, 0, (size_t)n + 8, st));
     HIPCHECK(s, hipStreamSynchronize(st));
-    s->rdy_waiting += n;
+    return ACCORD_OK;
+}
+} // namespace
+
+// the last computed batch (its WaitingOn just initialised) joins the waiting set.  The generation is
+// built completely before it joins (a failed copy or allocation leaves the set as it was), and it
+// replaces an unevaluated generation of the same batch (ready_batch_check)
+int32_t ready_track_batch(accord_store *s)
+{
+    if (s->n == 0) return ACCORD_OK;
+    int32_t rc = ready_batch_check(s);
+    if (rc != ACCORD_OK) return rc;
+    ReadyGen *r = new (std::nothrow) ReadyGen();
+    if (!r) return fail(s, ACCORD_ERR_OOM, "out of host memory");
+    rc = ready_gen_fill(s, r);
+    if (rc == ACCORD_OK) {
+        try { s->rdy_gens.reserve(s->rdy_gens.size() + 1); }
+        catch (...) { rc = fail(s, ACCORD_ERR_OOM, "out of host memory"); }
+    }
+    if (rc != ACCORD_OK) { r->release(); delete r; return rc; }
+    if (ReadyGen *old = s->rdy_batch_gen) {                    // an unevaluated generation of this batch
+        for (size_t i = 0; i < s->rdy_gens.size(); ++i)
+            if (s->rdy_gens[i] == old) { s->rdy_gens.erase(s->rdy_gens.begin() + i); break; }
+        s->rdy_waiting -= old->left;
+        old->release();
+        delete old;
+    }
+    s->rdy_gens.push_back(r);
+    s->rdy_batch_gen = r;
+    s->rdy_waiting += r->n;
     return ACCORD_OK;
 }
 
@@ -570,7 +617,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     if (cap == 0) return ACCORD_OK;
     constexpr uint32_t PEEK = 4096;            // ready txns read back with the count in one copy
     HIPCHECK(s, s->rdy_sum.ensure((size_t)nkeys * sizeof(KeySummary) + 64));
-    HIPCHECK(s, s->rdy_out.ensure(cap * 4 + 256));
+    HIPCHECK(s, s->rdy_out.ensure(cap * 8 + 512));      // header, ready list [cap], dropped list [cap]
     const uint32_t ngens = (uint32_t)s->rdy_gens.size();
     const uint32_t nl = (ngens + RD_GENS - 1) / RD_GENS;
     HIPCHECK(s, s->rdy_launch.ensure((size_t)std::max(1u, nl) * sizeof(ReadyLaunch)));
@@ -580,11 +627,14 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     constexpr uint32_t HDR = 64;               // rdy_out header words: ready count, dirty keys, work counts
     HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, HDR * 4, st));
     // everything is re-evaluated after a new carry (batch, truncation) or RedundantBefore bound
-    const bool full = s->rdy_kb_dirty || s->rdy_sum_version != s->carry_version;
+    // (and after a call that failed part-way: its bookkeeping below may be ahead of the device)
+    const bool force = s->rdy_force_full;
+    const bool full = force || s->rdy_kb_dirty || s->rdy_sum_version != s->carry_version;
     const uint32_t seen = s->rdy_seen, call = ++s->rdy_call;
+    s->rdy_force_full = true;                  // cleared once this call has synchronised
     s->rdy_seen = s->rg_epoch;
     s->rdy_sum_version = s->carry_version;
-    if (s->rdy_kb_dirty) {
+    if (s->rdy_kb_dirty || force) {
         HIPCHECK(s, s->rdy_kb.ensure((size_t)nkeys * 4 + 4));
         HIPCHECK(s, hipMemcpyAsync(s->rdy_kb.p, s->rdy_kb_host.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
         s->rdy_kb_dirty = false;
@@ -597,7 +647,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     HIPCHECK(s, s->rdy_dirty.ensure_zeroed((size_t)nkeys * 4 + 4, st));
     HIPCHECK(s, s->rdy_dirty2.ensure_zeroed((size_t)nkeys * 4 + 4, st));
     HIPCHECK(s, s->rdy_dlist.ensure((size_t)nkeys * 4 + 4));
-    uint32_t *cnt = s->rdy_out.as<uint32_t>(), *list = cnt + HDR;    // cnt[0]: ready txns, cnt[1]: dirty keys
+    // cnt[0]: ready txns, cnt[1]: dirty keys, cnt[HDR - 1]: dropped txns
+    uint32_t *cnt = s->rdy_out.as<uint32_t>(), *list = cnt + HDR, *drop = list + cap;
     DirtyMark dm{};
     if (!full) {
         dm.chg = s->rg_chg.as<uint32_t>(); dm.cchg = s->rg_cchg.as<uint32_t>(); dm.seen = seen; dm.call = call;
@@ -606,7 +657,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     }
     if (C) hipLaunchKernelGGL(rd_part_kernel, dim3(grid_for_waves((C + 63) / 64)), dim3(256), 0, st, C,
                               s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), v, s->rdy_part.as<KeyPart>(), dm);
-    if (s->rdy_kseg_version != s->carry_version || !s->rdy_kseg0.p) {
+    if (s->rdy_kseg_version != s->carry_version || !s->rdy_kseg0.p || force) {
         HIPCHECK(s, s->rdy_kseg0.ensure((size_t)nkeys * 4 + 4));
         HIPCHECK(s, s->rdy_kseg1.ensure((size_t)nkeys * 4 + 4));
         HIPCHECK(s, hipMemsetAsync(s->rdy_kseg0.p, 0, (size_t)nkeys * 4, st));
@@ -639,6 +690,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.wo_off = r->wo_off.as<uint32_t>(); p.words = r->wo.as<unsigned long long>(); p.aoi = r->aoi.as<unsigned long long>();
         p.pend = r->pend.as<uint8_t>(); p.until = r->until.as<uint32_t>(); p.done = r->done.as<uint8_t>();
         p.out = list; p.out_cnt = cnt;
+        p.drop = drop; p.drop_cnt = cnt + (HDR - 1);
         p.sum = s->rdy_sum.as<KeySummary>();
         p.kb = s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
         p.v = v;
@@ -654,7 +706,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     if (any_inc) {          // a work list per launch: cap entries, counts in rdy_wcnt
         HIPCHECK(s, s->rdy_work.ensure(cap * 4 + 64));
         uint32_t *wc = cnt + 2;                // in the header (cleared above) unless too many launches
-        if (tabs.size() > HDR - 2) {
+        if (tabs.size() > HDR - 3) {
             HIPCHECK(s, s->rdy_wcnt.ensure(tabs.size() * 4 + 64));
             HIPCHECK(s, hipMemsetAsync(s->rdy_wcnt.p, 0, tabs.size() * 4, st));
             wc = s->rdy_wcnt.as<uint32_t>();
@@ -690,10 +742,10 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     uint32_t *peek = (uint32_t *)s->rdy_host;
     HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK)) * 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));       // also: the parameter tables were consumed
-    const uint32_t nr = peek[0];
+    const uint32_t nr = peek[0], nd = peek[HDR - 1];
     if (s->rdy_stats) {                          // ACCORD_READY_STATS: diagnostic totals (ready_destroy prints)
         s->rdy_stats[0] += 1; s->rdy_stats[1] += peek[1]; s->rdy_stats[2] += cap;
-        if (any_inc && tabs.size() <= HDR - 2)
+        if (any_inc && tabs.size() <= HDR - 3)
             for (size_t i = 0; i < tabs.size(); ++i) s->rdy_stats[3] += peek[2 + i];
         else s->rdy_stats[3] += cap;
     }
@@ -707,20 +759,35 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         }
         std::sort(s->rdy_list.begin(), s->rdy_list.end());
     }
-    // generations drain in stream order: count each one's released txns, free the empty ones
-    size_t a = 0;
-    for (accord_impl::ReadyGen *r : s->rdy_gens) {
-        uint32_t c = 0;
-        while (a < s->rdy_list.size() && s->rdy_list[a] <= r->ghi) { c += s->rdy_list[a] >= r->glo; ++a; }
-        r->left -= c;
+    std::vector<uint32_t> dropped(nd);
+    if (nd) {
+        HIPCHECK(s, hipMemcpyAsync(dropped.data(), drop, (size_t)nd * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+        std::sort(dropped.begin(), dropped.end());
     }
+    s->rdy_force_full = false;                 // the device and the bookkeeping below agree again
+    // generations drain in stream order: count each one's released (or dropped) txns, free the empty ones
+    auto settle = [&](const std::vector<uint32_t> &l) {
+        size_t a = 0;
+        for (accord_impl::ReadyGen *r : s->rdy_gens) {
+            uint32_t c = 0;
+            while (a < l.size() && l[a] <= r->ghi) { c += l[a] >= r->glo; ++a; }
+            r->left -= c;
+        }
+    };
+    settle(s->rdy_list);
+    settle(dropped);
     std::vector<accord_impl::ReadyGen *> keep;
     for (accord_impl::ReadyGen *r : s->rdy_gens) {
-        if (r->left == 0) { r->release(); delete r; }
+        if (r->left == 0) {
+            if (r == s->rdy_batch_gen) s->rdy_batch_gen = nullptr;
+            r->release();
+            delete r;
+        }
         else keep.push_back(r);
     }
     s->rdy_gens.swap(keep);
-    s->rdy_waiting -= nr;
+    s->rdy_waiting -= (uint64_t)nr + nd;
     out->n = nr;
     out->txn = s->rdy_list.data();
     out->waiting = s->rdy_waiting;

@@ -111,7 +111,7 @@ int32_t accord_store_destroy(accord_store *s)
     (void)hipSetDevice(s->cfg.device);
     (void)hipStreamSynchronize(s->stream);
     DevBuf *bufs[] = {&s->msb, &s->lsb, &s->node, &s->key_off, &s->key_ord, &s->rng_off, &s->rng_start, &s->rng_end,
-                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->tmp_ent, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list, &s->cv_tmp,
+                      &s->pair_key, &s->pair_ent, &s->sort_key, &s->sort_pair, &s->tmp_key, &s->tmp_val, &s->tmp_ent, &s->hist, &s->slice, &s->hist_tmp, &s->cnt_vub, &s->vub_off, &s->vgap, &s->fk_recs, &s->fk_list, &s->cv_tmp, &s->fk_ubits, &s->fk_umode,
                       &s->seg_start, &s->seg_end, &s->mc_state, &s->mc_state2, &s->mc_out, &s->mc_cnt, &s->mc_po, &s->radix_tmp, &s->cnt_keys, &s->cnt_vals, &s->cnt_k2v,
                       &s->kd_key_off, &s->kd_val_off, &s->kd_k2v_off, &s->scan_tmp, &s->status_totals,
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
@@ -219,6 +219,7 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
                     (unsigned long long)s->rk_keys_total);
     s->has_batch = false; s->computed = false; s->merged = false; s->m_pending = false; s->ds_cur = -1; s->mc_next = 0;
     s->b_registered = false;
+    s->rdy_batch_gen = nullptr;
     HIPCHECK(s, s->msb.ensure((size_t)n * 8));
     HIPCHECK(s, s->lsb.ensure((size_t)n * 8));
     HIPCHECK(s, s->node.ensure((size_t)n * 4));
@@ -290,6 +291,7 @@ int32_t accord_deps_compute(accord_store *s)
     s->m_pending = false;
     s->ds_cur = -1;
     s->wo_done = false;
+    s->rdy_batch_gen = nullptr;
 
     // history = [entries a resident store carried over | this batch's pairs], key-major after the sort
     const uint32_t C = s->resident ? s->carry_n : 0u;
@@ -568,6 +570,18 @@ int32_t accord_deps_compute(accord_store *s)
     kp.big_wex = s->bk_wex.as<uint32_t>();
     kp.tiny = (uint64_t)P <= 2ull * n ? 1u : 0u;      // <= 2 keys per txn on average: a store's key block
     if (const char *e = getenv("ACCORD_TINY")) kp.tiny = e[0] == '1' ? 1u : 0u;   // dev aid: force on / off
+    // emit mode: the fast kernel (16 map bits per lane: windows up to 384) leaves union records and
+    // the txnIds are written once, at their exact offsets, by launch_emit_vals instead of being
+    // scattered at upper-bound offsets and compacted (ACCORD_FILL_EMIT=0: the compaction, for A/B)
+    const char *em = getenv("ACCORD_FILL_EMIT");
+    const bool emit = s->cfg.window <= 384u && em && em[0] == '1';   // off until measured
+    kp.ubits = nullptr; kp.umode = nullptr;
+    if (emit) {
+        HIPCHECK(s, s->fk_ubits.ensure((size_t)n * 128 + 64));
+        HIPCHECK(s, s->fk_umode.ensure((size_t)n + 64));
+        kp.ubits = s->fk_ubits.as<uint16_t>();
+        kp.umode = s->fk_umode.as<uint8_t>();
+    }
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {
@@ -582,9 +596,14 @@ int32_t accord_deps_compute(accord_store *s)
     if (rdeps) accord::launch_rangedeps_fill(rp, st);
     record(s, EV_RANGE);
     accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[7], s->scan_tmp.p, st);
-    HIPCHECK(s, s->cv_tmp.ensure(accord::compact_temp_bytes(vub_total)));
-    accord::launch_compact_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, s->kd_vals.as<uint32_t>(),
-                                vub_total, s->cv_tmp.p, st);
+    if (emit) {
+        accord::launch_emit_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, kp.ubits, kp.umode, s->fk_recs.p,
+                                 s->kd_vals.as<uint32_t>(), st);
+    } else {
+        HIPCHECK(s, s->cv_tmp.ensure(accord::compact_temp_bytes(vub_total)));
+        accord::launch_compact_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, s->kd_vals.as<uint32_t>(),
+                                    vub_total, s->cv_tmp.p, st);
+    }
     if (s->resident) {
         // what the next batch needs of this history (the stream ends at b_end)
         const uint32_t thr = s->b_end > s->cfg.window ? s->b_end - s->cfg.window : 0u;

@@ -84,7 +84,7 @@ struct accord_store {
     DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
     // work
     DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, tmp_ent, seg_start, seg_end, radix_tmp;
-    DevBuf hist, slice, hist_tmp, cnt_vub, vub_off, vgap, fk_recs, fk_list, cv_tmp;
+    DevBuf hist, slice, hist_tmp, cnt_vub, vub_off, vgap, fk_recs, fk_list, cv_tmp, fk_ubits, fk_umode;
     DevBuf bk_list, bk_wex;        // big txns (keydeps_big_kernel): count | list, per-pair scratch
     DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
     DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v, rd_big, rk_cp, rk_cnt, rk_off, rk_slices, rk_cls;
@@ -162,6 +162,8 @@ struct accord_store {
     DepSet rb_set;
     // execution readiness (ready.hip): the waiting set, one generation per initialised batch
     std::vector<accord_impl::ReadyGen *> rdy_gens;
+    accord_impl::ReadyGen *rdy_batch_gen = nullptr;   // the current batch's generation (until the next batch)
+    bool rdy_force_full = false;             // an accord_ready_update failed part-way: evaluate everything next
     uint64_t rdy_waiting = 0;
     DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dirty2, rdy_dlist, rdy_work, rdy_wcnt;
     uint32_t rdy_call = 0;                    // accord_ready_update calls (ids of the dirty marks)
@@ -203,6 +205,7 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
                                unsigned long long *aoi);
 // execution readiness (ready.hip)
 int32_t ready_track_batch(accord_store *s);
+int32_t ready_batch_check(accord_store *s);
 void ready_destroy(accord_store *s);
 // RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp)
 int32_t redundant_apply(accord_store *s);

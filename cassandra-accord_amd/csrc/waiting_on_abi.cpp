@@ -112,6 +112,10 @@ int32_t accord_waiting_on_initialise(accord_store *s)
     if (s->merged || (s->ds_cur >= 0 && !s->ds_rb))
         return fail(s, ACCORD_ERR_STATE, "accord_waiting_on_initialise runs on the batch's computed deps "
                                          "(or their RedundantBefore union), not a union / slice result");
+    {
+        const int32_t rc = accord_impl::ready_batch_check(s);   // at most one evaluated generation per batch
+        if (rc != ACCORD_OK) return rc;
+    }
     const accord_impl::CurDeps cd = accord_impl::cur_deps(s);
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     const uint32_t n = s->n;

@@ -2283,7 +2283,9 @@ int or_lstore_truncate(or_lstore *s, uint32_t m, const uint32_t *start, const ui
  *    (:1264-1283) with next / minUncommitted as the constructor derives them (:422-470).
  * The reference evaluates these tests when an event reaches the key (notifyAndUpdatePending,
  * :1163-1215); here they are evaluated for every waiting txn at every call (a txn is released at
- * the first call at which its test holds).  Ready = no bit left and status STABLE.
+ * the first call at which its test holds).  Ready = no bit left and status STABLE.  A waiting txn
+ * that is invalidated or truncated (INVALID_OR_TRUNCATED, Erased) leaves the set unreported: the
+ * reference never executes it (Commands.maybeExecute needs Stable).
  * ------------------------------------------------------------------------------------------ */
 typedef struct or_waiter {
     uint32_t g, nr, nk;
@@ -2409,6 +2411,11 @@ int or_lstore_ready(or_lstore *s, uint32_t *ready_out, uint32_t *nready)
         const int kind = kind_of(s->tbl[g].lsb), rdom = domain_of(s->tbl[g].lsb);
         const int only_deps = kind == K_EXCL_SYNC_POINT || kind == K_EPHEMERAL_READ;   /* awaitsOnlyDeps */
         const ts_t *ex = &s->exec[g];
+        if (st >= S_INVALID_OR_TRUNCATED) {      /* invalidated / truncated: leaves the waiting set, never ready */
+            free(x->rdeps); free(x->keys); free(x->kdoff); free(x->kdeps); free(x->words); free(x->aoi);
+            free(x->pend); free(x->until);
+            continue;
+        }
         /* range-dep bits: Commands.updateWaitingOn (forEachWaitingOnId: reverse order) */
         for (uint32_t j = x->nr; j-- > 0;) {
             if (!w_test(x->words, j)) continue;

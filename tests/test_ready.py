@@ -236,6 +236,26 @@ def test_gpu_kat(gpu_device):
         kat_run(dev)
 
 
+@pytest.mark.gpu
+def test_gpu_initialise_twice(gpu_device):
+    """A second accord_waiting_on_initialise of the same batch replaces its unevaluated generation (no
+    txn reported twice, the waiting count unchanged); after an accord_ready_update has evaluated it,
+    a third is refused (its released txns were reported already)."""
+    from accord_amd import IllegalStateException
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        s = mk(KAT)
+        d = Driver(s, 4, dev)
+        part = d.batch(0, 8)
+        d.register([0, 1, 2, 3, 4, 6, 7], STABLE)
+        d.initialise(0, part)
+        dev.waiting_on_initialise()                       # again: replaces the first generation
+        assert list(d.round()) == [0]                     # Driver.round: == oracle, waiting counts equal
+        with pytest.raises(IllegalStateException):
+            dev.waiting_on_initialise()
+        d.apply([0])
+        assert list(d.round()) == [1]
+
+
 def test_sync_points_oracle_progress():
     """SyncPoints / ExclusiveSyncPoints (awaitsOnlyDeps, witness everything) at executeAt = TxnId
     drain too.  (With executeAts past the TxnId a range XSP's unmanaged APPLY record can wait for a
@@ -342,7 +362,7 @@ def test_schedule_rb_oracle_progress():
     out, inval, d = schedule_rb(s, 40, 300, 10)
     allr = np.concatenate(out)
     assert np.array_equal(np.sort(np.concatenate([allr, inval])), np.arange(s.n))
-    assert d.ora.waiting == inval.size                   # invalidated txns never become ready
+    assert d.ora.waiting == 0                            # invalidated txns leave the set, never ready
 
 
 @pytest.mark.gpu
