@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = [
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
     "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset", "accord_txn_register",
     "accord_deps_visit", "accord_deps_range_stab", "accord_range_stab_release",
-    "accord_redundant_before_set",
+    "accord_redundant_before_set", "accord_redundant_before_set_ex",
 ]
 NO_TXN = 0xFFFFFFFF          # RedundantBefore bound Timestamp.NONE
 VISIT_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32)
@@ -120,7 +120,8 @@ class _Deps(C.Structure):
 
 
 class _Ready(C.Structure):
-    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("waiting", C.c_uint64), ("txn", C.POINTER(C.c_uint32))]
+    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("waiting", C.c_uint64), ("txn", C.POINTER(C.c_uint32)),
+                ("eal_msb", _u64p), ("eal_lsb", _u64p), ("eal_node", _i32p)]
 
 
 class _WaitingOn(C.Structure):
@@ -216,6 +217,8 @@ def lib() -> C.CDLL:
         L.accord_max_conflicts_reset.argtypes = [C.c_void_p]
         L.accord_redundant_before_set.argtypes = [C.c_void_p, C.c_uint32, _u32p, _u32p, _u64p, _u64p, _u32p,
                                                   C.c_uint64]
+        L.accord_redundant_before_set_ex.argtypes = [C.c_void_p, C.c_uint32, _u32p, _u32p, _u64p, _u64p, _u32p,
+                                                     _u32p, _u32p, _u8p, C.c_uint64]
         L.accord_store_state.argtypes = [C.c_void_p, C.POINTER(_StoreState)]
         L.accord_store_reset.argtypes = [C.c_void_p]
         L.accord_deps_visit.argtypes = [C.POINTER(_Deps), C.c_uint32, VISIT_FN, C.c_void_p]
@@ -693,20 +696,28 @@ class CommandStore:
             self._check(lib().accord_max_conflicts_fold_from(self._h, first, int(em), int(el), int(en), C.byref(o)))
         return msb, lsb, node, present, fast, int(o.folded)
 
-    def redundant_before(self, start=(), end=(), start_epoch=(), end_epoch=(), bound=(), min_epoch: int = 0):
+    def redundant_before(self, start=(), end=(), start_epoch=(), end_epoch=(), bound=(), min_epoch: int = 0,
+                         locally_applied=None, bootstrapped_at=None, stale=None):
         """RedundantBefore of this store (local/RedundantBefore.java): its non-null entries (start, end]
         ascending and disjoint, with [start_epoch, end_epoch) and shardAppliedOrInvalidatedBefore as a
         stream position (NO_TXN = NONE); min_epoch = minUnsyncedEpoch.  Every later calculation returns
         builder.build().with(RedundantBefore.collectDeps(...)) (messages/PreAccept.java:260-263).  No
-        entries = RedundantBefore.EMPTY."""
+        entries = RedundantBefore.EMPTY.  locally_applied / bootstrapped_at (positions, NO_TXN = NONE)
+        and stale (staleUntilAtLeast != null) complete each Entry: readiness then applies
+        removeRedundantDependencies (accord_redundant_before_set_ex)."""
         a = [np.ascontiguousarray(start, np.uint32), np.ascontiguousarray(end, np.uint32),
              np.ascontiguousarray(start_epoch, np.uint64), np.ascontiguousarray(end_epoch, np.uint64),
              np.ascontiguousarray(bound, np.uint32)]
-        if len({len(x) for x in a}) != 1:
+        ext = [None if x is None else np.ascontiguousarray(x, t)
+               for x, t in ((locally_applied, np.uint32), (bootstrapped_at, np.uint32), (stale, np.uint8))]
+        if len({len(x) for x in a + [e for e in ext if e is not None]}) != 1:
             raise IllegalArgumentException(-1, "RedundantBefore arrays differ in length")
-        self._check(lib().accord_redundant_before_set(
+        self._check(lib().accord_redundant_before_set_ex(
             self._h, len(a[0]), a[0].ctypes.data_as(_u32p), a[1].ctypes.data_as(_u32p), a[2].ctypes.data_as(_u64p),
-            a[3].ctypes.data_as(_u64p), a[4].ctypes.data_as(_u32p), int(min_epoch)))
+            a[3].ctypes.data_as(_u64p), a[4].ctypes.data_as(_u32p),
+            None if ext[0] is None else ext[0].ctypes.data_as(_u32p),
+            None if ext[1] is None else ext[1].ctypes.data_as(_u32p),
+            None if ext[2] is None else ext[2].ctypes.data_as(_u8p), int(min_epoch)))
 
     def max_conflicts_reset(self):
         self._check(lib().accord_max_conflicts_reset(self._h))
@@ -874,10 +885,20 @@ class CommandStore:
         Commands.updateWaitingOn for range deps, CommandsForKey.notify / notifyUnmanaged for keys --
         and returns the global positions (ascending) of the txns now ReadyToExecute, and how many
         txns still wait."""
+        got, waiting, _ = self.ready_update_ex()
+        return got, waiting
+
+    def ready_update_ex(self):
+        """ready_update, plus each ready txn's Command.executesAtLeast as (msb, lsb, node) arrays."""
         r = _Ready()
         self._check(lib().accord_ready_update(self._h, C.byref(r)))
-        got = np.ctypeslib.as_array(r.txn, shape=(r.n,)).copy() if r.n else np.zeros(0, np.uint32)
-        return got, int(r.waiting)
+        if not r.n:
+            z = np.zeros(0, np.uint64)
+            return np.zeros(0, np.uint32), int(r.waiting), (z, z.copy(), np.zeros(0, np.int32))
+        got = np.ctypeslib.as_array(r.txn, shape=(r.n,)).copy()
+        eal = (np.ctypeslib.as_array(r.eal_msb, shape=(r.n,)).copy(), np.ctypeslib.as_array(r.eal_lsb, shape=(r.n,)).copy(),
+               np.ctypeslib.as_array(r.eal_node, shape=(r.n,)).copy())
+        return got, int(r.waiting), eal
 
     def waiting_on_timing(self):
         a, b, c = C.c_float(), C.c_float(), C.c_float()

@@ -321,13 +321,20 @@ CurDeps cur_deps(const accord_store *s)
         c.kd_val_off = x.val_off.as<uint32_t>(); c.kd_vals = x.vals.as<uint32_t>();
         c.kd_k2v_off = x.x_off.as<uint32_t>(); c.kd_k2v = x.x.as<uint32_t>();
         c.rd_val_off = x.rval_off.as<uint32_t>(); c.rd_vals = x.rvals.as<uint32_t>();
+        c.rd_rng_off = x.rng_off.as<uint32_t>(); c.rd_rng_start = x.rng_start.as<uint32_t>();
+        c.rd_rng_end = x.rng_end.as<uint32_t>(); c.rd_r2v_off = x.r_off.as<uint32_t>(); c.rd_r2v = x.r.as<uint32_t>();
         c.tot_keys = x.tot_keys; c.tot_vals = x.tot_vals; c.tot_k2v = x.tot_x; c.tot_rvals = x.tot_rvals;
+        c.tot_rngs = x.tot_rngs; c.tot_r2v = x.tot_r;
     } else {
         c.kd_key_off = s->kd_key_off.as<uint32_t>(); c.kd_keys = s->kd_keys.as<uint32_t>();
         c.kd_val_off = s->kd_val_off.as<uint32_t>(); c.kd_vals = s->kd_vals.as<uint32_t>();
         c.kd_k2v_off = s->kd_k2v_off.as<uint32_t>(); c.kd_k2v = s->kd_k2v.as<uint32_t>();
         c.rd_val_off = s->rd_val_off.as<uint32_t>(); c.rd_vals = s->rd_vals.as<uint32_t>();
+        c.rd_rng_off = s->rd_rng_off.as<uint32_t>(); c.rd_rng_start = s->rd_rng_start.as<uint32_t>();
+        c.rd_rng_end = s->rd_rng_end.as<uint32_t>(); c.rd_r2v_off = s->rd_r2v_off.as<uint32_t>();
+        c.rd_r2v = s->rd_r2v.as<uint32_t>();
         c.tot_keys = s->tot_keys; c.tot_vals = s->tot_vals; c.tot_k2v = s->tot_k2v; c.tot_rvals = s->tot_rvals;
+        c.tot_rngs = s->tot_rngs; c.tot_r2v = s->tot_r2v;
     }
     return c;
 }
@@ -339,6 +346,15 @@ extern "C" {
 int32_t accord_redundant_before_set(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
                                     const uint64_t *start_epoch, const uint64_t *end_epoch, const uint32_t *bound,
                                     uint64_t min_epoch)
+{
+    return accord_redundant_before_set_ex(s, m, start, end, start_epoch, end_epoch, bound, nullptr, nullptr, nullptr,
+                                          min_epoch);
+}
+
+int32_t accord_redundant_before_set_ex(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
+                                       const uint64_t *start_epoch, const uint64_t *end_epoch, const uint32_t *bound,
+                                       const uint32_t *local, const uint32_t *boot, const uint8_t *stale,
+                                       uint64_t min_epoch)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     if (m && (!start || !end || !start_epoch || !end_epoch || !bound)) return fail(s, ACCORD_ERR_ARG, "null argument");
@@ -359,6 +375,27 @@ int32_t accord_redundant_before_set(accord_store *s, uint32_t m, const uint32_t 
         HIPCHECK(s, hipMemcpyAsync(s->rb_eep.p, end_epoch, (size_t)m * 8, hipMemcpyHostToDevice, s->stream));
         HIPCHECK(s, hipStreamSynchronize(s->stream));
     }
+    // the rest of each entry (removeRedundantDependencies); absent arrays: NONE, NONE, not stale
+    bool ext = false;
+    for (uint32_t i = 0; i < m && !ext; ++i)
+        ext = (local && local[i] != ACCORD_NO_TXN) || (boot && boot[i] != ACCORD_NO_TXN) || (stale && stale[i]);
+    if (ext) {
+        std::vector<uint32_t> lo(m, ACCORD_NO_TXN), bo(m, ACCORD_NO_TXN);
+        std::vector<uint8_t> st(m, 0);
+        for (uint32_t i = 0; i < m; ++i) {
+            if (local) lo[i] = local[i];
+            if (boot) bo[i] = boot[i];
+            if (stale) st[i] = stale[i] ? 1 : 0;
+        }
+        HIPCHECK(s, s->rb_local.ensure((size_t)m * 4)); HIPCHECK(s, s->rb_boot.ensure((size_t)m * 4));
+        HIPCHECK(s, s->rb_stale.ensure((size_t)m + 8));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_local.p, lo.data(), (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_boot.p, bo.data(), (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipMemcpyAsync(s->rb_stale.p, st.data(), (size_t)m, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+    }
+    if (ext != s->rb_ext || ext) s->rdy_force_full = true;   // readiness re-evaluates everything
+    s->rb_ext = ext;
     s->rb_m = m;
     s->rb_min_epoch = min_epoch;
     if (accord_impl::registered_mode(s)) RC(accord_impl::status_truncate_carry(s, m, start, end, bound));

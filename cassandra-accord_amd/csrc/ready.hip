@@ -36,6 +36,7 @@
 // literal CommandsForKey objects.
 #include "store_impl.h"
 #include "status_view.h"
+#include "redundant_wait.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -230,6 +231,12 @@ __global__ __launch_bounds__(256) void rd_summary_kernel(uint32_t nkeys, const u
     }
 }
 
+struct ReadyOut {
+    uint32_t g;
+    int32_t node;                     // Command.executesAtLeast
+    uint64_t msb, lsb;
+};
+
 struct ReadyParams {
     uint32_t n, key_lo;
     const uint32_t *g;                // [n] global positions
@@ -246,8 +253,17 @@ struct ReadyParams {
     uint8_t *pend;                    // per key slot: 0 unregistered, 1 COMMIT, 2 APPLY, 3 released
     uint32_t *until;                  // unmanaged: the pending record's txn; managed: the committed-deps cursor
     uint8_t *done;
-    uint32_t *out, *out_cnt;          // txns that became ready (positions)
+    ReadyOut *out;                    // txns that became ready: position + executesAtLeast
+    uint32_t *out_cnt;
     uint32_t *drop, *drop_cnt;        // waiting txns invalidated / truncated: leave the set unreported
+    EalRec *eal;                      // [n] WaitingOn.executeAtLeast
+    // removeRedundantDependencies (redundant_wait.h; rbx = the map can remove a dep): the txns'
+    // participants (keys / ranges) and RangeDeps ranges + rangesToTxnIds
+    uint32_t rbx;
+    RrMap M;
+    const uint32_t *pkoff, *pkeys, *proff, *prs, *pre;
+    const uint32_t *rrng_off, *rrs, *rre, *rr2v_off, *rr2v;
+    uint32_t *ovf;
     const KeySummary *sum;
     const uint32_t *kb;               // per key: shardRedundantBefore as a position (0: none)
     StatusView v;
@@ -270,8 +286,9 @@ __device__ __forceinline__ Ts tid_of(const ReadyParams &p, uint32_t g)
 // registerUnmanaged (reg) / updatePending over the deps [d0, d1) of one key: 1 = ready, 0 = APPLY
 // pending (*until = the relevant dep executing last), -1 = COMMIT pending (*until = the last dep)
 __device__ int unmanaged_eval(const ReadyParams &p, uint32_t t, uint32_t d0, uint32_t d1, uint32_t kbound,
-                              const Ts &ex, bool only_deps, bool reg, uint32_t &until)
+                              const Ts &ex, bool only_deps, bool reg, uint32_t &until, uint32_t &executes_at)
 {
+    executes_at = NONE;
     const uint32_t vb = p.val_off[t], kb0 = p.k2v_off[t];
     uint32_t x = d0;
     while (x < d1 && p.vals[vb + p.k2v[kb0 + x]] < kbound) ++x;    // txnIds.find(shardRedundantBefore)
@@ -288,6 +305,7 @@ __device__ int unmanaged_eval(const ReadyParams &p, uint32_t t, uint32_t d0, uin
         }
     }
     if (ready) return 1;
+    executes_at = best;                                              // the relevant dep executing last
     const uint32_t last = p.vals[vb + p.k2v[kb0 + d1 - 1]];
     if (to_apply) { until = best == NONE ? last : best; return 0; }
     until = last;
@@ -304,7 +322,7 @@ struct ReadyLaunch {
     ReadyParams g[RD_GENS];
 };
 
-__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane);
+__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane, RrLds *rl);
 
 // Incremental calls: a lane per waiting txn keeps those whose inputs changed since the last call
 // (the txn itself, the key of a set key bit dirty -- for a managed txn: and no longer blocked by the
@@ -367,17 +385,18 @@ __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__res
 // a wave per txn: every txn of the launch (work == nullptr) or the listed ones
 __global__ __launch_bounds__(256) void rd_eval_kernel(const ReadyLaunch *__restrict__ L, uint32_t listed)
 {
+    extern __shared__ RrLds rr_lds[];                // removal scratch, a wave each (when the map can remove)
     const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
     const uint32_t ngen = L->ngen, m = listed ? *L->wcnt : L->total;
     for (uint32_t i = blockIdx.x * (blockDim.x / 64) + wave_id(); i < m; i += waves) {
         const uint32_t u = listed ? L->work[i] : i;
         uint32_t gi = 0;
         while (gi + 1 < ngen && L->gbase[gi + 1] <= u) ++gi;
-        rd_eval_txn(L->g[gi], u - L->gbase[gi], lane);
+        rd_eval_txn(L->g[gi], u - L->gbase[gi], lane, rr_lds + wave_id());
     }
 }
 
-__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane)
+__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane, RrLds *rl)
 {
     {
         if (p.done[t]) return;
@@ -398,14 +417,49 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, ui
         const uint32_t wmask = witness_mask(kind);
         const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], K = p.key_off[t + 1] - p.key_off[t];
         const uint32_t w0 = p.wo_off[t], nw = p.wo_off[t + 1] - w0;
+        // removeRedundantDependencies (redundant_wait.h) when minWaitingOnTxnId is a range dep
+        bool removal = false;
+        RrTxn T{};
+        if (p.rbx && R) {
+            uint32_t j0 = NONE;
+            for (uint32_t q = 0; q < nw && j0 == NONE; ++q) {
+                const unsigned long long wq = p.words[w0 + q];
+                if (wq) j0 = q * 64u + (uint32_t)__builtin_ctzll(wq);
+            }
+            if (j0 < R) {
+                T.rdom = rdom;
+                if (rdom) { T.np = p.proff[t + 1] - p.proff[t]; T.ps = p.prs + p.proff[t]; T.pe = p.pre + p.proff[t]; }
+                else { T.np = p.pkoff[t + 1] - p.pkoff[t]; T.pk = p.pkeys + p.pkoff[t]; }
+                T.R = R; T.rvals = p.rd_vals + p.rd_off[t];
+                T.nrr = p.rrng_off[t + 1] - p.rrng_off[t];
+                T.rs = p.rrs + p.rrng_off[t]; T.re = p.rre + p.rrng_off[t];
+                T.r2v = p.rr2v + p.rr2v_off[t];
+                const uint32_t mpos = T.rvals[j0];
+                bool o = false;
+                removal = rr_removal(p.M, T, *rl, lane, mpos, tid_of(p, mpos).msb >> 15, ex.msb >> 15, &o);
+                if (o && lane == 0) atomicAdd(p.ovf, 1u);
+            }
+        }
+        Ts own{0, 0, 0};                                                // own TxnId (executeAtLeast)
+        if (only_deps) own = tid_of(p, g);
+        bool eh = false;                                                // this lane's executeAtLeast candidate
+        Ts ev{0, 0, 0};
+        auto cand = [&](const Ts &x) {
+            if (!eh || tcmp(ev, x) < 0) { ev = x; eh = true; }
+        };
         bool waiting = false;
         for (uint32_t q = 0; q < nw; ++q) {
-            const unsigned long long old = p.words[w0 + q];
+            const unsigned long long rclr = removal ? rr_clear(*rl, T, q) : 0ull;
+            const unsigned long long old = p.words[w0 + q] & ~rclr;
             const uint32_t b = q * 64u + lane;
             bool clear = false, applied = false;
             if (b < R + K && ((old >> lane) & 1ull)) {
                 if (b < R) {                                             // range-dep bit
                     const uint32_t d = p.rd_vals[p.rd_off[t] + b], ds = status_of(p.v, d);
+                    if (only_deps && ds >= ST_COMMITTED && ds <= ST_APPLIED) {   // updateExecuteAtLeast
+                        const Ts de = exec_of(p.v, d);
+                        if (tcmp(de, own) > 0) cand(de);
+                    }
                     if (ds >= ST_COMMITTED) {                            // hasBeen(PreCommitted)
                         if (ds >= ST_INVALID) clear = applied = true;
                         else if (!only_deps && tcmp(exec_of(p.v, d), ex) > 0) clear = true;
@@ -440,17 +494,19 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, ui
                             clear = !blocked;
                         }
                     } else if (st >= ST_STABLE && st < ST_INVALID) {     // hasBeen(Stable), not truncated
-                        uint32_t pd = p.pend[slot], un = p.until[slot];
+                        uint32_t pd = p.pend[slot], un = p.until[slot], ea = NONE;
                         if (pd == 0) {                                   // registerUnmanaged
-                            const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, true, un);
+                            const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, true, un, ea);
                             pd = r == 1 ? 3u : r == 0 ? 2u : 1u;
+                            if (r == 0 && only_deps && ea != NONE) cand(exec_of(p.v, ea));   // :1470-1478
                         }
                         uint32_t nx = s.next;
                         if (nx != NONE && s.min_unc != NONE && tcmp(tid_of(p, s.min_unc), exec_of(p.v, nx)) < 0)
                             nx = NONE;                                   // nulled by minUncommitted (:454-455)
                         if (pd == 1 && (s.min_unc == NONE || s.min_unc > un)) {   // COMMIT -> updatePending
-                            const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, false, un);
+                            const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, false, un, ea);
                             pd = r == 1 ? 3u : 2u;
+                            if (r == 0 && only_deps && ea != NONE) cand(exec_of(p.v, ea));   // :1370-1380
                         }
                         if (pd == 2 && (s.min_unc == NONE || nx != NONE)) {       // notifyUnmanaged(APPLY, next)
                             if (nx == NONE || tcmp(exec_of(p.v, un), exec_of(p.v, nx)) < 0) pd = 3;
@@ -465,14 +521,22 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, ui
             const unsigned long long am = __ballot(applied && rdom);   // appliedOrInvalidated: Range-domain txns
             const unsigned long long nwv = old & ~cm;
             if (lane == 0) {
-                if (cm) p.words[w0 + q] = nwv;
+                if (cm || rclr) p.words[w0 + q] = nwv;
                 if (am) p.aoi[w0 + q] |= am;
             }
             waiting |= nwv != 0ull;
         }
+        EalRec ea{0, 0, 0, 0u};
+        if (only_deps) {
+            ea = p.eal[t];
+            eal_merge(ea, eal_wave_max(eh, ev));
+            if (lane == 0 && ea.has) p.eal[t] = ea;
+        }
         if (!waiting && st == ST_STABLE && lane == 0) {
             p.done[t] = 1;
-            p.out[atomicAdd(p.out_cnt, 1u)] = g;
+            const bool use = only_deps && ea.has;                       // Command.executesAtLeast
+            p.out[atomicAdd(p.out_cnt, 1u)] = ReadyOut{g, use ? ea.node : ex.node, use ? ea.msb : ex.msb,
+                                                       use ? ea.lsb : ex.lsb};
         }
     }
 }
@@ -492,10 +556,12 @@ struct ReadyGen {
     bool fresh = true;                            // not evaluated yet
     uint64_t words = 0;
     DevBuf g, lsb, rd_off, rd_vals, key_off, keys, val_off, vals, k2v_off, k2v, wo_off, wo, aoi, pend, until, done;
+    DevBuf eal, pkoff, pkeys, proff, prs, pre, rrng_off, rrs, rre, rr2v_off, rr2v;
     void release()
     {
         DevBuf *b[] = {&g, &lsb, &rd_off, &rd_vals, &key_off, &keys, &val_off, &vals, &k2v_off, &k2v, &wo_off, &wo, &aoi,
-                       &pend, &until, &done};
+                       &pend, &until, &done, &eal, &pkoff, &pkeys, &proff, &prs, &pre, &rrng_off, &rrs, &rre,
+                       &rr2v_off, &rr2v};
         for (DevBuf *x : b) x->release();
     }
 };
@@ -558,6 +624,23 @@ int32_t ready_gen_fill(accord_store *s, ReadyGen *r)
     HIPCHECK(s, copy(r->wo_off, s->wo_off.p, n1 * 4));
     HIPCHECK(s, copy(r->wo, s->wo_words.p, s->wo_words_total * 8));
     HIPCHECK(s, copy(r->aoi, s->wo_aoi.p, s->wo_words_total * 8));
+    HIPCHECK(s, copy(r->eal, s->wo_eal.p, (size_t)n * sizeof(EalRec)));
+    // the participants (the batch's keys / ranges) and RangeDeps ranges: removeRedundantDependencies
+    HIPCHECK(s, copy(r->pkoff, s->key_off.p, n1 * 4));
+    HIPCHECK(s, copy(r->pkeys, s->key_ord.p, (size_t)s->P * 4));
+    if (s->R) {
+        HIPCHECK(s, copy(r->proff, s->rng_off.p, n1 * 4));
+        HIPCHECK(s, copy(r->prs, s->rng_start.p, (size_t)s->R * 4));
+        HIPCHECK(s, copy(r->pre, s->rng_end.p, (size_t)s->R * 4));
+    } else {
+        HIPCHECK(s, r->proff.ensure(n1 * 4 + 8));
+        HIPCHECK(s, hipMemsetAsync(r->proff.p, 0, n1 * 4, st));
+    }
+    HIPCHECK(s, copy(r->rrng_off, cd.rd_rng_off, n1 * 4));
+    HIPCHECK(s, copy(r->rrs, cd.rd_rng_start, cd.tot_rngs * 4));
+    HIPCHECK(s, copy(r->rre, cd.rd_rng_end, cd.tot_rngs * 4));
+    HIPCHECK(s, copy(r->rr2v_off, cd.rd_r2v_off, n1 * 4));
+    HIPCHECK(s, copy(r->rr2v, cd.rd_r2v, cd.tot_r2v * 4));
     HIPCHECK(s, r->pend.ensure(cd.tot_keys + 8));
     HIPCHECK(s, r->until.ensure(cd.tot_keys * 4 + 8));
     HIPCHECK(s, r->done.ensure((size_t)n + 8));
@@ -607,6 +690,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         return fail(s, ACCORD_ERR_STATE, "accord_ready_update needs a registered-status store (resident, ACCORD_WINDOW_NONE)");
     out->n = 0;
     out->txn = nullptr;
+    out->eal_msb = out->eal_lsb = nullptr;
+    out->eal_node = nullptr;
     out->waiting = s->rdy_waiting;
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     hipStream_t st = s->stream;
@@ -615,14 +700,15 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     for (accord_impl::ReadyGen *r : s->rdy_gens) cap += r->left ? r->n : 0;
     s->rdy_list.clear();
     if (cap == 0) return ACCORD_OK;
-    constexpr uint32_t PEEK = 4096;            // ready txns read back with the count in one copy
+    constexpr uint32_t PEEK = 1024;            // ready records read back with the count in one copy
+    constexpr uint32_t RW = sizeof(ReadyOut) / 4;
     HIPCHECK(s, s->rdy_sum.ensure((size_t)nkeys * sizeof(KeySummary) + 64));
-    HIPCHECK(s, s->rdy_out.ensure(cap * 8 + 512));      // header, ready list [cap], dropped list [cap]
+    HIPCHECK(s, s->rdy_out.ensure(cap * (4 * RW + 4) + 512));   // header, ready records [cap], dropped [cap]
     const uint32_t ngens = (uint32_t)s->rdy_gens.size();
     const uint32_t nl = (ngens + RD_GENS - 1) / RD_GENS;
     HIPCHECK(s, s->rdy_launch.ensure((size_t)std::max(1u, nl) * sizeof(ReadyLaunch)));
     if (!s->rdy_host) {
-        HIPCHECK(s, hipHostMalloc(&s->rdy_host, (PEEK + 64) * 4, hipHostMallocDefault));
+        HIPCHECK(s, hipHostMalloc(&s->rdy_host, (PEEK * RW + 64) * 4, hipHostMallocDefault));
     }
     constexpr uint32_t HDR = 64;               // rdy_out header words: ready count, dirty keys, work counts
     HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, HDR * 4, st));
@@ -634,7 +720,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     s->rdy_force_full = true;                  // cleared once this call has synchronised
     s->rdy_seen = s->rg_epoch;
     s->rdy_sum_version = s->carry_version;
-    if (s->rdy_kb_dirty || force) {
+    const bool has_kb = s->rdy_kb_host.size() == nkeys;     // a shardRedundantBefore bound was set
+    if ((s->rdy_kb_dirty || force) && has_kb) {
         HIPCHECK(s, s->rdy_kb.ensure((size_t)nkeys * 4 + 4));
         HIPCHECK(s, hipMemcpyAsync(s->rdy_kb.p, s->rdy_kb_host.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
         s->rdy_kb_dirty = false;
@@ -648,7 +735,9 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     HIPCHECK(s, s->rdy_dirty2.ensure_zeroed((size_t)nkeys * 4 + 4, st));
     HIPCHECK(s, s->rdy_dlist.ensure((size_t)nkeys * 4 + 4));
     // cnt[0]: ready txns, cnt[1]: dirty keys, cnt[HDR - 1]: dropped txns
-    uint32_t *cnt = s->rdy_out.as<uint32_t>(), *list = cnt + HDR, *drop = list + cap;
+    uint32_t *cnt = s->rdy_out.as<uint32_t>();
+    ReadyOut *list = (ReadyOut *)(cnt + HDR);
+    uint32_t *drop = (uint32_t *)(list + cap);
     DirtyMark dm{};
     if (!full) {
         dm.chg = s->rg_chg.as<uint32_t>(); dm.cchg = s->rg_cchg.as<uint32_t>(); dm.seen = seen; dm.call = call;
@@ -691,8 +780,16 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.pend = r->pend.as<uint8_t>(); p.until = r->until.as<uint32_t>(); p.done = r->done.as<uint8_t>();
         p.out = list; p.out_cnt = cnt;
         p.drop = drop; p.drop_cnt = cnt + (HDR - 1);
+        p.eal = r->eal.as<EalRec>();
+        p.rbx = s->rb_ext && s->rb_m ? 1u : 0u;
+        p.M = rr_map_of(s);
+        p.pkoff = r->pkoff.as<uint32_t>(); p.pkeys = r->pkeys.as<uint32_t>();
+        p.proff = r->proff.as<uint32_t>(); p.prs = r->prs.as<uint32_t>(); p.pre = r->pre.as<uint32_t>();
+        p.rrng_off = r->rrng_off.as<uint32_t>(); p.rrs = r->rrs.as<uint32_t>(); p.rre = r->rre.as<uint32_t>();
+        p.rr2v_off = r->rr2v_off.as<uint32_t>(); p.rr2v = r->rr2v.as<uint32_t>();
+        p.ovf = cnt + (HDR - 2);
         p.sum = s->rdy_sum.as<KeySummary>();
-        p.kb = s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
+        p.kb = has_kb && s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
         p.v = v;
         p.full = full || r->fresh;
         any_inc |= !p.full;
@@ -706,7 +803,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     if (any_inc) {          // a work list per launch: cap entries, counts in rdy_wcnt
         HIPCHECK(s, s->rdy_work.ensure(cap * 4 + 64));
         uint32_t *wc = cnt + 2;                // in the header (cleared above) unless too many launches
-        if (tabs.size() > HDR - 3) {
+        if (tabs.size() > HDR - 4) {
             HIPCHECK(s, s->rdy_wcnt.ensure(tabs.size() * 4 + 64));
             HIPCHECK(s, hipMemsetAsync(s->rdy_wcnt.p, 0, tabs.size() * 4, st));
             wc = s->rdy_wcnt.as<uint32_t>();
@@ -728,36 +825,46 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     }
     std::memcpy(s->rdy_tab_host, tabs.data(), tab_bytes);
     HIPCHECK(s, hipMemcpyAsync(s->rdy_launch.p, s->rdy_tab_host, tab_bytes, hipMemcpyHostToDevice, st));
+    const size_t rr_lds = s->rb_ext && s->rb_m ? 4 * sizeof(RrLds) : 0;   // removal scratch, a wave each
     for (size_t i = 0; i < tabs.size(); ++i) {
         const ReadyLaunch *L = s->rdy_launch.as<ReadyLaunch>() + i;
         if (any_inc) {
             hipLaunchKernelGGL(rd_filter_kernel, dim3((tabs[i].total + 255) / 256), dim3(256), 0, st, L);
-            hipLaunchKernelGGL(rd_eval_kernel, dim3(std::min(grid_for_waves(tabs[i].total), 1024u)), dim3(256), 0, st, L, 1u);
+            hipLaunchKernelGGL(rd_eval_kernel, dim3(std::min(grid_for_waves(tabs[i].total), 1024u)), dim3(256), rr_lds, st, L, 1u);
         } else {
-            hipLaunchKernelGGL(rd_eval_kernel, dim3(grid_for_waves(tabs[i].total)), dim3(256), 0, st, L, 0u);
+            hipLaunchKernelGGL(rd_eval_kernel, dim3(grid_for_waves(tabs[i].total)), dim3(256), rr_lds, st, L, 0u);
         }
     }
     HIPCHECK(s, hipGetLastError());
     if (!s->rdy_stats && getenv("ACCORD_READY_STATS")) s->rdy_stats = new uint64_t[4]{0, 0, 0, 0};
     uint32_t *peek = (uint32_t *)s->rdy_host;
-    HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK)) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK) * RW) * 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));       // also: the parameter tables were consumed
     const uint32_t nr = peek[0], nd = peek[HDR - 1];
+    if (peek[HDR - 2])
+        return fail(s, ACCORD_ERR_CAPACITY, "%u waiting txns wait on more than %u range deps or touch more than %u "
+                                            "RedundantBefore entries", peek[HDR - 2], RR_MAXR, RR_MAXE);
     if (s->rdy_stats) {                          // ACCORD_READY_STATS: diagnostic totals (ready_destroy prints)
         s->rdy_stats[0] += 1; s->rdy_stats[1] += peek[1]; s->rdy_stats[2] += cap;
-        if (any_inc && tabs.size() <= HDR - 3)
+        if (any_inc && tabs.size() <= HDR - 4)
             for (size_t i = 0; i < tabs.size(); ++i) s->rdy_stats[3] += peek[2 + i];
         else s->rdy_stats[3] += cap;
     }
     s->rdy_list.resize(nr);
+    s->rdy_eal_msb.resize(nr); s->rdy_eal_lsb.resize(nr); s->rdy_eal_node.resize(nr);
     if (nr) {
+        std::vector<ReadyOut> recs(nr);
         if (nr <= PEEK) {
-            std::copy(peek + HDR, peek + HDR + nr, s->rdy_list.begin());
+            std::memcpy(recs.data(), peek + HDR, (size_t)nr * sizeof(ReadyOut));
         } else {
-            HIPCHECK(s, hipMemcpyAsync(s->rdy_list.data(), list, (size_t)nr * 4, hipMemcpyDeviceToHost, st));
+            HIPCHECK(s, hipMemcpyAsync(recs.data(), list, (size_t)nr * sizeof(ReadyOut), hipMemcpyDeviceToHost, st));
             HIPCHECK(s, hipStreamSynchronize(st));
         }
-        std::sort(s->rdy_list.begin(), s->rdy_list.end());
+        std::sort(recs.begin(), recs.end(), [](const ReadyOut &a, const ReadyOut &b) { return a.g < b.g; });
+        for (uint32_t i = 0; i < nr; ++i) {
+            s->rdy_list[i] = recs[i].g;
+            s->rdy_eal_msb[i] = recs[i].msb; s->rdy_eal_lsb[i] = recs[i].lsb; s->rdy_eal_node[i] = recs[i].node;
+        }
     }
     std::vector<uint32_t> dropped(nd);
     if (nd) {
@@ -790,6 +897,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     s->rdy_waiting -= (uint64_t)nr + nd;
     out->n = nr;
     out->txn = s->rdy_list.data();
+    out->eal_msb = s->rdy_eal_msb.data(); out->eal_lsb = s->rdy_eal_lsb.data(); out->eal_node = s->rdy_eal_node.data();
     out->waiting = s->rdy_waiting;
     return ACCORD_OK;
 }

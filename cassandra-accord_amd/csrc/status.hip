@@ -20,6 +20,7 @@
 // without knowing the future events).
 #include "store_impl.h"
 #include "status_view.h"
+#include "redundant_wait.h"
 
 #include <algorithm>
 #include <vector>
@@ -647,6 +648,10 @@ namespace {
 // empty) -- the KeyDeps key bits stay set (CommandsForKey.notify clears them later).  The
 // appliedOrInvalidated set exists for Range-domain txns only (Update(TxnId, Keys, ...) :1431-1437).
 // A thread per txn builds its words one at a time.
+// With a RedundantBefore map that can remove deps (pre != nullptr), rr_init_kernel ran first and left
+// in words[] the range deps removeRedundantDependencies keeps: the others are not visited.
+// executeAtLeast (awaitsOnlyDeps kinds): every visited range dep committed with an executeAt after the
+// txn's TxnId (local/Commands.java:782-783) -> eal[t].
 __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t *__restrict__ msb,
                                                       const uint64_t *__restrict__ lsb, const int32_t *__restrict__ node,
                                                       const uint32_t *__restrict__ txn_index,
@@ -655,7 +660,7 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
                                                       const uint32_t *__restrict__ rd_vals,
                                                       const uint32_t *__restrict__ wo_off, StatusView v,
                                                       unsigned long long *__restrict__ words,
-                                                      unsigned long long *__restrict__ aoi)
+                                                      unsigned long long *__restrict__ aoi, bool pre, EalRec *__restrict__ eal)
 {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t g = txn_index[t], ost = status_of(v, g);
@@ -668,14 +673,21 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
         const uint32_t r0 = rd_val_off[t], R = rd_val_off[t + 1] - r0;
         const uint32_t bits = R + (kd_key_off[t + 1] - kd_key_off[t]);
         const uint32_t w0 = wo_off[t], nw = wo_off[t + 1] - w0;
+        EalRec ea{0, 0, 0, 0u};
         for (uint32_t q = 0; q < nw; ++q) {
             unsigned long long wv = 0, av = 0;
+            const unsigned long long kept = pre ? words[w0 + q] : ~0ull;   // removeRedundantDependencies
             const uint32_t b0 = q * 64u, b1 = min(bits, b0 + 64u);
             for (uint32_t b = b0; b < b1; ++b) {
                 const unsigned long long bit = 1ull << (b & 63u);
                 if (b >= R) { wv |= bit; continue; }            // key bits
+                if (!(kept & bit)) continue;                    // removed: not waited on, not visited
                 const uint32_t d = rd_vals[r0 + b], st = status_of(v, d);
                 bool wait = true, applied = false;
+                if (only_deps && st >= ST_COMMITTED && st <= ST_APPLIED) {   // updateExecuteAtLeast
+                    const Ts de = exec_of(v, d);
+                    if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0) eal_merge(ea, EalRec{de.msb, de.lsb, de.node, 1u});
+                }
                 if (st >= ST_COMMITTED) {                       // hasBeen(PreCommitted)
                     if (st >= ST_INVALID) { wait = false; applied = true; }                 // truncated / invalidated
                     else if (!only_deps && tcmp(exec_of(v, d), own) > 0) wait = false;     // executes after us
@@ -687,6 +699,55 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
             words[w0 + q] = wv;
             aoi[w0 + q] = av;
         }
+        eal[t] = ea;
+    }
+}
+
+// removeRedundantDependencies at initialiseWaitingOn (every bit set: minWaitingOnTxnId = the first
+// range dep), a wave per txn: words[] = the range deps it keeps, key bits set.
+__global__ __launch_bounds__(256) void rr_init_kernel(uint32_t n, const uint64_t *__restrict__ msb,
+                                                      const uint64_t *__restrict__ lsb, const uint32_t *__restrict__ txn_index,
+                                                      const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ key_ord,
+                                                      const uint32_t *__restrict__ rng_off, const uint32_t *__restrict__ rng_start,
+                                                      const uint32_t *__restrict__ rng_end, accord_impl::CurDeps cd,
+                                                      const uint64_t *__restrict__ tmsb, const uint32_t *__restrict__ tg,
+                                                      uint32_t tx_n, RrMap M, const uint32_t *__restrict__ wo_off,
+                                                      StatusView v, unsigned long long *__restrict__ words,
+                                                      uint32_t *__restrict__ ovf)
+{
+    __shared__ RrLds lds[4];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    RrLds &L = lds[w];
+    for (uint32_t t = blockIdx.x * 4u + w; t < n; t += gridDim.x * 4u) {
+        const uint32_t r0 = cd.rd_val_off[t], R = cd.rd_val_off[t + 1] - r0;
+        const uint32_t bits = R + (cd.kd_key_off[t + 1] - cd.kd_key_off[t]);
+        const uint32_t w0 = wo_off[t], nw = wo_off[t + 1] - w0;
+        bool removal = false, o = false;
+        RrTxn T{};
+        if (R) {
+            const uint64_t l = lsb[t];
+            T.rdom = (l & 1u) != 0;
+            if (T.rdom) { T.np = rng_off[t + 1] - rng_off[t]; T.ps = rng_start + rng_off[t]; T.pe = rng_end + rng_off[t]; }
+            else { T.np = key_off[t + 1] - key_off[t]; T.pk = key_ord + key_off[t]; }
+            T.R = R; T.rvals = cd.rd_vals + r0;
+            T.nrr = cd.rd_rng_off[t + 1] - cd.rd_rng_off[t];
+            T.rs = cd.rd_rng_start + cd.rd_rng_off[t]; T.re = cd.rd_rng_end + cd.rd_rng_off[t];
+            T.r2v = cd.rd_r2v + cd.rd_r2v_off[t];
+            const uint32_t g = txn_index[t], ost = status_of(v, g);
+            const uint64_t em = ost >= ST_ACCEPTED && ost <= ST_APPLIED ? v.emsb[g] : msb[t];
+            const uint32_t mpos = T.rvals[0];
+            uint32_t lo = 0, hi = tx_n;                          // TxnId of the dep at mpos (epoch)
+            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (tg[m] < mpos) lo = m + 1; else hi = m; }
+            removal = rr_removal(M, T, L, lane, mpos, tmsb[lo] >> 15, em >> 15, &o);
+        }
+        if (o && lane == 0) atomicAdd(ovf, 1u);
+        for (uint32_t q = lane; q < nw; q += 64) {
+            const uint32_t b0 = q * 64u;
+            unsigned long long wv = b0 + 64u <= bits ? ~0ull : ((1ull << (bits - b0)) - 1ull);
+            if (removal) wv &= ~rr_clear(L, T, q);
+            words[w0 + q] = wv;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -701,12 +762,33 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
                                unsigned long long *aoi)
 {
     const CurDeps cd = cur_deps(s);
-    if (s->n)
-        hipLaunchKernelGGL(wo_init_kernel, dim3(grid_for(s->n)), dim3(256), 0, s->stream, s->n, s->msb.as<uint64_t>(),
-                           s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
-                           cd.kd_key_off, cd.rd_val_off, cd.rd_vals, wo_off, view_of(s), words, aoi);
+    const uint32_t n = s->n;
+    HIPCHECK(s, s->wo_eal.ensure((size_t)n * sizeof(EalRec) + 64));
+    if (!n) return ACCORD_OK;
+    const bool pre = s->rb_ext && s->rb_m && cd.tot_rvals;
+    if (pre) {                     // removeRedundantDependencies first (redundant_wait.h)
+        HIPCHECK(s, s->rr_ovf.ensure(64));
+        uint32_t *ovf = s->rr_ovf.as<uint32_t>();
+        HIPCHECK(s, hipMemsetAsync(ovf, 0, 8, s->stream));
+        hipLaunchKernelGGL(rr_init_kernel, dim3(std::min<uint32_t>((n + 3) / 4, 8192u)), dim3(256), 0, s->stream, n,
+                           s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->txn_index.as<uint32_t>(),
+                           s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->R ? s->rng_off.as<uint32_t>() : nullptr,
+                           s->R ? s->rng_start.as<uint32_t>() : nullptr, s->R ? s->rng_end.as<uint32_t>() : nullptr, cd,
+                           s->rg_tmsb.as<uint64_t>(), s->rg_tg.as<uint32_t>(), s->rg_tx_n, rr_map_of(s), wo_off, view_of(s),
+                           words, ovf);
+        uint32_t h = 0;
+        HIPCHECK(s, hipMemcpyAsync(&h, ovf, 4, hipMemcpyDeviceToHost, s->stream));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+        if (h) return fail(s, ACCORD_ERR_CAPACITY, "%u txns wait on more than %u range deps or touch more than %u "
+                                                   "RedundantBefore entries", h, RR_MAXR, RR_MAXE);
+    }
+    hipLaunchKernelGGL(wo_init_kernel, dim3(grid_for(n)), dim3(256), 0, s->stream, n, s->msb.as<uint64_t>(),
+                       s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
+                       cd.kd_key_off, cd.rd_val_off, cd.rd_vals, wo_off, view_of(s), words, aoi, pre,
+                       s->wo_eal.as<EalRec>());
     return ACCORD_OK;
 }
+
 
 // After the segment stage of a registered-status store: pairs on keys with registered entries get
 // their emitted entries materialised; returns the history array the fill must read.

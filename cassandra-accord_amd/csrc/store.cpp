@@ -125,7 +125,8 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2, &s->rg_kbound, &s->rg_cwflag, &s->rg_cwoff, &s->rg_cwpos, &s->rg_cwpm, &s->rg_cwchunk, &s->rg_hx, &s->rg_hu,
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
                       &s->rc_end2, &s->rc_kind2, &s->rc_first, &s->rc_flag, &s->rc_offs, &s->rdy_kseg0, &s->rdy_kseg1, &s->rdy_dirty, &s->rdy_dirty2, &s->rg_cchg, &s->rdy_dlist, &s->rdy_work, &s->rdy_wcnt, &s->rg_chg, &s->rdy_part, &s->rdy_sum, &s->rdy_out, &s->rdy_kb, &s->rdy_launch,
-                      &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero};
+                      &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero,
+                      &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->rr_ovf};
     accord_impl::shard_comm_destroy(s);
     accord_impl::ready_destroy(s);
     accord_impl::pinned_arena_destroy(s);
@@ -721,7 +722,7 @@ int32_t accord_store_reset(accord_store *s)
     s->has_batch = false; s->b_registered = false; s->computed = false; s->merged = false; s->m_pending = false;
     s->ds_cur = -1; s->wo_done = false; s->mc_next = 0;
     // RedundantBefore.EMPTY (its bounds are positions of the old stream) and MaxConflicts.EMPTY
-    s->rb_m = 0; s->rb_min_epoch = 0;
+    s->rb_m = 0; s->rb_min_epoch = 0; s->rb_ext = false;
     ++s->carry_version;
     accord_impl::ready_destroy(s);
     s->rdy_kb_host.clear(); s->rdy_kb_dirty = false; s->rdy_kb.release();

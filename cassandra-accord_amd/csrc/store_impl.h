@@ -160,6 +160,12 @@ struct accord_store {
     uint64_t rb_min_epoch = 0;
     DevBuf rb_start, rb_end, rb_bound, rb_sep, rb_eep, rb_cnt, rb_zero;
     DepSet rb_set;
+    // the rest of each Entry (accord_redundant_before_set_ex): locallyAppliedOrInvalidatedBefore,
+    // bootstrappedAt (positions, NONE = ACCORD_NO_TXN), stale; rb_ext = some entry can remove a dep
+    DevBuf rb_local, rb_boot, rb_stale;
+    bool rb_ext = false;
+    DevBuf wo_eal;                 // WaitingOn.executeAtLeast per txn of the initialised batch (EalRec)
+    DevBuf rr_ovf;                 // capacity counter of the removal kernels
     // execution readiness (ready.hip): the waiting set, one generation per initialised batch
     std::vector<accord_impl::ReadyGen *> rdy_gens;
     accord_impl::ReadyGen *rdy_batch_gen = nullptr;   // the current batch's generation (until the next batch)
@@ -177,6 +183,8 @@ struct accord_store {
     std::vector<uint32_t> rdy_kb_host;       // per key: shardRedundantBefore as a position (cumulative max)
     bool rdy_kb_dirty = false;
     std::vector<uint32_t> rdy_list;          // the last accord_ready_update's ready txns
+    std::vector<uint64_t> rdy_eal_msb, rdy_eal_lsb;   // and their executesAtLeast
+    std::vector<int32_t> rdy_eal_node;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
     accord_impl::PinnedBlock *dl_arena = nullptr;   // page-locked host arena of accord_deps_download
@@ -213,7 +221,8 @@ int32_t redundant_apply(accord_store *s);
 struct CurDeps {
     const uint32_t *kd_key_off, *kd_keys, *kd_val_off, *kd_vals, *kd_k2v_off, *kd_k2v;
     const uint32_t *rd_val_off, *rd_vals;
-    uint64_t tot_keys, tot_vals, tot_k2v, tot_rvals;
+    const uint32_t *rd_rng_off, *rd_rng_start, *rd_rng_end, *rd_r2v_off, *rd_r2v;
+    uint64_t tot_keys, tot_vals, tot_k2v, tot_rvals, tot_rngs, tot_r2v;
 };
 CurDeps cur_deps(const accord_store *s);
 }

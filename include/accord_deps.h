@@ -220,6 +220,25 @@ int32_t accord_store_reset(accord_store *store);               /* back to an emp
 int32_t accord_redundant_before_set(accord_store *store, uint32_t m, const uint32_t *start, const uint32_t *end,
                                     const uint64_t *start_epoch, const uint64_t *end_epoch, const uint32_t *bound,
                                     uint64_t min_epoch);
+/* The same map with the rest of each Entry (local/RedundantBefore.java:63-110):
+ * locallyAppliedOrInvalidatedBefore and bootstrappedAt as stream positions of this store
+ * (ACCORD_NO_TXN = TxnId.NONE; a TxnId the stream does not hold is given as the first position whose
+ * TxnId follows it -- the comparisons below only ask which positions precede it), and
+ * staleUntilAtLeast != null as stale[e] = 1 (NULL arrays: NONE, NONE, not stale -- accord_redundant_
+ * before_set).  The entries are the map's values as the reference holds them (Entry.merge has already
+ * cleared a locallyAppliedOrInvalidatedBefore at or below bootstrappedAt).  Readiness (accord_waiting_on_
+ * initialise, accord_ready_update) then applies Commands.updateWaitingOn's removal step
+ * (local/Commands.java:755-761): when CommandStore.hasLocallyRedundantDependencies(minWaitingOnTxnId,
+ * executeAt, participants) holds (RedundantBefore.status >= PARTIALLY_PRE_BOOTSTRAP_OR_STALE,
+ * local/CommandStore.java:672-678), CommandStore.removeRedundantDependencies (:601-670) stops waiting on
+ * the range deps in [bootstrappedAt, locallyAppliedOrInvalidatedBefore) of every entry their ranges
+ * meet, and on those before bootstrappedAt whose ranges the bootstrapping entries cover completely
+ * (RangeState.isFullyBootstrapping).  A waiting txn with more than 4096 RangeDeps txnIds, or whose
+ * participants touch more than 64 entries, is ACCORD_ERR_CAPACITY there while the map is set. */
+int32_t accord_redundant_before_set_ex(accord_store *store, uint32_t m, const uint32_t *start, const uint32_t *end,
+                                       const uint64_t *start_epoch, const uint64_t *end_epoch, const uint32_t *shard_bound,
+                                       const uint32_t *locally_applied_before, const uint32_t *bootstrapped_at,
+                                       const uint8_t *stale, uint64_t min_epoch);
 
 /* ---- synchronous batch entry: host in, host out ----
  * CommandStore.calculateDepsBatch(TxnId[], Seekables[], Timestamp[] executeAt, ...) ->
@@ -418,8 +437,9 @@ int32_t accord_waiting_on_compute(accord_store *store);                 /* devic
  * setAppliedOrInvalidated), executes after the txn (dep executeAt > own executeAt, own kind not
  * awaitsOnlyDeps: removeWaitingOn) or is APPLIED (setAppliedAndPropagate); bits [R_i, R_i + K_i) =
  * KeyDeps keys, set (CommandsForKey.notify clears them as the keys' predecessors apply).  The
- * propagation of an applied dep's own appliedOrInvalidated set is not modelled (taken as empty), nor
- * are pre-bootstrap / stale ranges (removeRedundantDependencies) or executeAtLeast.  hasBeen(PreCommitted)
+ * propagation of an applied dep's own appliedOrInvalidated set is not modelled (taken as empty).  With a
+ * RedundantBefore map set by accord_redundant_before_set_ex the removal step of updateWaitingOn
+ * (removeRedundantDependencies) runs first: a removed dep is not waited on and not visited.  hasBeen(PreCommitted)
  * is read from the InternalStatus (>= COMMITTED): a dep at SaveStatus PreCommitted* (InternalStatus
  * PREACCEPTED / ACCEPTED, local/CommandsForKey.java:213-215) is treated as uncommitted -- the bit stays
  * set until the dep commits (conservative: never released earlier than the reference).  level = 0,
@@ -446,17 +466,30 @@ int32_t accord_waiting_on_initialise(accord_store *store);
  *                    (:1406-1498), COMMIT records re-evaluated by updatePending once minUncommitted
  *                    passes them (:1315-1360), APPLY records released by notifyUnmanaged(APPLY,
  *                    next.executeAt) (:1264-1283).
- * The reference evaluates these tests when an event reaches the key (notifyAndUpdatePending,
- * :1163-1215); every call here evaluates them for every waiting txn, so a txn is reported at the first
- * call at which its test holds.  Not modelled: removeRedundantDependencies (bootstrap / stale ranges,
- * local/CommandStore.java:601-678) and executeAtLeast; setAppliedAndPropagate's propagation is implied
- * by the store-wide statuses (a propagated txn is APPLIED / invalidated here already).
- * `txn` stays valid until the next call on the store; `waiting` = txns still in the set. */
+ *   removal          with a map from accord_redundant_before_set_ex, each evaluation first applies
+ *                    updateWaitingOn's removeRedundantDependencies step (see there) to the range deps;
+ *   executeAtLeast   awaitsOnlyDeps kinds (ExclusiveSyncPoint, EphemeralRead): WaitingOn.updateExecuteAtLeast
+ *                    (local/Command.java:1511-1514) with the executeAt of every range dep visited while
+ *                    committed with a known executeAt after the txn's TxnId (local/Commands.java:782-783;
+ *                    an INVALID_OR_TRUNCATED / ERASED event carries none), and of the dep executing last
+ *                    when registerUnmanaged / updatePending leave an APPLY record (local/CommandsForKey.java:
+ *                    1370-1380, 1470-1478).
+ * The reference evaluates the key tests when an event reaches the key (notifyAndUpdatePending,
+ * :1163-1215); every call here evaluates them for every waiting txn whose inputs changed, so a txn is
+ * reported at the first call at which its test holds -- never later than the reference releases it
+ * (tests/test_ready.py compares with an event-driven restatement).  A waiting txn that is invalidated
+ * or truncated leaves the set unreported.  setAppliedAndPropagate's propagation is implied by the
+ * store-wide statuses (a propagated txn is APPLIED / invalidated here already).
+ * The arrays stay valid until the next call on the store; `waiting` = txns still in the set. */
 typedef struct {
     uint32_t  n;
     uint32_t  reserved;
     uint64_t  waiting;
     const uint32_t *txn;        /* [n] ascending global positions */
+    /* [n] Command.executesAtLeast() of each (local/Command.java:1145-1150): executeAtLeast for
+     * awaitsOnlyDeps kinds when it was updated, else the registered executeAt */
+    const uint64_t *eal_msb, *eal_lsb;
+    const int32_t  *eal_node;
 } accord_ready;
 int32_t accord_ready_update(accord_store *store, accord_ready *out);
 int32_t accord_waiting_on_download(accord_store *store, accord_waiting_on *out);

@@ -1980,9 +1980,29 @@ struct or_lstore {
     /* execution readiness: the txns whose WaitingOn was initialised and that are not ready yet */
     struct or_waiter *wt;
     uint32_t nwt, cwt;
+    /* RedundantBefore as readiness reads it (or_lstore_redundant): entries (rr_s, rr_e] ascending and
+     * disjoint, [rr_sep, rr_eep), locallyAppliedOrInvalidatedBefore / bootstrappedAt as positions
+     * (0xFFFFFFFF = TxnId.NONE), staleUntilAtLeast != null */
+    uint32_t rr_m;
+    uint32_t *rr_s, *rr_e, *rr_local, *rr_boot;
+    uint64_t *rr_sep, *rr_eep;
+    uint8_t *rr_stale;
+    /* event mode (or_lstore_event_mode): key bits are cleared only when notifyAndUpdatePending's events
+     * reach the key; wix[g] = waiter index + 1 of the txn at position g (0: not waiting) */
+    int event_mode;
+    uint32_t *wix;
+    uint32_t wix_cap;
 };
 
 static void or_lstore_waiters_free(or_lstore *s);
+typedef struct or_waiter or_waiter;
+static or_waiter *waiter_of(const or_lstore *s, uint32_t g);
+static int waiter_unmanaged(const or_lstore *s, const or_waiter *x);
+static void lstore_register_unmanaged(or_lstore *s, or_waiter *x);
+static void lstore_event(or_lstore *s, uint32_t k, uint32_t X, uint8_t prev, uint8_t nw, const ts_t *exec);
+static void cfk_nexts(const or_lstore *s, const cfk_t *c, long *min_unc, long *next, long *next_write);
+static void cfk_notify_unmanaged(or_lstore *s, uint32_t k, int commit, long min_unc, long next);
+static int wix_rebuild(or_lstore *s);
 
 or_lstore *or_lstore_create(uint32_t nkeys)
 {
@@ -2003,6 +2023,8 @@ void or_lstore_free(or_lstore *s)
     free(s->cfks); free(s->tbl); free(s->koff); free(s->kord); free(s->status); free(s->exec);
     free(s->roff); free(s->rst); free(s->ren);
     or_lstore_waiters_free(s);
+    free(s->rr_s); free(s->rr_e); free(s->rr_local); free(s->rr_boot); free(s->rr_sep); free(s->rr_eep); free(s->rr_stale);
+    free(s->wix);
     free(s);
 }
 
@@ -2224,8 +2246,13 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
         const int has_info = nw >= S_ACCEPTED && nw <= S_APPLIED;
         ts_t ex = s->exec[g];
         if (has_info) { ex.msb = emsb[r]; ex.lsb = elsb[r]; ex.node = enode[r]; }
+        const uint8_t was = s->status[g];
         s->status[g] = nw;
         s->exec[g] = ex;
+        if (s->event_mode && nw >= S_STABLE && nw < S_INVALID_OR_TRUNCATED && was < S_STABLE) {
+            or_waiter *x = waiter_of(s, g);                  /* hasBeen(Stable): registerUnmanaged */
+            if (x && waiter_unmanaged(s, x)) lstore_register_unmanaged(s, x);
+        }
         if (is_globally_visible(kind_of(s->tbl[g].lsb)) != 1) continue;   /* never inserted into CFK */
         if (domain_of(s->tbl[g].lsb) != 0) continue;                       /* range command: status only */
         /* Erased / Invalidated leave CommandsForKey as INVALID_OR_TRUNCATED does */
@@ -2233,7 +2260,10 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
         for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p) {
             cfk_t *c = &s->cfks[s->kord[p]];
             if (g < c->redundant_before) continue;       /* truncated from this key */
+            const long at = cfk_search(c, s->tbl, &s->tbl[g]);
+            const uint8_t prev = at >= 0 ? c->txns[at].status : S_TRANSITIVELY_KNOWN;
             if (cfk_update_status(c, s->tbl, g, cs, &ex)) { free(pos); return -1; }
+            if (s->event_mode) lstore_event(s, s->kord[p], g, prev, cs, &ex);
         }
     }
     free(pos);
@@ -2260,6 +2290,11 @@ int or_lstore_truncate(or_lstore *s, uint32_t m, const uint32_t *start, const ui
         if (!nt) return -1;
         memcpy(nt, c->txns + pos, (size_t)(c->n - pos) * sizeof(txninfo_t));
         if (cfk_rebuild(c, nt, c->n - pos)) return -1;
+        if (s->event_mode) {                 /* notifyAndUpdatePending(safeStore, prevCfk) (:1205-1213) */
+            long min_unc, next, nwr;
+            cfk_nexts(s, c, &min_unc, &next, &nwr);
+            if (min_unc < 0 || next >= 0) cfk_notify_unmanaged(s, k, 0, min_unc, next);
+        }
     }
     return 0;
 }
@@ -2295,18 +2330,26 @@ typedef struct or_waiter {
     uint64_t *words, *aoi;       /* WaitingOn bits: [0, nr) txnIds, [nr, nr + nk) keys */
     uint8_t *pend;               /* per key (unmanaged): 0 unregistered, 1 COMMIT, 2 APPLY, 3 released */
     uint32_t *until;             /* per key: the waitingUntil txn (position) */
+    uint32_t nrr;                /* its RangeDeps ranges (rrs, rre] and their txn index lists */
+    uint32_t *rrs, *rre, *r2voff, *r2v;
+    ts_t eal;                    /* WaitingOn.executeAtLeast (local/Command.java:1409-1513), when has_eal */
+    int has_eal;
 } or_waiter;
+
+static void waiter_free(or_waiter *x)
+{
+    free(x->rdeps); free(x->keys); free(x->kdoff); free(x->kdeps); free(x->words); free(x->aoi);
+    free(x->pend); free(x->until); free(x->rrs); free(x->rre); free(x->r2voff); free(x->r2v);
+}
 
 static void or_lstore_waiters_free(or_lstore *s)
 {
-    for (uint32_t w = 0; w < s->nwt; ++w) {
-        or_waiter *x = &s->wt[w];
-        free(x->rdeps); free(x->keys); free(x->kdoff); free(x->kdeps); free(x->words); free(x->aoi);
-        free(x->pend); free(x->until);
-    }
+    for (uint32_t w = 0; w < s->nwt; ++w) waiter_free(&s->wt[w]);
     free(s->wt);
     s->wt = NULL; s->nwt = s->cwt = 0;
 }
+
+static int lstore_remove_redundant(const or_lstore *s, struct or_waiter *x, const ts_t *ex);
 
 int or_lstore_waiting_add(or_lstore *s, uint32_t base, const or_deps *d, uint32_t n)
 {
@@ -2335,6 +2378,22 @@ int or_lstore_waiting_add(or_lstore *s, uint32_t base, const or_deps *d, uint32_
         x->pend = (uint8_t *)calloc((size_t)x->nk + 1, 1);
         x->until = (uint32_t *)calloc((size_t)x->nk + 1, 4);
         if (!x->rdeps || !x->keys || !x->kdoff || !x->kdeps || !x->words || !x->aoi || !x->pend || !x->until) return -1;
+        x->nrr = d->rd_rng_off ? d->rd_rng_off[i + 1] - d->rd_rng_off[i] : 0;
+        const uint32_t rbody = x->nrr ? d->rd_r2v_off[i + 1] - d->rd_r2v_off[i] - x->nrr : 0;
+        x->rrs = (uint32_t *)malloc(((size_t)x->nrr + 1) * 4);
+        x->rre = (uint32_t *)malloc(((size_t)x->nrr + 1) * 4);
+        x->r2voff = (uint32_t *)malloc(((size_t)x->nrr + 1) * 4);
+        x->r2v = (uint32_t *)malloc(((size_t)rbody + 1) * 4);
+        if (!x->rrs || !x->rre || !x->r2voff || !x->r2v) return -1;
+        x->r2voff[0] = 0;
+        for (uint32_t q = 0; q < x->nrr; ++q) {           /* RangeDeps: ranges, then per range its txn indices */
+            x->rrs[q] = d->rd_rng_start[d->rd_rng_off[i] + q];
+            x->rre[q] = d->rd_rng_end[d->rd_rng_off[i] + q];
+            const int32_t *blk = d->rd_r2v + d->rd_r2v_off[i];
+            const uint32_t b = q == 0 ? x->nrr : (uint32_t)blk[q - 1], e = (uint32_t)blk[q];
+            for (uint32_t y = b; y < e; ++y) x->r2v[x->r2voff[q] + (y - b)] = (uint32_t)blk[y];
+            x->r2voff[q + 1] = x->r2voff[q] + (e - b);
+        }
         for (uint32_t j = 0; j < x->nr; ++j) x->rdeps[j] = d->rd_vals[d->rd_val_off[i] + j];
         x->kdoff[0] = 0;
         for (uint32_t q = 0; q < x->nk; ++q) {
@@ -2345,6 +2404,25 @@ int or_lstore_waiting_add(or_lstore *s, uint32_t base, const or_deps *d, uint32_
         }
         for (uint32_t b = 0; b < x->nr + x->nk; ++b) x->words[b / 64] |= 1ULL << (b & 63);
         ++s->nwt;
+        /* initialiseWaitingOn's updateWaitingOn removes the redundant deps under the map of that time
+         * (local/Commands.java:735-761); its dep visit is the first or_lstore_ready evaluation */
+        if (lstore_remove_redundant(s, x, &s->exec[x->g])) return -1;
+    }
+    if (s->event_mode) {
+        /* the WaitingOn exists from the txn's STABLE transition (initialiseWaitingOn): the txns that are
+         * Stable already take that transition's CommandsForKey step now, in TxnId order */
+        if (wix_rebuild(s)) return -1;
+        for (uint32_t i = 0; i < n; ++i) {
+            or_waiter *x = waiter_of(s, base + i);
+            if (!x) continue;
+            const uint32_t g = x->g;
+            const uint8_t st = s->status[g];
+            if (st < S_STABLE || st >= S_INVALID_OR_TRUNCATED) continue;
+            if (waiter_unmanaged(s, x)) { lstore_register_unmanaged(s, x); continue; }
+            if (st != S_STABLE) continue;
+            for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p)
+                if (g >= s->cfks[s->kord[p]].redundant_before) lstore_event(s, s->kord[p], g, S_STABLE, S_STABLE, &s->exec[g]);
+        }
     }
     return 0;
 }
@@ -2376,8 +2454,9 @@ static void cfk_next(const cfk_t *c, long *min_unc, long *next)
  * ready, 0 = pending APPLY (*until = the relevant dep executing last), -1 = pending COMMIT (*until =
  * the last dep), for a waiter at executeAt ex; `reg` = registration (uncommitted deps -> COMMIT) */
 static int unmanaged_eval(const or_lstore *s, const cfk_t *c, const or_waiter *x, uint32_t q, const ts_t *ex,
-                          int only_deps, int reg, uint32_t *until)
+                          int only_deps, int reg, uint32_t *until, long *executes_at)
 {
+    *executes_at = -1;
     const uint32_t *dl = x->kdeps + x->kdoff[q];
     const uint32_t nd = x->kdoff[q + 1] - x->kdoff[q];
     uint32_t i = 0;
@@ -2396,12 +2475,362 @@ static int unmanaged_eval(const or_lstore *s, const cfk_t *c, const or_waiter *x
         }
     }
     if (ready) return 1;
+    *executes_at = best;                                        /* executesAt: the relevant dep executing last */
     if (to_apply) { *until = best < 0 ? dl[nd - 1] : (uint32_t)best; return 0; }
     *until = dl[nd - 1];
     return -1;
 }
 
+int or_lstore_redundant(or_lstore *s, uint32_t m, const uint32_t *start, const uint32_t *end, const uint64_t *sep,
+                        const uint64_t *eep, const uint32_t *local, const uint32_t *boot, const uint8_t *stale)
+{
+    for (uint32_t e = 0; e < m; ++e) if (start[e] >= end[e] || (e && end[e - 1] > start[e])) return -1;
+    free(s->rr_s); free(s->rr_e); free(s->rr_local); free(s->rr_boot); free(s->rr_sep); free(s->rr_eep); free(s->rr_stale);
+    s->rr_s = s->rr_e = s->rr_local = s->rr_boot = NULL; s->rr_sep = s->rr_eep = NULL; s->rr_stale = NULL;
+    s->rr_m = 0;
+    if (!m) return 0;
+    s->rr_s = (uint32_t *)malloc((size_t)m * 4); s->rr_e = (uint32_t *)malloc((size_t)m * 4);
+    s->rr_local = (uint32_t *)malloc((size_t)m * 4); s->rr_boot = (uint32_t *)malloc((size_t)m * 4);
+    s->rr_sep = (uint64_t *)malloc((size_t)m * 8); s->rr_eep = (uint64_t *)malloc((size_t)m * 8);
+    s->rr_stale = (uint8_t *)malloc(m);
+    if (!s->rr_s || !s->rr_e || !s->rr_local || !s->rr_boot || !s->rr_sep || !s->rr_eep || !s->rr_stale) return -1;
+    memcpy(s->rr_s, start, (size_t)m * 4); memcpy(s->rr_e, end, (size_t)m * 4);
+    memcpy(s->rr_local, local, (size_t)m * 4); memcpy(s->rr_boot, boot, (size_t)m * 4);
+    memcpy(s->rr_sep, sep, (size_t)m * 8); memcpy(s->rr_eep, eep, (size_t)m * 8);
+    memcpy(s->rr_stale, stale, m);
+    s->rr_m = m;
+    return 0;
+}
+
+/* RedundantStatus (local/RedundantStatus.java) in declaration order, and its merge table (:91-141) */
+enum { RS_NOT_OWNED, RS_LIVE, RS_PARTIALLY_PRE_BOOTSTRAP_OR_STALE, RS_PRE_BOOTSTRAP_OR_STALE,
+       RS_REDUNDANT_PRE_BOOTSTRAP_OR_STALE, RS_LOCALLY_REDUNDANT, RS_SHARD_REDUNDANT };
+static const uint8_t RS_MERGE[7][7] = {
+    /* NOT_OWNED */ {0, 1, 2, 3, 4, 5, 6},
+    /* LIVE      */ {1, 1, 2, 2, 4, 4, 4},
+    /* PARTIALLY */ {2, 2, 2, 2, 4, 4, 4},
+    /* PRE_BOOT  */ {3, 2, 2, 3, 4, 4, 4},
+    /* RED_PRE   */ {4, 4, 4, 4, 4, 4, 4},
+    /* LOCALLY   */ {5, 4, 4, 4, 4, 5, 5},
+    /* SHARD     */ {6, 4, 4, 4, 4, 5, 6},
+};
+
+/* does the map entry (es, ee] meet the participants of the txn at position g (its keys or ranges)? */
+static int rr_meets(const or_lstore *s, uint32_t g, uint32_t es, uint32_t ee)
+{
+    if (domain_of(s->tbl[g].lsb) != 0) {
+        for (uint32_t a = s->roff[g]; a < s->roff[g + 1]; ++a)
+            if (range_intersects_range(es, ee, s->rst[a], s->ren[a])) return 1;
+        return 0;
+    }
+    for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p)
+        if (range_intersects_key(es, ee, s->kord[p])) return 1;
+    return 0;
+}
+
+/* d.txnIds().find(bound), insertion point (positions ascend with TxnIds); TxnId.NONE precedes all */
+static uint32_t rr_find(const or_waiter *x, uint32_t bound)
+{
+    if (bound == 0xFFFFFFFFu) return 0;
+    uint32_t lo = 0, hi = x->nr;
+    while (lo < hi) { uint32_t m = (lo + hi) / 2; if (x->rdeps[m] < bound) lo = m + 1; else hi = m; }
+    return lo;
+}
+
+typedef struct { uint32_t n, cap; uint32_t *a, *b; } rr_set;   /* disjoint intervals (a, b] */
+
+static int rr_set_push(rr_set *r, uint32_t a, uint32_t b)
+{
+    if (r->n == r->cap) {
+        uint32_t c = r->cap ? r->cap * 2 : 8;
+        uint32_t *na = (uint32_t *)realloc(r->a, (size_t)c * 4), *nb;
+        if (!na) return -1;
+        r->a = na;
+        nb = (uint32_t *)realloc(r->b, (size_t)c * 4);
+        if (!nb) return -1;
+        r->b = nb; r->cap = c;
+    }
+    r->a[r->n] = a; r->b[r->n] = b; ++r->n;
+    return 0;
+}
+
+/* Commands.updateWaitingOn's removal step (local/Commands.java:755-761):
+ * CommandStore.hasLocallyRedundantDependencies(minWaitingOnTxnId, executeAt, participants)
+ * (local/CommandStore.java:672-678: RedundantBefore.status >= PARTIALLY_PRE_BOOTSTRAP_OR_STALE, folding
+ * Entry.getAndMerge :157-161 / get :225-240 over the entries the participants touch), then
+ * CommandStore.removeRedundantDependencies (:601-670) literally: per entry, ascending, the range deps
+ * meeting its range with txnIdx in [bootstrapIdx, appliedIdx) stop being waited on, and those below
+ * bootstrapIdx whose every range is covered by bootstrapping entries (RangeState.isFullyBootstrapping,
+ * the remaining ranges carried across entries).  Range-dep bits only (WaitingOn.txnIds = RangeDeps). */
+static int lstore_remove_redundant(const or_lstore *s, or_waiter *x, const ts_t *ex)
+{
+    if (!s->rr_m || !x->nr) return 0;
+    uint32_t j0 = 0xFFFFFFFFu;                            /* WaitingOn.Update.minWaitingOnTxnId (:1500-1504) */
+    for (uint32_t b = 0; b < x->nr + x->nk; ++b) if (w_test(x->words, b)) { j0 = b; break; }
+    if (j0 >= x->nr) return 0;
+    const uint32_t g = x->g, mpos = x->rdeps[j0];
+    const uint64_t min_epoch = s->tbl[mpos].msb >> 15, exec_epoch = ex->msb >> 15;
+    int st = RS_NOT_OWNED;
+    for (uint32_t e = 0; e < s->rr_m; ++e) {
+        if (!rr_meets(s, g, s->rr_s[e], s->rr_e[e])) continue;
+        if (exec_epoch < s->rr_sep[e] || min_epoch >= s->rr_eep[e]) continue;        /* outOfBounds */
+        int es;                                                                        /* Entry.get(minId) */
+        if (s->rr_stale[e] || (s->rr_boot[e] != 0xFFFFFFFFu && s->rr_boot[e] > mpos)) es = RS_PRE_BOOTSTRAP_OR_STALE;
+        else if (s->rr_local[e] != 0xFFFFFFFFu && s->rr_local[e] > mpos) es = RS_LOCALLY_REDUNDANT;   /* or SHARD_: same here */
+        else es = RS_LIVE;
+        st = RS_MERGE[st][es];
+    }
+    if (st < RS_PARTIALLY_PRE_BOOTSTRAP_OR_STALE) return 0;
+    rr_set *part = (rr_set *)calloc(x->nr ? x->nr : 1, sizeof(rr_set));   /* partiallyBootstrapping */
+    uint8_t *has = (uint8_t *)calloc(x->nr ? x->nr : 1, 1);
+    int rc = -1;
+    if (!part || !has) goto out;
+    for (uint32_t e = 0; e < s->rr_m; ++e) {
+        if (!rr_meets(s, g, s->rr_s[e], s->rr_e[e])) continue;
+        const uint32_t es = s->rr_s[e], ee = s->rr_e[e];
+        const uint32_t bidx = rr_find(x, s->rr_boot[e]), aidx = rr_find(x, s->rr_local[e]);
+        if (aidx > bidx)                                   /* d.forEach(e.range): the txns of its ranges meeting it */
+            for (uint32_t q = 0; q < x->nrr; ++q) {
+                if (!range_intersects_range(x->rrs[q], x->rre[q], es, ee)) continue;
+                for (uint32_t y = x->r2voff[q]; y < x->r2voff[q + 1]; ++y) {
+                    const uint32_t j = x->r2v[y];
+                    if (j >= bidx && j < aidx) w_clear(x->words, j);
+                }
+            }
+        if (bidx > 0)
+            for (uint32_t q = 0; q < x->nrr; ++q) {
+                if (!range_intersects_range(x->rrs[q], x->rre[q], es, ee)) continue;
+                for (uint32_t y = x->r2voff[q]; y < x->r2voff[q + 1]; ++y) {
+                    const uint32_t j = x->r2v[y];
+                    if (!(j < bidx && w_test(x->words, j))) continue;
+                    /* isFullyBootstrapping(j): every range of j inside e.range, else j's remaining ranges
+                     * (first: all of them) minus e.range, fully when none remain */
+                    int fully = 1;
+                    for (uint32_t q2 = 0; q2 < x->nrr && fully; ++q2)
+                        for (uint32_t y2 = x->r2voff[q2]; y2 < x->r2voff[q2 + 1]; ++y2)
+                            if (x->r2v[y2] == j && !(es <= x->rrs[q2] && x->rre[q2] <= ee)) { fully = 0; break; }
+                    if (!fully) {
+                        rr_set *r = &part[j];
+                        if (!has[j]) {
+                            has[j] = 1;
+                            for (uint32_t q2 = 0; q2 < x->nrr; ++q2)
+                                for (uint32_t y2 = x->r2voff[q2]; y2 < x->r2voff[q2 + 1]; ++y2)
+                                    if (x->r2v[y2] == j && rr_set_push(r, x->rrs[q2], x->rre[q2])) goto out;
+                        }
+                        rr_set nr = {0, 0, NULL, NULL};
+                        for (uint32_t u = 0; u < r->n; ++u) {          /* remaining.subtract(e.range) */
+                            const uint32_t a = r->a[u], b = r->b[u];
+                            if (a < (b < es ? b : es) && rr_set_push(&nr, a, b < es ? b : es)) { free(nr.a); free(nr.b); goto out; }
+                            if ((a > ee ? a : ee) < b && rr_set_push(&nr, a > ee ? a : ee, b)) { free(nr.a); free(nr.b); goto out; }
+                        }
+                        free(r->a); free(r->b);
+                        *r = nr;
+                        fully = r->n == 0;
+                    }
+                    if (fully) w_clear(x->words, j);
+                }
+            }
+    }
+    rc = 0;
+out:
+    if (part) for (uint32_t j = 0; j < x->nr; ++j) { free(part[j].a); free(part[j].b); }
+    free(part); free(has);
+    return rc;
+}
+
+static void eal_merge(or_waiter *x, const ts_t *t)          /* updateExecuteAtLeast: Timestamp.nonNullOrMax */
+{
+    if (!x->has_eal || ts_cmp(&x->eal, t) < 0) { x->eal = *t; x->has_eal = 1; }
+}
+
+/* CommandsForKey.notify's test for the STABLE managed waiter x on its key slot q
+ * (local/CommandsForKey.java:1512-1635): expectMissingCount == |missing| */
+static int managed_test(const or_lstore *s, const cfk_t *c, const or_waiter *x, uint32_t q)
+{
+    const uint32_t g = x->g;
+    const ts_t *ex = &s->exec[g];
+    const int wk = witnesses_of(kind_of(s->tbl[g].lsb));
+    uint32_t expect = 0, missing = 0;
+    for (uint32_t a = 0; a < c->nc; ++a) {              /* committed[], executeAt order */
+        const txninfo_t *t = &c->txns[c->committed[a]];
+        if (ts_cmp(&t->execute_at, ex) >= 0) break;
+        if (t->status == S_APPLIED) continue;
+        if (kinds_test(wk, kind_of(s->tbl[t->txn].lsb))) ++expect;
+    }
+    const uint32_t *dl = x->kdeps + x->kdoff[q];
+    const uint32_t nd = x->kdoff[q + 1] - x->kdoff[q];
+    for (uint32_t a = 0; a < c->n; ++a) {               /* backfill: uncommitted, TxnId order */
+        const txninfo_t *t = &c->txns[a];
+        if (ts_cmp(&s->tbl[t->txn], ex) >= 0) break;
+        if (t->status >= S_COMMITTED || t->txn == g) continue;
+        if (!kinds_test(wk, kind_of(s->tbl[t->txn].lsb))) continue;
+        ++expect;
+        uint32_t lo = 0, hi = nd;                        /* in its deps? */
+        while (lo < hi) { uint32_t m = (lo + hi) / 2; if (dl[m] < t->txn) lo = m + 1; else hi = m; }
+        if (!(lo < nd && dl[lo] == t->txn)) ++missing;
+    }
+    return expect == missing;
+}
+
+/* the unmanaged waiter x's key slot q: registerUnmanaged (:1406-1498) */
+static void unmanaged_register(const or_lstore *s, const cfk_t *c, or_waiter *x, uint32_t q)
+{
+    const int kind = kind_of(s->tbl[x->g].lsb), only_deps = kind == K_EXCL_SYNC_POINT || kind == K_EPHEMERAL_READ;
+    long ea;
+    const int r = unmanaged_eval(s, c, x, q, &s->exec[x->g], only_deps, 1, &x->until[q], &ea);
+    if (r == 1) { x->pend[q] = 3; w_clear(x->words, x->nr + q); return; }
+    x->pend[q] = r == 0 ? 2 : 1;
+    if (r == 0 && only_deps && ea >= 0) eal_merge(x, &s->exec[ea]);   /* :1470-1478 */
+}
+
+/* notifyUnmanaged(COMMIT, minUncommitted) for a COMMIT record: updatePending (:1315-1360) */
+static void unmanaged_commit(const or_lstore *s, const cfk_t *c, or_waiter *x, uint32_t q, long min_unc)
+{
+    if (x->pend[q] != 1 || !(min_unc < 0 || (uint32_t)min_unc > x->until[q])) return;
+    const int kind = kind_of(s->tbl[x->g].lsb), only_deps = kind == K_EXCL_SYNC_POINT || kind == K_EPHEMERAL_READ;
+    long ea;
+    const int r = unmanaged_eval(s, c, x, q, &s->exec[x->g], only_deps, 0, &x->until[q], &ea);
+    if (r == 1) { x->pend[q] = 3; w_clear(x->words, x->nr + q); return; }
+    x->pend[q] = 2;
+    if (only_deps && ea >= 0) eal_merge(x, &s->exec[ea]);                /* :1370-1380 */
+}
+
+/* notifyUnmanaged(APPLY, next.executeAt) for an APPLY record (:1264-1283); next < 0: Timestamp.MAX */
+static void unmanaged_apply(const or_lstore *s, or_waiter *x, uint32_t q, long next)
+{
+    if (x->pend[q] == 2 && (next < 0 || ts_cmp(&s->exec[x->until[q]], &s->exec[next]) < 0)) {
+        x->pend[q] = 3; w_clear(x->words, x->nr + q);
+    }
+}
+
+/* ---- event mode: key bits are cleared when notifyAndUpdatePending's events reach the key ---- */
+void or_lstore_event_mode(or_lstore *s, int on) { s->event_mode = on; }
+
+static int wix_rebuild(or_lstore *s)
+{
+    if (s->wix_cap < s->n + 1) {
+        uint32_t *w = (uint32_t *)realloc(s->wix, ((size_t)s->cap + 1) * 4);
+        if (!w) return -1;
+        s->wix = w; s->wix_cap = s->cap + 1;
+    }
+    memset(s->wix, 0, (size_t)s->wix_cap * 4);
+    for (uint32_t w = 0; w < s->nwt; ++w) s->wix[s->wt[w].g] = w + 1;
+    return 0;
+}
+
+static or_waiter *waiter_of(const or_lstore *s, uint32_t g)
+{
+    return s->wix && g < s->wix_cap && s->wix[g] ? &s->wt[s->wix[g] - 1] : NULL;
+}
+
+static long waiter_slot(const or_waiter *x, uint32_t k)          /* KeyDeps key slot of k, or -1 */
+{
+    uint32_t lo = 0, hi = x->nk;
+    while (lo < hi) { uint32_t m = (lo + hi) / 2; if (x->keys[m] < k) lo = m + 1; else hi = m; }
+    return lo < x->nk && x->keys[lo] == k ? (long)lo : -1;
+}
+
+/* the CommandsForKey constructor's minUncommitted, next, nextWrite (:432-461), positions or -1 */
+static void cfk_nexts(const or_lstore *s, const cfk_t *c, long *min_unc, long *next, long *next_write)
+{
+    *min_unc = *next = *next_write = -1;
+    for (uint32_t i = 0; i < c->n; ++i) {
+        const txninfo_t *t = &c->txns[i];
+        if (t->status == S_INVALID_OR_TRUNCATED) continue;
+        if (t->status >= S_COMMITTED) {
+            if (t->status < S_APPLIED) {
+                if (kind_of(s->tbl[t->txn].lsb) == K_WRITE && (*next_write < 0 || ts_cmp(&s->exec[*next_write], &t->execute_at) > 0))
+                    *next_write = t->txn;
+                if (*next < 0 || ts_cmp(&s->exec[*next], &t->execute_at) > 0) *next = t->txn;
+            }
+        } else if (*min_unc < 0) *min_unc = t->txn;
+    }
+    if (*min_unc >= 0) {
+        if (*next >= 0 && ts_cmp(&s->tbl[*min_unc], &s->exec[*next]) < 0) *next = -1;
+        if (*next_write >= 0 && ts_cmp(&s->tbl[*min_unc], &s->exec[*next_write]) < 0) *next_write = -1;
+    }
+}
+
+/* notify(kinds, from, to) (:1501-1511): the STABLE waiters in committed[] executing in [from, to]
+ * (from NULL = Timestamp.NONE, to NULL = Timestamp.MAX) run the count test on key k */
+static void cfk_notify(or_lstore *s, uint32_t k, const ts_t *from, const ts_t *to)
+{
+    const cfk_t *c = &s->cfks[k];
+    uint32_t i = 0;
+    if (from) while (i < c->nc && ts_cmp(&c->txns[c->committed[i]].execute_at, from) < 0) ++i;
+    for (; i < c->nc; ++i) {
+        const txninfo_t *t = &c->txns[c->committed[i]];
+        if (to && ts_cmp(&t->execute_at, to) > 0) break;
+        if (t->status != S_STABLE) continue;
+        or_waiter *x = waiter_of(s, t->txn);
+        if (!x || s->status[x->g] != S_STABLE) continue;
+        const long q = waiter_slot(x, k);
+        if (q < 0 || !w_test(x->words, x->nr + (uint32_t)q)) continue;
+        if (managed_test(s, c, x, (uint32_t)q)) w_clear(x->words, x->nr + (uint32_t)q);
+    }
+}
+
+static int waiter_unmanaged(const or_lstore *s, const or_waiter *x)
+{
+    return !(domain_of(s->tbl[x->g].lsb) == 0 && is_globally_visible(kind_of(s->tbl[x->g].lsb)) == 1);
+}
+
+/* notifyUnmanaged(COMMIT / APPLY) over the unmanaged records of key k (:1264-1283) */
+static void cfk_notify_unmanaged(or_lstore *s, uint32_t k, int commit, long min_unc, long next)
+{
+    const cfk_t *c = &s->cfks[k];
+    for (uint32_t w = 0; w < s->nwt; ++w) {
+        or_waiter *x = &s->wt[w];
+        if (!waiter_unmanaged(s, x)) continue;
+        const long q = waiter_slot(x, k);
+        if (q < 0 || !w_test(x->words, x->nr + (uint32_t)q)) continue;
+        if (commit) unmanaged_commit(s, c, x, (uint32_t)q, min_unc);
+        else unmanaged_apply(s, x, (uint32_t)q, next);
+    }
+}
+
+/* CommandsForKey.notifyAndUpdatePending(safeStore, txnId, newStatus, newExecuteAt, prevCfk)
+ * (:1163-1215) after the txn at position X moved from prev to nw on key k */
+static void lstore_event(or_lstore *s, uint32_t k, uint32_t X, uint8_t prev, uint8_t nw, const ts_t *exec)
+{
+    long min_unc, next, nwr;
+    cfk_nexts(s, &s->cfks[k], &min_unc, &next, &nwr);
+    switch (nw) {
+    case S_STABLE: case S_COMMITTED: {
+        const int cmp = nwr < 0 ? -1 : ts_cmp(exec, &s->exec[nwr]);
+        if (cmp <= 0) {
+            if (nw == S_COMMITTED) break;
+            cfk_notify(s, k, next >= 0 ? &s->exec[next] : NULL, exec);     /* the txn itself may execute */
+        } else {
+            /* waiters on us may be ready, if we execute after them, were known and not committed */
+            if (prev == S_COMMITTED || ts_cmp(&s->exec[nwr], &s->tbl[X]) < 0 || ts_cmp(exec, &s->tbl[X]) == 0) break;
+            cfk_notify(s, k, &s->exec[next], &s->exec[nwr]);
+        }
+        break;
+    }
+    case S_APPLIED: case S_INVALID_OR_TRUNCATED:
+        if (next >= 0) cfk_notify(s, k, &s->exec[next], nwr >= 0 ? &s->exec[nwr] : NULL);
+        break;
+    default: break;
+    }
+    if (nw >= S_COMMITTED && prev < S_COMMITTED) cfk_notify_unmanaged(s, k, 1, min_unc, next);
+    if (min_unc < 0 || next >= 0) cfk_notify_unmanaged(s, k, 0, min_unc, next);
+}
+
+/* an unmanaged waiter that has now been Stable: registerUnmanaged on its keys */
+static void lstore_register_unmanaged(or_lstore *s, or_waiter *x)
+{
+    for (uint32_t q = 0; q < x->nk; ++q)
+        if (w_test(x->words, x->nr + q) && x->pend[q] == 0) unmanaged_register(s, &s->cfks[x->keys[q]], x, q);
+}
+
 int or_lstore_ready(or_lstore *s, uint32_t *ready_out, uint32_t *nready)
+{
+    return or_lstore_ready_ex(s, ready_out, nready, NULL, NULL, NULL);
+}
+
+int or_lstore_ready_ex(or_lstore *s, uint32_t *ready_out, uint32_t *nready, uint64_t *eal_msb, uint64_t *eal_lsb,
+                       int32_t *eal_node)
 {
     uint32_t nout = 0, keep = 0;
     for (uint32_t w = 0; w < s->nwt; ++w) {
@@ -2412,85 +2841,70 @@ int or_lstore_ready(or_lstore *s, uint32_t *ready_out, uint32_t *nready)
         const int only_deps = kind == K_EXCL_SYNC_POINT || kind == K_EPHEMERAL_READ;   /* awaitsOnlyDeps */
         const ts_t *ex = &s->exec[g];
         if (st >= S_INVALID_OR_TRUNCATED) {      /* invalidated / truncated: leaves the waiting set, never ready */
-            free(x->rdeps); free(x->keys); free(x->kdoff); free(x->kdeps); free(x->words); free(x->aoi);
-            free(x->pend); free(x->until);
+            waiter_free(x);
             continue;
         }
+        if (lstore_remove_redundant(s, x, ex)) return -1;
         /* range-dep bits: Commands.updateWaitingOn (forEachWaitingOnId: reverse order) */
         for (uint32_t j = x->nr; j-- > 0;) {
             if (!w_test(x->words, j)) continue;
             const uint32_t dg = x->rdeps[j];
             const uint8_t ds = s->status[dg];
             if (ds < S_COMMITTED) continue;                     /* !hasBeen(PreCommitted) */
+            /* updateExecuteAtLeast (:782-783): a dep with a known executeAt after the waiter's TxnId;
+             * an INVALID_OR_TRUNCATED event carries no executeAt */
+            if (only_deps && ds <= S_APPLIED && ts_cmp(&s->exec[dg], &s->tbl[g]) > 0) eal_merge(x, &s->exec[dg]);
             if (ds >= S_INVALID_OR_TRUNCATED) { w_clear(x->words, j); if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63); }
             else if (!only_deps && ts_cmp(&s->exec[dg], ex) > 0) w_clear(x->words, j);
             else if (ds == S_APPLIED) { w_clear(x->words, j); if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63); }
         }
         const int managed = rdom == 0 && is_globally_visible(kind) == 1;
-        for (uint32_t q = 0; q < x->nk; ++q) {
+        for (uint32_t q = 0; q < x->nk && !s->event_mode; ++q) {   /* event mode: the events clear key bits */
             const uint32_t b = x->nr + q;
             if (!w_test(x->words, b)) continue;
             const cfk_t *c = &s->cfks[x->keys[q]];
             if (managed) {
-                if (st != S_STABLE) continue;
-                /* CommandsForKey.notify's test for this txn on this key */
-                const int wk = witnesses_of(kind);
-                uint32_t expect = 0, missing = 0;
-                for (uint32_t a = 0; a < c->nc; ++a) {              /* committed[], executeAt order */
-                    const txninfo_t *t = &c->txns[c->committed[a]];
-                    if (ts_cmp(&t->execute_at, ex) >= 0) break;
-                    if (t->status == S_APPLIED) continue;
-                    if (kinds_test(wk, kind_of(s->tbl[t->txn].lsb))) ++expect;
-                }
-                const uint32_t *dl = x->kdeps + x->kdoff[q];
-                const uint32_t nd = x->kdoff[q + 1] - x->kdoff[q];
-                for (uint32_t a = 0; a < c->n; ++a) {               /* backfill: uncommitted, TxnId order */
-                    const txninfo_t *t = &c->txns[a];
-                    if (ts_cmp(&s->tbl[t->txn], ex) >= 0) break;
-                    if (t->status >= S_COMMITTED || t->txn == g) continue;
-                    if (!kinds_test(wk, kind_of(s->tbl[t->txn].lsb))) continue;
-                    ++expect;
-                    uint32_t lo = 0, hi = nd;                        /* in its deps? */
-                    while (lo < hi) { uint32_t m = (lo + hi) / 2; if (dl[m] < t->txn) lo = m + 1; else hi = m; }
-                    if (!(lo < nd && dl[lo] == t->txn)) ++missing;
-                }
-                if (expect == missing) w_clear(x->words, b);
+                if (st == S_STABLE && managed_test(s, c, x, q)) w_clear(x->words, b);
                 continue;
             }
             if (st < S_STABLE || st >= S_INVALID_OR_TRUNCATED) continue;   /* hasBeen(Stable), not truncated */
             if (x->pend[q] == 0) {                                   /* registerUnmanaged */
-                const int r = unmanaged_eval(s, c, x, q, ex, only_deps, 1, &x->until[q]);
-                if (r == 1) { x->pend[q] = 3; w_clear(x->words, b); continue; }
-                x->pend[q] = r == 0 ? 2 : 1;
+                unmanaged_register(s, c, x, q);
+                if (x->pend[q] == 3) continue;
             }
             long min_unc, next;
             cfk_next(c, &min_unc, &next);
             if (next >= 0 && min_unc >= 0 && ts_cmp(&s->tbl[min_unc], &s->exec[next]) < 0) next = -1;
-            if (x->pend[q] == 1 && (min_unc < 0 || (uint32_t)min_unc > x->until[q])) {   /* COMMIT -> updatePending */
-                const int r = unmanaged_eval(s, c, x, q, ex, only_deps, 0, &x->until[q]);
-                if (r == 1) { x->pend[q] = 3; w_clear(x->words, b); continue; }
-                x->pend[q] = 2;
-            }
-            if (x->pend[q] == 2 && (min_unc < 0 || next >= 0)) {      /* notifyUnmanaged(APPLY, next) */
-                if (next < 0 || ts_cmp(&s->exec[x->until[q]], &s->exec[next]) < 0) { x->pend[q] = 3; w_clear(x->words, b); }
-            }
+            unmanaged_commit(s, c, x, q, min_unc);                   /* COMMIT -> updatePending */
+            if (x->pend[q] == 3) continue;
+            if (min_unc < 0 || next >= 0) unmanaged_apply(s, x, q, next);   /* notifyUnmanaged(APPLY, next) */
         }
         int waiting = 0;
         for (uint32_t a = 0; a < (x->nr + x->nk + 63) / 64; ++a) waiting |= x->words[a] != 0;
         if (!waiting && st == S_STABLE) {
+            /* Command.executesAtLeast (local/Command.java:1145-1150) */
+            const ts_t *ea = only_deps && x->has_eal ? &x->eal : ex;
+            if (eal_msb) { eal_msb[nout] = ea->msb; eal_lsb[nout] = ea->lsb; eal_node[nout] = ea->node; }
             ready_out[nout++] = g;
-            free(x->rdeps); free(x->keys); free(x->kdoff); free(x->kdeps); free(x->words); free(x->aoi);
-            free(x->pend); free(x->until);
+            waiter_free(x);
             continue;
         }
         s->wt[keep++] = *x;
     }
     s->nwt = keep;
-    /* ascending positions */
+    if (s->event_mode && wix_rebuild(s)) return -1;
+    /* ascending positions (the executesAtLeast values move with their txns) */
     for (uint32_t a = 1; a < nout; ++a) {
         uint32_t v = ready_out[a], b = a;
-        while (b > 0 && ready_out[b - 1] > v) { ready_out[b] = ready_out[b - 1]; --b; }
+        uint64_t m0 = eal_msb ? eal_msb[a] : 0, l0 = eal_msb ? eal_lsb[a] : 0;
+        int32_t n0 = eal_msb ? eal_node[a] : 0;
+        while (b > 0 && ready_out[b - 1] > v) {
+            ready_out[b] = ready_out[b - 1];
+            if (eal_msb) { eal_msb[b] = eal_msb[b - 1]; eal_lsb[b] = eal_lsb[b - 1]; eal_node[b] = eal_node[b - 1]; }
+            --b;
+        }
         ready_out[b] = v;
+        if (eal_msb) { eal_msb[b] = m0; eal_lsb[b] = l0; eal_node[b] = n0; }
     }
     *nready = nout;
     return 0;
@@ -2649,4 +3063,18 @@ done:
     mmo_free(&kd); mmo_free(&rd);
     free(tbl);
     return rc;
+}
+
+/* test aid: the WaitingOn words, pend and until of the waiting txn at position g (-1: not waiting) */
+int or_lstore_waiter_debug(const or_lstore *s, uint32_t g, uint64_t *words, uint32_t nwords, uint8_t *pend,
+                           uint32_t *until, uint32_t nslots)
+{
+    for (uint32_t w = 0; w < s->nwt; ++w) {
+        const or_waiter *x = &s->wt[w];
+        if (x->g != g) continue;
+        for (uint32_t a = 0; a < nwords && a < (x->nr + x->nk + 63) / 64; ++a) words[a] = x->words[a];
+        for (uint32_t q = 0; q < nslots && q < x->nk; ++q) { pend[q] = x->pend[q]; until[q] = x->until[q]; }
+        return (int)(x->nr << 16 | x->nk);
+    }
+    return -1;
 }

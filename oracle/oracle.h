@@ -116,6 +116,22 @@ int        or_lstore_truncate(or_lstore *s, uint32_t m, const uint32_t *start, c
  * leave the set. */
 int        or_lstore_waiting_add(or_lstore *s, uint32_t base, const or_deps *d, uint32_t n);
 int        or_lstore_ready(or_lstore *s, uint32_t *ready_out, uint32_t *nready);
+/* as or_lstore_ready, plus each ready txn's Command.executesAtLeast (executeAtLeast for awaitsOnlyDeps
+ * kinds when set, else executeAt) */
+int        or_lstore_ready_ex(or_lstore *s, uint32_t *ready_out, uint32_t *nready, uint64_t *eal_msb, uint64_t *eal_lsb,
+                              int32_t *eal_node);
+/* event mode (default off): key bits are cleared only when CommandsForKey.notifyAndUpdatePending
+ * (local/CommandsForKey.java:1163-1215) would evaluate them -- notify over committed[] between next /
+ * nextWrite per the event's status (COMMITTED before nextWrite notifies nobody), notifyUnmanaged COMMIT
+ * on a txn committing, APPLY while minUncommitted is null or next is not; events are the register calls
+ * (one txn at a time, array order), a waiter's own STABLE transition (replayed at waiting_add when it is
+ * Stable already) and truncations (APPLY only).  Range-dep bits follow their deps' statuses as before. */
+void       or_lstore_event_mode(or_lstore *s, int on);
+/* the RedundantBefore map readiness reads (removeRedundantDependencies, local/CommandStore.java:601-678):
+ * m entries (start, end] ascending and disjoint, [sep, eep), locallyAppliedOrInvalidatedBefore and
+ * bootstrappedAt as positions (0xFFFFFFFF = TxnId.NONE), stale = staleUntilAtLeast != null; m = 0 clears */
+int        or_lstore_redundant(or_lstore *s, uint32_t m, const uint32_t *start, const uint32_t *end, const uint64_t *sep,
+                               const uint64_t *eep, const uint32_t *local, const uint32_t *boot, const uint8_t *stale);
 uint32_t   or_lstore_waiting(const or_lstore *s);
 
 /* ---- primitives restated for the reference's own property tests ---- */

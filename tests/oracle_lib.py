@@ -489,7 +489,7 @@ class LStore:
     SaveStatus Erased / Invalidated: off the range scan, INVALID_OR_TRUNCATED for CommandsForKey."""
     TK, HISTORICAL, PREACCEPTED, ACCEPTED, COMMITTED, STABLE, APPLIED, INVALID, ERASED = range(9)
 
-    def __init__(self, nkeys: int):
+    def __init__(self, nkeys: int, event_mode: bool = False):
         L = lib()
         if not getattr(L, "_lstore_typed", False):
             L.or_lstore_create.argtypes = [C.c_uint32]
@@ -503,10 +503,16 @@ class LStore:
             L.or_lstore_truncate.argtypes = [C.c_void_p, C.c_uint32, _u32p, _u32p, _u32p]
             L.or_lstore_waiting_add.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_OrDeps), C.c_uint32]
             L.or_lstore_ready.argtypes = [C.c_void_p, _u32p, _u32p]
+            L.or_lstore_ready_ex.argtypes = [C.c_void_p, _u32p, _u32p, _u64p, _u64p, _i32p]
+            L.or_lstore_redundant.argtypes = [C.c_void_p, C.c_uint32, _u32p, _u32p, _u64p, _u64p, _u32p, _u32p, _u8p]
+            L.or_lstore_event_mode.argtypes = [C.c_void_p, C.c_int]
+            L.or_lstore_event_mode.restype = None
             L.or_lstore_waiting.argtypes = [C.c_void_p]
             L.or_lstore_waiting.restype = C.c_uint32
             L._lstore_typed = True
         self._h = L.or_lstore_create(nkeys)
+        if event_mode:      # key bits cleared only on notifyAndUpdatePending's events (oracle.h)
+            L.or_lstore_event_mode(self._h, 1)
 
     def close(self):
         if self._h:
@@ -541,13 +547,32 @@ class LStore:
     def ready(self):
         """Execution readiness (or_lstore_ready): the waiting txns that became ReadyToExecute,
         ascending positions; they leave the set."""
+        return self.ready_ex()[0]
+
+    def ready_ex(self):
+        """ready(), plus each ready txn's Command.executesAtLeast as (msb, lsb, node) arrays."""
         w = lib().or_lstore_waiting(self._h)
         out = np.zeros(max(1, w), np.uint32)
+        em = np.zeros(max(1, w), np.uint64); el = np.zeros(max(1, w), np.uint64); en = np.zeros(max(1, w), np.int32)
         cnt = np.zeros(1, np.uint32)
-        rc = lib().or_lstore_ready(self._h, out.ctypes.data_as(_u32p), cnt.ctypes.data_as(_u32p))
+        rc = lib().or_lstore_ready_ex(self._h, out.ctypes.data_as(_u32p), cnt.ctypes.data_as(_u32p),
+                                      em.ctypes.data_as(_u64p), el.ctypes.data_as(_u64p), en.ctypes.data_as(_i32p))
         if rc != 0:
             raise OracleError(rc)
-        return out[:int(cnt[0])].copy()
+        c = int(cnt[0])
+        return out[:c].copy(), (em[:c].copy(), el[:c].copy(), en[:c].copy())
+
+    def redundant(self, start, end, start_epoch, end_epoch, locally_applied, bootstrapped_at, stale):
+        """The RedundantBefore map readiness reads (or_lstore_redundant): removeRedundantDependencies."""
+        a = [np.ascontiguousarray(start, np.uint32), np.ascontiguousarray(end, np.uint32),
+             np.ascontiguousarray(start_epoch, np.uint64), np.ascontiguousarray(end_epoch, np.uint64),
+             np.ascontiguousarray(locally_applied, np.uint32), np.ascontiguousarray(bootstrapped_at, np.uint32),
+             np.ascontiguousarray(stale, np.uint8)]
+        rc = lib().or_lstore_redundant(self._h, len(a[0]), a[0].ctypes.data_as(_u32p), a[1].ctypes.data_as(_u32p),
+                                       a[2].ctypes.data_as(_u64p), a[3].ctypes.data_as(_u64p), a[4].ctypes.data_as(_u32p),
+                                       a[5].ctypes.data_as(_u32p), a[6].ctypes.data_as(_u8p))
+        if rc != 0:
+            raise OracleError(rc)
 
     @property
     def waiting(self) -> int:

@@ -16,7 +16,7 @@ feedback, with range txns and EphemeralReads, through the C ABI.
 import numpy as np
 import pytest
 
-from accord_amd import CommandStore, Stream, WINDOW_NONE, generate_stream
+from accord_amd import NO_TXN, CommandStore, Stream, WINDOW_NONE, generate_stream
 import oracle_lib as O
 from status_events import APPLIED, INVALID, STABLE, rb_map
 
@@ -42,12 +42,18 @@ def mk(txns):
 class Driver:
     """One schedule driven into the oracle and (optionally) the device store in lockstep."""
 
-    def __init__(self, s, nkeys, dev=None):
+    def __init__(self, s, nkeys, dev=None, events=False):
         self.s, self.ora, self.dev = s, O.LStore(nkeys), dev
         self.status = np.zeros(s.n, np.uint8)
         self.execs = [None] * s.n
+        # events: an event-driven restatement (or_lstore_event_mode) fed the same schedule in lockstep;
+        # ev_rounds[c] = what it releases at call c
+        self.ev = O.LStore(nkeys, event_mode=True) if events else None
+        self.ev_rounds = []
 
     def batch(self, lo, hi):
+        if self.ev is not None:
+            self.ev.batch(self.s.slice(lo, hi))
         part = self.ora.batch(self.s.slice(lo, hi))
         if self.dev is not None:
             got = self.dev.calculate_deps_batch(self.s.slice(lo, hi))
@@ -71,22 +77,44 @@ class Driver:
             em[r], el[r], en[r] = self.execs[g]
         stv = np.full(idx.size, st, np.uint8)
         self.ora.register(s.msb[idx], s.lsb[idx], s.node[idx], stv, em, el, en)
+        if self.ev is not None:
+            self.ev.register(s.msb[idx], s.lsb[idx], s.node[idx], stv, em, el, en)
         if self.dev is not None:
             self.dev.register(s.msb[idx], s.lsb[idx], s.node[idx], stv, em, el, en)
         self.status[idx] = st
 
     def initialise(self, lo, part):
         self.ora.waiting_add(lo, part)
+        if self.ev is not None:
+            self.ev.waiting_add(lo, part)
         if self.dev is not None:
             self.dev.waiting_on_initialise()
 
     def round(self):
-        want = self.ora.ready()
+        if self.ev is not None:
+            self.ev_rounds.append(self.ev.ready())
+        want, weal = self.ora.ready_ex()
+        self.eal = weal                                   # Command.executesAtLeast of the ready txns
         if self.dev is not None:
-            got, waiting = self.dev.ready_update()
+            got, waiting, geal = self.dev.ready_update_ex()
             assert np.array_equal(got, want), (got[:20], want[:20])
             assert waiting == self.ora.waiting
+            for a, b in zip(geal, weal):
+                assert np.array_equal(a, b), (got, a, b)
         return want
+
+    def redundant(self, start, end, locally_applied, bootstrapped_at, stale=None, start_epoch=None, end_epoch=None):
+        """The store's RedundantBefore with the rest of each entry (removeRedundantDependencies); the
+        shard bound stays NONE (no truncation, no collectDeps union)."""
+        m = len(start)
+        se = [0] * m if start_epoch is None else start_epoch
+        ee = [1 << 62] * m if end_epoch is None else end_epoch
+        st = [0] * m if stale is None else stale
+        self.ora.redundant(start, end, se, ee, locally_applied, bootstrapped_at, st)
+        if self.dev is not None:
+            self.dev.redundant_before(start=start, end=end, start_epoch=se, end_epoch=ee, bound=[NO_TXN] * m,
+                                      min_epoch=0, locally_applied=locally_applied, bootstrapped_at=bootstrapped_at,
+                                      stale=st)
 
     def apply(self, ready):
         self.register(ready, APPLIED)
@@ -149,6 +177,193 @@ def kat_run(dev=None):
 
 def test_kat_oracle():
     kat_run()
+
+
+# ---- the reference's event order (CommandsForKey.notifyAndUpdatePending, :1163-1215) ----
+# The device (and or_lstore_ready) re-test a waiting txn whenever an input of its test changed; the
+# reference tests it only when an event reaches the key.  KAT of the difference: t1 (R) waits for t0
+# (W, uncommitted).  t0 COMMITs at an executeAt after t1: t1's test holds (nothing unapplied executes
+# before it, no dep uncommitted), but a COMMITTED event executing no later than nextWrite (t0 itself)
+# notifies nobody -- the reference releases t1 only at t0's STABLE event, one call later.
+EV_KAT = [(10, "W", 1, [1], None), (11, "R", 1, [1], None)]
+
+
+def test_event_order_kat():
+    s = mk(EV_KAT)
+    d = Driver(s, 4, events=True)
+    part = d.batch(0, 2)
+    d.register([1], STABLE)
+    d.initialise(0, part)
+    assert list(d.round()) == [] and list(d.ev_rounds[-1]) == []
+    t0x = (int(s.msb[0]), 20 << 16 | int(s.lsb[0]) & 0xFFFF, 1)
+    d.register([0], 4, [t0x])                             # COMMITTED at hlc 20
+    assert list(d.round()) == [1]                         # device / polling: at once
+    assert list(d.ev_rounds[-1]) == []                    # reference: not notified
+    d.register([0], STABLE)
+    assert list(d.round()) == [0]
+    assert list(d.ev_rounds[-1]) == [0, 1]                # t0's STABLE event notifies t1
+
+
+def event_schedule(s, nkeys, bsz, seed, late_frac=0.15, delay=0.2, cf=0.0, rounds=3):
+    """The interleaved schedule of the GPU tests (batches; STABLE, some late, some at an executeAt past
+    the TxnId, a share cf COMMITTED one batch before STABLE; ready -> APPLIED rounds), fed ONE event at a
+    time to the polling restatement (or_lstore_ready, what the device computes) and to the event-driven
+    one (or_lstore_event_mode), both asked for ready txns after every event.  Returns, per txn, the
+    index of the event after which each released it (int64 max: never)."""
+    rng = np.random.default_rng(seed)
+    poll, ev = O.LStore(nkeys), O.LStore(nkeys, event_mode=True)
+    never = np.iinfo(np.int64).max
+    at_p, at_e = np.full(s.n, never, np.int64), np.full(s.n, never, np.int64)
+    clock = [0]
+    execs = [None] * s.n
+
+    def step():
+        for o, at in ((poll, at_p), (ev, at_e)):
+            r = o.ready().astype(np.int64)
+            at[r] = np.minimum(at[r], clock[0])
+        clock[0] += 1
+
+    def event(g, st):
+        e = execs[g] or (int(s.msb[g]), int(s.lsb[g]), int(s.node[g]))
+        for o in (poll, ev):
+            o.register(s.msb[g:g + 1], s.lsb[g:g + 1], s.node[g:g + 1], np.array([st], np.uint8),
+                       np.array([e[0]], np.uint64), np.array([e[1]], np.uint64), np.array([e[2]], np.int32))
+        step()
+
+    late, applied = np.zeros(0, np.int64), np.zeros(s.n, bool)
+    for lo in range(0, s.n, bsz):
+        hi = min(s.n, lo + bsz)
+        part = poll.batch(s.slice(lo, hi))
+        ev.batch(s.slice(lo, hi))
+        idx = np.arange(lo, hi)
+        is_late = rng.random(hi - lo) < late_frac
+        now = np.concatenate([late, idx[~is_late]])
+        first = []
+        for g in now:
+            if g >= lo and rng.random() < delay:
+                execs[g] = (int(s.msb[g]), ((int(s.lsb[g]) >> 16) + int(rng.integers(1, 30))) << 16, int(rng.integers(8, 16)))
+            if g >= lo and rng.random() < cf:
+                first.append(g)
+                event(g, 4)                                  # COMMITTED first, STABLE next batch
+            else:
+                event(g, STABLE)
+        late = np.concatenate([idx[is_late], np.array(first, np.int64)]).astype(np.int64)
+        poll.waiting_add(lo, part)
+        ev.waiting_add(lo, part)
+        step()
+        for _ in range(rounds):                              # the polling releases are executed
+            r = np.nonzero((at_p < never) & ~applied)[0]
+            for g in r:
+                applied[g] = True
+                event(g, APPLIED)
+    for g in np.sort(late):
+        event(g, STABLE)
+    for _ in range(5000):
+        r = np.nonzero((at_p < never) & ~applied)[0]
+        if r.size == 0:
+            break
+        for g in r:
+            applied[g] = True
+            event(g, APPLIED)
+    return at_p, at_e
+
+
+@pytest.mark.parametrize("seed,rf,sp,delay,cf", [(31, 0.0, False, 0.2, 0.0), (32, 0.1, False, 0.2, 0.0),
+                                                (33, 0.1, True, 0.0, 0.0), (34, 0.05, False, 0.2, 0.3)])
+def test_event_order_never_later(seed, rf, sp, delay, cf):
+    """Event by event, the polling restatement (the device's semantics: tests/test_ready.py GPU cases
+    check device == polling round by round) releases every txn the event-driven restatement releases
+    no later; it releases some strictly earlier (EV_KAT: a test that holds between events), and a txn
+    no event reaches stays for the reference's progress log.  (Between calls the device sees only the
+    state after all of a call's events; a transient state inside one call -- e.g. next before a
+    non-dep commits earlier -- can release an unmanaged APPLY record in the reference and not at the
+    call's end: the device is event-exact at one event per call, as here.)"""
+    s = stable_stream(900, 40, seed, rf, sync_points=sp)
+    at_p, at_e = event_schedule(s, 40, 150, seed, delay=delay, cf=cf)
+    never = np.iinfo(np.int64).max
+    released = at_e < never
+    assert released.sum() > s.n // 4
+    assert (at_p[released] <= at_e[released]).all(), np.nonzero(at_p > at_e)[0][:10]
+    print("event-driven releases", int(released.sum()), "of", s.n, "; polling earlier for",
+          int((at_p[released] < at_e[released]).sum()), "; never reached by an event:", int((~released).sum()))
+
+
+# removeRedundantDependencies (local/CommandStore.java:601-670) KAT over keys 0..13, every txn Write:
+# t0 (0,4], t3 (4,8], t6 (6,10], t8 (8,12] are range txns that never commit; t1 range (0,2] and t2
+# key 3 wait on t0; t4 key 6 and t5 keys {5, 9} on t3; t7 key 7 on t3, t6; t9 key 9 on t6, t8.
+RR_KAT = [(10, "W", 1, None, [(0, 4)]), (11, "W", 1, None, [(0, 2)]), (12, "W", 1, [3], None),
+          (13, "W", 1, None, [(4, 8)]), (14, "W", 1, [6], None), (15, "W", 1, [5, 9], None),
+          (16, "W", 1, None, [(6, 10)]), (17, "W", 1, [7], None), (18, "W", 1, None, [(8, 12)]),
+          (19, "W", 1, [9], None)]
+
+
+def rr_kat_run(dev=None):
+    s = mk(RR_KAT)
+    d = Driver(s, 14, dev)
+    part = d.batch(0, 10)
+    d.register([1, 2, 4, 5, 7, 9], STABLE)
+    d.initialise(0, part)
+    assert list(d.round()) == []                          # every one waits on an uncommitted range txn
+    # (0,4] locally applied before t1: t0 is redundant for t1, t2 (rule 1: [bootstrapIdx 0, appliedIdx 1));
+    # (4,10] bootstrapped at t7: t3's range (4,8] lies inside it -> fully bootstrapping for t4, t5, t7
+    # (rule 2); t6 (position 6 < 7) too, for t7; t9's deps t6 (6,10] covered, t8 (8,12] not (its
+    # bootstrapIdx is 1: t8 follows t7)
+    d.redundant(start=[0, 4], end=[4, 10], locally_applied=[1, NO_TXN], bootstrapped_at=[NO_TXN, 7])
+    assert list(d.round()) == [1, 2, 4, 5, 7]
+    d.apply([1, 2, 4, 5, 7])                              # t9's key 9 waits for t5 (a Write) to apply
+    # bootstrapped at t9 over (4,10] and (10,12]: t8's range is covered only with (10,12], which t9's
+    # key 9 does not touch -- not in the fold, so (10,12] remains and t9 keeps waiting
+    d.redundant(start=[0, 4, 10], end=[4, 10, 12], locally_applied=[1, NO_TXN, NO_TXN],
+                bootstrapped_at=[NO_TXN, 9, 9])
+    assert list(d.round()) == []
+    d.redundant(start=[0, 4], end=[4, 12], locally_applied=[1, NO_TXN], bootstrapped_at=[NO_TXN, 9])
+    assert list(d.round()) == [9]
+    return d
+
+
+def test_rr_kat_oracle():
+    rr_kat_run()
+
+
+def test_rr_gate_epoch_oracle():
+    """hasLocallyRedundantDependencies folds only in-bounds entries (Entry.outOfBounds): with the
+    entry's epochs after the txns', nothing is removed."""
+    s = mk(RR_KAT)
+    d = Driver(s, 14)
+    part = d.batch(0, 10)
+    d.register([1, 2, 4, 5, 7, 9], STABLE)
+    d.initialise(0, part)
+    d.redundant(start=[0, 4], end=[4, 10], locally_applied=[1, NO_TXN], bootstrapped_at=[NO_TXN, 7],
+                start_epoch=[5, 5], end_epoch=[9, 9])
+    assert list(d.round()) == []
+
+
+# executeAtLeast (WaitingOn.updateExecuteAtLeast, local/Command.java:1511-1514): t1, an
+# ExclusiveSyncPoint over (0,2] (awaitsOnlyDeps), waits on t0 (key 1) committed at an executeAt after
+# t1's TxnId (registerUnmanaged leaves an APPLY record: executesAt = t0's executeAt); t2 a range Write
+# over (0,2] (not awaitsOnlyDeps: executesAtLeast = its own executeAt)
+EAL_KAT = [(10, "W", 1, [1], None), (11, "XSP", 1, None, [(0, 2)]), (12, "W", 1, None, [(0, 2)])]
+
+
+def eal_kat_run(dev=None):
+    s = mk(EAL_KAT)
+    d = Driver(s, 4, dev)
+    part = d.batch(0, 3)
+    t0x = (int(s.msb[0]), 30 << 16 | int(s.lsb[0]) & 0xFFFF, 1)    # t0 executes at hlc 30
+    d.register([0, 1, 2], STABLE, [t0x, None, None])
+    d.initialise(0, part)
+    # t2 (not awaitsOnlyDeps) stops waiting for t0, which executes after it (removeWaitingOn)
+    assert list(d.round()) == [0, 2]
+    assert int(d.eal[1][1]) >> 16 == 12                            # t2: its own executeAt (= TxnId)
+    d.apply([0, 2])
+    assert list(d.round()) == [1]
+    em, el, en = d.eal
+    assert (int(em[0]), int(el[0]), int(en[0])) == t0x             # t1: the dep's executeAt
+    return d
+
+
+def test_eal_kat_oracle():
+    eal_kat_run()
 
 
 def stable_stream(n, ks, seed, range_frac=0.0, sync_points=False):
@@ -234,6 +449,81 @@ def test_schedule_oracle_progress():
 def test_gpu_kat(gpu_device):
     with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
         kat_run(dev)
+
+
+@pytest.mark.gpu
+def test_gpu_rr_kat(gpu_device):
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=14, window=WINDOW_NONE, resident=True) as dev:
+        rr_kat_run(dev)
+
+
+@pytest.mark.gpu
+def test_gpu_eal_kat(gpu_device):
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        eal_kat_run(dev)
+
+
+def schedule_rr(s, nkeys, bsz, seed, dev=None, late_frac=0.1, rounds_per_batch=4, nent=5, remove=True):
+    """Range and key txns, some committing two batches late (late_frac), and after every batch a new
+    RedundantBefore map of nent entries over the keyspace with random locallyAppliedOrInvalidatedBefore
+    (mostly recent) / bootstrappedAt positions (some NONE, some stale): readiness removes redundant
+    range deps (removeRedundantDependencies) == the oracle's literal fold, round by round.
+    remove=False: the same maps with NONE bounds (nothing removable).  Returns the rounds and the driver."""
+    rng = np.random.default_rng(seed)
+    d = Driver(s, nkeys, dev)
+    out, late = [], []
+    for b, lo in enumerate(range(0, s.n, bsz)):
+        hi = min(s.n, lo + bsz)
+        part = d.batch(lo, hi)
+        idx = np.arange(lo, hi)
+        is_late = rng.random(hi - lo) < late_frac
+        d.register(idx[~is_late], STABLE)
+        if b >= 2 and late[b - 2].size:
+            d.register(late[b - 2], STABLE)
+        late.append(idx[is_late])
+        d.initialise(lo, part)
+        cuts = np.sort(rng.choice(np.arange(1, nkeys - 1), size=nent - 1, replace=False))
+        bounds = np.concatenate([[0], cuts, [nkeys - 1]])
+        keep = rng.random(nent) < 0.8                       # a few gaps in the map
+        st, en = bounds[:-1][keep], bounds[1:][keep]
+        m = len(st)
+        loc = np.where(rng.random(m) < 0.7, rng.integers(max(0, hi - 2 * bsz), hi + 1, m), NO_TXN).astype(np.uint32)
+        boot = np.where(rng.random(m) < 0.4, rng.integers(0, hi + 1, m), NO_TXN).astype(np.uint32)
+        # Entry.merge clears a locallyAppliedOrInvalidatedBefore at or below bootstrappedAt
+        loc = np.where((boot != NO_TXN) & (loc != NO_TXN) & (boot >= loc), NO_TXN, loc).astype(np.uint32)
+        stale = (rng.random(m) < 0.1).astype(np.uint8)
+        if not remove:
+            loc[:] = NO_TXN; boot[:] = NO_TXN; stale[:] = 0
+        d.redundant(start=st, end=en, locally_applied=loc, bootstrapped_at=boot, stale=stale)
+        for _ in range(rounds_per_batch):
+            r = d.round()
+            out.append(r)
+            d.apply(r)
+    for x in late[-2:]:
+        d.register(x, STABLE)
+    out.extend(drain(d))
+    return out, d
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_schedule_rr_oracle(seed):
+    """The maps release range-dep waiters earlier than the same schedule without removable bounds."""
+    s = stable_stream(900, 30, seed, 0.25, sync_points=True)
+    out, d = schedule_rr(s, 30, 150, seed)
+    got = np.concatenate(out)
+    assert np.unique(got).size == got.size
+    out0, _ = schedule_rr(s, 30, 150, seed, remove=False)
+    nb = (900 // 150) * 4                                  # rounds before the final drain
+    assert sum(len(r) for r in out[:nb]) > sum(len(r) for r in out0[:nb])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ks,bsz,seed,rf", [(2000, 40, 250, 23, 0.25), (3000, 100, 500, 24, 0.15)])
+def test_gpu_schedule_rr_equals_oracle(gpu_device, n, ks, bsz, seed, rf):
+    """removeRedundantDependencies + executeAtLeast under random maps: device == literal oracle fold."""
+    s = stable_stream(n, ks, seed, rf, sync_points=True)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=ks, window=WINDOW_NONE, resident=True) as dev:
+        out, d = schedule_rr(s, ks, bsz, seed, dev)
 
 
 @pytest.mark.gpu
