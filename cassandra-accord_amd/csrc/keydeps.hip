@@ -98,23 +98,41 @@ __global__ __launch_bounds__(256) void validate_pack_kernel(
         }
         const uint32_t pbase = __shfl(ko, 0, 64);
         const uint32_t pend = key_off[t0 + cnt];
-        for (uint32_t p0 = pbase; p0 < pend; p0 += 64) {
-            const uint32_t p = p0 + lane;
-            uint32_t j = 0;                          // largest lane j < cnt with ko_j <= p
+        // the pairs in rounds of VP x 64: every key of a round is loaded before any is used (one
+        // memory round trip per round), its predecessor comes from the lane below
+        constexpr int VP = 8;
+        uint32_t carry = pbase > 0 ? key_ord[pbase - 1] : 0u;   // the key before the round's first pair
+        for (uint32_t r0 = pbase; r0 < pend; r0 += VP * 64) {
+            uint32_t kv[VP];
 #pragma unroll
-            for (uint32_t step = 32; step >= 1; step >>= 1) {
-                const uint32_t c = j + step;
-                const uint32_t kc = __shfl(ko, (int)(c & 63), 64);
-                if (c < cnt && kc <= p) j = c;
+            for (int v = 0; v < VP; ++v) {
+                const uint32_t p = r0 + v * 64 + lane;
+                kv[v] = p < pend ? key_ord[p] : 0u;
             }
-            const uint32_t e = __shfl(ent, (int)j, 64);
-            const uint32_t kj = __shfl(ko, (int)j, 64);
-            if (p < pend) {
-                const uint32_t key = key_ord[p];
-                const bool in_range = key >= key_lo && key < key_hi;
-                if (!in_range || (p > kj && key_ord[p - 1] >= key)) record_error(st, t0 + j, ACCORD_ERR_KEYS);
-                pair_key[p] = in_range ? key - key_lo : 0u;      // keep the pipeline in bounds on error
-                pair_ent[p] = e;
+#pragma unroll
+            for (int v = 0; v < VP; ++v) {
+                const uint32_t p0 = r0 + v * 64;
+                if (p0 >= pend) break;                   // wave-uniform
+                const uint32_t p = p0 + lane;
+                uint32_t j = 0;                          // largest lane j < cnt with ko_j <= p
+#pragma unroll
+                for (uint32_t step = 32; step >= 1; step >>= 1) {
+                    const uint32_t c = j + step;
+                    const uint32_t kc = __shfl(ko, (int)(c & 63), 64);
+                    if (c < cnt && kc <= p) j = c;
+                }
+                const uint32_t e = __shfl(ent, (int)j, 64);
+                const uint32_t kj = __shfl(ko, (int)j, 64);
+                const uint32_t key = kv[v];
+                uint32_t prev = __shfl_up(key, 1, 64);
+                if (lane == 0) prev = carry;
+                carry = __shfl(key, 63, 64);
+                if (p < pend) {
+                    const bool in_range = key >= key_lo && key < key_hi;
+                    if (!in_range || (p > kj && prev >= key)) record_error(st, t0 + j, ACCORD_ERR_KEYS);
+                    pair_key[p] = in_range ? key - key_lo : 0u;      // keep the pipeline in bounds on error
+                    pair_ent[p] = e;
+                }
             }
         }
     }
@@ -524,11 +542,58 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
 // Per key txn: KeyDeps sizes from the per-pair witnessed counts.  keys = pairs with >= 1
 // witnessed entry, keysToTxnIds = keys + body; txnIds <= body (an upper bound: the fill pass
 // writes the exact count and the values are compacted afterwards).
+// A wave per 64 consecutive txns: their pairs are one contiguous run, read coalesced (a lane per
+// pair, its wcnt word), and summed per txn in LDS.
 __global__ __launch_bounds__(256) void keydeps_sizes_kernel(uint32_t n, const uint32_t *__restrict__ key_off,
                                                             const PairSlice *__restrict__ slice,
                                                             uint32_t *__restrict__ cnt_keys,
                                                             uint32_t *__restrict__ cnt_vub,
                                                             uint32_t *__restrict__ cnt_k2v, DevStatus *status)
+{
+    __shared__ uint32_t s_kc[4][64], s_body[4][64];
+    const uint32_t lane = lane_id(), w = wave_id();
+    const uint32_t gw = blockIdx.x * 4u + w, nwv = gridDim.x * 4u;
+    for (uint32_t t0 = gw * 64u; t0 < n; t0 += nwv * 64u) {
+        const uint32_t cnt = min(64u, n - t0);
+        const uint32_t ko = key_off[t0 + min(lane, cnt)];        // lanes >= cnt: the end
+        s_kc[w][lane] = 0u;
+        s_body[w][lane] = 0u;
+        const uint32_t pbase = readlane(ko, 0), pend = key_off[t0 + cnt];   // (no lane holds it at cnt = 64)
+        wave_lds_sync();
+        for (uint32_t p0 = pbase; p0 < pend; p0 += 64u) {
+            const uint32_t p = p0 + lane;
+            uint32_t j = 0;                          // largest lane j < cnt with ko_j <= p
+#pragma unroll
+            for (uint32_t step = 32; step >= 1; step >>= 1) {
+                const uint32_t c = j + step;
+                const uint32_t kc = __shfl(ko, (int)(c & 63), 64);
+                if (c < cnt && kc <= p) j = c;
+            }
+            if (p < pend) {
+                const uint32_t c = slice[p].wcnt;
+                if (c) {
+                    atomicAdd(&s_kc[w][j], 1u);
+                    atomicAdd(&s_body[w][j], c);
+                }
+            }
+        }
+        wave_lds_sync();
+        if (lane < cnt) {
+            const uint32_t kc = s_kc[w][lane], body = s_body[w][lane];
+            cnt_keys[t0 + lane] = kc;
+            cnt_vub[t0 + lane] = body;
+            cnt_k2v[t0 + lane] = kc + body;
+        }
+        wave_lds_sync();
+    }
+}
+
+// (the thread-per-txn form, kept for reference of the per-txn definition)
+__global__ __launch_bounds__(256) void keydeps_sizes_txn_kernel(uint32_t n, const uint32_t *__restrict__ key_off,
+                                                                const PairSlice *__restrict__ slice,
+                                                                uint32_t *__restrict__ cnt_keys,
+                                                                uint32_t *__restrict__ cnt_vub,
+                                                                uint32_t *__restrict__ cnt_k2v, DevStatus *status)
 {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t k0 = key_off[i], k1 = key_off[i + 1];
@@ -1453,7 +1518,9 @@ void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_
     if (rb > 4096) rb = 4096;
     hipLaunchKernelGGL(txnrec_kernel, dim3(rb), dim3(256), 0, s, p, (TxnRec *)recs);
     uint32_t blocks = (p.n + KD_WAVES - 1) / KD_WAVES;
-    if (blocks > 256u * 16u) blocks = 256u * 16u;
+    uint32_t cap = 256u * 16u;
+    if (const char *e = getenv("ACCORD_FK_BLOCKS")) cap = (uint32_t)atoi(e);   // dev aid (A/B of the grid)
+    if (blocks > cap) blocks = cap;
     blocks = (blocks + 7u) & ~7u;                       // a multiple of 8: one block class per XCD
     (void)wpl;
     // near span: 1024 txns below the bound for windows up to 384 (config 2: 94 % of the distinct
@@ -1488,6 +1555,7 @@ void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
 // large txnIds lists (measured against one output per lane with 4 searches in flight: config 2
 // compact 209 -> 201 us, config 3 488 -> 468 us).
 constexpr uint32_t CV_OUT = 4096, CV_WIN = 256;
+struct __attribute__((aligned(4))) CvU4 { uint32_t x, y, z, w; };
 // bstart[b] = the last txn t with val_off[t] <= b * CV_OUT (thread per txn; the blocks whose first
 // output lies in [val_off[t], val_off[t+1]) are t's)
 __global__ __launch_bounds__(256) void cv_bstart_kernel(uint32_t n, const uint32_t *__restrict__ val_off,
@@ -1529,13 +1597,20 @@ __global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uin
                 if (h - l > 1) { if (s_off[m] <= xs) l = m; else h = m; }
             }
             uint32_t v[4];
+            if (x0 >= o && x0 + 4u <= oe && s_off[l + 1] >= x0 + 4u) {
+                // the quad inside one txn's run (most quads): its 4 gapped values are contiguous too --
+                // one 16-byte load (4-byte aligned; gfx950 takes unaligned dwordx4)
+                const CvU4 q = *(const CvU4 *)(vgap + s_src[l] + (x0 - s_off[l]));
+                v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t x = x0 + j;
-                v[j] = 0u;
-                if (x >= o && x < oe) {
-                    while (s_off[l + 1] <= x) ++l;    // s_off[CV_WIN] >= oe ends it
-                    v[j] = vgap[s_src[l] + (x - s_off[l])];
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t x = x0 + j;
+                    v[j] = 0u;
+                    if (x >= o && x < oe) {
+                        while (s_off[l + 1] <= x) ++l;    // s_off[CV_WIN] >= oe ends it
+                        v[j] = vgap[s_src[l] + (x - s_off[l])];
+                    }
                 }
             }
             if (x0 >= o && x0 + 4u <= oe) {
@@ -1652,8 +1727,8 @@ void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, 
                           const uint32_t *txn_index, const StreamPos &sp, DevStatus *status, hipStream_t s)
 {
     if (n == 0) return;
-    uint32_t blocks = (n + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
+    uint32_t blocks = (n + 255) / 256;               // a wave per 64 txns
+    if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(validate_pack_kernel, dim3(blocks), dim3(256), 0, s, n, msb, lsb, node, key_off, key_ord,
                        rng_off, rng_start, rng_end, key_lo, key_hi, pair_key, pair_ent, rng_owner, is_range,
                        txn_index, sp, status);
@@ -1753,10 +1828,14 @@ void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *
                           uint32_t *cnt_vub, uint32_t *cnt_k2v, DevStatus *status, hipStream_t s)
 {
     if (n == 0) return;
-    uint32_t blocks = (n + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(keydeps_sizes_kernel, dim3(blocks), dim3(256), 0, s, n, key_off, slice, cnt_keys, cnt_vub,
-                       cnt_k2v, status);
+    uint32_t blocks = (n + 255) / 256;               // a wave per 64 txns
+    if (blocks > 16384) blocks = 16384;
+    if (getenv("ACCORD_SIZES_TXN"))                  // dev aid (A/B): thread per txn
+        hipLaunchKernelGGL(keydeps_sizes_txn_kernel, dim3(std::min(blocks, 4096u)), dim3(256), 0, s, n, key_off, slice,
+                           cnt_keys, cnt_vub, cnt_k2v, status);
+    else
+        hipLaunchKernelGGL(keydeps_sizes_kernel, dim3(blocks), dim3(256), 0, s, n, key_off, slice, cnt_keys, cnt_vub,
+                           cnt_k2v, status);
 }
 
 size_t keydeps_fast_temp_bytes(uint32_t n) { return fk_temp_bytes(n); }

@@ -872,6 +872,30 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         HIPCHECK(s, hipStreamSynchronize(st));
         std::sort(dropped.begin(), dropped.end());
     }
+    if (const char *tr = getenv("ACCORD_READY_TRACE")) {     // dev aid: "g,d1,d2,...": g's executeAtLeast record
+        std::vector<uint32_t> ids;
+        for (const char *c = tr; *c;) { ids.push_back((uint32_t)strtoul(c, (char **)&c, 10)); if (*c == ',') ++c; else break; }
+        for (accord_impl::ReadyGen *r : s->rdy_gens)
+            if (!ids.empty() && ids[0] >= r->glo && ids[0] <= r->ghi) {
+                EalRec e{};
+                uint8_t dn = 0;
+                HIPCHECK(s, hipMemcpy(&e, r->eal.as<EalRec>() + (ids[0] - r->glo), sizeof(e), hipMemcpyDeviceToHost));
+                HIPCHECK(s, hipMemcpy(&dn, r->done.as<uint8_t>() + (ids[0] - r->glo), 1, hipMemcpyDeviceToHost));
+                fprintf(stderr, "trace call %u txn %u done %u eal has %u (%llu, %llu, %d)\n", call, ids[0], dn, e.has,
+                        (unsigned long long)e.msb, (unsigned long long)e.lsb, e.node);
+            }
+        for (size_t i = 1; i < ids.size(); ++i) {
+            uint64_t m = 0, l = 0; int32_t nd = 0; uint8_t stt = 0;
+            const uint32_t d = ids[i];
+            if (d >= s->rg_known) continue;
+            HIPCHECK(s, hipMemcpy(&m, s->rg_emsb.as<uint64_t>() + d, 8, hipMemcpyDeviceToHost));
+            HIPCHECK(s, hipMemcpy(&l, s->rg_elsb.as<uint64_t>() + d, 8, hipMemcpyDeviceToHost));
+            HIPCHECK(s, hipMemcpy(&nd, s->rg_enode.as<int32_t>() + d, 4, hipMemcpyDeviceToHost));
+            HIPCHECK(s, hipMemcpy(&stt, s->rg_status.as<uint8_t>() + d, 1, hipMemcpyDeviceToHost));
+            fprintf(stderr, "  dep %u status %u exec (%llu, %llu, %d)\n", d, stt, (unsigned long long)m,
+                    (unsigned long long)l, nd);
+        }
+    }
     s->rdy_force_full = false;                 // the device and the bookkeeping below agree again
     // generations drain in stream order: count each one's released (or dropped) txns, free the empty ones
     auto settle = [&](const std::vector<uint32_t> &l) {
