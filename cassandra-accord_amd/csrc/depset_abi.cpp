@@ -4,6 +4,7 @@
 #include "store_impl.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -150,6 +151,33 @@ int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool r
     HIPCHECK(s, hipGetLastError());
     if (range) { o.tot_rngs = UK; o.tot_rvals = UV; o.tot_r = UK + UB; }
     else { o.tot_keys = UK; o.tot_vals = UV; o.tot_x = UK + UB; }
+    return ACCORD_OK;
+}
+
+// linearUnion with an empty side is the other side verbatim (both are in canonical form): its
+// arrays copied into o in one launch instead of the union's passes and host reads
+int32_t copy_side(accord_store *s, const accord_deps &src, bool range, DepSet &o)
+{
+    const size_t n1 = (size_t)src.n + 1;
+    const uint64_t K = range ? src.rd_rngs_total : src.kd_keys_total, V = range ? src.rd_vals_total : src.kd_vals_total;
+    const uint64_t X = range ? src.rd_r2v_total : src.kd_k2v_total;
+    DevBuf &key_off = range ? o.rng_off : o.key_off, &val_off = range ? o.rval_off : o.val_off, &x_off = range ? o.r_off : o.x_off;
+    DevBuf &lo = range ? o.rng_start : o.keys, &vals = range ? o.rvals : o.vals, &x = range ? o.r : o.x;
+    HIPCHECK(s, key_off.ensure(n1 * 4)); HIPCHECK(s, val_off.ensure(n1 * 4)); HIPCHECK(s, x_off.ensure(n1 * 4));
+    HIPCHECK(s, lo.ensure(K * 4 + 4)); HIPCHECK(s, vals.ensure(V * 4 + 4)); HIPCHECK(s, x.ensure(X * 4 + 4));
+    if (range) HIPCHECK(s, o.rng_end.ensure(K * 4 + 4));
+    accord::CopyList cl;
+    cl.add(range ? src.rd_rng_off : src.kd_key_off, key_off.p, n1 * 4);
+    cl.add(range ? src.rd_val_off : src.kd_val_off, val_off.p, n1 * 4);
+    cl.add(range ? src.rd_r2v_off : src.kd_k2v_off, x_off.p, n1 * 4);
+    cl.add(range ? src.rd_rng_start : src.kd_keys, lo.p, K * 4);
+    cl.add(range ? src.rd_vals : src.kd_vals, vals.p, V * 4);
+    cl.add(range ? (const void *)src.rd_r2v : (const void *)src.kd_k2v, x.p, X * 4);
+    if (range) cl.add(src.rd_rng_end, o.rng_end.p, K * 4);
+    accord::launch_copy_words(cl, s->stream);
+    HIPCHECK(s, hipGetLastError());
+    if (range) { o.tot_rngs = K; o.tot_rvals = V; o.tot_r = X; }
+    else { o.tot_keys = K; o.tot_vals = V; o.tot_x = X; }
     return ACCORD_OK;
 }
 
@@ -304,8 +332,15 @@ int32_t redundant_apply(accord_store *s)
     parts[1].rd_vals = r.rvals.as<uint32_t>(); parts[1].rd_r2v_off = r.r_off.as<uint32_t>();
     parts[1].rd_r2v = r.r.as<int32_t>();
     DepSet &o = next_set(s);
-    RC(union_side(s, parts, 2, false, o));
-    RC(union_side(s, parts, 2, true, o));
+    // the redundant deps are RangeDeps only: the KeyDeps side is the computed one verbatim, and a
+    // RangeDeps side with an empty part is the other part (ACCORD_RB_UNION=1: always the union)
+    const char *ru = getenv("ACCORD_RB_UNION");
+    const bool always = ru && ru[0] == '1';
+    if (always) RC(union_side(s, parts, 2, false, o));
+    else RC(copy_side(s, parts[0], false, o));
+    if (!always && parts[0].rd_rngs_total == 0) RC(copy_side(s, parts[1], true, o));
+    else if (!always && tot[0] == 0) RC(copy_side(s, parts[0], true, o));
+    else RC(union_side(s, parts, 2, true, o));
     HIPCHECK(s, hipStreamSynchronize(st));
     publish(s, o, n);
     s->ds_rb = true;

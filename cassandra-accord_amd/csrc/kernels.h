@@ -24,6 +24,15 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
                       uint32_t *keys_tmp, uint32_t *vals_tmp, const uint32_t *ents_in, uint32_t *ents_out,
                       uint32_t *ents_tmp, uint32_t n, int bits, void *temp, void *scan_state, hipStream_t s);
 
+// A resident store's batch (P pairs: keys bkey, entries bent, TxnId order) joined to its carried
+// key-major history (C entries) without re-sorting the carry: the same sort_key / sort_pair / hist
+// as radix_sort_pairs over [carry | batch].  comp_tmp: P words.  merge_join_fits: P and the key
+// bits qualify (one workgroup sorts the batch in LDS).
+bool merge_join_fits(uint32_t P, int bits);
+void merge_join_batch(const uint32_t *ckey, const uint32_t *cent, uint32_t C, const uint32_t *bkey,
+                      const uint32_t *bent, uint32_t P, uint32_t *comp_tmp, uint32_t *sort_key, uint32_t *sort_pair,
+                      uint32_t *hist, hipStream_t s);
+
 // ---- small fills in one launch (scan.hip): descriptor k sets words [0, d[k].words) of d[k].p ----
 struct FillDesc {
     uint32_t *p;
@@ -38,6 +47,21 @@ struct FillList {
     }
 };
 void launch_fill_words(const FillList &L, hipStream_t s);
+// small device-to-device copies in one launch: descriptor k copies d[k].words words
+struct CopyDesc {
+    const uint32_t *src;
+    uint32_t *dst;
+    uint32_t words;
+};
+struct CopyList {
+    CopyDesc d[8];
+    uint32_t nd = 0;
+    void add(const void *src, void *dst, size_t bytes)
+    {
+        if (bytes >= 4) d[nd++] = CopyDesc{(const uint32_t *)src, (uint32_t *)dst, (uint32_t)(bytes / 4)};
+    }
+};
+void launch_copy_words(const CopyList &L, hipStream_t s);
 
 // ---- scan (scan.hip) ----
 // temp: a scan-state buffer of at least scan_temp_bytes(n) bytes, ZERO when allocated

@@ -197,6 +197,20 @@ struct EalRec {
     uint32_t has;
 };
 
+// a = take ? b : a, every field blended with one all-ones / zero word the compiler cannot see
+// through (status.hip wo_init_kernel: a running merge there combined one candidate's msb / lsb
+// with another's node on gfx950, whatever the merge's form; it now keeps the winner's position)
+__device__ __forceinline__ void eal_blend(EalRec &a, const EalRec &b, bool take)
+{
+    uint32_t mk = take ? 0xFFFFFFFFu : 0u;
+    asm volatile("" : "+v"(mk));
+    const uint64_t mk64 = ((uint64_t)mk << 32) | mk;
+    a.msb = (b.msb & mk64) | (a.msb & ~mk64);
+    a.lsb = (b.lsb & mk64) | (a.lsb & ~mk64);
+    a.node = (int32_t)(((uint32_t)b.node & mk) | ((uint32_t)a.node & ~mk));
+    a.has = (b.has & mk) | (a.has & ~mk);
+}
+
 // wave maximum of the lanes' candidates (has = false: none); the result is uniform
 __device__ inline EalRec eal_wave_max(bool has, const Ts &t)
 {
@@ -206,15 +220,14 @@ __device__ inline EalRec eal_wave_max(bool has, const Ts &t)
         EalRec u;
         u.msb = __shfl_xor(r.msb, o, 64); u.lsb = __shfl_xor(r.lsb, o, 64);
         u.node = __shfl_xor(r.node, o, 64); u.has = __shfl_xor(r.has, o, 64);
-        const bool take = u.has && (!r.has || ts_cmp(r.msb, r.lsb, r.node, u.msb, u.lsb, u.node) < 0);
-        if (take) r = u;
+        eal_blend(r, u, u.has && (!r.has || ts_cmp(r.msb, r.lsb, r.node, u.msb, u.lsb, u.node) < 0));
     }
     return r;
 }
 
 __device__ __forceinline__ void eal_merge(EalRec &a, const EalRec &b)      // Timestamp.nonNullOrMax
 {
-    if (b.has && (!a.has || ts_cmp(a.msb, a.lsb, a.node, b.msb, b.lsb, b.node) < 0)) a = b;
+    eal_blend(a, b, b.has && (!a.has || ts_cmp(a.msb, a.lsb, a.node, b.msb, b.lsb, b.node) < 0));
 }
 
 } // namespace accord_status

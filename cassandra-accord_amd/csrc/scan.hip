@@ -247,7 +247,22 @@ __global__ __launch_bounds__(256) void fill_words_kernel(FillList L)
     const FillDesc d = L.d[blockIdx.y];
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.words; i += gridDim.x * blockDim.x) d.p[i] = d.value;
 }
+__global__ __launch_bounds__(256) void copy_words_kernel(CopyList L)
+{
+    const CopyDesc d = L.d[blockIdx.y];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.words; i += gridDim.x * blockDim.x) d.dst[i] = d.src[i];
+}
 } // namespace
+
+void launch_copy_words(const CopyList &L, hipStream_t s)
+{
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k < L.nd; ++k) mx = L.d[k].words > mx ? L.d[k].words : mx;
+    if (L.nd == 0 || mx == 0) return;
+    uint32_t bx = (mx + 255) / 256;
+    if (bx > 2048) bx = 2048;
+    hipLaunchKernelGGL(copy_words_kernel, dim3(bx, L.nd), dim3(256), 0, s, L);
+}
 
 void launch_fill_words(const FillList &L, hipStream_t s)
 {

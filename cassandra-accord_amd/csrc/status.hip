@@ -23,6 +23,8 @@
 #include "redundant_wait.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -673,7 +675,8 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
         const uint32_t r0 = rd_val_off[t], R = rd_val_off[t + 1] - r0;
         const uint32_t bits = R + (kd_key_off[t + 1] - kd_key_off[t]);
         const uint32_t w0 = wo_off[t], nw = wo_off[t + 1] - w0;
-        EalRec ea{0, 0, 0, 0u};
+        uint32_t best = 0xFFFFFFFFu;                       // the dep executing last among the candidates
+        Ts bex{0, 0, 0};
         for (uint32_t q = 0; q < nw; ++q) {
             unsigned long long wv = 0, av = 0;
             const unsigned long long kept = pre ? words[w0 + q] : ~0ull;   // removeRedundantDependencies
@@ -686,7 +689,11 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
                 bool wait = true, applied = false;
                 if (only_deps && st >= ST_COMMITTED && st <= ST_APPLIED) {   // updateExecuteAtLeast
                     const Ts de = exec_of(v, d);
-                    if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0) eal_merge(ea, EalRec{de.msb, de.lsb, de.node, 1u});
+                    if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0 &&
+                        (best == 0xFFFFFFFFu || tcmp(bex, de) < 0)) {
+                        best = d;
+                        bex = de;
+                    }
                 }
                 if (st >= ST_COMMITTED) {                       // hasBeen(PreCommitted)
                     if (st >= ST_INVALID) { wait = false; applied = true; }                 // truncated / invalidated
@@ -698,6 +705,14 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
             }
             words[w0 + q] = wv;
             aoi[w0 + q] = av;
+        }
+        // the record from the winner's executeAt, loaded once more: merging each candidate's fields
+        // into a running record here (eal_merge, in any form) was seen to combine the winner's msb /
+        // lsb with an earlier candidate's node on gfx950 (test_ready.py::test_gpu_schedule_equals_oracle)
+        EalRec ea{0, 0, 0, 0u};
+        if (best != 0xFFFFFFFFu) {
+            const Ts be = exec_of(v, best);
+            ea = EalRec{be.msb, be.lsb, be.node, 1u};
         }
         eal[t] = ea;
     }
@@ -804,8 +819,8 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     HIPCHECK(s, s->rg_goff.ensure(((size_t)P + 1) * 4));
     HIPCHECK(s, hipMemsetAsync(s->rg_flag.p, 0, (size_t)nkeys * 4, st));
     const StatusView v = view_of(s);
-    hipLaunchKernelGGL(flag_keys_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->pair_key.as<uint32_t>(),
-                       s->pair_ent.as<uint32_t>(), v, s->rg_flag.as<uint32_t>());
+    hipLaunchKernelGGL(flag_keys_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->cy_key.as<uint32_t>(),
+                       s->cy_ent.as<uint32_t>(), v, s->rg_flag.as<uint32_t>());
     s->rg_flag_ok = true;
     GenParams g{};
     g.n = n; g.key_lo = s->cfg.key_lo;

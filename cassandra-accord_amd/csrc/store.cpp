@@ -379,7 +379,12 @@ int32_t accord_deps_compute(accord_store *s)
         }
         accord::launch_fill_words(fl, st);
     }
-    if (C) {
+    // ACCORD_MERGE_JOIN=1: a resident store's batch of a few thousand pairs joins the key-major carry
+    // by a merge (accord::merge_join_batch) instead of a re-sort of [carry | batch]; off until its
+    // one-workgroup batch sort beats the radix passes (measured 126 us vs ~40 us, profiles/r04_b)
+    const char *mj = getenv("ACCORD_MERGE_JOIN");
+    const bool merge = C && accord::merge_join_fits(P, bits_for(nkeys - 1)) && mj && mj[0] == '1';
+    if (C && !merge) {
         HIPCHECK(s, hipMemcpyAsync(s->pair_key.p, s->cy_key.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
         HIPCHECK(s, hipMemcpyAsync(s->pair_ent.p, s->cy_ent.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
     }
@@ -412,10 +417,15 @@ int32_t accord_deps_compute(accord_store *s)
         bound_l = s->bound_l.as<uint32_t>(); bound_g = s->bound_g.as<uint32_t>(); pair_bound = s->pair_bound.as<uint32_t>();
     }
     record(s, EV_VALIDATE);
-    accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
-                             s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
-                             s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), PH,
-                             bits_for(nkeys - 1), s->radix_tmp.p, s->scan_tmp.p, st);
+    if (merge)
+        accord::merge_join_batch(s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), C, s->pair_key.as<uint32_t>() + C,
+                                 s->pair_ent.as<uint32_t>() + C, P, s->tmp_key.as<uint32_t>(), s->sort_key.as<uint32_t>(),
+                                 s->sort_pair.as<uint32_t>(), s->hist.as<uint32_t>(), st);
+    else
+        accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
+                                 s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
+                                 s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), PH,
+                                 bits_for(nkeys - 1), s->radix_tmp.p, s->scan_tmp.p, st);
     record(s, EV_SORT);
     accord::launch_history(PH, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
