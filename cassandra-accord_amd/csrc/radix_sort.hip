@@ -12,6 +12,8 @@
 #include "device_common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace accord {
 
 namespace {
@@ -281,12 +283,18 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
     const size_t a = ((hist_cap * 4 + (hist_cap + 1) * 4) + 15) & ~(size_t)15;
     unsigned long long *total = (unsigned long long *)((char *)temp + a);
     if (bits < 1) bits = 1;
-    const int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
+    int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
+    // dev aids (A/B): ACCORD_RS_PASSES=k more passes of fewer bits; ACCORD_RS_LOWFIRST=1 the
+    // narrower digits first
+    if (const char *e = getenv("ACCORD_RS_PASSES")) { const int k = atoi(e); if (k > passes && k <= bits) passes = k; }
+    const char *lf = getenv("ACCORD_RS_LOWFIRST");
+    const bool low_first = lf && lf[0] == '1';
     // ping-pong so that the last pass lands in *_out; vals_in == nullptr means identity values
     const uint32_t *ki = keys_in, *vi = vals_in, *ei = ents_in;
     int shift = 0;
     for (int p = 0; p < passes; ++p) {
-        const int pb = (bits - shift + (passes - p) - 1) / (passes - p);   // split bits evenly
+        const int pb = low_first ? (bits - shift) / (passes - p)                  // split bits evenly
+                                 : (bits - shift + (passes - p) - 1) / (passes - p);
         const uint32_t mask = (1u << pb) - 1;
         const bool to_out = ((passes - 1 - p) % 2) == 0;
         uint32_t *ko = to_out ? keys_out : keys_tmp;

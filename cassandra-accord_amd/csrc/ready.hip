@@ -625,6 +625,8 @@ int32_t ready_gen_fill(accord_store *s, ReadyGen *r)
     HIPCHECK(s, copy(r->wo, s->wo_words.p, s->wo_words_total * 8));
     HIPCHECK(s, copy(r->aoi, s->wo_aoi.p, s->wo_words_total * 8));
     HIPCHECK(s, copy(r->eal, s->wo_eal.p, (size_t)n * sizeof(EalRec)));
+    if (const char *f = getenv("ACCORD_INJECT_FAIL"); f && std::strcmp(f, "ready_gen") == 0)   // test hook
+        return fail(s, ACCORD_ERR_OOM, "injected failure (ACCORD_INJECT_FAIL=ready_gen) with the generation half built");
     // the participants (the batch's keys / ranges) and RangeDeps ranges: removeRedundantDependencies
     HIPCHECK(s, copy(r->pkoff, s->key_off.p, n1 * 4));
     HIPCHECK(s, copy(r->pkeys, s->key_ord.p, (size_t)s->P * 4));

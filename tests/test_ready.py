@@ -546,6 +546,31 @@ def test_gpu_initialise_twice(gpu_device):
         assert list(d.round()) == [1]
 
 
+@pytest.mark.gpu
+def test_gpu_initialise_failure_leaves_set(gpu_device, monkeypatch):
+    """A generation that fails half built (ACCORD_INJECT_FAIL=ready_gen: after its buffers are
+    allocated and partly copied) never joins the waiting set: the waiting count and the next calls
+    are those of the set without it, and initialising the batch again afterwards works."""
+    from accord_amd import AccordError
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        s = mk(KAT)
+        d = Driver(s, 4, dev)
+        part = d.batch(0, 4)
+        d.register([0, 1, 2, 3], STABLE)
+        d.initialise(0, part)
+        part2 = d.batch(4, 8)
+        d.register([4, 6, 7], STABLE)
+        monkeypatch.setenv("ACCORD_INJECT_FAIL", "ready_gen")
+        with pytest.raises(AccordError):
+            dev.waiting_on_initialise()
+        monkeypatch.delenv("ACCORD_INJECT_FAIL")
+        assert list(d.round()) == [0]                     # == the oracle, which has only batch 1 waiting
+        d.apply([0])
+        d.initialise(4, part2)                            # the retry joins batch 2
+        released = [0] + [int(x) for r in drain(d) for x in r]   # every round == the oracle
+        assert sorted(released) == [0, 1, 2, 3, 4]        # t5 stays PREACCEPTED: t6 / t7 wait on it
+
+
 def test_sync_points_oracle_progress():
     """SyncPoints / ExclusiveSyncPoints (awaitsOnlyDeps, witness everything) at executeAt = TxnId
     drain too.  (With executeAts past the TxnId a range XSP's unmanaged APPLY record can wait for a
