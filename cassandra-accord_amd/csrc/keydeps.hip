@@ -435,7 +435,10 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
 // number at most W + 1 and the bound lies in [p - W, p]: the predicate "same key and txn >= i - W"
 // is monotone over that range of the key-major history, and the search needs neither the segment
 // start nor a global fallback.
-template <uint32_t HALO>
+// COMB: one 64-bit LDS word per position, key << 32 | txn -- inside [p - W, p] every position of an
+// earlier key compares below (k << 32 | i - W) and of key k exactly when its txn does, so a probe
+// is one ds_read_b64 and one compare instead of two reads (the entry's kind bits come from hist[]).
+template <uint32_t HALO, bool COMB>
 __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     uint32_t P, uint32_t window, uint32_t steps, const uint32_t *__restrict__ sorted_key,
     const uint32_t *__restrict__ sorted_pair, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ seg_start,
@@ -443,8 +446,9 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     const ClassCarry *__restrict__ ccarry, const uint32_t *__restrict__ seg_end, const uint32_t *__restrict__ pair_bound,
     PairSlice *__restrict__ slice, uint32_t ncarry)
 {
-    __shared__ uint32_t tx[HALO + H2_TILE];
-    __shared__ uint32_t tk[HALO + H2_TILE];
+    __shared__ uint32_t tx[COMB ? 1 : HALO + H2_TILE];
+    __shared__ uint32_t tk[COMB ? 1 : HALO + H2_TILE];
+    __shared__ unsigned long long tkx[COMB ? HALO + H2_TILE : 1];
     const uint32_t base = blockIdx.x * H2_TILE;
     const uint32_t lds_lo = base > HALO ? base - HALO : 0u;
     const uint32_t end = min(P, base + H2_TILE);
@@ -458,16 +462,26 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     }
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) a[j] = seg_start[key[j]];   // issued early, used late
-    for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) {
-        tx[x - lds_lo] = hist[x];
-        tk[x - lds_lo] = sorted_key[x];
+    uint32_t ent[H2_ITEMS], lo[H2_ITEMS], len[H2_ITEMS], thr[H2_ITEMS];
+    if (COMB) {
+#pragma unroll
+        for (uint32_t j = 0; j < H2_ITEMS; ++j) {
+            const uint32_t p = base + j * H2_THREADS + threadIdx.x;
+            ent[j] = p < end ? hist[p] : 0u;
+        }
+        for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS)
+            tkx[x - lds_lo] = ((unsigned long long)sorted_key[x] << 32) | (hist[x] & ENT_TXN_MASK);
+    } else {
+        for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) {
+            tx[x - lds_lo] = hist[x];
+            tk[x - lds_lo] = sorted_key[x];
+        }
     }
     __syncthreads();
-    uint32_t ent[H2_ITEMS], lo[H2_ITEMS], len[H2_ITEMS], thr[H2_ITEMS];
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
-        ent[j] = p < end ? tx[p - lds_lo] : 0u;
+        if (!COMB) ent[j] = p < end ? tx[p - lds_lo] : 0u;
         const uint32_t i = ent[j] & ENT_TXN_MASK;
         thr[j] = i > window ? i - window : 0u;
         const uint32_t lb = p > window ? max(p - window, lds_lo) : lds_lo;
@@ -480,7 +494,10 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
         for (uint32_t j = 0; j < H2_ITEMS; ++j) {
             const uint32_t half = len[j] >> 1;
             const uint32_t m = lo[j] + half;
-            probe[j] = len[j] ? (tk[m - lds_lo] == key[j] && (tx[m - lds_lo] & ENT_TXN_MASK) >= thr[j] ? 1u : 0u) : 1u;
+            if (COMB)
+                probe[j] = len[j] ? (tkx[m - lds_lo] >= (((unsigned long long)key[j] << 32) | thr[j]) ? 1u : 0u) : 1u;
+            else
+                probe[j] = len[j] ? (tk[m - lds_lo] == key[j] && (tx[m - lds_lo] & ENT_TXN_MASK) >= thr[j] ? 1u : 0u) : 1u;
         }
 #pragma unroll
         for (uint32_t j = 0; j < H2_ITEMS; ++j) {
@@ -588,34 +605,6 @@ __global__ __launch_bounds__(256) void keydeps_sizes_kernel(uint32_t n, const ui
     }
 }
 
-// (the thread-per-txn form, kept for reference of the per-txn definition)
-__global__ __launch_bounds__(256) void keydeps_sizes_txn_kernel(uint32_t n, const uint32_t *__restrict__ key_off,
-                                                                const PairSlice *__restrict__ slice,
-                                                                uint32_t *__restrict__ cnt_keys,
-                                                                uint32_t *__restrict__ cnt_vub,
-                                                                uint32_t *__restrict__ cnt_k2v, DevStatus *status)
-{
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t k0 = key_off[i], k1 = key_off[i + 1];
-        uint32_t kc = 0, body = 0;
-        if (k1 - k0 <= 8) {                   // all loads issued before any is consumed
-            uint32_t c[8];
-#pragma unroll
-            for (uint32_t j = 0; j < 8; ++j) c[j] = k0 + j < k1 ? slice[k0 + j].wcnt : 0u;
-#pragma unroll
-            for (uint32_t j = 0; j < 8; ++j) { kc += c[j] ? 1u : 0u; body += c[j]; }
-        } else {
-            for (uint32_t q = k0; q < k1; ++q) {
-                const uint32_t c = slice[q].wcnt;
-                kc += c ? 1u : 0u;
-                body += c;
-            }
-        }
-        cnt_keys[i] = kc;
-        cnt_vub[i] = body;
-        cnt_k2v[i] = kc + body;
-    }
-}
 
 template <int WPL>
 struct WaveLds {
@@ -1559,11 +1548,11 @@ struct __attribute__((aligned(4))) CvU4 { uint32_t x, y, z, w; };
 // bstart[b] = the last txn t with val_off[t] <= b * CV_OUT (thread per txn; the blocks whose first
 // output lies in [val_off[t], val_off[t+1]) are t's)
 __global__ __launch_bounds__(256) void cv_bstart_kernel(uint32_t n, const uint32_t *__restrict__ val_off,
-                                                        uint32_t *__restrict__ bstart)
+                                                        uint32_t *__restrict__ bstart, uint32_t cvo)
 {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t a = val_off[t], e = val_off[t + 1];
-        for (uint32_t b = (a + CV_OUT - 1) / CV_OUT; b * CV_OUT < e; ++b) bstart[b] = t;
+        for (uint32_t b = (a + cvo - 1) / cvo; b * cvo < e; ++b) bstart[b] = t;
     }
 }
 
@@ -1571,13 +1560,13 @@ __global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uin
                                                            const uint32_t *__restrict__ val_off,
                                                            const uint32_t *__restrict__ vgap,
                                                            const uint32_t *__restrict__ bstart,
-                                                           uint32_t *__restrict__ vals)
+                                                           uint32_t *__restrict__ vals, uint32_t cvo)
 {
     __shared__ uint32_t s_off[CV_WIN + 1], s_src[CV_WIN];
     const uint32_t total = val_off[n];
-    const uint32_t o0 = blockIdx.x * CV_OUT;
+    const uint32_t o0 = blockIdx.x * cvo;
     if (o0 >= total) return;                          // block-uniform
-    const uint32_t o1 = min(total, o0 + CV_OUT);
+    const uint32_t o1 = min(total, o0 + cvo);
     uint32_t t0 = bstart[blockIdx.x], o = o0;         // last txn with val_off <= o0
     while (o < o1) {                                  // block-uniform
         const uint32_t tw = t0 + threadIdx.x;
@@ -1812,8 +1801,12 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
         uint32_t steps = 0;
         while ((1u << steps) <= window) ++steps;     // ceil(log2(window + 1)) halvings of a <= window range
         // the halo only has to reach back W positions: the smallest that does keeps the block's LDS small
-        auto h2 = window <= 256 ? history2_lockstep_kernel<256> : window <= 512 ? history2_lockstep_kernel<512>
-                : window <= 1024 ? history2_lockstep_kernel<1024> : history2_lockstep_kernel<H2_HALO>;
+        const char *cb = getenv("ACCORD_H2_COMB");      // dev aid (A/B): 0 = the two-array probe
+        auto h2 = (cb && cb[0] == '0')
+                      ? (window <= 256 ? history2_lockstep_kernel<256, false> : window <= 512 ? history2_lockstep_kernel<512, false>
+                         : window <= 1024 ? history2_lockstep_kernel<1024, false> : history2_lockstep_kernel<H2_HALO, false>)
+                      : (window <= 256 ? history2_lockstep_kernel<256, true> : window <= 512 ? history2_lockstep_kernel<512, true>
+                         : window <= 1024 ? history2_lockstep_kernel<1024, true> : history2_lockstep_kernel<H2_HALO, true>);
         hipLaunchKernelGGL(h2, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P,
                            window, steps, sorted_key, sorted_pair, hist, seg_start, pw_local, tile_max, c_local, ccarry,
                            seg_end, pair_bound, slice, carry);
@@ -1830,12 +1823,9 @@ void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *
     if (n == 0) return;
     uint32_t blocks = (n + 255) / 256;               // a wave per 64 txns
     if (blocks > 16384) blocks = 16384;
-    if (getenv("ACCORD_SIZES_TXN"))                  // dev aid (A/B): thread per txn
-        hipLaunchKernelGGL(keydeps_sizes_txn_kernel, dim3(std::min(blocks, 4096u)), dim3(256), 0, s, n, key_off, slice,
-                           cnt_keys, cnt_vub, cnt_k2v, status);
-    else
-        hipLaunchKernelGGL(keydeps_sizes_kernel, dim3(blocks), dim3(256), 0, s, n, key_off, slice, cnt_keys, cnt_vub,
-                           cnt_k2v, status);
+    // (a thread per txn measured 0.046 ms against 0.036 for config 2, profiles/r04_b)
+    hipLaunchKernelGGL(keydeps_sizes_kernel, dim3(blocks), dim3(256), 0, s, n, key_off, slice, cnt_keys, cnt_vub,
+                       cnt_k2v, status);
 }
 
 size_t keydeps_fast_temp_bytes(uint32_t n) { return fk_temp_bytes(n); }
@@ -1869,19 +1859,24 @@ void launch_keydeps_fill(const KeyDepsParams &p, int wpl, void *recs, hipStream_
     launch_keydeps_big(p, s);
 }
 
-size_t compact_temp_bytes(uint64_t max_total) { return ((max_total + CV_OUT - 1) / CV_OUT + 1) * 4 + 64; }
+size_t compact_temp_bytes(uint64_t max_total) { return ((max_total + 1023) / 1024 + 1) * 4 + 64; }
 
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
                          uint32_t *vals, uint64_t max_total, void *temp, hipStream_t s)
 {
     if (n == 0 || max_total == 0) return;
-    const uint64_t blocks = (max_total + CV_OUT - 1) / CV_OUT;   // blocks past the exact total exit
+    uint32_t cvo = CV_OUT;                              // ACCORD_CV_OUT: outputs per block (A/B), k * 1024
+    if (const char *e = getenv("ACCORD_CV_OUT")) {
+        const uint32_t v = (uint32_t)strtoul(e, nullptr, 10);
+        if (v >= 1024 && v <= 65536 && v % 1024 == 0) cvo = v;
+    }
+    const uint64_t blocks = (max_total + cvo - 1) / cvo;   // blocks past the exact total exit
     uint32_t *bstart = (uint32_t *)temp;
     uint32_t sb = (n + 255) / 256;
     if (sb > 4096) sb = 4096;
-    hipLaunchKernelGGL(cv_bstart_kernel, dim3(sb), dim3(256), 0, s, n, val_off, bstart);
+    hipLaunchKernelGGL(cv_bstart_kernel, dim3(sb), dim3(256), 0, s, n, val_off, bstart, cvo);
     hipLaunchKernelGGL(compact_vals_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, n, vub_off, val_off, vgap, bstart,
-                       vals);
+                       vals, cvo);
 }
 
 } // namespace accord
