@@ -435,10 +435,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_kernel(uint32_t P, uint32
 // number at most W + 1 and the bound lies in [p - W, p]: the predicate "same key and txn >= i - W"
 // is monotone over that range of the key-major history, and the search needs neither the segment
 // start nor a global fallback.
-// COMB: one 64-bit LDS word per position, key << 32 | txn -- inside [p - W, p] every position of an
-// earlier key compares below (k << 32 | i - W) and of key k exactly when its txn does, so a probe
-// is one ds_read_b64 and one compare instead of two reads (the entry's kind bits come from hist[]).
-template <uint32_t HALO, bool COMB>
+template <uint32_t HALO>
 __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     uint32_t P, uint32_t window, uint32_t steps, const uint32_t *__restrict__ sorted_key,
     const uint32_t *__restrict__ sorted_pair, const uint32_t *__restrict__ hist, const uint32_t *__restrict__ seg_start,
@@ -446,9 +443,8 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     const ClassCarry *__restrict__ ccarry, const uint32_t *__restrict__ seg_end, const uint32_t *__restrict__ pair_bound,
     PairSlice *__restrict__ slice, uint32_t ncarry)
 {
-    __shared__ uint32_t tx[COMB ? 1 : HALO + H2_TILE];
-    __shared__ uint32_t tk[COMB ? 1 : HALO + H2_TILE];
-    __shared__ unsigned long long tkx[COMB ? HALO + H2_TILE : 1];
+    __shared__ uint32_t tx[HALO + H2_TILE];
+    __shared__ uint32_t tk[HALO + H2_TILE];
     const uint32_t base = blockIdx.x * H2_TILE;
     const uint32_t lds_lo = base > HALO ? base - HALO : 0u;
     const uint32_t end = min(P, base + H2_TILE);
@@ -462,26 +458,16 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
     }
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) a[j] = seg_start[key[j]];   // issued early, used late
-    uint32_t ent[H2_ITEMS], lo[H2_ITEMS], len[H2_ITEMS], thr[H2_ITEMS];
-    if (COMB) {
-#pragma unroll
-        for (uint32_t j = 0; j < H2_ITEMS; ++j) {
-            const uint32_t p = base + j * H2_THREADS + threadIdx.x;
-            ent[j] = p < end ? hist[p] : 0u;
-        }
-        for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS)
-            tkx[x - lds_lo] = ((unsigned long long)sorted_key[x] << 32) | (hist[x] & ENT_TXN_MASK);
-    } else {
-        for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) {
-            tx[x - lds_lo] = hist[x];
-            tk[x - lds_lo] = sorted_key[x];
-        }
+    for (uint32_t x = lds_lo + threadIdx.x; x < end; x += H2_THREADS) {
+        tx[x - lds_lo] = hist[x];
+        tk[x - lds_lo] = sorted_key[x];
     }
     __syncthreads();
+    uint32_t ent[H2_ITEMS], lo[H2_ITEMS], len[H2_ITEMS], thr[H2_ITEMS];
 #pragma unroll
     for (uint32_t j = 0; j < H2_ITEMS; ++j) {
         const uint32_t p = base + j * H2_THREADS + threadIdx.x;
-        if (!COMB) ent[j] = p < end ? tx[p - lds_lo] : 0u;
+        ent[j] = p < end ? tx[p - lds_lo] : 0u;
         const uint32_t i = ent[j] & ENT_TXN_MASK;
         thr[j] = i > window ? i - window : 0u;
         const uint32_t lb = p > window ? max(p - window, lds_lo) : lds_lo;
@@ -494,10 +480,7 @@ __global__ __launch_bounds__(H2_THREADS) void history2_lockstep_kernel(
         for (uint32_t j = 0; j < H2_ITEMS; ++j) {
             const uint32_t half = len[j] >> 1;
             const uint32_t m = lo[j] + half;
-            if (COMB)
-                probe[j] = len[j] ? (tkx[m - lds_lo] >= (((unsigned long long)key[j] << 32) | thr[j]) ? 1u : 0u) : 1u;
-            else
-                probe[j] = len[j] ? (tk[m - lds_lo] == key[j] && (tx[m - lds_lo] & ENT_TXN_MASK) >= thr[j] ? 1u : 0u) : 1u;
+            probe[j] = len[j] ? (tk[m - lds_lo] == key[j] && (tx[m - lds_lo] & ENT_TXN_MASK) >= thr[j] ? 1u : 0u) : 1u;
         }
 #pragma unroll
         for (uint32_t j = 0; j < H2_ITEMS; ++j) {
@@ -1543,7 +1526,7 @@ void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
 // 16-byte coalesced stores, mostly coalesced loads, and no idle lanes whatever the mix of small and
 // large txnIds lists (measured against one output per lane with 4 searches in flight: config 2
 // compact 209 -> 201 us, config 3 488 -> 468 us).
-constexpr uint32_t CV_OUT = 4096, CV_WIN = 256;
+constexpr uint32_t CV_OUT = 8192, CV_WIN = 256;   // 8192: 0.194 ms vs 0.196 at 4096, 0.204 at 2048 (r04_b)
 struct __attribute__((aligned(4))) CvU4 { uint32_t x, y, z, w; };
 // bstart[b] = the last txn t with val_off[t] <= b * CV_OUT (thread per txn; the blocks whose first
 // output lies in [val_off[t], val_off[t+1]) are t's)
@@ -1801,12 +1784,11 @@ void launch_history(uint32_t P, uint32_t nkeys, uint32_t window, const uint32_t 
         uint32_t steps = 0;
         while ((1u << steps) <= window) ++steps;     // ceil(log2(window + 1)) halvings of a <= window range
         // the halo only has to reach back W positions: the smallest that does keeps the block's LDS small
-        const char *cb = getenv("ACCORD_H2_COMB");      // dev aid (A/B): 0 = the two-array probe
-        auto h2 = (cb && cb[0] == '0')
-                      ? (window <= 256 ? history2_lockstep_kernel<256, false> : window <= 512 ? history2_lockstep_kernel<512, false>
-                         : window <= 1024 ? history2_lockstep_kernel<1024, false> : history2_lockstep_kernel<H2_HALO, false>)
-                      : (window <= 256 ? history2_lockstep_kernel<256, true> : window <= 512 ? history2_lockstep_kernel<512, true>
-                         : window <= 1024 ? history2_lockstep_kernel<1024, true> : history2_lockstep_kernel<H2_HALO, true>);
+        // (one 64-bit LDS word per position, key << 32 | txn, and one compare per probe measured the
+        // same: segment 0.254 vs 0.250 ms, profiles/r04_b/segment_compact_ab.txt -- the probes are
+        // not what bounds it)
+        auto h2 = window <= 256 ? history2_lockstep_kernel<256> : window <= 512 ? history2_lockstep_kernel<512>
+                : window <= 1024 ? history2_lockstep_kernel<1024> : history2_lockstep_kernel<H2_HALO>;
         hipLaunchKernelGGL(h2, dim3((P + H2_TILE - 1) / H2_TILE), dim3(H2_THREADS), 0, s, P,
                            window, steps, sorted_key, sorted_pair, hist, seg_start, pw_local, tile_max, c_local, ccarry,
                            seg_end, pair_bound, slice, carry);

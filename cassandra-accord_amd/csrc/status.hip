@@ -162,7 +162,8 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q, uint32_
             if (!rej) {   // contiguous: the fill reads the history range itself
                 p.slice[q] = accord::PairSlice{c ? first : hi, hi, c, sl.key};
                 p.gcnt[q] = 0;
-            } else {
+            } else {      // the count now (the sizes pass reads it), the range until the emit pass
+                p.slice[q] = accord::PairSlice{lo, hi, c, sl.key};
                 p.gcnt[q] = c;
             }
         }
@@ -806,12 +807,33 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
 
 
 // After the segment stage of a registered-status store: pairs on keys with registered entries get
-// their emitted entries materialised; returns the history array the fill must read.
-int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill)
+// their emitted entries materialised in two steps, so the compute needs no host read of its own:
+//   status_general_count -- key flags, the committed-Write index, the per-pair counts and their
+//     scan (the total lands in the store's totals[9], read back with the output sizes);
+//   status_general_emit  -- once the total is known: the extended history (the batch history +
+//     the emitted entries) the fill must read.
+// Only the fill passes read the extension; the count passes read positions < PH, equal in both.
+static GenParams general_params(accord_store *s)
+{
+    GenParams g{};
+    g.n = s->n; g.key_lo = s->cfg.key_lo;
+    g.msb = s->msb.as<uint64_t>(); g.lsb = s->lsb.as<uint64_t>(); g.node = s->node.as<int32_t>();
+    if (s->has_exec) { g.xmsb = s->exec_msb.as<uint64_t>(); g.xlsb = s->exec_lsb.as<uint64_t>(); g.xnode = s->exec_node.as<int32_t>(); }
+    g.key_off = s->key_off.as<uint32_t>(); g.key_ord = s->key_ord.as<uint32_t>();
+    g.txn_index = s->txn_index.as<uint32_t>(); g.flag = s->rg_flag.as<uint32_t>(); g.hist = s->hist.as<uint32_t>();
+    g.slice = s->slice.as<accord::PairSlice>();
+    g.gcnt = s->rg_gcnt.as<uint32_t>(); g.goff = s->rg_goff.as<uint32_t>();
+    g.v = view_of(s);
+    g.cw_off = s->rg_cwoff.as<uint32_t>(); g.cw_pos = s->rg_cwpos.as<uint32_t>(); g.cw_pm = s->rg_cwpm.as<uint32_t>();
+    g.hx = s->rg_hx.as<uint32_t>(); g.hu = s->rg_hu.as<uint32_t>(); g.skey = s->sort_key.as<uint32_t>();
+    return g;
+}
+
+int32_t status_general_count(accord_store *s, uint32_t C, uint32_t PH, bool *pending)
 {
     const uint32_t n = s->n, P = s->P, nkeys = s->cfg.key_hi - s->cfg.key_lo;
     hipStream_t st = s->stream;
-    *hist_for_fill = s->hist.as<uint32_t>();
+    *pending = false;
     s->rg_flag_ok = false;
     if (C == 0 || s->next_global == 0) return ACCORD_OK;       // nothing registered can be on a key yet
     HIPCHECK(s, s->rg_flag.ensure((size_t)nkeys * 4 + 4));
@@ -822,15 +844,6 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
     hipLaunchKernelGGL(flag_keys_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->cy_key.as<uint32_t>(),
                        s->cy_ent.as<uint32_t>(), v, s->rg_flag.as<uint32_t>());
     s->rg_flag_ok = true;
-    GenParams g{};
-    g.n = n; g.key_lo = s->cfg.key_lo;
-    g.msb = s->msb.as<uint64_t>(); g.lsb = s->lsb.as<uint64_t>(); g.node = s->node.as<int32_t>();
-    if (s->has_exec) { g.xmsb = s->exec_msb.as<uint64_t>(); g.xlsb = s->exec_lsb.as<uint64_t>(); g.xnode = s->exec_node.as<int32_t>(); }
-    g.key_off = s->key_off.as<uint32_t>(); g.key_ord = s->key_ord.as<uint32_t>();
-    g.txn_index = s->txn_index.as<uint32_t>(); g.flag = s->rg_flag.as<uint32_t>(); g.hist = s->hist.as<uint32_t>();
-    g.slice = s->slice.as<accord::PairSlice>();
-    g.gcnt = s->rg_gcnt.as<uint32_t>(); g.goff = s->rg_goff.as<uint32_t>();
-    g.v = v;
     {   // the committed[] index of the Writes over the combined history
         HIPCHECK(s, s->rg_cwflag.ensure(((size_t)PH + 1) * 4));
         HIPCHECK(s, s->rg_cwoff.ensure(((size_t)PH + 1) * 4));
@@ -849,7 +862,6 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
         hipLaunchKernelGGL(cw_carry_kernel, dim3(cwb), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->sort_key.as<uint32_t>(), v, s->rg_cwchunk.as<uint4>(),
                            s->rg_cwpm.as<uint32_t>());
-        g.cw_off = off; g.cw_pos = s->rg_cwpos.as<uint32_t>(); g.cw_pm = s->rg_cwpm.as<uint32_t>();
         HIPCHECK(s, s->rg_hx.ensure((size_t)PH * 4 + 4));
         HIPCHECK(s, s->rg_hu.ensure((size_t)PH * 4 + 4));
         hipLaunchKernelGGL(hx_local_kernel, dim3(cwb), dim3(256), 0, st, PH, s->hist.as<uint32_t>(),
@@ -858,21 +870,29 @@ int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uin
         hipLaunchKernelGGL(hx_carry_kernel, dim3(cwb), dim3(256), 0, st, PH, s->hist.as<uint32_t>(),
                            s->sort_key.as<uint32_t>(), v, s->rg_cwchunk.as<uint4>(), s->rg_hx.as<uint32_t>(),
                            s->rg_hu.as<uint32_t>());
-        g.hx = s->rg_hx.as<uint32_t>(); g.hu = s->rg_hu.as<uint32_t>(); g.skey = s->sort_key.as<uint32_t>();
     }
+    const GenParams g = general_params(s);
     const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);     // a wave per txn
     if (n) hipLaunchKernelGGL(general_kernel<false>, dim3(gw), dim3(256), 0, st, g);
     HostTotals *dev = s->status_totals.as<HostTotals>();
     accord::exclusive_scan_u32(g.gcnt, s->rg_goff.as<uint32_t>(), P, &dev->totals[9], s->scan_tmp.p, st);
-    unsigned long long X = 0;
-    HIPCHECK(s, hipMemcpyAsync(&X, &dev->totals[9], 8, hipMemcpyDeviceToHost, st));
-    HIPCHECK(s, hipStreamSynchronize(st));
+    *pending = true;
+    return ACCORD_OK;
+}
+
+int32_t status_general_emit(accord_store *s, uint32_t PH, uint64_t X, const uint32_t **hist_for_fill)
+{
+    const uint32_t n = s->n;
+    hipStream_t st = s->stream;
+    *hist_for_fill = s->hist.as<uint32_t>();
     if (X == 0) return ACCORD_OK;
-    if ((uint64_t)PH + X >= (1ull << 31)) return fail(s, ACCORD_ERR_CAPACITY, "general deps of %llu entries", X);
+    if ((uint64_t)PH + X >= (1ull << 31)) return fail(s, ACCORD_ERR_CAPACITY, "general deps of %llu entries", (unsigned long long)X);
     HIPCHECK(s, s->rg_hist2.ensure(((size_t)PH + X) * 4));
     HIPCHECK(s, hipMemcpyAsync(s->rg_hist2.p, s->hist.p, (size_t)PH * 4, hipMemcpyDeviceToDevice, st));
+    GenParams g = general_params(s);
     g.hist2 = s->rg_hist2.as<uint32_t>();
     g.ext_base = PH;
+    const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);
     if (n) hipLaunchKernelGGL(general_kernel<true>, dim3(gw), dim3(256), 0, st, g);
     *hist_for_fill = s->rg_hist2.as<uint32_t>();
     return ACCORD_OK;

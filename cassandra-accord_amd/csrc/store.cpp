@@ -440,11 +440,10 @@ int32_t accord_deps_compute(accord_store *s)
     kp.txn_index = s->has_txn_index ? s->txn_index.as<uint32_t>() : nullptr;
     kp.key_lo = s->cfg.key_lo; kp.key_hi = s->cfg.key_hi; kp.window = s->cfg.window;
     kp.hist = s->hist.as<uint32_t>();
-    if (accord_impl::registered_mode(s)) {   // pairs on keys with registered statuses: general filter
-        const uint32_t *h = nullptr;
-        int32_t rc = accord_impl::status_general_pairs(s, C, PH, &h);
+    bool general = false;                    // pairs on keys with registered statuses: general filter
+    if (accord_impl::registered_mode(s)) {   // (its emitted entries are sized with the outputs below)
+        int32_t rc = accord_impl::status_general_count(s, C, PH, &general);
         if (rc) return rc;
-        kp.hist = h;
     }
     kp.slice = s->slice.as<accord::PairSlice>();
     kp.cnt_vub = s->cnt_vub.as<uint32_t>();
@@ -556,6 +555,13 @@ int32_t accord_deps_compute(accord_store *s)
         s->tot_rngs = h.totals[3]; s->tot_rvals = h.totals[4]; s->tot_r2v = h.totals[5];
     }
     const uint64_t vub_total = s->pinned->totals[1];
+    if (general) {                                      // the fill reads the extended history
+        const uint32_t *h = nullptr;
+        int32_t rc = accord_impl::status_general_emit(s, PH, s->pinned->totals[9], &h);
+        if (rc) return rc;
+        kp.hist = h;
+        rp.hist = h;
+    }
     HIPCHECK(s, s->kd_keys.ensure(s->tot_keys * 4));
     HIPCHECK(s, s->vgap.ensure(vub_total * 4));
     HIPCHECK(s, s->kd_vals.ensure(vub_total * 4));

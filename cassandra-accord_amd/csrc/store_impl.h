@@ -203,7 +203,8 @@ void shard_comm_destroy(accord_store *s);
 int32_t merge_finalize(accord_store *s);   // read a bounded merge's totals (shard.cpp)
 // registered statuses (status.hip)
 bool registered_mode(const accord_store *s);
-int32_t status_general_pairs(accord_store *s, uint32_t C, uint32_t PH, const uint32_t **hist_for_fill);
+int32_t status_general_count(accord_store *s, uint32_t C, uint32_t PH, bool *pending);
+int32_t status_general_emit(accord_store *s, uint32_t PH, uint64_t X, const uint32_t **hist_for_fill);
 int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
 int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
                               const uint32_t *bound);
