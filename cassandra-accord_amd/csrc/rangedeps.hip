@@ -420,29 +420,6 @@ __global__ __launch_bounds__(256) void rk_checkpoint_kernel(uint32_t P, const ui
     }
 }
 
-// The same table, a thread per (block, key) cell, consecutive threads on consecutive keys of one
-// block row: every row store coalesces (the position-parallel form above writes each cell with
-// its own 8-byte store, a row stride apart).  x = the first position of the key's segment with
-// txn >= the block's first txn, by bisection; cells of empty segments are left alone (never read).
-__global__ __launch_bounds__(256) void rk_checkpoint_cells_kernel(RangeDepsParams p)
-{
-    const uint64_t cells = (uint64_t)p.ncp * p.nkeys;
-    for (uint64_t cell = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; cell < cells;
-         cell += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t b = (uint32_t)(cell / p.nkeys), k = (uint32_t)(cell - (uint64_t)b * p.nkeys);
-        const uint32_t a = p.seg_start[k], c = p.seg_end[k];
-        if (a >= c) continue;
-        const uint32_t T = (p.cp_base + b) << RK_CP_SHIFT;
-        uint32_t lo = a, hi = c;
-        while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if ((p.hist[m] & ENT_TXN_MASK) < T) lo = m + 1; else hi = m;
-        }
-        const uint32_t yo = lo < c ? min((p.hist[lo] & ENT_TXN_MASK) - T, RK_CP_YMAX) : RK_CP_YMAX;
-        p.cp[cell] = rk_cp_make(lo, yo, rk_pw_before(p, lo));
-    }
-}
-
 // first position q in [from, to) with txn(q) >= t, given txn(from - 1) < t: gallop then bisect
 __device__ __forceinline__ uint32_t rk_first_ge(const uint32_t *__restrict__ hist, uint32_t from, uint32_t to,
                                                 uint32_t t)
@@ -1028,16 +1005,11 @@ size_t rangekeys_cp_bytes(uint32_t ncp, uint32_t nkeys)
 void launch_rangekeys_checkpoints(uint32_t PH, const uint32_t *sorted_key, const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n_range_txns == 0 || PH == 0) return;
-    const char *e = getenv("ACCORD_RK_CP_CELLS");        // dev aid (A/B): 0 = the position-parallel form
-    if (e && e[0] == '0') {
-        uint32_t blocks = (PH + 255) / 256;
-        if (blocks > 8192) blocks = 8192;
-        hipLaunchKernelGGL(rk_checkpoint_kernel, dim3(blocks), dim3(256), 0, s, PH, sorted_key, p);
-        return;
-    }
-    const uint64_t cells = (uint64_t)p.ncp * p.nkeys;
-    const uint64_t blocks = std::min<uint64_t>((cells + 255) / 256, 65536u);
-    hipLaunchKernelGGL(rk_checkpoint_cells_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, p);
+    // (a thread per (block, key) cell with coalesced row stores and a bisection per cell measured
+    // slower: config-3 count 2.88 vs 2.40 ms, profiles/r04_b/rangekeys_ab.txt)
+    uint32_t blocks = (PH + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(rk_checkpoint_kernel, dim3(blocks), dim3(256), 0, s, PH, sorted_key, p);
 }
 
 namespace {

@@ -1003,7 +1003,7 @@ int32_t status_join_batch(accord_store *s)
                        s->rg_tmsb.as<uint64_t>(), s->rg_tlsb.as<uint64_t>(), s->rg_tnode.as<int32_t>(),
                        s->rg_tg.as<uint32_t>(), s->rg_status.as<uint8_t>(), s->rg_emsb.as<uint64_t>(),
                        s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>(), s->rg_chg.as<uint32_t>(), s->rg_epoch);
-    HIPCHECK(s, hipStreamSynchronize(st));
+    HIPCHECK(s, hipGetLastError());          // stream-ordered before anything that reads the tables
     s->rg_tx_n = (uint32_t)(tx + n);
     s->rg_known = (uint32_t)G;
     return ACCORD_OK;
@@ -1076,7 +1076,8 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     if (s->rc_n)
         hipLaunchKernelGGL(reg_erase_ranges_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, s->rc_n,
                            s->rc_owner.as<uint32_t>(), s->rc_kind.as<uint32_t>());
-    HIPCHECK(s, hipStreamSynchronize(st));
+    // no wait: the host inputs were consumed before the check's read-back, and every later use of
+    // the tables is ordered after these kernels on the store's stream
     HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;
 }
