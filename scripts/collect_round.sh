@@ -1,4 +1,4 @@
-# Copy a gpu_round.sh result (gpurun_out/$TAG) into profiles/$TAG: bench lines, kernel-trace stats,
+# Copy a gpu_round_a.sh + gpu_round_b.sh result (gpurun_out/$TAG) into profiles/$TAG: bench lines, kernel-trace stats,
 # PMC table (all passes), the pytest log, and refresh profiles/traffic_config2.json.
 set -e
 TAG=${1:?tag}; O=gpurun_out/$TAG; P=profiles/$TAG
