@@ -488,9 +488,12 @@ def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
                 st.reset()
                 st.redundant_before()
                 acc = {"device_ms": 0.0, "fill_ms": 0.0, "count_ms": 0.0, "sort_ms": 0.0, "segment_ms": 0.0,
-                       "compact_ms": 0.0, "compute_wall_ms": 0.0, "register_wall_ms": 0.0, "rb_wall_ms": 0.0}
+                       "compact_ms": 0.0, "compute_wall_ms": 0.0, "register_wall_ms": 0.0, "rb_wall_ms": 0.0,
+                       "upload_wall_ms": 0.0}
                 for b, p in enumerate(parts):
+                    tu = time.perf_counter()
                     st.upload(p)
+                    acc["upload_wall_ms"] += (time.perf_counter() - tu) * 1e3
                     t0 = time.perf_counter()
                     st.compute()
                     t1 = time.perf_counter()

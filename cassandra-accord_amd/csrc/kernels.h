@@ -54,7 +54,7 @@ struct CopyDesc {
     uint32_t words;
 };
 struct CopyList {
-    CopyDesc d[8];
+    CopyDesc d[12];
     uint32_t nd = 0;
     void add(const void *src, void *dst, size_t bytes)
     {

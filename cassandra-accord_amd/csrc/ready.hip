@@ -267,8 +267,7 @@ struct ReadyParams {
     const KeySummary *sum;
     const uint32_t *kb;               // per key: shardRedundantBefore as a position (0: none)
     StatusView v;
-    uint32_t full;                    // evaluate every txn (else: only those whose inputs changed)
-    uint32_t seen, call;              // change epoch of the last call; this call's id
+    uint32_t full;                    // the generation is new: evaluate every txn of it
     const uint32_t *chg, *dirty;      // by position: change epoch; by key: id of the call it was dirty in
 };
 
@@ -328,7 +327,9 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, ui
 // (the txn itself, the key of a set key bit dirty -- for a managed txn: and no longer blocked by the
 // key's class minima --, the txn of a set range-dep bit changed) or that were never evaluated;
 // wave-aggregated appends to work[].
-__global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__restrict__ L)
+// (seen: the change epoch of the last call, call: this call's id, full: evaluate everything)
+__global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__restrict__ L, uint32_t seen, uint32_t call,
+                                                        uint32_t full)
 {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id();
     const uint32_t ngen = L->ngen, total = L->total;
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__res
         const uint32_t t = u - L->gbase[gi];
         if (!p.done[t]) {
             const uint32_t g = p.g[t];
-            need = p.full || p.chg[g] > p.seen;
+            need = full || p.full || p.chg[g] > seen;
             const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], RK = R + p.key_off[t + 1] - p.key_off[t];
             const uint32_t w0 = p.wo_off[t], nw = p.wo_off[t + 1] - w0;
             const uint64_t l = p.lsb[t];
@@ -358,9 +359,9 @@ __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__res
                     const uint32_t b = q * 64u + (uint32_t)__ffsll((long long)w) - 1u;
                     if (b >= RK) break;
                     w &= w - 1ull;
-                    if (b < R) { need = p.chg[p.rd_vals[p.rd_off[t] + b]] > p.seen; continue; }
+                    if (b < R) { need = p.chg[p.rd_vals[p.rd_off[t] + b]] > seen; continue; }
                     const uint32_t kk = p.keys[p.key_off[t] + b - R] - p.key_lo;
-                    if (p.dirty[kk] != p.call) continue;
+                    if (p.dirty[kk] != call) continue;
                     if (!managed) { need = true; continue; }
                     if (!stable) continue;                       // not STABLE: its key bits cannot clear
                     const KeySummary sm = p.sum[kk];
@@ -793,9 +794,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.sum = s->rdy_sum.as<KeySummary>();
         p.kb = has_kb && s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
         p.v = v;
-        p.full = full || r->fresh;
-        any_inc |= !p.full;
-        p.seen = seen; p.call = call;
+        p.full = r->fresh ? 1u : 0u;
+        any_inc |= !full && !r->fresh;
         p.chg = s->rg_chg.as<uint32_t>(); p.dirty = s->rdy_dirty2.as<uint32_t>();
         r->fresh = false;
         L.gbase[L.ngen] = L.total;
@@ -825,13 +825,22 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         HIPCHECK(s, hipHostMalloc(&s->rdy_tab_host, tab_bytes * 2, hipHostMallocDefault));
         s->rdy_tab_cap = tab_bytes * 2;
     }
-    std::memcpy(s->rdy_tab_host, tabs.data(), tab_bytes);
-    HIPCHECK(s, hipMemcpyAsync(s->rdy_launch.p, s->rdy_tab_host, tab_bytes, hipMemcpyHostToDevice, st));
+    // the tables change only when the generations or the buffers they point at do (the per-call
+    // epoch and id go to the filter as arguments): re-sent only then
+    const char *rs = getenv("ACCORD_READY_RESEND");           // dev aid (A/B): 1 = send every call
+    if ((rs && rs[0] == '1') || s->rdy_tab_last.size() != tab_bytes || s->rdy_tab_dev != s->rdy_launch.p ||
+        std::memcmp(s->rdy_tab_last.data(), tabs.data(), tab_bytes) != 0) {
+        std::memcpy(s->rdy_tab_host, tabs.data(), tab_bytes);
+        HIPCHECK(s, hipMemcpyAsync(s->rdy_launch.p, s->rdy_tab_host, tab_bytes, hipMemcpyHostToDevice, st));
+        s->rdy_tab_last.assign((const uint8_t *)tabs.data(), (const uint8_t *)tabs.data() + tab_bytes);
+        s->rdy_tab_dev = s->rdy_launch.p;
+    }
     const size_t rr_lds = s->rb_ext && s->rb_m ? 4 * sizeof(RrLds) : 0;   // removal scratch, a wave each
     for (size_t i = 0; i < tabs.size(); ++i) {
         const ReadyLaunch *L = s->rdy_launch.as<ReadyLaunch>() + i;
         if (any_inc) {
-            hipLaunchKernelGGL(rd_filter_kernel, dim3((tabs[i].total + 255) / 256), dim3(256), 0, st, L);
+            hipLaunchKernelGGL(rd_filter_kernel, dim3((tabs[i].total + 255) / 256), dim3(256), 0, st, L, seen, call,
+                               full ? 1u : 0u);
             hipLaunchKernelGGL(rd_eval_kernel, dim3(std::min(grid_for_waves(tabs[i].total), 1024u)), dim3(256), rr_lds, st, L, 1u);
         } else {
             hipLaunchKernelGGL(rd_eval_kernel, dim3(grid_for_waves(tabs[i].total)), dim3(256), rr_lds, st, L, 0u);

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 namespace {
@@ -1029,26 +1030,39 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
         return fail(s, ACCORD_ERR_ARG, "ACCEPTED..APPLIED events need an executeAt");
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     hipStream_t st = s->stream;
+    // the events in one host-to-device copy: packed into a pinned staging buffer (msb | lsb | exec
+    // msb | exec lsb | node | exec node | status), the device copy in op_tmp[0]
     DevBuf *T = s->op_tmp;
-    HIPCHECK(s, T[0].ensure((size_t)n * 8)); HIPCHECK(s, T[1].ensure((size_t)n * 8)); HIPCHECK(s, T[2].ensure((size_t)n * 4));
-    HIPCHECK(s, T[3].ensure((size_t)n)); HIPCHECK(s, T[4].ensure((size_t)n * 8)); HIPCHECK(s, T[5].ensure((size_t)n * 8));
-    HIPCHECK(s, T[6].ensure((size_t)n * 4)); HIPCHECK(s, T[7].ensure((size_t)n * 4));
-    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
-    HIPCHECK(s, hipMemcpyAsync(T[0].p, msb, (size_t)n * 8, hipMemcpyHostToDevice, st));
-    HIPCHECK(s, hipMemcpyAsync(T[1].p, lsb, (size_t)n * 8, hipMemcpyHostToDevice, st));
-    HIPCHECK(s, hipMemcpyAsync(T[2].p, node, (size_t)n * 4, hipMemcpyHostToDevice, st));
-    HIPCHECK(s, hipMemcpyAsync(T[3].p, status, n, hipMemcpyHostToDevice, st));
-    if (need_exec) {
-        HIPCHECK(s, hipMemcpyAsync(T[4].p, exec_msb, (size_t)n * 8, hipMemcpyHostToDevice, st));
-        HIPCHECK(s, hipMemcpyAsync(T[5].p, exec_lsb, (size_t)n * 8, hipMemcpyHostToDevice, st));
-        HIPCHECK(s, hipMemcpyAsync(T[6].p, exec_node, (size_t)n * 4, hipMemcpyHostToDevice, st));
+    const size_t o_lsb = (size_t)n * 8, o_emsb = o_lsb + (size_t)n * 8, o_elsb = o_emsb + (size_t)n * 8,
+                 o_node = o_elsb + (size_t)n * 8, o_enode = o_node + (size_t)n * 4, o_st = o_enode + (size_t)n * 4,
+                 bytes = (o_st + n + 15) & ~(size_t)15;
+    if (s->reg_host_cap < bytes) {
+        if (s->reg_host) (void)hipHostFree(s->reg_host);
+        s->reg_host = nullptr; s->reg_host_cap = 0;
+        HIPCHECK(s, hipHostMalloc(&s->reg_host, bytes * 2, hipHostMallocDefault));
+        s->reg_host_cap = bytes * 2;
     }
+    char *h = (char *)s->reg_host;
+    std::memcpy(h, msb, (size_t)n * 8);
+    std::memcpy(h + o_lsb, lsb, (size_t)n * 8);
+    std::memcpy(h + o_node, node, (size_t)n * 4);
+    std::memcpy(h + o_st, status, n);
+    if (need_exec) {
+        std::memcpy(h + o_emsb, exec_msb, (size_t)n * 8);
+        std::memcpy(h + o_elsb, exec_lsb, (size_t)n * 8);
+        std::memcpy(h + o_enode, exec_node, (size_t)n * 4);
+    }
+    HIPCHECK(s, T[0].ensure(bytes)); HIPCHECK(s, T[7].ensure((size_t)n * 4));
+    HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
+    HIPCHECK(s, hipMemcpyAsync(T[0].p, h, bytes, hipMemcpyHostToDevice, st));
     HostTotals *dev = s->status_totals.as<HostTotals>();
     HIPCHECK(s, hipMemsetAsync(&dev->status, 0xFF, sizeof(dev->status), st));
     RegParams p{};
     p.n = n; p.tx_n = s->rg_tx_n;
-    p.msb = T[0].as<uint64_t>(); p.lsb = T[1].as<uint64_t>(); p.node = T[2].as<int32_t>(); p.status = T[3].as<uint8_t>();
-    p.emsb = T[4].as<uint64_t>(); p.elsb = T[5].as<uint64_t>(); p.enode = T[6].as<int32_t>();
+    char *d = (char *)T[0].p;
+    p.msb = (const uint64_t *)d; p.lsb = (const uint64_t *)(d + o_lsb); p.node = (const int32_t *)(d + o_node);
+    p.status = (const uint8_t *)(d + o_st);
+    p.emsb = (const uint64_t *)(d + o_emsb); p.elsb = (const uint64_t *)(d + o_elsb); p.enode = (const int32_t *)(d + o_enode);
     p.tmsb = s->rg_tmsb.as<uint64_t>(); p.tlsb = s->rg_tlsb.as<uint64_t>(); p.tnode = s->rg_tnode.as<int32_t>();
     p.tg = s->rg_tg.as<uint32_t>();
     p.st = s->rg_status.as<uint8_t>();

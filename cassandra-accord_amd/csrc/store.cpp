@@ -126,7 +126,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
                       &s->rc_end2, &s->rc_kind2, &s->rc_first, &s->rc_flag, &s->rc_offs, &s->rdy_kseg0, &s->rdy_kseg1, &s->rdy_dirty, &s->rdy_dirty2, &s->rg_cchg, &s->rdy_dlist, &s->rdy_work, &s->rdy_wcnt, &s->rg_chg, &s->rdy_part, &s->rdy_sum, &s->rdy_out, &s->rdy_kb, &s->rdy_launch,
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero,
-                      &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->rr_ovf};
+                      &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->rr_ovf, &s->up_stage};
     accord_impl::shard_comm_destroy(s);
     accord_impl::ready_destroy(s);
     accord_impl::pinned_arena_destroy(s);
@@ -137,6 +137,8 @@ int32_t accord_store_destroy(accord_store *s)
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventDestroy(ev);
     if (s->pinned) (void)hipHostFree(s->pinned);
+    if (s->reg_host) (void)hipHostFree(s->reg_host);
+    if (s->up_host) (void)hipHostFree(s->up_host);
     (void)hipStreamDestroy(s->stream);
     delete s;
     return ACCORD_OK;
@@ -229,49 +231,66 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
     HIPCHECK(s, s->rng_off.ensure(((size_t)n + 1) * 4));
     HIPCHECK(s, s->rng_start.ensure((size_t)R * 4));
     HIPCHECK(s, s->rng_end.ensure((size_t)R * 4));
-    if (n) {
-        HIPCHECK(s, hipMemcpyAsync(s->msb.p, b->msb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->lsb.p, b->lsb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->node.p, b->node, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
+    if ((b->exec_msb != nullptr) != (b->exec_lsb != nullptr) || (b->exec_msb != nullptr) != (b->exec_node != nullptr))
+        return fail(s, ACCORD_ERR_ARG, "executeAt needs all of exec_msb, exec_lsb, exec_node");
+    // the batch's arrays: a small batch (a resident / registered store's) packed into pinned staging,
+    // one host-to-device copy and one device scatter; a large one copied array by array
+    struct Part { void *dst; const void *src; size_t bytes; };
+    std::vector<Part> parts;
+    parts.push_back({s->msb.p, b->msb, (size_t)n * 8});
+    parts.push_back({s->lsb.p, b->lsb, (size_t)n * 8});
+    parts.push_back({s->node.p, b->node, (size_t)n * 4});
+    parts.push_back({s->key_off.p, b->key_off, ((size_t)n + 1) * 4});
+    parts.push_back({s->key_ord.p, b->key_ord, (size_t)P * 4});
+    if (ro) parts.push_back({s->rng_off.p, ro, ((size_t)n + 1) * 4});
+    parts.push_back({s->rng_start.p, rs, (size_t)R * 4});
+    parts.push_back({s->rng_end.p, re, (size_t)R * 4});
+    if (b->txn_index || s->resident) HIPCHECK(s, s->txn_index.ensure((size_t)n * 4 + 4));
+    if (b->txn_index) parts.push_back({s->txn_index.p, b->txn_index, (size_t)n * 4});
+    if (b->exec_msb) {
+        HIPCHECK(s, s->exec_msb.ensure((size_t)n * 8));
+        HIPCHECK(s, s->exec_lsb.ensure((size_t)n * 8));
+        HIPCHECK(s, s->exec_node.ensure((size_t)n * 4));
+        parts.push_back({s->exec_msb.p, b->exec_msb, (size_t)n * 8});
+        parts.push_back({s->exec_lsb.p, b->exec_lsb, (size_t)n * 8});
+        parts.push_back({s->exec_node.p, b->exec_node, (size_t)n * 4});
     }
-    HIPCHECK(s, hipMemcpyAsync(s->key_off.p, b->key_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
-    if (P) HIPCHECK(s, hipMemcpyAsync(s->key_ord.p, b->key_ord, (size_t)P * 4, hipMemcpyHostToDevice, s->stream));
-    if (ro)
-        HIPCHECK(s, hipMemcpyAsync(s->rng_off.p, ro, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s->stream));
-    else
-        HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
-    if (R) {
-        HIPCHECK(s, hipMemcpyAsync(s->rng_start.p, rs, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rng_end.p, re, (size_t)R * 4, hipMemcpyHostToDevice, s->stream));
+    size_t packed = 0;
+    for (const Part &q : parts) packed += (q.bytes + 15) & ~(size_t)15;
+    if (!ro) HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
+    if (packed <= (8u << 20)) {
+        if (s->up_host_cap < packed) {
+            if (s->up_host) (void)hipHostFree(s->up_host);
+            s->up_host = nullptr; s->up_host_cap = 0;
+            HIPCHECK(s, hipHostMalloc(&s->up_host, std::max<size_t>(packed * 2, 1u << 16), hipHostMallocDefault));
+            s->up_host_cap = std::max<size_t>(packed * 2, 1u << 16);
+        }
+        HIPCHECK(s, s->up_stage.ensure(packed + 16));
+        accord::CopyList cl;
+        size_t off = 0;
+        for (const Part &q : parts) {
+            if (q.bytes) {
+                std::memcpy((char *)s->up_host + off, q.src, q.bytes);
+                cl.add((const char *)s->up_stage.p + off, q.dst, q.bytes);
+            }
+            off += (q.bytes + 15) & ~(size_t)15;
+        }
+        if (packed) HIPCHECK(s, hipMemcpyAsync(s->up_stage.p, s->up_host, packed, hipMemcpyHostToDevice, s->stream));
+        accord::launch_copy_words(cl, s->stream);
+    } else {
+        for (const Part &q : parts)
+            if (q.bytes) HIPCHECK(s, hipMemcpyAsync(q.dst, q.src, q.bytes, hipMemcpyHostToDevice, s->stream));
     }
     s->user_txn_index = b->txn_index != nullptr;
     s->has_txn_index = s->user_txn_index || s->resident;
-    if (s->has_txn_index) {
-        HIPCHECK(s, s->txn_index.ensure((size_t)n * 4 + 4));
-        if (s->user_txn_index) {
-            if (n) HIPCHECK(s, hipMemcpyAsync(s->txn_index.p, b->txn_index, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
-        } else {
-            accord::launch_gen_index(n, s->next_global, s->txn_index.as<uint32_t>(), s->stream);   // resident: next_global + t
-        }
-    }
+    if (s->has_txn_index && !s->user_txn_index)
+        accord::launch_gen_index(n, s->next_global, s->txn_index.as<uint32_t>(), s->stream);   // resident: next_global + t
     // where the batch ends in the stream (committed to the store when its compute succeeds)
     s->b_end = !s->resident ? n : (n == 0 ? s->next_global : (s->user_txn_index ? b->txn_index[n - 1] + 1u : s->next_global + n));
     if (s->resident && n && (uint64_t)s->next_global + n > (1ull << 29))
         return fail(s, ACCORD_ERR_CAPACITY, "resident store stream exceeds 2^29 txns");
     if (n) { s->b_last_msb = b->msb[n - 1]; s->b_last_lsb = b->lsb[n - 1]; s->b_last_node = b->node[n - 1]; }
-    if ((b->exec_msb != nullptr) != (b->exec_lsb != nullptr) || (b->exec_msb != nullptr) != (b->exec_node != nullptr))
-        return fail(s, ACCORD_ERR_ARG, "executeAt needs all of exec_msb, exec_lsb, exec_node");
     s->has_exec = b->exec_msb != nullptr;
-    if (s->has_exec) {
-        HIPCHECK(s, s->exec_msb.ensure((size_t)n * 8));
-        HIPCHECK(s, s->exec_lsb.ensure((size_t)n * 8));
-        HIPCHECK(s, s->exec_node.ensure((size_t)n * 4));
-        if (n) {
-            HIPCHECK(s, hipMemcpyAsync(s->exec_msb.p, b->exec_msb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
-            HIPCHECK(s, hipMemcpyAsync(s->exec_lsb.p, b->exec_lsb, (size_t)n * 8, hipMemcpyHostToDevice, s->stream));
-            HIPCHECK(s, hipMemcpyAsync(s->exec_node.p, b->exec_node, (size_t)n * 4, hipMemcpyHostToDevice, s->stream));
-        }
-    }
     HIPCHECK(s, hipStreamSynchronize(s->stream));
     s->has_batch = true;
     return ACCORD_OK;

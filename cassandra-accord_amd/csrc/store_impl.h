@@ -178,6 +178,13 @@ struct accord_store {
     uint64_t rdy_kseg_version = ~0ull, carry_version = 0;   // the carry's segment bounds are cached per carry version
     void *rdy_host = nullptr;                 // page-locked: the ready count + list readback
     void *rdy_tab_host = nullptr;             // pinned staging of the evaluation launch tables
+    std::vector<uint8_t> rdy_tab_last;        // the tables last sent, and where to
+    void *rdy_tab_dev = nullptr;
+    void *reg_host = nullptr;                 // pinned staging of accord_txn_register's events (one copy)
+    size_t reg_host_cap = 0;
+    void *up_host = nullptr;                  // pinned staging of a small batch's upload (one copy)
+    size_t up_host_cap = 0;
+    DevBuf up_stage;                          // its device side, scattered to the batch arrays
     size_t rdy_tab_cap = 0;
     uint64_t *rdy_stats = nullptr;            // ACCORD_READY_STATS diagnostics
     std::vector<uint32_t> rdy_kb_host;       // per key: shardRedundantBefore as a position (cumulative max)
