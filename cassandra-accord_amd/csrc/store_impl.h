@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 namespace accord_impl {
@@ -17,11 +18,16 @@ extern thread_local std::string g_last_error;
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    // a regrowth takes 1.5x: a resident store's history grows a little with every batch, and an
+    // exact-size buffer would be freed (a device-wide wait) and allocated again each time
     hipError_t ensure(size_t bytes)
     {
         if (bytes <= cap && p) return hipSuccess;
-        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
         size_t want = bytes < 256 ? 256 : bytes;
+        if (p) {
+            want = std::max(want, cap + cap / 2);
+            (void)hipFree(p); p = nullptr; cap = 0;
+        }
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         return e;
