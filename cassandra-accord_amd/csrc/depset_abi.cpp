@@ -91,7 +91,9 @@ int32_t check_views(accord_store *s, uint32_t np, const accord_deps *parts)
 }
 
 // Union of one side of G parts into the given output buffers of `o`.
-int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool range, DepSet &o)
+// totals_known: the parts' *_total fields are exact (the store's own views), so the input sizes
+// need no device read
+int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool range, DepSet &o, bool totals_known = false)
 {
     const uint32_t n = parts[0].n;
     const size_t nG = (size_t)n * G, n1 = (size_t)n + 1;
@@ -113,8 +115,18 @@ int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool r
     RC(sc.add(p.vlen, T[T_VEOFF].as<uint32_t>(), (uint32_t)nG));
     RC(sc.add(p.klen, T[T_KEOFF].as<uint32_t>(), (uint32_t)nG));
     RC(sc.add(p.blen, T[T_BEOFF].as<uint32_t>(), (uint32_t)nG));
-    unsigned long long tot[3];
-    RC(sc.read(tot));
+    unsigned long long tot[3] = {0, 0, 0};
+    if (totals_known) {
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint64_t nk = range ? parts[g].rd_rngs_total : parts[g].kd_keys_total;
+            tot[0] += range ? parts[g].rd_vals_total : parts[g].kd_vals_total;
+            tot[1] += nk;
+            tot[2] += (range ? parts[g].rd_r2v_total : parts[g].kd_k2v_total) - nk;
+        }
+        sc.k = 0;
+    } else {
+        RC(sc.read(tot));
+    }
     const uint64_t V = tot[0], K = tot[1], B = tot[2];
     if (V >= (1ull << 32) || K >= (1ull << 32) || B >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "union input over 2^32 elements");
     HIPCHECK(s, T[T_VOWN].ensure(V * 4 + 4)); HIPCHECK(s, T[T_VRANK].ensure(V * 4 + 4));
@@ -128,8 +140,14 @@ int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool r
     HIPCHECK(s, key_off.ensure(n1 * 4)); HIPCHECK(s, val_off.ensure(n1 * 4)); HIPCHECK(s, x_off.ensure(n1 * 4));
     RC(sc.add(p.cnt_vals, val_off.as<uint32_t>(), n));
     RC(sc.add(p.cnt_keys, key_off.as<uint32_t>(), n));
-    RC(sc.read(tot));
-    const uint64_t UV = tot[0], UK = tot[1];
+    // with the input sizes known the outputs are sized at their bounds (a union holds at most its
+    // inputs' elements; the body scan runs over K positions, zero past the union's) and the three
+    // totals are read once, at the end; otherwise each size is read before its buffers
+    uint64_t UV = V, UK = K;
+    if (!totals_known) {
+        RC(sc.read(tot));
+        UV = tot[0]; UK = tot[1];
+    }
     DevBuf &lo = range ? o.rng_start : o.keys, &vals = range ? o.rvals : o.vals, &x = range ? o.r : o.x;
     HIPCHECK(s, lo.ensure(UK * 4 + 4)); HIPCHECK(s, vals.ensure(UV * 4 + 4));
     if (range) HIPCHECK(s, o.rng_end.ensure(UK * 4 + 4));
@@ -141,14 +159,21 @@ int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool r
     p.out_vals = vals.as<uint32_t>(); p.out_lo = lo.as<uint32_t>(); p.out_hi = range ? o.rng_end.as<uint32_t>() : nullptr;
     accord::launch_union_ranks(p, s->stream);
     RC(sc.add(p.bsz, T[T_BSCAN].as<uint32_t>(), (uint32_t)UK));
-    RC(sc.read(tot));
-    const uint64_t UB = tot[0];
+    uint64_t UB = B;
+    if (!totals_known) {
+        RC(sc.read(tot));
+        UB = tot[0];
+    }
     HIPCHECK(s, x.ensure((UK + UB) * 4 + 4));
     p.bscan = T[T_BSCAN].as<uint32_t>();
     p.out_x_off = x_off.as<uint32_t>(); p.out_x = x.as<int32_t>();
     if (n == 0) HIPCHECK(s, hipMemsetAsync(x_off.p, 0, 4, s->stream));
     accord::launch_union_write(p, s->stream);
     HIPCHECK(s, hipGetLastError());
+    if (totals_known) {
+        RC(sc.read(tot));
+        UV = tot[0]; UK = tot[1]; UB = tot[2];
+    }
     if (range) { o.tot_rngs = UK; o.tot_rvals = UV; o.tot_r = UK + UB; }
     else { o.tot_keys = UK; o.tot_vals = UV; o.tot_x = UK + UB; }
     return ACCORD_OK;
@@ -266,24 +291,11 @@ namespace accord_impl {
 // The redundant RangeDeps of every txn of the computed batch (RedundantBefore.collectDeps,
 // redundant.hip), then PartialDeps.with of the computed deps and it (linearUnion on both sides,
 // as accord_deps_union): messages/PreAccept.java:262-263.
-int32_t redundant_apply(accord_store *s)
+static accord::RbParams rb_params(accord_store *s)
 {
     const uint32_t n = s->n;
     const size_t n1 = (size_t)n + 1;
-    hipStream_t st = s->stream;
-    DepSet &r = s->rb_set;
-    HIPCHECK(s, s->rb_cnt.ensure(3 * n1 * 4));
-    HIPCHECK(s, s->rb_zero.ensure(n1 * 4));
-    HIPCHECK(s, hipMemsetAsync(s->rb_zero.p, 0, n1 * 4, st));
-    HIPCHECK(s, r.rng_off.ensure(n1 * 4)); HIPCHECK(s, r.rval_off.ensure(n1 * 4)); HIPCHECK(s, r.r_off.ensure(n1 * 4));
     HostTotals *dev = s->status_totals.as<HostTotals>();
-    {
-        accord::FillList fl;
-        fl.add(&dev->status.first, sizeof(dev->status.first), 0xFFFFFFFFu);
-        fl.add(&dev->status.overflow, 4, 0u);
-        fl.add(&dev->status.overflow_first, 4, 0xFFFFFFFFu);
-        accord::launch_fill_words(fl, st);
-    }
     accord::RbParams p{};
     p.n = n;
     p.msb = s->msb.as<uint64_t>();
@@ -298,22 +310,50 @@ int32_t redundant_apply(accord_store *s)
     p.min_epoch = s->rb_min_epoch;
     uint32_t *cnt = s->rb_cnt.as<uint32_t>();
     p.cnt_rngs = cnt; p.cnt_vals = cnt + n1; p.cnt_r2v = cnt + 2 * n1;
-    p.status = &dev->status;
-    accord::launch_rb_count(p, st);
-    Scans sc;
-    RC(scans_init(s, sc));
-    RC(sc.add(p.cnt_rngs, r.rng_off.as<uint32_t>(), n));
-    RC(sc.add(p.cnt_vals, r.rval_off.as<uint32_t>(), n));
-    RC(sc.add(p.cnt_r2v, r.r_off.as<uint32_t>(), n));
-    unsigned long long tot[3];
-    RC(sc.read(tot));
+    p.status = &dev->rb_status;
+    return p;
+}
+
+int32_t redundant_count(accord_store *s)
+{
+    const uint32_t n = s->n;
+    const size_t n1 = (size_t)n + 1;
+    hipStream_t st = s->stream;
+    DepSet &r = s->rb_set;
+    HIPCHECK(s, s->rb_cnt.ensure(3 * n1 * 4));
+    HIPCHECK(s, r.rng_off.ensure(n1 * 4)); HIPCHECK(s, r.rval_off.ensure(n1 * 4)); HIPCHECK(s, r.r_off.ensure(n1 * 4));
+    HostTotals *dev = s->status_totals.as<HostTotals>();
     {
-        HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(accord::DevStatus), hipMemcpyDeviceToHost, st));
-        HIPCHECK(s, hipStreamSynchronize(st));
-        if (s->pinned->status.overflow)
-            return fail(s, ACCORD_ERR_CAPACITY, "%u txns touch more than %u RedundantBefore entries (first: txn %u)",
-                        s->pinned->status.overflow, accord::RB_MAX, s->pinned->status.overflow_first);
+        accord::FillList fl;
+        fl.add(&dev->rb_status.first, sizeof(dev->rb_status.first), 0xFFFFFFFFu);
+        fl.add(&dev->rb_status.overflow, 4, 0u);
+        fl.add(&dev->rb_status.overflow_first, 4, 0xFFFFFFFFu);
+        accord::launch_fill_words(fl, st);
     }
+    const accord::RbParams p = rb_params(s);
+    accord::launch_rb_count(p, st);
+    HIPCHECK(s, s->op_tmp[T_SCAN].ensure_zeroed(accord::scan_temp_bytes(n), st));
+    void *tmp = s->op_tmp[T_SCAN].p;
+    accord::exclusive_scan_u32(p.cnt_rngs, r.rng_off.as<uint32_t>(), n, &dev->rb_tot[0], tmp, st);
+    accord::exclusive_scan_u32(p.cnt_vals, r.rval_off.as<uint32_t>(), n, &dev->rb_tot[1], tmp, st);
+    accord::exclusive_scan_u32(p.cnt_r2v, r.r_off.as<uint32_t>(), n, &dev->rb_tot[2], tmp, st);
+    HIPCHECK(s, hipGetLastError());
+    return ACCORD_OK;
+}
+
+int32_t redundant_apply(accord_store *s)
+{
+    const uint32_t n = s->n;
+    const size_t n1 = (size_t)n + 1;
+    hipStream_t st = s->stream;
+    DepSet &r = s->rb_set;
+    if (s->pinned->rb_status.overflow)
+        return fail(s, ACCORD_ERR_CAPACITY, "%u txns touch more than %u RedundantBefore entries (first: txn %u)",
+                    s->pinned->rb_status.overflow, accord::RB_MAX, s->pinned->rb_status.overflow_first);
+    const unsigned long long tot[3] = {s->pinned->rb_tot[0], s->pinned->rb_tot[1], s->pinned->rb_tot[2]};
+    HIPCHECK(s, s->rb_zero.ensure(n1 * 4));
+    HIPCHECK(s, hipMemsetAsync(s->rb_zero.p, 0, n1 * 4, st));
+    accord::RbParams p = rb_params(s);
     HIPCHECK(s, r.rng_start.ensure(tot[0] * 4 + 4)); HIPCHECK(s, r.rng_end.ensure(tot[0] * 4 + 4));
     HIPCHECK(s, r.rvals.ensure(tot[1] * 4 + 4)); HIPCHECK(s, r.r.ensure(tot[2] * 4 + 4));
     p.rng_off_out = r.rng_off.as<uint32_t>(); p.val_off_out = r.rval_off.as<uint32_t>(); p.r2v_off_out = r.r_off.as<uint32_t>();
@@ -336,11 +376,11 @@ int32_t redundant_apply(accord_store *s)
     // RangeDeps side with an empty part is the other part (ACCORD_RB_UNION=1: always the union)
     const char *ru = getenv("ACCORD_RB_UNION");
     const bool always = ru && ru[0] == '1';
-    if (always) RC(union_side(s, parts, 2, false, o));
+    if (always) RC(union_side(s, parts, 2, false, o, true));
     else RC(copy_side(s, parts[0], false, o));
     if (!always && parts[0].rd_rngs_total == 0) RC(copy_side(s, parts[1], true, o));
     else if (!always && tot[0] == 0) RC(copy_side(s, parts[0], true, o));
-    else RC(union_side(s, parts, 2, true, o));
+    else RC(union_side(s, parts, 2, true, o, true));
     HIPCHECK(s, hipStreamSynchronize(st));
     publish(s, o, n);
     s->ds_rb = true;

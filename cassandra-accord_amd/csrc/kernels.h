@@ -217,6 +217,7 @@ struct RangeDepsParams {
     const uint32_t *range_txns;
     uint32_t *rk_cls;                   // union size classes: counts [0, 8), then per class n_range_txns
                                         //   records {txn, D, body base, txnIds base} (uint4)
+    uint32_t rk_bitmap;                 // union by span bitmap when the body spans < 4096 txns (else sort)
     const uint32_t *bound_l;            // Accept batch: txns started before executeAt (nullptr = i)
     // resident stores: txn i of the batch is stream position g0 + i; the range commands carried
     // from earlier batches (owner positions ascending, all before g0) precede the batch's own in

@@ -533,6 +533,7 @@ __device__ __forceinline__ void rk_slices(const RangeDepsParams &p, uint32_t i, 
 // Stored slice (count pass -> fill pass): lo, and raw | wcnt << 16; RK_SLICE_WIDE marks a slice
 // too long for 16-bit fields (the fill pass recomputes it).
 constexpr uint32_t RK_SLICE_WIDE = 0xFFFFFFFFu;
+constexpr uint32_t RK_BITMAP_SPAN = 4096;      // 128 LDS words of one wave's union buffer
 
 // Per range txn (one wave): count pass computes and stores every key's slice (keys of its ranges
 // in ascending order, clipped to the store) and the KeyDeps sizes; the fill pass writes keys, the
@@ -819,6 +820,43 @@ __device__ __forceinline__ void rk_union(const RangeDepsParams &p, uint32_t i, u
     }
     vmin = ~readlane(wave_incl_max(~vmin), 63);
     vmax = readlane(wave_incl_max(vmax), 63);
+    if (vmax - vmin < RK_BITMAP_SPAN && p.rk_bitmap) {
+        // the body's values span < 4096 txns (always, in a store whose window is <= 4096): the union
+        // is a bitmap over the span in LDS (lane l owns words 2l, 2l+1), the unique txns its set bits
+        // in order and each entry's rank the set bits below it -- no sort
+        lds[lane] = 0u; lds[64 + lane] = 0u;
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const uint32_t g = (uint32_t)r * 64 + lane;
+            if (g < D) {
+                const uint32_t off = v[r] - vmin;
+                atomicOr(&lds[off >> 5], 1u << (off & 31));
+            }
+        }
+        wave_lds_sync();
+        const uint32_t w0 = lds[2 * lane], w1 = lds[2 * lane + 1];
+        const uint32_t c0 = (uint32_t)__popc(w0), c = c0 + (uint32_t)__popc(w1);
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t U = readlane(incl, 63), excl = incl - c;
+        lds[128 + 2 * lane] = excl;
+        lds[128 + 2 * lane + 1] = excl + c0;
+        if (lane == 0) p.cnt_vals_exact[i] = U;
+        wave_lds_sync();
+        uint32_t pos = vb + excl;
+        for (uint32_t m = w0; m; m &= m - 1) p.kd_vals[pos++] = vmin + 64 * lane + (uint32_t)__builtin_ctz(m);
+        for (uint32_t m = w1; m; m &= m - 1) p.kd_vals[pos++] = vmin + 64 * lane + 32 + (uint32_t)__builtin_ctz(m);
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const uint32_t g = (uint32_t)r * 64 + lane;
+            if (g < D) {
+                const uint32_t off = v[r] - vmin, wd = off >> 5;
+                p.kd_k2v[k2v_base + g] = (int32_t)(lds[128 + wd] + (uint32_t)__popc(lds[wd] & ((1u << (off & 31)) - 1u)));
+            }
+        }
+        wave_lds_sync();
+        return;
+    }
     const bool packed = vmax - vmin < (1u << (32 - IB)) - 1u;
     if (packed) {
 #pragma unroll

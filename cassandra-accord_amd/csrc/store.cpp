@@ -504,6 +504,10 @@ int32_t accord_deps_compute(accord_store *s)
     }
     rp.n_range_txns = nrt; rp.range_txns = s->range_txns.as<uint32_t>();
     rp.rk_cls = s->rk_cls.as<uint32_t>();
+    {
+        const char *e = getenv("ACCORD_RK_BITMAP");       // A/B: 0 = the sort for every body
+        rp.rk_bitmap = (e && e[0] == '0') ? 0u : 1u;
+    }
     rp.cnt_rngs = s->cnt_rngs.as<uint32_t>(); rp.cnt_vals = s->cnt_rvals.as<uint32_t>(); rp.cnt_r2v = s->cnt_r2v.as<uint32_t>();
     // range txns' KeyDeps: exact txnIds count into the upper-bound array (their bound is exact)
     rp.cnt_keys = s->cnt_keys.as<uint32_t>(); rp.cnt_vals_k = s->cnt_vub.as<uint32_t>(); rp.cnt_k2v = s->cnt_k2v.as<uint32_t>();
@@ -669,6 +673,10 @@ int32_t accord_deps_compute(accord_store *s)
         }
     }
     record(s, EV_COMPACT);
+    if (s->rb_m) {      // RedundantBefore.collectDeps' sizes travel with this copy
+        int32_t rc = accord_impl::redundant_count(s);
+        if (rc) return rc;
+    }
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     if (s->events)
         HIPCHECK(s, hipMemcpyAsync(&s->pinned->scan, accord::scan_counters(s->scan_tmp.p), sizeof(accord::ScanCounters),

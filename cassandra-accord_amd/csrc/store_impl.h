@@ -49,6 +49,8 @@ struct HostTotals {
     accord::DevStatus status;
     unsigned long long totals[10];  // kd keys, kd vals bound, kd k2v, rd ranges, rd vals, rd r2v, range txns,
                                     // kd vals, resident carry entries, spare
+    unsigned long long rb_tot[3];   // RedundantBefore deps: ranges, vals, r2v (counted during compute)
+    accord::DevStatus rb_status;    // its capacity status, apart from the compute's
     accord::ScanCounters scan;      // the store's scan-state counters (profiled stores read them)
 };
 
@@ -229,7 +231,10 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
 int32_t ready_track_batch(accord_store *s);
 int32_t ready_batch_check(accord_store *s);
 void ready_destroy(accord_store *s);
-// RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp)
+// RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp):
+// the count and its scans are queued inside the compute (totals arrive with its final copy), the
+// fill and the union after it
+int32_t redundant_count(accord_store *s);
 int32_t redundant_apply(accord_store *s);
 // The batch's current deps (device): the pipeline's own output, or its RedundantBefore union.
 struct CurDeps {
