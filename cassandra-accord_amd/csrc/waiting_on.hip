@@ -175,10 +175,13 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 // 1 + b(i,j); bq = b(i, slot) bytes in slot order, b = dist + 1 (0 = j does not reach i).  Slots:
 // late entries, then early entries, then non-entries.  ref[s][slot] = the slot's far predecessors.
 // hdr = nl | ne << 8 | slow << 16 (slow: some entry has more than LV_REFS far predecessors).
+// late_chunks: an entry is late when a predecessor lies in the previous late_chunks chunks (1 for
+// lv_resolve_kernel, 2 for the staged resolver lv_staged_kernel).
 __global__ __launch_bounds__(256) void lv_closure_kernel(uint32_t n, uint32_t nchunks,
                                                          const uint32_t *__restrict__ pred_off,
                                                          const uint32_t *__restrict__ preds,
-                                                         uint32_t *__restrict__ rec, uint32_t *__restrict__ info)
+                                                         uint32_t *__restrict__ rec, uint32_t *__restrict__ info,
+                                                         uint32_t late_chunks)
 {
     __shared__ __attribute__((aligned(16))) uint8_t rows_all[4][64 * LV_ROW];
     __shared__ uint32_t snode_all[4][64];
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(256) void lv_closure_kernel(uint32_t n, uint32_t nc
 #pragma unroll
             for (int s = 0; s < LV_REFS; ++s) dup = dup || ref[s] == f;
             if (dup) continue;
-            late = late || f + LC >= base;
+            late = late || f + late_chunks * LC >= base;
 #pragma unroll
             for (int s = 0; s < LV_REFS; ++s)
                 if (s == (int)nfar) ref[s] = f;
@@ -462,6 +465,264 @@ __global__ __launch_bounds__(LV_WAVES * 64) void lv_resolve_kernel(uint32_t n, u
     }
 }
 
+// ---- staged resolve: one resolver wave walks the chain, helper waves stage each chunk ----
+// Late entry columns (lv_closure_kernel with late_chunks = 2) have a predecessor in chunk x-1 or
+// x-2; everything else of chunk x depends on chunks <= x-3 only.  The helpers (waves 1..7, chunk x
+// to wave 1 + x % 7) compute that part while the resolver is still two chunks behind -- the early
+// bases and the product over the early columns (acc_e per row), the late columns' bases from their
+// older predecessors (bv_e), their predecessors in x-1 / x-2 as ring indices, and the late
+// columns' closure expanded to ints -- and hand it over in one of LS_K LDS slots.  The resolver's
+// step per chunk is then only: the late predecessors' values from the ring (8 LDS reads; its own
+// earlier writes, in order on its LDS queue), the late bases, and the product over the late
+// columns; no wave-to-wave hand-off sits on the chain unless a helper falls behind.
+constexpr uint32_t LS_K = 4;                  // staged chunks in flight
+constexpr int LS_LREF = 8;                    // late predecessors per column in the slot
+constexpr int LS_HELPERS = 7;
+constexpr uint32_t LS_ZERO = LV_RING;         // ring word that stays 0: an absent reference
+struct LsSlot {
+    int4 d[16][64];                           // d[g][row] = b(row, 4g..4g+3), INT_MIN if unreachable
+    int32_t acc_e[64];                        // per row: max(cst, early columns' products)
+    uint32_t bv_e[64];                        // per column slot: base from predecessors in chunks <= x-3
+    uint32_t lref[LS_LREF / 2][64];           // per column slot: two 16-bit ring indices per word
+    uint32_t node[64];                        // column slot -> row
+    uint32_t hdr;                             // nl | slowlate << 16
+    uint32_t ready;                           // chunk + 1 once staged
+};
+struct LsShared {
+    uint32_t ring[LV_RING + 1];
+    LsSlot slot[LS_K];
+    uint32_t done, abort_flag, maxlv;
+};
+
+// Spin until *flag == target (EQ) or >= target; false once any wave gave up.  The asm barrier keeps
+// the compiler from moving the caller's LDS reads above the wait (LDS ops of a wave execute in
+// order, and the writer's data lands before its flag).  Helpers sleep between polls so their spins
+// leave the LDS and the issue slots to the resolver.
+template <bool EQ, bool SLEEP>
+__device__ __forceinline__ bool ls_spin(const uint32_t *flag, uint32_t *abort_flag, uint32_t target)
+{
+    uint32_t spins = 0;
+    for (;;) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (EQ ? v == target : v >= target) break;
+        if (SLEEP) __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 255u) == 0) {
+            if (__builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                return false;
+            if (spins > (1u << 26)) {
+                __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+        }
+    }
+    asm volatile("" ::: "memory");
+    return true;
+}
+__device__ __forceinline__ bool ls_wait_ready(const uint32_t *ready, uint32_t *abort_flag, uint32_t target)
+{
+    return ls_spin<true, false>(ready, abort_flag, target);
+}
+__device__ __forceinline__ bool ls_wait_done(const uint32_t *done, uint32_t *abort_flag, uint32_t target)
+{
+    return ls_spin<false, true>(done, abort_flag, target);
+}
+
+// Helper: stage chunk x (record `cur`) into its slot.  False on abort.
+__device__ __forceinline__ bool ls_stage(LsShared &S, uint32_t n, uint32_t x, const LvRec &cur,
+                                         const uint32_t *__restrict__ pred_off, const uint32_t *__restrict__ preds,
+                                         const uint32_t *level, uint32_t lane, unsigned long long *stats)
+{
+    const uint32_t base = x * LC;
+    const uint32_t hdr = __builtin_amdgcn_readfirstlane(cur.hdr);
+    const uint32_t nl = hdr & 0xFFu, ne = (hdr >> 8) & 0xFFu;
+    const bool slow = (hdr >> 16) & 1u;
+    // predecessors older than the ring: final long ago, loaded now
+    uint32_t oldv[LV_REFS];
+#pragma unroll
+    for (int s = 0; s < LV_REFS; ++s) {
+        const uint32_t f = cur.ref[s];
+        const bool old = !slow && f != REF_NONE && f + LV_RING < base;
+        oldv[s] = level[old ? f : 0u];
+    }
+    int32_t d[64];
+    lv_expand(cur.bq, d);
+    LsSlot &sl = S.slot[x % LS_K];
+    // the slot is free once the resolver has finished chunk x - LS_K
+    if (!ls_wait_done(&S.done, &S.abort_flag, x + 1 >= LS_K ? x + 1 - LS_K : 0u)) return false;
+    // the late columns' closure, in the resolver's groups of 8 columns
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+        if ((uint32_t)(8 * (g >> 1)) < nl) sl.d[g][lane] = make_int4(d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]);
+    // chunks <= x-3 final
+    if (!ls_wait_done(&S.done, &S.abort_flag, x >= 2 ? x - 2 : 0u)) return false;
+    const unsigned long long tp = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    uint32_t e = 0, lr[LS_LREF];
+#pragma unroll
+    for (int s = 0; s < LS_LREF; ++s) lr[s] = LS_ZERO;
+    bool slowlate = false;
+    if (!slow) {
+        uint32_t rv[LV_REFS];
+#pragma unroll
+        for (int s = 0; s < LV_REFS; ++s) {          // LDS reads issued together
+            const uint32_t f = cur.ref[s];
+            const bool mid = f != REF_NONE && f + 2 * LC < base && f + LV_RING >= base;
+            rv[s] = S.ring[mid ? f % LV_RING : LS_ZERO];
+        }
+#pragma unroll
+        for (int s = 0; s < LV_REFS; ++s) {
+            const uint32_t f = cur.ref[s];
+            if (f == REF_NONE) continue;
+            if (f + 2 * LC >= base) lr[s] = f % LV_RING;
+            else e = max(e, f + LV_RING < base ? oldv[s] + 1u : rv[s]);
+        }
+    } else if (lane < ne) {
+        // some entry has more predecessors than the record holds: its full list
+        const uint32_t t = base + cur.node;
+        uint32_t nlr = 0;
+        if (t < n) {
+            for (uint32_t q = pred_off[t], q1 = pred_off[t + 1]; q < q1; ++q) {
+                const uint32_t f = preds[q];
+                if (f >= base) continue;
+                if (f + 2 * LC >= base) {
+                    bool dup = false;
+#pragma unroll
+                    for (int s = 0; s < LS_LREF; ++s) dup = dup || lr[s] == f % LV_RING;
+                    if (dup) continue;
+#pragma unroll
+                    for (int s = 0; s < LS_LREF; ++s)
+                        if (s == (int)nlr) lr[s] = f % LV_RING;
+                    if (nlr == (uint32_t)LS_LREF) slowlate = true;
+                    else ++nlr;
+                } else {
+                    e = max(e, f + LV_RING >= base ? S.ring[f % LV_RING] : level[f] + 1u);
+                }
+            }
+        }
+    }
+    const uint32_t bv = e + 1u;
+    int32_t acc = lv_matvec((int32_t)cur.cst, d, bv, nl, ne);
+    sl.acc_e[lane] = acc;
+    sl.bv_e[lane] = bv;
+#pragma unroll
+    for (int s = 0; s < LS_LREF / 2; ++s) sl.lref[s][lane] = lr[2 * s] | lr[2 * s + 1] << 16;
+    sl.node[lane] = cur.node;
+    const bool any_slowlate = __ballot(slowlate) != 0;
+    if (lane == 0) sl.hdr = nl | (any_slowlate ? 1u << 16 : 0u);
+    wave_lds_sync();                                  // the slot's contents before its flag
+    if (lane == 0) __hip_atomic_store(&sl.ready, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (stats) *stats += __builtin_amdgcn_s_memtime() - tp;
+    return true;
+}
+
+// Resolver: chunk x from its staged slot.  False on abort.
+__device__ __forceinline__ bool ls_resolve(LsShared &S, uint32_t n, uint32_t x, const uint32_t *__restrict__ pred_off,
+                                           const uint32_t *__restrict__ preds, uint32_t *level, uint32_t lane,
+                                           uint32_t &mymax)
+{
+    const uint32_t base = x * LC;
+    LsSlot &sl = S.slot[x % LS_K];
+    if (!ls_wait_ready(&sl.ready, &S.abort_flag, x + 1)) return false;
+    const uint32_t hdr = __builtin_amdgcn_readfirstlane(sl.hdr);
+    const uint32_t nl = hdr & 0xFFu;
+    int32_t d[64];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {                    // unconditional: columns past nl are not used
+        const int4 v = sl.d[g][lane];
+        d[4 * g] = v.x; d[4 * g + 1] = v.y; d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+    }
+    const int32_t acc_e = sl.acc_e[lane];
+    const uint32_t bv_e = sl.bv_e[lane];
+    uint32_t lw[LS_LREF / 2];
+#pragma unroll
+    for (int s = 0; s < LS_LREF / 2; ++s) lw[s] = sl.lref[s][lane];
+    uint32_t rv[LS_LREF];
+#pragma unroll
+    for (int s = 0; s < LS_LREF; ++s) rv[s] = S.ring[(lw[s >> 1] >> (16 * (s & 1))) & 0xFFFFu];
+    uint32_t lat = max(max(max(rv[0], rv[1]), max(rv[2], rv[3])), max(max(rv[4], rv[5]), max(rv[6], rv[7])));
+    if (hdr >> 16) {                                  // a late column with more than LS_LREF: its full list
+        const uint32_t t = base + sl.node[lane];
+        if (lane < nl && t < n) {
+            for (uint32_t q = pred_off[t], q1 = pred_off[t + 1]; q < q1; ++q) {
+                const uint32_t f = preds[q];
+                if (f < base && f + 2 * LC >= base) lat = max(lat, S.ring[f % LV_RING]);
+            }
+        }
+    }
+    const uint32_t bv = max(bv_e, lat + 1u);
+    const int32_t acc = lv_matvec(acc_e, d, bv, 0, nl);
+    const uint32_t t = base + lane;
+    if (t < n) {
+        const uint32_t v = (uint32_t)acc - 1u;
+        S.ring[t % LV_RING] = v;
+        level[t] = v - 1u;
+        mymax = max(mymax, v - 1u);
+    }
+    // same wave, in-order LDS: the ring entries land before the count
+    if (lane == 0) __hip_atomic_store(&S.done, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return true;
+}
+
+// DBG (ACCORD_LV_STATS=1): s_memtime sums -- dbg[0] resolver cycles waiting for a slot, [1] its
+// cycles from slot to published chunk, [2] chunks it waited > 100 cycles for, [3] helpers' cycles
+// from "chunks <= x-3 final" to the slot's flag, [4] chunks staged
+template <bool DBG>
+__global__ __launch_bounds__((LS_HELPERS + 1) * 64) void lv_staged_kernel(uint32_t n, uint32_t nchunks,
+                                                                        const uint32_t *__restrict__ rec,
+                                                                        const uint32_t *__restrict__ pred_off,
+                                                                        const uint32_t *__restrict__ preds,
+                                                                        uint32_t *level, uint32_t *__restrict__ info,
+                                                                        unsigned long long *dbg)
+{
+    __shared__ LsShared S;
+    const uint32_t w = wave_id(), lane = lane_id();
+    if (threadIdx.x == 0) { S.done = 0; S.abort_flag = 0; S.maxlv = 0; S.ring[LS_ZERO] = 0; }
+    if (threadIdx.x < LS_K) S.slot[threadIdx.x].ready = 0;
+    __syncthreads();
+    uint32_t mymax = 0;
+    if (w == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        unsigned long long tw = 0, tc = 0, ns = 0;
+        for (uint32_t x = 0; x < nchunks; ++x) {
+            unsigned long long t0 = 0, t1 = 0;
+            if (DBG) {
+                t0 = __builtin_amdgcn_s_memtime();
+                if (!ls_wait_ready(&S.slot[x % LS_K].ready, &S.abort_flag, x + 1)) break;
+                t1 = __builtin_amdgcn_s_memtime();
+            }
+            if (!ls_resolve(S, n, x, pred_off, preds, level, lane, mymax)) break;
+            if (DBG) {
+                const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+                tw += t1 - t0; tc += t2 - t1; ns += (t1 - t0 > 100) ? 1 : 0;
+            }
+        }
+        if (DBG && lane == 0) { dbg[0] = tw; dbg[1] = tc; dbg[2] = ns; }
+    } else {
+        LvRec ra, rb;
+        const uint32_t h = w - 1;
+        unsigned long long tp = 0, *st = DBG ? &tp : nullptr;
+        uint32_t cnt = 0;
+        lv_load(rec, h, nchunks, lane, ra);
+        for (uint32_t x = h; x < nchunks; x += 2 * LS_HELPERS) {
+            lv_load(rec, x + LS_HELPERS, nchunks, lane, rb);      // the next record, in flight meanwhile
+            if (!ls_stage(S, n, x, ra, pred_off, preds, level, lane, st)) break;
+            ++cnt;
+            if (x + LS_HELPERS >= nchunks) break;
+            lv_load(rec, x + 2 * LS_HELPERS, nchunks, lane, ra);
+            if (!ls_stage(S, n, x + LS_HELPERS, rb, pred_off, preds, level, lane, st)) break;
+            ++cnt;
+        }
+        if (DBG && lane == 0) { atomicAdd(&dbg[3], tp); atomicAdd(&dbg[4], (unsigned long long)cnt); }
+    }
+    atomicMax(&S.maxlv, mymax);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (S.abort_flag) info[0] = 1 + S.done;
+        info[1] = S.maxlv;
+    }
+}
+
 } // namespace
 
 void launch_wo_words_count(uint32_t n, const uint32_t *kd_key_off, const uint32_t *rd_val_off, uint32_t *cnt,
@@ -510,15 +771,36 @@ void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, 
     if (n == 0) return;
     const uint32_t nchunks = (n + LC - 1) / LC;
     uint32_t *rec = (uint32_t *)temp;
+    // ACCORD_LV_STAGED=0: the pipelined all-waves resolver instead of the staged one (A/B)
+    const char *st = getenv("ACCORD_LV_STAGED");
+    const bool staged = !(st && st[0] == '0');
     hipLaunchKernelGGL(lv_closure_kernel, dim3((nchunks + 3) / 4), dim3(256), 0, s, n, nchunks, pred_off, preds, rec,
-                       info);
+                       info, staged ? 2u : 1u);
     // ACCORD_LV_DEBUG=<file>: per-chunk s_memtime stamps of the resolve pass (development aid)
     const char *dbg_path = getenv("ACCORD_LV_DEBUG");
     unsigned long long *dbg = nullptr;
     if (dbg_path && hipMalloc(&dbg, (size_t)nchunks * 5 * 8) != hipSuccess) dbg = nullptr;
     // 8 waves (2 per SIMD): 4 and 12 measured within noise / slower (profiles/r01_v13)
-    hipLaunchKernelGGL(lv_resolve_kernel<8>, dim3(1), dim3(8 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
-                       info, dbg);
+    const char *sts = getenv("ACCORD_LV_STATS");
+    unsigned long long *sdbg = nullptr;
+    if (staged && sts && sts[0] == '1' && hipMalloc(&sdbg, 64) == hipSuccess) (void)hipMemsetAsync(sdbg, 0, 64, s);
+    if (staged && sdbg)
+        hipLaunchKernelGGL(lv_staged_kernel<true>, dim3(1), dim3((LS_HELPERS + 1) * 64), 0, s, n, nchunks, rec,
+                           pred_off, preds, level, info, sdbg);
+    else if (staged)
+        hipLaunchKernelGGL(lv_staged_kernel<false>, dim3(1), dim3((LS_HELPERS + 1) * 64), 0, s, n, nchunks, rec,
+                           pred_off, preds, level, info, (unsigned long long *)nullptr);
+    else
+        hipLaunchKernelGGL(lv_resolve_kernel<8>, dim3(1), dim3(8 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
+                           info, dbg);
+    if (sdbg) {
+        unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyAsync(h, sdbg, 64, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess)
+            fprintf(stderr, "lv_staged: chunks %u resolver wait %.1f compute %.1f cycles/chunk, waited on %llu chunks; "
+                    "helper stage-after-final %.1f cycles/chunk (%llu)\n", nchunks, (double)h[0] / nchunks,
+                    (double)h[1] / nchunks, h[2], h[4] ? (double)h[3] / h[4] : 0.0, h[4]);
+        (void)hipFree(sdbg);
+    }
     if (dbg) {
         std::vector<unsigned long long> h((size_t)nchunks * 5);
         if (hipMemcpyAsync(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
