@@ -485,8 +485,8 @@ struct LsSlot {
     uint32_t bv_e[64];                        // per column slot: base from predecessors in chunks <= x-3
     uint32_t lref[LS_LREF / 2][64];           // per column slot: two 16-bit ring indices per word
     uint32_t node[64];                        // column slot -> row
-    uint32_t hdr;                             // nl | slowlate << 16
-    uint32_t ready;                           // chunk + 1 once staged
+    uint32_t ready;                           // (chunk + 1) << 9 | slowlate << 8 | nl, once staged
+    uint32_t dready;                          // chunk + 1 once d is staged (the resolver prefetches it)
 };
 struct LsShared {
     uint32_t ring[LV_RING + 1];
@@ -520,10 +520,6 @@ __device__ __forceinline__ bool ls_spin(const uint32_t *flag, uint32_t *abort_fl
     asm volatile("" ::: "memory");
     return true;
 }
-__device__ __forceinline__ bool ls_wait_ready(const uint32_t *ready, uint32_t *abort_flag, uint32_t target)
-{
-    return ls_spin<true, false>(ready, abort_flag, target);
-}
 __device__ __forceinline__ bool ls_wait_done(const uint32_t *done, uint32_t *abort_flag, uint32_t target)
 {
     return ls_spin<false, true>(done, abort_flag, target);
@@ -532,7 +528,7 @@ __device__ __forceinline__ bool ls_wait_done(const uint32_t *done, uint32_t *abo
 // Helper: stage chunk x (record `cur`) into its slot.  False on abort.
 __device__ __forceinline__ bool ls_stage(LsShared &S, uint32_t n, uint32_t x, const LvRec &cur,
                                          const uint32_t *__restrict__ pred_off, const uint32_t *__restrict__ preds,
-                                         const uint32_t *level, uint32_t lane, unsigned long long *stats)
+                                         uint32_t *level, uint32_t lane, unsigned long long *stats)
 {
     const uint32_t base = x * LC;
     const uint32_t hdr = __builtin_amdgcn_readfirstlane(cur.hdr);
@@ -555,9 +551,15 @@ __device__ __forceinline__ bool ls_stage(LsShared &S, uint32_t n, uint32_t x, co
 #pragma unroll
     for (int g = 0; g < 16; ++g)
         if ((uint32_t)(8 * (g >> 1)) < nl) sl.d[g][lane] = make_int4(d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]);
+    wave_lds_sync();
+    if (lane == 0) __hip_atomic_store(&sl.dready, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // chunks <= x-3 final
     if (!ls_wait_done(&S.done, &S.abort_flag, x >= 2 ? x - 2 : 0u)) return false;
     const unsigned long long tp = stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (x >= 3) {                                     // chunk x-3 is final: its levels to HBM (the
+        const uint32_t c = (x - 3) * LC + lane;       // resolver itself issues no vector-memory op)
+        if (c < n) level[c] = S.ring[c % LV_RING] - 1u;
+    }
     uint32_t e = 0, lr[LS_LREF];
 #pragma unroll
     for (int s = 0; s < LS_LREF; ++s) lr[s] = LS_ZERO;
@@ -609,39 +611,76 @@ __device__ __forceinline__ bool ls_stage(LsShared &S, uint32_t n, uint32_t x, co
     for (int s = 0; s < LS_LREF / 2; ++s) sl.lref[s][lane] = lr[2 * s] | lr[2 * s + 1] << 16;
     sl.node[lane] = cur.node;
     const bool any_slowlate = __ballot(slowlate) != 0;
-    if (lane == 0) sl.hdr = nl | (any_slowlate ? 1u << 16 : 0u);
     wave_lds_sync();                                  // the slot's contents before its flag
-    if (lane == 0) __hip_atomic_store(&sl.ready, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0)
+        __hip_atomic_store(&sl.ready, (x + 1) << 9 | (any_slowlate ? 1u << 8 : 0u) | nl, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
     if (stats) *stats += __builtin_amdgcn_s_memtime() - tp;
     return true;
 }
 
-// Resolver: chunk x from its staged slot.  False on abort.
-__device__ __forceinline__ bool ls_resolve(LsShared &S, uint32_t n, uint32_t x, const uint32_t *__restrict__ pred_off,
-                                           const uint32_t *__restrict__ preds, uint32_t *level, uint32_t lane,
-                                           uint32_t &mymax)
+// Resolver: chunk x from its staged slot.  (Prefetching the next chunk's closure into a second
+// register set measured slower: the compiler's register shuffles between the two sets drain the
+// prefetch loads.)  The poll reads the flag and the slot's small fields together (LDS ops of a wave
+// run in order: fields read after a flag that shows the chunk are the staged ones).  False on abort.
+// lv_matvec over the resolver's int4 register image of the late columns
+__device__ __forceinline__ int32_t ls_matvec(int32_t acc, const int4 (&d)[16], uint32_t bv, uint32_t hi)
+{
+    int32_t acc2 = acc;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        if ((uint32_t)(8 * g) < hi) {                 // wave-uniform
+            const int4 p = d[2 * g], q = d[2 * g + 1];
+            const int m = 8 * g;
+            const int32_t s0 = (int32_t)readlane(bv, m), s1 = (int32_t)readlane(bv, m + 1);
+            const int32_t s2 = (int32_t)readlane(bv, m + 2), s3 = (int32_t)readlane(bv, m + 3);
+            acc = max(acc, max(s0 + p.x, s1 + p.y));
+            acc2 = max(acc2, max(s2 + p.z, s3 + p.w));
+            const int32_t s4 = (int32_t)readlane(bv, m + 4), s5 = (int32_t)readlane(bv, m + 5);
+            const int32_t s6 = (int32_t)readlane(bv, m + 6), s7 = (int32_t)readlane(bv, m + 7);
+            acc = max(acc, max(s4 + q.x, s5 + q.y));
+            acc2 = max(acc2, max(s6 + q.z, s7 + q.w));
+        }
+    }
+    return max(acc, acc2);
+}
+
+__device__ __forceinline__ bool ls_resolve(LsShared &S, uint32_t n, uint32_t nchunks, uint32_t x,
+                                           const uint32_t *__restrict__ pred_off, const uint32_t *__restrict__ preds,
+                                           uint32_t *level, uint32_t lane, uint32_t &mymax, unsigned long long *tmid)
 {
     const uint32_t base = x * LC;
     LsSlot &sl = S.slot[x % LS_K];
-    if (!ls_wait_ready(&sl.ready, &S.abort_flag, x + 1)) return false;
-    const uint32_t hdr = __builtin_amdgcn_readfirstlane(sl.hdr);
-    const uint32_t nl = hdr & 0xFFu;
-    int32_t d[64];
+    uint32_t hdr, spins = 0;
+    int32_t acc_e;
+    uint32_t bv_e, lw[LS_LREF / 2];
+    for (;;) {
+        hdr = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&sl.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        asm volatile("" ::: "memory");
+        acc_e = sl.acc_e[lane];
+        bv_e = sl.bv_e[lane];
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {                    // unconditional: columns past nl are not used
-        const int4 v = sl.d[g][lane];
-        d[4 * g] = v.x; d[4 * g + 1] = v.y; d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+        for (int s = 0; s < LS_LREF / 2; ++s) lw[s] = sl.lref[s][lane];
+        if ((hdr >> 9) == x + 1) break;
+        if ((++spins & 255u) == 0) {
+            if (__builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(&S.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                return false;
+            if (spins > (1u << 26)) {
+                __hip_atomic_store(&S.abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return false;
+            }
+        }
     }
-    const int32_t acc_e = sl.acc_e[lane];
-    const uint32_t bv_e = sl.bv_e[lane];
-    uint32_t lw[LS_LREF / 2];
-#pragma unroll
-    for (int s = 0; s < LS_LREF / 2; ++s) lw[s] = sl.lref[s][lane];
+    const uint32_t nl = hdr & 0xFFu;
     uint32_t rv[LS_LREF];
 #pragma unroll
     for (int s = 0; s < LS_LREF; ++s) rv[s] = S.ring[(lw[s >> 1] >> (16 * (s & 1))) & 0xFFFFu];
+    int4 d[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) d[g] = sl.d[g][lane];   // unconditional: columns past nl are not used
     uint32_t lat = max(max(max(rv[0], rv[1]), max(rv[2], rv[3])), max(max(rv[4], rv[5]), max(rv[6], rv[7])));
-    if (hdr >> 16) {                                  // a late column with more than LS_LREF: its full list
+    if ((hdr >> 8) & 1u) {                            // a late column with more than LS_LREF: its full list
         const uint32_t t = base + sl.node[lane];
         if (lane < nl && t < n) {
             for (uint32_t q = pred_off[t], q1 = pred_off[t + 1]; q < q1; ++q) {
@@ -651,12 +690,12 @@ __device__ __forceinline__ bool ls_resolve(LsShared &S, uint32_t n, uint32_t x, 
         }
     }
     const uint32_t bv = max(bv_e, lat + 1u);
-    const int32_t acc = lv_matvec(acc_e, d, bv, 0, nl);
+    if (tmid) *tmid = __builtin_amdgcn_s_memtime();
+    const int32_t acc = ls_matvec(acc_e, d, bv, nl);
     const uint32_t t = base + lane;
-    if (t < n) {
+    if (t < n) {                                      // level[] is written from the ring by a helper
         const uint32_t v = (uint32_t)acc - 1u;
         S.ring[t % LV_RING] = v;
-        level[t] = v - 1u;
         mymax = max(mymax, v - 1u);
     }
     // same wave, in-order LDS: the ring entries land before the count
@@ -673,50 +712,59 @@ __global__ __launch_bounds__((LS_HELPERS + 1) * 64) void lv_staged_kernel(uint32
                                                                         const uint32_t *__restrict__ pred_off,
                                                                         const uint32_t *__restrict__ preds,
                                                                         uint32_t *level, uint32_t *__restrict__ info,
-                                                                        unsigned long long *dbg)
+                                                                        unsigned long long *dbg, uint32_t solo)
 {
     __shared__ LsShared S;
     const uint32_t w = wave_id(), lane = lane_id();
     if (threadIdx.x == 0) { S.done = 0; S.abort_flag = 0; S.maxlv = 0; S.ring[LS_ZERO] = 0; }
-    if (threadIdx.x < LS_K) S.slot[threadIdx.x].ready = 0;
+    if (threadIdx.x < LS_K) { S.slot[threadIdx.x].ready = 0; S.slot[threadIdx.x].dready = 0; }
     __syncthreads();
     uint32_t mymax = 0;
     if (w == 0) {
         __builtin_amdgcn_s_setprio(3);
-        unsigned long long tw = 0, tc = 0, ns = 0;
+        unsigned long long tw = 0, tc = 0, ns = 0, tg = 0, tm = 0;
         for (uint32_t x = 0; x < nchunks; ++x) {
             unsigned long long t0 = 0, t1 = 0;
             if (DBG) {
                 t0 = __builtin_amdgcn_s_memtime();
-                if (!ls_wait_ready(&S.slot[x % LS_K].ready, &S.abort_flag, x + 1)) break;
+                if (!ls_spin<false, false>(&S.slot[x % LS_K].ready, &S.abort_flag, (x + 1) << 9)) break;
                 t1 = __builtin_amdgcn_s_memtime();
             }
-            if (!ls_resolve(S, n, x, pred_off, preds, level, lane, mymax)) break;
+            if (!ls_resolve(S, n, nchunks, x, pred_off, preds, level, lane, mymax, DBG ? &tm : nullptr)) break;
             if (DBG) {
                 const unsigned long long t2 = __builtin_amdgcn_s_memtime();
                 tw += t1 - t0; tc += t2 - t1; ns += (t1 - t0 > 100) ? 1 : 0;
+                tg += tm - t1;
             }
         }
-        if (DBG && lane == 0) { dbg[0] = tw; dbg[1] = tc; dbg[2] = ns; }
-    } else {
+        if (DBG && lane == 0) { dbg[0] = tw; dbg[1] = tc; dbg[2] = ns; dbg[5] = tg; }
+    } else if (!(solo && w == 4)) {
+        // solo: wave 4 (the resolver's SIMD, waves being placed round-robin) stays idle
         LvRec ra, rb;
-        const uint32_t h = w - 1;
+        const uint32_t H = solo ? LS_HELPERS - 1 : LS_HELPERS;
+        const uint32_t h = w - 1 - (solo && w > 4 ? 1u : 0u);
         unsigned long long tp = 0, *st = DBG ? &tp : nullptr;
         uint32_t cnt = 0;
         lv_load(rec, h, nchunks, lane, ra);
-        for (uint32_t x = h; x < nchunks; x += 2 * LS_HELPERS) {
-            lv_load(rec, x + LS_HELPERS, nchunks, lane, rb);      // the next record, in flight meanwhile
+        for (uint32_t x = h; x < nchunks; x += 2 * H) {
+            lv_load(rec, x + H, nchunks, lane, rb);      // the next record, in flight meanwhile
             if (!ls_stage(S, n, x, ra, pred_off, preds, level, lane, st)) break;
             ++cnt;
-            if (x + LS_HELPERS >= nchunks) break;
-            lv_load(rec, x + 2 * LS_HELPERS, nchunks, lane, ra);
-            if (!ls_stage(S, n, x + LS_HELPERS, rb, pred_off, preds, level, lane, st)) break;
+            if (x + H >= nchunks) break;
+            lv_load(rec, x + 2 * H, nchunks, lane, ra);
+            if (!ls_stage(S, n, x + H, rb, pred_off, preds, level, lane, st)) break;
             ++cnt;
         }
         if (DBG && lane == 0) { atomicAdd(&dbg[3], tp); atomicAdd(&dbg[4], (unsigned long long)cnt); }
     }
     atomicMax(&S.maxlv, mymax);
     __syncthreads();
+    // the chunks no helper stage copied (the last three)
+    const uint32_t c0 = nchunks > 3 ? nchunks - 3 : 0u;
+    if (!S.abort_flag && c0 + w < nchunks) {
+        const uint32_t c = (c0 + w) * LC + lane;
+        if (c < n) level[c] = S.ring[c % LV_RING] - 1u;
+    }
     if (threadIdx.x == 0) {
         if (S.abort_flag) info[0] = 1 + S.done;
         info[1] = S.maxlv;
@@ -784,12 +832,14 @@ void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, 
     const char *sts = getenv("ACCORD_LV_STATS");
     unsigned long long *sdbg = nullptr;
     if (staged && sts && sts[0] == '1' && hipMalloc(&sdbg, 64) == hipSuccess) (void)hipMemsetAsync(sdbg, 0, 64, s);
-    if (staged && sdbg)
-        hipLaunchKernelGGL(lv_staged_kernel<true>, dim3(1), dim3((LS_HELPERS + 1) * 64), 0, s, n, nchunks, rec,
-                           pred_off, preds, level, info, sdbg);
-    else if (staged)
-        hipLaunchKernelGGL(lv_staged_kernel<false>, dim3(1), dim3((LS_HELPERS + 1) * 64), 0, s, n, nchunks, rec,
-                           pred_off, preds, level, info, (unsigned long long *)nullptr);
+    auto kern = sdbg ? lv_staged_kernel<true> : lv_staged_kernel<false>;
+    // the resolver alone on its SIMD (wave 4, which round-robin placement puts there, idles): 48.3 ->
+    // 44.7 ms on config 5 (profiles/r04_b/levels_staged_ab.txt); ACCORD_LV_SOLO=0 puts a helper there
+    const char *so = getenv("ACCORD_LV_SOLO");
+    const uint32_t solo = so && so[0] == '0' ? 0u : 1u;
+    if (staged)
+        hipLaunchKernelGGL(kern, dim3(1), dim3((LS_HELPERS + 1) * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
+                           info, sdbg, solo);
     else
         hipLaunchKernelGGL(lv_resolve_kernel<8>, dim3(1), dim3(8 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
                            info, dbg);
@@ -797,8 +847,9 @@ void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, 
         unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyAsync(h, sdbg, 64, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess)
             fprintf(stderr, "lv_staged: chunks %u resolver wait %.1f compute %.1f cycles/chunk, waited on %llu chunks; "
-                    "helper stage-after-final %.1f cycles/chunk (%llu)\n", nchunks, (double)h[0] / nchunks,
-                    (double)h[1] / nchunks, h[2], h[4] ? (double)h[3] / h[4] : 0.0, h[4]);
+                    "helper stage-after-final %.1f cycles/chunk (%llu); resolver slot+gather %.1f\n", nchunks,
+                    (double)h[0] / nchunks, (double)h[1] / nchunks, h[2], h[4] ? (double)h[3] / h[4] : 0.0, h[4],
+                    (double)h[5] / nchunks);
         (void)hipFree(sdbg);
     }
     if (dbg) {
