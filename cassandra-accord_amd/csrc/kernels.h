@@ -169,6 +169,7 @@ void launch_keydeps_sizes(uint32_t n, const uint32_t *key_off, const PairSlice *
 // fill = fast kernel over every txn (k <= 8, <= 256 candidates, deps in the near span) + the general
 // kernel over the txns it hands back (p.fb_list / p.fb_count, count zeroed before the launch)
 size_t keydeps_fast_temp_bytes(uint32_t n);
+void launch_keydeps_recs(const KeyDepsParams &p, void *recs, hipStream_t s);   // before launch_keydeps_fill
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, void *recs, hipStream_t s);
 void launch_keydeps_big(const KeyDepsParams &p, hipStream_t s);
 // vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
@@ -193,6 +194,7 @@ void launch_carry(uint32_t P, uint32_t nkeys, uint32_t thr, const uint32_t *sort
                   hipStream_t s);
 
 // ---- range txns (rangedeps.hip) ----
+constexpr uint32_t RT_HIT_WORDS = 8;   // 16 hits per txn (rangedeps_tile_kernel's RT_HL)
 struct RangeDepsParams {
     uint32_t n;
     const uint64_t *lsb;
@@ -211,6 +213,8 @@ struct RangeDepsParams {
     uint32_t *cnt_vals_exact;           // exact txnIds count per txn (range txns: written by the union pass)
     uint32_t *rd_big_list, *rd_big_count;   // txns with more range hits than the per-txn pass holds
     uint32_t *rd_fb_list, *rd_fb_count;     // txns the tile pass hands to the per-txn pass
+    uint32_t *rt_h, *rt_hits;               // tile pass: per txn its hit count (~0: per-txn pass) and
+                                            //   RT_HIT_WORDS words of 16-bit candidate slots, count -> fill
     const uint32_t *rk_off;             // per range txn: first of its stored key slices
     uint2 *rk_slices;                   // (lo, raw | wcnt << 16) per key of every range txn's ranges
     uint32_t n_range_txns;

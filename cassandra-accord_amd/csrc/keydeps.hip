@@ -1486,9 +1486,6 @@ __global__ __launch_bounds__(256) void keydeps_tiny_kernel(KeyDepsParams p)
 void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_t s)
 {
     if (p.n == 0) return;
-    uint32_t rb = (p.n + 255) / 256;
-    if (rb > 4096) rb = 4096;
-    hipLaunchKernelGGL(txnrec_kernel, dim3(rb), dim3(256), 0, s, p, (TxnRec *)recs);
     uint32_t blocks = (p.n + KD_WAVES - 1) / KD_WAVES;
     uint32_t cap = 256u * 16u;
     if (const char *e = getenv("ACCORD_FK_BLOCKS")) cap = (uint32_t)atoi(e);   // dev aid (A/B of the grid)
@@ -1819,10 +1816,20 @@ void launch_keydeps_big(const KeyDepsParams &p, hipStream_t s)
     hipLaunchKernelGGL(keydeps_big_kernel, dim3(512), dim3(BK_THREADS), 0, s, p);
 }
 
+// The fast fill's per-txn records (offsets and kind only): launched before the host reads the
+// output sizes, so it runs during that wait instead of after it.
+void launch_keydeps_recs(const KeyDepsParams &p, void *recs, hipStream_t s)
+{
+    if (p.n == 0 || p.window > 512u) return;
+    uint32_t rb = (p.n + 255) / 256;
+    if (rb > 4096) rb = 4096;
+    hipLaunchKernelGGL(txnrec_kernel, dim3(rb), dim3(256), 0, s, p, (TxnRec *)recs);
+}
+
 void launch_keydeps_fill(const KeyDepsParams &p, int wpl, void *recs, hipStream_t s)
 {
-    // fast path over every txn; the general kernel over the fallback list (fb_count zeroed by the
-    // caller).  Windows past 512 txns put most txns over the fast path's 256 candidates: general only.
+    // fast path over every txn (its records from launch_keydeps_recs); the general kernel over the
+    // fallback list (fb_count zeroed by the caller).  Windows past 512 txns put most txns over the fast path's 256 candidates: general only.
     if (p.window > 512u) {
         KeyDepsParams q = p;
         q.fb_list = nullptr;

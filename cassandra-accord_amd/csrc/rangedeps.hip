@@ -255,6 +255,7 @@ __global__ __launch_bounds__(RT_WAVES * 64) void rangedeps_tile_kernel(RangeDeps
             if (!FILL && valid) rd_fb_push(p, i);
             continue;
         }
+        static_assert(RT_HL == 2 * RT_HIT_WORDS, "hit words");
         for (uint32_t c = lane; R_lo + c < R_hi; c += 64) {
             const uint32_t r = R_lo + c;
             uint32_t j, s, e, kind;
@@ -270,7 +271,20 @@ __global__ __launch_bounds__(RT_WAVES * 64) void rangedeps_tile_kernel(RangeDeps
         wave_lds_sync();
         bool fb = false;
         uint32_t H = 0;
-        if (valid) {
+        if (FILL && valid && p.rt_h) {
+            // the count pass kept every txn's hits (candidate slots of this same window): no rescan
+            const uint32_t hh = p.rt_h[i];
+            fb = hh == 0xFFFFFFFFu;
+            if (!fb) {
+                H = hh;
+                const uint32_t *src = p.rt_hits + (size_t)i * RT_HIT_WORDS;
+                for (uint32_t h = 0; h < H; h += 2) {
+                    const uint32_t v = src[h >> 1];
+                    L.hit[lane * RT_HL + h] = v & 0xFFFFu;
+                    if (h + 1 < H) L.hit[lane * RT_HL + h + 1] = v >> 16;
+                }
+            }
+        } else if (valid) {
             const uint64_t lsb_i = p.lsb[i];
             const uint32_t wmask = witness_mask((uint32_t)(lsb_i >> 1) & 7);
             const bool key_query = (lsb_i & 1) == 0;
@@ -299,6 +313,14 @@ __global__ __launch_bounds__(RT_WAVES * 64) void rangedeps_tile_kernel(RangeDeps
                 }
             }
             if (H > RT_HL) fb = true;
+            if (!FILL && p.rt_h) {                        // the hits, for the fill pass
+                p.rt_h[i] = fb ? 0xFFFFFFFFu : H;
+                if (!fb) {
+                    const uint32_t *hs = L.hit + lane * RT_HL;
+                    uint32_t *dst = p.rt_hits + (size_t)i * RT_HIT_WORDS;
+                    for (uint32_t h = 0; h < H; h += 2) dst[h >> 1] = hs[h] | (h + 1 < H ? hs[h + 1] << 16 : 0u);
+                }
+            }
         }
         if (fb) {
             if (!FILL) rd_fb_push(p, i);

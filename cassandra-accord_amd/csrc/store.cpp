@@ -117,7 +117,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->kd_keys, &s->kd_vals, &s->kd_k2v, &s->rd_zero_off,
                       &s->rng_owner, &s->is_range, &s->rt_excl, &s->range_txns, &s->cnt_rngs, &s->cnt_rvals,
                       &s->cnt_r2v, &s->rd_rng_off, &s->rd_val_off, &s->rd_r2v_off, &s->rd_rng_start, &s->rd_rng_end,
-                      &s->rd_vals, &s->rd_r2v, &s->rd_big, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->rk_cls, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
+                      &s->rd_vals, &s->rd_r2v, &s->rd_big, &s->rt_hits, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->rk_cls, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->wo_aoi, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
@@ -374,6 +374,7 @@ int32_t accord_deps_compute(accord_store *s)
     const uint32_t ncr = s->resident ? s->rc_n : 0u;
     const bool rdeps = R || ncr;
     if (rdeps) HIPCHECK(s, s->rd_big.ensure(((size_t)2 * n + 64) * 4));   // big list | tile fallback list
+    if (rdeps) HIPCHECK(s, s->rt_hits.ensure((size_t)n * (1 + accord::RT_HIT_WORDS) * 4 + 64));
 
     HostTotals *dev = s->status_totals.as<HostTotals>();
     record(s, EV_START);
@@ -536,6 +537,9 @@ int32_t accord_deps_compute(accord_store *s)
         rp.rd_big_count = s->rd_big.as<uint32_t>();
         rp.rd_big_list = rp.rd_big_count + 16;
         rp.rd_fb_count = rp.rd_big_count + 32 + n;
+        const char *ru = getenv("ACCORD_RT_REUSE");                 // A/B: 0 = the fill pass rescans
+        rp.rt_h = ru && ru[0] == '0' ? nullptr : s->rt_hits.as<uint32_t>();
+        rp.rt_hits = s->rt_hits.as<uint32_t>() + n;
         rp.rd_fb_list = rp.rd_fb_count + 16;
         accord::launch_rangedeps_count(rp, st);
     }
@@ -553,6 +557,14 @@ int32_t accord_deps_compute(accord_store *s)
         accord::exclusive_scan_multi(3, in, out, tot, n, s->scan_tmp.p, st);
     }
     record(s, EV_SCAN);
+    // the fast fill's per-txn records need only the offsets: built while the host reads the sizes
+    // (ACCORD_RECS_EARLY=0: after, for A/B)
+    HIPCHECK(s, s->fk_recs.ensure(accord::keydeps_fast_temp_bytes(n)));
+    kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.vub_off = s->vub_off.as<uint32_t>();
+    kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
+    const char *re = getenv("ACCORD_RECS_EARLY");
+    const bool recs_early = !(re && re[0] == '0');
+    if (recs_early) accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
 
@@ -602,7 +614,6 @@ int32_t accord_deps_compute(accord_store *s)
     rp.rd_r2v_off = s->rd_r2v_off.as<uint32_t>();
     rp.rd_rng_start = s->rd_rng_start.as<uint32_t>(); rp.rd_rng_end = s->rd_rng_end.as<uint32_t>();
     rp.rd_vals = s->rd_vals.as<uint32_t>(); rp.rd_r2v = s->rd_r2v.as<int32_t>();
-    HIPCHECK(s, s->fk_recs.ensure(accord::keydeps_fast_temp_bytes(n)));
     kp.fb_count = s->fk_list.as<uint32_t>();
     kp.fb_list = kp.fb_count + 16;
     kp.big_count = s->bk_list.as<uint32_t>();
@@ -622,6 +633,7 @@ int32_t accord_deps_compute(accord_store *s)
         kp.ubits = s->fk_ubits.as<uint16_t>();
         kp.umode = s->fk_umode.as<uint8_t>();
     }
+    if (!recs_early) accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {

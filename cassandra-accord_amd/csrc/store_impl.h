@@ -96,6 +96,7 @@ struct accord_store {
     DevBuf bk_list, bk_wex;        // big txns (keydeps_big_kernel): count | list, per-pair scratch
     DevBuf rng_owner, is_range, rt_excl, range_txns, cnt_rngs, cnt_rvals, cnt_r2v, rd_rng_off, rd_val_off, rd_r2v_off;
     DevBuf rd_rng_start, rd_rng_end, rd_vals, rd_r2v, rd_big, rk_cp, rk_cnt, rk_off, rk_slices, rk_cls;
+    DevBuf rt_hits;                      // RangeDeps tile pass: each txn's hit count and hits, count -> fill
     uint64_t rk_keys_total = 0;      // keys of all range txns' ranges clipped to the store (upload)
     uint32_t n_range_txns = 0;
     uint64_t tot_rngs = 0, tot_rvals = 0, tot_r2v = 0;

@@ -676,9 +676,15 @@ __device__ __forceinline__ bool ls_resolve(LsShared &S, uint32_t n, uint32_t nch
     uint32_t rv[LS_LREF];
 #pragma unroll
     for (int s = 0; s < LS_LREF; ++s) rv[s] = S.ring[(lw[s >> 1] >> (16 * (s & 1))) & 0xFFFFu];
+    // the first 40 columns' closure unconditionally (columns past nl are not used; a uniform branch
+    // per read would make the compiler wait after each), the rest only for the rare wider chunk
     int4 d[16];
 #pragma unroll
-    for (int g = 0; g < 16; ++g) d[g] = sl.d[g][lane];   // unconditional: columns past nl are not used
+    for (int g = 0; g < 10; ++g) d[g] = sl.d[g][lane];
+    if (nl > 40) {                                    // (else d[10..15] stay unset: not read)
+#pragma unroll
+        for (int g = 10; g < 16; ++g) d[g] = sl.d[g][lane];
+    }
     uint32_t lat = max(max(max(rv[0], rv[1]), max(rv[2], rv[3])), max(max(rv[4], rv[5]), max(rv[6], rv[7])));
     if ((hdr >> 8) & 1u) {                            // a late column with more than LS_LREF: its full list
         const uint32_t t = base + sl.node[lane];
