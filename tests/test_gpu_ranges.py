@@ -84,3 +84,18 @@ def test_mixed_kinds_vs_literal(gpu_device, seed, kinds_p):
     got = run_gpu(s2, 64, 400)
     want = O.deps_literal(s2, 64)
     assert got.first_difference(want) is None, got.first_difference(want)
+
+
+@pytest.mark.parametrize("env", [{"ACCORD_RT_REUSE": "1"}, {"ACCORD_RT_REUSE": "0"},
+                                 {"ACCORD_RK_BITMAP": "0"}, {"ACCORD_RK_BITMAP": "1"}],
+                         ids=["hit-reuse", "hit-rescan", "union-sort", "union-bitmap"])
+def test_range_pass_variants_vs_literal(gpu_device, monkeypatch, env):
+    """The RangeDeps fill with the count pass's hits reused or rescanned, and the range txns' union
+    by span bitmap or by sort, all equal to the literal oracle (knobs read per compute)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for seed, W, rl in ((21, 64, 100), (22, 256, 1000), (23, 16, 30)):
+        s = generate_stream(2500, 8, 1500, 0.99, 0.5, range_frac=0.25, range_len_max=rl, seed=seed)
+        got = run_gpu(s, W, 1500)
+        want = O.deps_literal(s, W)
+        assert got.first_difference(want) is None, (env, seed, got.first_difference(want))
