@@ -268,13 +268,14 @@ def main():
     n = s.n
     P = s.pairs
     kc = int(view["kd_keys_total"])
-    U = int(view["kd_vals_total"])
+    # the exact |txnIds| (the device view's txnIds are gapped: kd_vals_total is the array length)
+    dd = store.download()
+    U = int(dd.kd_val_off[-1])
     D = int(view["kd_k2v_total"]) - kc
     fill_sizes = (n, P, kc, U, D)
     if s.rng_off[-1] > 0:
         # the fill stage only builds key txns' KeyDeps (range txns' come from range_fill): size the
         # roofline unit by the key txns alone
-        dd = store.download()
         key_txn = ~s.domains().astype(bool)
         d_keys = np.diff(dd.kd_key_off.astype(np.int64))[key_txn]
         d_vals = np.diff(dd.kd_val_off.astype(np.int64))[key_txn]

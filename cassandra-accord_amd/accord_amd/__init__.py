@@ -116,7 +116,7 @@ class _Deps(C.Structure):
                 ("kd_k2v_off", _u32p), ("kd_k2v", _i32p),
                 ("rd_rng_off", _u32p), ("rd_rng_start", _u32p), ("rd_rng_end", _u32p),
                 ("rd_val_off", _u32p), ("rd_vals", _u32p), ("rd_r2v_off", _u32p), ("rd_r2v", _i32p),
-                ("owner", C.c_void_p)]
+                ("kd_val_cnt", _u32p), ("owner", C.c_void_p)]
 
 
 class _Ready(C.Structure):
@@ -376,6 +376,18 @@ def _arr(ptr, n, dtype):
     return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
 
 
+def _dense_vals(off: np.ndarray, cnt: np.ndarray, vals: np.ndarray):
+    """Gapped txnIds (txn i: vals[off[i] .. off[i] + cnt[i])) -> dense CSR (offsets, values)."""
+    n = cnt.size
+    dense = np.zeros(n + 1, np.int64)
+    np.cumsum(cnt, out=dense[1:])
+    if np.any(off[:-1].astype(np.int64) + cnt > off[1:]):
+        raise ValueError("gapped txnIds: a count runs past the next txn's offset")
+    idx = np.repeat(off[:-1].astype(np.int64) - dense[:-1], cnt.astype(np.int64))
+    idx += np.arange(int(dense[-1]), dtype=np.int64)
+    return dense.astype(np.uint32), vals[idx]
+
+
 def generate_stream(n: int, keys_per_txn: int = 4, keyspace: int = 100_000, zipf_s: float = 0.0,
                     write_frac: float = 0.5, range_frac: float = 0.0, ranges_max: int = 2,
                     range_len_max: int = 1000, node_mod: int = 7, seed: int = 1) -> Stream:
@@ -453,13 +465,19 @@ class PartialDeps:
 
     @staticmethod
     def from_c(d: _Deps) -> "PartialDeps":
+        """From a host accord_deps (accord_deps_download / _batch).  A compute result's txnIds are
+        gapped (kd_val_cnt, include/accord_deps.h): each txn's list is read by (start, count), as
+        KeyDeps.SerializerSupport.create takes it per txn, and the set here is kept dense."""
         n = d.n
         kw = {}
         kw["kd_key_off"] = _arr(d.kd_key_off, n + 1, np.uint32)
-        kw["kd_val_off"] = _arr(d.kd_val_off, n + 1, np.uint32)
         kw["kd_k2v_off"] = _arr(d.kd_k2v_off, n + 1, np.uint32)
         kw["kd_keys"] = _arr(d.kd_keys, int(kw["kd_key_off"][-1]), np.uint32)
-        kw["kd_vals"] = _arr(d.kd_vals, int(kw["kd_val_off"][-1]), np.uint32)
+        voff = _arr(d.kd_val_off, n + 1, np.uint32)
+        vals = _arr(d.kd_vals, int(voff[-1]), np.uint32)
+        if d.kd_val_cnt:
+            voff, vals = _dense_vals(voff, _arr(d.kd_val_cnt, n, np.uint32), vals)
+        kw["kd_val_off"], kw["kd_vals"] = voff, vals
         kw["kd_k2v"] = _arr(d.kd_k2v, int(kw["kd_k2v_off"][-1]), np.int32)
         kw["rd_rng_off"] = _arr(d.rd_rng_off, n + 1, np.uint32)
         kw["rd_val_off"] = _arr(d.rd_val_off, n + 1, np.uint32)
@@ -735,7 +753,7 @@ class CommandStore:
         self._check(lib().accord_deps_device_view(self._h, C.byref(d)))
         out = {"n": d.n, "kd_keys_total": d.kd_keys_total, "kd_vals_total": d.kd_vals_total,
                "kd_k2v_total": d.kd_k2v_total}
-        for f in PartialDeps.FIELDS:
+        for f in PartialDeps.FIELDS + ("kd_val_cnt",):
             out[f] = C.cast(getattr(d, f), C.c_void_p).value or 0
         return out
 

@@ -38,7 +38,7 @@ __device__ __forceinline__ PI part_info(const DsSide &S, uint32_t g, uint32_t t)
     PI p;
     const uint32_t *ko = S.key_off[g], *vo = S.val_off[g], *xo = S.x_off[g];
     p.kb = ko[t] - ko[0]; p.nk = ko[t + 1] - ko[t];
-    p.vb = vo[t] - vo[0]; p.nv = vo[t + 1] - vo[t];
+    p.vb = vo[t] - vo[0]; p.nv = S.val_cnt[g] ? S.val_cnt[g][t] : vo[t + 1] - vo[t];
     p.xb = xo[t] - xo[0]; p.nx = xo[t + 1] - xo[t];
     return p;
 }
@@ -509,11 +509,12 @@ __global__ __launch_bounds__(DS_WAVES * 64) void sl_write_body_kernel(DsSlicePar
 // invert
 // ------------------------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void inv_offsets_kernel(DsInvertParams p)
+// per txn the inverse's size: |txnIds| header + one entry per body element (scanned into out_off)
+__global__ __launch_bounds__(256) void inv_sizes_kernel(DsInvertParams p)
 {
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t <= p.n; t += gridDim.x * blockDim.x) {
-        const uint32_t *ko = p.S.key_off[0], *vo = p.S.val_off[0], *xo = p.S.x_off[0];
-        p.out_off[t] = (vo[t] - vo[0]) + (xo[t] - xo[0]) - (ko[t] - ko[0]);
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < p.n; t += gridDim.x * blockDim.x) {
+        const PI pi = part_info(p.S, 0, t);
+        p.sizes[t] = pi.nv + pi.nx - pi.nk;
     }
 }
 
@@ -620,9 +621,13 @@ void launch_slice_write(const DsSliceParams &p, hipStream_t s)
     hipLaunchKernelGGL(sl_write_body_kernel, dim3(wave_blocks(p.n)), dim3(DS_WAVES * 64), 0, s, p);
 }
 
+void launch_invert_sizes(const DsInvertParams &p, hipStream_t s)
+{
+    if (p.n) hipLaunchKernelGGL(inv_sizes_kernel, dim3(flat_blocks(p.n)), dim3(256), 0, s, p);
+}
+
 void launch_invert(const DsInvertParams &p, hipStream_t s)
 {
-    hipLaunchKernelGGL(inv_offsets_kernel, dim3(flat_blocks((uint64_t)p.n + 1)), dim3(256), 0, s, p);
     if (!p.n) return;
     hipLaunchKernelGGL(inv_count_kernel, dim3(wave_blocks(p.n)), dim3(DS_WAVES * 64), 0, s, p);
     hipLaunchKernelGGL(inv_scan_kernel, dim3(wave_blocks(p.n)), dim3(DS_WAVES * 64), 0, s, p);

@@ -17,25 +17,28 @@ enum Tmp { T_VLEN, T_KLEN, T_BLEN, T_VEOFF, T_KEOFF, T_BEOFF, T_VOWN, T_VLST, T_
 struct SideView {   // one side of one host-described device view
     const uint32_t *key_off, *lo, *hi, *val_off, *vals, *x_off;
     const int32_t *x;
+    const uint32_t *val_cnt;          // gapped txnIds (KeyDeps of a compute result), else nullptr
 };
 
 SideView side_of(const accord_deps &d, bool range)
 {
-    if (!range) return SideView{d.kd_key_off, d.kd_keys, nullptr, d.kd_val_off, d.kd_vals, d.kd_k2v_off, d.kd_k2v};
-    return SideView{d.rd_rng_off, d.rd_rng_start, d.rd_rng_end, d.rd_val_off, d.rd_vals, d.rd_r2v_off, d.rd_r2v};
+    if (!range) return SideView{d.kd_key_off, d.kd_keys, nullptr, d.kd_val_off, d.kd_vals, d.kd_k2v_off, d.kd_k2v,
+                                d.kd_val_cnt};
+    return SideView{d.rd_rng_off, d.rd_rng_start, d.rd_rng_end, d.rd_val_off, d.rd_vals, d.rd_r2v_off, d.rd_r2v, nullptr};
 }
 
 // device pointer table of G views' side -> DsSide
 int32_t make_side(accord_store *s, const std::vector<SideView> &v, bool range, DevBuf &buf, accord::DsSide &S)
 {
     const size_t G = v.size();
-    std::vector<const void *> tbl(7 * G);
+    std::vector<const void *> tbl(8 * G);
     for (size_t g = 0; g < G; ++g) {
         if (!v[g].key_off || !v[g].val_off || !v[g].x_off)
             return fail(s, ACCORD_ERR_ARG, "deps view %zu has no %s offsets", g, range ? "RangeDeps" : "KeyDeps");
         tbl[0 * G + g] = v[g].key_off; tbl[1 * G + g] = v[g].lo; tbl[2 * G + g] = v[g].hi;
         tbl[3 * G + g] = v[g].val_off; tbl[4 * G + g] = v[g].vals; tbl[5 * G + g] = v[g].x_off;
         tbl[6 * G + g] = v[g].x;
+        tbl[7 * G + g] = v[g].val_cnt;
     }
     HIPCHECK(s, buf.ensure(tbl.size() * sizeof(void *)));
     HIPCHECK(s, hipMemcpyAsync(buf.p, tbl.data(), tbl.size() * sizeof(void *), hipMemcpyHostToDevice, s->stream));
@@ -44,6 +47,7 @@ int32_t make_side(accord_store *s, const std::vector<SideView> &v, bool range, D
     S.hi = (const uint32_t *const *)(p + 2 * G); S.val_off = (const uint32_t *const *)(p + 3 * G);
     S.vals = (const uint32_t *const *)(p + 4 * G); S.x_off = (const uint32_t *const *)(p + 5 * G);
     S.x = (const int32_t *const *)(p + 6 * G);
+    S.val_cnt = (const uint32_t *const *)(p + 7 * G);
     S.G = (uint32_t)G;
     S.range = range;
     return ACCORD_OK;
@@ -183,6 +187,19 @@ int32_t union_side(accord_store *s, const accord_deps *parts, uint32_t G, bool r
 // arrays copied into o in one launch instead of the union's passes and host reads
 int32_t copy_side(accord_store *s, const accord_deps &src, bool range, DepSet &o)
 {
+    if (!range && src.kd_val_cnt) {        // gapped txnIds (a compute result): the dense form, then copy it
+        if (src.kd_val_off != s->vub_off.as<uint32_t>())
+            return fail(s, ACCORD_ERR_ARG, "copy of a gapped deps view of another store");
+        RC(accord_impl::store_dense_keydeps(s));
+        HIPCHECK(s, hipMemcpyAsync(s->pinned->totals, &s->status_totals.as<HostTotals>()->totals[7], 8,
+                                   hipMemcpyDeviceToHost, s->stream));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+        accord_deps d = src;
+        d.kd_val_off = s->kd_val_off.as<uint32_t>(); d.kd_vals = s->kd_vals.as<uint32_t>();
+        d.kd_val_cnt = nullptr;
+        d.kd_vals_total = s->pinned->totals[0];
+        return copy_side(s, d, range, o);
+    }
     const size_t n1 = (size_t)src.n + 1;
     const uint64_t K = range ? src.rd_rngs_total : src.kd_keys_total, V = range ? src.rd_vals_total : src.kd_vals_total;
     const uint64_t X = range ? src.rd_r2v_total : src.kd_k2v_total;
@@ -402,7 +419,8 @@ CurDeps cur_deps(const accord_store *s)
         c.tot_rngs = x.tot_rngs; c.tot_r2v = x.tot_r;
     } else {
         c.kd_key_off = s->kd_key_off.as<uint32_t>(); c.kd_keys = s->kd_keys.as<uint32_t>();
-        c.kd_val_off = s->kd_val_off.as<uint32_t>(); c.kd_vals = s->kd_vals.as<uint32_t>();
+        c.kd_val_off = s->vub_off.as<uint32_t>(); c.kd_vals = s->vgap.as<uint32_t>();   // gapped
+        c.kd_val_cnt = s->cnt_vals.as<uint32_t>();
         c.kd_k2v_off = s->kd_k2v_off.as<uint32_t>(); c.kd_k2v = s->kd_k2v.as<uint32_t>();
         c.rd_val_off = s->rd_val_off.as<uint32_t>(); c.rd_vals = s->rd_vals.as<uint32_t>();
         c.rd_rng_off = s->rd_rng_off.as<uint32_t>(); c.rd_rng_start = s->rd_rng_start.as<uint32_t>();
@@ -559,20 +577,27 @@ int32_t accord_deps_invert(accord_store *s, const accord_deps *src, accord_deps_
     int32_t rc = ACCORD_OK;
     for (int side = 0; side < 2 && rc == ACCORD_OK; ++side) {
         const bool range = side == 1;
-        const uint64_t total = range ? src->rd_vals_total + src->rd_r2v_total - src->rd_rngs_total
-                                     : src->kd_vals_total + src->kd_k2v_total - src->kd_keys_total;
-        const uint64_t V = range ? src->rd_vals_total : src->kd_vals_total;
+        const uint64_t V = range ? src->rd_vals_total : src->kd_vals_total;   // (gapped: the array length)
         accord::DsInvertParams p{};
         p.n = n;
         std::vector<SideView> v{side_of(*src, range)};
         if ((rc = make_side(s, v, range, s->op_tmp[T_PTRS], p.S))) break;
         DevBuf *T = s->op_tmp;
         hipError_t e = T[T_VLEN].ensure(((size_t)n + 1) * 4);
-        if (e == hipSuccess) e = T[T_RB].ensure(total * 4 + 4);
+        if (e == hipSuccess) e = T[T_KLEN].ensure(((size_t)n + 1) * 4);
+        if (e != hipSuccess) { rc = fail(s, ACCORD_ERR_HIP, "invert: %s", hipGetErrorString(e)); break; }
+        // per txn |txnIds| + body, scanned: the inverse's offsets and its exact size
+        p.sizes = T[T_KLEN].as<uint32_t>(); p.out_off = T[T_VLEN].as<uint32_t>();
+        accord::launch_invert_sizes(p, s->stream);
+        Scans sc;
+        unsigned long long tot[1] = {0};
+        if ((rc = scans_init(s, sc)) || (rc = sc.add(p.sizes, p.out_off, n)) || (rc = sc.read(tot))) break;
+        const uint64_t total = tot[0];
+        e = T[T_RB].ensure(total * 4 + 4);
         if (e == hipSuccess) e = T[T_VRANK].ensure(V * 4 + 4);
         if (e == hipSuccess) e = hipMemsetAsync(T[T_RB].p, 0, total * 4 + 4, s->stream);
         if (e != hipSuccess) { rc = fail(s, ACCORD_ERR_HIP, "invert: %s", hipGetErrorString(e)); break; }
-        p.out_off = T[T_VLEN].as<uint32_t>(); p.out = T[T_RB].as<int32_t>(); p.cursor = T[T_VRANK].as<uint32_t>();
+        p.out = T[T_RB].as<int32_t>(); p.cursor = T[T_VRANK].as<uint32_t>();
         accord::launch_invert(p, s->stream);
         std::vector<uint32_t> &ho = range ? own->roff : own->koff;
         std::vector<int32_t> &hv = range ? own->r : own->k;
@@ -606,6 +631,22 @@ int32_t accord_deps_upload(accord_store *s, const accord_deps *h)
         if (offs[a][0] != 0 || offs[a][n] != tots[a]) return fail(s, ACCORD_ERR_ARG, "accord_deps_upload: offsets/totals mismatch");
         for (uint32_t t = 0; t < n; ++t)
             if (offs[a][t + 1] < offs[a][t]) return fail(s, ACCORD_ERR_ARG, "accord_deps_upload: offsets decrease at txn %u", t);
+    }
+    // gapped txnIds (a downloaded compute result): made dense on the host, then uploaded
+    std::vector<uint32_t> dv_off, dv;
+    accord_deps hd = *h;
+    if (h->kd_val_cnt) {
+        dv_off.assign(n1, 0);
+        for (uint32_t t = 0; t < n; ++t) {
+            if ((uint64_t)h->kd_val_off[t] + h->kd_val_cnt[t] > h->kd_val_off[t + 1])
+                return fail(s, ACCORD_ERR_ARG, "accord_deps_upload: txnIds count past the next offset at txn %u", t);
+            dv_off[t + 1] = dv_off[t] + h->kd_val_cnt[t];
+        }
+        dv.resize(dv_off[n]);
+        for (uint32_t t = 0; t < n; ++t)
+            std::memcpy(dv.data() + dv_off[t], h->kd_vals + h->kd_val_off[t], (size_t)h->kd_val_cnt[t] * 4);
+        hd.kd_val_off = dv_off.data(); hd.kd_vals = dv.data(); hd.kd_vals_total = dv_off[n]; hd.kd_val_cnt = nullptr;
+        h = &hd;
     }
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     DepSet &o = next_set(s);

@@ -87,15 +87,19 @@ __host__ __device__ __forceinline__ uint32_t witness_mask(uint32_t kind)
     return (uint32_t)(T >> ((kind & 7u) * 8u)) & 0xFFu;
 }
 
+// Timestamp.compareTo (primitives/Timestamp.java:209-217): unsigned msb, then the low hlc, then the
+// identity flags, then the signed node.  Branch-free: every field is compared and the first
+// difference selected, so the result is a value, not a control-flow join (a branchy form fed into a
+// running max was miscompiled on gfx950: profiles/r05_eal).
 __device__ __forceinline__ int ts_cmp(uint64_t am, uint64_t al, int32_t an, uint64_t bm, uint64_t bl, int32_t bn)
 {
-    if (am != bm) return am < bm ? -1 : 1;
-    uint64_t ah = al >> 16, bh = bl >> 16;
-    if (ah != bh) return ah < bh ? -1 : 1;
-    uint64_t af = al & 0x1Eull, bf = bl & 0x1Eull;
-    if (af != bf) return af < bf ? -1 : 1;
-    if (an != bn) return an < bn ? -1 : 1;
-    return 0;
+    const uint64_t ah = al >> 16, bh = bl >> 16;
+    const uint32_t af = (uint32_t)al & 0x1Eu, bf = (uint32_t)bl & 0x1Eu;
+    const int c0 = (int)(am > bm) - (int)(am < bm);
+    const int c1 = (int)(ah > bh) - (int)(ah < bh);
+    const int c2 = (int)(af > bf) - (int)(af < bf);
+    const int c3 = (int)(an > bn) - (int)(an < bn);
+    return c0 ? c0 : c1 ? c1 : c2 ? c2 : c3;
 }
 
 // History entry: txn index in the low 29 bits, entry kind in the top 3 bits.

@@ -117,12 +117,6 @@ struct KeyDepsParams {
     // far list): listed by the general kernel, built by a workgroup each (big_wex: scratch per pair)
     uint32_t *big_list, *big_count, *big_wex;
     uint32_t tiny;                     // thread-per-txn pass for tiny txns (batches of few keys per txn)
-    // union records (emit mode, nullptr = off): the fast kernel leaves a txn's near union as its
-    // near-map bits, 16 per lane (ubits[t*64 + lane]), instead of scattering its near txnIds into
-    // vgap, and umode[t] = far deps + 1 (0: the txn's txnIds are in vgap, written by another kernel);
-    // launch_emit_vals then writes every txn's txnIds once at its exact offset
-    uint16_t *ubits;
-    uint8_t *umode;
 };
 
 // Where a batch sits in the store's stream: global positions start at min_gi, and (has_prev) the
@@ -172,12 +166,9 @@ size_t keydeps_fast_temp_bytes(uint32_t n);
 void launch_keydeps_recs(const KeyDepsParams &p, void *recs, hipStream_t s);   // before launch_keydeps_fill
 void launch_keydeps_fill(const KeyDepsParams &p, int span_words_per_lane, void *recs, hipStream_t s);
 void launch_keydeps_big(const KeyDepsParams &p, hipStream_t s);
-// vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries)
+// vals[val_off[i] ..] = vgap[vub_off[i] ..] (val_off[i+1] - val_off[i] entries): the dense form of a
+// gapped KeyDeps txnIds array, for the operations that ship or copy it (store_dense_keydeps)
 size_t compact_temp_bytes(uint64_t max_total);
-// txnIds at exact offsets from the fast kernel's union records (umode[t] > 0) or the gapped vgap
-// lists (umode[t] == 0): a wave per txn
-void launch_emit_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
-                      const uint16_t *ubits, const uint8_t *umode, const void *recs, uint32_t *vals, hipStream_t s);
 void launch_compact_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
                          uint32_t *vals, uint64_t max_total, void *temp, hipStream_t s);
 
@@ -272,6 +263,7 @@ struct MergeParams {
     const uint32_t *const *key_off;
     const uint32_t *const *keys;
     const uint32_t *const *val_off;
+    const uint32_t *const *val_cnt;   // per part: gapped txnIds' counts, or nullptr (dense)
     const uint32_t *const *vals;
     const uint32_t *const *k2v_off;
     const int32_t *const *k2v;
@@ -331,6 +323,7 @@ void launch_ri_stab(const RangeIndexParams &p, bool fill, hipStream_t s);
 // data array is at index off[t] - off[0]).
 struct DsSide {
     const uint32_t *const *key_off, *const *lo, *const *hi, *const *val_off, *const *vals, *const *x_off;
+    const uint32_t *const *val_cnt;   // per part: gapped txnIds' counts, or nullptr (dense)
     const int32_t *const *x;
     uint32_t G;
     bool range;
@@ -361,7 +354,8 @@ struct DsSliceParams {
 struct DsInvertParams {
     uint32_t n;
     DsSide S;                                       // G = 1
-    uint32_t *out_off;                              // [n+1]
+    uint32_t *sizes;                                // [n] per txn (launch_invert_sizes)
+    uint32_t *out_off;                              // [n+1] = exclusive scan of sizes
     int32_t *out;                                   // zeroed before the launch
     uint32_t *cursor;                               // per txnId element
 };
@@ -374,6 +368,7 @@ void launch_union_write(const DsUnionParams &p, hipStream_t s);
 // slice: select + mark (used zeroed) + counts -> (scans) -> write
 void launch_slice_select(const DsSliceParams &p, hipStream_t s);
 void launch_slice_write(const DsSliceParams &p, hipStream_t s);
+void launch_invert_sizes(const DsInvertParams &p, hipStream_t s);
 void launch_invert(const DsInvertParams &p, hipStream_t s);
 
 // ---- WaitingOn bitsets + execution levelling (waiting_on.hip) ----
@@ -385,6 +380,7 @@ struct WaitingOnParams {
     const uint32_t *hist, *pw_local, *pw_carry;
     uint32_t pw_tile;
     const uint32_t *kd_val_off, *kd_vals;          // full KeyDeps (non-reduced txns)
+    const uint32_t *kd_val_cnt;                    // gapped txnIds: per-txn count (nullptr: dense)
     const uint32_t *rd_val_off, *rd_vals;          // RangeDeps txnIds
     uint32_t *pred_cnt;
     const uint32_t *pred_off;

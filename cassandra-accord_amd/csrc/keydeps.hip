@@ -1072,8 +1072,6 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     // XCD's L2 instead of being fetched into all eight
     const uint32_t xg = blockIdx.x & 7u, B = gridDim.x >> 3;
     const uint32_t n = (uint32_t)(((uint64_t)p.n * (xg + 1)) >> 3), S = B * KD_WAVES;
-    // emit mode (16 map bits per lane only): near txnIds leave as union records, not vgap scatters
-    const bool emit = BPL == 16 && p.ubits != nullptr;
     uint32_t t = (uint32_t)(((uint64_t)p.n * xg) >> 3) + (blockIdx.x >> 3) * KD_WAVES + w;
 
     // software pipeline: records three txns ahead, slices two ahead, candidates one ahead
@@ -1105,10 +1103,8 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             const uint32_t k = readlane(a.rec, 1);
             if (k == 0) {                             // range txn / no key in this store
                 if (lane == 0) stg(p.cnt_vals, t, 0u);
-                if (emit && lane == 0) p.umode[t] = 0;
                 break;
             }
-            if (emit && lane == 0) p.umode[t] = 0;    // unless this kernel completes the txn (below)
             if (p.tiny && tn_take(k, rta)) break;     // a tiny txn: keydeps_tiny_kernel builds it
             bool fallback = k > 8 || rta > FK_RAW;
             const uint32_t kind = readlane(a.rec, 2), gi = readlane(a.rec, 3);
@@ -1174,10 +1170,6 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             const uint32_t incl = wave_incl_scan(pc);
             const uint32_t pre = incl - pc + far_u;
             if (lane == 0) stg(p.cnt_vals, t, readlane(incl, 63) + far_u);
-            if (emit) {                               // the union record (one 128-byte store)
-                stg(p.ubits, t * 64u + lane, (uint16_t)bits);
-                if (lane == 0) p.umode[t] = (uint8_t)(far_u + 1u);
-            }
             FK_STAMP(3);                              // union
             // keys and keysToTxnIds header from the witnessed counts
             const uint32_t key_base = readlane(a.rec, 4), val_base = readlane(a.rec, 5), k2v_base = readlane(a.rec, 6);
@@ -1217,7 +1209,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 const uint64_t wb = __ballot(wit);
                 if (wit) {
                     stg(p.kd_k2v, k2v_base + kc + run + (uint32_t)__popcll(wb & lt), (int32_t)rank);
-                    if (nr && !emit) stg(p.vgap, val_base + rank, j);  // every holder of j writes the same word
+                    if (nr) stg(p.vgap, val_base + rank, j);           // every holder of j writes the same word
                 }
                 run += (uint32_t)__popcll(wb);
             }
@@ -1596,98 +1588,7 @@ __global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uin
     }
 }
 
-// txnIds at their exact offsets (emit mode), a wave per txn.  A txn the fast kernel built
-// (umode[t] = far deps + 1) left its far deps in vgap at ranks [0, far) and its near union as 16
-// map bits per lane: lane L's bit b is txn bound - SPAN + 16 L + b, ranked after the far deps and
-// the set bits of lanes < L.  Output rank r >= far: the owner lane (largest L with pre_L <= r, by
-// six lane permutes) and the (r - pre_L)-th set bit of its word.  Other txns (umode 0: general /
-// tiny / big kernels, range txns) are copied from their gapped vgap list.  A lane writes 4
-// consecutive outputs of the quad-aligned grid (16-byte stores inside the txn's run, dword stores
-// on its edges, which it shares with the neighbouring txns).
-constexpr uint32_t EM_SPAN = 1024;   // 64 lanes x 16 bits: keydeps_fast_kernel<16>
-
-__device__ __forceinline__ uint32_t em_select16(uint32_t w, uint32_t k)   // k-th set bit of w (k < popc(w))
-{
-    uint32_t b = 0;
-    uint32_t c = (uint32_t)__popc(w & 0xFFu);
-    if (k >= c) { k -= c; b += 8; w >>= 8; }
-    c = (uint32_t)__popc(w & 0xFu);
-    if (k >= c) { k -= c; b += 4; w >>= 4; }
-    c = (uint32_t)__popc(w & 0x3u);
-    if (k >= c) { k -= c; b += 2; w >>= 2; }
-    c = w & 1u;
-    if (k >= c) b += 1;
-    return b;
-}
-
-__global__ __launch_bounds__(256) void emit_vals_kernel(uint32_t n, const uint32_t *__restrict__ vub_off,
-                                                        const uint32_t *__restrict__ val_off,
-                                                        const uint32_t *__restrict__ vgap,
-                                                        const uint16_t *__restrict__ ubits,
-                                                        const uint8_t *__restrict__ umode,
-                                                        const TxnRec *__restrict__ recs,
-                                                        uint32_t *__restrict__ vals)
-{
-    const uint32_t lane = lane_id();
-    const uint32_t W = gridDim.x * (blockDim.x / 64);
-    for (uint32_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / 64) + wave_id()); t < n; t += W) {
-        const uint32_t a = val_off[t], e = val_off[t + 1];
-        if (a == e) continue;                                    // wave-uniform
-        const uint32_t src = vub_off[t];
-        const uint32_t mode = umode ? umode[t] : 0u;
-        uint32_t word = 0, far = 0, jbase = 0;
-        if (mode) {                                              // the union record: pre << 16 | bits
-            const uint32_t bits = ldg(ubits, t * 64u + lane);
-            const uint32_t pc = (uint32_t)__popc(bits);
-            far = mode - 1u;
-            word = ((wave_incl_scan(pc) - pc + far) << 16) | bits;
-            jbase = recs[t].bound - EM_SPAN;                     // txn of map byte 0 (mod 2^32)
-        }
-        for (uint32_t q0 = a & ~3u; q0 < e; q0 += 256u) {       // wave-uniform
-            const uint32_t x0 = q0 + 4u * lane;
-            uint32_t v[4], nv[4] = {0u, 0u, 0u, 0u};
-            if (mode) {                                          // wave-uniform: every lane permutes
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t r = x0 + j - a;
-                    uint32_t m = 0;
-#pragma unroll
-                    for (uint32_t st = 32; st >= 1; st >>= 1) {
-                        const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m + st) << 2), (int)word);
-                        if ((pw >> 16) <= r) m += st;
-                    }
-                    const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(m << 2), (int)word);
-                    nv[j] = jbase + m * 16u + em_select16(w & 0xFFFFu, r - (w >> 16));
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t x = x0 + j, r = x - a;
-                v[j] = nv[j];
-                if ((!mode || r < far) && x >= a && x < e) v[j] = vgap[src + r];
-            }
-            if (x0 >= a && x0 + 4u <= e) {
-                *(uint4 *)(vals + x0) = make_uint4(v[0], v[1], v[2], v[3]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (x0 + j >= a && x0 + j < e) vals[x0 + j] = v[j];
-            }
-        }
-    }
-}
-
 } // namespace
-
-void launch_emit_vals(uint32_t n, const uint32_t *vub_off, const uint32_t *val_off, const uint32_t *vgap,
-                      const uint16_t *ubits, const uint8_t *umode, const void *recs, uint32_t *vals, hipStream_t s)
-{
-    if (n == 0) return;
-    uint32_t blocks = (n + 3) / 4;
-    if (blocks > 256u * 16u) blocks = 256u * 16u;
-    hipLaunchKernelGGL(emit_vals_kernel, dim3(blocks), dim3(256), 0, s, n, vub_off, val_off, vgap, ubits, umode,
-                       (const TxnRec *)recs, vals);
-}
 
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,

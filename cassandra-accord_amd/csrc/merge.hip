@@ -62,7 +62,8 @@ __global__ __launch_bounds__(MG_WAVES * 64) void merge_kernel(MergeParams p)
         uint32_t nv = 0, nk = 0, nb = 0, vo = 0, ko = 0, xo = 0, first_key = 0, last_key = 0;
         if (lane < G) {
             const uint32_t *vof = p.val_off[lane], *kof = p.key_off[lane], *xof = p.k2v_off[lane];
-            vo = vof[t] - vof[0]; nv = vof[t + 1] - vof[t];   // offsets relative to the part's slice
+            vo = vof[t] - vof[0];                             // offsets relative to the part's slice
+            nv = p.val_cnt[lane] ? p.val_cnt[lane][t] : vof[t + 1] - vof[t];   // gapped txnIds: counts
             ko = kof[t] - kof[0]; nk = kof[t + 1] - kof[t];
             xo = xof[t] - xof[0]; nb = (xof[t + 1] - xof[t]) - nk;
             if (nk) { first_key = p.keys[lane][ko]; last_key = p.keys[lane][ko + nk - 1]; }

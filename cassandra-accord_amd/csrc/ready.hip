@@ -263,7 +263,8 @@ struct ReadyParams {
     RrMap M;
     const uint32_t *pkoff, *pkeys, *proff, *prs, *pre;
     const uint32_t *rrng_off, *rrs, *rre, *rr2v_off, *rr2v;
-    uint32_t *ovf;
+    RrSpill spill;                    // txns over the LDS removal scratch (ids: ubase + launch index)
+    uint32_t ubase;                   // index of this table's launch's first txn over all launches
     const KeySummary *sum;
     const uint32_t *kb;               // per key: shardRedundantBefore as a position (0: none)
     StatusView v;
@@ -315,13 +316,14 @@ __device__ int unmanaged_eval(const ReadyParams &p, uint32_t t, uint32_t d0, uin
 // (the waves walk the concatenated txn index space, gbase[] = each generation's first index)
 constexpr uint32_t RD_GENS = 32;          // generations evaluated per launch
 struct ReadyLaunch {
-    uint32_t ngen, total;
+    uint32_t ngen, total, base;       // base: the launch's first txn over all launches of the call
     uint32_t gbase[RD_GENS + 1];
     uint32_t *work, *wcnt;            // incremental calls: the txns to evaluate (rd_filter_kernel)
     ReadyParams g[RD_GENS];
 };
 
-__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane, RrLds *rl);
+__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, uint32_t t, uint32_t lane, const RrBuf &rl,
+                                            bool spill);
 
 // Incremental calls: a lane per waiting txn keeps those whose inputs changed since the last call
 // (the txn itself, the key of a set key bit dirty -- for a managed txn: and no longer blocked by the
@@ -389,15 +391,38 @@ __global__ __launch_bounds__(256) void rd_eval_kernel(const ReadyLaunch *__restr
     extern __shared__ RrLds rr_lds[];                // removal scratch, a wave each (when the map can remove)
     const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
     const uint32_t ngen = L->ngen, m = listed ? *L->wcnt : L->total;
+    const RrBuf rl = rr_buf_lds(rr_lds[wave_id()]);
     for (uint32_t i = blockIdx.x * (blockDim.x / 64) + wave_id(); i < m; i += waves) {
         const uint32_t u = listed ? L->work[i] : i;
         uint32_t gi = 0;
         while (gi + 1 < ngen && L->gbase[gi + 1] <= u) ++gi;
-        rd_eval_txn(L->g[gi], u - L->gbase[gi], lane, rr_lds + wave_id());
+        rd_eval_txn(L->g[gi], u, u - L->gbase[gi], lane, rl, false);
     }
 }
 
-__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, uint32_t lane, RrLds *rl)
+// The spill pass: the txns rd_eval_kernel left for exceeding its LDS removal scratch, a wave each with
+// HBM scratch sized for the largest of them (launch index and txn index packed in the list)
+__global__ __launch_bounds__(256) void rd_spill_kernel(const ReadyLaunch *__restrict__ L0, uint32_t nl, RrSpill sp,
+                                                       void *base, uint32_t cap_r, uint32_t cap_e)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    const uint32_t gw = blockIdx.x * (blockDim.x / 64) + wave_id();
+    const RrBuf rl = rr_buf_hbm(base, gw, cap_r, cap_e);
+    const uint32_t m = *sp.count;
+    for (uint32_t i = gw; i < m; i += waves) {
+        const uint32_t id = sp.list[i];
+        uint32_t k = 0;
+        while (k + 1 < nl && L0[k + 1].base <= id) ++k;
+        const ReadyLaunch *L = L0 + k;
+        const uint32_t u = id - L->base;
+        uint32_t gi = 0;
+        while (gi + 1 < L->ngen && L->gbase[gi + 1] <= u) ++gi;
+        rd_eval_txn(L->g[gi], u, u - L->gbase[gi], lane, rl, true);
+    }
+}
+
+__device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, uint32_t t, uint32_t lane, const RrBuf &rl,
+                                            bool spill)
 {
     {
         if (p.done[t]) return;
@@ -437,8 +462,12 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, ui
                 T.r2v = p.rr2v + p.rr2v_off[t];
                 const uint32_t mpos = T.rvals[j0];
                 bool o = false;
-                removal = rr_removal(p.M, T, *rl, lane, mpos, tid_of(p, mpos).msb >> 15, ex.msb >> 15, &o);
-                if (o && lane == 0) atomicAdd(p.ovf, 1u);
+                uint32_t ne = 0;
+                removal = rr_removal(p.M, T, rl, lane, mpos, tid_of(p, mpos).msb >> 15, ex.msb >> 15, &o, &ne);
+                if (o) {                 // over the scratch: nothing decided, the spill pass evaluates it
+                    if (lane == 0 && !spill) rr_spill_add(p.spill, p.ubase + u, R, ne);
+                    return;
+                }
             }
         }
         Ts own{0, 0, 0};                                                // own TxnId (executeAtLeast)
@@ -450,7 +479,7 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t t, ui
         };
         bool waiting = false;
         for (uint32_t q = 0; q < nw; ++q) {
-            const unsigned long long rclr = removal ? rr_clear(*rl, T, q) : 0ull;
+            const unsigned long long rclr = removal ? rr_clear(rl, T, q) : 0ull;
             const unsigned long long old = p.words[w0 + q] & ~rclr;
             const uint32_t b = q * 64u + lane;
             bool clear = false, applied = false;
@@ -707,6 +736,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     constexpr uint32_t RW = sizeof(ReadyOut) / 4;
     HIPCHECK(s, s->rdy_sum.ensure((size_t)nkeys * sizeof(KeySummary) + 64));
     HIPCHECK(s, s->rdy_out.ensure(cap * (4 * RW + 4) + 512));   // header, ready records [cap], dropped [cap]
+    HIPCHECK(s, s->rdy_spill.ensure(cap * 4 + 64));              // txns left to the removal spill pass
     const uint32_t ngens = (uint32_t)s->rdy_gens.size();
     const uint32_t nl = (ngens + RD_GENS - 1) / RD_GENS;
     HIPCHECK(s, s->rdy_launch.ensure((size_t)std::max(1u, nl) * sizeof(ReadyLaunch)));
@@ -767,7 +797,11 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     bool any_inc = false;
     for (accord_impl::ReadyGen *r : s->rdy_gens) {
         if (r->left == 0) continue;
-        if (tabs.empty() || tabs.back().ngen == RD_GENS) { tabs.emplace_back(); tabs.back().ngen = 0; tabs.back().total = 0; }
+        if (tabs.empty() || tabs.back().ngen == RD_GENS) {
+            const uint32_t b = tabs.empty() ? 0u : tabs.back().base + tabs.back().total;
+            tabs.emplace_back();
+            tabs.back().ngen = 0; tabs.back().total = 0; tabs.back().base = b;
+        }
         ReadyLaunch &L = tabs.back();
         ReadyParams &p = L.g[L.ngen];
         p = ReadyParams{};
@@ -790,7 +824,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.proff = r->proff.as<uint32_t>(); p.prs = r->prs.as<uint32_t>(); p.pre = r->pre.as<uint32_t>();
         p.rrng_off = r->rrng_off.as<uint32_t>(); p.rrs = r->rrs.as<uint32_t>(); p.rre = r->rre.as<uint32_t>();
         p.rr2v_off = r->rr2v_off.as<uint32_t>(); p.rr2v = r->rr2v.as<uint32_t>();
-        p.ovf = cnt + (HDR - 2);
+        p.spill = RrSpill{cnt + (HDR - 2), cnt + (HDR - 3), cnt + (HDR - 4), s->rdy_spill.as<uint32_t>()};
+        p.ubase = L.base;
         p.sum = s->rdy_sum.as<KeySummary>();
         p.kb = has_kb && s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
         p.v = v;
@@ -805,7 +840,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     if (any_inc) {          // a work list per launch: cap entries, counts in rdy_wcnt
         HIPCHECK(s, s->rdy_work.ensure(cap * 4 + 64));
         uint32_t *wc = cnt + 2;                // in the header (cleared above) unless too many launches
-        if (tabs.size() > HDR - 4) {
+        if (tabs.size() > HDR - 8) {
             HIPCHECK(s, s->rdy_wcnt.ensure(tabs.size() * 4 + 64));
             HIPCHECK(s, hipMemsetAsync(s->rdy_wcnt.p, 0, tabs.size() * 4, st));
             wc = s->rdy_wcnt.as<uint32_t>();
@@ -852,13 +887,20 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     uint32_t *peek = (uint32_t *)s->rdy_host;
     HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK) * RW) * 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));       // also: the parameter tables were consumed
+    if (peek[HDR - 2]) {    // txns over the LDS removal scratch: the spill pass, then the header again
+        const uint32_t nsp = peek[HDR - 2], blocks = std::min<uint32_t>((nsp + 3) / 4, 64u);
+        HIPCHECK(s, s->rdy_spill_mem.ensure((size_t)blocks * 4 * rr_spill_wave_bytes(peek[HDR - 3], peek[HDR - 4])));
+        const RrSpill sp{cnt + (HDR - 2), cnt + (HDR - 3), cnt + (HDR - 4), s->rdy_spill.as<uint32_t>()};
+        hipLaunchKernelGGL(rd_spill_kernel, dim3(blocks), dim3(256), 0, st, s->rdy_launch.as<ReadyLaunch>(),
+                           (uint32_t)tabs.size(), sp, s->rdy_spill_mem.p, peek[HDR - 3], peek[HDR - 4]);
+        HIPCHECK(s, hipGetLastError());
+        HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK) * RW) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+    }
     const uint32_t nr = peek[0], nd = peek[HDR - 1];
-    if (peek[HDR - 2])
-        return fail(s, ACCORD_ERR_CAPACITY, "%u waiting txns wait on more than %u range deps or touch more than %u "
-                                            "RedundantBefore entries", peek[HDR - 2], RR_MAXR, RR_MAXE);
     if (s->rdy_stats) {                          // ACCORD_READY_STATS: diagnostic totals (ready_destroy prints)
         s->rdy_stats[0] += 1; s->rdy_stats[1] += peek[1]; s->rdy_stats[2] += cap;
-        if (any_inc && tabs.size() <= HDR - 4)
+        if (any_inc && tabs.size() <= HDR - 8)
             for (size_t i = 0; i < tabs.size(); ++i) s->rdy_stats[3] += peek[2 + i];
         else s->rdy_stats[3] += cap;
     }
@@ -883,30 +925,6 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         HIPCHECK(s, hipMemcpyAsync(dropped.data(), drop, (size_t)nd * 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(s, hipStreamSynchronize(st));
         std::sort(dropped.begin(), dropped.end());
-    }
-    if (const char *tr = getenv("ACCORD_READY_TRACE")) {     // dev aid: "g,d1,d2,...": g's executeAtLeast record
-        std::vector<uint32_t> ids;
-        for (const char *c = tr; *c;) { ids.push_back((uint32_t)strtoul(c, (char **)&c, 10)); if (*c == ',') ++c; else break; }
-        for (accord_impl::ReadyGen *r : s->rdy_gens)
-            if (!ids.empty() && ids[0] >= r->glo && ids[0] <= r->ghi) {
-                EalRec e{};
-                uint8_t dn = 0;
-                HIPCHECK(s, hipMemcpy(&e, r->eal.as<EalRec>() + (ids[0] - r->glo), sizeof(e), hipMemcpyDeviceToHost));
-                HIPCHECK(s, hipMemcpy(&dn, r->done.as<uint8_t>() + (ids[0] - r->glo), 1, hipMemcpyDeviceToHost));
-                fprintf(stderr, "trace call %u txn %u done %u eal has %u (%llu, %llu, %d)\n", call, ids[0], dn, e.has,
-                        (unsigned long long)e.msb, (unsigned long long)e.lsb, e.node);
-            }
-        for (size_t i = 1; i < ids.size(); ++i) {
-            uint64_t m = 0, l = 0; int32_t nd = 0; uint8_t stt = 0;
-            const uint32_t d = ids[i];
-            if (d >= s->rg_known) continue;
-            HIPCHECK(s, hipMemcpy(&m, s->rg_emsb.as<uint64_t>() + d, 8, hipMemcpyDeviceToHost));
-            HIPCHECK(s, hipMemcpy(&l, s->rg_elsb.as<uint64_t>() + d, 8, hipMemcpyDeviceToHost));
-            HIPCHECK(s, hipMemcpy(&nd, s->rg_enode.as<int32_t>() + d, 4, hipMemcpyDeviceToHost));
-            HIPCHECK(s, hipMemcpy(&stt, s->rg_status.as<uint8_t>() + d, 1, hipMemcpyDeviceToHost));
-            fprintf(stderr, "  dep %u status %u exec (%llu, %llu, %d)\n", d, stt, (unsigned long long)m,
-                    (unsigned long long)l, nd);
-        }
     }
     s->rdy_force_full = false;                 // the device and the bookkeeping below agree again
     // generations drain in stream order: count each one's released (or dropped) txns, free the empty ones

@@ -20,8 +20,10 @@
 //           uncovered) and each have j < bootstrapIdx_e: j < cb_r = min bootstrapIdx over them (0 when r
 //           is not tiled), for every r of j.  isFullyBootstrapping's remaining-ranges bookkeeping is
 //           that union, order-free.
-// A wave evaluates one txn: lane 0 lists the entries its participants touch (<= RR_MAXE), lanes take
-// the RangeDeps ranges; the bits to clear gather in LDS (<= RR_MAXR range deps).
+// A wave evaluates one txn: lane 0 lists the entries its participants touch, lanes take the RangeDeps
+// ranges; the bits to clear gather in the wave's scratch -- LDS (RrLds: <= RR_MAXE entries, <= RR_MAXR
+// range deps) or, for a txn over those caps, HBM sized by the spill pass (RrSpill below): the caps only
+// decide where the scratch lives, never whether a txn is evaluated.
 #pragma once
 #include "status_view.h"
 
@@ -44,6 +46,56 @@ struct RrLds {
     uint32_t E[RR_MAXE], bidx[RR_MAXE], aidx[RR_MAXE];
     uint32_t nE;
 };
+
+// One wave's removal scratch: the RrLds fields, in LDS or in HBM
+struct RrBuf {
+    unsigned long long *rm, *keep;           // [cap_r / 64]
+    uint32_t *E, *bidx, *aidx;               // [cap_e]
+    uint32_t *nE;
+    uint32_t cap_r, cap_e;
+};
+
+__device__ __forceinline__ RrBuf rr_buf_lds(RrLds &L)
+{
+    return RrBuf{L.rm, L.keep, L.E, L.bidx, L.aidx, &L.nE, RR_MAXR, RR_MAXE};
+}
+
+// HBM scratch per spill wave for txns of up to cap_r range deps touching up to cap_e entries
+__host__ __device__ __forceinline__ size_t rr_spill_wave_bytes(uint32_t cap_r, uint32_t cap_e)
+{
+    const size_t words = ((size_t)cap_r + 63u) / 64u;
+    return (16u * words + 4u * (3u * (size_t)cap_e + 1u) + 255u) & ~(size_t)255u;
+}
+
+__device__ __forceinline__ RrBuf rr_buf_hbm(void *base, uint32_t wave, uint32_t cap_r, uint32_t cap_e)
+{
+    char *p = (char *)base + (size_t)wave * rr_spill_wave_bytes(cap_r, cap_e);
+    const size_t words = ((size_t)cap_r + 63u) / 64u;
+    RrBuf b;
+    b.rm = (unsigned long long *)p;
+    b.keep = b.rm + words;
+    b.E = (uint32_t *)(b.keep + words);
+    b.bidx = b.E + cap_e;
+    b.aidx = b.bidx + cap_e;
+    b.nE = b.aidx + cap_e;
+    b.cap_r = (uint32_t)(words * 64u);
+    b.cap_e = cap_e;
+    return b;
+}
+
+// Txns over the LDS caps, evaluated again by a spill pass with HBM scratch: the ids, how many, and
+// the largest range-dep / entry counts among them (the spill pass sizes its scratch from these)
+struct RrSpill {
+    uint32_t *count, *max_r, *max_e;
+    uint32_t *list;
+};
+
+__device__ __forceinline__ void rr_spill_add(const RrSpill &sp, uint32_t id, uint32_t R, uint32_t nE)
+{
+    sp.list[atomicAdd(sp.count, 1u)] = id;
+    atomicMax(sp.max_r, R);
+    atomicMax(sp.max_e, nE);
+}
 
 // the waiting txn: its participants and its RangeDeps
 struct RrTxn {
@@ -119,11 +171,12 @@ __device__ __forceinline__ void rr_mark(unsigned long long *mask, const uint32_t
 }
 
 // The range-dep bits of a waiting txn to clear (words[] holds its current WaitingOn; minimum set bit j0
-// a range dep at position min_pos): returns false when the status fold keeps everything; *ovf set
-// when the txn exceeds RR_MAXE / RR_MAXR.  On true, clear(q) below gives word q's bits to clear.
-// Every lane of the wave calls it (wave-uniform arguments).
-__device__ inline bool rr_removal(const RrMap &M, const RrTxn &T, RrLds &L, uint32_t lane, uint32_t min_pos,
-                                  uint64_t min_epoch, uint64_t exec_epoch, bool *ovf)
+// a range dep at position min_pos): returns false when the status fold keeps everything; when the
+// txn exceeds the scratch's caps, returns false with *ovf set and *need_e = its entry count (nothing
+// was decided: the caller leaves the txn to the spill pass).  On true, rr_clear(q) below gives word q's
+// bits to clear.  Every lane of the wave calls it (wave-uniform arguments).
+__device__ inline bool rr_removal(const RrMap &M, const RrTxn &T, const RrBuf &L, uint32_t lane, uint32_t min_pos,
+                                  uint64_t min_epoch, uint64_t exec_epoch, bool *ovf, uint32_t *need_e)
 {
     if (lane == 0) {            // the entries the participants touch, ascending, once (ReducingRangeMap.foldl)
         uint32_t n = 0;
@@ -133,25 +186,26 @@ __device__ inline bool rr_removal(const RrMap &M, const RrTxn &T, RrLds &L, uint
             for (uint32_t x = rr_first_end_above(M, a); x < M.m && M.s[x] < b; ++x) {
                 if ((int64_t)x <= last) continue;
                 last = x;
-                if (n < RR_MAXE) L.E[n] = x;
+                if (n < L.cap_e) L.E[n] = x;
                 ++n;
             }
         }
-        L.nE = n;
+        *L.nE = n;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    const uint32_t nE = L.nE;
-    if (nE > RR_MAXE || T.R > RR_MAXR) { *ovf = true; return false; }
+    const uint32_t nE = *L.nE;
+    __builtin_amdgcn_wave_barrier();
+    if (nE > L.cap_e || T.R > L.cap_r) { *ovf = true; *need_e = nE; return false; }
     // the status fold: an in-bounds entry giving minWaitingOnTxnId a status other than LIVE
     bool hot = false;
-    if (lane < nE) {
-        const uint32_t x = L.E[lane];
+    for (uint32_t i = lane; i < nE; i += 64) {
+        const uint32_t x = L.E[i];
         const bool out = exec_epoch < M.sep[x] || min_epoch >= M.eep[x];                 // Entry.outOfBounds
-        hot = !out && (M.stale[x] || (M.boot[x] != RR_NONE && M.boot[x] > min_pos) ||
-                       (M.local[x] != RR_NONE && M.local[x] > min_pos));
-        L.bidx[lane] = rr_find(T, M.boot[x]);
-        L.aidx[lane] = rr_find(T, M.local[x]);
+        hot |= !out && (M.stale[x] || (M.boot[x] != RR_NONE && M.boot[x] > min_pos) ||
+                        (M.local[x] != RR_NONE && M.local[x] > min_pos));
+        L.bidx[i] = rr_find(T, M.boot[x]);
+        L.aidx[i] = rr_find(T, M.local[x]);
     }
     const uint32_t nw = (T.R + 63u) / 64u;
     for (uint32_t q = lane; q < nw; q += 64) { L.rm[q] = 0; L.keep[q] = 0; }
@@ -182,7 +236,7 @@ __device__ inline bool rr_removal(const RrMap &M, const RrTxn &T, RrLds &L, uint
 }
 
 // word q of the range bits to clear after rr_removal returned true
-__device__ __forceinline__ unsigned long long rr_clear(const RrLds &L, const RrTxn &T, uint32_t q)
+__device__ __forceinline__ unsigned long long rr_clear(const RrBuf &L, const RrTxn &T, uint32_t q)
 {
     const uint32_t nw = (T.R + 63u) / 64u;
     if (q >= nw) return 0ull;
@@ -197,18 +251,16 @@ struct EalRec {
     uint32_t has;
 };
 
-// a = take ? b : a, every field blended with one all-ones / zero word the compiler cannot see
-// through (status.hip wo_init_kernel: a running merge there combined one candidate's msb / lsb
-// with another's node on gfx950, whatever the merge's form; it now keeps the winner's position)
-__device__ __forceinline__ void eal_blend(EalRec &a, const EalRec &b, bool take)
+// a = take ? b : a, field by field.  Written as value selects with a non-short-circuit condition:
+// the branchy form (if (b.has && (!a.has || ts_cmp(a, b) < 0)) a = b) is miscompiled for gfx950 by
+// ROCm 7.2's clang inside wo_init_kernel's loop -- on the a.has path the node / has pair is carried
+// over unselected while msb / lsb take b's (profiles/r05_eal/wo_init_merge_isa_before.s).
+__device__ __forceinline__ void eal_take(EalRec &a, const EalRec &b, bool take)
 {
-    uint32_t mk = take ? 0xFFFFFFFFu : 0u;
-    asm volatile("" : "+v"(mk));
-    const uint64_t mk64 = ((uint64_t)mk << 32) | mk;
-    a.msb = (b.msb & mk64) | (a.msb & ~mk64);
-    a.lsb = (b.lsb & mk64) | (a.lsb & ~mk64);
-    a.node = (int32_t)(((uint32_t)b.node & mk) | ((uint32_t)a.node & ~mk));
-    a.has = (b.has & mk) | (a.has & ~mk);
+    a.msb = take ? b.msb : a.msb;
+    a.lsb = take ? b.lsb : a.lsb;
+    a.node = take ? b.node : a.node;
+    a.has = take ? b.has : a.has;
 }
 
 // wave maximum of the lanes' candidates (has = false: none); the result is uniform
@@ -220,14 +272,14 @@ __device__ inline EalRec eal_wave_max(bool has, const Ts &t)
         EalRec u;
         u.msb = __shfl_xor(r.msb, o, 64); u.lsb = __shfl_xor(r.lsb, o, 64);
         u.node = __shfl_xor(r.node, o, 64); u.has = __shfl_xor(r.has, o, 64);
-        eal_blend(r, u, u.has && (!r.has || ts_cmp(r.msb, r.lsb, r.node, u.msb, u.lsb, u.node) < 0));
+        eal_take(r, u, (u.has != 0u) & ((r.has == 0u) | (ts_cmp(r.msb, r.lsb, r.node, u.msb, u.lsb, u.node) < 0)));
     }
     return r;
 }
 
 __device__ __forceinline__ void eal_merge(EalRec &a, const EalRec &b)      // Timestamp.nonNullOrMax
 {
-    eal_blend(a, b, b.has && (!a.has || ts_cmp(a.msb, a.lsb, a.node, b.msb, b.lsb, b.node) < 0));
+    eal_take(a, b, (b.has != 0u) & ((a.has == 0u) | (ts_cmp(a.msb, a.lsb, a.node, b.msb, b.lsb, b.node) < 0)));
 }
 
 } // namespace accord_status

@@ -49,6 +49,7 @@ const int kGrp[ND] = {0, 1, 2, 3, 3, 4, 5};
 struct Part {
     const uint32_t *key_off, *keys, *val_off, *vals, *k2v_off;
     const int32_t *k2v;
+    const uint32_t *val_cnt;          // gapped txnIds: per-txn counts (nullptr: dense)
 };
 
 } // namespace
@@ -120,7 +121,7 @@ int32_t merge_parts(accord_store *s, const std::vector<Part> &parts, uint32_t n,
     if (G == 0 || G > 64) return fail(s, ACCORD_ERR_CAPACITY, "merge of %u parts (1..64 supported)", G);
     hipStream_t st = s->stream;
     const size_t n1 = (size_t)n + 1;
-    HIPCHECK(s, s->m_ptrs.ensure((size_t)6 * G * sizeof(void *)));
+    HIPCHECK(s, s->m_ptrs.ensure((size_t)7 * G * sizeof(void *)));
     HIPCHECK(s, s->m_cnt_keys.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->m_cnt_vals.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->m_cnt_k2v.ensure((size_t)n * 4 + 4));
@@ -137,11 +138,12 @@ int32_t merge_parts(accord_store *s, const std::vector<Part> &parts, uint32_t n,
     }
     // the pointer table (a pageable source: HIP stages the copy before returning, so the vector
     // may go out of scope right after)
-    std::vector<const void *> tbl(6 * (size_t)G);
+    std::vector<const void *> tbl(7 * (size_t)G);
     for (uint32_t g = 0; g < G; ++g) {
         tbl[0 * G + g] = parts[g].key_off; tbl[1 * G + g] = parts[g].keys;
         tbl[2 * G + g] = parts[g].val_off; tbl[3 * G + g] = parts[g].vals;
         tbl[4 * G + g] = parts[g].k2v_off; tbl[5 * G + g] = parts[g].k2v;
+        tbl[6 * G + g] = parts[g].val_cnt;
     }
     HIPCHECK(s, hipMemcpyAsync(s->m_ptrs.p, tbl.data(), tbl.size() * sizeof(void *), hipMemcpyHostToDevice, st));
     const void *const *ptab = (const void *const *)s->m_ptrs.p;
@@ -150,6 +152,7 @@ int32_t merge_parts(accord_store *s, const std::vector<Part> &parts, uint32_t n,
     mp.key_off = (const uint32_t *const *)(ptab + 0 * G); mp.keys = (const uint32_t *const *)(ptab + 1 * G);
     mp.val_off = (const uint32_t *const *)(ptab + 2 * G); mp.vals = (const uint32_t *const *)(ptab + 3 * G);
     mp.k2v_off = (const uint32_t *const *)(ptab + 4 * G); mp.k2v = (const int32_t *const *)(ptab + 5 * G);
+    mp.val_cnt = (const uint32_t *const *)(ptab + 6 * G);
     mp.cnt_keys = s->m_cnt_keys.as<uint32_t>(); mp.cnt_vals = s->m_cnt_vals.as<uint32_t>(); mp.cnt_k2v = s->m_cnt_k2v.as<uint32_t>();
     HostTotals *dev = s->status_totals.as<HostTotals>();
     mp.status = &dev->status;
@@ -257,6 +260,8 @@ int32_t xchg_prepare(accord_store *s, uint32_t n_total)
     if (!s->computed || s->merged) return fail(s, ACCORD_ERR_STATE, "exchange needs a freshly computed partial");
     if (!s->has_txn_index && s->n != n_total) return fail(s, ACCORD_ERR_ARG, "batch without txn_index must be the whole stream");
     if (s->ds_cur >= 0) return fail(s, ACCORD_ERR_STATE, "exchange of a store holding a deps-set result");
+    // the partials travel dense: the compute's gapped txnIds are compacted first (kd_val_off / kd_vals)
+    RC_FORWARD(accord_impl::store_dense_keydeps(s));
     if (s->has_txn_index) {
         HIPCHECK(s, c->ind.ensure((size_t)n_total * 4 + 4));
         HIPCHECK(s, c->cscan.ensure(((size_t)n_total + 1) * 4));
@@ -411,7 +416,7 @@ int32_t xchg_union(accord_store *s)
         uint64_t bounds[3] = {0, 0, 0};
         for (uint32_t src = 0; src < G; ++src) {
             const RecvView v = recv_view(s, src);
-            parts[src] = Part{v.off[0], v.dat[0], v.off[1], v.dat[1], v.off[2], (const int32_t *)v.dat[2]};
+            parts[src] = Part{v.off[0], v.dat[0], v.off[1], v.dat[1], v.off[2], (const int32_t *)v.dat[2], nullptr};
             for (int a = 0; a < 3; ++a) bounds[a] += c->cnt(src, me)[a];
         }
         return merge_parts(s, parts, c->nh, c->my_lo, bounds);
@@ -455,7 +460,7 @@ int32_t accord_deps_merge(accord_store *s, uint32_t nparts, const accord_deps *p
         if (parts[g].n != n) return fail(s, ACCORD_ERR_ARG, "merge parts cover different txn counts");
         ranges = ranges || parts[g].rd_rngs_total || parts[g].rd_vals_total;
         ps[g] = Part{parts[g].kd_key_off, parts[g].kd_keys, parts[g].kd_val_off, parts[g].kd_vals,
-                     parts[g].kd_k2v_off, parts[g].kd_k2v};
+                     parts[g].kd_k2v_off, parts[g].kd_k2v, parts[g].kd_val_cnt};
     }
     // RangeDeps, more parts than the merge kernel's lanes, or a txn past its union capacity: the
     // general union (linearUnion on both sides gives the same sets for key-disjoint parts)

@@ -677,8 +677,7 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
         const uint32_t r0 = rd_val_off[t], R = rd_val_off[t + 1] - r0;
         const uint32_t bits = R + (kd_key_off[t + 1] - kd_key_off[t]);
         const uint32_t w0 = wo_off[t], nw = wo_off[t + 1] - w0;
-        uint32_t best = 0xFFFFFFFFu;                       // the dep executing last among the candidates
-        Ts bex{0, 0, 0};
+        EalRec ea{0, 0, 0, 0u};                            // Timestamp.nonNullOrMax over the candidates
         for (uint32_t q = 0; q < nw; ++q) {
             unsigned long long wv = 0, av = 0;
             const unsigned long long kept = pre ? words[w0 + q] : ~0ull;   // removeRedundantDependencies
@@ -691,11 +690,7 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
                 bool wait = true, applied = false;
                 if (only_deps && st >= ST_COMMITTED && st <= ST_APPLIED) {   // updateExecuteAtLeast
                     const Ts de = exec_of(v, d);
-                    if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0 &&
-                        (best == 0xFFFFFFFFu || tcmp(bex, de) < 0)) {
-                        best = d;
-                        bex = de;
-                    }
+                    if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0) eal_merge(ea, EalRec{de.msb, de.lsb, de.node, 1u});
                 }
                 if (st >= ST_COMMITTED) {                       // hasBeen(PreCommitted)
                     if (st >= ST_INVALID) { wait = false; applied = true; }                 // truncated / invalidated
@@ -708,20 +703,15 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
             words[w0 + q] = wv;
             aoi[w0 + q] = av;
         }
-        // the record from the winner's executeAt, loaded once more: merging each candidate's fields
-        // into a running record here (eal_merge, in any form) was seen to combine the winner's msb /
-        // lsb with an earlier candidate's node on gfx950 (test_ready.py::test_gpu_schedule_equals_oracle)
-        EalRec ea{0, 0, 0, 0u};
-        if (best != 0xFFFFFFFFu) {
-            const Ts be = exec_of(v, best);
-            ea = EalRec{be.msb, be.lsb, be.node, 1u};
-        }
         eal[t] = ea;
     }
 }
 
 // removeRedundantDependencies at initialiseWaitingOn (every bit set: minWaitingOnTxnId = the first
-// range dep), a wave per txn: words[] = the range deps it keeps, key bits set.
+// range dep), a wave per txn: words[] = the range deps it keeps, key bits set.  SPILL = false: every
+// txn, scratch in LDS; a txn over its caps is listed in sp and left alone.  SPILL = true: the listed
+// txns, scratch in HBM (spill_base, sized for the largest of them).
+template <bool SPILL>
 __global__ __launch_bounds__(256) void rr_init_kernel(uint32_t n, const uint64_t *__restrict__ msb,
                                                       const uint64_t *__restrict__ lsb, const uint32_t *__restrict__ txn_index,
                                                       const uint32_t *__restrict__ key_off, const uint32_t *__restrict__ key_ord,
@@ -730,16 +720,22 @@ __global__ __launch_bounds__(256) void rr_init_kernel(uint32_t n, const uint64_t
                                                       const uint64_t *__restrict__ tmsb, const uint32_t *__restrict__ tg,
                                                       uint32_t tx_n, RrMap M, const uint32_t *__restrict__ wo_off,
                                                       StatusView v, unsigned long long *__restrict__ words,
-                                                      uint32_t *__restrict__ ovf)
+                                                      RrSpill sp, void *spill_base, uint32_t cap_r, uint32_t cap_e)
 {
     __shared__ RrLds lds[4];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-    RrLds &L = lds[w];
-    for (uint32_t t = blockIdx.x * 4u + w; t < n; t += gridDim.x * 4u) {
+    const uint32_t gw = blockIdx.x * 4u + w;
+    RrBuf L;
+    if constexpr (SPILL) L = rr_buf_hbm(spill_base, gw, cap_r, cap_e);
+    else L = rr_buf_lds(lds[w]);
+    const uint32_t m = SPILL ? *sp.count : n;
+    for (uint32_t i = gw; i < m; i += gridDim.x * 4u) {
+        const uint32_t t = SPILL ? sp.list[i] : i;
         const uint32_t r0 = cd.rd_val_off[t], R = cd.rd_val_off[t + 1] - r0;
         const uint32_t bits = R + (cd.kd_key_off[t + 1] - cd.kd_key_off[t]);
         const uint32_t w0 = wo_off[t], nw = wo_off[t + 1] - w0;
         bool removal = false, o = false;
+        uint32_t ne = 0;
         RrTxn T{};
         if (R) {
             const uint64_t l = lsb[t];
@@ -754,10 +750,13 @@ __global__ __launch_bounds__(256) void rr_init_kernel(uint32_t n, const uint64_t
             const uint64_t em = ost >= ST_ACCEPTED && ost <= ST_APPLIED ? v.emsb[g] : msb[t];
             const uint32_t mpos = T.rvals[0];
             uint32_t lo = 0, hi = tx_n;                          // TxnId of the dep at mpos (epoch)
-            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (tg[m] < mpos) lo = m + 1; else hi = m; }
-            removal = rr_removal(M, T, L, lane, mpos, tmsb[lo] >> 15, em >> 15, &o);
+            while (lo < hi) { const uint32_t mm = (lo + hi) >> 1; if (tg[mm] < mpos) lo = mm + 1; else hi = mm; }
+            removal = rr_removal(M, T, L, lane, mpos, tmsb[lo] >> 15, em >> 15, &o, &ne);
         }
-        if (o && lane == 0) atomicAdd(ovf, 1u);
+        if (o) {                                                 // over the LDS caps: the spill pass
+            if (lane == 0) rr_spill_add(sp, t, R, ne);
+            continue;
+        }
         for (uint32_t q = lane; q < nw; q += 64) {
             const uint32_t b0 = q * 64u;
             unsigned long long wv = b0 + 64u <= bits ? ~0ull : ((1ull << (bits - b0)) - 1ull);
@@ -784,20 +783,28 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
     if (!n) return ACCORD_OK;
     const bool pre = s->rb_ext && s->rb_m && cd.tot_rvals;
     if (pre) {                     // removeRedundantDependencies first (redundant_wait.h)
-        HIPCHECK(s, s->rr_ovf.ensure(64));
-        uint32_t *ovf = s->rr_ovf.as<uint32_t>();
-        HIPCHECK(s, hipMemsetAsync(ovf, 0, 8, s->stream));
-        hipLaunchKernelGGL(rr_init_kernel, dim3(std::min<uint32_t>((n + 3) / 4, 8192u)), dim3(256), 0, s->stream, n,
-                           s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->txn_index.as<uint32_t>(),
-                           s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->R ? s->rng_off.as<uint32_t>() : nullptr,
-                           s->R ? s->rng_start.as<uint32_t>() : nullptr, s->R ? s->rng_end.as<uint32_t>() : nullptr, cd,
-                           s->rg_tmsb.as<uint64_t>(), s->rg_tg.as<uint32_t>(), s->rg_tx_n, rr_map_of(s), wo_off, view_of(s),
-                           words, ovf);
-        uint32_t h = 0;
-        HIPCHECK(s, hipMemcpyAsync(&h, ovf, 4, hipMemcpyDeviceToHost, s->stream));
+        HIPCHECK(s, s->rr_ovf.ensure((size_t)n * 4 + 64));
+        uint32_t *hdr = s->rr_ovf.as<uint32_t>();
+        HIPCHECK(s, hipMemsetAsync(hdr, 0, 16, s->stream));
+        const RrSpill sp{hdr, hdr + 1, hdr + 2, hdr + 16};
+        auto launch = [&](bool spill, uint32_t grid, void *base, uint32_t cr, uint32_t ce) {
+            auto k = spill ? rr_init_kernel<true> : rr_init_kernel<false>;
+            hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s->stream, n,
+                               s->msb.as<uint64_t>(), s->lsb.as<uint64_t>(), s->txn_index.as<uint32_t>(),
+                               s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->R ? s->rng_off.as<uint32_t>() : nullptr,
+                               s->R ? s->rng_start.as<uint32_t>() : nullptr, s->R ? s->rng_end.as<uint32_t>() : nullptr, cd,
+                               s->rg_tmsb.as<uint64_t>(), s->rg_tg.as<uint32_t>(), s->rg_tx_n, rr_map_of(s), wo_off, view_of(s),
+                               words, sp, base, cr, ce);
+        };
+        launch(false, std::min<uint32_t>((n + 3) / 4, 8192u), nullptr, 0, 0);
+        uint32_t h[3] = {0, 0, 0};
+        HIPCHECK(s, hipMemcpyAsync(h, hdr, 12, hipMemcpyDeviceToHost, s->stream));
         HIPCHECK(s, hipStreamSynchronize(s->stream));
-        if (h) return fail(s, ACCORD_ERR_CAPACITY, "%u txns wait on more than %u range deps or touch more than %u "
-                                                   "RedundantBefore entries", h, RR_MAXR, RR_MAXE);
+        if (h[0]) {                // txns over the LDS caps: again, with HBM scratch sized for the largest
+            const uint32_t blocks = std::min<uint32_t>((h[0] + 3) / 4, 64u);
+            HIPCHECK(s, s->rr_spill.ensure((size_t)blocks * 4 * rr_spill_wave_bytes(h[1], h[2])));
+            launch(true, blocks, s->rr_spill.p, h[1], h[2]);
+        }
     }
     hipLaunchKernelGGL(wo_init_kernel, dim3(grid_for(n)), dim3(256), 0, s->stream, n, s->msb.as<uint64_t>(),
                        s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),

@@ -126,7 +126,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
                       &s->rc_end2, &s->rc_kind2, &s->rc_first, &s->rc_flag, &s->rc_offs, &s->rdy_kseg0, &s->rdy_kseg1, &s->rdy_dirty, &s->rdy_dirty2, &s->rg_cchg, &s->rdy_dlist, &s->rdy_work, &s->rdy_wcnt, &s->rg_chg, &s->rdy_part, &s->rdy_sum, &s->rdy_out, &s->rdy_kb, &s->rdy_launch,
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero,
-                      &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->rr_ovf, &s->up_stage};
+                      &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->rr_ovf, &s->rr_spill, &s->rdy_spill, &s->rdy_spill_mem, &s->up_stage};
     accord_impl::shard_comm_destroy(s);
     accord_impl::ready_destroy(s);
     accord_impl::pinned_arena_destroy(s);
@@ -307,6 +307,7 @@ int32_t accord_deps_compute(accord_store *s)
     const size_t n1 = (size_t)n + 1;
     hipStream_t st = s->stream;
     s->computed = false;
+    s->kd_dense = false;
     s->merged = false;
     s->m_pending = false;
     s->ds_cur = -1;
@@ -344,7 +345,6 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->cnt_rvals.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->cnt_r2v.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->kd_key_off.ensure(n1 * 4));
-    HIPCHECK(s, s->kd_val_off.ensure(n1 * 4));
     HIPCHECK(s, s->kd_k2v_off.ensure(n1 * 4));
     HIPCHECK(s, s->rd_rng_off.ensure(n1 * 4));
     HIPCHECK(s, s->rd_val_off.ensure(n1 * 4));
@@ -600,8 +600,7 @@ int32_t accord_deps_compute(accord_store *s)
         rp.hist = h;
     }
     HIPCHECK(s, s->kd_keys.ensure(s->tot_keys * 4));
-    HIPCHECK(s, s->vgap.ensure(vub_total * 4));
-    HIPCHECK(s, s->kd_vals.ensure(vub_total * 4));
+    HIPCHECK(s, s->vgap.ensure(vub_total * 4 + 4));   // KeyDeps txnIds, gapped (accord_deps.kd_val_cnt)
     HIPCHECK(s, s->kd_k2v.ensure(s->tot_k2v * 4));
     HIPCHECK(s, s->rd_rng_start.ensure(s->tot_rngs * 4));
     HIPCHECK(s, s->rd_rng_end.ensure(s->tot_rngs * 4));
@@ -623,18 +622,6 @@ int32_t accord_deps_compute(accord_store *s)
     kp.big_wex = s->bk_wex.as<uint32_t>();
     kp.tiny = (uint64_t)P <= 2ull * n ? 1u : 0u;      // <= 2 keys per txn on average: a store's key block
     if (const char *e = getenv("ACCORD_TINY")) kp.tiny = e[0] == '1' ? 1u : 0u;   // dev aid: force on / off
-    // emit mode: the fast kernel (16 map bits per lane: windows up to 384) leaves union records and
-    // the txnIds are written once, at their exact offsets, by launch_emit_vals instead of being
-    // scattered at upper-bound offsets and compacted (ACCORD_FILL_EMIT=0: the compaction, for A/B)
-    const char *em = getenv("ACCORD_FILL_EMIT");
-    const bool emit = s->cfg.window <= 384u && em && em[0] == '1';   // off until measured
-    kp.ubits = nullptr; kp.umode = nullptr;
-    if (emit) {
-        HIPCHECK(s, s->fk_ubits.ensure((size_t)n * 128 + 64));
-        HIPCHECK(s, s->fk_umode.ensure((size_t)n + 64));
-        kp.ubits = s->fk_ubits.as<uint16_t>();
-        kp.umode = s->fk_umode.as<uint8_t>();
-    }
     if (!recs_early) accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
@@ -649,15 +636,8 @@ int32_t accord_deps_compute(accord_store *s)
     }
     if (rdeps) accord::launch_rangedeps_fill(rp, st);
     record(s, EV_RANGE);
-    accord::exclusive_scan_u32(kp.cnt_vals, s->kd_val_off.as<uint32_t>(), n, &dev->totals[7], s->scan_tmp.p, st);
-    if (emit) {
-        accord::launch_emit_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, kp.ubits, kp.umode, s->fk_recs.p,
-                                 s->kd_vals.as<uint32_t>(), st);
-    } else {
-        HIPCHECK(s, s->cv_tmp.ensure(accord::compact_temp_bytes(vub_total)));
-        accord::launch_compact_vals(n, kp.vub_off, s->kd_val_off.as<uint32_t>(), kp.vgap, s->kd_vals.as<uint32_t>(),
-                                    vub_total, s->cv_tmp.p, st);
-    }
+    // the txnIds stay where the fill wrote them: each txn's list at its upper-bound offset (vub_off),
+    // its length in cnt_vals -- the gapped form of the ABI (include/accord_deps.h, kd_val_cnt)
     if (s->resident) {
         // what the next batch needs of this history (the stream ends at b_end)
         const uint32_t thr = s->b_end > s->cfg.window ? s->b_end - s->cfg.window : 0u;
@@ -700,7 +680,7 @@ int32_t accord_deps_compute(accord_store *s)
     {
         int32_t rc = check_status(*s->pinned);
         if (rc) return rc;
-        s->tot_vals = s->pinned->totals[7];
+        s->tot_vals = vub_total;
     }
     if (s->resident) {      // the batch is part of the store's stream now
         if (accord_impl::registered_mode(s)) {
@@ -832,7 +812,8 @@ int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
     d->n = s->n;
     d->kd_keys_total = s->tot_keys; d->kd_vals_total = s->tot_vals; d->kd_k2v_total = s->tot_k2v;
     d->kd_key_off = s->kd_key_off.as<uint32_t>(); d->kd_keys = s->kd_keys.as<uint32_t>();
-    d->kd_val_off = s->kd_val_off.as<uint32_t>(); d->kd_vals = s->kd_vals.as<uint32_t>();
+    d->kd_val_off = s->vub_off.as<uint32_t>(); d->kd_vals = s->vgap.as<uint32_t>();
+    d->kd_val_cnt = s->cnt_vals.as<uint32_t>();
     d->kd_k2v_off = s->kd_k2v_off.as<uint32_t>(); d->kd_k2v = s->kd_k2v.as<int32_t>();
     d->rd_rngs_total = s->tot_rngs; d->rd_vals_total = s->tot_rvals; d->rd_r2v_total = s->tot_r2v;
     d->rd_rng_off = s->rd_rng_off.as<uint32_t>(); d->rd_val_off = s->rd_val_off.as<uint32_t>();
@@ -845,6 +826,25 @@ int32_t accord_deps_device_view(accord_store *s, accord_deps *d)
 } // extern "C"
 
 namespace accord_impl {
+
+int32_t store_dense_keydeps(accord_store *s)
+{
+    if (s->kd_dense) return ACCORD_OK;
+    const uint32_t n = s->n;
+    const size_t n1 = (size_t)n + 1;
+    hipStream_t st = s->stream;
+    HostTotals *dev = s->status_totals.as<HostTotals>();
+    HIPCHECK(s, s->kd_val_off.ensure(n1 * 4));
+    HIPCHECK(s, s->kd_vals.ensure(s->tot_vals * 4 + 4));
+    HIPCHECK(s, s->cv_tmp.ensure(accord::compact_temp_bytes(s->tot_vals)));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n), st));
+    accord::exclusive_scan_u32(s->cnt_vals.as<uint32_t>(), s->kd_val_off.as<uint32_t>(), n, &dev->totals[7], s->scan_tmp.p, st);
+    accord::launch_compact_vals(n, s->vub_off.as<uint32_t>(), s->kd_val_off.as<uint32_t>(), s->vgap.as<uint32_t>(),
+                                s->kd_vals.as<uint32_t>(), s->tot_vals, s->cv_tmp.p, st);
+    HIPCHECK(s, hipGetLastError());
+    s->kd_dense = true;
+    return ACCORD_OK;
+}
 
 // Host memory of downloaded deps: one pinned block per result.  A store keeps its last block as a
 // reusable arena (page-locked allocation of ~1 GB costs far more than the copy); a result still
@@ -889,13 +889,15 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
     int32_t rc = accord_deps_device_view(s, &v);
     if (rc) return rc;
     const size_t n1 = (size_t)v.n + 1;
-    // layout: 13 arrays, each 64-byte aligned
-    const size_t cnt[13] = {n1, v.kd_keys_total, n1, v.kd_vals_total, n1, v.kd_k2v_total,
-                            n1, v.rd_rngs_total, v.rd_rngs_total, n1, v.rd_vals_total, n1, v.rd_r2v_total};
-    const void *src[13] = {v.kd_key_off, v.kd_keys, v.kd_val_off, v.kd_vals, v.kd_k2v_off, v.kd_k2v,
-                           v.rd_rng_off, v.rd_rng_start, v.rd_rng_end, v.rd_val_off, v.rd_vals, v.rd_r2v_off, v.rd_r2v};
-    size_t off[13], total = 0;
-    for (int a = 0; a < 13; ++a) { off[a] = total; total += (cnt[a] * 4 + 63) & ~(size_t)63; }
+    // layout: 14 arrays (the last: kd_val_cnt of a gapped result), each 64-byte aligned
+    const size_t cnt[14] = {n1, v.kd_keys_total, n1, v.kd_vals_total, n1, v.kd_k2v_total,
+                            n1, v.rd_rngs_total, v.rd_rngs_total, n1, v.rd_vals_total, n1, v.rd_r2v_total,
+                            v.kd_val_cnt ? (size_t)v.n : 0};
+    const void *src[14] = {v.kd_key_off, v.kd_keys, v.kd_val_off, v.kd_vals, v.kd_k2v_off, v.kd_k2v,
+                           v.rd_rng_off, v.rd_rng_start, v.rd_rng_end, v.rd_val_off, v.rd_vals, v.rd_r2v_off, v.rd_r2v,
+                           v.kd_val_cnt};
+    size_t off[14], total = 0;
+    for (int a = 0; a < 14; ++a) { off[a] = total; total += (cnt[a] * 4 + 63) & ~(size_t)63; }
     total += 64;
     HostDepsOwner *o = new (std::nothrow) HostDepsOwner();
     if (!o) return fail(s, ACCORD_ERR_OOM, "out of host memory");
@@ -922,7 +924,7 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
     }
     char *base = (char *)blk->p;
     hipError_t e = hipSuccess;
-    for (int a = 0; a < 13 && e == hipSuccess; ++a)
+    for (int a = 0; a < 14 && e == hipSuccess; ++a)
         if (cnt[a]) e = hipMemcpyAsync(base + off[a], src[a], cnt[a] * 4, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
@@ -936,12 +938,13 @@ int32_t accord_deps_download(accord_store *s, accord_deps *out)
     out->n = v.n;
     out->kd_keys_total = v.kd_keys_total; out->kd_vals_total = v.kd_vals_total; out->kd_k2v_total = v.kd_k2v_total;
     out->rd_rngs_total = v.rd_rngs_total; out->rd_vals_total = v.rd_vals_total; out->rd_r2v_total = v.rd_r2v_total;
-    uint32_t *ptr[13];
-    for (int a = 0; a < 13; ++a) ptr[a] = (uint32_t *)(base + off[a]);
+    uint32_t *ptr[14];
+    for (int a = 0; a < 14; ++a) ptr[a] = (uint32_t *)(base + off[a]);
     out->kd_key_off = ptr[0]; out->kd_keys = ptr[1]; out->kd_val_off = ptr[2]; out->kd_vals = ptr[3];
     out->kd_k2v_off = ptr[4]; out->kd_k2v = (int32_t *)ptr[5];
     out->rd_rng_off = ptr[6]; out->rd_rng_start = ptr[7]; out->rd_rng_end = ptr[8]; out->rd_val_off = ptr[9];
     out->rd_vals = ptr[10]; out->rd_r2v_off = ptr[11]; out->rd_r2v = (int32_t *)ptr[12];
+    out->kd_val_cnt = v.kd_val_cnt ? ptr[13] : nullptr;
     out->owner = o;
     return ACCORD_OK;
 }

@@ -89,6 +89,7 @@ struct accord_store {
     // batch (device)
     uint32_t n = 0, P = 0, R = 0;
     bool has_batch = false, computed = false;
+    bool kd_dense = false;         // kd_val_off / kd_vals hold the compute's txnIds densely (store_dense_keydeps)
     DevBuf msb, lsb, node, key_off, key_ord, rng_off, rng_start, rng_end;
     // work
     DevBuf pair_key, pair_ent, sort_key, sort_pair, tmp_key, tmp_val, tmp_ent, seg_start, seg_end, radix_tmp;
@@ -174,12 +175,14 @@ struct accord_store {
     DevBuf rb_local, rb_boot, rb_stale;
     bool rb_ext = false;
     DevBuf wo_eal;                 // WaitingOn.executeAtLeast per txn of the initialised batch (EalRec)
-    DevBuf rr_ovf;                 // capacity counter of the removal kernels
+    DevBuf rr_ovf;                 // removal kernels: spill header (count, max range deps, max entries) + list
+    DevBuf rr_spill;               // removal kernels: HBM scratch of the spill pass
     // execution readiness (ready.hip): the waiting set, one generation per initialised batch
     std::vector<accord_impl::ReadyGen *> rdy_gens;
     accord_impl::ReadyGen *rdy_batch_gen = nullptr;   // the current batch's generation (until the next batch)
     bool rdy_force_full = false;             // an accord_ready_update failed part-way: evaluate everything next
     uint64_t rdy_waiting = 0;
+    DevBuf rdy_spill, rdy_spill_mem;   // readiness: txns left to the removal spill pass, its HBM scratch
     DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dirty2, rdy_dlist, rdy_work, rdy_wcnt;
     uint32_t rdy_call = 0;                    // accord_ready_update calls (ids of the dirty marks)
     uint32_t rdy_seen = 0;                    // rg_epoch the last accord_ready_update saw
@@ -240,11 +243,15 @@ int32_t redundant_apply(accord_store *s);
 // The batch's current deps (device): the pipeline's own output, or its RedundantBefore union.
 struct CurDeps {
     const uint32_t *kd_key_off, *kd_keys, *kd_val_off, *kd_vals, *kd_k2v_off, *kd_k2v;
+    const uint32_t *kd_val_cnt;       // gapped KeyDeps txnIds (the compute's own output), else nullptr
     const uint32_t *rd_val_off, *rd_vals;
     const uint32_t *rd_rng_off, *rd_rng_start, *rd_rng_end, *rd_r2v_off, *rd_r2v;
     uint64_t tot_keys, tot_vals, tot_k2v, tot_rvals, tot_rngs, tot_r2v;
 };
 CurDeps cur_deps(const accord_store *s);
+// The compute's KeyDeps txnIds in dense form (kd_val_off / kd_vals: the scan of cnt_vals and the
+// compaction of vgap), for the operations that ship or copy them; once per compute
+int32_t store_dense_keydeps(accord_store *s);
 }
 using accord_impl::fail;
 

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
                 }
             }
         } else {
-            for (uint32_t v = p.kd_val_off[i]; v < p.kd_val_off[i + 1]; ++v) {
+            const uint32_t v1 = p.kd_val_cnt ? p.kd_val_off[i] + p.kd_val_cnt[i] : p.kd_val_off[i + 1];
+            for (uint32_t v = p.kd_val_off[i]; v < v1; ++v) {
                 ++cnt;
                 if (FILL) p.preds[o++] = p.kd_vals[v];
             }

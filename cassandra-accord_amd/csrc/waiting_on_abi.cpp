@@ -57,7 +57,8 @@ int32_t accord_waiting_on_compute(accord_store *s)
     p.pw_local = s->hist_tmp.as<uint32_t>();
     p.pw_carry = p.pw_local + s->P;
     p.pw_tile = accord::HISTORY_TILE;
-    p.kd_val_off = s->kd_val_off.as<uint32_t>(); p.kd_vals = s->kd_vals.as<uint32_t>();
+    p.kd_val_off = s->vub_off.as<uint32_t>(); p.kd_vals = s->vgap.as<uint32_t>();   // gapped: counts in cnt_vals
+    p.kd_val_cnt = s->cnt_vals.as<uint32_t>();
     p.rd_val_off = s->rd_val_off.as<uint32_t>(); p.rd_vals = s->rd_vals.as<uint32_t>();
     p.pred_cnt = s->pred_cnt.as<uint32_t>();
 

@@ -113,9 +113,16 @@ typedef struct {
 /* Per-txn PartialDeps, exact reference layout (KeyDeps.java:150-187, RangeDeps.java:81-99):
  * for txn i
  *   KeyDeps.keys         = kd_keys[kd_key_off[i] .. kd_key_off[i+1])
- *   KeyDeps.txnIds       = batch txns kd_vals[kd_val_off[i] .. kd_val_off[i+1])  (TxnId order)
+ *   KeyDeps.txnIds       = batch txns kd_vals[kd_val_off[i] .. kd_val_off[i] + kd_val_cnt[i])  (TxnId order)
+ *                          (kd_val_cnt == NULL: kd_vals[kd_val_off[i] .. kd_val_off[i+1]), dense)
  *   KeyDeps.keysToTxnIds = kd_k2v[kd_k2v_off[i] .. kd_k2v_off[i+1])   (the int[] verbatim)
- * and the same for RangeDeps (ranges as (rd_rng_start, rd_rng_end] pairs). */
+ * and the same for RangeDeps (ranges as (rd_rng_start, rd_rng_end] pairs, always dense).
+ * The txnIds of a compute result (accord_deps_compute / _batch / _download) are gapped: each txn's
+ * list starts at an upper bound of the lists before it (the union of its keys' witnessed entries is
+ * only known once built) and kd_val_cnt gives its length -- the reader (KeyDeps.SerializerSupport
+ * .create per txn) takes each txn's txnIds by (start, count) and never sees the gaps.
+ * kd_vals_total is the length of the kd_vals array (= kd_val_off[n]); the deps-set operations
+ * (union, slice, invert, merge, exchange, waiting-on) accept either form and produce dense sets. */
 typedef struct {
     uint32_t  n;
     uint32_t  reserved;
@@ -125,6 +132,7 @@ typedef struct {
     int32_t  *kd_k2v;
     uint32_t *rd_rng_off, *rd_rng_start, *rd_rng_end, *rd_val_off, *rd_vals, *rd_r2v_off;
     int32_t  *rd_r2v;
+    uint32_t *kd_val_cnt;       /* [n] KeyDeps.txnIds length per txn, or NULL (dense, see above) */
     void     *owner;            /* library-private */
 } accord_deps;
 
@@ -233,8 +241,9 @@ int32_t accord_redundant_before_set(accord_store *store, uint32_t m, const uint3
  * local/CommandStore.java:672-678), CommandStore.removeRedundantDependencies (:601-670) stops waiting on
  * the range deps in [bootstrappedAt, locallyAppliedOrInvalidatedBefore) of every entry their ranges
  * meet, and on those before bootstrappedAt whose ranges the bootstrapping entries cover completely
- * (RangeState.isFullyBootstrapping).  A waiting txn with more than 4096 RangeDeps txnIds, or whose
- * participants touch more than 64 entries, is ACCORD_ERR_CAPACITY there while the map is set. */
+ * (RangeState.isFullyBootstrapping).  No size limit: a waiting txn with more than 4096 RangeDeps
+ * txnIds, or whose participants touch more than 64 entries, is evaluated by a second pass with its
+ * scratch in HBM instead of LDS. */
 int32_t accord_redundant_before_set_ex(accord_store *store, uint32_t m, const uint32_t *start, const uint32_t *end,
                                        const uint64_t *start_epoch, const uint64_t *end_epoch, const uint32_t *shard_bound,
                                        const uint32_t *locally_applied_before, const uint32_t *bootstrapped_at,

@@ -47,8 +47,8 @@ def test_struct_layouts_match_header():
 int main(void){
  printf("%zu %zu %zu %zu %zu\n", sizeof(accord_store_cfg), sizeof(accord_batch), sizeof(accord_deps),
         sizeof(accord_timing), sizeof(accord_workload_cfg));
- printf("%zu %zu %zu %zu\n", offsetof(accord_deps, kd_key_off), offsetof(accord_deps, rd_r2v),
-        offsetof(accord_workload_cfg, seed), offsetof(accord_timing, pairs));
+ printf("%zu %zu %zu %zu %zu\n", offsetof(accord_deps, kd_key_off), offsetof(accord_deps, rd_r2v),
+        offsetof(accord_workload_cfg, seed), offsetof(accord_timing, pairs), offsetof(accord_deps, kd_val_cnt));
  return 0;}
 """
     with tempfile.TemporaryDirectory() as d:
@@ -62,7 +62,7 @@ int main(void){
     assert sizes == [C.sizeof(A._StoreCfg), C.sizeof(A._Batch), C.sizeof(A._Deps), C.sizeof(A._Timing),
                      C.sizeof(A._WorkloadCfg)]
     assert offs == [A._Deps.kd_key_off.offset, A._Deps.rd_r2v.offset, A._WorkloadCfg.seed.offset,
-                    A._Timing.pairs.offset]
+                    A._Timing.pairs.offset, A._Deps.kd_val_cnt.offset]
 
 
 def test_store_create_without_gpu_fails_loudly():

@@ -366,8 +366,38 @@ def test_eal_kat_oracle():
     eal_kat_run()
 
 
-def stable_stream(n, ks, seed, range_frac=0.0, sync_points=False):
-    s = generate_stream(n, 3, ks, 0.9, 0.5, seed=seed, range_frac=range_frac, range_len_max=8)
+# executeAtLeast over candidates on different nodes: t2, an EphemeralRead of key 1 (awaitsOnlyDeps),
+# has range deps t0 (executes at hlc 14 on node 13) and t1 (hlc 27 on node 9), both committed when
+# its WaitingOn is initialised; Timestamp.max keeps every field of the later one (t1, node 9).  The
+# device's running merge once combined t1's hlc with t0's node (profiles/r05_eal).
+EAL_MIX_KAT = [(10, "W", 1, None, [(0, 2)]), (11, "W", 1, None, [(0, 2)]), (12, "ER", 1, [1], None)]
+
+
+def eal_mix_run(dev=None):
+    s = mk(EAL_MIX_KAT)
+    d = Driver(s, 4, dev)
+    part = d.batch(0, 3)
+    x0 = (int(s.msb[0]), 14 << 16 | int(s.lsb[0]) & 0xFFFF, 13)
+    x1 = (int(s.msb[1]), 27 << 16 | int(s.lsb[1]) & 0xFFFF, 9)
+    d.register([0, 1, 2], STABLE, [x0, x1, None])
+    d.initialise(0, part)
+    for _ in range(4):
+        r = list(d.round())
+        if 2 in r:
+            em, el, en = d.eal
+            i = r.index(2)
+            assert (int(em[i]), int(el[i]), int(en[i])) == x1
+            return d
+        d.apply(r)
+    raise AssertionError("t2 never became ready")
+
+
+def test_eal_mixed_nodes_oracle():
+    eal_mix_run()
+
+
+def stable_stream(n, ks, seed, range_frac=0.0, sync_points=False, range_len_max=8):
+    s = generate_stream(n, 3, ks, 0.9, 0.5, seed=seed, range_frac=range_frac, range_len_max=range_len_max)
     # kinds: Read / Write / EphemeralRead (key txns); range txns keep their kind.  sync_points: also
     # SyncPoint / ExclusiveSyncPoint, key and range domain (Txn.Kind ordinals 3, 4)
     rng = np.random.default_rng(seed)
@@ -463,6 +493,12 @@ def test_gpu_eal_kat(gpu_device):
         eal_kat_run(dev)
 
 
+@pytest.mark.gpu
+def test_gpu_eal_mixed_nodes(gpu_device):
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        eal_mix_run(dev)
+
+
 def schedule_rr(s, nkeys, bsz, seed, dev=None, late_frac=0.1, rounds_per_batch=4, nent=5, remove=True):
     """Range and key txns, some committing two batches late (late_frac), and after every batch a new
     RedundantBefore map of nent entries over the keyspace with random locallyAppliedOrInvalidatedBefore
@@ -515,6 +551,31 @@ def test_schedule_rr_oracle(seed):
     out0, _ = schedule_rr(s, 30, 150, seed, remove=False)
     nb = (900 // 150) * 4                                  # rounds before the final drain
     assert sum(len(r) for r in out[:nb]) > sum(len(r) for r in out0[:nb])
+
+
+def spill_stream():
+    """Range txns up to 300 keys long over 400 keys, maps of 200 entries: most range txns touch more
+    RedundantBefore entries than the removal's LDS scratch holds (RR_MAXE = 64)."""
+    return stable_stream(700, 400, 31, 0.3, sync_points=True, range_len_max=300)
+
+
+def test_schedule_rr_spill_shape():
+    """The spill schedule really exceeds the LDS caps: some range txn's ranges meet > 64 map entries."""
+    s = spill_stream()
+    wide = [int(np.sum(s.rng_end[s.rng_off[i]:s.rng_off[i + 1]] - s.rng_start[s.rng_off[i]:s.rng_off[i + 1]]))
+            for i in range(s.n) if s.rng_off[i + 1] > s.rng_off[i]]
+    assert max(wide) > 2 * 64 * 400 // 200
+
+
+@pytest.mark.gpu
+def test_gpu_schedule_rr_spill(gpu_device):
+    """Txns over the removal's LDS caps go through the HBM spill pass: no capacity error,
+    and device == the literal oracle fold round by round, at initialise and at every evaluation."""
+    s = spill_stream()
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=400, window=WINDOW_NONE, resident=True) as dev:
+        out, d = schedule_rr(s, 400, 175, 31, dev, nent=200)
+    got = np.concatenate(out)
+    assert np.array_equal(np.sort(got), np.arange(s.n))
 
 
 @pytest.mark.gpu
