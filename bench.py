@@ -322,6 +322,9 @@ def main():
     cpu = None
     if not args.no_cpu:
         cpu = cpu_baseline(s_full, args)
+        if args.waiting_on and cpu is not None:
+            cpu["levelling_1core"] = levelling_cpu(s_full, wo.level if wo_info is not None else None,
+                                                   stage["wo_level"])
 
     line = {
         "metric": "PreAccept deps/sec (batched txns)",
@@ -712,6 +715,28 @@ def cpu_baseline(s, args):
         return out
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "txns/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
+
+
+def levelling_cpu(s, gpu_level, gpu_ms):
+    """One host core levelling the same reduced DAG the device levels (config 5): the oracle's
+    reduction of the stream (tests/oracle_lib.reduced_dag; built untimed) and or_levels_csr timed
+    alone, best of three; its levels compared with the device's."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        off, preds = oracle_lib.reduced_dag(s)
+        best, lv = None, None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            lv = oracle_lib.levels_csr(off, preds)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return {"ms": best * 1e3, "edges": int(preds.size), "cores": 1, "kind": "port",
+                "levels_equal_device": (bool(np.array_equal(lv, gpu_level)) if gpu_level is not None else None),
+                "device_wo_level_ms": gpu_ms,
+                "sample": "the whole reduced DAG of config 5 (every txn), or_levels_csr -O2, best of 3"}
+    except Exception as e:  # pragma: no cover
+        return {"ms": None, "sample": f"failed: {e}"}
 
 
 if __name__ == "__main__":

@@ -390,13 +390,10 @@ int32_t redundant_apply(accord_store *s)
     parts[1].rd_r2v = r.r.as<int32_t>();
     DepSet &o = next_set(s);
     // the redundant deps are RangeDeps only: the KeyDeps side is the computed one verbatim, and a
-    // RangeDeps side with an empty part is the other part (ACCORD_RB_UNION=1: always the union)
-    const char *ru = getenv("ACCORD_RB_UNION");
-    const bool always = ru && ru[0] == '1';
-    if (always) RC(union_side(s, parts, 2, false, o, true));
-    else RC(copy_side(s, parts[0], false, o));
-    if (!always && parts[0].rd_rngs_total == 0) RC(copy_side(s, parts[1], true, o));
-    else if (!always && tot[0] == 0) RC(copy_side(s, parts[0], true, o));
+    // RangeDeps side with an empty part is the other part
+    RC(copy_side(s, parts[0], false, o));
+    if (parts[0].rd_rngs_total == 0) RC(copy_side(s, parts[1], true, o));
+    else if (tot[0] == 0) RC(copy_side(s, parts[0], true, o));
     else RC(union_side(s, parts, 2, true, o, true));
     HIPCHECK(s, hipStreamSynchronize(st));
     publish(s, o, n);

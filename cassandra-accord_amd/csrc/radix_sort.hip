@@ -170,92 +170,6 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
 inline int rs_items(uint32_t n) { return n < RS_SMALL_N ? 4 : RS_ITEMS_MAX; }
 inline uint32_t rs_tiles(uint32_t n) { return (n + rs_tile(rs_items(n)) - 1) / rs_tile(rs_items(n)); }
 
-// ---- a resident store's batch joining its carried history: sort the batch, merge ----
-// The carry is key-major already (TxnId order inside a key); the batch's pairs are in TxnId order.
-// One workgroup sorts the batch's (key << ib | pair index) composites in LDS (bitonic: the index
-// keeps the sort stable), then every entry of carry and batch finds its place in the merged
-// history by a binary search in the other run: carry entry i of key k goes to i + #(batch keys < k),
-// batch entry j of key k to j + #(carry keys <= k) -- the carry's entries of a key stay first, as
-// the stable sort of [carry | batch] put them.
-namespace {
-constexpr uint32_t MS_MAX = 16384;
-constexpr int MS_THREADS = 1024;
-
-__global__ __launch_bounds__(MS_THREADS) void ms_batch_sort_kernel(uint32_t P, uint32_t ib,
-                                                                   const uint32_t *__restrict__ bkey,
-                                                                   uint32_t *__restrict__ comp)
-{
-    __shared__ uint32_t sh[MS_MAX];
-    uint32_t N = 1;
-    while (N < P) N <<= 1;
-    for (uint32_t i = threadIdx.x; i < N; i += MS_THREADS) sh[i] = i < P ? (bkey[i] << ib) | i : 0xFFFFFFFFu;
-    __syncthreads();
-    for (uint32_t k = 2; k <= N; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < N; i += MS_THREADS) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const uint32_t a = sh[i], b = sh[l];
-                    const bool up = (i & k) == 0;
-                    if (up ? a > b : a < b) { sh[i] = b; sh[l] = a; }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (uint32_t i = threadIdx.x; i < P; i += MS_THREADS) comp[i] = sh[i];
-}
-
-__global__ __launch_bounds__(256) void ms_merge_kernel(uint32_t C, uint32_t P, uint32_t ib,
-                                                       const uint32_t *__restrict__ ckey, const uint32_t *__restrict__ cent,
-                                                       const uint32_t *__restrict__ comp, const uint32_t *__restrict__ bent,
-                                                       uint32_t *__restrict__ sort_key, uint32_t *__restrict__ sort_pair,
-                                                       uint32_t *__restrict__ hist)
-{
-    const uint32_t mask = (1u << ib) - 1u;
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < C + P; x += gridDim.x * blockDim.x) {
-        uint32_t k, pair, ent, pos;
-        if (x < C) {
-            k = ckey[x];
-            const uint32_t c0 = k << ib;
-            uint32_t lo = 0, hi = P;                      // batch composites below key k
-            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (comp[m] < c0) lo = m + 1; else hi = m; }
-            pos = x + lo; pair = x; ent = cent[x];
-        } else {
-            const uint32_t j = x - C, c = comp[j], q = c & mask;
-            k = c >> ib;
-            uint32_t lo = 0, hi = C;                      // carry keys <= k
-            while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (ckey[m] <= k) lo = m + 1; else hi = m; }
-            pos = j + lo; pair = C + q; ent = bent[q];
-        }
-        sort_key[pos] = k;
-        sort_pair[pos] = pair;
-        hist[pos] = ent;
-    }
-}
-} // namespace
-
-bool merge_join_fits(uint32_t P, int bits)
-{
-    uint32_t ib = 0;
-    while ((1u << ib) < P) ++ib;
-    return P >= 1 && P <= MS_MAX && bits + (int)ib <= 32;
-}
-
-void merge_join_batch(const uint32_t *ckey, const uint32_t *cent, uint32_t C, const uint32_t *bkey,
-                      const uint32_t *bent, uint32_t P, uint32_t *comp_tmp, uint32_t *sort_key, uint32_t *sort_pair,
-                      uint32_t *hist, hipStream_t s)
-{
-    uint32_t ib = 0;
-    while ((1u << ib) < P) ++ib;
-    hipLaunchKernelGGL(ms_batch_sort_kernel, dim3(1), dim3(MS_THREADS), 0, s, P, ib, bkey, comp_tmp);
-    const uint32_t total = C + P;
-    uint32_t b = (total + 255) / 256;
-    if (b > 8192) b = 8192;
-    hipLaunchKernelGGL(ms_merge_kernel, dim3(b), dim3(256), 0, s, C, P, ib, ckey, cent, comp_tmp, bent, sort_key,
-                       sort_pair, hist);
-}
-
 size_t radix_sort_temp_bytes(uint32_t n)
 {
     uint32_t tiles = rs_tiles(n);
@@ -286,11 +200,8 @@ void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t
     int passes = (bits + RS_MAX_BITS - 1) / RS_MAX_BITS;
     // the narrower digit first: the first pass moves two arrays (keys, entries) and the second three,
     // and the 9-bit downsweep is the slower one (config 2, 17-bit keys: 8 + 9 bits sorts in 0.212 ms
-    // against 0.224 for 9 + 8, profiles/r04_b/sort_ab.txt).  Dev aids (A/B): ACCORD_RS_LOWFIRST=0
-    // the wider digit first; ACCORD_RS_PASSES=k more passes of fewer bits (3 passes: 0.244 ms)
-    if (const char *e = getenv("ACCORD_RS_PASSES")) { const int k = atoi(e); if (k > passes && k <= bits) passes = k; }
-    const char *lf = getenv("ACCORD_RS_LOWFIRST");
-    const bool low_first = !(lf && lf[0] == '0');
+    // against 0.224 for 9 + 8, profiles/r04_b/sort_ab.txt; 3 passes of fewer bits: 0.244 ms)
+    const bool low_first = true;
     // ping-pong so that the last pass lands in *_out; vals_in == nullptr means identity values
     const uint32_t *ki = keys_in, *vi = vals_in, *ei = ents_in;
     int shift = 0;

@@ -1161,10 +1161,9 @@ void launch_range_carry(const RangeDepsParams &p, uint32_t R, uint32_t thr, uint
 
 static uint32_t rk_blocks(uint32_t nrt)
 {
-    // grid cap (ACCORD_RK_BLOCKS for A/B): 32768 blocks (about a wave per range txn at config 3) put
-    // config 3 at 8.03 ms against 8.40 with 4096, 8.06 with 16384 and 8.13 with 65536 (profiles/r04_b/rangekeys_ab.txt)
-    uint32_t cap = 32768u;
-    if (const char *e = getenv("ACCORD_RK_BLOCKS")) { const uint32_t v = (uint32_t)strtoul(e, nullptr, 10); if (v >= 256) cap = v; }
+    // grid cap: 32768 blocks (about a wave per range txn at config 3) put config 3 at 8.03 ms against
+    // 8.40 with 4096, 8.06 with 16384 and 8.13 with 65536 (profiles/r04_b/rangekeys_ab.txt)
+    const uint32_t cap = 32768u;
     uint32_t b = (nrt + RK_WAVES - 1) / RK_WAVES;
     return b > cap ? cap : b;
 }

@@ -862,9 +862,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     }
     // the tables change only when the generations or the buffers they point at do (the per-call
     // epoch and id go to the filter as arguments): re-sent only then
-    const char *rs = getenv("ACCORD_READY_RESEND");           // dev aid (A/B): 1 = send every call
     // (and after a call that failed part-way: force)
-    if ((rs && rs[0] == '1') || force || s->rdy_tab_last.size() != tab_bytes || s->rdy_tab_dev != s->rdy_launch.p ||
+    if (force || s->rdy_tab_last.size() != tab_bytes || s->rdy_tab_dev != s->rdy_launch.p ||
         std::memcmp(s->rdy_tab_last.data(), tabs.data(), tab_bytes) != 0) {
         std::memcpy(s->rdy_tab_host, tabs.data(), tab_bytes);
         HIPCHECK(s, hipMemcpyAsync(s->rdy_launch.p, s->rdy_tab_host, tab_bytes, hipMemcpyHostToDevice, st));

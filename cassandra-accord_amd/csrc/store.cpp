@@ -399,12 +399,7 @@ int32_t accord_deps_compute(accord_store *s)
         }
         accord::launch_fill_words(fl, st);
     }
-    // ACCORD_MERGE_JOIN=1: a resident store's batch of a few thousand pairs joins the key-major carry
-    // by a merge (accord::merge_join_batch) instead of a re-sort of [carry | batch]; off until its
-    // one-workgroup batch sort beats the radix passes (measured 126 us vs ~40 us, profiles/r04_b)
-    const char *mj = getenv("ACCORD_MERGE_JOIN");
-    const bool merge = C && accord::merge_join_fits(P, bits_for(nkeys - 1)) && mj && mj[0] == '1';
-    if (C && !merge) {
+    if (C) {
         HIPCHECK(s, hipMemcpyAsync(s->pair_key.p, s->cy_key.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
         HIPCHECK(s, hipMemcpyAsync(s->pair_ent.p, s->cy_ent.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
     }
@@ -437,12 +432,7 @@ int32_t accord_deps_compute(accord_store *s)
         bound_l = s->bound_l.as<uint32_t>(); bound_g = s->bound_g.as<uint32_t>(); pair_bound = s->pair_bound.as<uint32_t>();
     }
     record(s, EV_VALIDATE);
-    if (merge)
-        accord::merge_join_batch(s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), C, s->pair_key.as<uint32_t>() + C,
-                                 s->pair_ent.as<uint32_t>() + C, P, s->tmp_key.as<uint32_t>(), s->sort_key.as<uint32_t>(),
-                                 s->sort_pair.as<uint32_t>(), s->hist.as<uint32_t>(), st);
-    else
-        accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
+    accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
                                  s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
                                  s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), PH,
                                  bits_for(nkeys - 1), s->radix_tmp.p, s->scan_tmp.p, st);
@@ -505,10 +495,7 @@ int32_t accord_deps_compute(accord_store *s)
     }
     rp.n_range_txns = nrt; rp.range_txns = s->range_txns.as<uint32_t>();
     rp.rk_cls = s->rk_cls.as<uint32_t>();
-    {
-        const char *e = getenv("ACCORD_RK_BITMAP");       // A/B: 0 = the sort for every body
-        rp.rk_bitmap = (e && e[0] == '0') ? 0u : 1u;
-    }
+    rp.rk_bitmap = 1u;          // span-bitmap union where a body spans < 4096 txns (else the sort)
     rp.cnt_rngs = s->cnt_rngs.as<uint32_t>(); rp.cnt_vals = s->cnt_rvals.as<uint32_t>(); rp.cnt_r2v = s->cnt_r2v.as<uint32_t>();
     // range txns' KeyDeps: exact txnIds count into the upper-bound array (their bound is exact)
     rp.cnt_keys = s->cnt_keys.as<uint32_t>(); rp.cnt_vals_k = s->cnt_vub.as<uint32_t>(); rp.cnt_k2v = s->cnt_k2v.as<uint32_t>();
@@ -560,13 +547,10 @@ int32_t accord_deps_compute(accord_store *s)
     }
     record(s, EV_SCAN);
     // the fast fill's per-txn records need only the offsets: built while the host reads the sizes
-    // (ACCORD_RECS_EARLY=0: after, for A/B)
     HIPCHECK(s, s->fk_recs.ensure(accord::keydeps_fast_temp_bytes(n)));
     kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.vub_off = s->vub_off.as<uint32_t>();
     kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
-    const char *re = getenv("ACCORD_RECS_EARLY");
-    const bool recs_early = !(re && re[0] == '0');
-    if (recs_early) accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
+    accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
 
@@ -621,8 +605,6 @@ int32_t accord_deps_compute(accord_store *s)
     kp.big_list = kp.big_count + 16;
     kp.big_wex = s->bk_wex.as<uint32_t>();
     kp.tiny = (uint64_t)P <= 2ull * n ? 1u : 0u;      // <= 2 keys per txn on average: a store's key block
-    if (const char *e = getenv("ACCORD_TINY")) kp.tiny = e[0] == '1' ? 1u : 0u;   // dev aid: force on / off
-    if (!recs_early) accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
     accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
     record(s, EV_FILL);
     if (nrt) {
@@ -703,11 +685,6 @@ int32_t accord_deps_compute(accord_store *s)
             s->prev_msb = s->b_last_msb; s->prev_lsb = s->b_last_lsb; s->prev_node = s->b_last_node;
         }
         s->b_registered = true;   // computing it again would register it twice
-    }
-    if (getenv("ACCORD_FILL_STATS")) {                 // dev aid: txns the fast fill handed on
-        uint32_t fb = 0;
-        HIPCHECK(s, hipMemcpy(&fb, kp.fb_count, 4, hipMemcpyDeviceToHost));
-        fprintf(stderr, "fill: %u of %u txns took the general kernel\n", fb, n);
     }
 
     if (s->events) {

@@ -1040,6 +1040,20 @@ int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level, uint32_t *wo_of
     return 0;
 }
 
+int or_levels_csr(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t lv = 0;
+        for (uint32_t q = pred_off[i]; q < pred_off[i + 1]; ++q) {
+            const uint32_t p = preds[q];
+            if (p >= i) return -1;
+            if (level[p] + 1 > lv) lv = level[p] + 1;
+        }
+        level[i] = lv;
+    }
+    return 0;
+}
+
 /* Commands.initialiseWaitingOn + the initial updateWaitingOn (see oracle.h).  Txn.Kind.awaitsOnlyDeps
  * (primitives/Txn.java:211-214): ExclusiveSyncPoint, EphemeralRead. */
 int or_initialise_waiting_on(const or_deps *d, uint32_t n, const uint64_t *lsb, const uint64_t *own_msb,

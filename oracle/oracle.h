@@ -167,6 +167,11 @@ uint32_t or_stab_key(uint32_t nr, const uint32_t *rs, const uint32_t *re, uint32
 int or_waiting_on(const or_deps *d, uint32_t n, uint32_t *level,
                   uint32_t *wo_off /* [n+1] */, uint64_t **wo_words /* malloc'd */);
 
+/* Levelling alone over a predecessor CSR in txn order (every pred p of i has p < i): level[i] = 0
+ * without preds, else 1 + max level(p).  The CPU baseline of the device levelling of config 5's
+ * reduced DAG (bench.py --config 5); returns -1 when a pred does not precede its txn. */
+int or_levels_csr(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level);
+
 /* Commands.initialiseWaitingOn (local/Commands.java:735-753) with its initial updateWaitingOn
  * (:755-830; WaitingOn.Update, local/Command.java:1403-1600) for the n txns of one batch of a
  * registered-status store: deps d hold global positions; status/emsb/elsb/enode give every

@@ -69,6 +69,7 @@ def lib():
         L.or_initialise_waiting_on.argtypes = [C.POINTER(_OrDeps), C.c_uint32, _u64p, _u64p, _u64p, _i32p, _u8p,
                                                _u64p, _u64p, _i32p, _u32p, C.POINTER(_u64p), C.POINTER(_u64p)]
         L.or_levels_cfk.argtypes = [C.POINTER(_OrStream), C.POINTER(_OrDeps), _u32p]
+        L.or_levels_csr.argtypes = [C.c_uint32, _u32p, _u32p, _u32p]
         L.or_deps_union.argtypes = [C.c_uint32, C.POINTER(_OrDeps), C.POINTER(_OrDeps)]
         L.or_stream_deps_stores.argtypes = [C.POINTER(_OrStream), C.c_uint32, _u32p, C.c_int, C.POINTER(_OrDeps)]
         L.or_deps_slice.argtypes = [C.POINTER(_OrDeps), _u32p, _u32p, _u32p, C.c_uint32, C.POINTER(_OrDeps)]
@@ -303,6 +304,60 @@ def stab_key(starts, ends, key):
     out = np.zeros(max(1, len(rs)), dtype=np.uint32)
     c = lib().or_stab_key(len(rs), rs.ctypes.data_as(_u32p), re.ctypes.data_as(_u32p), key, out.ctypes.data_as(_u32p))
     return out[:c].copy()
+
+
+def reduced_dag(s: Stream):
+    """The reduced WaitingOn DAG of a key-only Read/Write stream: on each key a txn
+    keeps the last Write before it and, when it is a Write, the Reads since that Write -- every other
+    dep on the key is implied through them (a Write depends on everything before it in its slice).
+    Independent of the window: the slice [lcw, i) always holds the key's last Write before i.
+    Returns the predecessor CSR (pred_off [n+1], preds) in txn order."""
+    n = s.n
+    kind = ((s.lsb >> np.uint64(1)) & np.uint64(7)).astype(np.int64)
+    if np.any((s.lsb & np.uint64(1)) != 0) or np.any(kind > 1):
+        raise ValueError("reduced_dag: key Read/Write streams only")
+    ko = s.key_off.astype(np.int64)
+    txn = np.repeat(np.arange(n, dtype=np.int64), np.diff(ko))
+    keys = s.key_ord.astype(np.int64)
+    w = kind[txn] == 1
+    order = np.lexsort((txn, keys))                      # key-major, TxnId order within a key
+    k_s, t_s, w_s = keys[order], txn[order], w[order]
+    idx = np.arange(order.size)
+    first = np.r_[True, k_s[1:] != k_s[:-1]]
+    seg = np.cumsum(first) - 1
+    seg_lo = np.flatnonzero(first)[seg]
+    seg_hi = np.r_[np.flatnonzero(first)[1:], order.size][seg]
+    last_w = np.maximum.accumulate(np.where(w_s, idx, -1))
+    prev_w = np.r_[-1, last_w[:-1]]
+    prev_w = np.where(prev_w >= seg_lo, prev_w, -1)
+    m = prev_w >= 0                                      # last Write before the entry
+    src = [t_s[prev_w[m]]]
+    dst = [t_s[m]]
+    next_w = np.minimum.accumulate(np.where(w_s, idx, order.size)[::-1])[::-1]
+    nxt = np.r_[next_w[1:], order.size]                  # first Write after the entry
+    r = (~w_s) & (nxt < seg_hi)                          # a Read -> the next Write on its key
+    src.append(t_s[r])
+    dst.append(t_s[nxt[r]])
+    src = np.concatenate(src)
+    dst = np.concatenate(dst)
+    o = np.lexsort((src, dst))
+    src, dst = src[o], dst[o]
+    off = np.zeros(n + 1, np.int64)
+    np.add.at(off, dst + 1, 1)
+    return np.cumsum(off).astype(np.uint32), src.astype(np.uint32)
+
+
+def levels_csr(pred_off: np.ndarray, preds: np.ndarray) -> np.ndarray:
+    """or_levels_csr: level[i] = 0 without preds, else 1 + max level(p) (one core, txn order)."""
+    n = int(pred_off.size) - 1
+    pred_off = np.ascontiguousarray(pred_off, np.uint32)
+    preds = np.ascontiguousarray(preds, np.uint32)
+    level = np.zeros(max(1, n), np.uint32)
+    rc = lib().or_levels_csr(n, pred_off.ctypes.data_as(_u32p), preds.ctypes.data_as(_u32p),
+                             level.ctypes.data_as(_u32p))
+    if rc != 0:
+        raise OracleError(rc)
+    return level[:n]
 
 
 def waiting_on(p: PartialDeps):

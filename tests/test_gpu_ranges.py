@@ -86,12 +86,12 @@ def test_mixed_kinds_vs_literal(gpu_device, seed, kinds_p):
     assert got.first_difference(want) is None, got.first_difference(want)
 
 
-@pytest.mark.parametrize("env", [{"ACCORD_RT_REUSE": "1"}, {"ACCORD_RT_REUSE": "0"},
-                                 {"ACCORD_RK_BITMAP": "0"}, {"ACCORD_RK_BITMAP": "1"}],
-                         ids=["hit-reuse", "hit-rescan", "union-sort", "union-bitmap"])
+@pytest.mark.parametrize("env", [{"ACCORD_RT_REUSE": "1"}, {"ACCORD_RT_REUSE": "0"}],
+                         ids=["hit-reuse", "hit-rescan"])
 def test_range_pass_variants_vs_literal(gpu_device, monkeypatch, env):
-    """The RangeDeps fill with the count pass's hits reused or rescanned, and the range txns' union
-    by span bitmap or by sort, all equal to the literal oracle (knobs read per compute)."""
+    """The RangeDeps fill with the count pass's hits reused or rescanned (the rescan is also the
+    path of a txn whose hits overflow the count pass's slots), both equal to the literal oracle
+    (knob read per compute)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     for seed, W, rl in ((21, 64, 100), (22, 256, 1000), (23, 16, 30)):
