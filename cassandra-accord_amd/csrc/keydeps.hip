@@ -1111,11 +1111,11 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
             const uint32_t wmask = witness_mask(kind);
             const uint32_t nb = SPAN - readlane(a.rec, 7);   // map byte of txn j: j + nb (< SPAN iff near)
             uint32_t F = 0;                           // far deps (older than the near span)
-            uint32_t fidx[FK_CB];
             if (!fallback) {
+                // each candidate's verdict replaces it in ea[]: KD_NONE (not witnessed), its near map
+                // byte (< SPAN), or KD_FAR | its far-list index -- phase 2 reads it back
 #pragma unroll
                 for (int cc = 0; cc < FK_CB; ++cc) {
-                    fidx[cc] = 0;
                     if ((uint32_t)cc * 64 >= rta) break;   // wave-uniform
                     const uint32_t ev = ea[cc];
                     const uint32_t j = ev & ENT_TXN_MASK;
@@ -1123,13 +1123,17 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                     const uint32_t off = j + nb;
                     const bool nr = wit && off < SPAN;
                     if (nr) map[off] = 1;
+                    uint32_t pv = nr ? off : KD_NONE;
                     const uint64_t fb = __ballot(wit && !nr);
                     if (fb) {                             // wave-uniform
                         const uint32_t f = F + (uint32_t)__popcll(fb & lt);
-                        if (wit && !nr && f < 64) fr[f] = j;
-                        fidx[cc] = f;
+                        if (wit && !nr) {
+                            if (f < 64) fr[f] = j;
+                            pv = KD_FAR | f;
+                        }
                         F += (uint32_t)__popcll(fb);
                     }
+                    ea[cc] = pv;
                 }
                 fallback = F > 64;
             }
@@ -1189,11 +1193,10 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
 #pragma unroll
             for (int cc = 0; cc < FK_CB; ++cc) {
                 if ((uint32_t)cc * 64 >= rta) break;
-                const uint32_t ev = ea[cc];
-                const uint32_t j = ev & ENT_TXN_MASK;
-                const bool wit = ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;   // p1
-                const uint32_t off = j + nb;
-                const bool nr = wit && off < SPAN;
+                const uint32_t pv = ea[cc];                            // phase 1's verdict
+                const bool wit = pv != KD_NONE;
+                const bool nr = pv < SPAN;
+                const uint32_t off = pv, j = pv - nb;                  // (near only)
                 const uint32_t src = (nr ? off : 0u) / BPL;            // the word owner of the byte
                 const uint32_t ob = (nr ? off : 0u) % BPL;
                 uint32_t rank;
@@ -1205,7 +1208,7 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                     const uint32_t wpre = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)pre);
                     rank = wpre + (uint32_t)__popc(wbits & ((1u << ob) - 1u));
                 }
-                if (F && wit && !nr) rank = fr[fidx[cc]];
+                if (F && wit && !nr) rank = fr[pv & ~KD_FAR];
                 const uint64_t wb = __ballot(wit);
                 if (wit) {
                     stg(p.kd_k2v, k2v_base + kc + run + (uint32_t)__popcll(wb & lt), (int32_t)rank);
