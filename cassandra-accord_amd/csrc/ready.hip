@@ -270,6 +270,9 @@ struct ReadyParams {
     StatusView v;
     uint32_t full;                    // the generation is new: evaluate every txn of it
     const uint32_t *chg, *dirty;      // by position: change epoch; by key: id of the call it was dirty in
+    // setAppliedAndPropagate (local/Command.java:1569-1583): released Range-domain txns' final
+    // appliedOrInvalidated (positions), per position pv_at = 1 + pool start (0: none), pv_len
+    uint32_t *pv_at, *pv_len, *pv_pool, *pv_cnt;
 };
 
 // the TxnId of global position g (the store's TxnId table is in stream order)
@@ -477,13 +480,74 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, ui
         auto cand = [&](const Ts &x) {
             if (!eh || tcmp(ev, x) < 0) { ev = x; eh = true; }
         };
+        // setAppliedAndPropagate: an applied range dep whose own WaitingOn recorded applied /
+        // invalidated txnIds clears those bits too, and updateWaitingOn's reverse walk
+        // (forEachWaitingOnId) then skips them -- an order the lane-parallel evaluation does not keep.
+        // A txn with such a dep walks its range-dep bits in that order on one lane (rare: the dep
+        // must be a released Range-domain txn with a set appliedOrInvalidated bit).
+        const uint32_t *rv = p.rd_vals + p.rd_off[t];
+        bool seqr = false;
+        if (R && p.pv_at) {
+            for (uint32_t q = 0; q < nw && q * 64u < R && !seqr; ++q) {
+                const unsigned long long rclr = removal ? rr_clear(rl, T, q) : 0ull;
+                const unsigned long long old = p.words[w0 + q] & ~rclr;
+                const uint32_t b = q * 64u + lane;
+                bool pr = false;
+                if (b < R && ((old >> lane) & 1ull)) {
+                    const uint32_t d = rv[b];
+                    pr = status_of(p.v, d) == ST_APPLIED && p.pv_at[d] != 0u &&
+                         (only_deps || tcmp(exec_of(p.v, d), ex) <= 0);
+                }
+                seqr = __ballot(pr) != 0ull;
+            }
+        }
+        if (seqr) {
+            for (uint32_t q = 0; q < nw && q * 64u < R; ++q) {             // the removal first, as below
+                const unsigned long long rclr = removal ? rr_clear(rl, T, q) : 0ull;
+                if (rclr && lane == 0) p.words[w0 + q] &= ~rclr;
+            }
+            if (lane == 0) {
+                for (uint32_t j = R; j-- > 0;) {
+                    const uint32_t q = j >> 6;
+                    const unsigned long long bit = 1ull << (j & 63u), wq = p.words[w0 + q];
+                    if (!(wq & bit)) continue;
+                    const uint32_t d = rv[j], ds = status_of(p.v, d);
+                    if (only_deps && ds >= ST_COMMITTED && ds <= ST_APPLIED) {   // updateExecuteAtLeast
+                        const Ts de = exec_of(p.v, d);
+                        if (tcmp(de, own) > 0) cand(de);
+                    }
+                    if (ds < ST_COMMITTED) continue;                           // !hasBeen(PreCommitted)
+                    bool clr = false, app = false;
+                    if (ds >= ST_INVALID) clr = app = true;
+                    else if (!only_deps && tcmp(exec_of(p.v, d), ex) > 0) clr = true;
+                    else if (ds == ST_APPLIED) clr = app = true;
+                    if (!clr) continue;
+                    p.words[w0 + q] = wq & ~bit;
+                    if (app && rdom) p.aoi[w0 + q] |= bit;
+                    if (!(ds == ST_APPLIED && app) || p.pv_at[d] == 0u) continue;
+                    // forEachIntersection(propagate.txnIds, txnIds): setAppliedOrInvalidated on ours
+                    const uint32_t *L = p.pv_pool + (p.pv_at[d] - 1u);
+                    for (uint32_t a = 0, nL = p.pv_len[d]; a < nL; ++a) {
+                        uint32_t lo = 0, hi = R;
+                        while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (rv[m] < L[a]) lo = m + 1; else hi = m; }
+                        if (lo >= R || rv[lo] != L[a]) continue;
+                        const uint32_t q2 = lo >> 6;
+                        const unsigned long long b2 = 1ull << (lo & 63u), w2 = p.words[w0 + q2];
+                        if (!(w2 & b2) || (rdom && (p.aoi[w0 + q2] & b2))) continue;   // :1551-1567
+                        p.words[w0 + q2] = w2 & ~b2;
+                        if (rdom) p.aoi[w0 + q2] |= b2;
+                    }
+                }
+            }
+            __threadfence();              // lane 0's words / aoi before the lanes read them below
+        }
         bool waiting = false;
         for (uint32_t q = 0; q < nw; ++q) {
             const unsigned long long rclr = removal ? rr_clear(rl, T, q) : 0ull;
             const unsigned long long old = p.words[w0 + q] & ~rclr;
             const uint32_t b = q * 64u + lane;
             bool clear = false, applied = false;
-            if (b < R + K && ((old >> lane) & 1ull)) {
+            if (b < R + K && ((old >> lane) & 1ull) && !(seqr && b < R)) {   // seqr: range bits walked above
                 if (b < R) {                                             // range-dep bit
                     const uint32_t d = p.rd_vals[p.rd_off[t] + b], ds = status_of(p.v, d);
                     if (only_deps && ds >= ST_COMMITTED && ds <= ST_APPLIED) {   // updateExecuteAtLeast
@@ -562,6 +626,28 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, ui
             eal_merge(ea, eal_wave_max(eh, ev));
             if (lane == 0 && ea.has) p.eal[t] = ea;
         }
+        if (!waiting && st == ST_STABLE && rdom && R && p.pv_pool) {
+            // released: its appliedOrInvalidated stays for setAppliedAndPropagate (positions, ascending)
+            __threadfence();
+            uint32_t cntv = 0;
+            for (uint32_t q = 0; q < nw && q * 64u < R; ++q) {
+                const unsigned long long m = R - q * 64u >= 64u ? ~0ull : ((1ull << (R - q * 64u)) - 1ull);
+                cntv += (uint32_t)__popcll(p.aoi[w0 + q] & m);
+            }
+            if (cntv) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(p.pv_cnt, cntv);
+                base = (uint32_t)__shfl((int)base, 0, 64);
+                uint32_t o = base;
+                for (uint32_t q = 0; q < nw && q * 64u < R; ++q) {
+                    const unsigned long long m = R - q * 64u >= 64u ? ~0ull : ((1ull << (R - q * 64u)) - 1ull);
+                    const unsigned long long a = p.aoi[w0 + q] & m;
+                    if ((a >> lane) & 1ull) p.pv_pool[o + (uint32_t)__popcll(a & ((1ull << lane) - 1ull))] = rv[q * 64u + lane];
+                    o += (uint32_t)__popcll(a);
+                }
+                if (lane == 0) { p.pv_len[g] = cntv; p.pv_at[g] = base + 1u; }
+            }
+        }
         if (!waiting && st == ST_STABLE && lane == 0) {
             p.done[t] = 1;
             const bool use = only_deps && ea.has;                       // Command.executesAtLeast
@@ -583,6 +669,7 @@ namespace accord_impl {
 
 struct ReadyGen {
     uint32_t n = 0, left = 0, glo = 0, ghi = 0;   // txns, not yet ready, first / last global position
+    uint64_t rvals = 0;                           // RangeDeps txnIds of its txns (setAppliedAndPropagate's pool bound)
     bool fresh = true;                            // not evaluated yet
     uint64_t words = 0;
     DevBuf g, lsb, rd_off, rd_vals, key_off, keys, val_off, vals, k2v_off, k2v, wo_off, wo, aoi, pend, until, done;
@@ -610,6 +697,9 @@ void ready_destroy(accord_store *s)
     s->rdy_waiting = 0;
     if (s->rdy_host) { (void)hipHostFree(s->rdy_host); s->rdy_host = nullptr; }
     if (s->rdy_tab_host) { (void)hipHostFree(s->rdy_tab_host); s->rdy_tab_host = nullptr; s->rdy_tab_cap = 0; }
+    s->rdy_pv_at.release(); s->rdy_pv_len.release(); s->rdy_pv_pool.release();
+    s->rdy_pv_n = 0;
+    s->rdy_pv_pos = 0;
 }
 
 // A batch's WaitingOn may be initialised again (a retry, or before and after its RedundantBefore
@@ -625,6 +715,21 @@ int32_t ready_batch_check(accord_store *s)
 }
 
 namespace {
+// a larger buffer keeping the first `used` bytes, the rest zeroed
+hipError_t grow_keep(DevBuf &b, size_t used, size_t want, hipStream_t st)
+{
+    if (want <= b.cap && b.p) return hipSuccess;
+    DevBuf nb;
+    hipError_t e = nb.ensure(std::max(want, b.cap * 2));
+    if (e == hipSuccess) e = hipMemsetAsync(nb.p, 0, nb.cap, st);
+    if (e == hipSuccess && used && b.p) e = hipMemcpyAsync(nb.p, b.p, std::min(used, b.cap), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { nb.release(); return e; }
+    b.release();
+    b = nb;
+    return hipSuccess;
+}
+
 // the generation's device copies of the batch's deps and WaitingOn; no state of the store changes
 int32_t ready_gen_fill(accord_store *s, ReadyGen *r)
 {
@@ -645,6 +750,7 @@ int32_t ready_gen_fill(accord_store *s, ReadyGen *r)
     HIPCHECK(s, copy(r->lsb, s->lsb.p, (size_t)n * 8));
     HIPCHECK(s, copy(r->rd_off, cd.rd_val_off, n1 * 4));
     HIPCHECK(s, copy(r->rd_vals, cd.rd_vals, cd.tot_rvals * 4));
+    r->rvals = cd.tot_rvals;
     HIPCHECK(s, copy(r->key_off, cd.kd_key_off, n1 * 4));
     HIPCHECK(s, copy(r->keys, cd.kd_keys, cd.tot_keys * 4));
     HIPCHECK(s, copy(r->val_off, cd.kd_val_off, n1 * 4));
@@ -745,6 +851,20 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     }
     constexpr uint32_t HDR = 64;               // rdy_out header words: ready count, dirty keys, work counts
     HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, HDR * 4, st));
+    // setAppliedAndPropagate's tables: every position of the store, and a pool for the
+    // appliedOrInvalidated of every waiting txn (bounded by its RangeDeps txnIds); the pool's fill
+    // count rides in the header (cnt[HDR - 5]) and comes back with it
+    {
+        uint64_t pool_need = s->rdy_pv_n;
+        for (accord_impl::ReadyGen *r : s->rdy_gens) pool_need += r->left ? r->rvals : 0;
+        const size_t pos_need = (size_t)s->next_global + s->n + 1;
+        HIPCHECK(s, accord_impl::grow_keep(s->rdy_pv_at, s->rdy_pv_pos * 4, pos_need * 4, st));
+        HIPCHECK(s, accord_impl::grow_keep(s->rdy_pv_len, s->rdy_pv_pos * 4, pos_need * 4, st));
+        s->rdy_pv_pos = std::min(s->rdy_pv_at.cap, s->rdy_pv_len.cap) / 4;
+        HIPCHECK(s, accord_impl::grow_keep(s->rdy_pv_pool, (size_t)s->rdy_pv_n * 4, pool_need * 4 + 4, st));
+        if (pool_need >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "appliedOrInvalidated pool exceeds 2^32 entries");
+        HIPCHECK(s, hipMemsetD32Async((hipDeviceptr_t)(s->rdy_out.as<uint32_t>() + (HDR - 5)), (int)s->rdy_pv_n, 1, st));
+    }
     // everything is re-evaluated after a new carry (batch, truncation) or RedundantBefore bound
     // (and after a call that failed part-way: its bookkeeping below may be ahead of the device)
     const bool force = s->rdy_force_full;
@@ -832,6 +952,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.full = r->fresh ? 1u : 0u;
         any_inc |= !full && !r->fresh;
         p.chg = s->rg_chg.as<uint32_t>(); p.dirty = s->rdy_dirty2.as<uint32_t>();
+        p.pv_at = s->rdy_pv_at.as<uint32_t>(); p.pv_len = s->rdy_pv_len.as<uint32_t>();
+        p.pv_pool = s->rdy_pv_pool.as<uint32_t>(); p.pv_cnt = cnt + (HDR - 5);
         r->fresh = false;
         L.gbase[L.ngen] = L.total;
         L.total += r->n;
@@ -897,6 +1019,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         HIPCHECK(s, hipStreamSynchronize(st));
     }
     const uint32_t nr = peek[0], nd = peek[HDR - 1];
+    s->rdy_pv_n = peek[HDR - 5];
     if (s->rdy_stats) {                          // ACCORD_READY_STATS: diagnostic totals (ready_destroy prints)
         s->rdy_stats[0] += 1; s->rdy_stats[1] += peek[1]; s->rdy_stats[2] += cap;
         if (any_inc && tabs.size() <= HDR - 8)

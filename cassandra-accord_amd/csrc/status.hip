@@ -664,7 +664,9 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
                                                       const uint32_t *__restrict__ rd_vals,
                                                       const uint32_t *__restrict__ wo_off, StatusView v,
                                                       unsigned long long *__restrict__ words,
-                                                      unsigned long long *__restrict__ aoi, bool pre, EalRec *__restrict__ eal)
+                                                      unsigned long long *__restrict__ aoi, bool pre, EalRec *__restrict__ eal,
+                                                      const uint32_t *__restrict__ pv_at, const uint32_t *__restrict__ pv_len,
+                                                      const uint32_t *__restrict__ pv_pool, uint32_t pv_pos)
 {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t g = txn_index[t], ost = status_of(v, g);
@@ -678,6 +680,60 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
         const uint32_t bits = R + (kd_key_off[t + 1] - kd_key_off[t]);
         const uint32_t w0 = wo_off[t], nw = wo_off[t + 1] - w0;
         EalRec ea{0, 0, 0, 0u};                            // Timestamp.nonNullOrMax over the candidates
+        // setAppliedAndPropagate: with an applied range dep whose own (released) WaitingOn recorded
+        // applied / invalidated txnIds, the visit order matters -- updateWaitingOn walks the bits in
+        // reverse (forEachWaitingOnId) and a propagated bit is never visited itself (ready.hip)
+        bool prop = false;
+        if (pv_at) {
+            for (uint32_t b = 0; b < R && !prop; ++b) {
+                if (pre && !((words[w0 + (b >> 6)] >> (b & 63u)) & 1ull)) continue;
+                const uint32_t d = rd_vals[r0 + b];
+                prop = d < pv_pos && pv_at[d] != 0u && status_of(v, d) == ST_APPLIED &&
+                       (only_deps || tcmp(exec_of(v, d), own) <= 0);
+            }
+        }
+        if (prop) {
+            for (uint32_t q = 0; q < nw; ++q) {
+                const uint32_t b0 = q * 64u;
+                const unsigned long long all = b0 + 64u <= bits ? ~0ull : ((1ull << (bits - b0)) - 1ull);
+                const unsigned long long rng = b0 >= R ? 0ull : b0 + 64u <= R ? ~0ull : ((1ull << (R - b0)) - 1ull);
+                const unsigned long long kept = pre ? words[w0 + q] : ~0ull;
+                words[w0 + q] = (all & ~rng) | (all & rng & kept);
+                aoi[w0 + q] = 0ull;
+            }
+            for (uint32_t j = R; j-- > 0;) {
+                const uint32_t q = j >> 6;
+                const unsigned long long bit = 1ull << (j & 63u), wq = words[w0 + q];
+                if (!(wq & bit)) continue;
+                const uint32_t d = rd_vals[r0 + j], st = status_of(v, d);
+                if (only_deps && st >= ST_COMMITTED && st <= ST_APPLIED) {   // updateExecuteAtLeast
+                    const Ts de = exec_of(v, d);
+                    if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0) eal_merge(ea, EalRec{de.msb, de.lsb, de.node, 1u});
+                }
+                if (st < ST_COMMITTED) continue;
+                bool clr = false, app = false;
+                if (st >= ST_INVALID) clr = app = true;
+                else if (!only_deps && tcmp(exec_of(v, d), own) > 0) clr = true;
+                else if (st == ST_APPLIED) clr = app = true;
+                if (!clr) continue;
+                words[w0 + q] = wq & ~bit;
+                if (app && range_domain) aoi[w0 + q] |= bit;
+                if (!(st == ST_APPLIED && app) || d >= pv_pos || pv_at[d] == 0u) continue;
+                const uint32_t *Lp = pv_pool + (pv_at[d] - 1u);
+                for (uint32_t a = 0, nL = pv_len[d]; a < nL; ++a) {
+                    uint32_t lo = 0, hi = R;
+                    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (rd_vals[r0 + m] < Lp[a]) lo = m + 1; else hi = m; }
+                    if (lo >= R || rd_vals[r0 + lo] != Lp[a]) continue;
+                    const uint32_t q2 = lo >> 6;
+                    const unsigned long long b2 = 1ull << (lo & 63u), w2 = words[w0 + q2];
+                    if (!(w2 & b2) || (range_domain && (aoi[w0 + q2] & b2))) continue;
+                    words[w0 + q2] = w2 & ~b2;
+                    if (range_domain) aoi[w0 + q2] |= b2;
+                }
+            }
+            eal[t] = ea;
+            continue;
+        }
         for (uint32_t q = 0; q < nw; ++q) {
             unsigned long long wv = 0, av = 0;
             const unsigned long long kept = pre ? words[w0 + q] : ~0ull;   // removeRedundantDependencies
@@ -809,7 +865,9 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
     hipLaunchKernelGGL(wo_init_kernel, dim3(grid_for(n)), dim3(256), 0, s->stream, n, s->msb.as<uint64_t>(),
                        s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
                        cd.kd_key_off, cd.rd_val_off, cd.rd_vals, wo_off, view_of(s), words, aoi, pre,
-                       s->wo_eal.as<EalRec>());
+                       s->wo_eal.as<EalRec>(), s->rdy_pv_at.as<uint32_t>(), s->rdy_pv_len.as<uint32_t>(),
+                       s->rdy_pv_pool.as<uint32_t>(),
+                       (uint32_t)std::min<size_t>(s->rdy_pv_pos, std::min(s->rdy_pv_at.cap, s->rdy_pv_len.cap) / 4));
     return ACCORD_OK;
 }
 

@@ -183,6 +183,11 @@ struct accord_store {
     bool rdy_force_full = false;             // an accord_ready_update failed part-way: evaluate everything next
     uint64_t rdy_waiting = 0;
     DevBuf rdy_spill, rdy_spill_mem;   // readiness: txns left to the removal spill pass, its HBM scratch
+    // setAppliedAndPropagate: every released Range-domain txn's final appliedOrInvalidated as the
+    // positions of its set RangeDeps txnIds (pv_at[g] = 1 + start in the pool, pv_len[g]; 0 = none)
+    DevBuf rdy_pv_at, rdy_pv_len, rdy_pv_pool, rdy_pv_cnt;
+    uint32_t rdy_pv_n = 0;                    // pool entries used (read back after every call)
+    size_t rdy_pv_pos = 0;                    // positions pv_at / pv_len cover
     DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dirty2, rdy_dlist, rdy_work, rdy_wcnt;
     uint32_t rdy_call = 0;                    // accord_ready_update calls (ids of the dirty marks)
     uint32_t rdy_seen = 0;                    // rg_epoch the last accord_ready_update saw

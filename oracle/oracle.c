@@ -2006,6 +2006,12 @@ struct or_lstore {
     int event_mode;
     uint32_t *wix;
     uint32_t wix_cap;
+    /* setAppliedAndPropagate (local/Command.java:1569-1583): the final WaitingOn.appliedOrInvalidated of
+     * every released Range-domain waiter, as the positions of its RangeDeps txnIds whose bit is set
+     * (pv_at[g] = 1 + start in pv_pool, pv_len[g] entries; 0 = none) */
+    uint32_t *pv_at, *pv_len, pv_cap_pos;
+    uint32_t *pv_pool;
+    size_t pv_n, pv_cap;
 };
 
 static void or_lstore_waiters_free(or_lstore *s);
@@ -2039,6 +2045,7 @@ void or_lstore_free(or_lstore *s)
     or_lstore_waiters_free(s);
     free(s->rr_s); free(s->rr_e); free(s->rr_local); free(s->rr_boot); free(s->rr_sep); free(s->rr_eep); free(s->rr_stale);
     free(s->wix);
+    free(s->pv_at); free(s->pv_len); free(s->pv_pool);
     free(s);
 }
 
@@ -2838,6 +2845,58 @@ static void lstore_register_unmanaged(or_lstore *s, or_waiter *x)
         if (w_test(x->words, x->nr + q) && x->pend[q] == 0) unmanaged_register(s, &s->cfks[x->keys[q]], x, q);
 }
 
+/* a released Range-domain waiter keeps its appliedOrInvalidated for setAppliedAndPropagate */
+static int pv_save(or_lstore *s, const or_waiter *x)
+{
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; j < x->nr; ++j) cnt += w_test(x->aoi, j);
+    if (!cnt) return 0;
+    if (s->pv_cap_pos < s->cap) {
+        uint32_t *a = (uint32_t *)realloc(s->pv_at, (size_t)s->cap * 4), *b;
+        if (!a) return -1;
+        s->pv_at = a;
+        b = (uint32_t *)realloc(s->pv_len, (size_t)s->cap * 4);
+        if (!b) return -1;
+        s->pv_len = b;
+        memset(s->pv_at + s->pv_cap_pos, 0, (size_t)(s->cap - s->pv_cap_pos) * 4);
+        memset(s->pv_len + s->pv_cap_pos, 0, (size_t)(s->cap - s->pv_cap_pos) * 4);
+        s->pv_cap_pos = s->cap;
+    }
+    if (s->pv_n + cnt > s->pv_cap) {
+        size_t c = s->pv_cap ? s->pv_cap : 4096;
+        while (c < s->pv_n + cnt) c *= 2;
+        uint32_t *p = (uint32_t *)realloc(s->pv_pool, c * 4);
+        if (!p) return -1;
+        s->pv_pool = p; s->pv_cap = c;
+    }
+    s->pv_at[x->g] = (uint32_t)s->pv_n + 1;
+    s->pv_len[x->g] = cnt;
+    for (uint32_t j = 0; j < x->nr; ++j)
+        if (w_test(x->aoi, j)) s->pv_pool[s->pv_n++] = x->rdeps[j];
+    return 0;
+}
+
+/* WaitingOn.setAppliedAndPropagate(dg, dg's WaitingOn) after dg's own bit was set applied: every txnId
+ * both lists hold whose appliedOrInvalidated bit dg has set takes setAppliedOrInvalidated here
+ * (forEachIntersection, utils/SortedArrays.java:1231): a waiter without appliedOrInvalidated (key
+ * domain) just stops waiting on it (removeWaitingOn), a Range-domain one also records it when it was
+ * still waiting on it (:1551-1567).  A dep whose WaitingOn this store never initialised propagates
+ * nothing. */
+static void pv_propagate(const or_lstore *s, or_waiter *x, uint32_t dg, int rdom)
+{
+    if (!s->pv_at || dg >= s->pv_cap_pos || !s->pv_at[dg]) return;
+    const uint32_t *L = s->pv_pool + (s->pv_at[dg] - 1);
+    for (uint32_t a = 0, j = 0; a < s->pv_len[dg] && j < x->nr;) {   /* both ascending */
+        if (L[a] < x->rdeps[j]) { ++a; continue; }
+        if (L[a] > x->rdeps[j]) { ++j; continue; }
+        if (w_test(x->words, j) && !(rdom && w_test(x->aoi, j))) {
+            w_clear(x->words, j);
+            if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63);
+        }
+        ++a; ++j;
+    }
+}
+
 int or_lstore_ready(or_lstore *s, uint32_t *ready_out, uint32_t *nready)
 {
     return or_lstore_ready_ex(s, ready_out, nready, NULL, NULL, NULL);
@@ -2870,7 +2929,11 @@ int or_lstore_ready_ex(or_lstore *s, uint32_t *ready_out, uint32_t *nready, uint
             if (only_deps && ds <= S_APPLIED && ts_cmp(&s->exec[dg], &s->tbl[g]) > 0) eal_merge(x, &s->exec[dg]);
             if (ds >= S_INVALID_OR_TRUNCATED) { w_clear(x->words, j); if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63); }
             else if (!only_deps && ts_cmp(&s->exec[dg], ex) > 0) w_clear(x->words, j);
-            else if (ds == S_APPLIED) { w_clear(x->words, j); if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63); }
+            else if (ds == S_APPLIED) {                     /* setAppliedAndPropagate */
+                w_clear(x->words, j);
+                if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63);
+                pv_propagate(s, x, dg, rdom);
+            }
         }
         const int managed = rdom == 0 && is_globally_visible(kind) == 1;
         for (uint32_t q = 0; q < x->nk && !s->event_mode; ++q) {   /* event mode: the events clear key bits */
@@ -2900,6 +2963,7 @@ int or_lstore_ready_ex(or_lstore *s, uint32_t *ready_out, uint32_t *nready, uint
             const ts_t *ea = only_deps && x->has_eal ? &x->eal : ex;
             if (eal_msb) { eal_msb[nout] = ea->msb; eal_lsb[nout] = ea->lsb; eal_node[nout] = ea->node; }
             ready_out[nout++] = g;
+            if (rdom && pv_save(s, x)) return -1;
             waiter_free(x);
             continue;
         }

@@ -396,6 +396,42 @@ def test_eal_mixed_nodes_oracle():
     eal_mix_run()
 
 
+# setAppliedAndPropagate (local/Command.java:1569-1583): t1, a Range-domain ExclusiveSyncPoint
+# (awaitsOnlyDeps), waits on t0, a range Write executing at hlc 30; t0 applied, t1 records it in its
+# appliedOrInvalidated and is applied.  t2, another ExclusiveSyncPoint over the same range, is
+# initialised only then: updateWaitingOn walks its range deps in reverse (forEachWaitingOnId), so t1
+# comes first and propagates t0 -- t0's bit is cleared without its executeAt ever reaching
+# updateExecuteAtLeast, and t2 executes at least at its own TxnId (hlc 12), not at t0's hlc 30.
+PROP_KAT = [(10, "W", 1, None, [(0, 4)]), (11, "XSP", 1, None, [(0, 4)]), (12, "XSP", 1, None, [(0, 4)])]
+
+
+def prop_kat_run(dev=None):
+    s = mk(PROP_KAT)
+    d = Driver(s, 6, dev)
+    part = d.batch(0, 2)
+    x0 = (int(s.msb[0]), 30 << 16 | int(s.lsb[0]) & 0xFFFF, 1)
+    d.register([0, 1], STABLE, [x0, None])
+    d.initialise(0, part)
+    assert list(d.round()) == [0]
+    d.apply([0])
+    assert list(d.round()) == [1]
+    em, el, en = d.eal
+    assert (int(em[0]), int(el[0]), int(en[0])) == x0                # t1 waited on t0 (awaitsOnlyDeps)
+    d.apply([1])
+    part2 = d.batch(2, 3)
+    assert list(part2.range_deps(0)[2]) == [0, 1], part2.range_deps(0)
+    d.register([2], STABLE)
+    d.initialise(2, part2)
+    assert list(d.round()) == [2]
+    em, el, en = d.eal
+    assert (int(em[0]), int(el[0]), int(en[0])) == (int(s.msb[2]), int(s.lsb[2]), int(s.node[2]))
+    return d
+
+
+def test_propagate_kat_oracle():
+    prop_kat_run()
+
+
 def stable_stream(n, ks, seed, range_frac=0.0, sync_points=False, range_len_max=8):
     s = generate_stream(n, 3, ks, 0.9, 0.5, seed=seed, range_frac=range_frac, range_len_max=range_len_max)
     # kinds: Read / Write / EphemeralRead (key txns); range txns keep their kind.  sync_points: also
@@ -491,6 +527,12 @@ def test_gpu_rr_kat(gpu_device):
 def test_gpu_eal_kat(gpu_device):
     with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
         eal_kat_run(dev)
+
+
+@pytest.mark.gpu
+def test_gpu_propagate_kat(gpu_device):
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=6, window=WINDOW_NONE, resident=True) as dev:
+        prop_kat_run(dev)
 
 
 @pytest.mark.gpu
