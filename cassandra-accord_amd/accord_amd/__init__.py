@@ -42,6 +42,7 @@ STORE_PROFILE = 1
 STORE_RESIDENT = 2
 WINDOW_NONE = 0xFFFFFFFF     # no status-at-time model: statuses from CommandStore.register
 KEY_END = 0xFFFFFFFF         # an open upper store bound (accord_store_cfg.store_bounds)
+READY_POLL, READY_EVENTS = 0, 1   # accord_ready_set_mode
 ST_ERASED = 8                # register(): SaveStatus Erased / Invalidated (range commands leave the range scan)
 
 EXPORTED_SYMBOLS = [
@@ -50,7 +51,7 @@ EXPORTED_SYMBOLS = [
     "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
     "accord_comm_init", "accord_comm_size", "accord_deps_exchange_merge", "accord_deps_exchange_local", "accord_shard_timing",
-    "accord_ready_update",
+    "accord_ready_update", "accord_ready_set_mode",
     "accord_waiting_on_compute", "accord_waiting_on_initialise", "accord_waiting_on_download", "accord_waiting_on_release",
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
@@ -200,6 +201,7 @@ def lib() -> C.CDLL:
         L.accord_waiting_on_compute.argtypes = [C.c_void_p]
         L.accord_waiting_on_initialise.argtypes = [C.c_void_p]
         L.accord_ready_update.argtypes = [C.c_void_p, C.POINTER(_Ready)]
+        L.accord_ready_set_mode.argtypes = [C.c_void_p, C.c_uint32]
         L.accord_waiting_on_download.argtypes = [C.c_void_p, C.POINTER(_WaitingOn)]
         L.accord_waiting_on_release.argtypes = [C.POINTER(_WaitingOn)]
         L.accord_waiting_on_release.restype = None
@@ -896,6 +898,12 @@ class CommandStore:
         statuses (registered-status stores; include/accord_deps.h accord_waiting_on_initialise)."""
         self._check(lib().accord_waiting_on_initialise(self._h))
         return self.waiting_on_download()
+
+    def ready_mode(self, events: bool):
+        """accord_ready_set_mode: ACCORD_READY_EVENTS (event-exact: key bits clear only when
+        notifyAndUpdatePending's events reach the key, replayed at registration) or ACCORD_READY_POLL
+        (the default: every call re-tests the waiting txns whose inputs changed).  Empty waiting set only."""
+        self._check(lib().accord_ready_set_mode(self._h, READY_EVENTS if events else READY_POLL))
 
     def ready_update(self):
         """Execution readiness (include/accord_deps.h accord_ready_update): re-evaluates every txn of

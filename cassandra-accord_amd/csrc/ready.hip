@@ -34,6 +34,10 @@
 // of a set bit is dirty or a range dep of a set bit changed.  A new batch or a truncation (a new carry)
 // and a txn's first evaluation evaluate everything.  oracle/oracle.c (or_lstore_ready) restates the same evaluation over
 // literal CommandsForKey objects.
+// Event-exact mode (accord_ready_set_mode ACCORD_READY_EVENTS): key bits clear only when
+// notifyAndUpdatePending's events reach the key, replayed in order by one wave per registration
+// (rd_event_kernel below); the calls then evaluate range-dep bits and release.  Equal to the
+// event-driven restatement (or_lstore_event_mode) call by call.
 #include "store_impl.h"
 #include "status_view.h"
 #include "redundant_wait.h"
@@ -45,6 +49,8 @@
 #include <vector>
 
 using namespace accord_status;
+
+#define EV_RC(expr) do { const int32_t rc_ = (expr); if (rc_ != ACCORD_OK) return rc_; } while (0)
 
 namespace {
 
@@ -273,6 +279,7 @@ struct ReadyParams {
     // setAppliedAndPropagate (local/Command.java:1569-1583): released Range-domain txns' final
     // appliedOrInvalidated (positions), per position pv_at = 1 + pool start (0: none), pv_len
     uint32_t *pv_at, *pv_len, *pv_pool, *pv_cnt;
+    uint32_t evmode;                  // event-exact mode: key bits clear on events only (rd_event_kernel)
 };
 
 // the TxnId of global position g (the store's TxnId table is in stream order)
@@ -547,7 +554,8 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, ui
             const unsigned long long old = p.words[w0 + q] & ~rclr;
             const uint32_t b = q * 64u + lane;
             bool clear = false, applied = false;
-            if (b < R + K && ((old >> lane) & 1ull) && !(seqr && b < R)) {   // seqr: range bits walked above
+            // seqr: range bits walked above; event mode: key bits clear on events only
+            if (b < R + K && ((old >> lane) & 1ull) && !(seqr && b < R) && !(p.evmode && b >= R)) {
                 if (b < R) {                                             // range-dep bit
                     const uint32_t d = p.rd_vals[p.rd_off[t] + b], ds = status_of(p.v, d);
                     if (only_deps && ds >= ST_COMMITTED && ds <= ST_APPLIED) {   // updateExecuteAtLeast
@@ -663,6 +671,401 @@ inline uint32_t grid_for_waves(uint64_t waves)
     return (uint32_t)(b < 1 ? 1 : b > 8192 ? 8192 : b);
 }
 
+
+// ---- event-exact readiness (accord_ready_set_mode(ACCORD_READY_EVENTS)) ----
+// The reference clears a key bit only when notifyAndUpdatePending's events reach the key
+// (local/CommandsForKey.java:1163-1215): a status change of txn X on key k computes k's
+// minUncommitted / next / nextWrite (:432-461) and notifies the STABLE waiters of committed[] in an
+// executeAt range that depends on the change (notify, :1501-1511, with the count test :1512-1635),
+// plus the unmanaged COMMIT / APPLY records of the key (notifyUnmanaged, :1264-1283, 1315-1360).
+// One wave replays a registration's events in order, each against the state after it: the status
+// is applied, then every key of X takes its event; device-scope fences between events make each
+// event's writes (statuses, WaitingOn words, pending records) visible to the next.  Orders the
+// reference leaves free (keys of one event, waiters of one notify) touch disjoint state.
+struct EvCtx {
+    const ReadyParams *gens;                 // the live generations (device copies)
+    uint32_t ngen;
+    const unsigned long long *wmap;          // position -> gi << 32 | t of its waiting txn (~0: none)
+    uint32_t wmap_n;
+    const uint32_t *ckey, *cent, *kseg0, *kseg1;   // the carried history (CommandsForKey), key-major
+    const uint32_t *pk_off, *pk_ent;         // position -> its carried entries
+    uint32_t pk_n;
+    const uint32_t *uk_off, *uk_slot;        // key -> the unmanaged waiters' key slots on it
+    const unsigned long long *uk_w;          //        (gi << 32 | t)
+    uint32_t nkeys, key_lo;
+    const uint32_t *kb;                      // shardRedundantBefore per key (positions), or null
+    StatusView v;
+    const uint64_t *tmsb, *tlsb;
+    const int32_t *tnode;
+    const uint32_t *tg;
+    uint32_t tx_n;
+    // registration: the events in order (statuses applied here, as reg_apply_kernel does)
+    uint32_t n;
+    const uint32_t *pos;
+    const uint8_t *status;
+    const uint64_t *emsb, *elsb;
+    const int32_t *enode;
+    uint8_t *st;
+    uint64_t *xmsb, *xlsb;
+    int32_t *xnode;
+    uint32_t *chg, *cchg;
+    uint32_t epoch;
+    uint32_t init_gi;                        // initialisation: the new generation
+    const uint32_t *tkeys;                   // truncation: the keys that lost entries
+    uint32_t ntkeys;
+};
+
+__device__ __forceinline__ Ts ev_tid(const EvCtx &c, uint32_t g)
+{
+    uint32_t lo = 0, hi = c.tx_n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (c.tg[m] < g) lo = m + 1; else hi = m;
+    }
+    return Ts{c.tmsb[lo], c.tlsb[lo], c.tnode[lo]};
+}
+
+__device__ __forceinline__ bool ev_waiter(const EvCtx &c, uint32_t g, uint32_t &gi, uint32_t &t)
+{
+    if (g >= c.wmap_n) return false;
+    const unsigned long long w = c.wmap[g];
+    if (w == ~0ull) return false;
+    gi = (uint32_t)(w >> 32); t = (uint32_t)w;
+    return !c.gens[gi].done[t];
+}
+
+// KeyDeps key slot of key (absolute ordinal) in waiter t's deps, NONE if absent
+__device__ __forceinline__ uint32_t ev_slot(const ReadyParams &p, uint32_t t, uint32_t key)
+{
+    const uint32_t a = p.key_off[t], b = p.key_off[t + 1];
+    uint32_t lo = a, hi = b;
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (p.keys[m] < key) lo = m + 1; else hi = m; }
+    return lo < b && p.keys[lo] == key ? lo - a : NONE;
+}
+
+__device__ __forceinline__ bool ev_bit(const ReadyParams &p, uint32_t t, uint32_t b)
+{
+    return (p.words[p.wo_off[t] + (b >> 6)] >> (b & 63u)) & 1ull;
+}
+
+__device__ __forceinline__ void ev_clear(const ReadyParams &p, uint32_t t, uint32_t b)
+{
+    p.words[p.wo_off[t] + (b >> 6)] &= ~(1ull << (b & 63u));
+}
+
+__device__ __forceinline__ Cand cand_xor(const Cand &c, uint32_t d)
+{
+    return Cand{(uint32_t)__shfl_xor((int)c.g, d, 64),
+                Ts{(uint64_t)__shfl_xor((long long)c.ex.msb, d, 64), (uint64_t)__shfl_xor((long long)c.ex.lsb, d, 64),
+                   __shfl_xor(c.ex.node, d, 64)}};
+}
+
+// the CommandsForKey constructor's minUncommitted, next, nextWrite of key kk (:432-461), next and
+// nextWrite nulled when minUncommitted's TxnId precedes their executeAt
+__device__ void ev_nexts(const EvCtx &c, uint32_t kk, uint32_t lane, uint32_t &mu, Cand &nx, Cand &nw)
+{
+    mu = NONE;
+    nx = Cand{NONE, {0, 0, 0}};
+    nw = Cand{NONE, {0, 0, 0}};
+    for (uint32_t x = c.kseg0[kk] + lane; x < c.kseg1[kk]; x += 64) {
+        const uint32_t e = c.cent[x], g = e & ENT_TXN_MASK, kind = e >> ENT_KIND_SHIFT;
+        const uint32_t st = kind == 2u ? ST_INVALID : status_of(c.v, g);
+        if (st < ST_COMMITTED) mu = min(mu, g);
+        else if (st < ST_APPLIED) {
+            const Cand me{g, exec_of(c.v, g)};
+            cand_min(nx, me);
+            if (kind == 1u) cand_min(nw, me);
+        }
+    }
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+        mu = min(mu, (uint32_t)__shfl_xor((int)mu, d, 64));
+        cand_min(nx, cand_xor(nx, d));
+        cand_min(nw, cand_xor(nw, d));
+    }
+    if (mu != NONE) {
+        const Ts tm = ev_tid(c, mu);
+        if (nx.g != NONE && tcmp(tm, nx.ex) < 0) nx.g = NONE;
+        if (nw.g != NONE && tcmp(tm, nw.ex) < 0) nw.g = NONE;
+    }
+}
+
+// notify's count test for waiter (gi, t) on key slot q of key kk (expectMissingCount == |missing|):
+// no unapplied committed txn of a witnessed kind executes before it on the key, and none of its
+// deps on the key is uncommitted (wave-uniform result)
+__device__ bool ev_managed_ok(const EvCtx &c, const ReadyParams &p, uint32_t t, uint32_t q, uint32_t kk, uint32_t lane)
+{
+    const uint32_t g = p.g[t], kind = (uint32_t)(p.lsb[t] >> 1) & 7u, wmask = witness_mask(kind);
+    const Ts ex = exec_of(c.v, g);
+    bool blocked = false;
+    for (uint32_t x = c.kseg0[kk] + lane; x < c.kseg1[kk]; x += 64) {
+        const uint32_t e = c.cent[x], u = e & ENT_TXN_MASK, uk = e >> ENT_KIND_SHIFT;
+        if (uk == 2u) continue;
+        const uint32_t st = status_of(c.v, u);
+        if (st < ST_COMMITTED || st >= ST_APPLIED) continue;
+        const uint32_t cls = kind_class(uk), gate = cls == 0u ? 0u : cls == 1u ? 1u : 3u;
+        if (((wmask >> gate) & 1u) && tcmp(exec_of(c.v, u), ex) < 0) blocked = true;
+    }
+    const uint32_t kbound = c.kb ? c.kb[kk] : 0u;
+    const uint32_t K = p.key_off[t + 1] - p.key_off[t], hb = p.k2v_off[t];
+    const uint32_t d0 = q == 0 ? K : (uint32_t)p.k2v[hb + q - 1], d1 = (uint32_t)p.k2v[hb + q];
+    for (uint32_t x = d0 + lane; x < d1; x += 64) {
+        const uint32_t u = p.vals[p.val_off[t] + p.k2v[hb + x]];
+        if (u >= kbound && status_of(c.v, u) < ST_COMMITTED) blocked = true;
+    }
+    return __ballot(blocked) == 0ull;
+}
+
+// notify(from, to) (:1501-1511): the STABLE waiters of committed[] executing in [from, to] on kk
+__device__ void ev_notify(const EvCtx &c, uint32_t kk, bool has_from, const Ts &from, bool has_to, const Ts &to,
+                          uint32_t lane)
+{
+    const uint32_t key = c.key_lo + kk;
+    for (uint32_t x0 = c.kseg0[kk]; x0 < c.kseg1[kk]; x0 += 64) {
+        const uint32_t x = x0 + lane;
+        bool cand = false;
+        uint32_t gi = 0, t = 0, q = NONE;
+        if (x < c.kseg1[kk]) {
+            const uint32_t e = c.cent[x], u = e & ENT_TXN_MASK;
+            if ((e >> ENT_KIND_SHIFT) != 2u && status_of(c.v, u) == ST_STABLE) {
+                const Ts ue = exec_of(c.v, u);
+                if ((!has_from || tcmp(ue, from) >= 0) && (!has_to || tcmp(ue, to) <= 0) && ev_waiter(c, u, gi, t)) {
+                    const ReadyParams &p = c.gens[gi];
+                    const uint32_t kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
+                    if ((p.lsb[t] & 1u) == 0 && kind != 2u) {                  // managed
+                        q = ev_slot(p, t, key);
+                        const uint32_t R = p.rd_off[t + 1] - p.rd_off[t];
+                        cand = q != NONE && ev_bit(p, t, R + q);
+                    }
+                }
+            }
+        }
+        unsigned long long m = __ballot(cand);
+        while (m) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            const uint32_t lgi = readlane(gi, (int)l), lt = readlane(t, (int)l), lq = readlane(q, (int)l);
+            const ReadyParams &p = c.gens[lgi];
+            if (ev_managed_ok(c, p, lt, lq, kk, lane) && lane == 0) {
+                const uint32_t R = p.rd_off[lt + 1] - p.rd_off[lt];
+                ev_clear(p, lt, R + lq);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void ev_eal(const ReadyParams &p, uint32_t t, const Ts &x)
+{
+    EalRec a = p.eal[t];
+    eal_merge(a, EalRec{x.msb, x.lsb, x.node, 1u});
+    p.eal[t] = a;
+}
+
+// notifyUnmanaged(COMMIT, minUncommitted) / (APPLY, next) over the unmanaged records of kk
+__device__ void ev_unmanaged(const EvCtx &c, uint32_t kk, bool commit, uint32_t mu, const Cand &nx, uint32_t lane)
+{
+    const uint32_t kbound = c.kb ? c.kb[kk] : 0u;
+    for (uint32_t j = c.uk_off[kk] + lane; j < c.uk_off[kk + 1]; j += 64) {
+        const unsigned long long w = c.uk_w[j];
+        const uint32_t gi = (uint32_t)(w >> 32), t = (uint32_t)w, q = c.uk_slot[j];
+        const ReadyParams &p = c.gens[gi];
+        if (p.done[t]) continue;
+        const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], slot = p.key_off[t] + q;
+        if (!ev_bit(p, t, R + q)) continue;
+        uint32_t pd = p.pend[slot], un = p.until[slot];
+        if (commit) {
+            if (pd != 1u || !(mu == NONE || mu > un)) continue;
+            const uint32_t kind = (uint32_t)(p.lsb[t] >> 1) & 7u, g = p.g[t];
+            const bool only_deps = kind == 4u || kind == 2u;
+            const uint32_t K = p.key_off[t + 1] - p.key_off[t], hb = p.k2v_off[t];
+            const uint32_t d0 = q == 0 ? K : (uint32_t)p.k2v[hb + q - 1], d1 = (uint32_t)p.k2v[hb + q];
+            uint32_t ea = NONE;
+            const int r = unmanaged_eval(p, t, d0, d1, kbound, exec_of(c.v, g), only_deps, false, un, ea);
+            if (r == 1) { pd = 3; ev_clear(p, t, R + q); }
+            else {
+                pd = 2;
+                if (only_deps && ea != NONE) ev_eal(p, t, exec_of(c.v, ea));   // :1370-1380
+            }
+            p.pend[slot] = (uint8_t)pd;
+            p.until[slot] = un;
+        } else if (pd == 2u && (nx.g == NONE || tcmp(exec_of(c.v, un), nx.ex) < 0)) {
+            p.pend[slot] = 3;
+            ev_clear(p, t, R + q);
+        }
+    }
+}
+
+// registerUnmanaged (:1406-1498) on every key slot of an unmanaged waiter that now hasBeen(Stable)
+__device__ void ev_register_unmanaged(const EvCtx &c, uint32_t gi, uint32_t t, uint32_t lane)
+{
+    const ReadyParams &p = c.gens[gi];
+    const uint32_t g = p.g[t], kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
+    const bool only_deps = kind == 4u || kind == 2u;
+    const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], K = p.key_off[t + 1] - p.key_off[t], hb = p.k2v_off[t];
+    const Ts ex = exec_of(c.v, g);
+    for (uint32_t q0 = 0; q0 < K; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        bool has = false;
+        Ts cand{0, 0, 0};
+        if (q < K) {
+            const uint32_t slot = p.key_off[t] + q;
+            if (ev_bit(p, t, R + q) && p.pend[slot] == 0u) {
+                const uint32_t kk = p.keys[slot] - c.key_lo, kbound = c.kb ? c.kb[kk] : 0u;
+                const uint32_t d0 = q == 0 ? K : (uint32_t)p.k2v[hb + q - 1], d1 = (uint32_t)p.k2v[hb + q];
+                uint32_t un = p.until[slot], ea = NONE;
+                const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, true, un, ea);
+                p.pend[slot] = (uint8_t)(r == 1 ? 3u : r == 0 ? 2u : 1u);
+                p.until[slot] = un;
+                if (r == 1) atomicAnd(&p.words[p.wo_off[t] + ((R + q) >> 6)], ~(1ull << ((R + q) & 63u)));
+                if (r == 0 && only_deps && ea != NONE) { has = true; cand = exec_of(c.v, ea); }   // :1470-1478
+            }
+        }
+        const EalRec m = eal_wave_max(has, cand);
+        if (lane == 0 && m.has) {
+            EalRec a = p.eal[t];
+            eal_merge(a, m);
+            p.eal[t] = a;
+        }
+    }
+}
+
+// notifyAndUpdatePending(safeStore, X, nw, exec, prev) on key kk (:1163-1215), after X's update
+__device__ void ev_key_event(const EvCtx &c, uint32_t kk, uint32_t X, uint32_t prev, uint32_t nw, const Ts &exec,
+                             uint32_t lane)
+{
+    uint32_t mu;
+    Cand nx, nwr;
+    ev_nexts(c, kk, lane, mu, nx, nwr);
+    if (nw == ST_STABLE || nw == ST_COMMITTED) {
+        const int cmp = nwr.g == NONE ? -1 : tcmp(exec, nwr.ex);
+        if (cmp <= 0) {
+            if (nw == ST_STABLE) ev_notify(c, kk, nx.g != NONE, nx.ex, true, exec, lane);   // we may execute
+        } else {
+            const Ts tx = ev_tid(c, X);
+            // waiters on us may be ready, if we execute after them, were known and not committed
+            if (!(prev == ST_COMMITTED || tcmp(nwr.ex, tx) < 0 || tcmp(exec, tx) == 0))
+                ev_notify(c, kk, true, nx.ex, true, nwr.ex, lane);
+        }
+    } else if ((nw == ST_APPLIED || nw == ST_INVALID) && nx.g != NONE) {
+        ev_notify(c, kk, true, nx.ex, nwr.g != NONE, nwr.ex, lane);
+    }
+    if (nw >= ST_COMMITTED && prev < ST_COMMITTED) ev_unmanaged(c, kk, true, mu, nx, lane);
+    if (mu == NONE || nx.g != NONE) ev_unmanaged(c, kk, false, mu, nx, lane);
+}
+
+// every key event of txn g (its carried entries; truncated keys excluded)
+__device__ void ev_txn_keys(const EvCtx &c, uint32_t g, uint32_t prev, uint32_t nw, const Ts &exec, uint32_t lane)
+{
+    if (g >= c.pk_n) return;
+    for (uint32_t j = c.pk_off[g]; j < c.pk_off[g + 1]; ++j) {
+        const uint32_t kk = c.ckey[c.pk_ent[j]];
+        if (c.kb && g < c.kb[kk]) continue;
+        ev_key_event(c, kk, g, prev, nw, exec, lane);
+        __threadfence();
+    }
+}
+
+// MODE 0: a registration's events; 1: a generation's initialisation; 2: truncated keys
+template <int MODE>
+__global__ __launch_bounds__(64) void rd_event_kernel(EvCtx c)
+{
+    const uint32_t lane = lane_id();
+    if (MODE == 0) {
+        for (uint32_t r = 0; r < c.n; ++r) {
+            const uint32_t g = c.pos[r], nw = c.status[r], cur = c.st[g];
+            if (lane == 0) {                                 // the status first (reg_apply_kernel's update)
+                c.st[g] = (uint8_t)nw;
+                c.chg[g] = c.epoch;
+                if (cur < ST_COMMITTED && nw >= ST_COMMITTED) c.cchg[g] = c.epoch;
+                if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) { c.xmsb[g] = c.emsb[r]; c.xlsb[g] = c.elsb[r]; c.xnode[g] = c.enode[r]; }
+            }
+            __threadfence();
+            uint32_t gi, t;
+            const bool w = ev_waiter(c, g, gi, t);
+            if (w && nw >= ST_STABLE && nw < ST_INVALID && cur < ST_STABLE) {
+                const ReadyParams &p = c.gens[gi];
+                const uint32_t kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
+                if ((p.lsb[t] & 1u) != 0 || kind == 2u) ev_register_unmanaged(c, gi, t, lane);   // unmanaged
+                __threadfence();
+            }
+            // CommandsForKey.update on every key (Erased leaves it as INVALID_OR_TRUNCATED)
+            const uint32_t cs = nw >= ST_ERASED ? ST_INVALID : nw, ps = cur >= ST_ERASED ? ST_INVALID : cur;
+            ev_txn_keys(c, g, ps, cs, exec_of(c.v, g), lane);
+        }
+    } else if (MODE == 1) {
+        const ReadyParams &p = c.gens[c.init_gi];
+        for (uint32_t t = 0; t < p.n; ++t) {
+            const uint32_t g = p.g[t], st = status_of(c.v, g);
+            if (st < ST_STABLE || st >= ST_INVALID) continue;
+            const uint32_t kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
+            if ((p.lsb[t] & 1u) != 0 || kind == 2u) {
+                ev_register_unmanaged(c, c.init_gi, t, lane);
+                __threadfence();
+                continue;
+            }
+            if (st != ST_STABLE) continue;
+            ev_txn_keys(c, g, ST_STABLE, ST_STABLE, exec_of(c.v, g), lane);
+        }
+    } else {
+        for (uint32_t j = 0; j < c.ntkeys; ++j) {        // notifyAndUpdatePending(safeStore, prevCfk)
+            const uint32_t kk = c.tkeys[j];
+            uint32_t mu;
+            Cand nx, nwr;
+            ev_nexts(c, kk, lane, mu, nx, nwr);
+            if (mu == NONE || nx.g != NONE) ev_unmanaged(c, kk, false, mu, nx, lane);
+            __threadfence();
+        }
+    }
+}
+
+// index builders: position -> waiting txn, key -> unmanaged slots, position -> carried entries
+__global__ __launch_bounds__(256) void ev_wmap_kernel(ReadyParams p, uint32_t gi, unsigned long long *wmap, uint32_t wn)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < p.n; t += gridDim.x * blockDim.x)
+        if (!p.done[t] && p.g[t] < wn) wmap[p.g[t]] = (unsigned long long)gi << 32 | t;
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void ev_uk_kernel(ReadyParams p, uint32_t gi, uint32_t *cnt, const uint32_t *off,
+                                                    uint32_t *cur, unsigned long long *uw, uint32_t *us)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < p.n; t += gridDim.x * blockDim.x) {
+        const uint32_t kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
+        if (p.done[t] || ((p.lsb[t] & 1u) == 0 && kind != 2u)) continue;     // unmanaged waiting txns
+        for (uint32_t q = 0, K = p.key_off[t + 1] - p.key_off[t]; q < K; ++q) {
+            const uint32_t kk = p.keys[p.key_off[t] + q] - p.key_lo;
+            if (!FILL) { atomicAdd(&cnt[kk], 1u); continue; }
+            const uint32_t j = off[kk] + atomicAdd(&cur[kk], 1u);
+            uw[j] = (unsigned long long)gi << 32 | t;
+            us[j] = q;
+        }
+    }
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(256) void ev_pk_kernel(uint32_t C, const uint32_t *__restrict__ cent, uint32_t pn,
+                                                    uint32_t *cnt, const uint32_t *off, uint32_t *cur, uint32_t *ent)
+{
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < C; x += gridDim.x * blockDim.x) {
+        const uint32_t e = cent[x], g = e & ENT_TXN_MASK;
+        if ((e >> ENT_KIND_SHIFT) == 2u || g >= pn) continue;             // not in CommandsForKey
+        if (!FILL) atomicAdd(&cnt[g], 1u);
+        else ent[off[g] + atomicAdd(&cur[g], 1u)] = x;
+    }
+}
+
+// truncation: keys whose carried history starts below their new bound (entries leave the CFK)
+__global__ __launch_bounds__(256) void ev_tkeys_kernel(uint32_t nkeys, const uint32_t *__restrict__ kseg0,
+                                                       const uint32_t *__restrict__ kseg1, const uint32_t *__restrict__ cent,
+                                                       const uint32_t *__restrict__ kb, uint32_t *list, uint32_t *cnt)
+{
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nkeys; k += gridDim.x * blockDim.x) {
+        bool any = false;
+        for (uint32_t x = kseg0[k]; x < kseg1[k] && !any; ++x) any = (cent[x] & ENT_TXN_MASK) < kb[k];
+        if (any) list[atomicAdd(cnt, 1u)] = k;
+    }
+}
+
 } // namespace
 
 namespace accord_impl {
@@ -728,6 +1131,146 @@ hipError_t grow_keep(DevBuf &b, size_t used, size_t want, hipStream_t st)
     b.release();
     b = nb;
     return hipSuccess;
+}
+
+StatusView store_view(accord_store *s)
+{
+    StatusView v;
+    v.status = s->rg_status.as<uint8_t>();
+    v.emsb = s->rg_emsb.as<uint64_t>(); v.elsb = s->rg_elsb.as<uint64_t>(); v.enode = s->rg_enode.as<int32_t>();
+    v.known = s->rg_known;
+    return v;
+}
+
+// the per-key shardRedundantBefore bounds on the device (null when none was set)
+int32_t store_kb(accord_store *s, bool force, const uint32_t **kb)
+{
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    const bool has_kb = s->rdy_kb_host.size() == nkeys;     // a shardRedundantBefore bound was set
+    if ((s->rdy_kb_dirty || force) && has_kb) {
+        HIPCHECK(s, s->rdy_kb.ensure((size_t)nkeys * 4 + 4));
+        HIPCHECK(s, hipMemcpyAsync(s->rdy_kb.p, s->rdy_kb_host.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, s->stream));
+        HIPCHECK(s, hipStreamSynchronize(s->stream));
+        s->rdy_kb_dirty = false;
+    }
+    *kb = has_kb && s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
+    return ACCORD_OK;
+}
+
+// segment bounds of the carried history per key, once per carry version
+int32_t store_kseg(accord_store *s, bool force)
+{
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo, C = s->carry_n;
+    hipStream_t st = s->stream;
+    if (s->rdy_kseg_version != s->carry_version || !s->rdy_kseg0.p || force) {
+        HIPCHECK(s, s->rdy_kseg0.ensure((size_t)nkeys * 4 + 4));
+        HIPCHECK(s, s->rdy_kseg1.ensure((size_t)nkeys * 4 + 4));
+        HIPCHECK(s, hipMemsetAsync(s->rdy_kseg0.p, 0, (size_t)nkeys * 4, st));
+        HIPCHECK(s, hipMemsetAsync(s->rdy_kseg1.p, 0, (size_t)nkeys * 4, st));
+        if (C) hipLaunchKernelGGL(rd_seg_kernel, dim3(std::min<uint32_t>((C + 255) / 256, 8192u)), dim3(256), 0, st, C,
+                                  s->cy_key.as<uint32_t>(), s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>());
+        s->rdy_kseg_version = s->carry_version;
+    }
+    return ACCORD_OK;
+}
+
+// a generation's table entry: its deps, WaitingOn and the store's shared tables
+ReadyParams gen_params(accord_store *s, ReadyGen *r, const StatusView &v, const uint32_t *kb)
+{
+    ReadyParams p{};
+    p.n = r->n; p.key_lo = s->cfg.key_lo;
+    p.g = r->g.as<uint32_t>(); p.lsb = r->lsb.as<uint64_t>();
+    p.tmsb = s->rg_tmsb.as<uint64_t>(); p.tlsb = s->rg_tlsb.as<uint64_t>(); p.tnode = s->rg_tnode.as<int32_t>();
+    p.tg = s->rg_tg.as<uint32_t>(); p.tx_n = s->rg_tx_n;
+    p.rd_off = r->rd_off.as<uint32_t>(); p.rd_vals = r->rd_vals.as<uint32_t>();
+    p.key_off = r->key_off.as<uint32_t>(); p.keys = r->keys.as<uint32_t>();
+    p.val_off = r->val_off.as<uint32_t>(); p.vals = r->vals.as<uint32_t>();
+    p.k2v_off = r->k2v_off.as<uint32_t>(); p.k2v = r->k2v.as<int32_t>();
+    p.wo_off = r->wo_off.as<uint32_t>(); p.words = r->wo.as<unsigned long long>(); p.aoi = r->aoi.as<unsigned long long>();
+    p.pend = r->pend.as<uint8_t>(); p.until = r->until.as<uint32_t>(); p.done = r->done.as<uint8_t>();
+    p.eal = r->eal.as<EalRec>();
+    p.kb = kb;
+    p.v = v;
+    return p;
+}
+
+// event-exact readiness: the generations' table, position -> waiting txn, key -> unmanaged slots,
+// position -> carried entries (rebuilt with the carry), the kernel's context
+int32_t ev_prepare(accord_store *s, EvCtx &c, ReadyGen *want, uint32_t *want_gi)
+{
+    hipStream_t st = s->stream;
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo, C = s->carry_n, pn = s->next_global;
+    const StatusView v = store_view(s);
+    const uint32_t *kb = nullptr;
+    EV_RC(store_kb(s, false, &kb));
+    EV_RC(store_kseg(s, false));
+    std::vector<ReadyParams> P;
+    size_t ukcap = 1;
+    for (ReadyGen *r : s->rdy_gens) {
+        if (r->left == 0) continue;
+        if (r == want && want_gi) *want_gi = (uint32_t)P.size();
+        P.push_back(gen_params(s, r, v, kb));
+        ukcap += r->keys.cap / 4;
+    }
+    HIPCHECK(s, s->ev_gens.ensure(P.size() * sizeof(ReadyParams) + 64));
+    if (!P.empty())
+        HIPCHECK(s, hipMemcpyAsync(s->ev_gens.p, P.data(), P.size() * sizeof(ReadyParams), hipMemcpyHostToDevice, st));
+    HIPCHECK(s, s->ev_tot.ensure(64));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max({nkeys, pn, 1u})), st));
+    // position -> waiting txn
+    HIPCHECK(s, s->ev_wmap.ensure((size_t)pn * 8 + 8));
+    HIPCHECK(s, hipMemsetAsync(s->ev_wmap.p, 0xFF, (size_t)pn * 8 + 8, st));
+    for (size_t i = 0; i < P.size(); ++i)
+        hipLaunchKernelGGL(ev_wmap_kernel, dim3(grid_for_waves((P[i].n + 63) / 64)), dim3(256), 0, st, P[i], (uint32_t)i,
+                           s->ev_wmap.as<unsigned long long>(), pn);
+    // key -> unmanaged slots (CSR)
+    HIPCHECK(s, s->ev_ukcnt.ensure((size_t)nkeys * 4 + 8));
+    HIPCHECK(s, s->ev_ukoff.ensure((size_t)nkeys * 4 + 8));
+    HIPCHECK(s, s->ev_ukw.ensure(ukcap * 8));
+    HIPCHECK(s, s->ev_uks.ensure(ukcap * 4));
+    HIPCHECK(s, hipMemsetAsync(s->ev_ukcnt.p, 0, (size_t)nkeys * 4 + 8, st));
+    for (size_t i = 0; i < P.size(); ++i)
+        hipLaunchKernelGGL(ev_uk_kernel<false>, dim3(grid_for_waves((P[i].n + 63) / 64)), dim3(256), 0, st, P[i],
+                           (uint32_t)i, s->ev_ukcnt.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr);
+    if (nkeys) accord::exclusive_scan_u32(s->ev_ukcnt.as<uint32_t>(), s->ev_ukoff.as<uint32_t>(), nkeys,
+                                          s->ev_tot.as<unsigned long long>(), s->scan_tmp.p, st);
+    HIPCHECK(s, hipMemsetAsync(s->ev_ukcnt.p, 0, (size_t)nkeys * 4 + 8, st));
+    for (size_t i = 0; i < P.size(); ++i)
+        hipLaunchKernelGGL(ev_uk_kernel<true>, dim3(grid_for_waves((P[i].n + 63) / 64)), dim3(256), 0, st, P[i],
+                           (uint32_t)i, nullptr, s->ev_ukoff.as<uint32_t>(), s->ev_ukcnt.as<uint32_t>(),
+                           s->ev_ukw.as<unsigned long long>(), s->ev_uks.as<uint32_t>());
+    // position -> carried entries (CommandsForKey membership), per carry version
+    if (s->ev_pk_version != s->carry_version || !s->ev_pkoff.p || s->ev_pk_n != pn) {
+        HIPCHECK(s, s->ev_pkcnt.ensure((size_t)pn * 4 + 8));
+        HIPCHECK(s, s->ev_pkoff.ensure((size_t)pn * 4 + 8));
+        HIPCHECK(s, s->ev_pkent.ensure((size_t)C * 4 + 8));
+        HIPCHECK(s, hipMemsetAsync(s->ev_pkcnt.p, 0, (size_t)pn * 4 + 8, st));
+        if (C) hipLaunchKernelGGL(ev_pk_kernel<false>, dim3(std::min<uint32_t>((C + 255) / 256, 8192u)), dim3(256), 0, st,
+                                  C, s->cy_ent.as<uint32_t>(), pn, s->ev_pkcnt.as<uint32_t>(), nullptr, nullptr, nullptr);
+        if (pn) accord::exclusive_scan_u32(s->ev_pkcnt.as<uint32_t>(), s->ev_pkoff.as<uint32_t>(), pn,
+                                           s->ev_tot.as<unsigned long long>(), s->scan_tmp.p, st);
+        else HIPCHECK(s, hipMemsetAsync(s->ev_pkoff.p, 0, 4, st));
+        HIPCHECK(s, hipMemsetAsync(s->ev_pkcnt.p, 0, (size_t)pn * 4 + 8, st));
+        if (C) hipLaunchKernelGGL(ev_pk_kernel<true>, dim3(std::min<uint32_t>((C + 255) / 256, 8192u)), dim3(256), 0, st,
+                                  C, s->cy_ent.as<uint32_t>(), pn, nullptr, s->ev_pkoff.as<uint32_t>(),
+                                  s->ev_pkcnt.as<uint32_t>(), s->ev_pkent.as<uint32_t>());
+        s->ev_pk_version = s->carry_version;
+        s->ev_pk_n = pn;
+    }
+    c = EvCtx{};
+    c.gens = s->ev_gens.as<ReadyParams>(); c.ngen = (uint32_t)P.size();
+    c.wmap = s->ev_wmap.as<unsigned long long>(); c.wmap_n = pn;
+    c.ckey = s->cy_key.as<uint32_t>(); c.cent = s->cy_ent.as<uint32_t>();
+    c.kseg0 = s->rdy_kseg0.as<uint32_t>(); c.kseg1 = s->rdy_kseg1.as<uint32_t>();
+    c.pk_off = s->ev_pkoff.as<uint32_t>(); c.pk_ent = s->ev_pkent.as<uint32_t>(); c.pk_n = s->ev_pk_n;
+    c.uk_off = s->ev_ukoff.as<uint32_t>(); c.uk_slot = s->ev_uks.as<uint32_t>(); c.uk_w = s->ev_ukw.as<unsigned long long>();
+    c.nkeys = nkeys; c.key_lo = s->cfg.key_lo;
+    c.kb = kb;
+    c.v = v;
+    c.tmsb = s->rg_tmsb.as<uint64_t>(); c.tlsb = s->rg_tlsb.as<uint64_t>(); c.tnode = s->rg_tnode.as<int32_t>();
+    c.tg = s->rg_tg.as<uint32_t>(); c.tx_n = s->rg_tx_n;
+    HIPCHECK(s, hipStreamSynchronize(st));          // the table copy's host source
+    return ACCORD_OK;
 }
 
 // the generation's device copies of the batch's deps and WaitingOn; no state of the store changes
@@ -819,7 +1362,87 @@ int32_t ready_track_batch(accord_store *s)
     return ACCORD_OK;
 }
 
+int32_t ready_register_events(accord_store *s, uint32_t n, const uint32_t *pos, const uint8_t *status,
+                              const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode, uint32_t epoch)
+{
+    EvCtx c;
+    EV_RC(ev_prepare(s, c, nullptr, nullptr));
+    c.n = n; c.pos = pos; c.status = status; c.emsb = emsb; c.elsb = elsb; c.enode = enode;
+    c.st = s->rg_status.as<uint8_t>();
+    c.xmsb = s->rg_emsb.as<uint64_t>(); c.xlsb = s->rg_elsb.as<uint64_t>(); c.xnode = s->rg_enode.as<int32_t>();
+    c.chg = s->rg_chg.as<uint32_t>(); c.cchg = s->rg_cchg.as<uint32_t>(); c.epoch = epoch;
+    hipLaunchKernelGGL(rd_event_kernel<0>, dim3(1), dim3(64), 0, s->stream, c);
+    HIPCHECK(s, hipGetLastError());
+    return ACCORD_OK;
+}
+
+int32_t ready_init_events(accord_store *s)
+{
+    ReadyGen *r = s->rdy_batch_gen;
+    if (!r || r->n == 0) return ACCORD_OK;
+    EvCtx c;
+    uint32_t gi = ~0u;
+    EV_RC(ev_prepare(s, c, r, &gi));
+    if (gi == ~0u) return ACCORD_OK;
+    c.init_gi = gi;
+    hipLaunchKernelGGL(rd_event_kernel<1>, dim3(1), dim3(64), 0, s->stream, c);
+    HIPCHECK(s, hipGetLastError());
+    return ACCORD_OK;
+}
+
+// before a truncation: the keys whose carried history has an entry below the key's new bound
+int32_t ready_truncate_keys(accord_store *s, const std::vector<uint32_t> &kb, std::vector<uint32_t> &keys)
+{
+    keys.clear();
+    const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
+    if (!nkeys || !s->carry_n) return ACCORD_OK;
+    hipStream_t st = s->stream;
+    EV_RC(store_kseg(s, false));
+    HIPCHECK(s, s->ev_tk.ensure((size_t)nkeys * 8 + 16));
+    uint32_t *kbd = s->ev_tk.as<uint32_t>(), *list = kbd + nkeys, *cnt = list + nkeys;
+    HIPCHECK(s, hipMemcpyAsync(kbd, kb.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
+    HIPCHECK(s, hipMemsetAsync(cnt, 0, 4, st));
+    hipLaunchKernelGGL(ev_tkeys_kernel, dim3(grid_for_waves((nkeys + 63) / 64)), dim3(256), 0, st, nkeys,
+                       s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>(), s->cy_ent.as<uint32_t>(), kbd, list, cnt);
+    uint32_t m = 0;
+    HIPCHECK(s, hipMemcpyAsync(&m, cnt, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipStreamSynchronize(st));
+    keys.resize(m);
+    if (m) {
+        HIPCHECK(s, hipMemcpyAsync(keys.data(), list, (size_t)m * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+    }
+    return ACCORD_OK;
+}
+
+// after it: notifyAndUpdatePending(safeStore, prevCfk) on those keys (the unmanaged APPLY records)
+int32_t ready_truncate_events(accord_store *s, const std::vector<uint32_t> &keys)
+{
+    if (keys.empty()) return ACCORD_OK;
+    EvCtx c;
+    EV_RC(ev_prepare(s, c, nullptr, nullptr));
+    if (c.ngen == 0) return ACCORD_OK;
+    HIPCHECK(s, s->ev_tk.ensure(keys.size() * 4 + 16));
+    HIPCHECK(s, hipMemcpyAsync(s->ev_tk.p, keys.data(), keys.size() * 4, hipMemcpyHostToDevice, s->stream));
+    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    c.tkeys = s->ev_tk.as<uint32_t>(); c.ntkeys = (uint32_t)keys.size();
+    hipLaunchKernelGGL(rd_event_kernel<2>, dim3(1), dim3(64), 0, s->stream, c);
+    HIPCHECK(s, hipGetLastError());
+    return ACCORD_OK;
+}
+
 } // namespace accord_impl
+
+extern "C" int32_t accord_ready_set_mode(accord_store *s, uint32_t mode)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (mode > ACCORD_READY_EVENTS) return fail(s, ACCORD_ERR_ARG, "unknown readiness mode %u", mode);
+    if (!accord_impl::registered_mode(s))
+        return fail(s, ACCORD_ERR_STATE, "accord_ready_set_mode needs a registered-status store (resident, ACCORD_WINDOW_NONE)");
+    if (s->rdy_waiting) return fail(s, ACCORD_ERR_STATE, "accord_ready_set_mode with txns in the waiting set");
+    s->rdy_event_mode = mode == ACCORD_READY_EVENTS;
+    return ACCORD_OK;
+}
 
 extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
 {
@@ -868,21 +1491,14 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     // everything is re-evaluated after a new carry (batch, truncation) or RedundantBefore bound
     // (and after a call that failed part-way: its bookkeeping below may be ahead of the device)
     const bool force = s->rdy_force_full;
-    const bool full = force || s->rdy_kb_dirty || s->rdy_sum_version != s->carry_version;
+    const bool full = force || s->rdy_kb_dirty || s->rdy_sum_version != s->carry_version || s->rdy_event_mode;
     const uint32_t seen = s->rdy_seen, call = ++s->rdy_call;
     s->rdy_force_full = true;                  // cleared once this call has synchronised
     s->rdy_seen = s->rg_epoch;
     s->rdy_sum_version = s->carry_version;
-    const bool has_kb = s->rdy_kb_host.size() == nkeys;     // a shardRedundantBefore bound was set
-    if ((s->rdy_kb_dirty || force) && has_kb) {
-        HIPCHECK(s, s->rdy_kb.ensure((size_t)nkeys * 4 + 4));
-        HIPCHECK(s, hipMemcpyAsync(s->rdy_kb.p, s->rdy_kb_host.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
-        s->rdy_kb_dirty = false;
-    }
-    StatusView v;
-    v.status = s->rg_status.as<uint8_t>();
-    v.emsb = s->rg_emsb.as<uint64_t>(); v.elsb = s->rg_elsb.as<uint64_t>(); v.enode = s->rg_enode.as<int32_t>();
-    v.known = s->rg_known;
+    const uint32_t *kbp = nullptr;
+    EV_RC(accord_impl::store_kb(s, force, &kbp));
+    const StatusView v = accord_impl::store_view(s);
     HIPCHECK(s, s->rdy_part.ensure((size_t)C * sizeof(KeyPart) + 64));
     HIPCHECK(s, s->rdy_dirty.ensure_zeroed((size_t)nkeys * 4 + 4, st));
     HIPCHECK(s, s->rdy_dirty2.ensure_zeroed((size_t)nkeys * 4 + 4, st));
@@ -899,15 +1515,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     }
     if (C) hipLaunchKernelGGL(rd_part_kernel, dim3(grid_for_waves((C + 63) / 64)), dim3(256), 0, st, C,
                               s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), v, s->rdy_part.as<KeyPart>(), dm);
-    if (s->rdy_kseg_version != s->carry_version || !s->rdy_kseg0.p || force) {
-        HIPCHECK(s, s->rdy_kseg0.ensure((size_t)nkeys * 4 + 4));
-        HIPCHECK(s, s->rdy_kseg1.ensure((size_t)nkeys * 4 + 4));
-        HIPCHECK(s, hipMemsetAsync(s->rdy_kseg0.p, 0, (size_t)nkeys * 4, st));
-        HIPCHECK(s, hipMemsetAsync(s->rdy_kseg1.p, 0, (size_t)nkeys * 4, st));
-        if (C) hipLaunchKernelGGL(rd_seg_kernel, dim3(std::min<uint32_t>((C + 255) / 256, 8192u)), dim3(256), 0, st, C,
-                                  s->cy_key.as<uint32_t>(), s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>());
-        s->rdy_kseg_version = s->carry_version;
-    }
+    EV_RC(accord_impl::store_kseg(s, force));
     if (nkeys) hipLaunchKernelGGL(rd_summary_kernel, dim3(full ? grid_for_waves(nkeys) : std::min(grid_for_waves(nkeys), 256u)),
                                   dim3(256), 0, st, nkeys, s->rdy_kseg0.as<uint32_t>(), s->rdy_kseg1.as<uint32_t>(),
                                   s->rdy_part.as<KeyPart>(), v, s->rdy_sum.as<KeySummary>(),
@@ -924,20 +1532,10 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         }
         ReadyLaunch &L = tabs.back();
         ReadyParams &p = L.g[L.ngen];
-        p = ReadyParams{};
-        p.n = r->n; p.key_lo = s->cfg.key_lo;
-        p.g = r->g.as<uint32_t>(); p.lsb = r->lsb.as<uint64_t>();
-        p.tmsb = s->rg_tmsb.as<uint64_t>(); p.tlsb = s->rg_tlsb.as<uint64_t>(); p.tnode = s->rg_tnode.as<int32_t>();
-        p.tg = s->rg_tg.as<uint32_t>(); p.tx_n = s->rg_tx_n;
-        p.rd_off = r->rd_off.as<uint32_t>(); p.rd_vals = r->rd_vals.as<uint32_t>();
-        p.key_off = r->key_off.as<uint32_t>(); p.keys = r->keys.as<uint32_t>();
-        p.val_off = r->val_off.as<uint32_t>(); p.vals = r->vals.as<uint32_t>();
-        p.k2v_off = r->k2v_off.as<uint32_t>(); p.k2v = r->k2v.as<int32_t>();
-        p.wo_off = r->wo_off.as<uint32_t>(); p.words = r->wo.as<unsigned long long>(); p.aoi = r->aoi.as<unsigned long long>();
-        p.pend = r->pend.as<uint8_t>(); p.until = r->until.as<uint32_t>(); p.done = r->done.as<uint8_t>();
+        p = accord_impl::gen_params(s, r, v, kbp);
+        p.evmode = s->rdy_event_mode ? 1u : 0u;
         p.out = list; p.out_cnt = cnt;
         p.drop = drop; p.drop_cnt = cnt + (HDR - 1);
-        p.eal = r->eal.as<EalRec>();
         p.rbx = s->rb_ext && s->rb_m ? 1u : 0u;
         p.M = rr_map_of(s);
         p.pkoff = r->pkoff.as<uint32_t>(); p.pkeys = r->pkeys.as<uint32_t>();
@@ -947,8 +1545,6 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.spill = RrSpill{cnt + (HDR - 2), cnt + (HDR - 3), cnt + (HDR - 4), s->rdy_spill.as<uint32_t>()};
         p.ubase = L.base;
         p.sum = s->rdy_sum.as<KeySummary>();
-        p.kb = has_kb && s->rdy_kb.p ? s->rdy_kb.as<uint32_t>() : nullptr;
-        p.v = v;
         p.full = r->fresh ? 1u : 0u;
         any_inc |= !full && !r->fresh;
         p.chg = s->rg_chg.as<uint32_t>(); p.dirty = s->rdy_dirty2.as<uint32_t>();

@@ -1012,6 +1012,11 @@ int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start
     }
     if (!any) return ACCORD_OK;
     // the readiness evaluation skips deps below each key's bound (ready.hip): a cumulative max
+    std::vector<uint32_t> tkeys;          // event-exact readiness: the keys that lose entries
+    if (s->rdy_event_mode) {
+        const int32_t rc = accord_impl::ready_truncate_keys(s, kb, tkeys);
+        if (rc != ACCORD_OK) return rc;
+    }
     if (s->rdy_kb_host.size() != nkeys) s->rdy_kb_host.assign(nkeys, 0u);
     for (uint32_t r = 0; r < nkeys; ++r) s->rdy_kb_host[r] = std::max(s->rdy_kb_host[r], kb[r]);
     s->rdy_kb_dirty = true;
@@ -1038,6 +1043,7 @@ int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start
     std::swap(s->cy_ent, s->cy_ent2);
     s->carry_n = (uint32_t)kept;
     ++s->carry_version;
+    if (s->rdy_event_mode) return accord_impl::ready_truncate_events(s, tkeys);
     return ACCORD_OK;
 }
 
@@ -1151,7 +1157,12 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
         return fail(s, code, "accord_txn_register: event %u rejected (%s); nothing applied", r, why);
     }
     ++s->rg_epoch;
-    hipLaunchKernelGGL(reg_apply_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
+    if (s->rdy_event_mode) {      // event-exact readiness: the events replayed in order (ready.hip)
+        const int32_t rc = accord_impl::ready_register_events(s, n, p.pos, p.status, p.emsb, p.elsb, p.enode, p.epoch);
+        if (rc != ACCORD_OK) return rc;
+    } else {
+        hipLaunchKernelGGL(reg_apply_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
+    }
     if (s->rc_n)
         hipLaunchKernelGGL(reg_erase_ranges_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, s->rc_n,
                            s->rc_owner.as<uint32_t>(), s->rc_kind.as<uint32_t>());

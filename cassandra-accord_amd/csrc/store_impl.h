@@ -186,6 +186,13 @@ struct accord_store {
     // setAppliedAndPropagate: every released Range-domain txn's final appliedOrInvalidated as the
     // positions of its set RangeDeps txnIds (pv_at[g] = 1 + start in the pool, pv_len[g]; 0 = none)
     DevBuf rdy_pv_at, rdy_pv_len, rdy_pv_pool, rdy_pv_cnt;
+    // event-exact readiness (accord_ready_set_mode ACCORD_READY_EVENTS, ready.hip): the live
+    // generations' parameters, position -> waiting txn, key -> unmanaged slots, position -> carried
+    // entries (per carry version), truncated keys
+    bool rdy_event_mode = false;
+    DevBuf ev_gens, ev_wmap, ev_ukcnt, ev_ukoff, ev_ukw, ev_uks, ev_pkcnt, ev_pkoff, ev_pkent, ev_tk, ev_tot;
+    uint64_t ev_pk_version = ~0ull;
+    uint32_t ev_pk_n = 0;
     uint32_t rdy_pv_n = 0;                    // pool entries used (read back after every call)
     size_t rdy_pv_pos = 0;                    // positions pv_at / pv_len cover
     DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dirty2, rdy_dlist, rdy_work, rdy_wcnt;
@@ -240,6 +247,13 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
 int32_t ready_track_batch(accord_store *s);
 int32_t ready_batch_check(accord_store *s);
 void ready_destroy(accord_store *s);
+// event-exact readiness: a registration's events replayed in order (instead of the bulk status
+// apply), a generation's initialisation, and the keys a truncation took entries from
+int32_t ready_register_events(accord_store *s, uint32_t n, const uint32_t *pos, const uint8_t *status,
+                              const uint64_t *emsb, const uint64_t *elsb, const int32_t *enode, uint32_t epoch);
+int32_t ready_init_events(accord_store *s);
+int32_t ready_truncate_keys(accord_store *s, const std::vector<uint32_t> &kb, std::vector<uint32_t> &keys);
+int32_t ready_truncate_events(accord_store *s, const std::vector<uint32_t> &keys);
 // RedundantBefore.collectDeps of the computed batch, unioned into the store's result (depset_abi.cpp):
 // the count and its scans are queued inside the compute (totals arrive with its final copy), the
 // fill and the union after it

@@ -145,7 +145,9 @@ int32_t accord_waiting_on_initialise(accord_store *s)
     s->max_level = 0;
     s->wo_has_aoi = true;
     s->wo_done = true;
-    return accord_impl::ready_track_batch(s);      // the batch joins the waiting set (ready.hip)
+    rc = accord_impl::ready_track_batch(s);        // the batch joins the waiting set (ready.hip)
+    if (rc == ACCORD_OK && s->rdy_event_mode) rc = accord_impl::ready_init_events(s);
+    return rc;
 }
 
 int32_t accord_waiting_on_download(accord_store *s, accord_waiting_on *out)

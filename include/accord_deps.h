@@ -487,8 +487,9 @@ int32_t accord_waiting_on_initialise(accord_store *store);
  * :1163-1215); every call here evaluates them for every waiting txn whose inputs changed, so a txn is
  * reported at the first call at which its test holds -- never later than the reference releases it
  * (tests/test_ready.py compares with an event-driven restatement).  A waiting txn that is invalidated
- * or truncated leaves the set unreported.  setAppliedAndPropagate's propagation is implied by the
- * store-wide statuses (a propagated txn is APPLIED / invalidated here already).
+ * or truncated leaves the set unreported.  An applied Range-domain dep propagates its own
+ * appliedOrInvalidated (setAppliedAndPropagate, local/Command.java:1569-1583) in updateWaitingOn's
+ * reverse walk.
  * The arrays stay valid until the next call on the store; `waiting` = txns still in the set. */
 typedef struct {
     uint32_t  n;
@@ -501,6 +502,23 @@ typedef struct {
     const int32_t  *eal_node;
 } accord_ready;
 int32_t accord_ready_update(accord_store *store, accord_ready *out);
+/* Readiness mode of a registered-status store (set while its waiting set is empty).
+ * ACCORD_READY_POLL (default): every accord_ready_update call re-evaluates the key tests of the
+ *   waiting txns whose inputs changed, so a txn is released at the first call at which its test
+ *   holds (never later than the reference).
+ * ACCORD_READY_EVENTS: event-exact -- a key bit clears only when one of
+ *   CommandsForKey.notifyAndUpdatePending's events reaches the key (local/CommandsForKey.java:
+ *   1163-1215): accord_txn_register replays its events in order on the device, each against the
+ *   state after it (the key's minUncommitted / next / nextWrite, :432-461; notify over committed[]
+ *   in the executeAt range the change selects, :1501-1511; the unmanaged COMMIT / APPLY records,
+ *   :1264-1283, 1315-1360; registerUnmanaged at the Stable transition); accord_waiting_on_initialise
+ *   gives the txns already Stable their transition's step; a truncation notifies the unmanaged
+ *   records of the keys it took entries from.  accord_ready_update then evaluates the range-dep bits
+ *   and releases.  Releases equal the event-driven restatement (oracle or_lstore_event_mode) call by
+ *   call.  The replay is one wave per registration (a correctness mode, not a throughput one). */
+#define ACCORD_READY_POLL   0u
+#define ACCORD_READY_EVENTS 1u
+int32_t accord_ready_set_mode(accord_store *store, uint32_t mode);
 int32_t accord_waiting_on_download(accord_store *store, accord_waiting_on *out);
 void    accord_waiting_on_release(accord_waiting_on *wo);
 /* device ms of the last accord_waiting_on_compute: bitsets, reduced predecessors, levelling */

@@ -42,14 +42,18 @@ def mk(txns):
 class Driver:
     """One schedule driven into the oracle and (optionally) the device store in lockstep."""
 
-    def __init__(self, s, nkeys, dev=None, events=False):
+    def __init__(self, s, nkeys, dev=None, events=False, dev_events=False):
         self.s, self.ora, self.dev = s, O.LStore(nkeys), dev
         self.status = np.zeros(s.n, np.uint8)
         self.execs = [None] * s.n
         # events: an event-driven restatement (or_lstore_event_mode) fed the same schedule in lockstep;
-        # ev_rounds[c] = what it releases at call c
-        self.ev = O.LStore(nkeys, event_mode=True) if events else None
+        # ev_rounds[c] = what it releases at call c.  dev_events: the device runs event-exact
+        # (accord_ready_set_mode ACCORD_READY_EVENTS) and is compared with that restatement instead
+        self.dev_events = dev_events
+        self.ev = O.LStore(nkeys, event_mode=True) if (events or dev_events) else None
         self.ev_rounds = []
+        if dev is not None and dev_events:
+            dev.ready_mode(True)
 
     def batch(self, lo, hi):
         if self.ev is not None:
@@ -91,6 +95,18 @@ class Driver:
             self.dev.waiting_on_initialise()
 
     def round(self):
+        if self.dev_events:
+            want, weal = self.ev.ready_ex()
+            self.ev_rounds.append(want)
+            self.eal = weal
+            if self.dev is not None:
+                got, waiting, geal = self.dev.ready_update_ex()
+                assert np.array_equal(got, want), (got[:20], want[:20])
+                assert waiting == self.ev.waiting
+                for a, b in zip(geal, weal):
+                    assert np.array_equal(a, b), (got, a, b)
+            self.ora.ready_ex()                            # the polling restatement keeps pace
+            return want
         if self.ev is not None:
             self.ev_rounds.append(self.ev.ready())
         want, weal = self.ora.ready_ex()
@@ -468,12 +484,12 @@ def test_all_stable_rounds_equal_cfk_simulation(n, ks, seed, rf):
     assert np.array_equal(got, want.astype(np.int64))
 
 
-def schedule(s, nkeys, bsz, seed, dev=None, late_frac=0.15, delay_frac=0.2, rounds_per_batch=2):
+def schedule(s, nkeys, bsz, seed, dev=None, late_frac=0.15, delay_frac=0.2, rounds_per_batch=2, dev_events=False):
     """Batches of bsz: computed, then STABLE for most txns (some at an executeAt past their TxnId),
     the rest (late) STABLE one batch later; WaitingOn initialised; a few ready -> APPLIED rounds per
     batch; finally drained.  Returns every round's ready list."""
     rng = np.random.default_rng(seed)
-    d = Driver(s, nkeys, dev)
+    d = Driver(s, nkeys, dev, dev_events=dev_events)
     out, late = [], np.zeros(0, np.int64)
     for lo in range(0, s.n, bsz):
         hi = min(s.n, lo + bsz)
@@ -498,6 +514,13 @@ def schedule(s, nkeys, bsz, seed, dev=None, late_frac=0.15, delay_frac=0.2, roun
     d.register(late, STABLE)
     out.extend(drain(d))
     return out, d
+
+
+def test_event_schedule_driver_oracle():
+    """The event-exact comparison path of the Driver on the CPU (the GPU test's reference side)."""
+    s = stable_stream(500, 30, 71, 0.1)
+    out, d = schedule(s, 30, 100, 71, dev_events=True)
+    assert sum(len(r) for r in out) > 500 // 4
 
 
 def test_schedule_oracle_progress():
@@ -527,6 +550,106 @@ def test_gpu_rr_kat(gpu_device):
 def test_gpu_eal_kat(gpu_device):
     with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
         eal_kat_run(dev)
+
+
+@pytest.mark.gpu
+def test_gpu_event_order_kat(gpu_device):
+    """EV_KAT on the device in event-exact mode: t1 is released only at t0's STABLE event."""
+    s = mk(EV_KAT)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        d = Driver(s, 4, dev, dev_events=True)
+        part = d.batch(0, 2)
+        d.register([1], STABLE)
+        d.initialise(0, part)
+        assert list(d.round()) == []
+        t0x = (int(s.msb[0]), 20 << 16 | int(s.lsb[0]) & 0xFFFF, 1)
+        d.register([0], 4, [t0x])                         # COMMITTED: notifies nobody
+        assert list(d.round()) == []
+        d.register([0], STABLE)
+        assert list(d.round()) == [0, 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ks,bsz,seed,rf,sp", [(600, 30, 100, 71, 0.0, False), (700, 40, 140, 72, 0.1, False),
+                                                  (600, 30, 120, 73, 0.1, True)])
+def test_gpu_event_mode_equals_event_oracle(gpu_device, n, ks, bsz, seed, rf, sp):
+    """Event-exact device readiness == or_lstore_event_mode call by call over the interleaved
+    schedule (batches; STABLE in bulk registrations, some late, some past their TxnId; ready ->
+    APPLIED rounds), incl. range txns (unmanaged records) and sync points."""
+    s = stable_stream(n, ks, seed, rf, sync_points=sp)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=ks, window=WINDOW_NONE, resident=True) as dev:
+        out, d = schedule(s, ks, bsz, seed, dev=dev, dev_events=True)
+    # every call compared inside Driver.round; the event-driven reference releases fewer (sync points
+    # wait for an event that may never reach their keys)
+    assert sum(len(r) for r in out) > 0
+
+
+def single_event_schedule(s, nkeys, bsz, seed, dev=None, cf=0.3, delay=0.2, rounds=3):
+    """event_schedule's shape through the Driver: ONE event per registration (a share cf COMMITTED one
+    batch before STABLE, executeAt sometimes past the TxnId), a ready call after every event and its
+    releases applied at once; the device (if any) runs event-exact and is compared at every call."""
+    rng = np.random.default_rng(seed)
+    d = Driver(s, nkeys, dev, dev_events=True)
+    total = [0]
+
+    def event(g, st, ex=None):
+        d.register([g], st, [ex] if ex is not None else None)
+        r = d.round()
+        total[0] += len(r)
+        if len(r):
+            d.apply(r)
+            total[0] += 0
+
+    late = np.zeros(0, np.int64)
+    for lo in range(0, s.n, bsz):
+        hi = min(s.n, lo + bsz)
+        part = d.batch(lo, hi)
+        idx = np.arange(lo, hi)
+        is_late = rng.random(hi - lo) < 0.15
+        now = np.concatenate([late, idx[~is_late]])
+        first = []
+        for g in now:
+            ex = None
+            if g >= lo and rng.random() < delay:
+                ex = (int(s.msb[g]), ((int(s.lsb[g]) >> 16) + int(rng.integers(1, 30))) << 16, int(rng.integers(8, 16)))
+            if g >= lo and rng.random() < cf:
+                first.append(g)
+                event(g, 4, ex if ex is not None else (int(s.msb[g]), int(s.lsb[g]), int(s.node[g])))
+            else:
+                event(g, STABLE, ex)
+        late = np.concatenate([idx[is_late], np.array(first, np.int64)]).astype(np.int64)
+        d.initialise(lo, part)
+        for _ in range(rounds):
+            r = d.round()
+            total[0] += len(r)
+            if len(r):
+                d.apply(r)
+    for g in np.sort(late):
+        event(int(g), STABLE)
+    for _ in range(2000):
+        r = d.round()
+        if not len(r):
+            break
+        total[0] += len(r)
+        d.apply(r)
+    return total[0], d
+
+
+def test_single_event_schedule_oracle():
+    s = stable_stream(300, 20, 81, 0.1)
+    released, _ = single_event_schedule(s, 20, 60, 81)
+    assert released > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ks,bsz,seed,rf,sp", [(400, 20, 80, 81, 0.1, False), (400, 24, 100, 82, 0.1, True)])
+def test_gpu_event_mode_single_events(gpu_device, n, ks, bsz, seed, rf, sp):
+    """Event-exact device readiness == or_lstore_event_mode with one event per registration and a
+    ready call after each, COMMITTED-before-STABLE events included (their nextWrite skip)."""
+    s = stable_stream(n, ks, seed, rf, sync_points=sp)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=ks, window=WINDOW_NONE, resident=True) as dev:
+        released, _ = single_event_schedule(s, ks, bsz, seed, dev=dev)
+    assert released > 0
 
 
 @pytest.mark.gpu
