@@ -856,7 +856,7 @@ def redundant(s, lo, hi, ks, bound):
     return O.redundant_collect(s.prefix(hi), **rb_map(ks, bound), min_epoch=0).txns(lo, hi)
 
 
-def schedule_rb(s, nkeys, bsz, seed, dev=None, inval_frac=0.05, rb_every=3, rounds_per_batch=3):
+def schedule_rb(s, nkeys, bsz, seed, dev=None, inval_frac=0.05, rb_every=3, rounds_per_batch=3, dev_events=False):
     """Batches STABLE at executeAt = TxnId except a few txns INVALIDATED (they never become ready;
     their dependents stop waiting for them), a few ready -> APPLIED rounds per batch, and every
     rb_every batches the store's RedundantBefore moves to shardAppliedOrInvalidatedBefore (the
@@ -864,11 +864,13 @@ def schedule_rb(s, nkeys, bsz, seed, dev=None, inval_frac=0.05, rb_every=3, roun
     histories (a new carry on the device: everything re-evaluated) and collectDeps adds the bound to
     the next batches' deps.  Returns every round's ready list, the invalidated txns and the driver."""
     rng = np.random.default_rng(seed)
-    d = Driver(s, nkeys, dev)
+    d = Driver(s, nkeys, dev, dev_events=dev_events)
     out, bound, inval = [], None, []
     for b, lo in enumerate(range(0, s.n, bsz)):
         hi = min(s.n, lo + bsz)
         part = d.ora.batch(s.slice(lo, hi))
+        if d.ev is not None:
+            d.ev.batch(s.slice(lo, hi))
         if bound is not None:
             part = O.deps_union([part, redundant(s, lo, hi, nkeys, bound)])
         if dev is not None:
@@ -891,6 +893,8 @@ def schedule_rb(s, nkeys, bsz, seed, dev=None, inval_frac=0.05, rb_every=3, roun
             if p > 0 and (bound is None or p > bound):
                 m = rb_map(nkeys, p)
                 d.ora.truncate(m["start"], m["end"], m["bound"])
+                if d.ev is not None:                     # event mode: notifyAndUpdatePending(prevCfk)
+                    d.ev.truncate(m["start"], m["end"], m["bound"])
                 if dev is not None:
                     dev.redundant_before(**m, min_epoch=0)
                 bound = p
@@ -904,6 +908,23 @@ def test_schedule_rb_oracle_progress():
     allr = np.concatenate(out)
     assert np.array_equal(np.sort(np.concatenate([allr, inval])), np.arange(s.n))
     assert d.ora.waiting == 0                            # invalidated txns leave the set, never ready
+
+
+def test_schedule_rb_events_oracle():
+    s = stable_stream(900, 30, 13, 0.1)
+    out, _, _ = schedule_rb(s, 30, 150, 13, dev_events=True)
+    assert sum(len(r) for r in out) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ks,bsz,seed,rf", [(1500, 40, 250, 13, 0.1), (1200, 30, 200, 14, 0.0)])
+def test_gpu_event_mode_truncation(gpu_device, n, ks, bsz, seed, rf):
+    """Event-exact mode with invalidations and RedundantBefore truncations (the truncated keys'
+    unmanaged records notified, or_lstore_truncate's notifyAndUpdatePending) == the event oracle."""
+    s = stable_stream(n, ks, seed, rf)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=ks, window=WINDOW_NONE, resident=True) as dev:
+        out, _, _ = schedule_rb(s, ks, bsz, seed, dev, dev_events=True)
+    assert sum(len(r) for r in out) > 0
 
 
 @pytest.mark.gpu
