@@ -1477,9 +1477,11 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     // setAppliedAndPropagate's tables: every position of the store, and a pool for the
     // appliedOrInvalidated of every waiting txn (bounded by its RangeDeps txnIds); the pool's fill
     // count rides in the header (cnt[HDR - 5]) and comes back with it
-    {
-        uint64_t pool_need = s->rdy_pv_n;
-        for (accord_impl::ReadyGen *r : s->rdy_gens) pool_need += r->left ? r->rvals : 0;
+    uint64_t rv_live = 0;                      // no range deps waiting: nothing to save or propagate
+    for (accord_impl::ReadyGen *r : s->rdy_gens) rv_live += r->left ? r->rvals : 0;
+    const bool pv_on = rv_live > 0;
+    if (pv_on) {
+        const uint64_t pool_need = s->rdy_pv_n + rv_live;
         const size_t pos_need = (size_t)s->next_global + s->n + 1;
         HIPCHECK(s, accord_impl::grow_keep(s->rdy_pv_at, s->rdy_pv_pos * 4, pos_need * 4, st));
         HIPCHECK(s, accord_impl::grow_keep(s->rdy_pv_len, s->rdy_pv_pos * 4, pos_need * 4, st));
@@ -1548,8 +1550,10 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.full = r->fresh ? 1u : 0u;
         any_inc |= !full && !r->fresh;
         p.chg = s->rg_chg.as<uint32_t>(); p.dirty = s->rdy_dirty2.as<uint32_t>();
-        p.pv_at = s->rdy_pv_at.as<uint32_t>(); p.pv_len = s->rdy_pv_len.as<uint32_t>();
-        p.pv_pool = s->rdy_pv_pool.as<uint32_t>(); p.pv_cnt = cnt + (HDR - 5);
+        if (pv_on) {
+            p.pv_at = s->rdy_pv_at.as<uint32_t>(); p.pv_len = s->rdy_pv_len.as<uint32_t>();
+            p.pv_pool = s->rdy_pv_pool.as<uint32_t>(); p.pv_cnt = cnt + (HDR - 5);
+        }
         r->fresh = false;
         L.gbase[L.ngen] = L.total;
         L.total += r->n;
@@ -1615,7 +1619,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         HIPCHECK(s, hipStreamSynchronize(st));
     }
     const uint32_t nr = peek[0], nd = peek[HDR - 1];
-    s->rdy_pv_n = peek[HDR - 5];
+    if (pv_on) s->rdy_pv_n = peek[HDR - 5];
     if (s->rdy_stats) {                          // ACCORD_READY_STATS: diagnostic totals (ready_destroy prints)
         s->rdy_stats[0] += 1; s->rdy_stats[1] += peek[1]; s->rdy_stats[2] += cap;
         if (any_inc && tabs.size() <= HDR - 8)
