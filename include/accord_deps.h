@@ -515,7 +515,8 @@ int32_t accord_ready_update(accord_store *store, accord_ready *out);
  *   gives the txns already Stable their transition's step; a truncation notifies the unmanaged
  *   records of the keys it took entries from.  accord_ready_update then evaluates the range-dep bits
  *   and releases.  Releases equal the event-driven restatement (oracle or_lstore_event_mode) call by
- *   call.  The replay is one wave per registration (a correctness mode, not a throughput one). */
+ *   call.  The replay is one wave per registration (a correctness mode, not a throughput one).
+ * The mode is a setting of the store: accord_store_reset empties the waiting set and keeps it. */
 #define ACCORD_READY_POLL   0u
 #define ACCORD_READY_EVENTS 1u
 int32_t accord_ready_set_mode(accord_store *store, uint32_t mode);

@@ -16,7 +16,7 @@ feedback, with range txns and EphemeralReads, through the C ABI.
 import numpy as np
 import pytest
 
-from accord_amd import NO_TXN, CommandStore, Stream, WINDOW_NONE, generate_stream
+from accord_amd import NO_TXN, CommandStore, IllegalStateException, Stream, WINDOW_NONE, generate_stream
 import oracle_lib as O
 from status_events import APPLIED, INVALID, STABLE, rb_map
 
@@ -650,6 +650,27 @@ def test_gpu_event_mode_single_events(gpu_device, n, ks, bsz, seed, rf, sp):
     with CommandStore(device=gpu_device, key_lo=0, key_hi=ks, window=WINDOW_NONE, resident=True) as dev:
         released, _ = single_event_schedule(s, ks, bsz, seed, dev=dev)
     assert released > 0
+
+
+@pytest.mark.gpu
+def test_gpu_ready_mode_guards(gpu_device):
+    """accord_ready_set_mode: registered-status stores only, never with txns waiting; the mode
+    survives accord_store_reset (a store setting, not state)."""
+    s = mk(EV_KAT)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=256) as plain:
+        with pytest.raises(IllegalStateException):
+            plain.ready_mode(True)
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        dev.ready_mode(True)
+        d = Driver(s, 4, dev, dev_events=True)
+        part = d.batch(0, 2)
+        d.register([0, 1], STABLE)
+        d.initialise(0, part)
+        with pytest.raises(IllegalStateException):
+            dev.ready_mode(False)                         # txns wait
+        assert list(d.round()) == [0]
+        dev.reset()
+        dev.ready_mode(False)
 
 
 @pytest.mark.gpu
