@@ -108,6 +108,9 @@ struct KeyDepsParams {
     // far list): listed by the general kernel, built by a workgroup each (big_wex: scratch per pair)
     uint32_t *big_list, *big_count, *big_wex;
     uint32_t tiny;                     // thread-per-txn pass for tiny txns (batches of few keys per txn)
+    // speculative fill (store.cpp): a word set by launch_spec_check when the outputs would not fit;
+    // every fill kernel then returns at once.  nullptr: the fill runs unconditionally
+    const uint32_t *abort;
 };
 
 // Where a batch sits in the store's stream: global positions start at min_gi, and (has_prev) the
@@ -117,6 +120,10 @@ struct StreamPos {
     uint64_t prev_msb, prev_lsb;
     int32_t prev_node, pad;
 };
+// speculative fill: *abort = 1 when a KeyDeps total (keys, txnIds bound, k2v) exceeds the capacity
+// the output arrays already have, or the batch failed validation -- the fill kernels then return
+void launch_spec_check(const unsigned long long *totals, const DevStatus *status, uint64_t cap_keys, uint64_t cap_vals,
+                       uint64_t cap_k2v, uint32_t *abort, hipStream_t s);
 // txn-major validation + (key, entry) pair packing; range CSR owners and range-txn flags
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,

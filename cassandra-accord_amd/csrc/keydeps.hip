@@ -714,6 +714,7 @@ __device__ __forceinline__ void slot_setup(uint32_t lo, uint32_t pos, uint32_t k
 template <int WPL, int MINW = (WPL == 1 ? 8 : 4)>
 __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void keydeps_kernel(KeyDepsParams p)
 {
+    if (p.abort && *p.abort) return;           // speculative fill: outputs too small
     __shared__ WaveLds<WPL> lds_all[KD_WAVES];
     const uint32_t w = wave_id(), lane = lane_id();
     WaveLds<WPL> &L = lds_all[w];
@@ -1057,6 +1058,7 @@ template <int BPL>
 __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void keydeps_fast_kernel(
     KeyDepsParams p, const TxnRec *__restrict__ recs)
 {
+    if (p.abort && *p.abort) return;           // speculative fill: outputs too small
     constexpr uint32_t SPAN = 64u * BPL;
     __shared__ __attribute__((aligned(16))) uint8_t map_all[KD_WAVES][SPAN];   // near map (bytes)
     __shared__ uint32_t fr_all[KD_WAVES][64];       // far deps: value, then its rank
@@ -1283,6 +1285,7 @@ __device__ __forceinline__ uint32_t bk_min(uint32_t v, uint32_t *sh)
 
 __global__ __launch_bounds__(BK_THREADS) void keydeps_big_kernel(KeyDepsParams p)
 {
+    if (p.abort && *p.abort) return;           // speculative fill: outputs too small
     __shared__ unsigned long long bm[BK_WORDS];
     __shared__ uint32_t pre[BK_WORDS];
     __shared__ uint32_t sh[BK_THREADS / 64];
@@ -1407,6 +1410,7 @@ __global__ __launch_bounds__(BK_THREADS) void keydeps_big_kernel(KeyDepsParams p
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void keydeps_tiny_kernel(KeyDepsParams p)
 {
+    if (p.abort && *p.abort) return;           // speculative fill: outputs too small
     // launched (and skipped by the fast kernel) only for batches of few keys per txn: with the
     // fast kernel's per-txn pipeline running over every txn anyway, a thread-per-txn pass pays off
     // only when tiny txns are the bulk (measured: config 5, 4 keys/txn, +0.26 ms; an 8-rank store
@@ -1492,6 +1496,16 @@ void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_
         hipLaunchKernelGGL((keydeps_fast_kernel<16>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs);
     } else {
         hipLaunchKernelGGL((keydeps_fast_kernel<32>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs);
+    }
+}
+
+__global__ void spec_check_kernel(const unsigned long long *__restrict__ totals, const DevStatus *__restrict__ st,
+                                  unsigned long long c0, unsigned long long c1, unsigned long long c2,
+                                  uint32_t *__restrict__ abort)
+{
+    if (threadIdx.x == 0) {
+        const bool bad = totals[0] > c0 || totals[1] > c1 || totals[2] > c2 || st->first != ~0ull || st->overflow;
+        *abort = bad ? 1u : 0u;
     }
 }
 
@@ -1591,6 +1605,15 @@ __global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uin
 }
 
 } // namespace
+
+void launch_spec_check(const unsigned long long *totals, const DevStatus *status, uint64_t cap_keys, uint64_t cap_vals,
+                       uint64_t cap_k2v, uint32_t *abort, hipStream_t s)
+{
+    // the kernels address every output array with 32-bit byte offsets: totals past 2^30 never fit
+    const uint64_t lim = (1ull << 30) - 1;
+    hipLaunchKernelGGL(spec_check_kernel, dim3(1), dim3(64), 0, s, totals, status, std::min(cap_keys, lim),
+                       std::min(cap_vals, lim), std::min(cap_k2v, lim), abort);
+}
 
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,

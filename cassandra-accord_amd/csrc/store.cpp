@@ -551,8 +551,21 @@ int32_t accord_deps_compute(accord_store *s)
     kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.vub_off = s->vub_off.as<uint32_t>();
     kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
     accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
-    HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
-    HIPCHECK(s, hipStreamSynchronize(st));
+    // Speculative fill (key-only batches of a status-at-time store): the output arrays keep the
+    // capacity earlier batches gave them, and the fill is queued behind the sizes without the host
+    // reading them first -- a device check (launch_spec_check) aborts it when a total would not fit or
+    // the batch failed validation, and only then does the host grow the arrays and fill again.  A
+    // stream of like-sized batches never waits on the host mid-pipeline.  ACCORD_SPEC_FILL=0: off.
+    static const bool spec_env = [] { const char *e = getenv("ACCORD_SPEC_FILL"); return !(e && e[0] == '0'); }();
+    const bool spec = spec_env && n && !nrt && !rdeps && !s->rb_m && !accord_impl::registered_mode(s) &&
+                      s->kd_keys.p && s->vgap.p && s->kd_k2v.p;
+    if (spec) {
+        accord::launch_spec_check(&dev->totals[0], &dev->status, s->kd_keys.cap / 4, s->vgap.cap / 4 - 1,
+                                  s->kd_k2v.cap / 4, &dev->spec_abort, st);
+    } else {
+        HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+    }
 
     auto check_status = [&](const HostTotals &h) -> int32_t {
         if (h.status.first != ~0ull) {
@@ -565,7 +578,8 @@ int32_t accord_deps_compute(accord_store *s)
                         h.status.overflow, h.status.overflow_first);
         return ACCORD_OK;
     };
-    {
+    // the sizes are on the host: check them, take them, size the outputs
+    auto take_sizes = [&]() -> int32_t {
         const HostTotals &h = *s->pinned;
         int32_t rc = check_status(h);
         if (rc) return rc;
@@ -574,8 +588,23 @@ int32_t accord_deps_compute(accord_store *s)
             if (h.totals[t] >= (1ull << 30)) return fail(s, ACCORD_ERR_CAPACITY, "deps output exceeds 2^30 entries");
         s->tot_keys = h.totals[0]; s->tot_k2v = h.totals[2];
         s->tot_rngs = h.totals[3]; s->tot_rvals = h.totals[4]; s->tot_r2v = h.totals[5];
+        return ACCORD_OK;
+    };
+    auto size_outputs = [&]() -> int32_t {
+        HIPCHECK(s, s->kd_keys.ensure(s->tot_keys * 4));
+        HIPCHECK(s, s->vgap.ensure(s->pinned->totals[1] * 4 + 4));   // KeyDeps txnIds, gapped (accord_deps.kd_val_cnt)
+        HIPCHECK(s, s->kd_k2v.ensure(s->tot_k2v * 4));
+        HIPCHECK(s, s->rd_rng_start.ensure(s->tot_rngs * 4));
+        HIPCHECK(s, s->rd_rng_end.ensure(s->tot_rngs * 4));
+        HIPCHECK(s, s->rd_vals.ensure(s->tot_rvals * 4));
+        HIPCHECK(s, s->rd_r2v.ensure(s->tot_r2v * 4));
+        kp.kd_keys = s->kd_keys.as<uint32_t>(); kp.vgap = s->vgap.as<uint32_t>(); kp.kd_k2v = s->kd_k2v.as<int32_t>();
+        return ACCORD_OK;
+    };
+    if (!spec) {
+        int32_t rc = take_sizes();
+        if (rc) return rc;
     }
-    const uint64_t vub_total = s->pinned->totals[1];
     if (general) {                                      // the fill reads the extended history
         const uint32_t *h = nullptr;
         int32_t rc = accord_impl::status_general_emit(s, PH, s->pinned->totals[9], &h);
@@ -583,16 +612,15 @@ int32_t accord_deps_compute(accord_store *s)
         kp.hist = h;
         rp.hist = h;
     }
-    HIPCHECK(s, s->kd_keys.ensure(s->tot_keys * 4));
-    HIPCHECK(s, s->vgap.ensure(vub_total * 4 + 4));   // KeyDeps txnIds, gapped (accord_deps.kd_val_cnt)
-    HIPCHECK(s, s->kd_k2v.ensure(s->tot_k2v * 4));
-    HIPCHECK(s, s->rd_rng_start.ensure(s->tot_rngs * 4));
-    HIPCHECK(s, s->rd_rng_end.ensure(s->tot_rngs * 4));
-    HIPCHECK(s, s->rd_vals.ensure(s->tot_rvals * 4));
-    HIPCHECK(s, s->rd_r2v.ensure(s->tot_r2v * 4));
+    if (spec) {     // the arrays as they are: the check aborts the fill if they are too small
+        kp.kd_keys = s->kd_keys.as<uint32_t>(); kp.vgap = s->vgap.as<uint32_t>(); kp.kd_k2v = s->kd_k2v.as<int32_t>();
+        kp.abort = &dev->spec_abort;
+    } else {
+        int32_t rc = size_outputs();
+        if (rc) return rc;
+    }
     kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.vub_off = s->vub_off.as<uint32_t>();
     kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
-    kp.kd_keys = s->kd_keys.as<uint32_t>(); kp.vgap = s->vgap.as<uint32_t>(); kp.kd_k2v = s->kd_k2v.as<int32_t>();
     rp.kd_key_off = kp.kd_key_off; rp.kd_val_off = kp.vub_off; rp.kd_k2v_off = kp.kd_k2v_off;
     rp.kd_keys = kp.kd_keys; rp.kd_vals = kp.vgap; rp.kd_k2v = kp.kd_k2v;
     rp.rd_rng_off = s->rd_rng_off.as<uint32_t>(); rp.rd_val_off = s->rd_val_off.as<uint32_t>();
@@ -659,10 +687,26 @@ int32_t accord_deps_compute(accord_store *s)
                                    hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
+    if (spec) {
+        int32_t rc = take_sizes();
+        if (rc) return rc;
+        if (s->pinned->spec_abort) {    // the outputs did not fit: grow them and fill again
+            rc = size_outputs();
+            if (rc) return rc;
+            kp.abort = nullptr;
+            accord::launch_keydeps_fill(kp, s->wpl, s->fk_recs.p, st);
+            record(s, EV_FILL);
+            record(s, EV_RANGE);
+            record(s, EV_COMPACT);
+            HIPCHECK(s, hipMemcpyAsync(&s->pinned->status, &dev->status, sizeof(accord::DevStatus), hipMemcpyDeviceToHost, st));
+            HIPCHECK(s, hipStreamSynchronize(st));
+            HIPCHECK(s, hipGetLastError());
+        }
+    }
     {
         int32_t rc = check_status(*s->pinned);
         if (rc) return rc;
-        s->tot_vals = vub_total;
+        s->tot_vals = s->pinned->totals[1];
     }
     if (s->resident) {      // the batch is part of the store's stream now
         if (accord_impl::registered_mode(s)) {

@@ -52,6 +52,7 @@ struct HostTotals {
     unsigned long long rb_tot[3];   // RedundantBefore deps: ranges, vals, r2v (counted during compute)
     accord::DevStatus rb_status;    // its capacity status, apart from the compute's
     accord::ScanCounters scan;      // the store's scan-state counters (profiled stores read them)
+    uint32_t spec_abort, spec_pad;  // speculative fill: the outputs did not fit (accord_deps_compute)
 };
 
 // A device-resident PartialDeps set (result of accord_deps_union / accord_deps_slice).

@@ -109,3 +109,20 @@ def test_device_resident_repeat(gpu_device):
     assert a.equals(b)
     assert t.total_ms > 0
     assert a.first_difference(O.deps_fast(s, 256)) is None
+
+
+def test_speculative_fill_grow_shrink_and_errors(gpu_device):
+    # one store over batches of changing size: after the first, the fill runs speculatively into the
+    # arrays an earlier batch sized (store.cpp, launch_spec_check) -- a larger batch aborts it and is
+    # filled again into grown arrays; an invalid batch fails as before and leaves the store usable
+    ks, W = 3000, 256
+    with CommandStore(device=0, key_lo=0, key_hi=ks, window=W) as st:
+        for n, k, z, seed in [(500, 4, 0.0, 21), (2000, 4, 0.0, 22), (60000, 8, 0.99, 23), (100, 2, 0.0, 24),
+                              (60000, 8, 0.99, 25), (30000, 12, 0.99, 26)]:
+            s = generate_stream(n, k, ks, z, 0.5, seed=seed)
+            got = st.calculate_deps_batch(s)
+            assert got.first_difference(O.deps_fast(s, W)) is None, (n, seed)
+            if n == 100:
+                bad = generate_stream(200, 2, ks * 2, seed=3)      # keys outside the store
+                with pytest.raises(IllegalArgumentException):
+                    st.calculate_deps_batch(bad)
