@@ -465,7 +465,8 @@ def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
     (accord_redundant_before_set: CommandsForKey.withRedundantBefore truncates the resident history,
     RedundantBefore.collectDeps adds the bound to every later txn's deps).  Per batch: the compute's
     device time (HIP events) and stages, and the host wall time of compute, register and
-    RedundantBefore calls (uploads excluded).  Beside it: the status-at-time resident store (window
+    RedundantBefore calls (uploads excluded) -- the walls from a second pass over a store without the
+    profiling events (compute_wall_profiled_ms_per_batch: with them).  Beside it: the status-at-time resident store (window
     W) fed the same batches, for the fill-stage comparison."""
     from accord_amd import CommandStore, WINDOW_NONE
     bsz, nb = args.reg_batch, args.reg_batches
@@ -485,9 +486,9 @@ def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
 
     evs = [events(b) for b in range(nb)]
 
-    def run(window, with_events):
+    def run(window, with_events, profile=True):
         best = None
-        with CommandStore(device=0, key_lo=0, key_hi=ks, window=window, profile=True, resident=True) as st:
+        with CommandStore(device=0, key_lo=0, key_hi=ks, window=window, profile=profile, resident=True) as st:
             for _ in range(reps + 1):
                 st.reset()
                 st.redundant_before()
@@ -501,13 +502,14 @@ def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
                     t0 = time.perf_counter()
                     st.compute()
                     t1 = time.perf_counter()
-                    t = st.timing()
-                    acc["device_ms"] += t.total_ms
-                    acc["fill_ms"] += t.fill_ms
-                    acc["count_ms"] += t.count_ms
-                    acc["sort_ms"] += t.sort_ms
-                    acc["segment_ms"] += t.segment_ms
-                    acc["compact_ms"] += t.compact_ms
+                    if profile:
+                        t = st.timing()
+                        acc["device_ms"] += t.total_ms
+                        acc["fill_ms"] += t.fill_ms
+                        acc["count_ms"] += t.count_ms
+                        acc["sort_ms"] += t.sort_ms
+                        acc["segment_ms"] += t.segment_ms
+                        acc["compact_ms"] += t.compact_ms
                     acc["compute_wall_ms"] += (t1 - t0) * 1e3
                     if with_events:
                         t2 = time.perf_counter()
@@ -526,9 +528,15 @@ def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
         per["carry_entries_end"] = carry
         return per, acc
 
+    # device stages from a profiled store (HIP events on its stream); the host walls from a store
+    # without them (the events' records cost ~2 us of host time each, a dozen per compute)
     reg, racc = run(WINDOW_NONE, True)
     sat, _ = run(args.window, False)
-    wall = racc["compute_wall_ms"] + racc["register_wall_ms"] + racc["rb_wall_ms"]
+    for per, win in ((reg, run(WINDOW_NONE, True, profile=False)[0]), (sat, run(args.window, False, profile=False)[0])):
+        per["compute_wall_profiled_ms_per_batch"] = per["compute_wall_ms_per_batch"]
+        for k in ("compute_wall_ms_per_batch", "register_wall_ms_per_batch", "rb_wall_ms_per_batch", "upload_wall_ms_per_batch"):
+            per[k] = win[k]
+    wall = (reg["compute_wall_ms_per_batch"] + reg["register_wall_ms_per_batch"] + reg["rb_wall_ms_per_batch"]) * nb
     return {"schedule": f"{nb} batches x {bsz} txns of the config-2 stream; after batch b: COMMITTED "
                         f"(executeAt = TxnId) for b, APPLIED for b-{lag_applied}, RedundantBefore = first txn "
                         f"of b-{lag_rb}",

@@ -351,9 +351,12 @@ int32_t redundant_count(accord_store *s)
     accord::launch_rb_count(p, st);
     HIPCHECK(s, s->op_tmp[T_SCAN].ensure_zeroed(accord::scan_temp_bytes(n), st));
     void *tmp = s->op_tmp[T_SCAN].p;
-    accord::exclusive_scan_u32(p.cnt_rngs, r.rng_off.as<uint32_t>(), n, &dev->rb_tot[0], tmp, st);
-    accord::exclusive_scan_u32(p.cnt_vals, r.rval_off.as<uint32_t>(), n, &dev->rb_tot[1], tmp, st);
-    accord::exclusive_scan_u32(p.cnt_r2v, r.r_off.as<uint32_t>(), n, &dev->rb_tot[2], tmp, st);
+    {   // the three offsets in one launch
+        const uint32_t *in[3] = {p.cnt_rngs, p.cnt_vals, p.cnt_r2v};
+        uint32_t *out[3] = {r.rng_off.as<uint32_t>(), r.rval_off.as<uint32_t>(), r.r_off.as<uint32_t>()};
+        unsigned long long *tot[3] = {&dev->rb_tot[0], &dev->rb_tot[1], &dev->rb_tot[2]};
+        accord::exclusive_scan_multi(3, in, out, tot, n, tmp, st);
+    }
     HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;
 }

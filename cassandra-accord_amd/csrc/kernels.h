@@ -53,6 +53,7 @@ struct CopyList {
     }
 };
 void launch_copy_words(const CopyList &L, hipStream_t s);
+void launch_init_words(const FillList &F, const CopyList &L, hipStream_t s);   // both in one launch
 
 // ---- scan (scan.hip) ----
 // temp: a scan-state buffer of at least scan_temp_bytes(n) bytes, ZERO when allocated
@@ -122,8 +123,9 @@ struct StreamPos {
 };
 // speculative fill: *abort = 1 when a KeyDeps total (keys, txnIds bound, k2v) exceeds the capacity
 // the output arrays already have, or the batch failed validation -- the fill kernels then return
+// (xtot: the registered store's general-pass extension total, *xtot > cap_x aborts too; nullptr: none)
 void launch_spec_check(const unsigned long long *totals, const DevStatus *status, uint64_t cap_keys, uint64_t cap_vals,
-                       uint64_t cap_k2v, uint32_t *abort, hipStream_t s);
+                       uint64_t cap_k2v, const unsigned long long *xtot, uint64_t cap_x, uint32_t *abort, hipStream_t s);
 // txn-major validation + (key, entry) pair packing; range CSR owners and range-txn flags
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,

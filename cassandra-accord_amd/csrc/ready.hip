@@ -335,15 +335,19 @@ struct ReadyLaunch {
 __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, uint32_t t, uint32_t lane, const RrBuf &rl,
                                             bool spill);
 
-// Incremental calls: a lane per waiting txn keeps those whose inputs changed since the last call
-// (the txn itself, the key of a set key bit dirty -- for a managed txn: and no longer blocked by the
-// key's class minima --, the txn of a set range-dep bit changed) or that were never evaluated;
-// wave-aggregated appends to work[].
+// Incremental calls: RF_LANES lanes per waiting txn keep those whose inputs changed since the last
+// call (the txn itself, the key of a set key bit dirty -- for a managed txn: and no longer blocked by
+// the key's class minima --, the txn of a set range-dep bit changed) or that were never evaluated;
+// wave-aggregated appends to work[].  The lanes of a txn take its set WaitingOn bits round-robin, so
+// a txn's bit tests (each a chain of dependent loads: key, dirty mark, summary, executeAt) run side
+// by side (a lane per txn walking its bits in turn took 14.8 us per call, profiles/r05_ready).
 // (seen: the change epoch of the last call, call: this call's id, full: evaluate everything)
+constexpr uint32_t RF_LANES = 8;
 __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__restrict__ L, uint32_t seen, uint32_t call,
                                                         uint32_t full)
 {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id();
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x, lane = lane_id();
+    const uint32_t u = gt / RF_LANES, sub = gt % RF_LANES;
     const uint32_t ngen = L->ngen, total = L->total;
     bool need = false;
     if (u < total) {
@@ -365,12 +369,18 @@ __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__res
             const uint32_t wmask = witness_mask(kind);
             Ts ex{0, 0, 0};
             if (stable) ex = exec_of(p.v, g);
+            uint32_t rank0 = 0;                       // set bits before word q
             for (uint32_t q = 0; q < nw && !need; ++q) {
-                unsigned long long w = p.words[w0 + q];
-                while (w && !need) {
+                const unsigned long long wq = p.words[w0 + q];
+                const uint32_t c = (uint32_t)__popcll(wq);
+                // this lane's bits of the word: ranks r = sub (mod RF_LANES) among the txn's set bits
+                uint32_t r = rank0 + ((sub + RF_LANES - rank0 % RF_LANES) % RF_LANES);
+                unsigned long long w = wq;
+                for (uint32_t k = rank0; k < r && w; ++k) w &= w - 1ull;   // drop the bits before rank r
+                for (; r < rank0 + c && !need; r += RF_LANES) {
                     const uint32_t b = q * 64u + (uint32_t)__ffsll((long long)w) - 1u;
+                    for (uint32_t k = 0; k < RF_LANES && w; ++k) w &= w - 1ull;   // next: rank r + RF_LANES
                     if (b >= RK) break;
-                    w &= w - 1ull;
                     if (b < R) { need = p.chg[p.rd_vals[p.rd_off[t] + b]] > seen; continue; }
                     const uint32_t kk = p.keys[p.key_off[t] + b - R] - p.key_lo;
                     if (p.dirty[kk] != call) continue;
@@ -383,16 +393,38 @@ __global__ __launch_bounds__(256) void rd_filter_kernel(const ReadyLaunch *__res
                     if (!blocked && ((wmask >> 3) & 1u) && sm.min_cls[2] != NONE && tcmp(exec_of(p.v, sm.min_cls[2]), ex) < 0) blocked = true;
                     need = !blocked;
                 }
+                rank0 += c;
             }
         }
     }
-    const unsigned long long m = __ballot(need);
+    // a txn is kept when any of its lanes needs it; its first lane appends it
+    const unsigned long long nb = __ballot(need);
+    const uint32_t gbase = lane & ~(RF_LANES - 1u);
+    const bool keep = sub == 0 && ((nb >> gbase) & ((1ull << RF_LANES) - 1ull)) != 0ull;
+    const unsigned long long m = __ballot(keep);
     if (m) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(L->wcnt, (uint32_t)__popcll(m));
         base = (uint32_t)__shfl((int)base, 0, 64);
-        if (need) L->work[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = u;
+        if (keep) L->work[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = u;
     }
+}
+
+// The call's result read-back without a copy engine: one block after the evaluation copies the
+// header and the first ready records into the page-locked host buffer the host reads once the stream
+// has synchronised (a device-to-host copy after the kernels cost ~15 us of a ~60 us call: the hand-off
+// to the copy queue and the copy; the kernel boundary orders the evaluation's writes before it).
+// It also zeroes the header for the next call (one memset fewer) unless the removal spill pass
+// still has to run on it.
+__global__ __launch_bounds__(256) void rd_host_out_kernel(uint32_t *__restrict__ cnt, uint32_t *__restrict__ host,
+                                                          uint32_t hdr, uint32_t rw, uint32_t peek)
+{
+    const uint32_t words = hdr + min(cnt[0], peek) * rw;
+    const bool spill = cnt[hdr - 2] != 0;
+    for (uint32_t x = threadIdx.x; x < words; x += blockDim.x) host[x] = cnt[x];
+    __syncthreads();
+    if (!spill)
+        for (uint32_t x = threadIdx.x; x < hdr; x += blockDim.x) cnt[x] = 0u;
 }
 
 // a wave per txn: every txn of the launch (work == nullptr) or the listed ones
@@ -1473,7 +1505,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         HIPCHECK(s, hipHostMalloc(&s->rdy_host, (PEEK * RW + 64) * 4, hipHostMallocDefault));
     }
     constexpr uint32_t HDR = 64;               // rdy_out header words: ready count, dirty keys, work counts
-    HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, HDR * 4, st));
+    if (s->rdy_hdr_zero != s->rdy_out.p) HIPCHECK(s, hipMemsetAsync(s->rdy_out.p, 0, HDR * 4, st));
+    s->rdy_hdr_zero = nullptr;                 // until this call has read its header back
     // setAppliedAndPropagate's tables: every position of the store, and a pool for the
     // appliedOrInvalidated of every waiting txn (bounded by its RangeDeps txnIds); the pool's fill
     // count rides in the header (cnt[HDR - 5]) and comes back with it
@@ -1505,7 +1538,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     HIPCHECK(s, s->rdy_dirty.ensure_zeroed((size_t)nkeys * 4 + 4, st));
     HIPCHECK(s, s->rdy_dirty2.ensure_zeroed((size_t)nkeys * 4 + 4, st));
     HIPCHECK(s, s->rdy_dlist.ensure((size_t)nkeys * 4 + 4));
-    // cnt[0]: ready txns, cnt[1]: dirty keys, cnt[HDR - 1]: dropped txns
+    // cnt[0]: ready txns, cnt[1]: dirty keys, cnt[2 ..]: work counts, cnt[HDR - 5]: pool fill,
+    // cnt[HDR - 4 .. HDR - 2]: spill, cnt[HDR - 1]: dropped txns
     uint32_t *cnt = s->rdy_out.as<uint32_t>();
     ReadyOut *list = (ReadyOut *)(cnt + HDR);
     uint32_t *drop = (uint32_t *)(list + cap);
@@ -1593,21 +1627,29 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         s->rdy_tab_dev = s->rdy_launch.p;
     }
     const size_t rr_lds = s->rb_ext && s->rb_m ? 4 * sizeof(RrLds) : 0;   // removal scratch, a wave each
+    // (evaluating every txn of an incremental call instead of the filtered ones measured slower even
+    // at 8 k waiting txns: 23-42 us against 13 + 6 us, profiles/r05_ready)
     for (size_t i = 0; i < tabs.size(); ++i) {
         const ReadyLaunch *L = s->rdy_launch.as<ReadyLaunch>() + i;
         if (any_inc) {
-            hipLaunchKernelGGL(rd_filter_kernel, dim3((tabs[i].total + 255) / 256), dim3(256), 0, st, L, seen, call,
-                               full ? 1u : 0u);
+            hipLaunchKernelGGL(rd_filter_kernel, dim3(((uint64_t)tabs[i].total * RF_LANES + 255) / 256), dim3(256), 0, st, L,
+                               seen, call, full ? 1u : 0u);
             hipLaunchKernelGGL(rd_eval_kernel, dim3(std::min(grid_for_waves(tabs[i].total), 1024u)), dim3(256), rr_lds, st, L, 1u);
         } else {
             hipLaunchKernelGGL(rd_eval_kernel, dim3(grid_for_waves(tabs[i].total)), dim3(256), rr_lds, st, L, 0u);
         }
     }
+    uint32_t *peek = (uint32_t *)s->rdy_host;
+    {
+        void *peek_dev = nullptr;
+        HIPCHECK(s, hipHostGetDevicePointer(&peek_dev, peek, 0));
+        hipLaunchKernelGGL(rd_host_out_kernel, dim3(1), dim3(256), 0, st, cnt, (uint32_t *)peek_dev, HDR, RW,
+                           (uint32_t)std::min<uint64_t>(cap, PEEK));
+    }
     HIPCHECK(s, hipGetLastError());
     if (!s->rdy_stats && getenv("ACCORD_READY_STATS")) s->rdy_stats = new uint64_t[4]{0, 0, 0, 0};
-    uint32_t *peek = (uint32_t *)s->rdy_host;
-    HIPCHECK(s, hipMemcpyAsync(peek, cnt, (HDR + std::min<uint64_t>(cap, PEEK) * RW) * 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(s, hipStreamSynchronize(st));       // also: the parameter tables were consumed
+    HIPCHECK(s, hipStreamSynchronize(st));       // the header is in peek; the parameter tables were consumed
+    if (!peek[HDR - 2]) s->rdy_hdr_zero = s->rdy_out.p;   // rd_host_out_kernel zeroed it
     if (peek[HDR - 2]) {    // txns over the LDS removal scratch: the spill pass, then the header again
         const uint32_t nsp = peek[HDR - 2], blocks = std::min<uint32_t>((nsp + 3) / 4, 64u);
         HIPCHECK(s, s->rdy_spill_mem.ensure((size_t)blocks * 4 * rr_spill_wave_bytes(peek[HDR - 3], peek[HDR - 4])));

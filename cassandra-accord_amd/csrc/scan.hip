@@ -242,6 +242,63 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
         __hip_atomic_store(&hdr->ctl, (unsigned long long)e << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
+// n <= one tile: the same block scan without the tile id draw, the status publication or the look
+// back -- three device-scope atomics fewer on a small batch's many short scans (the state buffer's
+// epoch is untouched: the next multi-tile launch continues from it)
+template <int NA>
+__global__ __launch_bounds__(SC_THREADS) void sc_one_tile(ScanArgs a, uint32_t n)
+{
+    __shared__ uint64_t s_wsum[NA][SC_THREADS / 64];
+    __shared__ uint32_t tile[NA][SC_TILE];
+    const uint32_t tid = threadIdx.x, w = wave_id(), lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) {
+            const uint32_t idx = j * SC_THREADS + tid;
+            tile[k][idx] = idx < n ? a.in[k][idx] : 0u;
+        }
+    __syncthreads();
+    uint64_t local[NA], incl[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) acc += tile[k][tid * SC_ITEMS + j];
+        local[k] = acc;
+        incl[k] = wave_incl_scan64(acc);
+        if (lane == 63) s_wsum[k][w] = incl[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        uint64_t o = 0, t = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < SC_THREADS / 64; ++q) {
+            if (q < w) o += s_wsum[k][q];
+            t += s_wsum[k][q];
+        }
+        uint64_t run = o + incl[k] - local[k];
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) {
+            const uint32_t v = tile[k][tid * SC_ITEMS + j];
+            tile[k][tid * SC_ITEMS + j] = (uint32_t)run;
+            run += v;
+        }
+        if (tid == 0) {
+            a.out[k][n] = (uint32_t)t;
+            if (a.total[k]) *a.total[k] = t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+#pragma unroll
+        for (int j = 0; j < SC_ITEMS; ++j) {
+            const uint32_t idx = j * SC_THREADS + tid;
+            if (idx < n) a.out[k][idx] = tile[k][idx];
+        }
+}
 __global__ __launch_bounds__(256) void fill_words_kernel(FillList L)
 {
     const FillDesc d = L.d[blockIdx.y];
@@ -252,7 +309,31 @@ __global__ __launch_bounds__(256) void copy_words_kernel(CopyList L)
     const CopyDesc d = L.d[blockIdx.y];
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.words; i += gridDim.x * blockDim.x) d.dst[i] = d.src[i];
 }
+// fills and copies in one launch (a pipeline's small initialisations): blockIdx.y over the fills,
+// then the copies
+__global__ __launch_bounds__(256) void init_words_kernel(FillList F, CopyList L)
+{
+    const uint32_t y = blockIdx.y;
+    if (y < F.nd) {
+        const FillDesc d = F.d[y];
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.words; i += gridDim.x * blockDim.x) d.p[i] = d.value;
+    } else {
+        const CopyDesc d = L.d[y - F.nd];
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.words; i += gridDim.x * blockDim.x) d.dst[i] = d.src[i];
+    }
+}
 } // namespace
+
+void launch_init_words(const FillList &F, const CopyList &L, hipStream_t s)
+{
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k < F.nd; ++k) mx = F.d[k].words > mx ? F.d[k].words : mx;
+    for (uint32_t k = 0; k < L.nd; ++k) mx = L.d[k].words > mx ? L.d[k].words : mx;
+    if (F.nd + L.nd == 0 || mx == 0) return;
+    uint32_t bx = (mx + 255) / 256;
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(init_words_kernel, dim3(bx, F.nd + L.nd), dim3(256), 0, s, F, L);
+}
 
 void launch_copy_words(const CopyList &L, hipStream_t s)
 {
@@ -287,6 +368,15 @@ void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *ou
     if (tiles == 0) tiles = 1;
     ScanArgs a{};
     for (int k = 0; k < na; ++k) { a.in[k] = in[k]; a.out[k] = out[k]; a.total[k] = total[k]; }
+    if (tiles == 1) {
+        switch (na) {
+        case 1: hipLaunchKernelGGL(sc_one_tile<1>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        case 2: hipLaunchKernelGGL(sc_one_tile<2>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        case 3: hipLaunchKernelGGL(sc_one_tile<3>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        default: hipLaunchKernelGGL(sc_one_tile<4>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        }
+        return;
+    }
     ScanHeader *hdr = (ScanHeader *)temp;
     uint64_t *status = (uint64_t *)((char *)temp + sizeof(ScanHeader));
     switch (na) {

@@ -41,14 +41,6 @@ __device__ __forceinline__ void record_error(accord::DevStatus *st, uint32_t i, 
 }
 
 // keys whose carried history holds a txn with a registered status
-__global__ __launch_bounds__(256) void flag_keys_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
-                                                        const uint32_t *__restrict__ cent, StatusView v,
-                                                        uint32_t *__restrict__ flag)
-{
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x)
-        if (status_of(v, cent[c] & ENT_TXN_MASK) != ST_PREACCEPTED) flag[ckey[c]] = 1u;
-}
-
 struct GenParams {
     uint32_t n, key_lo;
     const uint64_t *msb, *lsb;
@@ -69,6 +61,7 @@ struct GenParams {
     // per history position (hx_*): hx = the committed entry of [key's first entry, x] executing last
     // (NONE: none), hu = the uncommitted entries there; skey = each position's key
     const uint32_t *hx, *hu, *skey;
+    const uint32_t *abort;            // speculative fill (store.cpp): the extension would not fit
 };
 
 // One pair, one wave (lanes stride over the pair's slice [lo, pos) of the key's history):
@@ -184,23 +177,8 @@ __device__ void general_pair(const GenParams &p, uint32_t t, uint32_t q, uint32_
     if (lane == 0) p.slice[q] = accord::PairSlice{out, out + c, c, sl.key};
 }
 
-// committed[] index of the Writes (see GenParams): flags, positions, running argmax by executeAt
-__global__ __launch_bounds__(256) void cw_flag_kernel(uint32_t P, const uint32_t *__restrict__ hist, StatusView v,
-                                                      uint32_t *__restrict__ flag)
-{
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x) {
-        const uint32_t e = hist[x];
-        flag[x] = (e >> ENT_KIND_SHIFT) == 1u && committed(status_of(v, e & ENT_TXN_MASK)) ? 1u : 0u;
-    }
-}
-
-__global__ __launch_bounds__(256) void cw_scatter_kernel(uint32_t P, const uint32_t *__restrict__ flag,
-                                                         const uint32_t *__restrict__ off, uint32_t *__restrict__ pos)
-{
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x)
-        if (flag[x]) pos[off[x]] = x;
-}
-
+// committed[] index of the Writes (see GenParams): flags and positions (gen_pre_kernel / gen_mid_kernel),
+// running argmax by executeAt
 // cw_pm[j] = the argmax by executeAt over the key's committed Writes up to j (ties: the later one;
 // executeAts are unique), as a segmented scan over the index in two passes so a hot key's long run
 // spreads over many waves:
@@ -294,13 +272,12 @@ __global__ __launch_bounds__(256) void cw_carry_kernel(uint32_t PH, const uint32
 
 // hx / hu (GenParams) in the same two passes as cw_pm: chunk-local segmented scans, then the
 // carries of runs crossing chunks.  chunk = {first key, last key, hx of the trailing run, hu of it}.
-__global__ __launch_bounds__(256) void hx_local_kernel(uint32_t PH, const uint32_t *__restrict__ hist,
-                                                       const uint32_t *__restrict__ skey, StatusView v,
-                                                       uint32_t *__restrict__ hx, uint32_t *__restrict__ hu,
-                                                       uint4 *__restrict__ chunk)
+__device__ __forceinline__ void hx_local_chunk(uint32_t PH, const uint32_t *__restrict__ hist,
+                                               const uint32_t *__restrict__ skey, const StatusView &v,
+                                               uint32_t *__restrict__ hx, uint32_t *__restrict__ hu,
+                                               uint4 *__restrict__ chunk, uint32_t c0, uint32_t lane)
 {
-    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t c0 = (blockIdx.x * (blockDim.x / 64) + wave_id()) * 64u; c0 < PH; c0 += waves * 64u) {
+    {
         const uint32_t x = c0 + lane;
         const bool valid = x < PH;
         const uint32_t key = valid ? skey[x] : 0xFFFFFFFFu;
@@ -326,16 +303,14 @@ __global__ __launch_bounds__(256) void hx_local_kernel(uint32_t PH, const uint32
     }
 }
 
-__global__ __launch_bounds__(256) void hx_carry_kernel(uint32_t PH, const uint32_t *__restrict__ hist,
-                                                       const uint32_t *__restrict__ skey, StatusView v,
-                                                       const uint4 *__restrict__ chunk, uint32_t *__restrict__ hx,
-                                                       uint32_t *__restrict__ hu)
+__device__ __forceinline__ void hx_carry_chunk(uint32_t PH, const uint32_t *__restrict__ hist,
+                                               const uint32_t *__restrict__ skey, const StatusView &v,
+                                               const uint4 *__restrict__ chunk, uint32_t *__restrict__ hx,
+                                               uint32_t *__restrict__ hu, uint32_t c, uint32_t lane)
 {
-    const uint32_t nch = (PH + 63u) / 64u;
-    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t c = blockIdx.x * (blockDim.x / 64) + wave_id(); c < nch; c += waves) {
+    {
         const uint32_t kf = chunk[c].x;
-        if (c == 0 || chunk[c - 1].y != kf) continue;             // wave-uniform: the run starts here
+        if (c == 0 || chunk[c - 1].y != kf) return;               // wave-uniform: the run starts here
         uint32_t best = 0xFFFFFFFFu, cnt = 0;
         Ts bex{0, 0, 0};
         for (uint32_t top = c; top > 0; top = top > 64u ? top - 64u : 0u) {
@@ -373,19 +348,79 @@ __global__ __launch_bounds__(256) void hx_carry_kernel(uint32_t PH, const uint32
     }
 }
 
-// A wave per txn over its keys that hold a registered status: the count pass narrows contiguous
-// pairs' slices itself and counts the others, the fill pass writes the counted ones.
+// The committed[] index and hx / hu in three launches instead of eight: a wave per 64 items of
+// each independent pass, the passes' wave ranges laid end to end in one grid.
+//   gen_pre_kernel : carried keys' flags (flag_keys), the committed-Write flags (cw_flag), hx / hu
+//                    chunk-local scans (hx_local)
+//   (scan of the committed-Write flags)
+//   gen_mid_kernel : the committed-Writes' positions (cw_scatter), hx / hu carries (hx_carry)
+//   cw_local_kernel, cw_carry_kernel as before
+__global__ __launch_bounds__(256) void gen_pre_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
+                                                      const uint32_t *__restrict__ cent, uint32_t PH,
+                                                      const uint32_t *__restrict__ hist, const uint32_t *__restrict__ skey,
+                                                      StatusView v, uint32_t *__restrict__ kflag, uint32_t *__restrict__ cwflag,
+                                                      uint32_t *__restrict__ hx, uint32_t *__restrict__ hu,
+                                                      uint4 *__restrict__ hxchunk)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    const uint32_t nC = (C + 63u) / 64u, nP = (PH + 63u) / 64u;
+    for (uint32_t w = blockIdx.x * (blockDim.x / 64) + wave_id(); w < nC + 2u * nP; w += waves) {
+        if (w < nC) {
+            const uint32_t c = w * 64u + lane;
+            if (c < C && status_of(v, cent[c] & ENT_TXN_MASK) != ST_PREACCEPTED) kflag[ckey[c]] = 1u;
+        } else if (w < nC + nP) {
+            const uint32_t x = (w - nC) * 64u + lane;
+            if (x < PH) {
+                const uint32_t e = hist[x];
+                cwflag[x] = (e >> ENT_KIND_SHIFT) == 1u && committed(status_of(v, e & ENT_TXN_MASK)) ? 1u : 0u;
+            }
+        } else {
+            hx_local_chunk(PH, hist, skey, v, hx, hu, hxchunk, (w - nC - nP) * 64u, lane);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void gen_mid_kernel(uint32_t PH, const uint32_t *__restrict__ cwflag,
+                                                      const uint32_t *__restrict__ cwoff, uint32_t *__restrict__ cwpos,
+                                                      const uint32_t *__restrict__ hist, const uint32_t *__restrict__ skey,
+                                                      StatusView v, const uint4 *__restrict__ hxchunk,
+                                                      uint32_t *__restrict__ hx, uint32_t *__restrict__ hu)
+{
+    const uint32_t lane = lane_id(), waves = gridDim.x * (blockDim.x / 64);
+    const uint32_t nP = (PH + 63u) / 64u;
+    for (uint32_t w = blockIdx.x * (blockDim.x / 64) + wave_id(); w < 2u * nP; w += waves) {
+        if (w < nP) {
+            const uint32_t x = w * 64u + lane;
+            if (x < PH && cwflag[x]) cwpos[cwoff[x]] = x;
+        } else {
+            hx_carry_chunk(PH, hist, skey, v, hxchunk, hx, hu, w - nP, lane);
+        }
+    }
+}
+
+// GEN_SPLIT waves per txn, each over every GEN_SPLIT-th of its keys that hold a registered status
+// (a pair's walk is a chain of dependent loads: a small batch's txns run their pairs side by side --
+// one wave per txn had taken 37 us per 1024-txn batch): the count pass narrows contiguous pairs'
+// slices itself and counts the others, the fill pass writes the counted ones.
+constexpr uint32_t GEN_SPLIT = 8;
 template <bool FILL>
 __global__ __launch_bounds__(256) void general_kernel(GenParams p)
 {
+    if (FILL && p.abort && *p.abort) return;
+    if (FILL)       // the extended history starts as the batch history (a copy launch fewer)
+        for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < p.ext_base; x += gridDim.x * blockDim.x)
+            p.hist2[x] = p.hist[x];
     const uint32_t lane = lane_id();
     const uint32_t waves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t t = blockIdx.x * (blockDim.x / 64) + wave_id(); t < p.n; t += waves)
-        for (uint32_t q = p.key_off[t]; q < p.key_off[t + 1]; ++q) {
+    const uint64_t total = (uint64_t)p.n * GEN_SPLIT;
+    for (uint64_t w = blockIdx.x * (blockDim.x / 64) + wave_id(); w < total; w += waves) {
+        const uint32_t t = (uint32_t)(w / GEN_SPLIT), k0 = (uint32_t)(w % GEN_SPLIT);
+        for (uint32_t q = p.key_off[t] + k0; q < p.key_off[t + 1]; q += GEN_SPLIT) {
             if (!p.flag[p.key_ord[q] - p.key_lo]) { if (!FILL && lane == 0) p.gcnt[q] = 0; continue; }
             if (FILL && p.gcnt[q] == 0) continue;          // contiguous pair: slice already set
             general_pair<FILL>(p, t, q, lane);
         }
+    }
 }
 
 // carry flags of a registered-status store: an entry stays until its txn is INVALID_OR_TRUNCATED
@@ -497,11 +532,20 @@ __global__ __launch_bounds__(256) void join_kernel(uint32_t n, uint32_t tx_n, co
                                                    uint64_t *__restrict__ tlsb, int32_t *__restrict__ tnode,
                                                    uint32_t *__restrict__ tg, uint8_t *__restrict__ st,
                                                    uint64_t *__restrict__ xmsb, uint64_t *__restrict__ xlsb,
-                                                   int32_t *__restrict__ xnode, uint32_t *__restrict__ chg, uint32_t epoch)
+                                                   int32_t *__restrict__ xnode, uint32_t *__restrict__ chg, uint32_t epoch,
+                                                   uint32_t *__restrict__ cchg, uint32_t known, uint32_t G)
 {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t g = gidx[t];
+        // the store's new positions [known, G): those no txn of this store holds (txn_index gaps, never
+        // looked at) before g -- and after the last txn -- start PREACCEPTED and unchanged
+        const uint32_t to = t + 1 == n ? G : g;
+        for (uint32_t q = t ? gidx[t - 1] + 1u : known; q < to; ++q) {
+            if (q == g) continue;
+            chg[q] = 0u; cchg[q] = 0u; st[q] = ST_PREACCEPTED;
+        }
         chg[g] = epoch;
+        cchg[g] = 0u;
         tmsb[tx_n + t] = msb[t]; tlsb[tx_n + t] = lsb[t]; tnode[tx_n + t] = node[t]; tg[tx_n + t] = g;
         st[g] = ST_PREACCEPTED;
         xmsb[g] = msb[t]; xlsb[g] = lsb[t]; xnode[g] = node[t];
@@ -907,20 +951,28 @@ int32_t status_general_count(accord_store *s, uint32_t C, uint32_t PH, bool *pen
     HIPCHECK(s, s->rg_goff.ensure(((size_t)P + 1) * 4));
     HIPCHECK(s, hipMemsetAsync(s->rg_flag.p, 0, (size_t)nkeys * 4, st));
     const StatusView v = view_of(s);
-    hipLaunchKernelGGL(flag_keys_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->cy_key.as<uint32_t>(),
-                       s->cy_ent.as<uint32_t>(), v, s->rg_flag.as<uint32_t>());
     s->rg_flag_ok = true;
-    {   // the committed[] index of the Writes over the combined history
+    {   // the committed[] index of the Writes over the combined history, hx / hu
         HIPCHECK(s, s->rg_cwflag.ensure(((size_t)PH + 1) * 4));
         HIPCHECK(s, s->rg_cwoff.ensure(((size_t)PH + 1) * 4));
         HIPCHECK(s, s->rg_cwpos.ensure((size_t)PH * 4 + 4));
         HIPCHECK(s, s->rg_cwpm.ensure((size_t)PH * 4 + 4));
+        HIPCHECK(s, s->rg_cwchunk.ensure(((size_t)PH / 64 + 2) * sizeof(uint4)));
+        HIPCHECK(s, s->rg_hxchunk.ensure(((size_t)PH / 64 + 2) * sizeof(uint4)));
+        HIPCHECK(s, s->rg_hx.ensure((size_t)PH * 4 + 4));
+        HIPCHECK(s, s->rg_hu.ensure((size_t)PH * 4 + 4));
         uint32_t *flag = s->rg_cwflag.as<uint32_t>(), *off = s->rg_cwoff.as<uint32_t>();
-        hipLaunchKernelGGL(cw_flag_kernel, dim3(grid_for(PH)), dim3(256), 0, st, PH, s->hist.as<uint32_t>(), v, flag);
+        const uint64_t w1 = (uint64_t)(C + 63) / 64 + 2ull * ((PH + 63) / 64);
+        hipLaunchKernelGGL(gen_pre_kernel, dim3((uint32_t)std::min<uint64_t>((w1 + 3) / 4, 8192u)), dim3(256), 0, st, C,
+                           s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), PH, s->hist.as<uint32_t>(),
+                           s->sort_key.as<uint32_t>(), v, s->rg_flag.as<uint32_t>(), flag, s->rg_hx.as<uint32_t>(),
+                           s->rg_hu.as<uint32_t>(), s->rg_hxchunk.as<uint4>());
         HostTotals *dv = s->status_totals.as<HostTotals>();
         accord::exclusive_scan_u32(flag, off, PH, &dv->totals[9], s->scan_tmp.p, st);
-        hipLaunchKernelGGL(cw_scatter_kernel, dim3(grid_for(PH)), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>());
-        HIPCHECK(s, s->rg_cwchunk.ensure(((size_t)PH / 64 + 2) * sizeof(uint4)));
+        const uint64_t w2 = 2ull * ((PH + 63) / 64);
+        hipLaunchKernelGGL(gen_mid_kernel, dim3((uint32_t)std::min<uint64_t>((w2 + 3) / 4, 8192u)), dim3(256), 0, st, PH,
+                           flag, off, s->rg_cwpos.as<uint32_t>(), s->hist.as<uint32_t>(), s->sort_key.as<uint32_t>(), v,
+                           s->rg_hxchunk.as<uint4>(), s->rg_hx.as<uint32_t>(), s->rg_hu.as<uint32_t>());
         const uint32_t cwb = std::min<uint32_t>((PH / 64 + 4) / 4, 8192u);
         hipLaunchKernelGGL(cw_local_kernel, dim3(cwb), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->sort_key.as<uint32_t>(), v, s->rg_cwpm.as<uint32_t>(),
@@ -928,17 +980,9 @@ int32_t status_general_count(accord_store *s, uint32_t C, uint32_t PH, bool *pen
         hipLaunchKernelGGL(cw_carry_kernel, dim3(cwb), dim3(256), 0, st, PH, flag, off, s->rg_cwpos.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->sort_key.as<uint32_t>(), v, s->rg_cwchunk.as<uint4>(),
                            s->rg_cwpm.as<uint32_t>());
-        HIPCHECK(s, s->rg_hx.ensure((size_t)PH * 4 + 4));
-        HIPCHECK(s, s->rg_hu.ensure((size_t)PH * 4 + 4));
-        hipLaunchKernelGGL(hx_local_kernel, dim3(cwb), dim3(256), 0, st, PH, s->hist.as<uint32_t>(),
-                           s->sort_key.as<uint32_t>(), v, s->rg_hx.as<uint32_t>(), s->rg_hu.as<uint32_t>(),
-                           s->rg_cwchunk.as<uint4>());
-        hipLaunchKernelGGL(hx_carry_kernel, dim3(cwb), dim3(256), 0, st, PH, s->hist.as<uint32_t>(),
-                           s->sort_key.as<uint32_t>(), v, s->rg_cwchunk.as<uint4>(), s->rg_hx.as<uint32_t>(),
-                           s->rg_hu.as<uint32_t>());
     }
     const GenParams g = general_params(s);
-    const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);     // a wave per txn
+    const uint32_t gw = (uint32_t)std::min<uint64_t>(((uint64_t)n * GEN_SPLIT + 3) / 4, 8192u);
     if (n) hipLaunchKernelGGL(general_kernel<false>, dim3(gw), dim3(256), 0, st, g);
     HostTotals *dev = s->status_totals.as<HostTotals>();
     accord::exclusive_scan_u32(g.gcnt, s->rg_goff.as<uint32_t>(), P, &dev->totals[9], s->scan_tmp.p, st);
@@ -946,19 +990,23 @@ int32_t status_general_count(accord_store *s, uint32_t C, uint32_t PH, bool *pen
     return ACCORD_OK;
 }
 
-int32_t status_general_emit(accord_store *s, uint32_t PH, uint64_t X, const uint32_t **hist_for_fill)
+// abort != nullptr (speculative fill): X is not known on the host yet -- the extension goes into
+// rg_hist2 as sized (the caller ensured PH + 1 entries), and the device check aborts the pass when
+// it does not fit
+int32_t status_general_emit(accord_store *s, uint32_t PH, uint64_t X, const uint32_t *abort,
+                            const uint32_t **hist_for_fill)
 {
     const uint32_t n = s->n;
     hipStream_t st = s->stream;
     *hist_for_fill = s->hist.as<uint32_t>();
-    if (X == 0) return ACCORD_OK;
+    if (X == 0 && !abort) return ACCORD_OK;
     if ((uint64_t)PH + X >= (1ull << 31)) return fail(s, ACCORD_ERR_CAPACITY, "general deps of %llu entries", (unsigned long long)X);
-    HIPCHECK(s, s->rg_hist2.ensure(((size_t)PH + X) * 4));
-    HIPCHECK(s, hipMemcpyAsync(s->rg_hist2.p, s->hist.p, (size_t)PH * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHECK(s, s->rg_hist2.ensure(((size_t)PH + (abort ? 1 : X)) * 4));
     GenParams g = general_params(s);
     g.hist2 = s->rg_hist2.as<uint32_t>();
     g.ext_base = PH;
-    const uint32_t gw = std::min<uint32_t>((n + 3) / 4, 8192u);
+    g.abort = abort;
+    const uint32_t gw = (uint32_t)std::min<uint64_t>(((uint64_t)n * GEN_SPLIT + 3) / 4, 8192u);
     if (n) hipLaunchKernelGGL(general_kernel<true>, dim3(gw), dim3(256), 0, st, g);
     *hist_for_fill = s->rg_hist2.as<uint32_t>();
     return ACCORD_OK;
@@ -1065,16 +1113,14 @@ int32_t status_join_batch(accord_store *s)
     HIPCHECK(s, grow_keep(s->rg_enode, G * 4, known * 4, st));
     HIPCHECK(s, grow_keep(s->rg_chg, G * 4, known * 4, st));
     HIPCHECK(s, grow_keep(s->rg_cchg, G * 4, known * 4, st));
-    if (G > known) HIPCHECK(s, hipMemsetAsync(s->rg_chg.as<uint32_t>() + known, 0, (G - known) * 4, st));
-    if (G > known) HIPCHECK(s, hipMemsetAsync(s->rg_cchg.as<uint32_t>() + known, 0, (G - known) * 4, st));
     ++s->rg_epoch;
-    if (G > known)   // positions no txn of this store holds (txn_index gaps): never looked at
-        HIPCHECK(s, hipMemsetAsync(s->rg_status.as<uint8_t>() + known, ST_PREACCEPTED, G - known, st));
+    // (the new positions' change words and statuses are initialised by the kernel: three memsets fewer)
     hipLaunchKernelGGL(join_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, (uint32_t)tx, s->msb.as<uint64_t>(),
                        s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
                        s->rg_tmsb.as<uint64_t>(), s->rg_tlsb.as<uint64_t>(), s->rg_tnode.as<int32_t>(),
                        s->rg_tg.as<uint32_t>(), s->rg_status.as<uint8_t>(), s->rg_emsb.as<uint64_t>(),
-                       s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>(), s->rg_chg.as<uint32_t>(), s->rg_epoch);
+                       s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>(), s->rg_chg.as<uint32_t>(), s->rg_epoch,
+                       s->rg_cchg.as<uint32_t>(), (uint32_t)known, (uint32_t)G);
     HIPCHECK(s, hipGetLastError());          // stream-ordered before anything that reads the tables
     s->rg_tx_n = (uint32_t)(tx + n);
     s->rg_known = (uint32_t)G;

@@ -122,7 +122,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->wo_aoi, &s->pred_cnt, &s->pred_off, &s->preds,
                       &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
                       &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
-                      &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2, &s->rg_kbound, &s->rg_cwflag, &s->rg_cwoff, &s->rg_cwpos, &s->rg_cwpm, &s->rg_cwchunk, &s->rg_hx, &s->rg_hu,
+                      &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2, &s->rg_kbound, &s->rg_cwflag, &s->rg_cwoff, &s->rg_cwpos, &s->rg_cwpm, &s->rg_cwchunk, &s->rg_hxchunk, &s->rg_hx, &s->rg_hu,
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
                       &s->rc_end2, &s->rc_kind2, &s->rc_first, &s->rc_flag, &s->rc_offs, &s->rdy_kseg0, &s->rdy_kseg1, &s->rdy_dirty, &s->rdy_dirty2, &s->rg_cchg, &s->rdy_dlist, &s->rdy_work, &s->rdy_wcnt, &s->rg_chg, &s->rdy_part, &s->rdy_sum, &s->rdy_out, &s->rdy_kb, &s->rdy_launch,
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero,
@@ -397,11 +397,12 @@ int32_t accord_deps_compute(accord_store *s)
             fl.add(s->rd_r2v_off.p, n1 * 4, 0u);
             fl.add(&dev->totals[3], 3 * sizeof(unsigned long long), 0u);
         }
-        accord::launch_fill_words(fl, st);
-    }
-    if (C) {
-        HIPCHECK(s, hipMemcpyAsync(s->pair_key.p, s->cy_key.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
-        HIPCHECK(s, hipMemcpyAsync(s->pair_ent.p, s->cy_ent.p, (size_t)C * 4, hipMemcpyDeviceToDevice, st));
+        accord::CopyList cl;          // a resident store's carried history heads the pairs
+        if (C) {
+            cl.add(s->cy_key.p, s->pair_key.p, (size_t)C * 4);
+            cl.add(s->cy_ent.p, s->pair_ent.p, (size_t)C * 4);
+        }
+        accord::launch_init_words(fl, cl, st);
     }
     accord::StreamPos sp{};
     sp.min_gi = s->resident ? s->next_global : 0u;
@@ -551,17 +552,22 @@ int32_t accord_deps_compute(accord_store *s)
     kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.vub_off = s->vub_off.as<uint32_t>();
     kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
     accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
-    // Speculative fill (key-only batches of a status-at-time store): the output arrays keep the
-    // capacity earlier batches gave them, and the fill is queued behind the sizes without the host
-    // reading them first -- a device check (launch_spec_check) aborts it when a total would not fit or
-    // the batch failed validation, and only then does the host grow the arrays and fill again.  A
-    // stream of like-sized batches never waits on the host mid-pipeline.  ACCORD_SPEC_FILL=0: off.
+    // Speculative fill (key-only batches): the output arrays -- and a registered store's extended
+    // history -- keep the capacity earlier batches gave them, and the fill is queued behind the sizes
+    // without the host reading them first; a device check (launch_spec_check) aborts it when a total
+    // would not fit or the batch failed validation, and only then does the host grow the arrays and
+    // fill again.  A stream of like-sized batches never waits on the host mid-pipeline.
+    // ACCORD_SPEC_FILL=0: off.
     static const bool spec_env = [] { const char *e = getenv("ACCORD_SPEC_FILL"); return !(e && e[0] == '0'); }();
-    const bool spec = spec_env && n && !nrt && !rdeps && !s->rb_m && !accord_impl::registered_mode(s) &&
-                      s->kd_keys.p && s->vgap.p && s->kd_k2v.p;
+    const bool spec = spec_env && n && !nrt && !rdeps && s->kd_keys.p && s->vgap.p && s->kd_k2v.p;
     if (spec) {
+        uint64_t cap_x = 0;
+        if (general) {
+            HIPCHECK(s, s->rg_hist2.ensure(((size_t)PH + 1) * 4));
+            cap_x = s->rg_hist2.cap / 4 - PH;
+        }
         accord::launch_spec_check(&dev->totals[0], &dev->status, s->kd_keys.cap / 4, s->vgap.cap / 4 - 1,
-                                  s->kd_k2v.cap / 4, &dev->spec_abort, st);
+                                  s->kd_k2v.cap / 4, general ? &dev->totals[9] : nullptr, cap_x, &dev->spec_abort, st);
     } else {
         HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
         HIPCHECK(s, hipStreamSynchronize(st));
@@ -607,7 +613,8 @@ int32_t accord_deps_compute(accord_store *s)
     }
     if (general) {                                      // the fill reads the extended history
         const uint32_t *h = nullptr;
-        int32_t rc = accord_impl::status_general_emit(s, PH, s->pinned->totals[9], &h);
+        int32_t rc = accord_impl::status_general_emit(s, PH, spec ? 0 : s->pinned->totals[9],
+                                                      spec ? &dev->spec_abort : nullptr, &h);
         if (rc) return rc;
         kp.hist = h;
         rp.hist = h;
@@ -691,6 +698,13 @@ int32_t accord_deps_compute(accord_store *s)
         int32_t rc = take_sizes();
         if (rc) return rc;
         if (s->pinned->spec_abort) {    // the outputs did not fit: grow them and fill again
+            if (general) {
+                const uint32_t *h = nullptr;
+                rc = accord_impl::status_general_emit(s, PH, s->pinned->totals[9], nullptr, &h);
+                if (rc) return rc;
+                kp.hist = h;
+                rp.hist = h;
+            }
             rc = size_outputs();
             if (rc) return rc;
             kp.abort = nullptr;

@@ -126,7 +126,7 @@ struct accord_store {
     // (rg_t*, rg_tx_n entries, rg_tg = global position), InternalStatus + executeAt by global
     // position (rg_known positions), per-batch work
     DevBuf rg_tmsb, rg_tlsb, rg_tnode, rg_tg, rg_status, rg_emsb, rg_elsb, rg_enode;
-    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound, rg_cwflag, rg_cwoff, rg_cwpos, rg_cwpm, rg_cwchunk, rg_hx, rg_hu;
+    DevBuf rg_flag, rg_gcnt, rg_goff, rg_hist2, rg_kbound, rg_cwflag, rg_cwoff, rg_cwpos, rg_cwpm, rg_cwchunk, rg_hxchunk, rg_hx, rg_hu;
     DevBuf rg_chg;                 // per global position: the registration epoch of its last status change
     DevBuf rg_cchg;                // ... of its last change from uncommitted to committed / invalid
     uint32_t rg_epoch = 1;
@@ -198,6 +198,7 @@ struct accord_store {
     size_t rdy_pv_pos = 0;                    // positions pv_at / pv_len cover
     DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dirty2, rdy_dlist, rdy_work, rdy_wcnt;
     uint32_t rdy_call = 0;                    // accord_ready_update calls (ids of the dirty marks)
+    const void *rdy_hdr_zero = nullptr;       // rdy_out whose header the last call left zeroed (rd_host_out_kernel)
     uint32_t rdy_seen = 0;                    // rg_epoch the last accord_ready_update saw
     uint64_t rdy_sum_version = ~0ull;         // carry version the key summaries belong to
     uint64_t rdy_kseg_version = ~0ull, carry_version = 0;   // the carry's segment bounds are cached per carry version
@@ -236,7 +237,8 @@ int32_t merge_finalize(accord_store *s);   // read a bounded merge's totals (sha
 // registered statuses (status.hip)
 bool registered_mode(const accord_store *s);
 int32_t status_general_count(accord_store *s, uint32_t C, uint32_t PH, bool *pending);
-int32_t status_general_emit(accord_store *s, uint32_t PH, uint64_t X, const uint32_t **hist_for_fill);
+int32_t status_general_emit(accord_store *s, uint32_t PH, uint64_t X, const uint32_t *abort,
+                            const uint32_t **hist_for_fill);
 int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
 int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
                               const uint32_t *bound);

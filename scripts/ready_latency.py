@@ -1,4 +1,4 @@
-"""Readiness call latency (accord_ready_update) on the bench's readiness schedule (bench.py
+"""Readiness call latency (and, --registered, the registered-batches compute leg) (accord_ready_update) on the bench's readiness schedule (bench.py
 ready_schedule): per-call host wall, and -- with --trace CSV from `rocprofv3 --kernel-trace
 --memory-copy-trace --output-format csv` -- the device work inside the calls (kernel busy time, copy
 time, idle gaps).  python scripts/ready_latency.py [--batches 4] [--batch 4096]
@@ -14,6 +14,16 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
 sys.path.insert(0, ROOT)
+
+
+def run_registered(a):
+    """the bench's registered-batches leg (bench.py registered_batches) alone"""
+    import types
+    import bench
+    from accord_amd import generate_stream
+    s = generate_stream(a.batches * a.batch, 8, 100_000, 0.99, 0.5, seed=2)
+    args = types.SimpleNamespace(reg_batch=a.batch, reg_batches=a.batches, keyspace=100_000, window=256)
+    print(json.dumps(bench.registered_batches(s, args)), flush=True)
 
 
 def run(a):
@@ -66,8 +76,9 @@ def analyse(d):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batches", type=int, default=4)
+    ap.add_argument("--batches", type=int, default=16)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--analyse", default=None)
+    ap.add_argument("--registered", action="store_true", help="the registered-batches leg instead")
     a = ap.parse_args()
-    analyse(a.analyse) if a.analyse else run(a)
+    analyse(a.analyse) if a.analyse else run_registered(a) if a.registered else run(a)
