@@ -340,13 +340,14 @@ int32_t redundant_count(accord_store *s)
     HIPCHECK(s, s->rb_cnt.ensure(3 * n1 * 4));
     HIPCHECK(s, r.rng_off.ensure(n1 * 4)); HIPCHECK(s, r.rval_off.ensure(n1 * 4)); HIPCHECK(s, r.r_off.ensure(n1 * 4));
     HostTotals *dev = s->status_totals.as<HostTotals>();
-    {
+    if (!s->rb_status_zeroed) {   // (the compute's init launch zeroes them when it runs first)
         accord::FillList fl;
         fl.add(&dev->rb_status.first, sizeof(dev->rb_status.first), 0xFFFFFFFFu);
         fl.add(&dev->rb_status.overflow, 4, 0u);
         fl.add(&dev->rb_status.overflow_first, 4, 0xFFFFFFFFu);
         accord::launch_fill_words(fl, st);
     }
+    s->rb_status_zeroed = false;
     const accord::RbParams p = rb_params(s);
     accord::launch_rb_count(p, st);
     HIPCHECK(s, s->op_tmp[T_SCAN].ensure_zeroed(accord::scan_temp_bytes(n), st));

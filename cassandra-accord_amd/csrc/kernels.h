@@ -30,7 +30,7 @@ struct FillDesc {
     uint32_t words, value;
 };
 struct FillList {
-    FillDesc d[12];
+    FillDesc d[16];
     uint32_t nd = 0;
     void add(void *p, size_t bytes, uint32_t value)
     {
@@ -70,9 +70,20 @@ inline const void *scan_counters(const void *temp) { return (const char *)temp +
 // out[i] = sum(in[0..i)), i in [0, n]; out has n+1 entries; total also written to *total_dev (u64).
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, unsigned long long *total_dev, void *temp,
                         hipStream_t s);
-// the same for na (1..4) arrays of n counts in one launch (total[k] may be null)
+// The speculative fill's check (store.cpp), done by the scan of the KeyDeps sizes as it writes the
+// totals: *abort = 1 when a total exceeds its capacity (keys, txnIds bound, k2v -- the scan's three
+// arrays), the registered store's general-pass extension *xtot exceeds cap_x, or *status records a
+// failure; else 0.
+struct SpecCheck {
+    uint32_t *abort;
+    const DevStatus *status;
+    const unsigned long long *xtot;    // nullptr: no extension
+    unsigned long long cap[3], cap_x;
+};
+// the same for na (1..4) arrays of n counts in one launch (total[k] may be null); spec (na == 3):
+// the speculative fill's check on the totals
 void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *out, unsigned long long *const *total,
-                          uint32_t n, void *temp, hipStream_t s);
+                          uint32_t n, void *temp, hipStream_t s, const SpecCheck *spec = nullptr);
 
 // ---- key deps pipeline (keydeps.hip) ----
 // Per (txn, key) pair, txn-major: the deps slice [lo, pos) of the key's history, the number of
@@ -109,7 +120,7 @@ struct KeyDepsParams {
     // far list): listed by the general kernel, built by a workgroup each (big_wex: scratch per pair)
     uint32_t *big_list, *big_count, *big_wex;
     uint32_t tiny;                     // thread-per-txn pass for tiny txns (batches of few keys per txn)
-    // speculative fill (store.cpp): a word set by launch_spec_check when the outputs would not fit;
+    // speculative fill (store.cpp): a word set by the sizes' scan (SpecCheck) when the outputs would not fit;
     // every fill kernel then returns at once.  nullptr: the fill runs unconditionally
     const uint32_t *abort;
 };
@@ -121,11 +132,6 @@ struct StreamPos {
     uint64_t prev_msb, prev_lsb;
     int32_t prev_node, pad;
 };
-// speculative fill: *abort = 1 when a KeyDeps total (keys, txnIds bound, k2v) exceeds the capacity
-// the output arrays already have, or the batch failed validation -- the fill kernels then return
-// (xtot: the registered store's general-pass extension total, *xtot > cap_x aborts too; nullptr: none)
-void launch_spec_check(const unsigned long long *totals, const DevStatus *status, uint64_t cap_keys, uint64_t cap_vals,
-                       uint64_t cap_k2v, const unsigned long long *xtot, uint64_t cap_x, uint32_t *abort, hipStream_t s);
 // txn-major validation + (key, entry) pair packing; range CSR owners and range-txn flags
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,

@@ -1499,18 +1499,6 @@ void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_
     }
 }
 
-__global__ void spec_check_kernel(const unsigned long long *__restrict__ totals, const DevStatus *__restrict__ st,
-                                  unsigned long long c0, unsigned long long c1, unsigned long long c2,
-                                  const unsigned long long *__restrict__ xtot, unsigned long long cx,
-                                  uint32_t *__restrict__ abort)
-{
-    if (threadIdx.x == 0) {
-        const bool bad = totals[0] > c0 || totals[1] > c1 || totals[2] > c2 || st->first != ~0ull || st->overflow ||
-                         (xtot && *xtot > cx);
-        *abort = bad ? 1u : 0u;
-    }
-}
-
 size_t fk_temp_bytes(uint32_t n) { return (size_t)n * sizeof(TxnRec) + 64; }
 
 void launch_keydeps(const KeyDepsParams &p, int wpl, hipStream_t s)
@@ -1608,14 +1596,6 @@ __global__ __launch_bounds__(256) void compact_vals_kernel(uint32_t n, const uin
 
 } // namespace
 
-void launch_spec_check(const unsigned long long *totals, const DevStatus *status, uint64_t cap_keys, uint64_t cap_vals,
-                       uint64_t cap_k2v, const unsigned long long *xtot, uint64_t cap_x, uint32_t *abort, hipStream_t s)
-{
-    // the kernels address every output array with 32-bit byte offsets: totals past 2^30 never fit
-    const uint64_t lim = (1ull << 30) - 1;
-    hipLaunchKernelGGL(spec_check_kernel, dim3(1), dim3(64), 0, s, totals, status, std::min(cap_keys, lim),
-                       std::min(cap_vals, lim), std::min(cap_k2v, lim), xtot, cap_x, abort);
-}
 
 void launch_validate_pack(uint32_t n, const uint64_t *msb, const uint64_t *lsb, const int32_t *node,
                           const uint32_t *key_off, const uint32_t *key_ord, const uint32_t *rng_off,

@@ -52,7 +52,18 @@ struct ScanArgs {
     const uint32_t *in[SC_MAX_ARRAYS];
     uint32_t *out[SC_MAX_ARRAYS];
     unsigned long long *total[SC_MAX_ARRAYS];
+    SpecCheck spec;
+    uint32_t has_spec;
 };
+
+// the speculative fill's check, by the thread that writes the totals (kernels.h SpecCheck)
+__device__ __forceinline__ void spec_eval(const ScanArgs &a, const uint64_t *tot)
+{
+    const SpecCheck &c = a.spec;
+    const bool bad = tot[0] > c.cap[0] || tot[1] > c.cap[1] || tot[2] > c.cap[2] || c.status->first != ~0ull ||
+                     c.status->overflow || (c.xtot && *c.xtot > c.cap_x);
+    *c.abort = bad ? 1u : 0u;
+}
 
 __device__ __forceinline__ uint64_t ld_status(const uint64_t *p)
 {
@@ -232,12 +243,16 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
         }
     }
     if (b == tiles - 1 && tid == 0) {
+        uint64_t tt[NA];
 #pragma unroll
         for (int k = 0; k < NA; ++k) {
             const uint64_t tot = s_excl[k] + agg[k];
+            tt[k] = tot;
             a.out[k][n] = (uint32_t)tot;
             if (a.total[k]) *a.total[k] = tot;
         }
+        if constexpr (NA == 3)
+            if (a.has_spec) spec_eval(a, tt);
         // every block has drawn its id (this one drew the last): rewind for the next launch
         __hip_atomic_store(&hdr->ctl, (unsigned long long)e << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -259,7 +274,7 @@ __global__ __launch_bounds__(SC_THREADS) void sc_one_tile(ScanArgs a, uint32_t n
             tile[k][idx] = idx < n ? a.in[k][idx] : 0u;
         }
     __syncthreads();
-    uint64_t local[NA], incl[NA];
+    uint64_t local[NA], incl[NA], tt[NA];
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
         uint64_t acc = 0;
@@ -285,11 +300,14 @@ __global__ __launch_bounds__(SC_THREADS) void sc_one_tile(ScanArgs a, uint32_t n
             tile[k][tid * SC_ITEMS + j] = (uint32_t)run;
             run += v;
         }
+        tt[k] = t;
         if (tid == 0) {
             a.out[k][n] = (uint32_t)t;
             if (a.total[k]) *a.total[k] = t;
         }
     }
+    if constexpr (NA == 3)
+        if (tid == 0 && a.has_spec) spec_eval(a, tt);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < NA; ++k)
@@ -362,12 +380,13 @@ size_t scan_temp_bytes(uint32_t n)
 }
 
 void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *out, unsigned long long *const *total,
-                          uint32_t n, void *temp, hipStream_t s)
+                          uint32_t n, void *temp, hipStream_t s, const SpecCheck *spec)
 {
     uint32_t tiles = (n + SC_TILE - 1) / SC_TILE;
     if (tiles == 0) tiles = 1;
     ScanArgs a{};
     for (int k = 0; k < na; ++k) { a.in[k] = in[k]; a.out[k] = out[k]; a.total[k] = total[k]; }
+    if (spec && na == 3) { a.spec = *spec; a.has_spec = 1u; }
     if (tiles == 1) {
         switch (na) {
         case 1: hipLaunchKernelGGL(sc_one_tile<1>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;

@@ -533,8 +533,11 @@ __global__ __launch_bounds__(256) void join_kernel(uint32_t n, uint32_t tx_n, co
                                                    uint32_t *__restrict__ tg, uint8_t *__restrict__ st,
                                                    uint64_t *__restrict__ xmsb, uint64_t *__restrict__ xlsb,
                                                    int32_t *__restrict__ xnode, uint32_t *__restrict__ chg, uint32_t epoch,
-                                                   uint32_t *__restrict__ cchg, uint32_t known, uint32_t G)
+                                                   uint32_t *__restrict__ cchg, uint32_t known, uint32_t G,
+                                                   const accord::DevStatus *__restrict__ guard)
 {
+    // queued before the compute's final host read: a batch the compute rejected joins nothing
+    if (guard->first != ~0ull || guard->overflow) return;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t g = gidx[t];
         // the store's new positions [known, G): those no txn of this store holds (txn_index gaps, never
@@ -949,7 +952,8 @@ int32_t status_general_count(accord_store *s, uint32_t C, uint32_t PH, bool *pen
     HIPCHECK(s, s->rg_flag.ensure((size_t)nkeys * 4 + 4));
     HIPCHECK(s, s->rg_gcnt.ensure((size_t)P * 4 + 4));
     HIPCHECK(s, s->rg_goff.ensure(((size_t)P + 1) * 4));
-    HIPCHECK(s, hipMemsetAsync(s->rg_flag.p, 0, (size_t)nkeys * 4, st));
+    if (!s->rg_flag_zeroed) HIPCHECK(s, hipMemsetAsync(s->rg_flag.p, 0, (size_t)nkeys * 4, st));
+    s->rg_flag_zeroed = false;
     const StatusView v = view_of(s);
     s->rg_flag_ok = true;
     {   // the committed[] index of the Writes over the combined history, hx / hu
@@ -1096,7 +1100,10 @@ int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start
 }
 
 // A computed batch of a registered-status store joins its txn tables (after the compute succeeded).
-int32_t status_join_batch(accord_store *s)
+// queued inside the compute, before its final host read (the launch's host cost overlaps the device
+// work); the kernel checks the compute's status itself, and status_join_commit takes the batch into
+// the host bookkeeping once the compute has succeeded
+int32_t status_join_queue(accord_store *s, const accord::DevStatus *guard)
 {
     const uint32_t n = s->n;
     if (n == 0) return ACCORD_OK;
@@ -1113,18 +1120,23 @@ int32_t status_join_batch(accord_store *s)
     HIPCHECK(s, grow_keep(s->rg_enode, G * 4, known * 4, st));
     HIPCHECK(s, grow_keep(s->rg_chg, G * 4, known * 4, st));
     HIPCHECK(s, grow_keep(s->rg_cchg, G * 4, known * 4, st));
-    ++s->rg_epoch;
     // (the new positions' change words and statuses are initialised by the kernel: three memsets fewer)
     hipLaunchKernelGGL(join_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, (uint32_t)tx, s->msb.as<uint64_t>(),
                        s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
                        s->rg_tmsb.as<uint64_t>(), s->rg_tlsb.as<uint64_t>(), s->rg_tnode.as<int32_t>(),
                        s->rg_tg.as<uint32_t>(), s->rg_status.as<uint8_t>(), s->rg_emsb.as<uint64_t>(),
-                       s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>(), s->rg_chg.as<uint32_t>(), s->rg_epoch,
-                       s->rg_cchg.as<uint32_t>(), (uint32_t)known, (uint32_t)G);
+                       s->rg_elsb.as<uint64_t>(), s->rg_enode.as<int32_t>(), s->rg_chg.as<uint32_t>(), s->rg_epoch + 1u,
+                       s->rg_cchg.as<uint32_t>(), (uint32_t)known, (uint32_t)G, guard);
     HIPCHECK(s, hipGetLastError());          // stream-ordered before anything that reads the tables
-    s->rg_tx_n = (uint32_t)(tx + n);
-    s->rg_known = (uint32_t)G;
     return ACCORD_OK;
+}
+
+void status_join_commit(accord_store *s)
+{
+    if (s->n == 0) return;
+    ++s->rg_epoch;
+    s->rg_tx_n += s->n;
+    s->rg_known = (uint32_t)s->b_end;
 }
 
 } // namespace accord_impl

@@ -397,6 +397,20 @@ int32_t accord_deps_compute(accord_store *s)
             fl.add(s->rd_r2v_off.p, n1 * 4, 0u);
             fl.add(&dev->totals[3], 3 * sizeof(unsigned long long), 0u);
         }
+        // the registered store's key flags and the RedundantBefore status, zeroed here rather than by
+        // launches of their own (status_general_count, redundant_count)
+        s->rg_flag_zeroed = s->rb_status_zeroed = false;
+        if (accord_impl::registered_mode(s) && C && s->next_global) {
+            HIPCHECK(s, s->rg_flag.ensure((size_t)nkeys * 4 + 4));
+            fl.add(s->rg_flag.p, (size_t)nkeys * 4, 0u);
+            s->rg_flag_zeroed = true;
+        }
+        if (s->rb_m) {
+            fl.add(&dev->rb_status.first, sizeof(dev->rb_status.first), 0xFFFFFFFFu);
+            fl.add(&dev->rb_status.overflow, 4, 0u);
+            fl.add(&dev->rb_status.overflow_first, 4, 0xFFFFFFFFu);
+            s->rb_status_zeroed = true;
+        }
         accord::CopyList cl;          // a resident store's carried history heads the pairs
         if (C) {
             cl.add(s->cy_key.p, s->pair_key.p, (size_t)C * 4);
@@ -534,11 +548,33 @@ int32_t accord_deps_compute(accord_store *s)
         accord::launch_rangedeps_count(rp, st);
     }
     record(s, EV_COUNT);
+    // Speculative fill (key-only batches): the output arrays -- and a registered store's extended
+    // history -- keep the capacity earlier batches gave them, and the fill is queued behind the sizes
+    // without the host reading them first; the scan of the KeyDeps sizes checks the totals against the
+    // capacities as it writes them (kernels.h SpecCheck) and sets an abort word every fill kernel
+    // reads first -- only then does the host grow the arrays and fill again, after the final sync.  A
+    // stream of like-sized batches never waits on the host mid-pipeline.
+    const bool spec = n && !nrt && !rdeps && s->kd_keys.p && s->vgap.p && s->kd_k2v.p;
+    accord::SpecCheck sc{};
+    if (spec) {
+        // the kernels address every output array with 32-bit byte offsets: totals past 2^30 never fit
+        const uint64_t lim = (1ull << 30) - 1;
+        sc.abort = &dev->spec_abort;
+        sc.status = &dev->status;
+        sc.cap[0] = std::min<uint64_t>(s->kd_keys.cap / 4, lim);
+        sc.cap[1] = std::min<uint64_t>(s->vgap.cap / 4 - 1, lim);
+        sc.cap[2] = std::min<uint64_t>(s->kd_k2v.cap / 4, lim);
+        if (general) {
+            HIPCHECK(s, s->rg_hist2.ensure(((size_t)PH + 1) * 4));
+            sc.xtot = &dev->totals[9];
+            sc.cap_x = s->rg_hist2.cap / 4 - PH;
+        }
+    }
     {   // KeyDeps offsets (and RangeDeps offsets) in one launch each
         const uint32_t *in[3] = {rp.cnt_keys, kp.cnt_vub, rp.cnt_k2v};
         uint32_t *out[3] = {s->kd_key_off.as<uint32_t>(), s->vub_off.as<uint32_t>(), s->kd_k2v_off.as<uint32_t>()};
         unsigned long long *tot[3] = {&dev->totals[0], &dev->totals[1], &dev->totals[2]};
-        accord::exclusive_scan_multi(3, in, out, tot, n, s->scan_tmp.p, st);
+        accord::exclusive_scan_multi(3, in, out, tot, n, s->scan_tmp.p, st, spec ? &sc : nullptr);
     }
     if (rdeps) {
         const uint32_t *in[3] = {rp.cnt_rngs, rp.cnt_vals, rp.cnt_r2v};
@@ -552,23 +588,7 @@ int32_t accord_deps_compute(accord_store *s)
     kp.kd_key_off = s->kd_key_off.as<uint32_t>(); kp.vub_off = s->vub_off.as<uint32_t>();
     kp.kd_k2v_off = s->kd_k2v_off.as<uint32_t>();
     accord::launch_keydeps_recs(kp, s->fk_recs.p, st);
-    // Speculative fill (key-only batches): the output arrays -- and a registered store's extended
-    // history -- keep the capacity earlier batches gave them, and the fill is queued behind the sizes
-    // without the host reading them first; a device check (launch_spec_check) aborts it when a total
-    // would not fit or the batch failed validation, and only then does the host grow the arrays and
-    // fill again.  A stream of like-sized batches never waits on the host mid-pipeline.
-    // ACCORD_SPEC_FILL=0: off.
-    static const bool spec_env = [] { const char *e = getenv("ACCORD_SPEC_FILL"); return !(e && e[0] == '0'); }();
-    const bool spec = spec_env && n && !nrt && !rdeps && s->kd_keys.p && s->vgap.p && s->kd_k2v.p;
-    if (spec) {
-        uint64_t cap_x = 0;
-        if (general) {
-            HIPCHECK(s, s->rg_hist2.ensure(((size_t)PH + 1) * 4));
-            cap_x = s->rg_hist2.cap / 4 - PH;
-        }
-        accord::launch_spec_check(&dev->totals[0], &dev->status, s->kd_keys.cap / 4, s->vgap.cap / 4 - 1,
-                                  s->kd_k2v.cap / 4, general ? &dev->totals[9] : nullptr, cap_x, &dev->spec_abort, st);
-    } else {
+    if (!spec) {
         HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
         HIPCHECK(s, hipStreamSynchronize(st));
     }
@@ -688,6 +708,11 @@ int32_t accord_deps_compute(accord_store *s)
         int32_t rc = accord_impl::redundant_count(s);
         if (rc) return rc;
     }
+    const bool join = s->resident && accord_impl::registered_mode(s);
+    if (join) {         // the batch joins the store's TxnId / status tables unless the compute failed
+        int32_t rc = accord_impl::status_join_queue(s, &dev->status);
+        if (rc) return rc;
+    }
     HIPCHECK(s, hipMemcpyAsync(s->pinned, dev, sizeof(HostTotals), hipMemcpyDeviceToHost, st));
     if (s->events)
         HIPCHECK(s, hipMemcpyAsync(&s->pinned->scan, accord::scan_counters(s->scan_tmp.p), sizeof(accord::ScanCounters),
@@ -723,10 +748,7 @@ int32_t accord_deps_compute(accord_store *s)
         s->tot_vals = s->pinned->totals[1];
     }
     if (s->resident) {      // the batch is part of the store's stream now
-        if (accord_impl::registered_mode(s)) {
-            int32_t rc = accord_impl::status_join_batch(s);
-            if (rc) return rc;
-        }
+        if (join) accord_impl::status_join_commit(s);
         std::swap(s->cy_key, s->cy_key2);
         std::swap(s->cy_ent, s->cy_ent2);
         s->carry_n = (uint32_t)s->pinned->totals[8];

@@ -198,7 +198,9 @@ struct accord_store {
     size_t rdy_pv_pos = 0;                    // positions pv_at / pv_len cover
     DevBuf rdy_sum, rdy_out, rdy_kb, rdy_launch, rdy_part, rdy_kseg0, rdy_kseg1, rdy_dirty, rdy_dirty2, rdy_dlist, rdy_work, rdy_wcnt;
     uint32_t rdy_call = 0;                    // accord_ready_update calls (ids of the dirty marks)
-    const void *rdy_hdr_zero = nullptr;       // rdy_out whose header the last call left zeroed (rd_host_out_kernel)
+    bool rg_flag_zeroed = false;              // the compute's init launch zeroed rg_flag (status_general_count)
+    bool rb_status_zeroed = false;            // ... and the RedundantBefore status words (redundant_count)
+        const void *rdy_hdr_zero = nullptr;       // rdy_out whose header the last call left zeroed (rd_host_out_kernel)
     uint32_t rdy_seen = 0;                    // rg_epoch the last accord_ready_update saw
     uint64_t rdy_sum_version = ~0ull;         // carry version the key summaries belong to
     uint64_t rdy_kseg_version = ~0ull, carry_version = 0;   // the carry's segment bounds are cached per carry version
@@ -242,7 +244,8 @@ int32_t status_general_emit(accord_store *s, uint32_t PH, uint64_t X, const uint
 int32_t status_prune_flags(accord_store *s, uint32_t PH, uint32_t *keep_flag);
 int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start, const uint32_t *end,
                               const uint32_t *bound);
-int32_t status_join_batch(accord_store *s);
+int32_t status_join_queue(accord_store *s, const accord::DevStatus *guard);
+void status_join_commit(accord_store *s);
 int32_t status_range_keys(accord_store *s, const accord::RangeDepsParams &rp, bool fill);
 int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned long long *words,
                                unsigned long long *aoi);

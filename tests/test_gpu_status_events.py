@@ -44,6 +44,14 @@ def test_events_match_literal_oracle(gpu_device, n, k, ks, z, wf, parts, seed):
     run(s, ks, pts, seed)
 
 
+def test_events_uneven_batches(gpu_device):
+    # batches that grow and shrink: after the first, the compute fills speculatively into the arrays
+    # (and the general pass's history extension) an earlier batch sized -- a larger batch aborts it,
+    # grows them and fills again (store.cpp, SpecCheck); the deps stay the oracle's
+    s = generate_stream(6000, 4, 150, 0.99, 0.5, seed=31)
+    run(s, 150, [0, 60, 2500, 2560, 2700, 6000], 31)
+
+
 def test_events_with_accept_batches(gpu_device):
     s = generate_stream(3000, 4, 200, 0.99, 0.5, seed=5)
     acc = s.accept(frac=0.5, max_delay=30, seed=5)
