@@ -48,7 +48,7 @@ ST_ERASED = 8                # register(): SaveStatus Erased / Invalidated (rang
 EXPORTED_SYMBOLS = [
     "accord_store_create", "accord_store_destroy", "accord_last_error", "accord_store_stream",
     "accord_deps_batch", "accord_deps_release", "accord_batch_upload", "accord_deps_compute",
-    "accord_deps_device_view", "accord_deps_download", "accord_store_timing",
+    "accord_deps_device_view", "accord_deps_download", "accord_store_timing", "accord_store_set_profile",
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
     "accord_comm_init", "accord_comm_size", "accord_deps_exchange_merge", "accord_deps_exchange_local", "accord_shard_timing",
     "accord_ready_update", "accord_ready_set_mode",
@@ -189,6 +189,7 @@ def lib() -> C.CDLL:
         L.accord_deps_device_view.argtypes = [C.c_void_p, C.POINTER(_Deps)]
         L.accord_deps_download.argtypes = [C.c_void_p, C.POINTER(_Deps)]
         L.accord_store_timing.argtypes = [C.c_void_p, C.POINTER(_Timing)]
+        L.accord_store_set_profile.argtypes = [C.c_void_p, C.c_uint32]
         L.accord_workload_generate.argtypes = [C.POINTER(_WorkloadCfg), C.POINTER(_Batch)]
         L.accord_workload_free.argtypes = [C.POINTER(_Batch)]
         L.accord_workload_free.restype = None
@@ -930,6 +931,10 @@ class CommandStore:
         a, b, c = C.c_float(), C.c_float(), C.c_float()
         self._check(lib().accord_waiting_on_timing(self._h, C.byref(a), C.byref(b), C.byref(c)))
         return a.value, b.value, c.value
+
+    def set_profile(self, on: bool):
+        """Profiling events on / off from the next call on (include/accord_deps.h accord_store_set_profile)."""
+        self._check(lib().accord_store_set_profile(self._h, 1 if on else 0))
 
     def timing(self) -> Timing:
         t = _Timing()

@@ -99,6 +99,7 @@ int32_t accord_store_create(const accord_store_cfg *cfg, accord_store **out)
     s->resident = (cfg->flags & ACCORD_STORE_RESIDENT) != 0;
     if (s->events)
         for (auto &ev : s->ev) (void)hipEventCreate(&ev);
+    s->ev_created = s->events;
     const uint64_t span_need = (uint64_t)cfg->window + 2048;
     s->wpl = span_need <= 4096 ? 1 : span_need <= 8192 ? 2 : 4;
     *out = s;
@@ -134,7 +135,7 @@ int32_t accord_store_destroy(accord_store *s)
     for (DepSet &d : s->ds) d.release();
     s->rb_set.release();
     for (DevBuf &b : s->op_tmp) b.release();
-    if (s->events)
+    if (s->ev_created)
         for (auto &ev : s->ev) (void)hipEventDestroy(ev);
     if (s->pinned) (void)hipHostFree(s->pinned);
     if (s->reg_host) (void)hipHostFree(s->reg_host);
@@ -825,6 +826,18 @@ int32_t accord_store_reset(accord_store *s)
         HIPCHECK(s, hipMemsetAsync(s->mc_state.p, 0, s->mc_state.cap, s->stream));
         HIPCHECK(s, hipStreamSynchronize(s->stream));
     }
+    return ACCORD_OK;
+}
+
+int32_t accord_store_set_profile(accord_store *s, uint32_t on)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (on && !s->ev_created) {
+        HIPCHECK(s, hipSetDevice(s->cfg.device));
+        for (auto &ev : s->ev) HIPCHECK(s, hipEventCreate(&ev));
+        s->ev_created = true;
+    }
+    s->events = on != 0;
     return ACCORD_OK;
 }
 

@@ -225,6 +225,7 @@ struct accord_store {
     accord_impl::PinnedBlock *dl_arena = nullptr;   // page-locked host arena of accord_deps_download
     hipEvent_t ev[EV_COUNT_ALL] = {};
     bool events = false;
+    bool ev_created = false;                 // the HIP events exist (profiling switched on once)
     accord_timing timing{};
     accord::ScanCounters scan_seen{};   // scan counters at the end of the previous profiled compute
     uint32_t computes_since_zero = 0;   // computes since the scan state was last zeroed

@@ -274,6 +274,11 @@ int32_t accord_deps_compute(accord_store *store);          /* enqueue + run the 
 int32_t accord_deps_device_view(accord_store *store, accord_deps *dev);  /* device pointers */
 int32_t accord_deps_download(accord_store *store, accord_deps *out);     /* D2H copy, host-owned */
 int32_t accord_store_timing(accord_store *store, accord_timing *t);
+/* profiling events on (1) or off (0) from the next call on -- ACCORD_STORE_PROFILE at creation
+ * switches them on.  Operational, no reference counterpart: the bench times its steps without the
+ * events (their records cost host time and marker packets) and takes the stage split from a
+ * profiled pass.  Timings read after calls made without events are those of the last profiled one. */
+int32_t accord_store_set_profile(accord_store *store, uint32_t on);
 
 /* ---- union of per-store partials (K6; PreAccept.reduce, messages/PreAccept.java:140-156) ----
  * parts: G device views (accord_deps_device_view of stores on this GPU, or received buffers) of

@@ -126,3 +126,16 @@ def test_speculative_fill_grow_shrink_and_errors(gpu_device):
                 bad = generate_stream(200, 2, ks * 2, seed=3)      # keys outside the store
                 with pytest.raises(IllegalArgumentException):
                     st.calculate_deps_batch(bad)
+
+
+def test_profile_switch(gpu_device):
+    # accord_store_set_profile: a store created without events gains them, computes stay exact either way
+    s = generate_stream(3000, 4, 500, 0.99, 0.5, seed=41)
+    want = O.deps_fast(s, 64)
+    with CommandStore(device=0, key_lo=0, key_hi=500, window=64) as st:
+        assert st.calculate_deps_batch(s).first_difference(want) is None
+        st.set_profile(True)
+        assert st.calculate_deps_batch(s).first_difference(want) is None
+        assert st.timing().total_ms > 0
+        st.set_profile(False)
+        assert st.calculate_deps_batch(s).first_difference(want) is None
