@@ -76,14 +76,18 @@ __device__ __forceinline__ void st_status(uint64_t *p, uint64_t v)
 
 constexpr uint64_t OVF = 1ull << 32;
 
-template <int NA>
+// DIRECT (every array 16-byte aligned): a thread loads its 16 consecutive items with four 16-byte
+// loads and keeps them in registers -- no LDS staging of the tile (48 KB of LDS for three arrays
+// had held the kernel to a few blocks per CU)
+template <int NA, bool DIRECT>
 __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_t n, uint32_t tiles,
                                                              ScanHeader *__restrict__ hdr, uint64_t *__restrict__ status)
 {
     __shared__ uint32_t s_id, s_epoch;
     __shared__ uint64_t s_wsum[NA][SC_THREADS / 64];
     __shared__ uint64_t s_excl[NA];
-    __shared__ uint32_t tile[NA][SC_TILE];
+    __shared__ uint32_t tile[DIRECT ? 1 : NA][DIRECT ? 1 : SC_TILE];
+    uint32_t vals[DIRECT ? NA : 1][DIRECT ? SC_ITEMS : 1];
     const uint32_t tid = threadIdx.x, w = wave_id(), lane = lane_id();
     if (tid == 0) {
         const unsigned long long old = atomicAdd(&hdr->ctl, 1ull);
@@ -97,21 +101,43 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
 
     // load the tile (coalesced), then each thread owns 16 consecutive items
     uint64_t local[NA];
+    const uint32_t mine = base + tid * SC_ITEMS;       // DIRECT: this thread's first item
+    if constexpr (DIRECT) {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
+        for (int k = 0; k < NA; ++k) {
+            if (mine + SC_ITEMS <= n) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(a.in[k] + mine);
 #pragma unroll
-        for (int j = 0; j < SC_ITEMS; ++j) {
-            const uint32_t idx = base + j * SC_THREADS + tid;
-            tile[k][j * SC_THREADS + tid] = idx < n ? a.in[k][idx] : 0u;
+                for (int j = 0; j < SC_ITEMS / 4; ++j) {
+                    const uint4 v = q[j];
+                    vals[k][4 * j] = v.x; vals[k][4 * j + 1] = v.y; vals[k][4 * j + 2] = v.z; vals[k][4 * j + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < SC_ITEMS; ++j) vals[k][j] = mine + j < n ? a.in[k][mine + j] : 0u;
+            }
+            uint64_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < SC_ITEMS; ++j) acc += vals[k][j];
+            local[k] = acc;
         }
-    }
-    __syncthreads();
+    } else {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-        uint64_t acc = 0;
+        for (int k = 0; k < NA; ++k) {
 #pragma unroll
-        for (int j = 0; j < SC_ITEMS; ++j) acc += tile[k][tid * SC_ITEMS + j];
-        local[k] = acc;
+            for (int j = 0; j < SC_ITEMS; ++j) {
+                const uint32_t idx = base + j * SC_THREADS + tid;
+                tile[k][j * SC_THREADS + tid] = idx < n ? a.in[k][idx] : 0u;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NA; ++k) {
+            uint64_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < SC_ITEMS; ++j) acc += tile[k][tid * SC_ITEMS + j];
+            local[k] = acc;
+        }
     }
     // block scan of the per-thread sums
     uint64_t incl[NA];
@@ -223,23 +249,46 @@ __global__ __launch_bounds__(SC_THREADS) void sc_single_pass(ScanArgs a, uint32_
         }
     }
     __syncthreads();
+    if constexpr (DIRECT) {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-        uint64_t run = s_excl[k] + woff[k] + incl[k] - local[k];
+        for (int k = 0; k < NA; ++k) {
+            uint64_t run = s_excl[k] + woff[k] + incl[k] - local[k];
 #pragma unroll
-        for (int j = 0; j < SC_ITEMS; ++j) {
-            const uint32_t v = tile[k][tid * SC_ITEMS + j];
-            tile[k][tid * SC_ITEMS + j] = (uint32_t)run;
-            run += v;
+            for (int j = 0; j < SC_ITEMS; ++j) {
+                const uint32_t v = vals[k][j];
+                vals[k][j] = (uint32_t)run;
+                run += v;
+            }
+            if (mine + SC_ITEMS <= n) {
+                uint4 *q = reinterpret_cast<uint4 *>(a.out[k] + mine);
+#pragma unroll
+                for (int j = 0; j < SC_ITEMS / 4; ++j)
+                    q[j] = make_uint4(vals[k][4 * j], vals[k][4 * j + 1], vals[k][4 * j + 2], vals[k][4 * j + 3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < SC_ITEMS; ++j)
+                    if (mine + j < n) a.out[k][mine + j] = vals[k][j];
+            }
         }
-    }
-    __syncthreads();
+    } else {
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
+        for (int k = 0; k < NA; ++k) {
+            uint64_t run = s_excl[k] + woff[k] + incl[k] - local[k];
 #pragma unroll
-        for (int j = 0; j < SC_ITEMS; ++j) {
-            const uint32_t idx = base + j * SC_THREADS + tid;
-            if (idx < n) a.out[k][idx] = tile[k][j * SC_THREADS + tid];
+            for (int j = 0; j < SC_ITEMS; ++j) {
+                const uint32_t v = tile[k][tid * SC_ITEMS + j];
+                tile[k][tid * SC_ITEMS + j] = (uint32_t)run;
+                run += v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NA; ++k) {
+#pragma unroll
+            for (int j = 0; j < SC_ITEMS; ++j) {
+                const uint32_t idx = base + j * SC_THREADS + tid;
+                if (idx < n) a.out[k][idx] = tile[k][j * SC_THREADS + tid];
+            }
         }
     }
     if (b == tiles - 1 && tid == 0) {
@@ -398,12 +447,21 @@ void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *ou
     }
     ScanHeader *hdr = (ScanHeader *)temp;
     uint64_t *status = (uint64_t *)((char *)temp + sizeof(ScanHeader));
+    bool direct = true;
+    for (int k = 0; k < na; ++k)
+        direct = direct && ((uintptr_t)in[k] & 15u) == 0 && ((uintptr_t)out[k] & 15u) == 0;
+#define SC_LAUNCH(NA_)                                                                                              \
+    do {                                                                                                            \
+        if (direct) hipLaunchKernelGGL((sc_single_pass<NA_, true>), dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); \
+        else hipLaunchKernelGGL((sc_single_pass<NA_, false>), dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); \
+    } while (0)
     switch (na) {
-    case 1: hipLaunchKernelGGL(sc_single_pass<1>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
-    case 2: hipLaunchKernelGGL(sc_single_pass<2>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
-    case 3: hipLaunchKernelGGL(sc_single_pass<3>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
-    default: hipLaunchKernelGGL(sc_single_pass<4>, dim3(tiles), dim3(SC_THREADS), 0, s, a, n, tiles, hdr, status); break;
+    case 1: SC_LAUNCH(1); break;
+    case 2: SC_LAUNCH(2); break;
+    case 3: SC_LAUNCH(3); break;
+    default: SC_LAUNCH(4); break;
     }
+#undef SC_LAUNCH
 }
 
 void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint32_t n, unsigned long long *total_dev, void *temp,
