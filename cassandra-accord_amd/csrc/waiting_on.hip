@@ -15,7 +15,7 @@
 // of the slice (their slices nest), so max level over the slice = max over {the last Write lw of
 // the slice} and, when i is a Write, the Reads after lw.  Only those are kept as predecessors.
 // The levels themselves come from a chunked max-plus closure of that DAG (see lv_closure_kernel /
-// lv_resolve_kernel below).
+// lv_staged_kernel below).
 #include "device_common.h"
 #include "kernels.h"
 #include "../../include/accord_deps.h"
@@ -149,11 +149,12 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
 //     predecessors.  With v = level + 1 and basev(j) = 1 + max v over j's far predecessors (1
 //     without), v(i) = max over in-chunk ancestors j of i (and j = i) of basev(j) + dist(i, j).
 //     Columns of txns without far predecessors (basev = 1) fold into one constant per row.
-//   pass 2 (one workgroup, LV_WAVES waves, wave w owns chunks w, w + LV_WAVES, ...): per chunk
-//     gather the far predecessors' v (LDS ring of the last LV_RING txns, older ones from HBM,
-//     prefetched a round ahead), then one max-plus matrix-vector product (lane = row).  Columns
-//     whose predecessors lie in chunks <= x-2 are done while chunk x-1 is still being resolved by
-//     another wave; only the "late" columns (a predecessor in chunk x-1) sit on the critical path.
+//   pass 2 (one workgroup, lv_staged_kernel): helper waves stage each chunk -- its far
+//     predecessors' v (LDS ring of the last LV_RING txns, older ones from HBM) folded into the
+//     columns whose predecessors lie in chunks <= x-3 -- and one resolver wave, alone on its SIMD,
+//     walks the chain doing only the "late" columns (a predecessor in chunk x-1 or x-2) with a
+//     max-plus matrix-vector product (lane = row).  (The earlier all-waves resolver, every wave
+//     owning every 8th chunk, measured 48.3 against 44.7 ms and is gone, round 5.)
 constexpr uint32_t LC = 64;                 // txns per chunk
 constexpr int LV_REFS = 8;                  // far predecessors kept per entry column
 constexpr uint32_t LV_RING = 16384;         // pass-2 LDS ring of v (64 KiB)
@@ -163,8 +164,6 @@ constexpr uint32_t REF_NONE = 0xFFFFFFFFu;
 constexpr uint32_t RC_CST = 0, RC_BQ = 64, RC_REF = RC_BQ + 16 * 64, RC_NODE = RC_REF + LV_REFS * 64,
                    RC_HDR = RC_NODE + 64, RC_WORDS = RC_HDR + 64;
 static_assert(LV_RING % LC == 0, "ring holds whole chunks");
-constexpr int LV_WAVES_MAX = 16;
-static_assert(LV_RING >= 2 * LC * LV_WAVES_MAX, "old predecessors must be final one round ahead");
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 {
@@ -176,8 +175,8 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
 // 1 + b(i,j); bq = b(i, slot) bytes in slot order, b = dist + 1 (0 = j does not reach i).  Slots:
 // late entries, then early entries, then non-entries.  ref[s][slot] = the slot's far predecessors.
 // hdr = nl | ne << 8 | slow << 16 (slow: some entry has more than LV_REFS far predecessors).
-// late_chunks: an entry is late when a predecessor lies in the previous late_chunks chunks (1 for
-// lv_resolve_kernel, 2 for the staged resolver lv_staged_kernel).
+// late_chunks: an entry is late when a predecessor lies in the previous late_chunks chunks (2: the
+// staged resolver lv_staged_kernel).
 __global__ __launch_bounds__(256) void lv_closure_kernel(uint32_t n, uint32_t nchunks,
                                                          const uint32_t *__restrict__ pred_off,
                                                          const uint32_t *__restrict__ preds,
@@ -279,25 +278,6 @@ __device__ __forceinline__ void lv_load(const uint32_t *__restrict__ rec, uint32
     o.hdr = r[RC_HDR + lane];
 }
 
-// Spin on the LDS count of resolved chunks; false once any wave gave up (defensive bound).
-__device__ __forceinline__ bool lv_wait(uint32_t *done, uint32_t *abort_flag, uint32_t target)
-{
-    uint32_t spins = 0;
-    while (__builtin_amdgcn_readfirstlane(
-               __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
-        if ((++spins & 255u) == 0) {            // rarely: another wave gave up, or the bound is hit
-            if (__builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-                return false;
-            if (spins > (1u << 26)) {
-                __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return false;
-            }
-        }
-    }
-    return true;
-}
-
 // Column slot m of row `lane` as a signed addend: b(row, m) (= dist + 1) when m reaches the row,
 // INT_MIN otherwise, so basev(m) + d never wins a signed max (basev < 2^31).
 __device__ __forceinline__ void lv_expand(const uint32_t (&bq)[16], int32_t (&d)[64])
@@ -331,151 +311,6 @@ __device__ __forceinline__ int32_t lv_matvec(int32_t acc, const int32_t (&d)[64]
     return max(acc, acc2);
 }
 
-struct LvShared {
-    uint32_t ring[LV_RING];
-    uint32_t done, abort_flag, maxlv;
-};
-
-// One chunk of pass 2.  The far predecessors older than the ring are final a whole round before
-// the chunk is processed, so plain loads are safe: every line of level[] read here holds only
-// entries written rounds ago by this workgroup (its own CU), never a line that is still changing.
-// Returns false on abort.
-template <int LV_WAVES>
-__device__ __forceinline__ bool lv_chunk(LvShared &S, uint32_t n, uint32_t x, const LvRec &cur, LvRec &nxt,
-                                         const uint32_t *__restrict__ rec, uint32_t nchunks,
-                                         const uint32_t *__restrict__ pred_off, const uint32_t *__restrict__ preds,
-                                         uint32_t *level, uint32_t lane, uint32_t &mymax,
-                                         unsigned long long *dbg)
-{
-#define LV_STAMP(k) do { if (dbg && lane == 0) dbg[(size_t)x * 5 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
-    const uint32_t base = x * LC;
-    const uint32_t hdr = __builtin_amdgcn_readfirstlane(cur.hdr);
-    const uint32_t nl = hdr & 0xFFu, ne = (hdr >> 8) & 0xFFu;
-    const bool slow = (hdr >> 16) & 1u;
-    // issued unconditionally (index 0 when not an old predecessor) so the loads stay in flight
-    uint32_t oldv[LV_REFS];
-#pragma unroll
-    for (int s = 0; s < LV_REFS; ++s) {
-        const uint32_t f = cur.ref[s];
-        const bool old = !slow && f != REF_NONE && f + LV_RING < base;
-        oldv[s] = level[old ? f : 0u];
-    }
-    LV_STAMP(0);
-    int32_t d[64];
-    lv_expand(cur.bq, d);
-    int32_t acc = (int32_t)cur.cst;
-    uint32_t bv = 1, late_hi = nl;
-    if (!slow) {
-        // early columns: every predecessor in chunks <= x-2
-        if (!lv_wait(&S.done, &S.abort_flag, x ? x - 1 : 0)) return false;
-        LV_STAMP(1);
-        uint32_t rv[LV_REFS];
-#pragma unroll
-        for (int s = 0; s < LV_REFS; ++s) {              // LDS reads issued together
-            const uint32_t f = cur.ref[s];
-            rv[s] = S.ring[(f != REF_NONE && f + LC < base) ? f % LV_RING : 0u];
-        }
-        uint32_t e = 0;
-#pragma unroll
-        for (int s = 0; s < LV_REFS; ++s) {
-            const uint32_t f = cur.ref[s];
-            if (f == REF_NONE) continue;
-            e = max(e, f + LV_RING < base ? oldv[s] + 1u : f + LC < base ? rv[s] : 0u);
-        }
-        bv = e + 1u;
-        acc = lv_matvec(acc, d, bv, nl, ne);
-        LV_STAMP(2);
-        // late columns: a predecessor in chunk x-1 (the critical path: run at raised priority)
-        __builtin_amdgcn_s_setprio(2);
-        if (!lv_wait(&S.done, &S.abort_flag, x)) return false;
-        LV_STAMP(3);
-#pragma unroll
-        for (int s = 0; s < LV_REFS; ++s) {
-            const uint32_t f = cur.ref[s];
-            rv[s] = S.ring[(f != REF_NONE && f + LC >= base) ? f % LV_RING : 0u];
-        }
-        uint32_t l = 0;
-#pragma unroll
-        for (int s = 0; s < LV_REFS; ++s) {
-            const uint32_t f = cur.ref[s];
-            if (f != REF_NONE && f + LC >= base) l = max(l, rv[s]);
-        }
-        bv = max(bv, l + 1u);
-    } else {
-        // some entry has more predecessors than the record holds: walk its full list
-        if (!lv_wait(&S.done, &S.abort_flag, x)) return false;
-        __builtin_amdgcn_s_setprio(2);
-        uint32_t e = 0;
-        const uint32_t t = base + cur.node;
-        if (lane < ne && t < n) {
-            for (uint32_t q = pred_off[t], q1 = pred_off[t + 1]; q < q1; ++q) {
-                const uint32_t f = preds[q];
-                if (f >= base) continue;
-                e = max(e, f + LV_RING >= base ? S.ring[f % LV_RING] : level[f] + 1u);
-            }
-        }
-        bv = e + 1u;
-        late_hi = ne;
-    }
-    acc = lv_matvec(acc, d, bv, 0, late_hi);
-    const uint32_t t = base + lane;
-    if (t < n) {
-        const uint32_t v = (uint32_t)acc - 1u;
-        S.ring[t % LV_RING] = v;
-        level[t] = v - 1u;
-        mymax = max(mymax, v - 1u);
-    }
-    wave_lds_sync();
-    if (lane == 0) __hip_atomic_store(&S.done, x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    LV_STAMP(4);
-#undef LV_STAMP
-    __builtin_amdgcn_s_setprio(0);
-    // the wave's next record: lands while the wave waits for its next chunk's inputs
-    lv_load(rec, x + LV_WAVES, nchunks, lane, nxt);
-    return true;
-}
-
-// Pass 2.  info[0] = 1 + chunks resolved when a wave gave up (must stay 0), info[1] = max level.
-// Two record register sets alternate (no loop-carried copy, so the next record's loads stay in
-// flight across the whole chunk).
-template <int LV_WAVES>
-__global__ __launch_bounds__(LV_WAVES * 64) void lv_resolve_kernel(uint32_t n, uint32_t nchunks,
-                                                                  const uint32_t *__restrict__ rec,
-                                                                  const uint32_t *__restrict__ pred_off,
-                                                                  const uint32_t *__restrict__ preds,
-                                                                  uint32_t *level, uint32_t *__restrict__ info,
-                                                                  unsigned long long *dbg)
-{
-    __shared__ LvShared S;
-    const uint32_t w = wave_id(), lane = lane_id();
-    if (threadIdx.x == 0) { S.done = 0; S.abort_flag = 0; S.maxlv = 0; }
-    __syncthreads();
-    uint32_t mymax = 0;
-    LvRec ra, rb;
-    lv_load(rec, w, nchunks, lane, ra);
-    for (uint32_t x = w; x < nchunks; x += 2 * LV_WAVES) {
-        if (!lv_chunk<LV_WAVES>(S, n, x, ra, rb, rec, nchunks, pred_off, preds, level, lane, mymax, dbg)) break;
-        if (x + LV_WAVES >= nchunks) break;
-        if (!lv_chunk<LV_WAVES>(S, n, x + LV_WAVES, rb, ra, rec, nchunks, pred_off, preds, level, lane, mymax, dbg)) break;
-    }
-    atomicMax(&S.maxlv, mymax);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (S.abort_flag) info[0] = 1 + S.done;
-        info[1] = S.maxlv;
-    }
-}
-
-// ---- staged resolve: one resolver wave walks the chain, helper waves stage each chunk ----
-// Late entry columns (lv_closure_kernel with late_chunks = 2) have a predecessor in chunk x-1 or
-// x-2; everything else of chunk x depends on chunks <= x-3 only.  The helpers (waves 1..7, chunk x
-// to wave 1 + x % 7) compute that part while the resolver is still two chunks behind -- the early
-// bases and the product over the early columns (acc_e per row), the late columns' bases from their
-// older predecessors (bv_e), their predecessors in x-1 / x-2 as ring indices, and the late
-// columns' closure expanded to ints -- and hand it over in one of LS_K LDS slots.  The resolver's
-// step per chunk is then only: the late predecessors' values from the ring (8 LDS reads; its own
-// earlier writes, in order on its LDS queue), the late bases, and the product over the late
-// columns; no wave-to-wave hand-off sits on the chain unless a helper falls behind.
 constexpr uint32_t LS_K = 4;                  // staged chunks in flight
 constexpr int LS_LREF = 8;                    // late predecessors per column in the slot
 constexpr int LS_HELPERS = 7;
@@ -710,7 +545,7 @@ __device__ __forceinline__ bool ls_resolve(LsShared &S, uint32_t n, uint32_t nch
     return true;
 }
 
-// DBG (ACCORD_LV_STATS=1): s_memtime sums -- dbg[0] resolver cycles waiting for a slot, [1] its
+// DBG (a development instantiation, not launched by the product): s_memtime sums -- dbg[0] resolver cycles waiting for a slot, [1] its
 // cycles from slot to published chunk, [2] chunks it waited > 100 cycles for, [3] helpers' cycles
 // from "chunks <= x-3 final" to the slot's flag, [4] chunks staged
 template <bool DBG>
@@ -826,47 +661,12 @@ void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, 
     if (n == 0) return;
     const uint32_t nchunks = (n + LC - 1) / LC;
     uint32_t *rec = (uint32_t *)temp;
-    // ACCORD_LV_STAGED=0: the pipelined all-waves resolver instead of the staged one (A/B)
-    const char *st = getenv("ACCORD_LV_STAGED");
-    const bool staged = !(st && st[0] == '0');
     hipLaunchKernelGGL(lv_closure_kernel, dim3((nchunks + 3) / 4), dim3(256), 0, s, n, nchunks, pred_off, preds, rec,
-                       info, staged ? 2u : 1u);
-    // ACCORD_LV_DEBUG=<file>: per-chunk s_memtime stamps of the resolve pass (development aid)
-    const char *dbg_path = getenv("ACCORD_LV_DEBUG");
-    unsigned long long *dbg = nullptr;
-    if (dbg_path && hipMalloc(&dbg, (size_t)nchunks * 5 * 8) != hipSuccess) dbg = nullptr;
-    // 8 waves (2 per SIMD): 4 and 12 measured within noise / slower (profiles/r01_v13)
-    const char *sts = getenv("ACCORD_LV_STATS");
-    unsigned long long *sdbg = nullptr;
-    if (staged && sts && sts[0] == '1' && hipMalloc(&sdbg, 64) == hipSuccess) (void)hipMemsetAsync(sdbg, 0, 64, s);
-    auto kern = sdbg ? lv_staged_kernel<true> : lv_staged_kernel<false>;
+                       info, 2u);
     // the resolver alone on its SIMD (wave 4, which round-robin placement puts there, idles): 48.3 ->
-    // 44.7 ms on config 5 (profiles/r04_b/levels_staged_ab.txt); ACCORD_LV_SOLO=0 puts a helper there
-    const char *so = getenv("ACCORD_LV_SOLO");
-    const uint32_t solo = so && so[0] == '0' ? 0u : 1u;
-    if (staged)
-        hipLaunchKernelGGL(kern, dim3(1), dim3((LS_HELPERS + 1) * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
-                           info, sdbg, solo);
-    else
-        hipLaunchKernelGGL(lv_resolve_kernel<8>, dim3(1), dim3(8 * 64), 0, s, n, nchunks, rec, pred_off, preds, level,
-                           info, dbg);
-    if (sdbg) {
-        unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (hipMemcpyAsync(h, sdbg, 64, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess)
-            fprintf(stderr, "lv_staged: chunks %u resolver wait %.1f compute %.1f cycles/chunk, waited on %llu chunks; "
-                    "helper stage-after-final %.1f cycles/chunk (%llu); resolver slot+gather %.1f\n", nchunks,
-                    (double)h[0] / nchunks, (double)h[1] / nchunks, h[2], h[4] ? (double)h[3] / h[4] : 0.0, h[4],
-                    (double)h[5] / nchunks);
-        (void)hipFree(sdbg);
-    }
-    if (dbg) {
-        std::vector<unsigned long long> h((size_t)nchunks * 5);
-        if (hipMemcpyAsync(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
-            hipStreamSynchronize(s) == hipSuccess) {
-            if (FILE *fp = fopen(dbg_path, "wb")) { fwrite(h.data(), 8, h.size(), fp); fclose(fp); }
-        }
-        (void)hipFree(dbg);
-    }
+    // 44.7 ms on config 5 (profiles/r04_b/levels_staged_ab.txt)
+    hipLaunchKernelGGL(lv_staged_kernel<false>, dim3(1), dim3((LS_HELPERS + 1) * 64), 0, s, n, nchunks, rec, pred_off,
+                       preds, level, info, nullptr, 1u);
 }
 
 } // namespace accord
