@@ -417,12 +417,20 @@ __device__ __forceinline__ uint32_t rk_pw_before(const RangeDepsParams &p, uint3
     return x ? max(p.pw_local[x - 1], p.pw_carry[(x - 1) / p.pw_tile]) : 0u;
 }
 
+// Hot keys (segments of more than RK_CP_COLD entries): a thread per history position writes the
+// cells of the blocks it is the first entry at or after.  Cold keys: a lane per key walks the
+// blocks and its few entries together (rk_checkpoint_cold_kernel), so each row's cells are written
+// coalesced, where a thread per position had written a cold key's column of ~ncp cells as
+// scattered 8-byte stores (config 3 rk_checkpoints stage 0.325 -> 0.258 ms with 96; 32 / 256
+// measured 0.284 / 0.272, a walk prefetching the next entry 0.270; profiles/r05_cp/checkpoint_ab.txt).
+constexpr uint32_t RK_CP_COLD = 96;
 __global__ __launch_bounds__(256) void rk_checkpoint_kernel(uint32_t P, const uint32_t *__restrict__ sorted_key,
                                                             RangeDepsParams p)
 {
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < P; x += gridDim.x * blockDim.x) {
         const uint32_t k = sorted_key[x];
         const uint32_t a = p.seg_start[k], c = p.seg_end[k];
+        if (c - a <= RK_CP_COLD) continue;              // rk_checkpoint_cold_kernel's
         const uint32_t t = p.hist[x] & ENT_TXN_MASK;
         // absolute txn blocks [cp_base, cp_base + ncp) live in the table
         const uint32_t b_end = p.cp_base + p.ncp;
@@ -438,6 +446,30 @@ __global__ __launch_bounds__(256) void rk_checkpoint_kernel(uint32_t P, const ui
             const uint2 v = rk_cp_make(c, RK_CP_YMAX, rk_pw_before(p, c));
             for (uint32_t b = max(p.cp_base, (t >> RK_CP_SHIFT) + 1u); b < b_end; ++b)
                 p.cp[(size_t)(b - p.cp_base) * p.nkeys + k] = v;
+        }
+    }
+}
+
+// a lane per key with 0 < entries <= RK_CP_COLD: every block of the table, the key's first entry with
+// txn at or after the block's start (or the segment end), as rk_checkpoint_kernel would write it
+__global__ __launch_bounds__(256) void rk_checkpoint_cold_kernel(RangeDepsParams p)
+{
+    const uint32_t b_end = p.cp_base + p.ncp;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < p.nkeys; k += gridDim.x * blockDim.x) {
+        const uint32_t a = p.seg_start[k], c = p.seg_end[k];
+        if (a >= c || c - a > RK_CP_COLD) continue;
+        uint32_t q = a, tq = p.hist[a] & ENT_TXN_MASK;
+        uint32_t pwq = rk_pw_before(p, a);
+        for (uint32_t b = p.cp_base; b < b_end; ++b) {
+            bool moved = false;
+            while (q < c && tq < (b << RK_CP_SHIFT)) {
+                ++q;
+                tq = q < c ? p.hist[q] & ENT_TXN_MASK : 0xFFFFFFFFu;
+                moved = true;
+            }
+            if (moved) pwq = rk_pw_before(p, q);
+            const uint32_t yo = q < c && (tq >> RK_CP_SHIFT) == b ? (tq & RK_CP_YMAX) : RK_CP_YMAX;
+            p.cp[(size_t)(b - p.cp_base) * p.nkeys + k] = rk_cp_make(q, yo, pwq);
         }
     }
 }
@@ -1070,6 +1102,7 @@ void launch_rangekeys_checkpoints(uint32_t PH, const uint32_t *sorted_key, const
     uint32_t blocks = (PH + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(rk_checkpoint_kernel, dim3(blocks), dim3(256), 0, s, PH, sorted_key, p);
+    hipLaunchKernelGGL(rk_checkpoint_cold_kernel, dim3(std::min<uint32_t>((p.nkeys + 255) / 256, 8192u)), dim3(256), 0, s, p);
 }
 
 namespace {
