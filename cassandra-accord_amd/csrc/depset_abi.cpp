@@ -458,35 +458,51 @@ int32_t accord_redundant_before_set_ex(accord_store *s, uint32_t m, const uint32
             return fail(s, ACCORD_ERR_RANGES, "RedundantBefore entries %u, %u not ascending and disjoint", i - 1, i);
     }
     HIPCHECK(s, hipSetDevice(s->cfg.device));
-    if (m) {
-        HIPCHECK(s, s->rb_start.ensure((size_t)m * 4)); HIPCHECK(s, s->rb_end.ensure((size_t)m * 4));
-        HIPCHECK(s, s->rb_bound.ensure((size_t)m * 4));
-        HIPCHECK(s, s->rb_sep.ensure((size_t)m * 8)); HIPCHECK(s, s->rb_eep.ensure((size_t)m * 8));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_start.p, start, (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_end.p, end, (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_bound.p, bound, (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_sep.p, start_epoch, (size_t)m * 8, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_eep.p, end_epoch, (size_t)m * 8, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipStreamSynchronize(s->stream));
-    }
     // the rest of each entry (removeRedundantDependencies); absent arrays: NONE, NONE, not stale
     bool ext = false;
     for (uint32_t i = 0; i < m && !ext; ++i)
         ext = (local && local[i] != ACCORD_NO_TXN) || (boot && boot[i] != ACCORD_NO_TXN) || (stale && stale[i]);
-    if (ext) {
-        std::vector<uint32_t> lo(m, ACCORD_NO_TXN), bo(m, ACCORD_NO_TXN);
-        std::vector<uint8_t> st(m, 0);
-        for (uint32_t i = 0; i < m; ++i) {
-            if (local) lo[i] = local[i];
-            if (boot) bo[i] = boot[i];
-            if (stale) st[i] = stale[i] ? 1 : 0;
+    if (m) {   // every array staged in page-locked memory, one host-to-device copy, one scatter launch
+        const size_t w4 = ((size_t)m + 3) / 4;              // stale bytes, in words
+        const size_t words = (size_t)m * (3 + 2 + 2) + (ext ? (size_t)m * 2 + w4 : 0);
+        if (s->rb_host_cap < words * 4) {
+            if (s->rb_host) (void)hipHostFree(s->rb_host);
+            s->rb_host = nullptr; s->rb_host_cap = 0;
+            HIPCHECK(s, hipHostMalloc(&s->rb_host, words * 8, hipHostMallocDefault));
+            s->rb_host_cap = words * 8;
         }
-        HIPCHECK(s, s->rb_local.ensure((size_t)m * 4)); HIPCHECK(s, s->rb_boot.ensure((size_t)m * 4));
-        HIPCHECK(s, s->rb_stale.ensure((size_t)m + 8));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_local.p, lo.data(), (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_boot.p, bo.data(), (size_t)m * 4, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipMemcpyAsync(s->rb_stale.p, st.data(), (size_t)m, hipMemcpyHostToDevice, s->stream));
-        HIPCHECK(s, hipStreamSynchronize(s->stream));
+        HIPCHECK(s, s->rb_pack.ensure(words * 4));
+        HIPCHECK(s, s->rb_start.ensure((size_t)m * 4)); HIPCHECK(s, s->rb_end.ensure((size_t)m * 4));
+        HIPCHECK(s, s->rb_bound.ensure((size_t)m * 4));
+        HIPCHECK(s, s->rb_sep.ensure((size_t)m * 8)); HIPCHECK(s, s->rb_eep.ensure((size_t)m * 8));
+        uint32_t *h = (uint32_t *)s->rb_host;
+        const uint32_t *dp = s->rb_pack.as<uint32_t>();
+        accord::CopyList cl;
+        size_t o = 0;
+        auto put = [&](const void *src, size_t nw, void *dst) {
+            std::memcpy(h + o, src, nw * 4);
+            cl.add(dp + o, dst, nw * 4);
+            o += nw;
+        };
+        put(start, m, s->rb_start.p); put(end, m, s->rb_end.p); put(bound, m, s->rb_bound.p);
+        put(start_epoch, (size_t)m * 2, s->rb_sep.p); put(end_epoch, (size_t)m * 2, s->rb_eep.p);
+        if (ext) {
+            HIPCHECK(s, s->rb_local.ensure((size_t)m * 4)); HIPCHECK(s, s->rb_boot.ensure((size_t)m * 4));
+            HIPCHECK(s, s->rb_stale.ensure(w4 * 4 + 8));
+            uint32_t *lo = h + o;
+            for (uint32_t i = 0; i < m; ++i) lo[i] = local ? local[i] : ACCORD_NO_TXN;
+            cl.add(dp + o, s->rb_local.p, (size_t)m * 4); o += m;
+            uint32_t *bo = h + o;
+            for (uint32_t i = 0; i < m; ++i) bo[i] = boot ? boot[i] : ACCORD_NO_TXN;
+            cl.add(dp + o, s->rb_boot.p, (size_t)m * 4); o += m;
+            uint8_t *st = (uint8_t *)(h + o);
+            std::memset(st, 0, w4 * 4);
+            for (uint32_t i = 0; i < m; ++i) st[i] = stale && stale[i] ? 1 : 0;
+            cl.add(dp + o, s->rb_stale.p, w4 * 4); o += w4;
+        }
+        HIPCHECK(s, hipMemcpyAsync(s->rb_pack.p, s->rb_host, o * 4, hipMemcpyHostToDevice, s->stream));
+        accord::launch_copy_words(cl, s->stream);
+        HIPCHECK(s, hipStreamSynchronize(s->stream));     // the staging is reused by the next call
     }
     if (ext != s->rb_ext || ext) s->rdy_force_full = true;   // readiness re-evaluates everything
     s->rb_ext = ext;

@@ -436,13 +436,27 @@ __global__ __launch_bounds__(256) void prune_mark_kernel(uint32_t P, const uint3
 
 // CommandsForKey.withRedundantBefore (:1654-1684) on the carried history: entries below their key's
 // shardRedundantBefore leave
+// each carried entry's key bound from the store's RedundantBefore entries themselves (m ascending,
+// disjoint (start, end] ranges; a binary search per entry instead of a per-key table uploaded from
+// the host -- 400 KB per call at 100 k keys)
 __global__ __launch_bounds__(256) void truncate_mark_kernel(uint32_t C, const uint32_t *__restrict__ ckey,
-                                                            const uint32_t *__restrict__ cent,
-                                                            const uint32_t *__restrict__ key_bound,
+                                                            const uint32_t *__restrict__ cent, uint32_t key_lo,
+                                                            uint32_t m, const uint32_t *__restrict__ rs,
+                                                            const uint32_t *__restrict__ re,
+                                                            const uint32_t *__restrict__ rbound,
                                                             uint32_t *__restrict__ keep_flag)
 {
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x)
-        keep_flag[c] = (cent[c] & ENT_TXN_MASK) >= key_bound[ckey[c]] ? 1u : 0u;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+        const uint32_t k = ckey[c] + key_lo;
+        uint32_t lo = 0, hi = m;                       // first entry with end >= k
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (re[mid] < k) lo = mid + 1; else hi = mid;
+        }
+        uint32_t kb = 0;
+        if (lo < m && rs[lo] < k && rbound[lo] != ACCORD_NO_TXN) kb = rbound[lo];
+        keep_flag[c] = (cent[c] & ENT_TXN_MASK) >= kb ? 1u : 0u;
+    }
 }
 
 // ---- registration ----
@@ -1073,24 +1087,24 @@ int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start
     for (uint32_t r = 0; r < nkeys; ++r) s->rdy_kb_host[r] = std::max(s->rdy_kb_host[r], kb[r]);
     s->rdy_kb_dirty = true;
     hipStream_t st = s->stream;
-    HIPCHECK(s, s->rg_kbound.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->carry_tmp.ensure(accord::carry_temp_bytes(C, nkeys)));
     HIPCHECK(s, s->cy_key2.ensure((size_t)C * 4 + 4));
     HIPCHECK(s, s->cy_ent2.ensure((size_t)C * 4 + 4));
     HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(C), st));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
-    HIPCHECK(s, hipMemcpyAsync(s->rg_kbound.p, kb.data(), (size_t)nkeys * 4, hipMemcpyHostToDevice, st));
     uint32_t *flag = accord::carry_flags(s->carry_tmp.p, nkeys);
+    // (the entries are on the device: accord_redundant_before_set_ex uploaded them first)
     hipLaunchKernelGGL(truncate_mark_kernel, dim3(grid_for(C)), dim3(256), 0, st, C, s->cy_key.as<uint32_t>(),
-                       s->cy_ent.as<uint32_t>(), s->rg_kbound.as<uint32_t>(), flag);
+                       s->cy_ent.as<uint32_t>(), key_lo, m, s->rb_start.as<uint32_t>(), s->rb_end.as<uint32_t>(),
+                       s->rb_bound.as<uint32_t>(), flag);
     HostTotals *dev = s->status_totals.as<HostTotals>();
     accord::launch_carry(C, nkeys, 0u, s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), nullptr, nullptr,
                          accord::HistoryViews{}, s->carry_tmp.p, s->scan_tmp.p, s->cy_key2.as<uint32_t>(),
                          s->cy_ent2.as<uint32_t>(), &dev->totals[8], true, st);
-    unsigned long long kept = 0;
-    HIPCHECK(s, hipMemcpyAsync(&kept, &dev->totals[8], 8, hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipMemcpyAsync(&s->pinned->totals[8], &dev->totals[8], 8, hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
+    const unsigned long long kept = s->pinned->totals[8];
     std::swap(s->cy_key, s->cy_key2);
     std::swap(s->cy_ent, s->cy_ent2);
     s->carry_n = (uint32_t)kept;
@@ -1162,9 +1176,10 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     // the events in one host-to-device copy: packed into a pinned staging buffer (msb | lsb | exec
     // msb | exec lsb | node | exec node | status), the device copy in op_tmp[0]
     DevBuf *T = s->op_tmp;
+    // (+ the check's status words, staged as "no failure": no memset of their own)
     const size_t o_lsb = (size_t)n * 8, o_emsb = o_lsb + (size_t)n * 8, o_elsb = o_emsb + (size_t)n * 8,
                  o_node = o_elsb + (size_t)n * 8, o_enode = o_node + (size_t)n * 4, o_st = o_enode + (size_t)n * 4,
-                 bytes = (o_st + n + 15) & ~(size_t)15;
+                 o_err = (o_st + n + 15) & ~(size_t)15, bytes = o_err + ((sizeof(accord::DevStatus) + 15) & ~(size_t)15);
     if (s->reg_host_cap < bytes) {
         if (s->reg_host) (void)hipHostFree(s->reg_host);
         s->reg_host = nullptr; s->reg_host_cap = 0;
@@ -1176,6 +1191,7 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     std::memcpy(h + o_lsb, lsb, (size_t)n * 8);
     std::memcpy(h + o_node, node, (size_t)n * 4);
     std::memcpy(h + o_st, status, n);
+    std::memset(h + o_err, 0xFF, sizeof(accord::DevStatus));
     if (need_exec) {
         std::memcpy(h + o_emsb, exec_msb, (size_t)n * 8);
         std::memcpy(h + o_elsb, exec_lsb, (size_t)n * 8);
@@ -1184,8 +1200,6 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     HIPCHECK(s, T[0].ensure(bytes)); HIPCHECK(s, T[7].ensure((size_t)n * 4));
     HIPCHECK(s, s->status_totals.ensure(sizeof(HostTotals)));
     HIPCHECK(s, hipMemcpyAsync(T[0].p, h, bytes, hipMemcpyHostToDevice, st));
-    HostTotals *dev = s->status_totals.as<HostTotals>();
-    HIPCHECK(s, hipMemsetAsync(&dev->status, 0xFF, sizeof(dev->status), st));
     RegParams p{};
     p.n = n; p.tx_n = s->rg_tx_n;
     char *d = (char *)T[0].p;
@@ -1197,15 +1211,15 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     p.st = s->rg_status.as<uint8_t>();
     p.xmsb = s->rg_emsb.as<uint64_t>(); p.xlsb = s->rg_elsb.as<uint64_t>(); p.xnode = s->rg_enode.as<int32_t>();
     p.pos = T[7].as<uint32_t>();
-    p.err = &dev->status;
+    p.err = (accord::DevStatus *)(d + o_err);
     p.chg = s->rg_chg.as<uint32_t>();
     p.cchg = s->rg_cchg.as<uint32_t>();
     p.epoch = s->rg_epoch + 1;
     if (p.tx_n == 0) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: the store holds no txn yet");
     hipLaunchKernelGGL(reg_check_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
-    accord::DevStatus hs;
-    HIPCHECK(s, hipMemcpyAsync(&hs, &dev->status, sizeof(hs), hipMemcpyDeviceToHost, st));
+    HIPCHECK(s, hipMemcpyAsync(&s->pinned->reg_status, p.err, sizeof(accord::DevStatus), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
+    const accord::DevStatus hs = s->pinned->reg_status;
     if (hs.first != ~0ull) {
         const uint32_t r = (uint32_t)(hs.first >> 32);
         const int32_t code = -(int32_t)(uint32_t)hs.first;

@@ -139,6 +139,8 @@ int32_t accord_store_destroy(accord_store *s)
         for (auto &ev : s->ev) (void)hipEventDestroy(ev);
     if (s->pinned) (void)hipHostFree(s->pinned);
     if (s->reg_host) (void)hipHostFree(s->reg_host);
+    if (s->rb_host) (void)hipHostFree(s->rb_host);
+    s->rb_pack.release();
     if (s->up_host) (void)hipHostFree(s->up_host);
     (void)hipStreamDestroy(s->stream);
     delete s;

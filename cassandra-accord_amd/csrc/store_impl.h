@@ -53,6 +53,7 @@ struct HostTotals {
     accord::DevStatus rb_status;    // its capacity status, apart from the compute's
     accord::ScanCounters scan;      // the store's scan-state counters (profiled stores read them)
     uint32_t spec_abort, spec_pad;  // speculative fill: the outputs did not fit (accord_deps_compute)
+    accord::DevStatus reg_status;   // accord_txn_register's check, read back (host side only)
 };
 
 // A device-resident PartialDeps set (result of accord_deps_union / accord_deps_slice).
@@ -209,6 +210,9 @@ struct accord_store {
     std::vector<uint8_t> rdy_tab_last;        // the tables last sent, and where to
     void *rdy_tab_dev = nullptr;
     void *reg_host = nullptr;                 // pinned staging of accord_txn_register's events (one copy)
+    void *rb_host = nullptr;                  // pinned staging of accord_redundant_before_set's entries (one copy)
+    size_t rb_host_cap = 0;
+    DevBuf rb_pack;                           // ... their device landing, scattered by one launch
     size_t reg_host_cap = 0;
     void *up_host = nullptr;                  // pinned staging of a small batch's upload (one copy)
     size_t up_host_cap = 0;
