@@ -23,6 +23,14 @@ uint32_t radix_sort_scan_len(uint32_t n);   // longest scan the sort runs (size 
 void radix_sort_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys_out, uint32_t *vals_out,
                       uint32_t *keys_tmp, uint32_t *vals_tmp, const uint32_t *ents_in, uint32_t *ents_out,
                       uint32_t *ents_tmp, uint32_t n, int bits, void *temp, void *scan_state, hipStream_t s);
+// A resident store's batch (P pairs: keys bkey, entries bent, TxnId order) joined to its carried
+// key-major history (C entries) without re-sorting the carry: the same sort_key / sort_pair / hist
+// as radix_sort_pairs over [carry | batch].  comp_tmp, sorted_tmp: P words each.  merge_join_fits:
+// P and the key bits qualify (chunks of 1024 pairs sorted in LDS, up to 16 of them).
+bool merge_join_fits(uint32_t P, int bits);
+void merge_join_batch(const uint32_t *ckey, const uint32_t *cent, uint32_t C, const uint32_t *bkey,
+                      const uint32_t *bent, uint32_t P, int bits, uint32_t *comp_tmp, uint32_t *sorted_tmp,
+                      uint32_t *sort_key, uint32_t *sort_pair, uint32_t *hist, hipStream_t s);
 
 // ---- small fills in one launch (scan.hip): descriptor k sets words [0, d[k].words) of d[k].p ----
 struct FillDesc {

@@ -165,7 +165,187 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep(const uint32_t *__res
         }
     }
 }
+// ---- a resident store's batch joining its carried history: sort the batch, merge ----
+// The carry is key-major already (TxnId order inside a key) and the batch's pairs are in TxnId
+// order, so a batch of up to 16 Ki pairs is sorted apart and merged instead of re-sorting [carry |
+// batch] (six launches over C + P entries).  Every workgroup sorts one chunk of 1024 pairs as
+// (key << ib | pair index) composites -- a thread per pair, LSD passes of <= 9 key bits ranked with
+// wave ballots, re-ordered through LDS -- and every entry of the carry and of the chunks then finds
+// its place by counting, in each other run, the entries that precede it: carry entry i of key k goes
+// to i + #(batch keys < k); a batch pair of composite c and key k at position t of its chunk to
+// t + #(carry keys <= k) + #(other chunks' composites < c) -- the carry's entries of a key first, then
+// the batch's in TxnId order, as the stable sort of [carry | batch] put them.  The searches of one
+// entry run in lockstep (one load per run per step in flight).  (One workgroup sorting the whole
+// batch took 22 us for 8 Ki pairs: the ballot ranking is VALU-bound on one CU,
+// scripts/micro/batch_sort.hip.)
+constexpr uint32_t MS_CHUNK = 1024, MS_RUNS = 16, MS_MAX = MS_CHUNK * MS_RUNS;
+constexpr int MS_WAVES = MS_CHUNK / 64, MS_BITS = 9, MS_BINS = 1 << MS_BITS;
+
+__global__ __launch_bounds__(MS_CHUNK) void ms_chunk_sort_kernel(uint32_t P, uint32_t ib, int kbits,
+                                                                 const uint32_t *__restrict__ bkey,
+                                                                 uint32_t *__restrict__ comp)
+{
+    __shared__ uint32_t sh[MS_CHUNK];
+    __shared__ uint32_t wcnt[MS_WAVES][MS_BINS];     // per wave and digit: count, then wave offset
+    __shared__ uint32_t run[MS_BINS];
+    __shared__ uint32_t wsum[MS_WAVES];
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t base = blockIdx.x * MS_CHUNK, n = min(MS_CHUNK, P - base);
+    const bool valid = tid < n;
+    const uint64_t lt = lanemask_lt();
+    uint32_t v = valid ? (bkey[base + tid] << ib) | (base + tid) : 0u;
+    const int passes = (kbits + MS_BITS - 1) / MS_BITS;
+    int shift = (int)ib, left = kbits;
+    for (int p = 0; p < passes; ++p) {
+        const int pb = left / (passes - p);
+        const uint32_t mask = (1u << pb) - 1u, bins = mask + 1u;
+        for (uint32_t b = lane; b < bins; b += 64) wcnt[w][b] = 0;
+        const uint32_t d = (v >> shift) & mask;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < pb; ++b) {
+            const uint64_t bb = __ballot(valid && ((d >> b) & 1u));
+            peers &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        wave_lds_sync();
+        if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        {   // per digit: wave offsets (exclusive over waves), then the digits' exclusive scan
+            uint32_t tot = 0;
+            if (tid < bins)
+#pragma unroll
+                for (int ww = 0; ww < MS_WAVES; ++ww) { const uint32_t x = wcnt[ww][tid]; wcnt[ww][tid] = tot; tot += x; }
+            const uint32_t inc = wave_incl_scan(tot);
+            if (lane == 63) wsum[w] = inc;
+            __syncthreads();
+            uint32_t ex = inc - tot;
+            for (uint32_t ww = 0; ww < w; ++ww) ex += wsum[ww];
+            if (tid < bins) run[tid] = ex;
+        }
+        __syncthreads();
+        if (valid) sh[run[d] + wcnt[w][d] + rank] = v;
+        __syncthreads();
+        v = valid ? sh[tid] : 0u;
+        __syncthreads();
+        shift += pb;
+        left -= pb;
+    }
+    if (valid) comp[base + tid] = v;
+}
+
+// the chunks merged into one sorted run: every chunk in the LDS of each workgroup of 256 pairs; the
+// pair goes to #(composites below it) summed over the chunks, the chunks
+// searched in lockstep (one LDS read per chunk per step; 256-thread workgroups spread the searches'
+// VALU work over P / 256 CUs -- a workgroup per 1024-pair chunk took 15 us for 8 Ki pairs)
+constexpr uint32_t MS_MT = 256;
+__global__ __launch_bounds__(MS_MT) void ms_chunk_merge_kernel(uint32_t P, const uint32_t *__restrict__ comp,
+                                                               uint32_t *__restrict__ sorted)
+{
+    __shared__ uint32_t sh[MS_MAX];
+    const uint32_t tid = threadIdx.x, nb = (P + MS_CHUNK - 1) / MS_CHUNK;
+    for (uint32_t i0 = 0; i0 < P; i0 += MS_MT * 16) {     // 16 loads in flight per thread
+        uint32_t t[16];
+#pragma unroll
+        for (uint32_t u = 0; u < 16; ++u) {
+            const uint32_t i = i0 + u * MS_MT + tid;
+            t[u] = i < P ? comp[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 16; ++u) {
+            const uint32_t i = i0 + u * MS_MT + tid;
+            if (i < P) sh[i] = t[u];
+        }
+    }
+    __syncthreads();
+    const uint32_t g = blockIdx.x * MS_MT + tid;
+    if (g >= P) return;
+    const uint32_t c = sh[g];
+    // every run counted, its own included (composites are distinct: there it counts t itself);
+    // four runs searched together, branch-free steps (a fully unrolled 16-run search was 20 KB of
+    // code and took 21 us, instruction fetch on cold CUs)
+    uint32_t t = 0;
+    for (uint32_t r0 = 0; r0 < nb; r0 += 4) {
+        uint32_t pos[4], len[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            pos[u] = 0;
+            len[u] = r0 + u < nb ? min(MS_CHUNK, P - (r0 + u) * MS_CHUNK) : 0u;
+        }
+#pragma unroll
+        for (uint32_t step = MS_CHUNK; step >= 1; step >>= 1) {
+            uint32_t v[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u)
+                v[u] = sh[min((r0 + u) * MS_CHUNK + min(pos[u] + step, max(len[u], 1u)) - 1, MS_MAX - 1)];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u)
+                if (pos[u] + step <= len[u] && v[u] < c) pos[u] += step;
+        }
+        t += pos[0] + pos[1] + pos[2] + pos[3];
+    }
+    sorted[t] = c;
+}
+
+// carry entry i of key k to i + #(batch keys < k), batch pair at position j of the sorted batch to
+// j + #(carry keys <= k); branch-free searches (ctop, btop: the highest powers of two <= C, P)
+__global__ __launch_bounds__(256) void ms_merge_kernel(uint32_t C, uint32_t P, uint32_t ib, uint32_t ctop, uint32_t btop,
+                                                       const uint32_t *__restrict__ ckey, const uint32_t *__restrict__ cent,
+                                                       const uint32_t *__restrict__ comp, const uint32_t *__restrict__ bent,
+                                                       uint32_t *__restrict__ sort_key, uint32_t *__restrict__ sort_pair,
+                                                       uint32_t *__restrict__ hist)
+{
+    const uint32_t mask = (1u << ib) - 1u;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < C + P; x += gridDim.x * blockDim.x) {
+        uint32_t k, pair, ent, pos;
+        if (x < C) {
+            k = ckey[x];
+            const uint32_t c0 = k << ib;
+            uint32_t lo = 0;
+            for (uint32_t step = btop; step >= 1; step >>= 1)
+                if (lo + step <= P && comp[lo + step - 1] < c0) lo += step;
+            pos = x + lo; pair = x; ent = cent[x];
+        } else {
+            const uint32_t j = x - C, c = comp[j], q = c & mask;
+            k = c >> ib;
+            uint32_t lo = 0;
+            for (uint32_t step = ctop; step >= 1; step >>= 1)
+                if (lo + step <= C && ckey[lo + step - 1] <= k) lo += step;
+            pos = j + lo; pair = C + q; ent = bent[q];
+        }
+        sort_key[pos] = k;
+        sort_pair[pos] = pair;
+        hist[pos] = ent;
+    }
+}
 } // namespace
+
+inline uint32_t ms_index_bits(uint32_t P)
+{
+    uint32_t ib = 0;
+    while ((1u << ib) < P) ++ib;
+    return ib;
+}
+
+bool merge_join_fits(uint32_t P, int bits)
+{
+    return P >= 1 && P <= MS_MAX && std::max(bits, 1) + (int)ms_index_bits(P) <= 31;
+}
+
+void merge_join_batch(const uint32_t *ckey, const uint32_t *cent, uint32_t C, const uint32_t *bkey,
+                      const uint32_t *bent, uint32_t P, int bits, uint32_t *comp_tmp, uint32_t *sorted_tmp,
+                      uint32_t *sort_key, uint32_t *sort_pair, uint32_t *hist, hipStream_t s)
+{
+    const uint32_t ib = ms_index_bits(P), nb = (P + MS_CHUNK - 1) / MS_CHUNK;
+    hipLaunchKernelGGL(ms_chunk_sort_kernel, dim3(nb), dim3(MS_CHUNK), 0, s, P, ib, std::max(bits, 1), bkey, comp_tmp);
+    hipLaunchKernelGGL(ms_chunk_merge_kernel, dim3((P + MS_MT - 1) / MS_MT), dim3(MS_MT), 0, s, P, comp_tmp, sorted_tmp);
+    uint32_t ctop = 1, btop = 1;
+    while (ctop * 2 <= C) ctop *= 2;
+    while (btop * 2 <= P) btop *= 2;
+    const uint32_t total = C + P;
+    const uint32_t b = std::min<uint32_t>((total + 255) / 256, 8192u);
+    hipLaunchKernelGGL(ms_merge_kernel, dim3(b), dim3(256), 0, s, C, P, ib, ctop, btop, ckey, cent, sorted_tmp, bent, sort_key,
+                       sort_pair, hist);
+}
 
 inline int rs_items(uint32_t n) { return n < RS_SMALL_N ? 4 : RS_ITEMS_MAX; }
 inline uint32_t rs_tiles(uint32_t n) { return (n + rs_tile(rs_items(n)) - 1) / rs_tile(rs_items(n)); }

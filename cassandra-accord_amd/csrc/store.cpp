@@ -380,6 +380,10 @@ int32_t accord_deps_compute(accord_store *s)
     if (rdeps) HIPCHECK(s, s->rt_hits.ensure((size_t)n * (1 + accord::RT_HIT_WORDS) * 4 + 64));
 
     HostTotals *dev = s->status_totals.as<HostTotals>();
+    // a resident store's batch of up to 16 Ki pairs is sorted alone (one workgroup) and merged into
+    // its key-major carry (accord::merge_join_batch) instead of re-sorting [carry | batch]
+    const int kbits = bits_for(nkeys - 1);
+    const bool merge = C && accord::merge_join_fits(P, kbits);
     record(s, EV_START);
     {   // every small initialisation of the pipeline in one launch
         accord::FillList fl;
@@ -415,7 +419,7 @@ int32_t accord_deps_compute(accord_store *s)
             s->rb_status_zeroed = true;
         }
         accord::CopyList cl;          // a resident store's carried history heads the pairs
-        if (C) {
+        if (C && !merge) {
             cl.add(s->cy_key.p, s->pair_key.p, (size_t)C * 4);
             cl.add(s->cy_ent.p, s->pair_ent.p, (size_t)C * 4);
         }
@@ -450,10 +454,15 @@ int32_t accord_deps_compute(accord_store *s)
         bound_l = s->bound_l.as<uint32_t>(); bound_g = s->bound_g.as<uint32_t>(); pair_bound = s->pair_bound.as<uint32_t>();
     }
     record(s, EV_VALIDATE);
-    accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
+    if (merge)
+        accord::merge_join_batch(s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>(), C, s->pair_key.as<uint32_t>() + C,
+                                 s->pair_ent.as<uint32_t>() + C, P, kbits, s->tmp_key.as<uint32_t>(),
+                                 s->tmp_val.as<uint32_t>(), s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(), s->hist.as<uint32_t>(), st);
+    else
+        accord::radix_sort_pairs(s->pair_key.as<uint32_t>(), nullptr, s->sort_key.as<uint32_t>(),
                                  s->sort_pair.as<uint32_t>(), s->tmp_key.as<uint32_t>(), s->tmp_val.as<uint32_t>(),
                                  s->pair_ent.as<uint32_t>(), s->hist.as<uint32_t>(), s->tmp_ent.as<uint32_t>(), PH,
-                                 bits_for(nkeys - 1), s->radix_tmp.p, s->scan_tmp.p, st);
+                                 kbits, s->radix_tmp.p, s->scan_tmp.p, st);
     record(s, EV_SORT);
     accord::launch_history(PH, nkeys, s->cfg.window, s->sort_key.as<uint32_t>(), s->sort_pair.as<uint32_t>(),
                            s->hist.as<uint32_t>(), s->seg_start.as<uint32_t>(),
