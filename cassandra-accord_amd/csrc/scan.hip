@@ -366,6 +366,51 @@ __global__ __launch_bounds__(SC_THREADS) void sc_one_tile(ScanArgs a, uint32_t n
             if (idx < n) a.out[k][idx] = tile[k][idx];
         }
 }
+// n <= 1024 (a small batch's per-txn counts): four consecutive items per thread in registers --
+// a fraction of sc_one_tile's code (its 16 items per array are unrolled whatever n is, ~1,150
+// instructions for three arrays), which a short launch on a cold CU pays for in instruction fetch
+constexpr uint32_t SC_SMALL = SC_THREADS * 4;
+template <int NA>
+__global__ __launch_bounds__(SC_THREADS) void sc_small(ScanArgs a, uint32_t n)
+{
+    __shared__ uint64_t s_wsum[NA][SC_THREADS / 64];
+    const uint32_t tid = threadIdx.x, w = wave_id(), lane = lane_id(), first = tid * 4;
+    uint32_t v[NA][4];
+    uint64_t local[NA], incl[NA], tt[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[k][j] = first + j < n ? a.in[k][first + j] : 0u;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        local[k] = (uint64_t)v[k][0] + v[k][1] + v[k][2] + v[k][3];
+        incl[k] = wave_incl_scan64(local[k]);
+        if (lane == 63) s_wsum[k][w] = incl[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        uint64_t o = 0, t = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < SC_THREADS / 64; ++q) {
+            if (q < w) o += s_wsum[k][q];
+            t += s_wsum[k][q];
+        }
+        uint64_t run = o + incl[k] - local[k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (first + j < n) a.out[k][first + j] = (uint32_t)run;
+            run += v[k][j];
+        }
+        tt[k] = t;
+        if (tid == 0) {
+            a.out[k][n] = (uint32_t)t;
+            if (a.total[k]) *a.total[k] = t;
+        }
+    }
+    if constexpr (NA == 3)
+        if (tid == 0 && a.has_spec) spec_eval(a, tt);
+}
 __global__ __launch_bounds__(256) void fill_words_kernel(FillList L)
 {
     const FillDesc d = L.d[blockIdx.y];
@@ -436,6 +481,15 @@ void exclusive_scan_multi(int na, const uint32_t *const *in, uint32_t *const *ou
     ScanArgs a{};
     for (int k = 0; k < na; ++k) { a.in[k] = in[k]; a.out[k] = out[k]; a.total[k] = total[k]; }
     if (spec && na == 3) { a.spec = *spec; a.has_spec = 1u; }
+    if (n <= SC_SMALL) {
+        switch (na) {
+        case 1: hipLaunchKernelGGL(sc_small<1>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        case 2: hipLaunchKernelGGL(sc_small<2>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        case 3: hipLaunchKernelGGL(sc_small<3>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        default: hipLaunchKernelGGL(sc_small<4>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
+        }
+        return;
+    }
     if (tiles == 1) {
         switch (na) {
         case 1: hipLaunchKernelGGL(sc_one_tile<1>, dim3(1), dim3(SC_THREADS), 0, s, a, n); break;
