@@ -1067,24 +1067,41 @@ int32_t status_truncate_carry(accord_store *s, uint32_t m, const uint32_t *start
 {
     const uint32_t C = s->carry_n, key_lo = s->cfg.key_lo, nkeys = s->cfg.key_hi - key_lo;
     if (C == 0 || m == 0) return ACCORD_OK;
-    std::vector<uint32_t> kb(nkeys, 0u);
+    // entry e covers the keys (start[e], end[e]] of the store's [key_lo, key_hi): per entry, its
+    // clipped key range (store-relative, inclusive) -- no per-key table built on the host unless the
+    // event-exact readiness needs one (a 100 k-key table and its walk had cost ~90 us per call)
+    auto clip = [&](uint32_t e, uint32_t &lo, uint32_t &hi) {
+        if (bound[e] == ACCORD_NO_TXN || bound[e] == 0) return false;
+        const uint64_t a = std::max<uint64_t>((uint64_t)start[e] + 1, key_lo), b = std::min<uint64_t>(end[e], (uint64_t)key_lo + nkeys - 1);
+        if (a > b) return false;
+        lo = (uint32_t)(a - key_lo); hi = (uint32_t)(b - key_lo);
+        return true;
+    };
     bool any = false;
-    uint32_t e = 0;
-    for (uint32_t r = 0; r < nkeys; ++r) {         // key r + key_lo in (start, end]
-        const uint32_t k = key_lo + r;
-        while (e < m && end[e] < k) ++e;
-        if (e == m) break;
-        if (start[e] < k && bound[e] != ACCORD_NO_TXN && bound[e] > 0) { kb[r] = bound[e]; any = true; }
+    for (uint32_t e = 0; e < m && !any; ++e) {
+        uint32_t lo, hi;
+        any = clip(e, lo, hi);
     }
     if (!any) return ACCORD_OK;
     // the readiness evaluation skips deps below each key's bound (ready.hip): a cumulative max
     std::vector<uint32_t> tkeys;          // event-exact readiness: the keys that lose entries
     if (s->rdy_event_mode) {
+        std::vector<uint32_t> kb(nkeys, 0u);
+        for (uint32_t e = 0; e < m; ++e) {
+            uint32_t lo, hi;
+            if (clip(e, lo, hi)) std::fill(kb.begin() + lo, kb.begin() + hi + 1, bound[e]);
+        }
         const int32_t rc = accord_impl::ready_truncate_keys(s, kb, tkeys);
         if (rc != ACCORD_OK) return rc;
     }
     if (s->rdy_kb_host.size() != nkeys) s->rdy_kb_host.assign(nkeys, 0u);
-    for (uint32_t r = 0; r < nkeys; ++r) s->rdy_kb_host[r] = std::max(s->rdy_kb_host[r], kb[r]);
+    for (uint32_t e = 0; e < m; ++e) {
+        uint32_t lo, hi;
+        if (!clip(e, lo, hi)) continue;
+        uint32_t *kh = s->rdy_kb_host.data();
+        const uint32_t bv = bound[e];
+        for (uint32_t r = lo; r <= hi; ++r) kh[r] = kh[r] > bv ? kh[r] : bv;
+    }
     s->rdy_kb_dirty = true;
     hipStream_t st = s->stream;
     HIPCHECK(s, s->carry_tmp.ensure(accord::carry_temp_bytes(C, nkeys)));
