@@ -480,15 +480,34 @@ struct RegParams {
     uint32_t epoch;
 };
 
-__global__ __launch_bounds__(256) void reg_check_kernel(RegParams p)
+// The TxnId lookup in two levels: every stride-th TxnId of the store's table sampled into LDS by
+// each workgroup (<= REG_SAMPLES of them), a search there, then one inside a stride of the table --
+// log2(stride) dependent global loads instead of log2(tx_n) (a registration's check was 13 us on a
+// 65 k-txn table)
+constexpr uint32_t REG_SAMPLES = 2048;
+__global__ __launch_bounds__(256) void reg_check_kernel(RegParams p, uint32_t stride_log)
 {
+    __shared__ uint64_t smsb[REG_SAMPLES], slsb[REG_SAMPLES];
+    __shared__ int32_t snode[REG_SAMPLES];
+    const uint32_t stride = 1u << stride_log, ns = (p.tx_n + stride - 1) >> stride_log;
+    for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) {
+        const uint32_t t = j << stride_log;
+        smsb[j] = p.tmsb[t]; slsb[j] = p.tlsb[t]; snode[j] = p.tnode[t];
+    }
+    __syncthreads();
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += gridDim.x * blockDim.x) {
         const Ts id{p.msb[r], p.lsb[r], p.node[r]};
         if (r > 0 && ts_cmp(p.msb[r - 1], p.lsb[r - 1], p.node[r - 1], id.msb, id.lsb, id.node) >= 0)
             record_error(p.err, r, ACCORD_ERR_UNSORTED);
         const uint32_t nw = p.status[r];
         if (nw > ST_ERASED) { record_error(p.err, r, ACCORD_ERR_ARG); continue; }
-        uint32_t lo = 0, hi = p.tx_n;
+        uint32_t J = 0, jh = ns;                      // samples below id
+        while (J < jh) {
+            const uint32_t m = (J + jh) >> 1;
+            if (ts_cmp(smsb[m], slsb[m], snode[m], id.msb, id.lsb, id.node) < 0) J = m + 1; else jh = m;
+        }
+        // the first table entry >= id lies in ((J - 1) * stride, J * stride]
+        uint32_t lo = J ? ((J - 1) << stride_log) + 1 : 0u, hi = min(J << stride_log, p.tx_n);
         while (lo < hi) {
             const uint32_t m = (lo + hi) >> 1;
             if (ts_cmp(p.tmsb[m], p.tlsb[m], p.tnode[m], id.msb, id.lsb, id.node) < 0) lo = m + 1; else hi = m;
@@ -1233,7 +1252,9 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     p.cchg = s->rg_cchg.as<uint32_t>();
     p.epoch = s->rg_epoch + 1;
     if (p.tx_n == 0) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: the store holds no txn yet");
-    hipLaunchKernelGGL(reg_check_kernel, dim3(grid_for(n)), dim3(256), 0, st, p);
+    uint32_t stride_log = 0;
+    while (((uint64_t)p.tx_n + (1ull << stride_log) - 1) >> stride_log > REG_SAMPLES) ++stride_log;
+    hipLaunchKernelGGL(reg_check_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, stride_log);
     HIPCHECK(s, hipMemcpyAsync(&s->pinned->reg_status, p.err, sizeof(accord::DevStatus), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     const accord::DevStatus hs = s->pinned->reg_status;
