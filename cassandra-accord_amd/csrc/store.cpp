@@ -142,6 +142,8 @@ int32_t accord_store_destroy(accord_store *s)
     if (s->rb_host) (void)hipHostFree(s->rb_host);
     s->rb_pack.release();
     if (s->up_host) (void)hipHostFree(s->up_host);
+    for (hipEvent_t &e : s->up_ev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(s->stream);
     delete s;
     return ACCORD_OK;
@@ -258,43 +260,72 @@ int32_t accord_batch_upload(accord_store *s, const accord_batch *b)
         parts.push_back({s->exec_lsb.p, b->exec_lsb, (size_t)n * 8});
         parts.push_back({s->exec_node.p, b->exec_node, (size_t)n * 4});
     }
+    s->user_txn_index = b->txn_index != nullptr;
+    s->has_txn_index = s->user_txn_index || s->resident;
+    const bool gen_index = s->has_txn_index && !s->user_txn_index;     // resident: next_global + t
     size_t packed = 0;
     for (const Part &q : parts) packed += (q.bytes + 15) & ~(size_t)15;
-    if (!ro) HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
-    if (packed <= (8u << 20)) {
-        if (s->up_host_cap < packed) {
+    // zero range offsets and a resident store's stream positions ride in the pack (src nullptr: zeros)
+    const size_t extra = (!ro ? ((((size_t)n + 1) * 4 + 15) & ~(size_t)15) : 0) + (gen_index ? (((size_t)n * 4 + 15) & ~(size_t)15) : 0);
+    bool synced_copy = true;
+    if (packed + extra <= (8u << 20)) {
+        if (!ro) parts.push_back({s->rng_off.p, nullptr, ((size_t)n + 1) * 4});
+        if (gen_index) parts.push_back({s->txn_index.p, nullptr, (size_t)n * 4});
+        packed += extra;
+        // two halves of pinned staging used in turn: an upload waits only for the copy two uploads
+        // back (an event), not for its own (the compute is ordered after it on the stream)
+        const size_t half = std::max<size_t>(packed, 1u << 16);
+        if (s->up_host_cap < 2 * half) {
+            HIPCHECK(s, hipStreamSynchronize(s->stream));       // no copy still reads the old staging
             if (s->up_host) (void)hipHostFree(s->up_host);
             s->up_host = nullptr; s->up_host_cap = 0;
-            HIPCHECK(s, hipHostMalloc(&s->up_host, std::max<size_t>(packed * 2, 1u << 16), hipHostMallocDefault));
-            s->up_host_cap = std::max<size_t>(packed * 2, 1u << 16);
+            HIPCHECK(s, hipHostMalloc(&s->up_host, 4 * half, hipHostMallocDefault));
+            s->up_host_cap = 4 * half;
+            s->up_ev_live[0] = s->up_ev_live[1] = false;
         }
+        const uint32_t hb = s->up_half;
+        s->up_half ^= 1u;
+        if (s->up_ev_live[hb]) HIPCHECK(s, hipEventSynchronize(s->up_ev[hb]));
+        s->up_ev_live[hb] = false;
+        char *hp = (char *)s->up_host + hb * (s->up_host_cap / 2);
         HIPCHECK(s, s->up_stage.ensure(packed + 16));
         accord::CopyList cl;
         size_t off = 0;
         for (const Part &q : parts) {
             if (q.bytes) {
-                std::memcpy((char *)s->up_host + off, q.src, q.bytes);
+                if (q.src) std::memcpy(hp + off, q.src, q.bytes);
+                else if (q.dst == s->txn_index.p && gen_index) {
+                    uint32_t *ti = (uint32_t *)(hp + off);
+                    for (uint32_t t = 0; t < n; ++t) ti[t] = s->next_global + t;
+                } else std::memset(hp + off, 0, q.bytes);
                 cl.add((const char *)s->up_stage.p + off, q.dst, q.bytes);
             }
             off += (q.bytes + 15) & ~(size_t)15;
         }
-        if (packed) HIPCHECK(s, hipMemcpyAsync(s->up_stage.p, s->up_host, packed, hipMemcpyHostToDevice, s->stream));
+        if (packed) {
+            HIPCHECK(s, hipMemcpyAsync(s->up_stage.p, hp, packed, hipMemcpyHostToDevice, s->stream));
+            if (!s->up_ev[hb]) HIPCHECK(s, hipEventCreateWithFlags(&s->up_ev[hb], hipEventDisableTiming));
+            HIPCHECK(s, hipEventRecord(s->up_ev[hb], s->stream));
+            s->up_ev_live[hb] = true;
+            synced_copy = false;
+        }
         accord::launch_copy_words(cl, s->stream);
     } else {
+        if (!ro) HIPCHECK(s, hipMemsetAsync(s->rng_off.p, 0, ((size_t)n + 1) * 4, s->stream));
         for (const Part &q : parts)
             if (q.bytes) HIPCHECK(s, hipMemcpyAsync(q.dst, q.src, q.bytes, hipMemcpyHostToDevice, s->stream));
+        if (gen_index) accord::launch_gen_index(n, s->next_global, s->txn_index.as<uint32_t>(), s->stream);
     }
-    s->user_txn_index = b->txn_index != nullptr;
-    s->has_txn_index = s->user_txn_index || s->resident;
-    if (s->has_txn_index && !s->user_txn_index)
-        accord::launch_gen_index(n, s->next_global, s->txn_index.as<uint32_t>(), s->stream);   // resident: next_global + t
     // where the batch ends in the stream (committed to the store when its compute succeeds)
     s->b_end = !s->resident ? n : (n == 0 ? s->next_global : (s->user_txn_index ? b->txn_index[n - 1] + 1u : s->next_global + n));
     if (s->resident && n && (uint64_t)s->next_global + n > (1ull << 29))
         return fail(s, ACCORD_ERR_CAPACITY, "resident store stream exceeds 2^29 txns");
     if (n) { s->b_last_msb = b->msb[n - 1]; s->b_last_lsb = b->lsb[n - 1]; s->b_last_node = b->node[n - 1]; }
     s->has_exec = b->exec_msb != nullptr;
-    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    // the large path copied from the caller's pageable arrays: wait for it; the packed path's host
+    // inputs were consumed into the staging above
+    if (synced_copy) HIPCHECK(s, hipStreamSynchronize(s->stream));
+    else HIPCHECK(s, hipGetLastError());
     s->has_batch = true;
     return ACCORD_OK;
 }

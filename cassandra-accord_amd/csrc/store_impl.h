@@ -216,6 +216,9 @@ struct accord_store {
     size_t reg_host_cap = 0;
     void *up_host = nullptr;                  // pinned staging of a small batch's upload (one copy)
     size_t up_host_cap = 0;
+    hipEvent_t up_ev[2] = {nullptr, nullptr}; // the staging halves' copies (accord_batch_upload)
+    bool up_ev_live[2] = {false, false};
+    uint32_t up_half = 0;
     DevBuf up_stage;                          // its device side, scattered to the batch arrays
     size_t rdy_tab_cap = 0;
     uint64_t *rdy_stats = nullptr;            // ACCORD_READY_STATS diagnostics
