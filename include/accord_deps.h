@@ -269,7 +269,10 @@ typedef int32_t (*accord_visit_fn)(void *ctx, uint32_t is_range, uint32_t key_or
 int32_t accord_deps_visit(const accord_deps *deps, uint32_t txn, accord_visit_fn fn, void *ctx);
 
 /* ---- device-resident pipeline (inputs already in HBM; used by the bench) ---- */
-int32_t accord_batch_upload(accord_store *store, const accord_batch *host_batch);  /* H2D, sync */
+/* H2D.  The host arrays are consumed before it returns (a batch of <= 8 MiB is staged in page-locked
+ * memory and its copy left running on the store's stream, ordered before the compute; a larger one is
+ * copied and waited for); a failure of the copy itself is reported by the next call on the store. */
+int32_t accord_batch_upload(accord_store *store, const accord_batch *host_batch);
 int32_t accord_deps_compute(accord_store *store);          /* enqueue + run the whole pipeline */
 int32_t accord_deps_device_view(accord_store *store, accord_deps *dev);  /* device pointers */
 int32_t accord_deps_download(accord_store *store, accord_deps *out);     /* D2H copy, host-owned */
