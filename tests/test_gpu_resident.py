@@ -58,6 +58,28 @@ def test_batches_equal_single_and_literal(gpu_device, case):
     assert got.first_difference(lit) is None
 
 
+# batch pair counts around the merge join's chunk and size limits (csrc/radix_sort.hip: 1024-pair
+# chunks, up to 16 of them; a batch over 16 Ki pairs, or the first one, re-sorts with the radix passes)
+MERGE_CASES = [
+    # keys per txn, keyspace, batch sizes (txns)
+    (1, 3000, [5, 1, 1024, 1025, 1023, 16384, 16385, 3000, 2]),
+    (8, 100000, [7, 128, 2048, 2049, 1, 300]),
+]
+
+
+@pytest.mark.parametrize("case", MERGE_CASES, ids=[f"m{i}" for i in range(len(MERGE_CASES))])
+def test_merge_join_batch_sizes(gpu_device, case):
+    k, ks, sizes = case
+    n = sum(sizes)
+    s = generate_stream(n, k, ks, 0.99, 0.5, seed=11 + k)
+    pts = [0]
+    for b in sizes:
+        pts.append(pts[-1] + b)
+    got, state = run_batches(s, ks, 256, pts)
+    assert state["next_global"] == n
+    assert got.first_difference(single(s, ks, 256)) is None
+
+
 def test_accept_batches_see_only_registered_txns(gpu_device):
     # executeAt past the end of its batch: only txns registered so far are candidates
     n, ks, W = 12000, 400, 128
