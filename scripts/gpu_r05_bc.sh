@@ -1,4 +1,4 @@
-# Round 5, call bc: resident batch sizes around the merge join's limits
+# Round 5, calls bc, bd: resident batch sizes around the merge join's limits; uploads back to back
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R"; O="$R/gpurun_out/${TAG:-r05_bc}"; mkdir -p "$O"
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_resident.py > "$O/pytest_gpu.log" 2>&1 || { tail -30 "$O/pytest_gpu.log"; exit 1; }

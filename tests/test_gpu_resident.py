@@ -80,6 +80,20 @@ def test_merge_join_batch_sizes(gpu_device, case):
     assert got.first_difference(single(s, ks, 256)) is None
 
 
+def test_uploads_without_compute_between(gpu_device):
+    """accord_batch_upload leaves a small batch's copy running (two page-locked staging halves in
+    turn): uploads back to back, then one compute, give the last batch's deps, for plain and
+    resident stores"""
+    parts = [generate_stream(700 + 50 * i, 4, 500, 0.99, 0.5, seed=40 + i) for i in range(4)]
+    for resident in (False, True):
+        with CommandStore(device=0, key_lo=0, key_hi=500, window=64, resident=resident) as st:
+            for p in parts:
+                st.upload(p)
+            st.compute()
+            got = st.download()
+        assert got.first_difference(single(parts[-1], 500, 64)) is None
+
+
 def test_accept_batches_see_only_registered_txns(gpu_device):
     # executeAt past the end of its batch: only txns registered so far are candidates
     n, ks, W = 12000, 400, 128
