@@ -8,13 +8,18 @@ batch already resident in HBM.  Default workload (BASELINE.json configs[1]): 1,0
 8 keys each, Zipf(0.99) over 100,000 keys, 50% writes, window W=256, seed 2.
 
 Multi-GPU (`bench.py --gpus G`, which starts the G ranks itself, or `torchrun --nproc-per-node G`;
-config 4): one global stream of G x 1,048,576 txns
-(weak scaling: every GPU gets a config-2-sized share); the keyspace is split into 8G CommandStores
-by EvenSplit (local/ShardDistributor.java:46-157) and rank r owns the contiguous block of stores
-[8r, 8r+8).  A step is: compute the partial KeyDeps of the txns intersecting the rank's keys, one
-RCCL exchange (grouped send/recv over xGMI) that moves every txn's partial to its owner rank, and
-the on-device union of the G partials (PreAccept.reduce, messages/PreAccept.java:140-156) -- after
-the step every txn's node-level deps exist exactly once.
+config 4): one global stream of G x 1,048,576 txns (weak scaling: every GPU gets a config-2-sized
+share) over 8G EvenSplit CommandStores (local/ShardDistributor.java:46-157).  Default partition
+(`--partition segments`): rank r owns the r-th segment of the stream -- positions
+[r n, (r+1) n) -- of every CommandStore.  A step is: the segment's CommandsForKey summary (per key,
+what later txns can still reach), one all-gather of the summaries over RCCL/xGMI
+(torch.distributed nccl), the fold of the earlier segments' summaries into the CommandsForKey state
+at the segment's start, and the deps of the segment's txns -- node-level deps, the union
+PreAccept.reduce (messages/PreAccept.java:140-156) would assemble, so no partial deps travel.
+`--partition keys`: rank r owns the key block of stores [8r, 8r+8), computes the partial deps of
+the txns touching it, and one RCCL exchange moves every partial to the txn's owner for the on-device
+union (the round-3..5 design, kept for comparison).  `--one-device`: every rank on GPU 0 with the
+exchange over gloo (a one-GPU rehearsal of the multi-rank code path).
 """
 from __future__ import annotations
 
@@ -137,6 +142,10 @@ def main():
                          "(CPU) and by the device (0: skip)")
     ap.add_argument("--reg-batch", type=int, default=1024, help="txns per batch of the --registered leg")
     ap.add_argument("--reg-batches", type=int, default=64, help="batches of the --registered leg")
+    ap.add_argument("--partition", choices=("segments", "keys"), default="segments",
+                    help="--gpus G > 1: ownership by stream segments (default) or by key blocks of stores")
+    ap.add_argument("--one-device", action="store_true",
+                    help="--gpus G > 1 on one GPU: every rank uses device 0, the exchange runs over gloo")
     ap.add_argument("--launch-dry-run", action="store_true",
                     help="--gpus G > 1: start the G ranks, each prints its rank / world and exits before any GPU work")
     args = ap.parse_args()
@@ -161,43 +170,67 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    torch = None
+    segments = world > 1 and args.partition == "segments"
+    device_index = 0 if (world == 1 or args.one_device) else local_rank
+    xdev = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
+        torch.cuda.set_device(device_index)
+        dist.init_process_group("gloo" if args.one_device else "nccl", init_method="env://")
+        xdev = torch.device("cpu") if args.one_device else torch.device("cuda", device_index)
+        if not segments and args.one_device:
+            raise SystemExit("--one-device rehearses --partition segments only")
 
-    from accord_amd import CommandStore, generate_stream
+    from accord_amd import CommandStore, generate_stream, segment_bounds, segment_exchange
+
+    if args.waiting_on and world > 1:
+        raise SystemExit("config 5 levels one full stream per GPU (replicas only): run it with --gpus 1")
+    if world > 1 and args.range_frac > 0:
+        raise SystemExit("config 4 is the key-txn workload of config 2")
 
     n_total = args.n * world
     # one global stream (identical on every rank); weak scaling: n per GPU
     s_full = generate_stream(n_total, args.keys_per_txn, args.keyspace, args.zipf, args.write_frac,
                              range_frac=args.range_frac, range_len_max=args.range_len, seed=args.seed)
     stores_total = 8 * world
-    # EvenSplit over [0, keyspace): store b owns [b*ks/S, (b+1)*ks/S); rank r owns stores [8r, 8r+8)
-    key_lo = (8 * rank) * args.keyspace // stores_total
-    key_hi = (8 * rank + 8) * args.keyspace // stores_total
+    # EvenSplit over [0, keyspace): store b owns [b*ks/S, (b+1)*ks/S)
     bounds = [b * args.keyspace // stores_total for b in range(stores_total)] + [0xFFFFFFFF]
-    s = s_full if world == 1 else s_full.restrict_keys(key_lo, key_hi, drop_empty=True)
-
-    # one store handle per rank hosting its 8 CommandStores (one unbounded store at --gpus 1)
-    store = CommandStore(device=0 if world == 1 else local_rank, key_lo=key_lo, key_hi=key_hi,
-                         window=args.window, profile=True,
-                         store_bounds=bounds[8 * rank:8 * rank + 9] if world > 1 else None)
-    store.upload(s)
     rccl = None
-    if world > 1:
-        uid = [CommandStore.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        store.comm_init(world, rank, uid[0])
-        rccl = store.comm_size()
+    seg = None
+    if segments:
+        # rank r owns positions [a, b) of every CommandStore: one resident handle hosting all 8G
+        # stores, standing at a with the CommandsForKey state the exchange builds
+        a, b = segment_bounds(n_total, world)[rank]
+        seg = (a, b)
+        s = s_full.slice(a, b)
+        store = CommandStore(device=device_index, key_lo=0, key_hi=args.keyspace, window=args.window, profile=True,
+                             resident=True, store_bounds=bounds)
+        store.segment_begin(a)
+        store.upload(s)
+    else:
+        # rank r owns the key block of stores [8r, 8r+8) (one unbounded store at --gpus 1)
+        key_lo = (8 * rank) * args.keyspace // stores_total
+        key_hi = (8 * rank + 8) * args.keyspace // stores_total
+        s = s_full if world == 1 else s_full.restrict_keys(key_lo, key_hi, drop_empty=True)
+        store = CommandStore(device=device_index, key_lo=key_lo, key_hi=key_hi,
+                             window=args.window, profile=True,
+                             store_bounds=bounds[8 * rank:8 * rank + 9] if world > 1 else None)
+        store.upload(s)
+        if world > 1:
+            uid = [CommandStore.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            store.comm_init(world, rank, uid[0])
+            rccl = store.comm_size()
 
-    if args.waiting_on and world > 1:
-        raise SystemExit("config 5 levels one full stream per GPU (replicas only): run it with --gpus 1")
+    xinfo = {}
 
     def step():
+        if segments:
+            xinfo.update(segment_exchange(store, rank, world, xdev, store_device=torch.device("cuda", device_index)))
         store.compute()
-        if world > 1:
+        if world > 1 and not segments:
             store.exchange_merge(n_total)
         if args.waiting_on:
             store.waiting_on_compute()
@@ -224,17 +257,24 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed_local = elapsed
     if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     store.set_profile(True)
     prof_steps = max(1, min(args.steps, 5))
     stage = {"validate": 0.0, "sort": 0.0, "segment": 0.0, "count": 0.0, "scan": 0.0, "fill": 0.0, "range_fill": 0.0,
              "compact": 0.0, "total": 0.0, "exchange": 0.0, "merge": 0.0, "wo_bits": 0.0, "wo_preds": 0.0, "wo_level": 0.0}
+    if segments:
+        stage.update({"cfk_summary": 0.0, "cfk_carry": 0.0, "exchange_wall": 0.0})
     count_detail, scan_spins, scan_fallbacks = {}, 0, 0
     for _ in range(prof_steps):
+        tx = time.perf_counter()
         step()
+        if segments:
+            a_ms, c_ms = store.segment_timing()
+            stage["cfk_summary"] += a_ms
+            stage["cfk_carry"] += c_ms
+            stage["exchange_wall"] += (time.perf_counter() - tx) * 1e3     # summary + all-gather + carry + compute
         t = store.timing()
         stage["validate"] += t.validate_ms
         stage["sort"] += t.sort_ms
@@ -249,7 +289,7 @@ def main():
             count_detail[k] = count_detail.get(k, 0.0) + v
         scan_spins += t.scan_spins
         scan_fallbacks += t.scan_fallbacks
-        if world > 1:
+        if world > 1 and not segments:
             xms, mms = store.shard_timing()
             stage["exchange"] += xms
             stage["merge"] += mms
@@ -263,14 +303,26 @@ def main():
     for k in count_detail:
         count_detail[k] /= prof_steps
     per_rank = None
+    if segments:
+        stage["exchange_wall"] -= stage["total"]        # host wall of summary + all-gather + carry
     if dist is not None:
-        mine = {"rank": rank, "rccl": list(rccl), "txns": s.n, "pairs": s.pairs, "compute_ms": stage["total"],
-                "exchange_ms": stage["exchange"], "merge_ms": stage["merge"], "elapsed_s": elapsed_local}
+        mine = {"rank": rank, "txns": s.n, "pairs": s.pairs, "compute_ms": stage["total"], "elapsed_s": elapsed_local}
+        if segments:
+            mine.update({"segment": list(seg), "cfk_summary_ms": stage["cfk_summary"], "cfk_carry_ms": stage["cfk_carry"],
+                         "exchange_wall_ms": stage["exchange_wall"], "carry_entries": store.state()["carry_entries"],
+                         "summary_entries": xinfo["summary_entries"][rank], "allgather_bytes_sent": xinfo["bytes_sent"],
+                         "collective": "gloo (one-device rehearsal)" if args.one_device else "RCCL all_gather (torch.distributed nccl)"})
+        else:
+            mine.update({"rccl": list(rccl), "exchange_ms": stage["exchange"], "merge_ms": stage["merge"]})
         per_rank = [None] * world
         dist.all_gather_object(per_rank, mine)
 
-    # sizes for the byte model: the rank's own computed partial (before the exchange)
-    store.compute()
+    # sizes for the byte model: the rank's own computed deps (keys: the partial before the exchange;
+    # segments: the node-level deps of the segment's txns)
+    if segments:
+        step()
+    else:
+        store.compute()
     view = store.device_view()
     n = s.n
     P = s.pairs
@@ -351,8 +403,10 @@ def main():
                    "zipf": args.zipf, "window": args.window, "seed": args.seed,
                    "n_txns_total": n_total,
                    "gpu_stores": world, "evensplit_stores": stores_total if world > 1 else None,
-                   "parallelism": f"keyspace-sharded x{world}" + (" + RCCL exchange/union" if world > 1 else "")},
-        "rccl_ranks": per_rank[0]["rccl"][0] if per_rank else None,
+                   "parallelism": (f"stream segments x{world}: every rank owns 1/{world} of the stream for all "
+                                   f"{stores_total} CommandStores; CFK summaries all-gathered" if segments else
+                                   f"keyspace-sharded x{world}" + (" + RCCL exchange/union" if world > 1 else ""))},
+        "rccl_ranks": (per_rank[0]["rccl"][0] if per_rank and not segments else world if per_rank else None),
         "deps_per_s": D * world * args.steps / elapsed,
         "sizes": {"N": n, "P": P, "keys_out": kc, "U": U, "D": D},
         "stage_ms": stage,
@@ -392,6 +446,10 @@ def main():
 
 
 def workload_name(args, world=1):
+    if world > 1 and args.partition == "segments":
+        return (f"config4: {world} x {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over "
+                f"{args.keyspace} keys, {8 * world} EvenSplit CommandStores, W={args.window}; rank r owns stream "
+                f"segment r of every store: CFK summary + one all-gather + carry + node-level deps")
     if world > 1:
         return (f"config4: {world} x {args.n} key txns x {args.keys_per_txn} keys, Zipf({args.zipf}) over "
                 f"{args.keyspace} keys, {8 * world} EvenSplit CommandStores (8 per GPU), W={args.window}; per-rank "

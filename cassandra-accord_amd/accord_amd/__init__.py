@@ -26,7 +26,7 @@ import numpy as np
 __all__ = [
     "AccordError", "IllegalStateException", "IllegalArgumentException", "lib", "lib_path",
     "Stream", "generate_stream", "CommandStore", "PartialDeps", "Timing", "WaitingOn",
-    "txn_id_str", "keydeps_str", "rangedeps_str", "EXPORTED_SYMBOLS",
+    "txn_id_str", "keydeps_str", "rangedeps_str", "EXPORTED_SYMBOLS", "segment_bounds", "segment_exchange",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -58,8 +58,11 @@ EXPORTED_SYMBOLS = [
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
     "accord_max_conflicts_fold_from", "accord_store_state", "accord_store_reset", "accord_txn_register",
     "accord_deps_visit", "accord_deps_range_stab", "accord_range_stab_release",
-    "accord_redundant_before_set", "accord_redundant_before_set_ex",
+    "accord_redundant_before_set", "accord_redundant_before_set_ex", "accord_abi_version",
+    "accord_segment_begin", "accord_segment_summary", "accord_segment_summary_copy", "accord_segment_carry",
+    "accord_segment_timing",
 ]
+ABI_VERSION = 6              # include/accord_deps.h ACCORD_ABI_VERSION this mirror follows
 NO_TXN = 0xFFFFFFFF          # RedundantBefore bound Timestamp.NONE
 VISIT_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32)
 
@@ -158,6 +161,11 @@ class _Timing(C.Structure):
                 ("scan_spins", C.c_uint64), ("scan_fallbacks", C.c_uint64)]
 
 
+class _CfkPart(C.Structure):
+    """accord_cfk_part: a stream segment's CommandsForKey summary in device memory."""
+    _fields_ = [("n", C.c_uint64), ("key", C.c_void_p), ("ent", C.c_void_p)]
+
+
 class _WorkloadCfg(C.Structure):
     _fields_ = [("n", C.c_uint32), ("keys_per_txn", C.c_uint32), ("keyspace", C.c_uint32),
                 ("ranges_max", C.c_uint32), ("zipf_s", C.c_double), ("write_frac", C.c_double),
@@ -230,6 +238,15 @@ def lib() -> C.CDLL:
         L.accord_deps_range_stab.argtypes = [C.c_void_p, C.POINTER(_Deps), _u32p, _u32p, _u32p, C.POINTER(_RangeStab)]
         L.accord_range_stab_release.argtypes = [C.POINTER(_RangeStab)]
         L.accord_range_stab_release.restype = None
+        L.accord_abi_version.argtypes = []
+        L.accord_abi_version.restype = C.c_uint32
+        L.accord_segment_begin.argtypes = [C.c_void_p, C.c_uint32]
+        L.accord_segment_summary.argtypes = [C.c_void_p, C.POINTER(_CfkPart)]
+        L.accord_segment_summary_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.accord_segment_carry.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_CfkPart)]
+        L.accord_segment_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        if L.accord_abi_version() != ABI_VERSION:
+            raise ImportError(f"{lib_path}: ABI version {L.accord_abi_version()}, this mirror follows {ABI_VERSION}")
         for name in EXPORTED_SYMBOLS:
             f = getattr(L, name)
             if f.restype is C.c_int:  # default
@@ -873,6 +890,34 @@ class CommandStore:
         self._check(lib().accord_ops_timing(self._h, C.byref(f)))
         return f.value
 
+    # stream segments (config 4; include/accord_deps.h accord_segment_*)
+    def segment_begin(self, seg_base: int):
+        """This (resident) store owns stream positions seg_base.. of every CommandStore: reset, then
+        upload the segment's txns."""
+        self._check(lib().accord_segment_begin(self._h, int(seg_base)))
+
+    def segment_summary(self):
+        """The uploaded segment's CommandsForKey summary in device memory: (n, key_ptr, ent_ptr)."""
+        p = _CfkPart()
+        self._check(lib().accord_segment_summary(self._h, C.byref(p)))
+        return int(p.n), int(p.key or 0), int(p.ent or 0)
+
+    def segment_summary_copy(self, key_ptr: int, ent_ptr: int, cap: int):
+        """Copy the summary into caller device buffers of cap entries each."""
+        self._check(lib().accord_segment_summary_copy(self._h, C.c_void_p(key_ptr), C.c_void_p(ent_ptr), int(cap)))
+
+    def segment_carry(self, parts):
+        """The CommandsForKey state at the segment's start from the summaries [(n, key_ptr, ent_ptr)]
+        of every earlier segment, in stream order (device pointers); compute() then gives the
+        segment's node-level deps."""
+        arr = (_CfkPart * max(1, len(parts)))(*[_CfkPart(int(n), C.c_void_p(k), C.c_void_p(e)) for n, k, e in parts])
+        self._check(lib().accord_segment_carry(self._h, len(parts), arr))
+
+    def segment_timing(self):
+        a, b = C.c_float(), C.c_float()
+        self._check(lib().accord_segment_timing(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def waiting_on_compute(self):
         """WaitingOn bitsets + execution levels of the computed deps (device-resident)."""
         self._check(lib().accord_waiting_on_compute(self._h))
@@ -949,6 +994,42 @@ class CommandStore:
 # ---------------------------------------------------------------- string forms
 _DOMAIN = "KR"
 _KIND = "RWESXL"
+
+
+def segment_bounds(n_total: int, world: int):
+    """Segment r of a stream of n_total txns over `world` ranks: positions [a_r, b_r)."""
+    return [(r * n_total // world, (r + 1) * n_total // world) for r in range(world)]
+
+
+def segment_exchange(store, rank: int, world: int, device, group=None, store_device=None) -> dict:
+    """The config-4 exchange step: every rank's CommandsForKey summary reaches every
+    other rank with one all-gather over torch.distributed (nccl = RCCL over xGMI on the GPU box, gloo
+    on the CPU), and each rank folds the summaries of the segments before its own into the carry
+    (store.segment_carry).  `store` is a CommandStore after segment_begin + upload (or any object with
+    its segment_summary / segment_summary_copy / segment_carry methods); `device` is where the
+    exchange buffers live (the store's device, or the CPU for gloo); store_device, when it differs
+    from `device`, is where the received summaries are staged for the store's carry (a GPU store
+    exchanging over gloo).  Returns the byte counts."""
+    import torch
+    import torch.distributed as dist
+    n = store.segment_summary()[0]
+    mine_n = torch.tensor([n], dtype=torch.int64, device=device)
+    counts = [torch.empty(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(counts, mine_n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(1, max(counts))
+    mine = torch.empty((2, m), dtype=torch.int32, device=device)
+    store.segment_summary_copy(mine[0].data_ptr(), mine[1].data_ptr(), m)
+    gathered = [torch.empty((2, m), dtype=torch.int32, device=device) for _ in range(world)]
+    dist.all_gather(gathered, mine, group=group)
+    if store_device is not None and torch.device(store_device) != torch.device(device):
+        gathered = [g.to(store_device) for g in gathered[:rank]]
+    for d in (device, store_device):
+        if d is not None and torch.device(d).type == "cuda":
+            torch.cuda.synchronize(d)
+    store.segment_carry([(counts[q], gathered[q][0].data_ptr(), gathered[q][1].data_ptr()) for q in range(rank)])
+    return {"summary_entries": counts, "padded_entries": m, "bytes_sent": 8 * m * (world - 1),
+            "bytes_used": 8 * sum(counts[:rank])}
 
 
 def txn_id_str(msb: int, lsb: int, node: int) -> str:

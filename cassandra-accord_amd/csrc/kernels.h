@@ -37,12 +37,19 @@ struct FillDesc {
     uint32_t *p;
     uint32_t words, value;
 };
+// Capacity: the most descriptors any caller adds is 16 fills (the compute's init launch) and 12
+// copies (accord_batch_upload's pack); both lists keep headroom, and an add past the capacity is a
+// programming error that stops the process instead of writing past the array.
+[[noreturn]] void list_capacity_exceeded(const char *what);
 struct FillList {
-    FillDesc d[16];
+    static constexpr uint32_t CAP = 24;
+    FillDesc d[CAP];
     uint32_t nd = 0;
     void add(void *p, size_t bytes, uint32_t value)
     {
-        if (bytes >= 4) d[nd++] = FillDesc{(uint32_t *)p, (uint32_t)(bytes / 4), value};
+        if (bytes < 4) return;
+        if (nd >= CAP) list_capacity_exceeded("FillList");
+        d[nd++] = FillDesc{(uint32_t *)p, (uint32_t)(bytes / 4), value};
     }
 };
 void launch_fill_words(const FillList &L, hipStream_t s);
@@ -53,11 +60,14 @@ struct CopyDesc {
     uint32_t words;
 };
 struct CopyList {
-    CopyDesc d[12];
+    static constexpr uint32_t CAP = 20;
+    CopyDesc d[CAP];
     uint32_t nd = 0;
     void add(const void *src, void *dst, size_t bytes)
     {
-        if (bytes >= 4) d[nd++] = CopyDesc{(const uint32_t *)src, (uint32_t *)dst, (uint32_t)(bytes / 4)};
+        if (bytes < 4) return;
+        if (nd >= CAP) list_capacity_exceeded("CopyList");
+        d[nd++] = CopyDesc{(const uint32_t *)src, (uint32_t *)dst, (uint32_t)(bytes / 4)};
     }
 };
 void launch_copy_words(const CopyList &L, hipStream_t s);

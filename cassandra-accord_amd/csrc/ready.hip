@@ -1496,7 +1496,13 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     constexpr uint32_t PEEK = 1024;            // ready records read back with the count in one copy
     constexpr uint32_t RW = sizeof(ReadyOut) / 4;
     HIPCHECK(s, s->rdy_sum.ensure((size_t)nkeys * sizeof(KeySummary) + 64));
-    HIPCHECK(s, s->rdy_out.ensure(cap * (4 * RW + 4) + 512));   // header, ready records [cap], dropped [cap]
+    {   // header, ready records [cap], dropped [cap]; a reallocation (even at the same address) holds
+        // no zeroed header, so the skip below must not trust the cached pointer after one
+        const size_t out_cap = s->rdy_out.cap;
+        const void *out_p = s->rdy_out.p;
+        HIPCHECK(s, s->rdy_out.ensure(cap * (4 * RW + 4) + 512));
+        if (s->rdy_out.cap != out_cap || s->rdy_out.p != out_p) s->rdy_hdr_zero = nullptr;
+    }
     HIPCHECK(s, s->rdy_spill.ensure(cap * 4 + 64));              // txns left to the removal spill pass
     const uint32_t ngens = (uint32_t)s->rdy_gens.size();
     const uint32_t nl = (ngens + RD_GENS - 1) / RD_GENS;

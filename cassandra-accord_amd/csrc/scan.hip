@@ -25,6 +25,9 @@
 #include "device_common.h"
 #include "kernels.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace accord {
 
 namespace {
@@ -435,6 +438,12 @@ __global__ __launch_bounds__(256) void init_words_kernel(FillList F, CopyList L)
     }
 }
 } // namespace
+
+void list_capacity_exceeded(const char *what)
+{
+    std::fprintf(stderr, "accord_deps: %s capacity exceeded (a build bug: raise its CAP)\n", what);
+    std::abort();
+}
 
 void launch_init_words(const FillList &F, const CopyList &L, hipStream_t s)
 {

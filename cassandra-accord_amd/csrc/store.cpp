@@ -62,6 +62,8 @@ const char *code_name(int32_t c)
 
 extern "C" {
 
+uint32_t accord_abi_version(void) { return ACCORD_ABI_VERSION; }
+
 int32_t accord_store_create(const accord_store_cfg *cfg, accord_store **out)
 {
     if (!cfg || !out) return fail(nullptr, ACCORD_ERR_ARG, "accord_store_create: null argument");
@@ -129,6 +131,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero,
                       &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->rr_ovf, &s->rr_spill, &s->rdy_spill, &s->rdy_spill_mem, &s->up_stage};
     accord_impl::shard_comm_destroy(s);
+    accord_impl::segment_destroy(s);
     accord_impl::ready_destroy(s);
     accord_impl::pinned_arena_destroy(s);
     for (DevBuf *b : bufs) b->release();
@@ -854,6 +857,7 @@ int32_t accord_store_reset(accord_store *s)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     s->next_global = 0; s->carry_n = 0; s->rc_n = 0; s->hist_kinds = 0; s->has_prev = false;
+    s->seg_active = false; s->seg_sum_ok = false; s->seg_base = 0; s->seg_sum_n = 0;
     s->rg_tx_n = 0; s->rg_known = 0; s->rg_flag_ok = false;
     s->prev_msb = s->prev_lsb = 0; s->prev_node = 0;
     s->has_batch = false; s->b_registered = false; s->computed = false; s->merged = false; s->m_pending = false;

@@ -201,7 +201,8 @@ struct accord_store {
     uint32_t rdy_call = 0;                    // accord_ready_update calls (ids of the dirty marks)
     bool rg_flag_zeroed = false;              // the compute's init launch zeroed rg_flag (status_general_count)
     bool rb_status_zeroed = false;            // ... and the RedundantBefore status words (redundant_count)
-        const void *rdy_hdr_zero = nullptr;       // rdy_out whose header the last call left zeroed (rd_host_out_kernel)
+    const void *rdy_hdr_zero = nullptr;       // rdy_out whose header the last call left zeroed (rd_host_out_kernel);
+                                              // reset whenever rdy_out is reallocated
     uint32_t rdy_seen = 0;                    // rg_epoch the last accord_ready_update saw
     uint64_t rdy_sum_version = ~0ull;         // carry version the key summaries belong to
     uint64_t rdy_kseg_version = ~0ull, carry_version = 0;   // the carry's segment bounds are cached per carry version
@@ -227,6 +228,16 @@ struct accord_store {
     std::vector<uint32_t> rdy_list;          // the last accord_ready_update's ready txns
     std::vector<uint64_t> rdy_eal_msb, rdy_eal_lsb;   // and their executesAtLeast
     std::vector<int32_t> rdy_eal_node;
+    // stream segments (segment.hip): the store owns positions [seg_base, seg_base + n) of every
+    // CommandStore; its summary for later segments, and the fold of earlier ones into the carry
+    bool seg_active = false, seg_sum_ok = false;
+    uint32_t seg_base = 0;
+    uint64_t seg_sum_n = 0;
+    float seg_summary_ms = 0, seg_carry_ms = 0;
+    hipEvent_t seg_ev[4] = {};
+    bool seg_ev_created = false;
+    DevBuf sg_lastw, sg_flag, sg_off, sg_ckey, sg_cent, sg_key, sg_ent, sg_tmp0, sg_tmp1, sg_tmp2, sg_tmp3, sg_radix;
+    DevBuf sg_cnt, sg_koff, sg_word;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
     accord_impl::PinnedBlock *dl_arena = nullptr;   // page-locked host arena of accord_deps_download
@@ -243,6 +254,7 @@ struct accord_store {
 namespace accord_impl {
 int32_t fail(accord_store *s, int32_t code, const char *fmt, ...);
 void shard_comm_destroy(accord_store *s);
+void segment_destroy(accord_store *s);      // stream segments' buffers and events (segment.hip)
 int32_t merge_finalize(accord_store *s);   // read a bounded merge's totals (shard.cpp)
 // registered statuses (status.hip)
 bool registered_mode(const accord_store *s);

@@ -47,6 +47,13 @@ extern "C" {
 #define ACCORD_ERR_OOM         -9   /* host or device allocation failed */
 #define ACCORD_ERR_STATE      -10   /* call out of sequence */
 
+/* Version of this ABI: raised on every change of a struct layout or of a result's form that a
+ * binding must follow.  6: KeyDeps txnIds of compute results are gapped (accord_deps.kd_val_cnt,
+ * round 5); stream segments (accord_segment_*).  A binding compares accord_abi_version() with the
+ * value it was written against and refuses to run on a mismatch. */
+#define ACCORD_ABI_VERSION 6u
+uint32_t accord_abi_version(void);
+
 #define ACCORD_STORE_PROFILE   1u   /* record HIP events around every kernel */
 /* The store keeps its CommandsForKey state across batches (CommandStore semantics: every batch
  * continues the store's stream; see accord_store_resident below).  Without it every uploaded
@@ -314,6 +321,44 @@ int32_t accord_comm_size(accord_store *store, int32_t *nranks, int32_t *rank);
 int32_t accord_deps_exchange_merge(accord_store *store, uint32_t n_total);
 int32_t accord_deps_exchange_local(accord_store *const *stores, uint32_t nranks, uint32_t n_total);
 int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merge_ms);
+
+/* ---- multi-GPU by stream segments (config 4) ----
+ * The node's stream of TxnIds is cut into G consecutive segments; rank r owns segment r -- positions
+ * [a_r, b_r) -- of EVERY CommandStore the node hosts and computes the node-level deps of those txns in
+ * full (what PreAccept.reduce would have assembled from the per-store partials, messages/
+ * PreAccept.java:140-156), so no partial deps cross the links.  What a segment needs from before it
+ * is the CommandsForKey state at a_r: per key the entries a txn >= a_r can still reach, i.e. the run
+ * from the last Write before a_r - W on (mapReduceActive's maxCommittedBefore bound,
+ * local/CommandsForKey.java:620-645; earlier entries are pruned for good, as withRedundantBefore
+ * does, :1654-1684).  That state is built on each rank from the small summaries of the earlier
+ * segments (one all-gather):
+ *   accord_segment_begin    resident status-at-time store: reset, the segment starts at stream
+ *                           position seg_base; then accord_batch_upload of the segment (PreAccept
+ *                           batch of key txns, positions seg_base + t);
+ *   accord_segment_summary  per key, the segment's entries from its last Write before b - W on (all
+ *                           of them when it has none): key-major, positions ascending, in device
+ *                           memory owned by the store (valid until the next summary / begin);
+ *                           accord_segment_summary_copy copies them into caller buffers (device,
+ *                           or host memory for an exchange staged through the host);
+ *   accord_segment_carry    the CommandsForKey state at seg_base from the summaries of segments
+ *                           0..r-1 (device memory, stream order): per key, every entry from the
+ *                           newest part back to and including the first Write before seg_base - W.
+ *                           The store then stands at seg_base with that state, and accord_deps_compute
+ *                           gives the segment's deps -- equal to one store computing the whole stream
+ *                           (tests/test_gpu_segments.py).  Calling it again rewinds the store to the
+ *                           segment's start (a bench step is carry + compute).
+ * Every rank's store must cover the same key range; keys in a part are relative to key_lo. */
+typedef struct {
+    uint64_t        n;      /* entries */
+    const uint32_t *key;    /* [n] device: key ordinal - key_lo, ascending */
+    const uint32_t *ent;    /* [n] device: Txn.Kind ordinal << 29 | global stream position, ascending per key */
+} accord_cfk_part;
+int32_t accord_segment_begin(accord_store *store, uint32_t seg_base);
+int32_t accord_segment_summary(accord_store *store, accord_cfk_part *out);
+int32_t accord_segment_summary_copy(accord_store *store, uint32_t *key_dst, uint32_t *ent_dst, uint64_t cap);
+int32_t accord_segment_carry(accord_store *store, uint32_t nparts, const accord_cfk_part *parts);
+/* device ms of the last summary and carry (ACCORD_STORE_PROFILE stores, else 0) */
+int32_t accord_segment_timing(accord_store *store, float *summary_ms, float *carry_ms);
 
 /* ---- deps-set operations on device ----
  * Sources are device views (accord_deps_device_view) of stores on this store's device; the values

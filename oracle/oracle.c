@@ -3156,3 +3156,115 @@ int or_lstore_waiter_debug(const or_lstore *s, uint32_t g, uint64_t *words, uint
     }
     return -1;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Stream segments (multi-GPU ownership by TxnId range)
+ *
+ * Under the status-at-time model a txn i computing its deps on key k starts at maxCommittedBefore
+ * = the last Write j < i - W of the key (local/CommandsForKey.java:620-645): every entry before it
+ * is pruned for good for every later txn (the analogue of withRedundantBefore, :1654-1684).  So
+ * what a txn at position >= thr + W can still reach of a key's history is the run from the last
+ * Write with position < thr on (the whole history when there is none).
+ * ------------------------------------------------------------------------------------------ */
+#define SEG_ENT(kind, pos) (((uint32_t)(kind) << 29) | (uint32_t)(pos))
+
+int or_cfk_reachable(const or_stream *s, uint32_t lo, uint32_t hi, uint32_t thr, uint32_t *n_out,
+                     uint32_t **key_out, uint32_t **ent_out)
+{
+    *n_out = 0; *key_out = NULL; *ent_out = NULL;
+    if (lo > hi || hi > s->n) return -1;
+    uint32_t nkeys = 0;
+    for (uint32_t i = lo; i < hi; ++i)
+        if (domain_of(s->lsb[i]) == 0)
+            for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p)
+                if (s->key_ord[p] + 1 > nkeys) nkeys = s->key_ord[p] + 1;
+    uint32_t *hoff = (uint32_t *)calloc((size_t)nkeys + 1, sizeof(uint32_t));
+    uint32_t *cur = (uint32_t *)malloc(((size_t)nkeys + 1) * sizeof(uint32_t));
+    uint32_t P = s->key_off[hi] - s->key_off[lo];
+    uint32_t *hist = (uint32_t *)malloc((size_t)(P ? P : 1) * sizeof(uint32_t));
+    uint32_t *ok = NULL, *oe = NULL;
+    int rc = -1;
+    if (!hoff || !cur || !hist) goto done;
+    /* the key's history in TxnId (= position) order: a stable counting sort of the pairs */
+    for (uint32_t i = lo; i < hi; ++i)
+        if (domain_of(s->lsb[i]) == 0)
+            for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) hoff[s->key_ord[p] + 1]++;
+    for (uint32_t k = 0; k < nkeys; ++k) hoff[k + 1] += hoff[k];
+    memcpy(cur, hoff, ((size_t)nkeys + 1) * sizeof(uint32_t));
+    for (uint32_t i = lo; i < hi; ++i)
+        if (domain_of(s->lsb[i]) == 0)
+            for (uint32_t p = s->key_off[i]; p < s->key_off[i + 1]; ++p) hist[cur[s->key_ord[p]]++] = i;
+    /* per key: from the last Write before thr on */
+    size_t total = 0;
+    for (uint32_t k = 0; k < nkeys; ++k) {
+        uint32_t a = hoff[k], b = hoff[k + 1], st = a;
+        for (uint32_t e = b; e > a; --e)
+            if (hist[e - 1] < thr && kind_of(s->lsb[hist[e - 1]]) == K_WRITE) { st = e - 1; break; }
+        cur[k] = st;
+        total += b - st;
+    }
+    ok = (uint32_t *)malloc((total ? total : 1) * sizeof(uint32_t));
+    oe = (uint32_t *)malloc((total ? total : 1) * sizeof(uint32_t));
+    if (!ok || !oe) goto done;
+    size_t w = 0;
+    for (uint32_t k = 0; k < nkeys; ++k)
+        for (uint32_t e = cur[k]; e < hoff[k + 1]; ++e) {
+            ok[w] = k;
+            oe[w] = SEG_ENT(kind_of(s->lsb[hist[e]]), hist[e]);
+            ++w;
+        }
+    *n_out = (uint32_t)total; *key_out = ok; *ent_out = oe;
+    ok = oe = NULL;
+    rc = 0;
+done:
+    free(hoff); free(cur); free(hist); free(ok); free(oe);
+    return rc;
+}
+
+/* The reachable entries at the start of segment r (thr = a_r - W) from the reachable summaries of
+ * segments 0..r-1 in stream order (part q = or_cfk_reachable over [a_q, b_q) with thr b_q - W).
+ * A later segment's summary keeps every entry a later txn can reach of its own txns; when it holds
+ * no Write before thr on a key, the key's run continues into the segments before it.  So, per key,
+ * walk back from the newest part, keeping every entry, up to and including the first Write with
+ * position < thr. */
+int or_cfk_fold(uint32_t nparts, const uint32_t *part_n, const uint32_t *const *keys, const uint32_t *const *ents,
+                uint32_t thr, uint32_t *n_out, uint32_t **key_out, uint32_t **ent_out)
+{
+    *n_out = 0; *key_out = NULL; *ent_out = NULL;
+    uint32_t nkeys = 0;
+    size_t cap = 0;
+    for (uint32_t q = 0; q < nparts; ++q) {
+        cap += part_n[q];
+        for (uint32_t j = 0; j < part_n[q]; ++j) {
+            if (j && keys[q][j] < keys[q][j - 1]) return -1;     /* parts are key-major */
+            if (keys[q][j] + 1 > nkeys) nkeys = keys[q][j] + 1;
+        }
+    }
+    uint32_t *ok = (uint32_t *)malloc((cap ? cap : 1) * sizeof(uint32_t));
+    uint32_t *oe = (uint32_t *)malloc((cap ? cap : 1) * sizeof(uint32_t));
+    uint32_t *pos = (uint32_t *)calloc((size_t)nparts + 1, sizeof(uint32_t));   /* cursor per part */
+    uint32_t *tmp = (uint32_t *)malloc((cap ? cap : 1) * sizeof(uint32_t));
+    if (!ok || !oe || !pos || !tmp) { free(ok); free(oe); free(pos); free(tmp); return -1; }
+    size_t w = 0;
+    for (uint32_t k = 0; k < nkeys; ++k) {
+        size_t m = 0;                         /* the key's kept entries, newest first */
+        int done = 0;
+        for (uint32_t q = nparts; q-- > 0 && !done;) {
+            uint32_t a = pos[q], b = a;
+            while (b < part_n[q] && keys[q][b] == k) ++b;
+            for (uint32_t e = b; e > a; --e) {
+                uint32_t x = ents[q][e - 1];
+                tmp[m++] = x;
+                if ((x >> 29) == K_WRITE && (x & 0x1FFFFFFFu) < thr) { done = 1; break; }
+            }
+        }
+        for (uint32_t q = 0; q < nparts; ++q)
+            while (pos[q] < part_n[q] && keys[q][pos[q]] == k) ++pos[q];
+        for (size_t e = m; e > 0; --e) { ok[w] = k; oe[w] = tmp[e - 1]; ++w; }
+    }
+    free(pos); free(tmp);
+    *n_out = (uint32_t)w; *key_out = ok; *ent_out = oe;
+    return 0;
+}
+
+void or_free(void *p) { free(p); }

@@ -223,6 +223,23 @@ int or_deps_slice(const or_deps *d, const uint32_t *sel_off, const uint32_t *sel
 /* RelationMultiMap.invert of keysToTxnIds (range 0) / rangesToTxnIds (range 1) of every txn */
 int or_deps_invert(const or_deps *d, int range, uint32_t *off /* [n+1] */, int32_t **out /* malloc'd */);
 
+/* ---- stream segments (multi-GPU ownership by TxnId range) ----
+ * or_cfk_reachable: per key, the CommandsForKey entries of txns [lo, hi) that a txn at position
+ * >= thr + W can still reach under the status-at-time model -- the run from the last Write with
+ * position < thr on, or the key's whole run when it has none (mapReduceActive's maxCommittedBefore
+ * bound, local/CommandsForKey.java:620-645).  Key-domain txns' entries (EphemeralReads included, as
+ * the device history keeps them; no kind witnesses them).  Key-major, positions ascending:
+ * key[] absolute ordinals, ent[] = kind << 29 | position.  A segment's summary is
+ * or_cfk_reachable(s, a, b, b - W); the CommandsForKey state at the start of segment r is
+ * or_cfk_reachable(s, 0, a_r, a_r - W).
+ * or_cfk_fold: that state from the summaries of segments 0..r-1 (stream order) with thr = a_r - W.
+ * Outputs malloc'd (or_free). */
+int or_cfk_reachable(const or_stream *s, uint32_t lo, uint32_t hi, uint32_t thr, uint32_t *n_out,
+                     uint32_t **key, uint32_t **ent);
+int or_cfk_fold(uint32_t nparts, const uint32_t *part_n, const uint32_t *const *keys, const uint32_t *const *ents,
+                uint32_t thr, uint32_t *n_out, uint32_t **key, uint32_t **ent);
+void or_free(void *p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -76,6 +76,12 @@ def lib():
         L.or_deps_invert.argtypes = [C.POINTER(_OrDeps), C.c_int, _u32p, C.POINTER(_i32p)]
         L.or_redundant_collect.argtypes = [C.POINTER(_OrStream), C.c_uint32, _u32p, _u32p, _u64p, _u64p, _u32p,
                                            C.c_uint64, C.POINTER(_OrDeps)]
+        L.or_cfk_reachable.argtypes = [C.POINTER(_OrStream), C.c_uint32, C.c_uint32, C.c_uint32, _u32p,
+                                       C.POINTER(_u32p), C.POINTER(_u32p)]
+        L.or_cfk_fold.argtypes = [C.c_uint32, _u32p, C.POINTER(_u32p), C.POINTER(_u32p), C.c_uint32, _u32p,
+                                  C.POINTER(_u32p), C.POINTER(_u32p)]
+        L.or_free.argtypes = [C.c_void_p]
+        L.or_free.restype = None
         _LIB = L
     return _LIB
 
@@ -187,6 +193,42 @@ def deps_fast(s: Stream, window: int, batch_end=None, applied_before=None, floor
         return _to_partial(d)
     finally:
         lib().or_deps_free(C.byref(d))
+
+
+def _take_entries(n, kp, ep):
+    try:
+        return _arr(kp, n.value, np.uint32), _arr(ep, n.value, np.uint32)
+    finally:
+        lib().or_free(C.cast(kp, C.c_void_p))
+        lib().or_free(C.cast(ep, C.c_void_p))
+
+
+def cfk_reachable(s: Stream, lo: int, hi: int, thr: int):
+    """or_cfk_reachable: per key, the CommandsForKey entries of txns [lo, hi) a txn at position
+    >= thr + W can still reach -- (key[], ent[] = kind << 29 | position), key-major.  A segment's
+    summary is cfk_reachable(s, a, b, b - W); the state at the start of segment r is
+    cfk_reachable(s, 0, a_r, a_r - W)."""
+    o, keep = _or_stream(s, 0)
+    n, kp, ep = C.c_uint32(), _u32p(), _u32p()
+    rc = lib().or_cfk_reachable(C.byref(o), lo, hi, max(0, thr), C.byref(n), C.byref(kp), C.byref(ep))
+    if rc != 0:
+        raise OracleError(rc)
+    return _take_entries(n, kp, ep)
+
+
+def cfk_fold(parts, thr: int):
+    """or_cfk_fold: the state at the start of a segment (thr = its first position - W) from the
+    summaries [(key[], ent[]), ...] of every earlier segment, in stream order."""
+    keep = [(np.ascontiguousarray(k, np.uint32), np.ascontiguousarray(e, np.uint32)) for k, e in parts]
+    G = len(keep)
+    pn = np.array([k.size for k, _ in keep], np.uint32)
+    kt = (_u32p * max(G, 1))(*[k.ctypes.data_as(_u32p) for k, _ in keep])
+    et = (_u32p * max(G, 1))(*[e.ctypes.data_as(_u32p) for _, e in keep])
+    n, kp, ep = C.c_uint32(), _u32p(), _u32p()
+    rc = lib().or_cfk_fold(G, pn.ctypes.data_as(_u32p), kt, et, max(0, thr), C.byref(n), C.byref(kp), C.byref(ep))
+    if rc != 0:
+        raise OracleError(rc)
+    return _take_entries(n, kp, ep)
 
 
 KEY_END = 0xFFFFFFFF     # an open upper store bound (include/accord_deps.h ACCORD_KEY_END)
