@@ -44,6 +44,7 @@ WINDOW_NONE = 0xFFFFFFFF     # no status-at-time model: statuses from CommandSto
 KEY_END = 0xFFFFFFFF         # an open upper store bound (accord_store_cfg.store_bounds)
 READY_POLL, READY_EVENTS = 0, 1   # accord_ready_set_mode
 ST_ERASED = 8                # register(): SaveStatus Erased / Invalidated (range commands leave the range scan)
+ST_TRUNCATED_APPLY = 9       # register(): SaveStatus TruncatedApply* (INVALID for CFK, executeAt known)
 
 EXPORTED_SYMBOLS = [
     "accord_store_create", "accord_store_destroy", "accord_last_error", "accord_store_stream",

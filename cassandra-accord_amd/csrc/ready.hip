@@ -280,6 +280,8 @@ struct ReadyParams {
     // appliedOrInvalidated (positions), per position pv_at = 1 + pool start (0: none), pv_len
     uint32_t *pv_at, *pv_len, *pv_pool, *pv_cnt;
     uint32_t evmode;                  // event-exact mode: key bits clear on events only (rd_event_kernel)
+    uint32_t *inv;                    // 1 + the position of a waiter whose TruncatedApply dep breaks
+                                      // updateWaitingOn's checkState (local/Commands.java:789-791); 0 = none
 };
 
 // the TxnId of global position g (the store's TxnId table is in stream order)
@@ -551,10 +553,11 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, ui
                     const unsigned long long bit = 1ull << (j & 63u), wq = p.words[w0 + q];
                     if (!(wq & bit)) continue;
                     const uint32_t d = rv[j], ds = status_of(p.v, d);
-                    if (only_deps && ds >= ST_COMMITTED && ds <= ST_APPLIED) {   // updateExecuteAtLeast
+                    if (only_deps && exec_known(ds)) {                           // updateExecuteAtLeast
                         const Ts de = exec_of(p.v, d);
                         if (tcmp(de, own) > 0) cand(de);
                     }
+                    if (ds == ST_TRUNC_APPLY && !only_deps && tcmp(exec_of(p.v, d), ex) >= 0) *p.inv = g + 1u;
                     if (ds < ST_COMMITTED) continue;                           // !hasBeen(PreCommitted)
                     bool clr = false, app = false;
                     if (ds >= ST_INVALID) clr = app = true;
@@ -590,10 +593,12 @@ __device__ __forceinline__ void rd_eval_txn(const ReadyParams &p, uint32_t u, ui
             if (b < R + K && ((old >> lane) & 1ull) && !(seqr && b < R) && !(p.evmode && b >= R)) {
                 if (b < R) {                                             // range-dep bit
                     const uint32_t d = p.rd_vals[p.rd_off[t] + b], ds = status_of(p.v, d);
-                    if (only_deps && ds >= ST_COMMITTED && ds <= ST_APPLIED) {   // updateExecuteAtLeast
+                    if (only_deps && exec_known(ds)) {                           // updateExecuteAtLeast
                         const Ts de = exec_of(p.v, d);
                         if (tcmp(de, own) > 0) cand(de);
                     }
+                    // Invariants.checkState(executeAt < waitingExecuteAt || awaitsOnlyDeps) (:789-791)
+                    if (ds == ST_TRUNC_APPLY && !only_deps && tcmp(exec_of(p.v, d), ex) >= 0) *p.inv = g + 1u;
                     if (ds >= ST_COMMITTED) {                            // hasBeen(PreCommitted)
                         if (ds >= ST_INVALID) clear = applied = true;
                         else if (!only_deps && tcmp(exec_of(p.v, d), ex) > 0) clear = true;
@@ -1009,7 +1014,9 @@ __global__ __launch_bounds__(64) void rd_event_kernel(EvCtx c)
                 c.st[g] = (uint8_t)nw;
                 c.chg[g] = c.epoch;
                 if (cur < ST_COMMITTED && nw >= ST_COMMITTED) c.cchg[g] = c.epoch;
-                if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) { c.xmsb[g] = c.emsb[r]; c.xlsb[g] = c.elsb[r]; c.xnode[g] = c.enode[r]; }
+                if ((nw >= ST_ACCEPTED && nw <= ST_APPLIED) || nw == ST_TRUNC_APPLY) {
+                    c.xmsb[g] = c.emsb[r]; c.xlsb[g] = c.elsb[r]; c.xnode[g] = c.enode[r];
+                }
             }
             __threadfence();
             uint32_t gi, t;
@@ -1020,8 +1027,8 @@ __global__ __launch_bounds__(64) void rd_event_kernel(EvCtx c)
                 if ((p.lsb[t] & 1u) != 0 || kind == 2u) ev_register_unmanaged(c, gi, t, lane);   // unmanaged
                 __threadfence();
             }
-            // CommandsForKey.update on every key (Erased leaves it as INVALID_OR_TRUNCATED)
-            const uint32_t cs = nw >= ST_ERASED ? ST_INVALID : nw, ps = cur >= ST_ERASED ? ST_INVALID : cur;
+            // CommandsForKey.update on every key (TruncatedApply and Erased leave it as INVALID_OR_TRUNCATED)
+            const uint32_t cs = nw >= ST_INVALID ? ST_INVALID : nw, ps = cur >= ST_INVALID ? ST_INVALID : cur;
             ev_txn_keys(c, g, ps, cs, exec_of(c.v, g), lane);
         }
     } else if (MODE == 1) {
@@ -1578,6 +1585,7 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
         p.evmode = s->rdy_event_mode ? 1u : 0u;
         p.out = list; p.out_cnt = cnt;
         p.drop = drop; p.drop_cnt = cnt + (HDR - 1);
+        p.inv = cnt + (HDR - 6);
         p.rbx = s->rb_ext && s->rb_m ? 1u : 0u;
         p.M = rr_map_of(s);
         p.pkoff = r->pkoff.as<uint32_t>(); p.pkeys = r->pkeys.as<uint32_t>();
@@ -1668,6 +1676,9 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     }
     const uint32_t nr = peek[0], nd = peek[HDR - 1];
     if (pv_on) s->rdy_pv_n = peek[HDR - 5];
+    if (peek[HDR - 6])
+        return fail(s, ACCORD_ERR_STATE, "Invariants.checkState: txn %u waits on a TruncatedApply dep executing at or "
+                    "after it (local/Commands.java:789-791)", peek[HDR - 6] - 1u);
     if (s->rdy_stats) {                          // ACCORD_READY_STATS: diagnostic totals (ready_destroy prints)
         s->rdy_stats[0] += 1; s->rdy_stats[1] += peek[1]; s->rdy_stats[2] += cap;
         if (any_inc && tabs.size() <= HDR - 8)

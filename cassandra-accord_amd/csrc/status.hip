@@ -500,7 +500,7 @@ __global__ __launch_bounds__(256) void reg_check_kernel(RegParams p, uint32_t st
         if (r > 0 && ts_cmp(p.msb[r - 1], p.lsb[r - 1], p.node[r - 1], id.msb, id.lsb, id.node) >= 0)
             record_error(p.err, r, ACCORD_ERR_UNSORTED);
         const uint32_t nw = p.status[r];
-        if (nw > ST_ERASED) { record_error(p.err, r, ACCORD_ERR_ARG); continue; }
+        if (nw > ST_TRUNC_APPLY) { record_error(p.err, r, ACCORD_ERR_ARG); continue; }
         uint32_t J = 0, jh = ns;                      // samples below id
         while (J < jh) {
             const uint32_t m = (J + jh) >> 1;
@@ -519,8 +519,8 @@ __global__ __launch_bounds__(256) void reg_check_kernel(RegParams p, uint32_t st
         const uint32_t g = p.tg[lo];
         p.pos[r] = g;
         const uint32_t cur = p.st[g];
-        if (nw < cur) { record_error(p.err, r, ACCORD_ERR_STATE); continue; }   // statuses never go back
-        if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) {
+        if (status_rank(nw) < status_rank(cur)) { record_error(p.err, r, ACCORD_ERR_STATE); continue; }   // never back
+        if ((nw >= ST_ACCEPTED && nw <= ST_APPLIED) || nw == ST_TRUNC_APPLY) {
             const Ts ex{p.emsb[r], p.elsb[r], p.enode[r]};
             if (ts_cmp(ex.msb, ex.lsb, ex.node, id.msb, id.lsb, id.node) < 0) record_error(p.err, r, ACCORD_ERR_ARG);
             if (committed(cur) && (ex.msb != p.xmsb[g] || ex.lsb != p.xlsb[g] || ex.node != p.xnode[g]))
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(256) void reg_erase_ranges_kernel(RegParams p, uint
                                                                uint32_t *__restrict__ rc_kind)
 {
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += gridDim.x * blockDim.x) {
-        if (p.status[r] < ST_ERASED || !(p.lsb[r] & 1ull)) continue;
+        if (p.status[r] != ST_ERASED || !(p.lsb[r] & 1ull)) continue;
         const uint32_t g = p.pos[r];
         uint32_t lo = 0, hi = rc_n;
         while (lo < hi) {
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(256) void reg_apply_kernel(RegParams p)
         p.st[g] = (uint8_t)nw;
         p.chg[g] = p.epoch;                 // readiness re-evaluates the keys of changed txns
         if (cur < ST_COMMITTED && nw >= ST_COMMITTED) p.cchg[g] = p.epoch;
-        if (nw >= ST_ACCEPTED && nw <= ST_APPLIED) { p.xmsb[g] = p.emsb[r]; p.xlsb[g] = p.elsb[r]; p.xnode[g] = p.enode[r]; }
+        if ((nw >= ST_ACCEPTED && nw <= ST_APPLIED) || nw == ST_TRUNC_APPLY) { p.xmsb[g] = p.emsb[r]; p.xlsb[g] = p.elsb[r]; p.xnode[g] = p.enode[r]; }
     }
 }
 
@@ -746,7 +746,8 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
                                                       unsigned long long *__restrict__ words,
                                                       unsigned long long *__restrict__ aoi, bool pre, EalRec *__restrict__ eal,
                                                       const uint32_t *__restrict__ pv_at, const uint32_t *__restrict__ pv_len,
-                                                      const uint32_t *__restrict__ pv_pool, uint32_t pv_pos)
+                                                      const uint32_t *__restrict__ pv_pool, uint32_t pv_pos,
+                                                      accord::DevStatus *__restrict__ err)
 {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t g = txn_index[t], ost = status_of(v, g);
@@ -786,10 +787,11 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
                 const unsigned long long bit = 1ull << (j & 63u), wq = words[w0 + q];
                 if (!(wq & bit)) continue;
                 const uint32_t d = rd_vals[r0 + j], st = status_of(v, d);
-                if (only_deps && st >= ST_COMMITTED && st <= ST_APPLIED) {   // updateExecuteAtLeast
+                if (only_deps && exec_known(st)) {                            // updateExecuteAtLeast
                     const Ts de = exec_of(v, d);
                     if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0) eal_merge(ea, EalRec{de.msb, de.lsb, de.node, 1u});
                 }
+                if (st == ST_TRUNC_APPLY && !only_deps && tcmp(exec_of(v, d), own) >= 0) trunc_check_fail(err, t);
                 if (st < ST_COMMITTED) continue;
                 bool clr = false, app = false;
                 if (st >= ST_INVALID) clr = app = true;
@@ -824,10 +826,12 @@ __global__ __launch_bounds__(256) void wo_init_kernel(uint32_t n, const uint64_t
                 if (!(kept & bit)) continue;                    // removed: not waited on, not visited
                 const uint32_t d = rd_vals[r0 + b], st = status_of(v, d);
                 bool wait = true, applied = false;
-                if (only_deps && st >= ST_COMMITTED && st <= ST_APPLIED) {   // updateExecuteAtLeast
+                if (only_deps && exec_known(st)) {                            // updateExecuteAtLeast
                     const Ts de = exec_of(v, d);
                     if (ts_cmp(de.msb, de.lsb, de.node, msb[t], l, node[t]) > 0) eal_merge(ea, EalRec{de.msb, de.lsb, de.node, 1u});
                 }
+                // Invariants.checkState(executeAt < waitingExecuteAt || awaitsOnlyDeps) (:789-791)
+                if (st == ST_TRUNC_APPLY && !only_deps && tcmp(exec_of(v, d), own) >= 0) trunc_check_fail(err, t);
                 if (st >= ST_COMMITTED) {                       // hasBeen(PreCommitted)
                     if (st >= ST_INVALID) { wait = false; applied = true; }                 // truncated / invalidated
                     else if (!only_deps && tcmp(exec_of(v, d), own) > 0) wait = false;     // executes after us
@@ -942,12 +946,22 @@ int32_t status_waiting_on_init(accord_store *s, const uint32_t *wo_off, unsigned
             launch(true, blocks, s->rr_spill.p, h[1], h[2]);
         }
     }
+    HIPCHECK(s, s->wo_err.ensure(sizeof(HostTotals)));
+    HostTotals *err = s->wo_err.as<HostTotals>();
+    HIPCHECK(s, hipMemsetAsync(&err->status, 0xFF, sizeof(unsigned long long), s->stream));
     hipLaunchKernelGGL(wo_init_kernel, dim3(grid_for(n)), dim3(256), 0, s->stream, n, s->msb.as<uint64_t>(),
                        s->lsb.as<uint64_t>(), s->node.as<int32_t>(), s->txn_index.as<uint32_t>(),
                        cd.kd_key_off, cd.rd_val_off, cd.rd_vals, wo_off, view_of(s), words, aoi, pre,
                        s->wo_eal.as<EalRec>(), s->rdy_pv_at.as<uint32_t>(), s->rdy_pv_len.as<uint32_t>(),
                        s->rdy_pv_pool.as<uint32_t>(),
-                       (uint32_t)std::min<size_t>(s->rdy_pv_pos, std::min(s->rdy_pv_at.cap, s->rdy_pv_len.cap) / 4));
+                       (uint32_t)std::min<size_t>(s->rdy_pv_pos, std::min(s->rdy_pv_at.cap, s->rdy_pv_len.cap) / 4),
+                       &err->status);
+    HIPCHECK(s, hipMemcpyAsync(&s->pinned->reg_status, &err->status, sizeof(accord::DevStatus), hipMemcpyDeviceToHost,
+                               s->stream));
+    HIPCHECK(s, hipStreamSynchronize(s->stream));
+    if (s->pinned->reg_status.first != ~0ull)
+        return fail(s, ACCORD_ERR_STATE, "Invariants.checkState: txn %u waits on a TruncatedApply dep executing at or "
+                    "after it (local/Commands.java:789-791)", (uint32_t)(s->pinned->reg_status.first >> 32));
     return ACCORD_OK;
 }
 
@@ -1202,8 +1216,8 @@ extern "C" int32_t accord_txn_register(accord_store *s, uint32_t n, const uint64
     if (!msb || !lsb || !node || !status) return fail(s, ACCORD_ERR_ARG, "accord_txn_register: null argument");
     bool need_exec = false;
     for (uint32_t r = 0; r < n; ++r) {
-        if (status[r] > ST_ERASED) return fail(s, ACCORD_ERR_ARG, "event %u: status ordinal %u", r, status[r]);
-        need_exec |= status[r] >= ST_ACCEPTED && status[r] <= ST_APPLIED;
+        if (status[r] > ST_TRUNC_APPLY) return fail(s, ACCORD_ERR_ARG, "event %u: status ordinal %u", r, status[r]);
+        need_exec |= (status[r] >= ST_ACCEPTED && status[r] <= ST_APPLIED) || status[r] == ST_TRUNC_APPLY;
     }
     if (need_exec && (!exec_msb || !exec_lsb || !exec_node))
         return fail(s, ACCORD_ERR_ARG, "ACCEPTED..APPLIED events need an executeAt");

@@ -129,7 +129,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,
                       &s->rc_end2, &s->rc_kind2, &s->rc_first, &s->rc_flag, &s->rc_offs, &s->rdy_kseg0, &s->rdy_kseg1, &s->rdy_dirty, &s->rdy_dirty2, &s->rg_cchg, &s->rdy_dlist, &s->rdy_work, &s->rdy_wcnt, &s->rg_chg, &s->rdy_part, &s->rdy_sum, &s->rdy_out, &s->rdy_kb, &s->rdy_launch,
                       &s->bk_list, &s->bk_wex, &s->rb_start, &s->rb_end, &s->rb_bound, &s->rb_sep, &s->rb_eep, &s->rb_cnt, &s->rb_zero,
-                      &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->rr_ovf, &s->rr_spill, &s->rdy_spill, &s->rdy_spill_mem, &s->up_stage};
+                      &s->rb_local, &s->rb_boot, &s->rb_stale, &s->wo_eal, &s->wo_err, &s->rr_ovf, &s->rr_spill, &s->rdy_spill, &s->rdy_spill_mem, &s->up_stage};
     accord_impl::shard_comm_destroy(s);
     accord_impl::segment_destroy(s);
     accord_impl::ready_destroy(s);

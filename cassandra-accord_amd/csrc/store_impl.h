@@ -177,6 +177,7 @@ struct accord_store {
     DevBuf rb_local, rb_boot, rb_stale;
     bool rb_ext = false;
     DevBuf wo_eal;                 // WaitingOn.executeAtLeast per txn of the initialised batch (EalRec)
+    DevBuf wo_err;                 // accord_waiting_on_initialise's invariant check (a HostTotals' status word)
     DevBuf rr_ovf;                 // removal kernels: spill header (count, max range deps, max entries) + list
     DevBuf rr_spill;               // removal kernels: HBM scratch of the spill pass
     // execution readiness (ready.hip): the waiting set, one generation per initialised batch

@@ -204,6 +204,15 @@ void       *accord_store_stream(accord_store *store);        /* the store's hipS
  * impl/InMemoryCommandStore.java:891).  A range command at INVALID_OR_TRUNCATED (ErasedOrInvalidated,
  * Truncated*: before Erased in SaveStatus order, :80-85) is still visited. */
 #define ACCORD_ST_ERASED             8
+/* SaveStatus TruncatedApply / TruncatedApplyWithOutcome / TruncatedApplyWithDeps (local/SaveStatus.java:
+ * 79-81): INVALID_OR_TRUNCATED for CommandsForKey (InternalStatus.convert, local/CommandsForKey.java:
+ * 222-224) and still visited by the range-command scan (before Erased), but its executeAt is known
+ * (ExecuteAtKnown) and the event carries it: Commands.updateWaitingOn feeds it to an awaitsOnlyDeps
+ * waiter's updateExecuteAtLeast before taking the truncation branch (local/Commands.java:782-783), and
+ * checks executeAt < the waiter's executeAt for every other waiter (:789-791; a violation fails
+ * accord_waiting_on_initialise / accord_ready_update with ACCORD_ERR_STATE).  Statuses advance in
+ * SaveStatus order: ... APPLIED < TRUNCATED_APPLY < INVALID_OR_TRUNCATED < ERASED. */
+#define ACCORD_ST_TRUNCATED_APPLY    9
 int32_t accord_txn_register(accord_store *store, uint32_t n, const uint64_t *msb, const uint64_t *lsb,
                             const int32_t *node, const uint8_t *status, const uint64_t *exec_msb,
                             const uint64_t *exec_lsb, const int32_t *exec_node);
@@ -532,8 +541,9 @@ int32_t accord_waiting_on_initialise(accord_store *store);
  *                    updateWaitingOn's removeRedundantDependencies step (see there) to the range deps;
  *   executeAtLeast   awaitsOnlyDeps kinds (ExclusiveSyncPoint, EphemeralRead): WaitingOn.updateExecuteAtLeast
  *                    (local/Command.java:1511-1514) with the executeAt of every range dep visited while
- *                    committed with a known executeAt after the txn's TxnId (local/Commands.java:782-783;
- *                    an INVALID_OR_TRUNCATED / ERASED event carries none), and of the dep executing last
+ *                    committed or TruncatedApply with a known executeAt after the txn's TxnId
+ *                    (local/Commands.java:782-783; an INVALID_OR_TRUNCATED / ERASED event carries none), and
+ *                    of the dep executing last
  *                    when registerUnmanaged / updatePending leave an APPLY record (local/CommandsForKey.java:
  *                    1370-1380, 1470-1478).
  * The reference evaluates the key tests when an event reaches the key (notifyAndUpdatePending,

@@ -2098,6 +2098,13 @@ static int lstore_reserve_ranges(or_lstore *s, uint32_t nr)
 }
 
 #define S_ERASED 8             /* SaveStatus >= Erased (Erased, Invalidated): local/SaveStatus.java:83-87 */
+/* SaveStatus TruncatedApply* (local/SaveStatus.java:79-81): INVALID_OR_TRUNCATED in CommandsForKey
+ * (InternalStatus.convert, local/CommandsForKey.java:222-224), before Erased (still visited by the
+ * range scan), with a known executeAt (updateWaitingOn's updateExecuteAtLeast, local/Commands.java:782) */
+#define S_TRUNC_APPLY 9
+/* the order statuses advance in: ... Applied < TruncatedApply < ErasedOrInvalidated / Invalidated <
+ * Erased (SaveStatus order) */
+static int status_rank(int st) { return st == S_TRUNC_APPLY ? 13 : 2 * st; }
 
 /* mapReduceRangesInternal (impl/InMemoryCommandStore.java:883-1016) over the store's range commands
  * [0, reg): skip SaveStatus >= Erased (:891; ErasedOrInvalidated is before Erased and still visited),
@@ -2112,7 +2119,7 @@ static int lstore_range_scan(const or_lstore *s, const or_stream *b, uint32_t i,
     int rc = -1;
     for (uint32_t g = 0; g < reg; ++g) {
         if (s->roff[g + 1] == s->roff[g]) continue;                          /* not a range command */
-        if (s->status[g] >= S_ERASED) continue;
+        if (s->status[g] == S_ERASED) continue;
         if (ts_cmp(&s->tbl[g], sb) >= 0) continue;
         if (p1 >= 0 && (uint32_t)p1 == g) continue;
         if (!kinds_test(test_kinds, kind_of(s->tbl[g].lsb))) continue;
@@ -2240,7 +2247,7 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
     if (!pos) return -1;
     for (uint32_t r = 0; r < n; ++r) {                 /* validate everything before changing anything */
         if (r && or_ts_compare(msb[r - 1], lsb[r - 1], node[r - 1], msb[r], lsb[r], node[r]) >= 0) { free(pos); return -2; }
-        if (status[r] > S_ERASED) { free(pos); return -1; }
+        if (status[r] > S_TRUNC_APPLY) { free(pos); return -1; }
         uint32_t lo = 0, hi = s->n;
         while (lo < hi) {
             uint32_t m = (lo + hi) / 2;
@@ -2249,8 +2256,8 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
         if (lo >= s->n || !or_ts_equals(s->tbl[lo].msb, s->tbl[lo].lsb, s->tbl[lo].node, msb[r], lsb[r], node[r])) { free(pos); return -1; }
         const uint32_t g = lo;
         const uint8_t cur = s->status[g], nw = status[r];
-        if (nw < cur) { free(pos); return -10; }
-        const int has_info = nw >= S_ACCEPTED && nw <= S_APPLIED;
+        if (status_rank(nw) < status_rank(cur)) { free(pos); return -10; }
+        const int has_info = (nw >= S_ACCEPTED && nw <= S_APPLIED) || nw == S_TRUNC_APPLY;
         if (has_info) {
             if (!emsb) { free(pos); return -1; }
             if (or_ts_compare(emsb[r], elsb[r], enode[r], s->tbl[g].msb, s->tbl[g].lsb, s->tbl[g].node) < 0) { free(pos); return -1; }
@@ -2264,7 +2271,7 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
     for (uint32_t r = 0; r < n; ++r) {
         const uint32_t g = pos[r];
         const uint8_t nw = status[r];
-        const int has_info = nw >= S_ACCEPTED && nw <= S_APPLIED;
+        const int has_info = (nw >= S_ACCEPTED && nw <= S_APPLIED) || nw == S_TRUNC_APPLY;
         ts_t ex = s->exec[g];
         if (has_info) { ex.msb = emsb[r]; ex.lsb = elsb[r]; ex.node = enode[r]; }
         const uint8_t was = s->status[g];
@@ -2276,8 +2283,8 @@ int or_lstore_register(or_lstore *s, uint32_t n, const uint64_t *msb, const uint
         }
         if (is_globally_visible(kind_of(s->tbl[g].lsb)) != 1) continue;   /* never inserted into CFK */
         if (domain_of(s->tbl[g].lsb) != 0) continue;                       /* range command: status only */
-        /* Erased / Invalidated leave CommandsForKey as INVALID_OR_TRUNCATED does */
-        const uint8_t cs = nw >= S_ERASED ? (uint8_t)S_INVALID_OR_TRUNCATED : nw;
+        /* TruncatedApply, Erased and Invalidated leave CommandsForKey as INVALID_OR_TRUNCATED does */
+        const uint8_t cs = nw >= S_INVALID_OR_TRUNCATED ? (uint8_t)S_INVALID_OR_TRUNCATED : nw;
         for (uint32_t p = s->koff[g]; p < s->koff[g + 1]; ++p) {
             cfk_t *c = &s->cfks[s->kord[p]];
             if (g < c->redundant_before) continue;       /* truncated from this key */
@@ -2924,9 +2931,13 @@ int or_lstore_ready_ex(or_lstore *s, uint32_t *ready_out, uint32_t *nready, uint
             const uint32_t dg = x->rdeps[j];
             const uint8_t ds = s->status[dg];
             if (ds < S_COMMITTED) continue;                     /* !hasBeen(PreCommitted) */
-            /* updateExecuteAtLeast (:782-783): a dep with a known executeAt after the waiter's TxnId;
-             * an INVALID_OR_TRUNCATED event carries no executeAt */
-            if (only_deps && ds <= S_APPLIED && ts_cmp(&s->exec[dg], &s->tbl[g]) > 0) eal_merge(x, &s->exec[dg]);
+            /* updateExecuteAtLeast (:782-783): a dep with a known executeAt after the waiter's TxnId --
+             * committed, or TruncatedApply (ExecuteAtKnown); an ErasedOrInvalidated / Erased /
+             * Invalidated event carries none */
+            const int exec_known = ds <= S_APPLIED || ds == S_TRUNC_APPLY;
+            if (only_deps && exec_known && ts_cmp(&s->exec[dg], &s->tbl[g]) > 0) eal_merge(x, &s->exec[dg]);
+            /* TruncatedApply: Invariants.checkState(executeAt < waitingExecuteAt || awaitsOnlyDeps) (:789-791) */
+            if (ds == S_TRUNC_APPLY && !only_deps && ts_cmp(&s->exec[dg], ex) >= 0) return -10;
             if (ds >= S_INVALID_OR_TRUNCATED) { w_clear(x->words, j); if (rdom) x->aoi[j / 64] |= 1ULL << (j & 63); }
             else if (!only_deps && ts_cmp(&s->exec[dg], ex) > 0) w_clear(x->words, j);
             else if (ds == S_APPLIED) {                     /* setAppliedAndPropagate */

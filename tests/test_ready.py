@@ -448,6 +448,69 @@ def test_propagate_kat_oracle():
     prop_kat_run()
 
 
+# TruncatedApply carries its executeAt (ACCORD_ST_TRUNCATED_APPLY; local/SaveStatus.java:79-81): t0, a
+# range Write over (0,2] committed at hlc 30, is TruncatedApply when t1 -- an ExclusiveSyncPoint over
+# (0,2], awaitsOnlyDeps -- initialises its WaitingOn.  updateWaitingOn reads ExecuteAtKnown before the
+# truncation branch (local/Commands.java:782-783), so t1 executes at least at t0's executeAt and its
+# bit clears as applied-or-invalidated; with t0 Erased / Invalidated (INVALID: no executeAt) t1
+# executes at its own TxnId.  t2, a range Write (not awaitsOnlyDeps) executing at its TxnId (hlc 12)
+# before t0's executeAt, breaks checkState(executeAt < waitingExecuteAt || awaitsOnlyDeps) (:789-791):
+# an IllegalStateException.
+TRUNC_KAT = [(10, "W", 1, None, [(0, 2)]), (11, "XSP", 1, None, [(0, 2)]), (12, "W", 1, None, [(0, 2)])]
+TRUNCATED_APPLY = 9
+
+
+def trunc_kat_run(dev=None, status=TRUNCATED_APPLY):
+    s = mk(TRUNC_KAT)
+    d = Driver(s, 4, dev)
+    part = d.batch(0, 2)
+    x0 = (int(s.msb[0]), 30 << 16 | int(s.lsb[0]) & 0xFFFF, 1)
+    d.register([0], STABLE, [x0])
+    d.register([0], status, [x0])
+    d.register([1], STABLE)
+    d.initialise(0, part)
+    assert list(d.round()) == [1]
+    em, el, en = d.eal
+    own = (int(s.msb[1]), int(s.lsb[1]), int(s.node[1]))
+    assert (int(em[0]), int(el[0]), int(en[0])) == (x0 if status == TRUNCATED_APPLY else own)
+    return d, s, x0
+
+
+def trunc_kat_violation(dev=None):
+    d, s, x0 = trunc_kat_run(dev)
+    part = d.batch(2, 3)
+    assert list(part.range_deps(0)[2]) == [0]           # a Write does not witness the ExclusiveSyncPoint
+    d.register([2], STABLE)
+    if dev is not None:
+        with pytest.raises(IllegalStateException):
+            dev.waiting_on_initialise()                 # the initial updateWaitingOn visits t0
+        return
+    d.ora.waiting_add(2, part)
+    with pytest.raises(O.OracleError) as e:
+        d.ora.ready_ex()
+    assert e.value.rc == -10
+
+
+def test_truncated_apply_kat_oracle():
+    trunc_kat_run()
+    trunc_kat_run(status=INVALID)
+    trunc_kat_violation()
+
+
+def test_truncated_apply_status_order_oracle():
+    # statuses advance in SaveStatus order: TruncatedApply after Applied, before Invalid / Erased
+    s = mk(TRUNC_KAT)
+    L = O.LStore(4)
+    L.batch(s)
+    x = (s.msb[:1], s.lsb[:1], s.node[:1])
+    L.register(*x, np.array([APPLIED], np.uint8), *x)
+    L.register(*x, np.array([TRUNCATED_APPLY], np.uint8), *x)
+    L.register(*x, np.array([INVALID], np.uint8), *x)
+    with pytest.raises(O.OracleError):
+        L.register(*x, np.array([TRUNCATED_APPLY], np.uint8), *x)     # back from Invalid
+    L.close()
+
+
 def stable_stream(n, ks, seed, range_frac=0.0, sync_points=False, range_len_max=8):
     s = generate_stream(n, 3, ks, 0.9, 0.5, seed=seed, range_frac=range_frac, range_len_max=range_len_max)
     # kinds: Read / Write / EphemeralRead (key txns); range txns keep their kind.  sync_points: also
@@ -677,6 +740,22 @@ def test_gpu_ready_mode_guards(gpu_device):
 def test_gpu_propagate_kat(gpu_device):
     with CommandStore(device=gpu_device, key_lo=0, key_hi=6, window=WINDOW_NONE, resident=True) as dev:
         prop_kat_run(dev)
+
+
+@pytest.mark.gpu
+def test_gpu_truncated_apply_kat(gpu_device):
+    for status in (TRUNCATED_APPLY, INVALID):
+        with CommandStore(device=0, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+            trunc_kat_run(dev, status)
+    with CommandStore(device=0, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        trunc_kat_violation(dev)
+    with CommandStore(device=0, key_lo=0, key_hi=4, window=WINDOW_NONE, resident=True) as dev:
+        s = mk(TRUNC_KAT)
+        dev.calculate_deps_batch(s)
+        x = (s.msb[:1], s.lsb[:1], s.node[:1])
+        dev.register(*x, np.array([INVALID], np.uint8), *x)
+        with pytest.raises(IllegalStateException):
+            dev.register(*x, np.array([TRUNCATED_APPLY], np.uint8), *x)   # statuses never go back
 
 
 @pytest.mark.gpu
