@@ -13,7 +13,10 @@
 //   summary(q) = per key, the entries of segment q from its last Write before b_q - W on (all of
 //                them when it has none): what any later txn can still reach of segment q's txns;
 //   carry(r)   = per key, walk back from summary(r-1) towards summary(0), keeping every entry, up
-//                to and including the first Write before a_r - W.
+//                to and including the first Write before a_r - W -- i.e. every summary entry at or
+//                after the key's last Write before a_r - W over all of them.
+// Both stay in stream order (no key sort): the carry heads the compute's pairs, whose stable
+// bucketing sort makes the history key-major with each key's entries in stream order.
 //
 // An entry the single-store run would still reach at a_r lies at or after the key's last Write
 // before a_r - W, so no Write of the key lies between it and b_q - W <= a_r - W: its own summary
@@ -37,111 +40,242 @@ inline uint32_t grid_for(uint64_t n)
     return (uint32_t)(b < 1 ? 1 : b > 65535 ? 65535 : b);
 }
 
-int bits_for(uint32_t maxval)
+constexpr uint32_t SEG_T = 256;                    // txns (summary) / entries (fold) per block
+constexpr uint32_t SEG_HASH = 2048;                 // LDS slots of a block's (key -> last Write) table
+constexpr uint32_t SEG_EMPTY = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t l2_load(const uint32_t *p)
 {
-    int b = 0;
-    while (b < 32 && (maxval >> b) != 0) ++b;
-    return b < 1 ? 1 : b;
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// (last Write position before thr) + 1 per key, 0 = none.  Txns are walked from the segment's end,
-// so the newest Writes land first and older ones see a larger value and skip their atomic (the
-// hottest key's Writes would otherwise all contend on one word).
-__global__ __launch_bounds__(256) void seg_lastw_kernel(uint32_t n, uint32_t base, uint32_t thr,
-                                                        const uint64_t *__restrict__ lsb,
-                                                        const uint32_t *__restrict__ key_off,
-                                                        const uint32_t *__restrict__ key_ord, uint32_t key_lo,
-                                                        uint32_t nkeys, uint32_t *lastw)
+// exclusive sum over the block's 256 threads (4 waves); *total = the block's sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *total)
 {
-    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= n) return;
-    const uint32_t t = n - 1 - x;
-    const uint32_t gp = base + t;
-    if (gp >= thr) return;
-    if (((lsb[t] >> 1) & 7u) != 1u) return;          // Writes only bound maxCommittedBefore
-    const uint32_t v = gp + 1;
-    for (uint32_t p = key_off[t], e = key_off[t + 1]; p < e; ++p) {
-        const uint32_t k = key_ord[p] - key_lo;
-        if (k >= nkeys) continue;
-        if (*(volatile const uint32_t *)&lastw[k] < v) atomicMax(&lastw[k], v);
+    __shared__ uint32_t wsum[SEG_T / 64];
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < SEG_T / 64; ++u) {
+        before += u < w ? wsum[u] : 0u;
+        all += wsum[u];
     }
+    *total = all;
+    return before + inc - v;
 }
 
-// per (txn, key) pair: kept in the summary iff at or after the key's last Write before thr
-__global__ __launch_bounds__(256) void seg_flag_kernel(uint32_t n, uint32_t base, const uint32_t *__restrict__ key_off,
-                                                       const uint32_t *__restrict__ key_ord, uint32_t key_lo,
-                                                       uint32_t nkeys, const uint32_t *__restrict__ lastw,
-                                                       uint32_t *__restrict__ flag)
+// A block's txns and their (txn, key) pairs staged in LDS with coalesced loads: key ordinals sk[],
+// the local txn of every pair st[], the txns' kinds.  (A thread per txn walking its own pairs issues
+// one dependent global load per pair -- 8 round trips per thread -- and strides 32 bytes across the
+// lanes: the first form of these kernels spent 30 us per launch on that.)  A block whose pairs
+// exceed the stage takes the per-thread walk.
+constexpr uint32_t SEG_STAGE = 4096, SEG_PER = SEG_STAGE / SEG_T;
+struct SegTile {
+    uint32_t t0, t1, p0, np;
+    bool staged;
+};
+__device__ __forceinline__ SegTile seg_stage(uint32_t t0, uint32_t t1, const uint32_t *__restrict__ key_off,
+                                             const uint32_t *__restrict__ key_ord, const uint64_t *__restrict__ lsb,
+                                             uint32_t *sk, uint16_t *st, uint8_t *skind)
 {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const uint32_t gp = base + t;
-    for (uint32_t p = key_off[t], e = key_off[t + 1]; p < e; ++p) {
-        const uint32_t k = key_ord[p] - key_lo;
-        flag[p] = (k < nkeys && gp + 1 >= lastw[k]) ? 1u : 0u;
+    SegTile g{t0, t1, key_off[t0], 0u, false};
+    g.np = key_off[t1] - g.p0;
+    g.staged = g.np <= SEG_STAGE;
+    const uint32_t t = t0 + threadIdx.x;
+    if (t < t1) skind[threadIdx.x] = (uint8_t)((lsb[t] >> 1) & 7u);
+    if (g.staged) {
+        for (uint32_t i = threadIdx.x; i < g.np; i += SEG_T) sk[i] = key_ord[g.p0 + i];
+        if (t < t1)
+            for (uint32_t p = key_off[t], e = key_off[t + 1]; p < e; ++p) st[p - g.p0] = (uint16_t)threadIdx.x;
     }
+    __syncthreads();
+    return g;
 }
 
-__global__ __launch_bounds__(256) void seg_scatter_kernel(uint32_t n, uint32_t base, const uint64_t *__restrict__ lsb,
+__device__ __forceinline__ void seg_hash_put(uint32_t *hk, uint32_t *hv, uint32_t k, uint32_t v, uint32_t *lastw)
+{
+    for (uint32_t probe = 0, h = (k * 2654435761u) >> 21; probe < 16; ++probe) {
+        const uint32_t slot = (h + probe) & (SEG_HASH - 1);
+        const uint32_t prev = atomicCAS(&hk[slot], SEG_EMPTY, k);
+        if (prev == SEG_EMPTY || prev == k) { atomicMax(&hv[slot], v); return; }
+    }
+    if (l2_load(&lastw[k]) < v) atomicMax(&lastw[k], v);        // table full around h: directly
+}
+
+// (last Write position before thr) + 1 per key, 0 = none.  A block's Writes first meet in an LDS
+// table (a hot key's Writes of the block become one entry) and each key of the table then raises
+// the global word once, skipped when an L2-coherent read already shows a later Write (every Write of
+// the hottest key going to the global atomic took 0.5 ms: half the grid is resident at once and
+// reads the word before any of them raised it).  The segment is walked in launches from its end
+// (the last eighth, the eighth before, the quarter before, the first half): most keys have a Write
+// in the latest txns, and once it has landed the older Writes of the key are read and skipped.
+__global__ __launch_bounds__(SEG_T) void seg_lastw_kernel(uint32_t t_lo, uint32_t t_hi, uint32_t base, uint32_t thr,
+                                                          const uint64_t *__restrict__ lsb,
                                                           const uint32_t *__restrict__ key_off,
                                                           const uint32_t *__restrict__ key_ord, uint32_t key_lo,
-                                                          const uint32_t *__restrict__ flag,
-                                                          const uint32_t *__restrict__ off, uint32_t *__restrict__ out_key,
-                                                          uint32_t *__restrict__ out_ent)
+                                                          uint32_t nkeys, uint32_t *lastw)
 {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const uint32_t ent = ((uint32_t)((lsb[t] >> 1) & 7u) << ENT_KIND_SHIFT) | (base + t);
-    for (uint32_t p = key_off[t], e = key_off[t + 1]; p < e; ++p)
-        if (flag[p]) {
-            const uint32_t o = off[p];
-            out_key[o] = key_ord[p] - key_lo;
-            out_ent[o] = ent;
+    __shared__ uint32_t hk[SEG_HASH], hv[SEG_HASH], sk[SEG_STAGE];
+    __shared__ uint16_t st[SEG_STAGE];
+    __shared__ uint8_t skind[SEG_T];
+    for (uint32_t i = threadIdx.x; i < SEG_HASH; i += SEG_T) { hk[i] = SEG_EMPTY; hv[i] = 0u; }
+    const uint32_t t1 = t_hi - blockIdx.x * SEG_T;                 // blocks from the range's end
+    const uint32_t t0 = t1 - t_lo > SEG_T ? t1 - SEG_T : t_lo;
+    const SegTile g = seg_stage(t0, t1, key_off, key_ord, lsb, sk, st, skind);
+    if (g.staged) {
+        for (uint32_t i = threadIdx.x; i < g.np; i += SEG_T) {
+            const uint32_t lt = st[i], gp = base + t0 + lt, k = sk[i] - key_lo;
+            if (skind[lt] == 1u && gp < thr && k < nkeys) seg_hash_put(hk, hv, k, gp + 1u, lastw);
         }
+    } else {
+        const uint32_t t = t0 + threadIdx.x, gp = base + t;
+        if (t < t1 && skind[threadIdx.x] == 1u && gp < thr)          // Writes bound maxCommittedBefore
+            for (uint32_t p = key_off[t], e = key_off[t + 1]; p < e; ++p) {
+                const uint32_t k = key_ord[p] - key_lo;
+                if (k < nkeys) seg_hash_put(hk, hv, k, gp + 1u, lastw);
+            }
+    }
+    __syncthreads();
+    uint32_t kk[SEG_HASH / SEG_T], vv[SEG_HASH / SEG_T], cur[SEG_HASH / SEG_T];
+#pragma unroll
+    for (uint32_t j = 0; j < SEG_HASH / SEG_T; ++j) { kk[j] = hk[threadIdx.x + j * SEG_T]; vv[j] = hv[threadIdx.x + j * SEG_T]; }
+#pragma unroll
+    for (uint32_t j = 0; j < SEG_HASH / SEG_T; ++j) cur[j] = kk[j] != SEG_EMPTY ? l2_load(&lastw[kk[j]]) : ~0u;
+#pragma unroll
+    for (uint32_t j = 0; j < SEG_HASH / SEG_T; ++j)
+        if (kk[j] != SEG_EMPTY && cur[j] < vv[j]) atomicMax(&lastw[kk[j]], vv[j]);
+}
+
+// Per block of SEG_T txns: the pairs a later txn can still reach (at or after the key's last Write
+// before thr), each thread a contiguous run of the block's pairs (stream order): its kept count,
+// and with WRITE the kept pairs written at the block's offset + the block's exclusive scan.
+template <bool WRITE>
+__global__ __launch_bounds__(SEG_T) void seg_keep_kernel(uint32_t n, uint32_t base, const uint64_t *__restrict__ lsb,
+                                                         const uint32_t *__restrict__ key_off,
+                                                         const uint32_t *__restrict__ key_ord, uint32_t key_lo,
+                                                         uint32_t nkeys, const uint32_t *__restrict__ lastw,
+                                                         uint32_t *__restrict__ tile_cnt, const uint32_t *__restrict__ tile_off,
+                                                         uint32_t *__restrict__ out_key, uint32_t *__restrict__ out_ent)
+{
+    __shared__ uint32_t sk[SEG_STAGE];
+    __shared__ uint16_t st[SEG_STAGE];
+    __shared__ uint8_t skind[SEG_T];
+    const uint32_t t0 = blockIdx.x * SEG_T, t1 = min(n, t0 + SEG_T);
+    const SegTile g = seg_stage(t0, t1, key_off, key_ord, lsb, sk, st, skind);
+    uint32_t c = 0, tot;
+    if (g.staged) {
+        const uint32_t per = (g.np + SEG_T - 1) / SEG_T, i0 = threadIdx.x * per;
+        uint32_t keep = 0;                                     // bit j: pair i0 + j is kept
+        uint32_t lw[SEG_PER];
+#pragma unroll
+        for (uint32_t j = 0; j < SEG_PER; ++j) {               // every gather issued before any is used
+            const uint32_t i = i0 + j;
+            const uint32_t k = (j < per && i < g.np) ? sk[i] - key_lo : nkeys;
+            lw[j] = k < nkeys ? lastw[k] : ~0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < SEG_PER; ++j) {
+            const uint32_t i = i0 + j;
+            if (j < per && i < g.np && base + t0 + st[i] + 1u >= lw[j]) keep |= 1u << j;
+        }
+        c = __popc(keep);
+        if (!WRITE) {
+            (void)block_excl_scan(c, &tot);
+        } else {
+            uint32_t o = tile_off[blockIdx.x] + block_excl_scan(c, &tot);
+            for (; keep; keep &= keep - 1) {
+                const uint32_t i = i0 + __ffs(keep) - 1, lt = st[i];
+                out_key[o] = sk[i] - key_lo;
+                out_ent[o] = ((uint32_t)skind[lt] << ENT_KIND_SHIFT) | (base + t0 + lt);
+                ++o;
+            }
+        }
+    } else {                                                   // a thread per txn over its own pairs
+        const uint32_t t = t0 + threadIdx.x;
+        uint32_t a = 0, e = 0;
+        if (t < t1) { a = key_off[t]; e = key_off[t + 1]; }
+        for (uint32_t p = a; p < e; ++p) {
+            const uint32_t k = key_ord[p] - key_lo;
+            c += (k < nkeys && base + t + 1u >= lastw[k]) ? 1u : 0u;
+        }
+        if (!WRITE) {
+            (void)block_excl_scan(c, &tot);
+        } else {
+            uint32_t o = tile_off[blockIdx.x] + block_excl_scan(c, &tot);
+            for (uint32_t p = a; p < e && c; ++p) {
+                const uint32_t k = key_ord[p] - key_lo;
+                if (k < nkeys && base + t + 1u >= lastw[k]) {
+                    out_key[o] = k;
+                    out_ent[o] = ((uint32_t)skind[threadIdx.x] << ENT_KIND_SHIFT) | (base + t);
+                    ++o;
+                }
+            }
+        }
+    }
+    if (!WRITE && threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
 }
 
 struct SegParts {
     const uint32_t *key[SEG_MAX_PARTS];
     const uint32_t *ent[SEG_MAX_PARTS];
-    uint32_t n[SEG_MAX_PARTS];
+    uint32_t off[SEG_MAX_PARTS + 1];   // prefix of the parts' entry counts: a flat index space
     uint32_t np;
 };
 
-// Per key: walk the parts from the newest back, keeping every entry, up to and including the first
-// Write before thr.  Count pass (cnt) and fill pass (entries written backwards from off[k + 1], so
-// they land in ascending position order).  kinds |= the entry kinds kept.
-template <bool FILL>
-__global__ __launch_bounds__(256) void seg_fold_kernel(SegParts P, uint32_t nkeys, uint32_t thr,
-                                                       uint32_t *__restrict__ cnt, const uint32_t *__restrict__ off,
-                                                       uint32_t *__restrict__ out_key, uint32_t *__restrict__ out_ent,
-                                                       uint32_t *kinds)
+__device__ __forceinline__ uint32_t seg_part_of(const SegParts &P, uint32_t x)
 {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nkeys) return;
-    uint32_t c = 0, w = FILL ? off[k + 1] : 0u, km = 0;
-    bool done = false;
-    for (int q = (int)P.np - 1; q >= 0 && !done; --q) {
-        const uint32_t *K = P.key[q];
-        uint32_t lo = 0, hi = P.n[q];
-        while (lo < hi) {                              // first entry of key > k
-            const uint32_t m = (lo + hi) >> 1;
-            if (K[m] <= k) lo = m + 1; else hi = m;
-        }
-        const uint32_t *E = P.ent[q];
-        for (uint32_t j = lo; j > 0 && K[j - 1] == k; --j) {
-            const uint32_t e = E[j - 1];
-            ++c;
-            if (FILL) {
-                --w;
-                out_key[w] = k;
-                out_ent[w] = e;
-                km |= 1u << (e >> ENT_KIND_SHIFT);
-            }
-            if ((e >> ENT_KIND_SHIFT) == 1u && (e & ENT_TXN_MASK) < thr) { done = true; break; }
-        }
+    uint32_t q = 0;
+    while (q + 1 < P.np && P.off[q + 1] <= x) ++q;
+    return q;
+}
+
+// The fold, over the concatenated parts (stream order, each part in stream order): the entries
+// kept are those at or after LW(k) = the key's last Write before thr over all parts -- a walk back
+// from the newest part to that Write keeps exactly them -- written in stream order (the compute's
+// stable bucketing sort makes them key-major).
+//   lw: LW(k) + 1 per key;  count: kept entries per block;  write: tile offset + block scan
+__global__ __launch_bounds__(SEG_T) void seg_fold_lw_kernel(SegParts P, uint32_t thr, uint32_t *__restrict__ lw)
+{
+    const uint32_t x = blockIdx.x * SEG_T + threadIdx.x;
+    if (x >= P.off[P.np]) return;
+    const uint32_t q = seg_part_of(P, x), j = x - P.off[q];
+    const uint32_t e = P.ent[q][j];
+    if ((e >> ENT_KIND_SHIFT) == 1u && (e & ENT_TXN_MASK) < thr) atomicMax(&lw[P.key[q][j]], (e & ENT_TXN_MASK) + 1u);
+}
+
+__device__ __forceinline__ bool seg_fold_kept(const SegParts &P, uint32_t x, const uint32_t *__restrict__ lw,
+                                              uint32_t &k, uint32_t &e)
+{
+    if (x >= P.off[P.np]) return false;
+    const uint32_t q = seg_part_of(P, x), j = x - P.off[q];
+    k = P.key[q][j];
+    e = P.ent[q][j];
+    return (e & ENT_TXN_MASK) + 1u >= lw[k];
+}
+
+__global__ __launch_bounds__(SEG_T) void seg_fold_count_kernel(SegParts P, const uint32_t *__restrict__ lw,
+                                                               uint32_t *__restrict__ tile_cnt)
+{
+    uint32_t k, e, tot;
+    const bool kept = seg_fold_kept(P, blockIdx.x * SEG_T + threadIdx.x, lw, k, e);
+    (void)block_excl_scan(kept ? 1u : 0u, &tot);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SEG_T) void seg_fold_write_kernel(SegParts P, const uint32_t *__restrict__ lw,
+                                                               const uint32_t *__restrict__ tile_off,
+                                                               uint32_t *__restrict__ out_key, uint32_t *__restrict__ out_ent)
+{
+    uint32_t k = 0, e = 0, tot;
+    const bool kept = seg_fold_kept(P, blockIdx.x * SEG_T + threadIdx.x, lw, k, e);
+    const uint32_t o = tile_off[blockIdx.x] + block_excl_scan(kept ? 1u : 0u, &tot);
+    if (kept) {
+        out_key[o] = k;
+        out_ent[o] = e;
     }
-    if (!FILL) cnt[k] = c;
-    else if (km) atomicOr(kinds, km);
 }
 
 void seg_record(accord_store *s, int i)
@@ -167,8 +301,8 @@ namespace accord_impl {
 
 void segment_destroy(accord_store *s)
 {
-    DevBuf *bufs[] = {&s->sg_lastw, &s->sg_flag, &s->sg_off, &s->sg_ckey, &s->sg_cent, &s->sg_key, &s->sg_ent,
-                      &s->sg_tmp0, &s->sg_tmp1, &s->sg_tmp2, &s->sg_tmp3, &s->sg_radix, &s->sg_cnt, &s->sg_koff, &s->sg_word};
+    DevBuf *bufs[] = {&s->sg_lastw, &s->sg_flag, &s->sg_off, &s->sg_key, &s->sg_ent, &s->sg_cnt, &s->sg_koff,
+                      &s->sg_word, &s->sg_lw};
     for (DevBuf *b : bufs) b->release();
     if (s->seg_ev_created)
         for (hipEvent_t &e : s->seg_ev) (void)hipEventDestroy(e);
@@ -210,44 +344,39 @@ int32_t accord_segment_summary(accord_store *s, accord_cfk_part *out)
     const uint32_t thr = end > s->cfg.window ? end - s->cfg.window : 0u;
     hipStream_t st = s->stream;
     seg_record(s, 0);
+    const uint32_t tiles = (n + SEG_T - 1) / SEG_T;
     HIPCHECK(s, s->sg_lastw.ensure((size_t)nkeys * 4 + 4));
-    HIPCHECK(s, s->sg_flag.ensure((size_t)P * 4 + 16));
-    HIPCHECK(s, s->sg_off.ensure((size_t)P * 4 + 16));
+    HIPCHECK(s, s->sg_flag.ensure((size_t)tiles * 4 + 16));          // per block: kept pairs
+    HIPCHECK(s, s->sg_off.ensure((size_t)tiles * 4 + 16));           // ... and their offsets
     HIPCHECK(s, s->sg_word.ensure(64));
-    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max(P, 1u)), st));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max(tiles, 1u)), st));
     unsigned long long *dtot = s->sg_word.as<unsigned long long>();
     uint64_t T = 0;
     if (n && P) {
         HIPCHECK(s, hipMemsetAsync(s->sg_lastw.p, 0, (size_t)nkeys * 4, st));
-        hipLaunchKernelGGL(seg_lastw_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, base, thr, s->lsb.as<uint64_t>(),
+        const uint32_t cut[5] = {0u, n / 2, n / 4 * 3, n / 8 * 7, n};
+        for (int c = 3; c >= 0; --c) {                 // from the segment's end
+            if (cut[c + 1] <= cut[c]) continue;
+            const uint32_t blocks = (cut[c + 1] - cut[c] + SEG_T - 1) / SEG_T;
+            hipLaunchKernelGGL(seg_lastw_kernel, dim3(blocks), dim3(SEG_T), 0, st, cut[c], cut[c + 1], base, thr,
+                               s->lsb.as<uint64_t>(), s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(),
+                               s->cfg.key_lo, nkeys, s->sg_lastw.as<uint32_t>());
+        }
+        hipLaunchKernelGGL(seg_keep_kernel<false>, dim3(tiles), dim3(SEG_T), 0, st, n, base, s->lsb.as<uint64_t>(),
                            s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->cfg.key_lo, nkeys,
-                           s->sg_lastw.as<uint32_t>());
-        hipLaunchKernelGGL(seg_flag_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, base, s->key_off.as<uint32_t>(),
-                           s->key_ord.as<uint32_t>(), s->cfg.key_lo, nkeys, s->sg_lastw.as<uint32_t>(),
-                           s->sg_flag.as<uint32_t>());
-        accord::exclusive_scan_u32(s->sg_flag.as<uint32_t>(), s->sg_off.as<uint32_t>(), P, dtot, s->scan_tmp.p, st);
+                           s->sg_lastw.as<uint32_t>(), s->sg_flag.as<uint32_t>(), nullptr, nullptr, nullptr);
+        accord::exclusive_scan_u32(s->sg_flag.as<uint32_t>(), s->sg_off.as<uint32_t>(), tiles, dtot, s->scan_tmp.p, st);
         HIPCHECK(s, hipMemcpyAsync(&s->pinned->totals[9], dtot, 8, hipMemcpyDeviceToHost, st));
         HIPCHECK(s, hipStreamSynchronize(st));
         T = s->pinned->totals[9];
     }
-    HIPCHECK(s, s->sg_ckey.ensure(T * 4 + 4)); HIPCHECK(s, s->sg_cent.ensure(T * 4 + 4));
-    HIPCHECK(s, s->sg_key.ensure(T * 4 + 4)); HIPCHECK(s, s->sg_ent.ensure(T * 4 + 4));
-    HIPCHECK(s, s->sg_tmp0.ensure(T * 4 + 4)); HIPCHECK(s, s->sg_tmp1.ensure(T * 4 + 4));
-    HIPCHECK(s, s->sg_tmp2.ensure(T * 4 + 4)); HIPCHECK(s, s->sg_tmp3.ensure(T * 4 + 4));
-    if (T) {
-        hipLaunchKernelGGL(seg_scatter_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, base, s->lsb.as<uint64_t>(),
-                           s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->cfg.key_lo,
-                           s->sg_flag.as<uint32_t>(), s->sg_off.as<uint32_t>(), s->sg_ckey.as<uint32_t>(),
-                           s->sg_cent.as<uint32_t>());
-        // key-major, positions ascending within a key: a stable sort by key of the txn-major entries
-        HIPCHECK(s, s->sg_radix.ensure(accord::radix_sort_temp_bytes((uint32_t)T)));
-        HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max<uint32_t>(
-                                                  P, accord::radix_sort_scan_len((uint32_t)T))), st));
-        accord::radix_sort_pairs(s->sg_ckey.as<uint32_t>(), nullptr, s->sg_key.as<uint32_t>(), s->sg_tmp0.as<uint32_t>(),
-                                 s->sg_tmp1.as<uint32_t>(), s->sg_tmp2.as<uint32_t>(), s->sg_cent.as<uint32_t>(),
-                                 s->sg_ent.as<uint32_t>(), s->sg_tmp3.as<uint32_t>(), (uint32_t)T, bits_for(nkeys - 1),
-                                 s->sg_radix.p, s->scan_tmp.p, st);
-    }
+    HIPCHECK(s, s->sg_key.ensure(T * 4 + 4));
+    HIPCHECK(s, s->sg_ent.ensure(T * 4 + 4));
+    if (T)   // in stream order (txn-major): the fold and the compute's stable sort need no key order
+        hipLaunchKernelGGL(seg_keep_kernel<true>, dim3(tiles), dim3(SEG_T), 0, st, n, base, s->lsb.as<uint64_t>(),
+                           s->key_off.as<uint32_t>(), s->key_ord.as<uint32_t>(), s->cfg.key_lo, nkeys,
+                           s->sg_lastw.as<uint32_t>(), nullptr, s->sg_off.as<uint32_t>(), s->sg_key.as<uint32_t>(),
+                           s->sg_ent.as<uint32_t>());
     seg_record(s, 1);
     // the summary may be read by another store's stream (one-GPU simulation) or a collective: ready
     HIPCHECK(s, hipStreamSynchronize(st));
@@ -291,29 +420,34 @@ int32_t accord_segment_carry(accord_store *s, uint32_t nparts, const accord_cfk_
     uint64_t cap = 0;
     for (uint32_t q = 0; q < nparts; ++q) {
         if (parts[q].n && (!parts[q].key || !parts[q].ent)) return fail(s, ACCORD_ERR_ARG, "part %u without arrays", q);
-        if (parts[q].n >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "part %u over 2^32 entries", q);
-        sp.key[q] = parts[q].key; sp.ent[q] = parts[q].ent; sp.n[q] = (uint32_t)parts[q].n;
+        sp.key[q] = parts[q].key; sp.ent[q] = parts[q].ent; sp.off[q] = (uint32_t)cap;
         cap += parts[q].n;
+        if (cap >= (1ull << 28)) return fail(s, ACCORD_ERR_CAPACITY, "carry of up to %llu entries exceeds 2^28",
+                                             (unsigned long long)cap);
     }
+    sp.off[nparts] = (uint32_t)cap;
     sp.np = nparts;
-    if (cap >= (1ull << 28)) return fail(s, ACCORD_ERR_CAPACITY, "carry of up to %llu entries exceeds 2^28",
-                                         (unsigned long long)cap);
     seg_record(s, 2);
-    HIPCHECK(s, s->sg_cnt.ensure((size_t)nkeys * 4 + 4));
-    HIPCHECK(s, s->sg_koff.ensure(((size_t)nkeys + 1) * 4));
+    const uint32_t tiles = (uint32_t)((cap + SEG_T - 1) / SEG_T);
+    HIPCHECK(s, s->sg_lw.ensure((size_t)nkeys * 4 + 4));
+    HIPCHECK(s, s->sg_cnt.ensure((size_t)tiles * 4 + 16));
+    HIPCHECK(s, s->sg_koff.ensure((size_t)tiles * 4 + 16));
     HIPCHECK(s, s->sg_word.ensure(64));
     HIPCHECK(s, s->cy_key.ensure(cap * 4 + 4));
     HIPCHECK(s, s->cy_ent.ensure(cap * 4 + 4));
-    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(nkeys), st));
+    HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(std::max(tiles, 1u)), st));
     unsigned long long *dw = s->sg_word.as<unsigned long long>();   // [0] total, [1] kinds
-    HIPCHECK(s, hipMemsetAsync(dw, 0, 16, st));
-    if (nparts) {
-        hipLaunchKernelGGL(seg_fold_kernel<false>, dim3(grid_for(nkeys)), dim3(256), 0, st, sp, nkeys, thr,
-                           s->sg_cnt.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr);
-        accord::exclusive_scan_u32(s->sg_cnt.as<uint32_t>(), s->sg_koff.as<uint32_t>(), nkeys, dw, s->scan_tmp.p, st);
-        hipLaunchKernelGGL(seg_fold_kernel<true>, dim3(grid_for(nkeys)), dim3(256), 0, st, sp, nkeys, thr,
-                           s->sg_cnt.as<uint32_t>(), s->sg_koff.as<uint32_t>(), s->cy_key.as<uint32_t>(),
-                           s->cy_ent.as<uint32_t>(), (uint32_t *)(dw + 1));
+    accord::FillList fl;
+    fl.add(dw, 16, 0u);
+    if (cap) fl.add(s->sg_lw.p, (size_t)nkeys * 4, 0u);
+    accord::launch_fill_words(fl, st);
+    if (cap) {
+        hipLaunchKernelGGL(seg_fold_lw_kernel, dim3(tiles), dim3(SEG_T), 0, st, sp, thr, s->sg_lw.as<uint32_t>());
+        hipLaunchKernelGGL(seg_fold_count_kernel, dim3(tiles), dim3(SEG_T), 0, st, sp, s->sg_lw.as<uint32_t>(),
+                           s->sg_cnt.as<uint32_t>());
+        accord::exclusive_scan_u32(s->sg_cnt.as<uint32_t>(), s->sg_koff.as<uint32_t>(), tiles, dw, s->scan_tmp.p, st);
+        hipLaunchKernelGGL(seg_fold_write_kernel, dim3(tiles), dim3(SEG_T), 0, st, sp, s->sg_lw.as<uint32_t>(),
+                           s->sg_koff.as<uint32_t>(), s->cy_key.as<uint32_t>(), s->cy_ent.as<uint32_t>());
     }
     seg_record(s, 3);
     HIPCHECK(s, hipMemcpyAsync(&s->pinned->totals[8], dw, 16, hipMemcpyDeviceToHost, st));
@@ -321,9 +455,11 @@ int32_t accord_segment_carry(accord_store *s, uint32_t nparts, const accord_cfk_
     HIPCHECK(s, hipGetLastError());
     // the store now stands at the start of its segment with the CommandsForKey state there; the
     // uploaded segment can be computed (again: a bench step repeats carry + compute)
-    s->carry_n = nparts ? (uint32_t)s->pinned->totals[8] : 0u;
-    s->hist_kinds = nparts ? (uint32_t)s->pinned->totals[9] : 0u;
+    s->carry_n = cap ? (uint32_t)s->pinned->totals[8] : 0u;
+    // every kind may be carried (kinds_present only selects range-txn kernels, which segments never run)
+    s->hist_kinds = cap ? 0xFFu : 0u;
     s->next_global = s->seg_base;
+    s->seg_carry_ok = true;
     s->has_prev = false;
     s->rc_n = 0;
     s->b_registered = false;

@@ -338,6 +338,11 @@ int32_t accord_deps_compute(accord_store *s)
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     if (!s->has_batch) return fail(s, ACCORD_ERR_STATE, "accord_deps_compute before accord_batch_upload");
     if (s->b_registered) return fail(s, ACCORD_ERR_STATE, "the uploaded batch is already part of the resident store's stream");
+    if (s->seg_active && !s->seg_carry_ok)
+        return fail(s, ACCORD_ERR_STATE, "a stream segment computes after accord_segment_carry (its CommandsForKey state)");
+    // a stream segment's store ends with its segment: no carry is kept for a next batch (the later
+    // segments build theirs from its summary, segment.hip)
+    const bool keep_carry = s->resident && !s->seg_active;
     HIPCHECK(s, hipSetDevice(s->cfg.device));
     const uint32_t n = s->n, P = s->P, R = s->R, nrt = s->n_range_txns;
     const uint32_t nkeys = s->cfg.key_hi - s->cfg.key_lo;
@@ -370,7 +375,7 @@ int32_t accord_deps_compute(accord_store *s)
     HIPCHECK(s, s->seg_start.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->seg_end.ensure((size_t)nkeys * 4));
     HIPCHECK(s, s->radix_tmp.ensure(accord::radix_sort_temp_bytes(PH)));
-    if (s->resident) {
+    if (keep_carry) {
         HIPCHECK(s, s->cy_key2.ensure((size_t)PH * 4 + 4));
         HIPCHECK(s, s->cy_ent2.ensure((size_t)PH * 4 + 4));
         HIPCHECK(s, s->carry_tmp.ensure(accord::carry_temp_bytes(PH, nkeys)));
@@ -417,7 +422,8 @@ int32_t accord_deps_compute(accord_store *s)
     // a resident store's batch of up to 16 Ki pairs is sorted alone (one workgroup) and merged into
     // its key-major carry (accord::merge_join_batch) instead of re-sorting [carry | batch]
     const int kbits = bits_for(nkeys - 1);
-    const bool merge = C && accord::merge_join_fits(P, kbits);
+    // (a stream segment's carry is in stream order, not key-major: it always takes the sort)
+    const bool merge = C && !s->seg_active && accord::merge_join_fits(P, kbits);
     record(s, EV_START);
     {   // every small initialisation of the pipeline in one launch
         accord::FillList fl;
@@ -721,7 +727,7 @@ int32_t accord_deps_compute(accord_store *s)
     record(s, EV_RANGE);
     // the txnIds stay where the fill wrote them: each txn's list at its upper-bound offset (vub_off),
     // its length in cnt_vals -- the gapped form of the ABI (include/accord_deps.h, kd_val_cnt)
-    if (s->resident) {
+    if (keep_carry) {
         // what the next batch needs of this history (the stream ends at b_end)
         const uint32_t thr = s->b_end > s->cfg.window ? s->b_end - s->cfg.window : 0u;
         const bool reg = accord_impl::registered_mode(s);
@@ -795,9 +801,13 @@ int32_t accord_deps_compute(accord_store *s)
     }
     if (s->resident) {      // the batch is part of the store's stream now
         if (join) accord_impl::status_join_commit(s);
-        std::swap(s->cy_key, s->cy_key2);
-        std::swap(s->cy_ent, s->cy_ent2);
-        s->carry_n = (uint32_t)s->pinned->totals[8];
+        if (keep_carry) {
+            std::swap(s->cy_key, s->cy_key2);
+            std::swap(s->cy_ent, s->cy_ent2);
+            s->carry_n = (uint32_t)s->pinned->totals[8];
+        } else {
+            s->seg_carry_ok = false;       // the segment's carry was consumed: a rerun takes it again
+        }
         ++s->carry_version;
         s->hist_kinds |= s->b_kinds;
         if (rdeps) {
@@ -857,7 +867,7 @@ int32_t accord_store_reset(accord_store *s)
 {
     if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
     s->next_global = 0; s->carry_n = 0; s->rc_n = 0; s->hist_kinds = 0; s->has_prev = false;
-    s->seg_active = false; s->seg_sum_ok = false; s->seg_base = 0; s->seg_sum_n = 0;
+    s->seg_active = false; s->seg_sum_ok = false; s->seg_carry_ok = false; s->seg_base = 0; s->seg_sum_n = 0;
     s->rg_tx_n = 0; s->rg_known = 0; s->rg_flag_ok = false;
     s->prev_msb = s->prev_lsb = 0; s->prev_node = 0;
     s->has_batch = false; s->b_registered = false; s->computed = false; s->merged = false; s->m_pending = false;

@@ -231,14 +231,13 @@ struct accord_store {
     std::vector<int32_t> rdy_eal_node;
     // stream segments (segment.hip): the store owns positions [seg_base, seg_base + n) of every
     // CommandStore; its summary for later segments, and the fold of earlier ones into the carry
-    bool seg_active = false, seg_sum_ok = false;
+    bool seg_active = false, seg_sum_ok = false, seg_carry_ok = false;
     uint32_t seg_base = 0;
     uint64_t seg_sum_n = 0;
     float seg_summary_ms = 0, seg_carry_ms = 0;
     hipEvent_t seg_ev[4] = {};
     bool seg_ev_created = false;
-    DevBuf sg_lastw, sg_flag, sg_off, sg_ckey, sg_cent, sg_key, sg_ent, sg_tmp0, sg_tmp1, sg_tmp2, sg_tmp3, sg_radix;
-    DevBuf sg_cnt, sg_koff, sg_word;
+    DevBuf sg_lastw, sg_flag, sg_off, sg_key, sg_ent, sg_cnt, sg_koff, sg_word, sg_lw;
     ShardComm *comm = nullptr;
     HostTotals *pinned = nullptr;
     accord_impl::PinnedBlock *dl_arena = nullptr;   // page-locked host arena of accord_deps_download

@@ -345,13 +345,15 @@ int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merg
  *                           position seg_base; then accord_batch_upload of the segment (PreAccept
  *                           batch of key txns, positions seg_base + t);
  *   accord_segment_summary  per key, the segment's entries from its last Write before b - W on (all
- *                           of them when it has none): key-major, positions ascending, in device
- *                           memory owned by the store (valid until the next summary / begin);
+ *                           of them when it has none), in stream order (positions ascending, a txn's
+ *                           keys ascending), in device memory owned by the store (valid until the
+ *                           next summary / begin);
  *                           accord_segment_summary_copy copies them into caller buffers (device,
  *                           or host memory for an exchange staged through the host);
  *   accord_segment_carry    the CommandsForKey state at seg_base from the summaries of segments
- *                           0..r-1 (device memory, stream order): per key, every entry from the
- *                           newest part back to and including the first Write before seg_base - W.
+ *                           0..r-1 (device memory, stream order): per key, every entry at or after
+ *                           the key's last Write before seg_base - W over all parts (the walk back from
+ *                           the newest part that stops at that Write).
  *                           The store then stands at seg_base with that state, and accord_deps_compute
  *                           gives the segment's deps -- equal to one store computing the whole stream
  *                           (tests/test_gpu_segments.py).  Calling it again rewinds the store to the
@@ -359,8 +361,8 @@ int32_t accord_shard_timing(accord_store *store, float *exchange_ms, float *merg
  * Every rank's store must cover the same key range; keys in a part are relative to key_lo. */
 typedef struct {
     uint64_t        n;      /* entries */
-    const uint32_t *key;    /* [n] device: key ordinal - key_lo, ascending */
-    const uint32_t *ent;    /* [n] device: Txn.Kind ordinal << 29 | global stream position, ascending per key */
+    const uint32_t *key;    /* [n] device: key ordinal - key_lo */
+    const uint32_t *ent;    /* [n] device: Txn.Kind ordinal << 29 | global stream position, ascending */
 } accord_cfk_part;
 int32_t accord_segment_begin(accord_store *store, uint32_t seg_base);
 int32_t accord_segment_summary(accord_store *store, accord_cfk_part *out);

@@ -3233,11 +3233,20 @@ done:
 }
 
 /* The reachable entries at the start of segment r (thr = a_r - W) from the reachable summaries of
- * segments 0..r-1 in stream order (part q = or_cfk_reachable over [a_q, b_q) with thr b_q - W).
- * A later segment's summary keeps every entry a later txn can reach of its own txns; when it holds
- * no Write before thr on a key, the key's run continues into the segments before it.  So, per key,
- * walk back from the newest part, keeping every entry, up to and including the first Write with
- * position < thr. */
+ * segments 0..r-1 (part q = or_cfk_reachable over [a_q, b_q) with thr b_q - W; any order inside a
+ * part).  A later segment's summary keeps every entry a later txn can reach of its own txns; when it
+ * holds no Write before thr on a key, the key's run continues into the segments before it -- so the
+ * state is, per key, every summary entry at or after the key's last Write before thr over all parts
+ * (the walk back from the newest part that stops at that Write).  Output key-major. */
+typedef struct { uint32_t key, ent; } seg_ent_t;
+static int cmp_seg_ent(const void *a, const void *b)
+{
+    const seg_ent_t *x = (const seg_ent_t *)a, *y = (const seg_ent_t *)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    const uint32_t px = x->ent & 0x1FFFFFFFu, py = y->ent & 0x1FFFFFFFu;
+    return px < py ? -1 : px > py;
+}
+
 int or_cfk_fold(uint32_t nparts, const uint32_t *part_n, const uint32_t *const *keys, const uint32_t *const *ents,
                 uint32_t thr, uint32_t *n_out, uint32_t **key_out, uint32_t **ent_out)
 {
@@ -3246,35 +3255,26 @@ int or_cfk_fold(uint32_t nparts, const uint32_t *part_n, const uint32_t *const *
     size_t cap = 0;
     for (uint32_t q = 0; q < nparts; ++q) {
         cap += part_n[q];
-        for (uint32_t j = 0; j < part_n[q]; ++j) {
-            if (j && keys[q][j] < keys[q][j - 1]) return -1;     /* parts are key-major */
-            if (keys[q][j] + 1 > nkeys) nkeys = keys[q][j] + 1;
-        }
+        for (uint32_t j = 0; j < part_n[q]; ++j) if (keys[q][j] + 1 > nkeys) nkeys = keys[q][j] + 1;
     }
+    uint32_t *lw = (uint32_t *)calloc((size_t)nkeys + 1, sizeof(uint32_t));   /* last Write < thr, + 1 */
+    seg_ent_t *e = (seg_ent_t *)malloc((cap ? cap : 1) * sizeof(seg_ent_t));
     uint32_t *ok = (uint32_t *)malloc((cap ? cap : 1) * sizeof(uint32_t));
     uint32_t *oe = (uint32_t *)malloc((cap ? cap : 1) * sizeof(uint32_t));
-    uint32_t *pos = (uint32_t *)calloc((size_t)nparts + 1, sizeof(uint32_t));   /* cursor per part */
-    uint32_t *tmp = (uint32_t *)malloc((cap ? cap : 1) * sizeof(uint32_t));
-    if (!ok || !oe || !pos || !tmp) { free(ok); free(oe); free(pos); free(tmp); return -1; }
-    size_t w = 0;
-    for (uint32_t k = 0; k < nkeys; ++k) {
-        size_t m = 0;                         /* the key's kept entries, newest first */
-        int done = 0;
-        for (uint32_t q = nparts; q-- > 0 && !done;) {
-            uint32_t a = pos[q], b = a;
-            while (b < part_n[q] && keys[q][b] == k) ++b;
-            for (uint32_t e = b; e > a; --e) {
-                uint32_t x = ents[q][e - 1];
-                tmp[m++] = x;
-                if ((x >> 29) == K_WRITE && (x & 0x1FFFFFFFu) < thr) { done = 1; break; }
-            }
+    if (!lw || !e || !ok || !oe) { free(lw); free(e); free(ok); free(oe); return -1; }
+    for (uint32_t q = 0; q < nparts; ++q)
+        for (uint32_t j = 0; j < part_n[q]; ++j) {
+            const uint32_t x = ents[q][j], pos = x & 0x1FFFFFFFu;
+            if ((x >> 29) == K_WRITE && pos < thr && pos + 1 > lw[keys[q][j]]) lw[keys[q][j]] = pos + 1;
         }
-        for (uint32_t q = 0; q < nparts; ++q)
-            while (pos[q] < part_n[q] && keys[q][pos[q]] == k) ++pos[q];
-        for (size_t e = m; e > 0; --e) { ok[w] = k; oe[w] = tmp[e - 1]; ++w; }
-    }
-    free(pos); free(tmp);
-    *n_out = (uint32_t)w; *key_out = ok; *ent_out = oe;
+    size_t m = 0;
+    for (uint32_t q = 0; q < nparts; ++q)
+        for (uint32_t j = 0; j < part_n[q]; ++j)
+            if ((ents[q][j] & 0x1FFFFFFFu) + 1 >= lw[keys[q][j]]) { e[m].key = keys[q][j]; e[m].ent = ents[q][j]; ++m; }
+    qsort(e, m, sizeof(seg_ent_t), cmp_seg_ent);
+    for (size_t i = 0; i < m; ++i) { ok[i] = e[i].key; oe[i] = e[i].ent; }
+    free(lw); free(e);
+    *n_out = (uint32_t)m; *key_out = ok; *ent_out = oe;
     return 0;
 }
 

@@ -38,8 +38,9 @@ def run_segments(s, G, ks, W, check_summary=True):
         parts.append(st.segment_summary())
         if check_summary:
             got = device_summary(st)
-            want = O.cfk_reachable(s, a, b, b - W)
-            assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), r
+            wk, we = O.cfk_reachable(s, a, b, b - W)              # key-major; the device's is in stream order
+            o = np.lexsort((wk, we & 0x1FFFFFFF))
+            assert np.array_equal(got[0], wk[o]) and np.array_equal(got[1], we[o]), r
         stores.append(st)
     for r, st in enumerate(stores):
         st.segment_carry(parts[:r])
