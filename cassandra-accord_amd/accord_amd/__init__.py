@@ -53,7 +53,7 @@ EXPORTED_SYMBOLS = [
     "accord_workload_generate", "accord_workload_free", "accord_deps_merge", "accord_comm_unique_id",
     "accord_comm_init", "accord_comm_size", "accord_deps_exchange_merge", "accord_deps_exchange_local", "accord_shard_timing",
     "accord_ready_update", "accord_ready_set_mode",
-    "accord_waiting_on_compute", "accord_waiting_on_initialise", "accord_waiting_on_download", "accord_waiting_on_release",
+    "accord_waiting_on_compute", "accord_waiting_on_levelling", "accord_waiting_on_initialise", "accord_waiting_on_download", "accord_waiting_on_release",
     "accord_waiting_on_timing", "accord_deps_union", "accord_deps_slice", "accord_deps_invert",
     "accord_deps_inverse_release", "accord_ops_timing", "accord_deps_upload",
     "accord_max_conflicts_fold", "accord_max_conflicts_reset", "accord_max_conflicts_state",
@@ -209,6 +209,7 @@ def lib() -> C.CDLL:
         L.accord_deps_exchange_local.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32]
         L.accord_shard_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.accord_waiting_on_compute.argtypes = [C.c_void_p]
+        L.accord_waiting_on_levelling.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.accord_waiting_on_initialise.argtypes = [C.c_void_p]
         L.accord_ready_update.argtypes = [C.c_void_p, C.POINTER(_Ready)]
         L.accord_ready_set_mode.argtypes = [C.c_void_p, C.c_uint32]
@@ -972,6 +973,13 @@ class CommandStore:
         eal = (np.ctypeslib.as_array(r.eal_msb, shape=(r.n,)).copy(), np.ctypeslib.as_array(r.eal_lsb, shape=(r.n,)).copy(),
                np.ctypeslib.as_array(r.eal_node, shape=(r.n,)).copy())
         return got, int(r.waiting), eal
+
+    def waiting_on_levelling(self):
+        """(stripe length, fell back to the serial resolver) of the last waiting_on_compute
+        (include/accord_deps.h accord_waiting_on_levelling)."""
+        a, b = C.c_uint32(), C.c_uint32()
+        self._check(lib().accord_waiting_on_levelling(self._h, C.byref(a), C.byref(b)))
+        return int(a.value), bool(b.value)
 
     def waiting_on_timing(self):
         a, b, c = C.c_float(), C.c_float(), C.c_float()

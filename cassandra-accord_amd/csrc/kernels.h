@@ -422,6 +422,17 @@ void launch_wo_preds_fill(const WaitingOnParams &p, hipStream_t s);
 size_t levels_temp_bytes(uint32_t n);
 void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level, uint32_t *info,
                    void *temp, hipStream_t s);
+// The same levels by stripes of `stripe` txns (levels.hip): per-stripe max-plus walks with 63
+// symbolic sources, the sources resolved in stripe order, relaxation to the fixpoint (at most
+// `relax` sweeps).  info[3] = 1 when the sweeps did not reach the fixpoint: level[] is then a lower
+// bound and the caller runs more sweeps (launch_levels_sweeps) or launch_levels.  info[1], info[2] as above; info zeroed by the caller.
+uint32_t levels_stripe_default(uint32_t n);
+size_t levels_striped_temp_bytes(uint32_t n, uint32_t stripe);
+void launch_levels_striped(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level,
+                           uint32_t *info, void *temp, uint32_t stripe, uint32_t relax, hipStream_t s);
+// further sweeps [from, to) of the same levelling (the flags of sweeps < from stay), then info[1] / info[3]
+void launch_levels_sweeps(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level,
+                          uint32_t *info, void *temp, uint32_t stripe, uint32_t from, uint32_t to, hipStream_t s);
 
 // ---- RedundantBefore.collectDeps (redundant.hip) ----
 constexpr uint32_t RB_NONE = 0xFFFFFFFFu;   // shardAppliedOrInvalidatedBefore == Timestamp.NONE

@@ -1054,7 +1054,11 @@ __device__ unsigned long long g_fk_stamps[16];
 #define FK_STAMP(seg) do {} while (0)
 #endif
 
-template <int BPL>
+// COPY (diagnostic, ACCORD_FILL_COPY=1, outputs meaningless): the same record / slice / candidate
+// loads and the same output stores -- keys, keysToTxnIds header and body at their positions, one
+// txnId store per witnessed candidate inside the txn's region -- without the union (near map, far
+// list, ranks): the address-path floor of this kernel.
+template <int BPL, bool COPY = false>
 __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void keydeps_fast_kernel(
     KeyDepsParams p, const TxnRec *__restrict__ recs)
 {
@@ -1108,6 +1112,35 @@ __global__ __launch_bounds__(KD_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                 break;
             }
             if (p.tiny && tn_take(k, rta)) break;     // a tiny txn: keydeps_tiny_kernel builds it
+            if (COPY) {
+                if (k > 8 || rta > FK_RAW) break;
+                const uint32_t kind = readlane(a.rec, 2), gi = readlane(a.rec, 3), wmask = witness_mask(kind);
+                const uint32_t key_base = readlane(a.rec, 4), val_base = readlane(a.rec, 5), k2v_base = readlane(a.rec, 6);
+                const bool ne = lane < k && a.wc != 0;
+                const uint64_t hb = __ballot(ne);
+                const uint32_t kc = (uint32_t)__popcll(hb);
+                const uint32_t wincl = scan8(lane < k ? a.wc : 0u);
+                if (ne) {
+                    const uint32_t ns = (uint32_t)__popcll(hb & lt);
+                    stg(p.kd_keys, key_base + ns, a.key);
+                    stg(p.kd_k2v, k2v_base + ns, (int32_t)(kc + wincl));
+                }
+                uint32_t run = 0;
+#pragma unroll
+                for (int cc = 0; cc < FK_CB; ++cc) {
+                    if ((uint32_t)cc * 64 >= rta) break;
+                    const uint32_t ev = ea[cc], j = ev & ENT_TXN_MASK;
+                    const bool wit = (uint32_t)cc * 64 + lane < rta && ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) && j != gi;
+                    const uint64_t wb = __ballot(wit);
+                    if (wit) {
+                        stg(p.kd_k2v, k2v_base + kc + run + (uint32_t)__popcll(wb & lt), (int32_t)j);
+                        stg(p.vgap, val_base + (j & 63u), j);
+                    }
+                    run += (uint32_t)__popcll(wb);
+                }
+                if (lane == 0) stg(p.cnt_vals, t, run);
+                break;
+            }
             bool fallback = k > 8 || rta > FK_RAW;
             const uint32_t kind = readlane(a.rec, 2), gi = readlane(a.rec, 3);
             const uint32_t wmask = witness_mask(kind);
@@ -1492,7 +1525,10 @@ void launch_keydeps_fast(const KeyDepsParams &p, int wpl, void *recs, hipStream_
     (void)wpl;
     // near span: 1024 txns below the bound for windows up to 384 (config 2: 94 % of the distinct
     // deps, p99 16 far ones per txn), else 2048
-    if (p.window <= 384u) {
+    static const bool copy = getenv("ACCORD_FILL_COPY") && atoi(getenv("ACCORD_FILL_COPY")) == 1;
+    if (copy && p.window <= 384u) {
+        hipLaunchKernelGGL((keydeps_fast_kernel<16, true>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs);
+    } else if (p.window <= 384u) {
         hipLaunchKernelGGL((keydeps_fast_kernel<16>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs);
     } else {
         hipLaunchKernelGGL((keydeps_fast_kernel<32>), dim3(blocks), dim3(KD_THREADS), 0, s, p, (const TxnRec *)recs);

@@ -2,7 +2,9 @@
 // Runs over the store's computed deps and the key histories the deps pipeline left in HBM.
 #include "store_impl.h"
 
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -43,7 +45,16 @@ int32_t accord_waiting_on_compute(accord_store *s)
     HIPCHECK(s, s->pred_cnt.ensure((size_t)n * 4 + 4));
     HIPCHECK(s, s->pred_off.ensure(n1 * 4));
     HIPCHECK(s, s->level.ensure((size_t)n * 4 + 4));
-    HIPCHECK(s, s->lv_tmp.ensure(accord::levels_temp_bytes(n)));
+    // levelling: by stripes (levels.hip) unless ACCORD_LV_MODE=serial; ACCORD_LV_STRIPE / ACCORD_LV_RELAX
+    // override the stripe length and the sweep bound (tests force the serial fallback with them)
+    const char *lv_mode = getenv("ACCORD_LV_MODE");
+    const bool striped = !(lv_mode && !strcmp(lv_mode, "serial"));
+    const char *lv_z = getenv("ACCORD_LV_STRIPE"), *lv_r = getenv("ACCORD_LV_RELAX");
+    const uint32_t stripe = lv_z ? (uint32_t)atoi(lv_z) : accord::levels_stripe_default(n);
+    // sweeps: 8 queued with the levelling (config 5 reaches the fixpoint in 6), then up to `relax`
+    // in a second round after the host has seen the first round's flag
+    const uint32_t relax = lv_r ? (uint32_t)atoi(lv_r) : 32u, relax1 = std::min(relax, 8u);
+    HIPCHECK(s, s->lv_tmp.ensure(std::max(accord::levels_temp_bytes(n), accord::levels_striped_temp_bytes(n, stripe))));
     HIPCHECK(s, s->wo_info.ensure(64));
     HIPCHECK(s, s->scan_tmp.ensure_zeroed(accord::scan_temp_bytes(n), s->stream));
     HostTotals *dev = s->status_totals.as<HostTotals>();
@@ -82,14 +93,40 @@ int32_t accord_waiting_on_compute(accord_store *s)
     accord::launch_wo_preds_fill(p, st);
     record(s, EV_WO_PREDS);
     HIPCHECK(s, hipMemsetAsync(s->wo_info.p, 0, 64, st));
-    accord::launch_levels(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
-                         s->lv_tmp.p, st);
+    if (striped)
+        accord::launch_levels_striped(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
+                                      s->lv_tmp.p, stripe, relax1, st);
+    else
+        accord::launch_levels(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
+                              s->lv_tmp.p, st);
     record(s, EV_WO_LEVEL);
-    uint32_t info[3] = {0, 0, 0};
+    uint32_t info[4] = {0, 0, 0, 0};
     HIPCHECK(s, hipMemcpyAsync(info, s->wo_info.p, sizeof(info), hipMemcpyDeviceToHost, st));
     HIPCHECK(s, hipStreamSynchronize(st));
     HIPCHECK(s, hipGetLastError());
     if (info[2]) return fail(s, ACCORD_ERR_STATE, "a dependency does not precede its txn");
+    s->lv_fallback = false;
+    s->lv_stripe = striped ? stripe : 0u;
+    if (striped && info[3] && relax > relax1) {   // a second round of sweeps
+        accord::launch_levels_sweeps(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
+                                     s->lv_tmp.p, stripe, relax1, relax, st);
+        record(s, EV_WO_LEVEL);
+        HIPCHECK(s, hipMemcpyAsync(info, s->wo_info.p, sizeof(info), hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+        HIPCHECK(s, hipGetLastError());
+        if (info[2]) return fail(s, ACCORD_ERR_STATE, "a dependency does not precede its txn");
+    }
+    if (striped && info[3]) {   // the sweeps did not reach the fixpoint: the serial resolver, exact
+        s->lv_fallback = true;
+        HIPCHECK(s, hipMemsetAsync(s->wo_info.p, 0, 64, st));
+        accord::launch_levels(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
+                              s->lv_tmp.p, st);
+        record(s, EV_WO_LEVEL);
+        HIPCHECK(s, hipMemcpyAsync(info, s->wo_info.p, sizeof(info), hipMemcpyDeviceToHost, st));
+        HIPCHECK(s, hipStreamSynchronize(st));
+        HIPCHECK(s, hipGetLastError());
+        if (info[2]) return fail(s, ACCORD_ERR_STATE, "a dependency does not precede its txn");
+    }
     if (info[0]) return fail(s, ACCORD_ERR_CAPACITY, "levelling did not drain (%u chunks resolved)", info[0] - 1);
     s->max_level = info[1];
     if (s->events) {
@@ -100,6 +137,15 @@ int32_t accord_waiting_on_compute(accord_store *s)
         s->wo_ms[2] = el(EV_WO_PREDS, EV_WO_LEVEL);
     }
     s->wo_done = true;
+    return ACCORD_OK;
+}
+
+int32_t accord_waiting_on_levelling(accord_store *s, uint32_t *stripe, uint32_t *fallback)
+{
+    if (!s) return fail(nullptr, ACCORD_ERR_ARG, "null store");
+    if (!s->wo_done) return fail(s, ACCORD_ERR_STATE, "no accord_waiting_on_compute result");
+    if (stripe) *stripe = s->lv_stripe;
+    if (fallback) *fallback = s->lv_fallback ? 1u : 0u;
     return ACCORD_OK;
 }
 

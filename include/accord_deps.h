@@ -589,6 +589,10 @@ int32_t accord_waiting_on_download(accord_store *store, accord_waiting_on *out);
 void    accord_waiting_on_release(accord_waiting_on *wo);
 /* device ms of the last accord_waiting_on_compute: bitsets, reduced predecessors, levelling */
 int32_t accord_waiting_on_timing(accord_store *store, float *bits_ms, float *preds_ms, float *level_ms);
+/* how the last accord_waiting_on_compute levelled: the stripe length of the striped levelling (0 =
+ * the serial resolver alone, ACCORD_LV_MODE=serial) and whether its sweeps fell back to the serial
+ * resolver (1) -- the levels are the same either way */
+int32_t accord_waiting_on_levelling(accord_store *store, uint32_t *stripe, uint32_t *fallback);
 
 /* ---- synthetic workload (SURVEY.md §8d stream; splitmix64 + Zipf rejection-inversion) ---- */
 typedef struct {
