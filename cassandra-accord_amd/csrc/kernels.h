@@ -409,6 +409,7 @@ struct WaitingOnParams {
     uint32_t *pred_cnt;
     const uint32_t *pred_off;
     uint32_t *preds;
+    uint8_t *pred_own;                             // fill: per predecessor, its txn's index mod 64 (or nullptr)
 };
 void launch_wo_words_count(uint32_t n, const uint32_t *kd_key_off, const uint32_t *rd_val_off, uint32_t *cnt,
                            hipStream_t s);
@@ -428,8 +429,8 @@ void launch_levels(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, 
 // bound and the caller runs more sweeps (launch_levels_sweeps) or launch_levels.  info[1], info[2] as above; info zeroed by the caller.
 uint32_t levels_stripe_default(uint32_t n);
 size_t levels_striped_temp_bytes(uint32_t n, uint32_t stripe);
-void launch_levels_striped(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level,
-                           uint32_t *info, void *temp, uint32_t stripe, uint32_t relax, hipStream_t s);
+void launch_levels_striped(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, const uint8_t *pred_own,
+                           uint32_t *level, uint32_t *info, void *temp, uint32_t stripe, uint32_t relax, hipStream_t s);
 // further sweeps [from, to) of the same levelling (the flags of sweeps < from stay), then info[1] / info[3]
 void launch_levels_sweeps(uint32_t n, const uint32_t *pred_off, const uint32_t *preds, uint32_t *level,
                           uint32_t *info, void *temp, uint32_t stripe, uint32_t from, uint32_t to, hipStream_t s);

@@ -123,7 +123,7 @@ int32_t accord_store_destroy(accord_store *s)
                       &s->rd_vals, &s->rd_r2v, &s->rd_big, &s->rt_hits, &s->rk_cp, &s->rk_cnt, &s->rk_off, &s->rk_slices, &s->rk_cls, &s->txn_index, &s->m_key_off, &s->m_val_off, &s->m_k2v_off,
                       &s->m_keys, &s->m_vals, &s->m_k2v, &s->m_cnt_keys, &s->m_cnt_vals, &s->m_cnt_k2v, &s->m_ptrs,
                       &s->m_zero, &s->wo_cnt, &s->wo_off, &s->wo_words, &s->wo_aoi, &s->pred_cnt, &s->pred_off, &s->preds,
-                      &s->level, &s->wo_info, &s->lv_tmp, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
+                      &s->level, &s->wo_info, &s->lv_tmp, &s->pred_own, &s->cy_key, &s->cy_ent, &s->cy_key2, &s->cy_ent2,
                       &s->carry_tmp, &s->rg_tmsb, &s->rg_tlsb, &s->rg_tnode, &s->rg_tg, &s->rg_status, &s->rg_emsb,
                       &s->rg_elsb, &s->rg_enode, &s->rg_flag, &s->rg_gcnt, &s->rg_goff, &s->rg_hist2, &s->rg_kbound, &s->rg_cwflag, &s->rg_cwoff, &s->rg_cwpos, &s->rg_cwpm, &s->rg_cwchunk, &s->rg_hxchunk, &s->rg_hx, &s->rg_hu,
                       &s->rc_owner, &s->rc_start, &s->rc_end, &s->rc_kind, &s->rc_owner2, &s->rc_start2,

@@ -151,7 +151,7 @@ struct accord_store {
     float xchg_ms = 0, merge_ms = 0;
     // WaitingOn + levelling (waiting_on_abi.cpp)
     bool wo_done = false;
-    DevBuf wo_cnt, wo_off, wo_words, wo_aoi, pred_cnt, pred_off, preds, level, wo_info, lv_tmp;
+    DevBuf wo_cnt, wo_off, wo_words, wo_aoi, pred_cnt, pred_off, preds, pred_own, level, wo_info, lv_tmp;
     bool lv_fallback = false;          // the last levelling fell back to the serial resolver
     uint32_t lv_stripe = 0;            // its stripe length (0: serial resolver alone)
     bool wo_has_aoi = false;       // accord_waiting_on_initialise: appliedOrInvalidated words in wo_aoi

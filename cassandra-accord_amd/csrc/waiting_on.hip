@@ -138,6 +138,8 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
             if (FILL) p.preds[o++] = p.rd_vals[v];
         }
         if (!FILL) p.pred_cnt[i] = cnt;
+        if (FILL && p.pred_own)
+            for (uint32_t e = p.pred_off[i]; e < o; ++e) p.pred_own[e] = (uint8_t)(i & 63u);
     }
 }
 

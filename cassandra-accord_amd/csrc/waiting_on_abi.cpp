@@ -85,16 +85,18 @@ int32_t accord_waiting_on_compute(accord_store *s)
     if (s->preds_total >= (1ull << 32)) return fail(s, ACCORD_ERR_CAPACITY, "reduced DAG exceeds 2^32 edges");
     HIPCHECK(s, s->wo_words.ensure(s->wo_words_total * 8));
     HIPCHECK(s, s->preds.ensure(s->preds_total * 4));
+    if (striped) HIPCHECK(s, s->pred_own.ensure(s->preds_total + 16));
     accord::launch_wo_bits(n, s->kd_key_off.as<uint32_t>(), p.rd_val_off, s->wo_off.as<uint32_t>(),
                            s->wo_words.as<unsigned long long>(), st);
     record(s, EV_WO_BITS);
     p.pred_off = s->pred_off.as<uint32_t>();
     p.preds = s->preds.as<uint32_t>();
+    p.pred_own = striped ? s->pred_own.as<uint8_t>() : nullptr;
     accord::launch_wo_preds_fill(p, st);
     record(s, EV_WO_PREDS);
     HIPCHECK(s, hipMemsetAsync(s->wo_info.p, 0, 64, st));
     if (striped)
-        accord::launch_levels_striped(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
+        accord::launch_levels_striped(n, p.pred_off, p.preds, p.pred_own, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
                                       s->lv_tmp.p, stripe, relax1, st);
     else
         accord::launch_levels(n, p.pred_off, p.preds, s->level.as<uint32_t>(), s->wo_info.as<uint32_t>(),
