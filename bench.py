@@ -135,6 +135,8 @@ def main():
     ap.add_argument("--ready", action="store_true",
                     help="also time execution readiness (accord_ready_update) over a registered-status "
                          "schedule: batches registered STABLE, ready txns registered APPLIED round by round")
+    ap.add_argument("--ready-events", action="store_true",
+                    help="--ready: also run the schedule in event-exact mode (accord_ready_set_mode EVENTS)")
     ap.add_argument("--ready-batch", type=int, default=4096, help="txns per batch of the --ready leg")
     ap.add_argument("--ready-batches", type=int, default=16, help="batches of the --ready leg")
     ap.add_argument("--ready-cpu-batch", type=int, default=2048,
@@ -360,6 +362,8 @@ def main():
             registered = registered_batches(s, args)
         if s.rng_off[-1] == 0 and args.ready:
             ready = ready_schedule(s, args)
+            if args.ready_events:
+                ready["events_mode"] = ready_schedule(s, args, events=True)
             if args.ready_cpu_batch:
                 one = types.SimpleNamespace(ready_batch=args.ready_cpu_batch, ready_batches=1, keyspace=args.keyspace)
                 ready["same_sample"] = {"device": ready_schedule(s, one), "cpu_baseline": ready_cpu(s, args)}
@@ -621,17 +625,20 @@ def registered_batches(s, args, lag_applied=4, lag_rb=8, reps=2):
 ST_STABLE = 5
 
 
-def ready_schedule(s, args, rounds_per_batch=4):
+def ready_schedule(s, args, rounds_per_batch=4, events=False):
     """Execution readiness (include/accord_deps.h accord_ready_update) over the
     first ready_batches x ready_batch txns of the stream in a registered-status store: per batch the
     deps are computed, the batch is registered STABLE at executeAt = TxnId and its WaitingOn
     initialised (the txns join the waiting set), then up to rounds_per_batch rounds of
     accord_ready_update -> the ready txns registered APPLIED; finally the set is drained.  Reports the
     wall time of the ready_update calls (device summaries + evaluation + one host read) against the
-    txns they released."""
+    txns they released.  events: the store in event-exact mode (accord_ready_set_mode(ACCORD_READY_
+    EVENTS)), where key bits clear when a registration's events reach the key -- that work is in the
+    registration calls, reported as register_ms_per_call beside the update calls."""
     from accord_amd import CommandStore, WINDOW_NONE
     bsz, nb = args.ready_batch, min(args.ready_batches, s.n // args.ready_batch)
     upd_ms, app_ms, calls, released, rounds = 0.0, 0.0, 0, 0, 0
+    reg_ms, regs = 0.0, 0
 
     def rnd(st):
         nonlocal upd_ms, app_ms, calls, released, rounds
@@ -649,13 +656,18 @@ def ready_schedule(s, args, rounds_per_batch=4):
         return ready.size, waiting
 
     with CommandStore(device=0, key_lo=0, key_hi=args.keyspace, window=WINDOW_NONE, resident=True) as st:
+        if events:
+            st.ready_mode(True)
         for b in range(nb):
             lo, hi = b * bsz, (b + 1) * bsz
             st.upload(s.slice(lo, hi))
             st.compute()
             idx = np.arange(lo, hi)
+            t2 = time.perf_counter()
             st.register(s.msb[idx], s.lsb[idx], s.node[idx], np.full(bsz, ST_STABLE, np.uint8),
                         s.msb[idx], s.lsb[idx], s.node[idx])
+            reg_ms += (time.perf_counter() - t2) * 1e3
+            regs += 1
             st.waiting_on_initialise()
             for _ in range(rounds_per_batch):
                 if rnd(st)[0] == 0:
@@ -670,6 +682,10 @@ def ready_schedule(s, args, rounds_per_batch=4):
                         f"per batch, then drained",
             "txns": nb * bsz, "released": released, "left_waiting": waiting, "update_calls": calls,
             "release_rounds": rounds, "update_ms_per_call": upd_ms / max(1, calls),
+            "mode": "events" if events else "poll",
+            "register_stable_ms_per_batch": reg_ms / max(1, regs),
+            "register_applied_ms_per_call": app_ms / max(1, rounds),
+            "per_call_ms_update_plus_register": (upd_ms + app_ms) / max(1, calls),
             "released_txns_per_s_update_wall": released / (upd_ms * 1e-3) if upd_ms else None,
             "apply_register_ms_total": app_ms}
 

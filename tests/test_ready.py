@@ -547,12 +547,14 @@ def test_all_stable_rounds_equal_cfk_simulation(n, ks, seed, rf):
     assert np.array_equal(got, want.astype(np.int64))
 
 
-def schedule(s, nkeys, bsz, seed, dev=None, late_frac=0.15, delay_frac=0.2, rounds_per_batch=2, dev_events=False):
+def schedule(s, nkeys, bsz, seed, dev=None, late_frac=0.15, delay_frac=0.2, rounds_per_batch=2, dev_events=False,
+             driver=None):
     """Batches of bsz: computed, then STABLE for most txns (some at an executeAt past their TxnId),
     the rest (late) STABLE one batch later; WaitingOn initialised; a few ready -> APPLIED rounds per
-    batch; finally drained.  Returns every round's ready list."""
+    batch; finally drained.  Returns every round's ready list.  driver: another object with the
+    Driver's interface (the golden replay below)."""
     rng = np.random.default_rng(seed)
-    d = Driver(s, nkeys, dev, dev_events=dev_events)
+    d = driver if driver is not None else Driver(s, nkeys, dev, dev_events=dev_events)
     out, late = [], np.zeros(0, np.int64)
     for lo in range(0, s.n, bsz):
         hi = min(s.n, lo + bsz)
@@ -645,6 +647,76 @@ def test_gpu_event_mode_equals_event_oracle(gpu_device, n, ks, bsz, seed, rf, sp
     # every call compared inside Driver.round; the event-driven reference releases fewer (sync points
     # wait for an event that may never reach their keys)
     assert sum(len(r) for r in out) > 0
+
+
+# Event-exact readiness at 20k txns: the event restatement takes ~9 min on one core for this
+# schedule, so its per-call releases and executesAtLeast are frozen in tests/golden/events_20k.npz
+# (tests/golden/make_event_golden.py) and the device replays the same schedule against them.
+EV20K = dict(n=20000, ks=2000, bsz=1000, seed=91, rf=0.05)
+
+
+class GoldenReplay:
+    """Driver's interface over the device alone: every ready call compared with the frozen
+    event-restatement output of the same call (releases, executesAtLeast, waiting count)."""
+
+    def __init__(self, s, dev, g):
+        self.s, self.dev, self.g, self.call = s, dev, g, 0
+        self.execs = [None] * s.n
+        dev.ready_mode(True)
+
+    def batch(self, lo, hi):
+        self.dev.calculate_deps_batch(self.s.slice(lo, hi))
+        return None
+
+    def register(self, idx, st, execs=None):
+        idx = np.asarray(idx, np.int64)
+        if idx.size == 0:
+            return
+        order = np.argsort(idx)
+        idx = idx[order]
+        s = self.s
+        em = s.msb[idx].copy(); el = s.lsb[idx].copy(); en = s.node[idx].copy()
+        for r, g in enumerate(idx):
+            if execs is not None and execs[order[r]] is not None:
+                self.execs[g] = execs[order[r]]
+            if self.execs[g] is None:
+                self.execs[g] = (int(s.msb[g]), int(s.lsb[g]), int(s.node[g]))
+            em[r], el[r], en[r] = self.execs[g]
+        self.dev.register(s.msb[idx], s.lsb[idx], s.node[idx], np.full(idx.size, st, np.uint8), em, el, en)
+
+    def initialise(self, lo, part):
+        self.dev.waiting_on_initialise()
+
+    def round(self):
+        g, c = self.g, self.call
+        a, b = int(g["off"][c]), int(g["off"][c + 1])
+        want = g["txn"][a:b]
+        got, waiting, geal = self.dev.ready_update_ex()
+        assert np.array_equal(got, want), (c, got[:20], want[:20])
+        assert waiting == int(g["waiting"][c]), (c, waiting, int(g["waiting"][c]))
+        for x, y in zip(geal, (g["eal_msb"][a:b], g["eal_lsb"][a:b], g["eal_node"][a:b])):
+            assert np.array_equal(x, y), c
+        self.call += 1
+        return want
+
+    def apply(self, ready):
+        self.register(ready, APPLIED)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpu_event_mode_20k_golden(gpu_device):
+    """Event-exact device readiness over 20,000 txns (2,000 keys, 5 % range txns) == the frozen
+    or_lstore_event_mode output, call by call."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "events_20k.npz"))
+    p = EV20K
+    s = stable_stream(p["n"], p["ks"], p["seed"], p["rf"])
+    with CommandStore(device=gpu_device, key_lo=0, key_hi=p["ks"], window=WINDOW_NONE, resident=True) as dev:
+        d = GoldenReplay(s, dev, g)
+        out, _ = schedule(s, p["ks"], p["bsz"], p["seed"], driver=d)
+    assert d.call == len(g["off"]) - 1
+    assert sum(len(r) for r in out) == int(g["released"])
 
 
 def single_event_schedule(s, nkeys, bsz, seed, dev=None, cf=0.3, delay=0.2, rounds=3):
