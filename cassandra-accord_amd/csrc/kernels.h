@@ -410,6 +410,7 @@ struct WaitingOnParams {
     const uint32_t *pred_off;
     uint32_t *preds;
     uint8_t *pred_own;                             // fill: per predecessor, its txn's index mod 64 (or nullptr)
+    uint32_t rw_only;                              // every history entry a Read or a Write (count pass: no entry reads)
 };
 void launch_wo_words_count(uint32_t n, const uint32_t *kd_key_off, const uint32_t *rd_val_off, uint32_t *cnt,
                            hipStream_t s);

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
                 pw[j] = ps[j].pos != ps[j].lo ? max(p.pw_local[x], p.pw_carry[x / p.pw_tile]) : 0u;   // (last Write <= x) + 1
             }
 #pragma unroll
-            for (uint32_t j = 0; j < WO_KB; ++j) lw[j] = pw[j] > ps[j].lo ? p.hist[pw[j] - 1] : 0u;
+            for (uint32_t j = 0; j < WO_KB; ++j) lw[j] = FILL && pw[j] > ps[j].lo ? p.hist[pw[j] - 1] : 0u;
 #pragma unroll
             for (uint32_t j = 0; j < WO_KB; ++j) {
                 const uint32_t pos = ps[j].pos, lo = ps[j].lo;
@@ -94,6 +94,10 @@ __global__ __launch_bounds__(256) void wo_preds_kernel(WaitingOnParams p)
                     from = pw[j];
                 }
                 if (wmask & 1u) {                                                   // Reads after lw
+                    if (!FILL && p.rw_only) {        // after the slice's last Write every entry is a Read
+                        cnt += pos - from;
+                        continue;
+                    }
                     for (uint32_t e = from; e < pos; ++e) {
                         const uint32_t ev = p.hist[e];
                         if ((wmask >> (ev >> ENT_KIND_SHIFT)) & 1u) {

@@ -72,6 +72,7 @@ int32_t accord_waiting_on_compute(accord_store *s)
     p.kd_val_cnt = s->cnt_vals.as<uint32_t>();
     p.rd_val_off = s->rd_val_off.as<uint32_t>(); p.rd_vals = s->rd_vals.as<uint32_t>();
     p.pred_cnt = s->pred_cnt.as<uint32_t>();
+    p.rw_only = (((s->resident ? s->hist_kinds : 0u) | s->b_kinds) & ~3u) == 0u ? 1u : 0u;
 
     record(s, EV_WO_START);
     accord::launch_wo_words_count(n, s->kd_key_off.as<uint32_t>(), p.rd_val_off, s->wo_cnt.as<uint32_t>(), st);
