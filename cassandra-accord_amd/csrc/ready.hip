@@ -715,8 +715,8 @@ inline uint32_t grid_for_waves(uint64_t waves)
 // minUncommitted / next / nextWrite (:432-461) and notifies the STABLE waiters of committed[] in an
 // executeAt range that depends on the change (notify, :1501-1511, with the count test :1512-1635),
 // plus the unmanaged COMMIT / APPLY records of the key (notifyUnmanaged, :1264-1283, 1315-1360).
-// One wave replays a registration's events in order, each against the state after it: the status
-// is applied, then every key of X takes its event; device-scope fences between events make each
+// One workgroup replays a registration's events in order, each against the state after it: the
+// status is applied, then every key of X takes its event; fences and barriers between events make each
 // event's writes (statuses, WaitingOn words, pending records) visible to the next.  Orders the
 // reference leaves free (keys of one event, waiters of one notify) touch disjoint state.
 struct EvCtx {
@@ -785,9 +785,16 @@ __device__ __forceinline__ bool ev_bit(const ReadyParams &p, uint32_t t, uint32_
     return (p.words[p.wo_off[t] + (b >> 6)] >> (b & 63u)) & 1ull;
 }
 
-__device__ __forceinline__ void ev_clear(const ReadyParams &p, uint32_t t, uint32_t b)
+// a key bit cleared by an event; in a registration the waiter is stamped changed at its epoch, so
+// the next accord_ready_update's filter lists it (its release is the update's) without a full pass
+__device__ __forceinline__ void ev_stamp(const EvCtx &c, const ReadyParams &p, uint32_t t)
+{
+    if (c.chg) c.chg[p.g[t]] = c.epoch;
+}
+__device__ __forceinline__ void ev_clear(const EvCtx &c, const ReadyParams &p, uint32_t t, uint32_t b)
 {
     p.words[p.wo_off[t] + (b >> 6)] &= ~(1ull << (b & 63u));
+    ev_stamp(c, p, t);
 }
 
 __device__ __forceinline__ Cand cand_xor(const Cand &c, uint32_t d)
@@ -797,14 +804,30 @@ __device__ __forceinline__ Cand cand_xor(const Cand &c, uint32_t d)
                    __shfl_xor(c.ex.node, d, 64)}};
 }
 
+// The replay runs on one workgroup of EV_T threads (round 6; it was one wave): events stay in order,
+// and every scan inside an event -- a key's carried entries (next / nextWrite / minUncommitted,
+// notify's candidates and count tests), its unmanaged records, a waiter's key slots -- is spread over
+// the workgroup, with barriers between the dependent steps (a status write before the reads of the
+// next step, a key's event before the next key's).
+constexpr uint32_t EV_T = 1024, EV_W = EV_T / 64;
+struct EvSh {
+    uint32_t mu[EV_W];
+    Cand nx[EV_W], nw[EV_W];
+    EalRec eal[EV_W];
+    uint32_t ncand;
+    uint32_t cgi[EV_T], ct[EV_T], cq[EV_T];
+};
+
 // the CommandsForKey constructor's minUncommitted, next, nextWrite of key kk (:432-461), next and
-// nextWrite nulled when minUncommitted's TxnId precedes their executeAt
-__device__ void ev_nexts(const EvCtx &c, uint32_t kk, uint32_t lane, uint32_t &mu, Cand &nx, Cand &nw)
+// nextWrite nulled when minUncommitted's TxnId precedes their executeAt (uniform results)
+__device__ void ev_nexts(const EvCtx &c, EvSh &S, uint32_t kk, uint32_t &mu, Cand &nx, Cand &nw)
 {
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
     mu = NONE;
     nx = Cand{NONE, {0, 0, 0}};
     nw = Cand{NONE, {0, 0, 0}};
-    for (uint32_t x = c.kseg0[kk] + lane; x < c.kseg1[kk]; x += 64) {
+#pragma unroll 4
+    for (uint32_t x = c.kseg0[kk] + tid; x < c.kseg1[kk]; x += EV_T) {
         const uint32_t e = c.cent[x], g = e & ENT_TXN_MASK, kind = e >> ENT_KIND_SHIFT;
         const uint32_t st = kind == 2u ? ST_INVALID : status_of(c.v, g);
         if (st < ST_COMMITTED) mu = min(mu, g);
@@ -820,6 +843,17 @@ __device__ void ev_nexts(const EvCtx &c, uint32_t kk, uint32_t lane, uint32_t &m
         cand_min(nx, cand_xor(nx, d));
         cand_min(nw, cand_xor(nw, d));
     }
+    if ((tid & 63u) == 0) { S.mu[w] = mu; S.nx[w] = nx; S.nw[w] = nw; }
+    __syncthreads();
+    mu = NONE;
+    nx = Cand{NONE, {0, 0, 0}};
+    nw = Cand{NONE, {0, 0, 0}};
+    for (uint32_t j = 0; j < EV_W; ++j) {
+        mu = min(mu, S.mu[j]);
+        cand_min(nx, S.nx[j]);
+        cand_min(nw, S.nw[j]);
+    }
+    __syncthreads();                              // (S reused by the next step)
     if (mu != NONE) {
         const Ts tm = ev_tid(c, mu);
         if (nx.g != NONE && tcmp(tm, nx.ex) < 0) nx.g = NONE;
@@ -829,13 +863,15 @@ __device__ void ev_nexts(const EvCtx &c, uint32_t kk, uint32_t lane, uint32_t &m
 
 // notify's count test for waiter (gi, t) on key slot q of key kk (expectMissingCount == |missing|):
 // no unapplied committed txn of a witnessed kind executes before it on the key, and none of its
-// deps on the key is uncommitted (wave-uniform result)
-__device__ bool ev_managed_ok(const EvCtx &c, const ReadyParams &p, uint32_t t, uint32_t q, uint32_t kk, uint32_t lane)
+// deps on the key is uncommitted (uniform result)
+__device__ bool ev_managed_ok(const EvCtx &c, const ReadyParams &p, uint32_t t, uint32_t q, uint32_t kk)
 {
+    const uint32_t tid = threadIdx.x;
     const uint32_t g = p.g[t], kind = (uint32_t)(p.lsb[t] >> 1) & 7u, wmask = witness_mask(kind);
     const Ts ex = exec_of(c.v, g);
     bool blocked = false;
-    for (uint32_t x = c.kseg0[kk] + lane; x < c.kseg1[kk]; x += 64) {
+#pragma unroll 4
+    for (uint32_t x = c.kseg0[kk] + tid; x < c.kseg1[kk]; x += EV_T) {
         const uint32_t e = c.cent[x], u = e & ENT_TXN_MASK, uk = e >> ENT_KIND_SHIFT;
         if (uk == 2u) continue;
         const uint32_t st = status_of(c.v, u);
@@ -846,20 +882,22 @@ __device__ bool ev_managed_ok(const EvCtx &c, const ReadyParams &p, uint32_t t, 
     const uint32_t kbound = c.kb ? c.kb[kk] : 0u;
     const uint32_t K = p.key_off[t + 1] - p.key_off[t], hb = p.k2v_off[t];
     const uint32_t d0 = q == 0 ? K : (uint32_t)p.k2v[hb + q - 1], d1 = (uint32_t)p.k2v[hb + q];
-    for (uint32_t x = d0 + lane; x < d1; x += 64) {
+    for (uint32_t x = d0 + tid; x < d1; x += EV_T) {
         const uint32_t u = p.vals[p.val_off[t] + p.k2v[hb + x]];
         if (u >= kbound && status_of(c.v, u) < ST_COMMITTED) blocked = true;
     }
-    return __ballot(blocked) == 0ull;
+    return __syncthreads_or(blocked ? 1 : 0) == 0;
 }
 
-// notify(from, to) (:1501-1511): the STABLE waiters of committed[] executing in [from, to] on kk
-__device__ void ev_notify(const EvCtx &c, uint32_t kk, bool has_from, const Ts &from, bool has_to, const Ts &to,
-                          uint32_t lane)
+// notify(from, to) (:1501-1511): the STABLE waiters of committed[] executing in [from, to] on kk.
+// A chunk's candidates are listed, then tested one by one (the tests read statuses only, and each
+// candidate is a different waiter, so their order does not matter)
+__device__ void ev_notify(const EvCtx &c, EvSh &S, uint32_t kk, bool has_from, const Ts &from, bool has_to,
+                          const Ts &to)
 {
-    const uint32_t key = c.key_lo + kk;
-    for (uint32_t x0 = c.kseg0[kk]; x0 < c.kseg1[kk]; x0 += 64) {
-        const uint32_t x = x0 + lane;
+    const uint32_t tid = threadIdx.x, key = c.key_lo + kk;
+    for (uint32_t x0 = c.kseg0[kk]; x0 < c.kseg1[kk]; x0 += EV_T) {
+        const uint32_t x = x0 + tid;
         bool cand = false;
         uint32_t gi = 0, t = 0, q = NONE;
         if (x < c.kseg1[kk]) {
@@ -877,17 +915,23 @@ __device__ void ev_notify(const EvCtx &c, uint32_t kk, bool has_from, const Ts &
                 }
             }
         }
-        unsigned long long m = __ballot(cand);
-        while (m) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1ull;
-            const uint32_t lgi = readlane(gi, (int)l), lt = readlane(t, (int)l), lq = readlane(q, (int)l);
+        if (tid == 0) S.ncand = 0;
+        __syncthreads();
+        if (cand) {
+            const uint32_t j = atomicAdd(&S.ncand, 1u);
+            S.cgi[j] = gi; S.ct[j] = t; S.cq[j] = q;
+        }
+        __syncthreads();
+        const uint32_t nc = S.ncand;
+        for (uint32_t j = 0; j < nc; ++j) {
+            const uint32_t lgi = S.cgi[j], lt = S.ct[j], lq = S.cq[j];
             const ReadyParams &p = c.gens[lgi];
-            if (ev_managed_ok(c, p, lt, lq, kk, lane) && lane == 0) {
+            if (ev_managed_ok(c, p, lt, lq, kk) && tid == 0) {
                 const uint32_t R = p.rd_off[lt + 1] - p.rd_off[lt];
-                ev_clear(p, lt, R + lq);
+                ev_clear(c, p, lt, R + lq);
             }
         }
+        __syncthreads();
     }
 }
 
@@ -898,11 +942,12 @@ __device__ __forceinline__ void ev_eal(const ReadyParams &p, uint32_t t, const T
     p.eal[t] = a;
 }
 
-// notifyUnmanaged(COMMIT, minUncommitted) / (APPLY, next) over the unmanaged records of kk
-__device__ void ev_unmanaged(const EvCtx &c, uint32_t kk, bool commit, uint32_t mu, const Cand &nx, uint32_t lane)
+// notifyUnmanaged(COMMIT, minUncommitted) / (APPLY, next) over the unmanaged records of kk (a thread
+// per record: each is a different waiter's slot on kk)
+__device__ void ev_unmanaged(const EvCtx &c, uint32_t kk, bool commit, uint32_t mu, const Cand &nx)
 {
     const uint32_t kbound = c.kb ? c.kb[kk] : 0u;
-    for (uint32_t j = c.uk_off[kk] + lane; j < c.uk_off[kk + 1]; j += 64) {
+    for (uint32_t j = c.uk_off[kk] + threadIdx.x; j < c.uk_off[kk + 1]; j += EV_T) {
         const unsigned long long w = c.uk_w[j];
         const uint32_t gi = (uint32_t)(w >> 32), t = (uint32_t)w, q = c.uk_slot[j];
         const ReadyParams &p = c.gens[gi];
@@ -918,7 +963,7 @@ __device__ void ev_unmanaged(const EvCtx &c, uint32_t kk, bool commit, uint32_t 
             const uint32_t d0 = q == 0 ? K : (uint32_t)p.k2v[hb + q - 1], d1 = (uint32_t)p.k2v[hb + q];
             uint32_t ea = NONE;
             const int r = unmanaged_eval(p, t, d0, d1, kbound, exec_of(c.v, g), only_deps, false, un, ea);
-            if (r == 1) { pd = 3; ev_clear(p, t, R + q); }
+            if (r == 1) { pd = 3; ev_clear(c, p, t, R + q); }
             else {
                 pd = 2;
                 if (only_deps && ea != NONE) ev_eal(p, t, exec_of(c.v, ea));   // :1370-1380
@@ -927,21 +972,22 @@ __device__ void ev_unmanaged(const EvCtx &c, uint32_t kk, bool commit, uint32_t 
             p.until[slot] = un;
         } else if (pd == 2u && (nx.g == NONE || tcmp(exec_of(c.v, un), nx.ex) < 0)) {
             p.pend[slot] = 3;
-            ev_clear(p, t, R + q);
+            ev_clear(c, p, t, R + q);
         }
     }
 }
 
 // registerUnmanaged (:1406-1498) on every key slot of an unmanaged waiter that now hasBeen(Stable)
-__device__ void ev_register_unmanaged(const EvCtx &c, uint32_t gi, uint32_t t, uint32_t lane)
+__device__ void ev_register_unmanaged(const EvCtx &c, EvSh &S, uint32_t gi, uint32_t t)
 {
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
     const ReadyParams &p = c.gens[gi];
     const uint32_t g = p.g[t], kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
     const bool only_deps = kind == 4u || kind == 2u;
     const uint32_t R = p.rd_off[t + 1] - p.rd_off[t], K = p.key_off[t + 1] - p.key_off[t], hb = p.k2v_off[t];
     const Ts ex = exec_of(c.v, g);
-    for (uint32_t q0 = 0; q0 < K; q0 += 64) {
-        const uint32_t q = q0 + lane;
+    for (uint32_t q0 = 0; q0 < K; q0 += EV_T) {
+        const uint32_t q = q0 + tid;
         bool has = false;
         Ts cand{0, 0, 0};
         if (q < K) {
@@ -953,64 +999,77 @@ __device__ void ev_register_unmanaged(const EvCtx &c, uint32_t gi, uint32_t t, u
                 const int r = unmanaged_eval(p, t, d0, d1, kbound, ex, only_deps, true, un, ea);
                 p.pend[slot] = (uint8_t)(r == 1 ? 3u : r == 0 ? 2u : 1u);
                 p.until[slot] = un;
-                if (r == 1) atomicAnd(&p.words[p.wo_off[t] + ((R + q) >> 6)], ~(1ull << ((R + q) & 63u)));
+                if (r == 1) {
+                    atomicAnd(&p.words[p.wo_off[t] + ((R + q) >> 6)], ~(1ull << ((R + q) & 63u)));
+                    ev_stamp(c, p, t);
+                }
                 if (r == 0 && only_deps && ea != NONE) { has = true; cand = exec_of(c.v, ea); }   // :1470-1478
             }
         }
         const EalRec m = eal_wave_max(has, cand);
-        if (lane == 0 && m.has) {
+        if ((tid & 63u) == 0) S.eal[w] = m;
+        __syncthreads();
+        if (tid == 0) {
             EalRec a = p.eal[t];
-            eal_merge(a, m);
+            for (uint32_t j = 0; j < EV_W; ++j) eal_merge(a, S.eal[j]);
             p.eal[t] = a;
         }
+        __syncthreads();
     }
 }
 
 // notifyAndUpdatePending(safeStore, X, nw, exec, prev) on key kk (:1163-1215), after X's update
-__device__ void ev_key_event(const EvCtx &c, uint32_t kk, uint32_t X, uint32_t prev, uint32_t nw, const Ts &exec,
-                             uint32_t lane)
+__device__ void ev_key_event(const EvCtx &c, EvSh &S, uint32_t kk, uint32_t X, uint32_t prev, uint32_t nw,
+                             const Ts &exec)
 {
     uint32_t mu;
     Cand nx, nwr;
-    ev_nexts(c, kk, lane, mu, nx, nwr);
+    ev_nexts(c, S, kk, mu, nx, nwr);
     if (nw == ST_STABLE || nw == ST_COMMITTED) {
         const int cmp = nwr.g == NONE ? -1 : tcmp(exec, nwr.ex);
         if (cmp <= 0) {
-            if (nw == ST_STABLE) ev_notify(c, kk, nx.g != NONE, nx.ex, true, exec, lane);   // we may execute
+            if (nw == ST_STABLE) ev_notify(c, S, kk, nx.g != NONE, nx.ex, true, exec);   // we may execute
         } else {
             const Ts tx = ev_tid(c, X);
             // waiters on us may be ready, if we execute after them, were known and not committed
             if (!(prev == ST_COMMITTED || tcmp(nwr.ex, tx) < 0 || tcmp(exec, tx) == 0))
-                ev_notify(c, kk, true, nx.ex, true, nwr.ex, lane);
+                ev_notify(c, S, kk, true, nx.ex, true, nwr.ex);
         }
     } else if ((nw == ST_APPLIED || nw == ST_INVALID) && nx.g != NONE) {
-        ev_notify(c, kk, true, nx.ex, nwr.g != NONE, nwr.ex, lane);
+        ev_notify(c, S, kk, true, nx.ex, nwr.g != NONE, nwr.ex);
     }
-    if (nw >= ST_COMMITTED && prev < ST_COMMITTED) ev_unmanaged(c, kk, true, mu, nx, lane);
-    if (mu == NONE || nx.g != NONE) ev_unmanaged(c, kk, false, mu, nx, lane);
+    if (nw >= ST_COMMITTED && prev < ST_COMMITTED) {
+        ev_unmanaged(c, kk, true, mu, nx);
+        __threadfence();
+        __syncthreads();
+    }
+    if (mu == NONE || nx.g != NONE) ev_unmanaged(c, kk, false, mu, nx);
 }
 
 // every key event of txn g (its carried entries; truncated keys excluded)
-__device__ void ev_txn_keys(const EvCtx &c, uint32_t g, uint32_t prev, uint32_t nw, const Ts &exec, uint32_t lane)
+__device__ void ev_txn_keys(const EvCtx &c, EvSh &S, uint32_t g, uint32_t prev, uint32_t nw, const Ts &exec)
 {
     if (g >= c.pk_n) return;
     for (uint32_t j = c.pk_off[g]; j < c.pk_off[g + 1]; ++j) {
         const uint32_t kk = c.ckey[c.pk_ent[j]];
         if (c.kb && g < c.kb[kk]) continue;
-        ev_key_event(c, kk, g, prev, nw, exec, lane);
+        ev_key_event(c, S, kk, g, prev, nw, exec);
         __threadfence();
+        __syncthreads();
     }
 }
 
 // MODE 0: a registration's events; 1: a generation's initialisation; 2: truncated keys
 template <int MODE>
-__global__ __launch_bounds__(64) void rd_event_kernel(EvCtx c)
+__global__ __launch_bounds__(EV_T) void rd_event_kernel(EvCtx c)
 {
-    const uint32_t lane = lane_id();
+    __shared__ EvSh S;
+    const uint32_t tid = threadIdx.x;
     if (MODE == 0) {
         for (uint32_t r = 0; r < c.n; ++r) {
             const uint32_t g = c.pos[r], nw = c.status[r], cur = c.st[g];
-            if (lane == 0) {                                 // the status first (reg_apply_kernel's update)
+            __syncthreads();                                 // every thread has read the old status
+            if (tid == 0) {                                  // the status first (reg_apply_kernel's update)
                 c.st[g] = (uint8_t)nw;
                 c.chg[g] = c.epoch;
                 if (cur < ST_COMMITTED && nw >= ST_COMMITTED) c.cchg[g] = c.epoch;
@@ -1019,17 +1078,19 @@ __global__ __launch_bounds__(64) void rd_event_kernel(EvCtx c)
                 }
             }
             __threadfence();
+            __syncthreads();
             uint32_t gi, t;
             const bool w = ev_waiter(c, g, gi, t);
             if (w && nw >= ST_STABLE && nw < ST_INVALID && cur < ST_STABLE) {
                 const ReadyParams &p = c.gens[gi];
                 const uint32_t kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
-                if ((p.lsb[t] & 1u) != 0 || kind == 2u) ev_register_unmanaged(c, gi, t, lane);   // unmanaged
+                if ((p.lsb[t] & 1u) != 0 || kind == 2u) ev_register_unmanaged(c, S, gi, t);   // unmanaged
                 __threadfence();
+                __syncthreads();
             }
             // CommandsForKey.update on every key (TruncatedApply and Erased leave it as INVALID_OR_TRUNCATED)
             const uint32_t cs = nw >= ST_INVALID ? ST_INVALID : nw, ps = cur >= ST_INVALID ? ST_INVALID : cur;
-            ev_txn_keys(c, g, ps, cs, exec_of(c.v, g), lane);
+            ev_txn_keys(c, S, g, ps, cs, exec_of(c.v, g));
         }
     } else if (MODE == 1) {
         const ReadyParams &p = c.gens[c.init_gi];
@@ -1038,21 +1099,23 @@ __global__ __launch_bounds__(64) void rd_event_kernel(EvCtx c)
             if (st < ST_STABLE || st >= ST_INVALID) continue;
             const uint32_t kind = (uint32_t)(p.lsb[t] >> 1) & 7u;
             if ((p.lsb[t] & 1u) != 0 || kind == 2u) {
-                ev_register_unmanaged(c, c.init_gi, t, lane);
+                ev_register_unmanaged(c, S, c.init_gi, t);
                 __threadfence();
+                __syncthreads();
                 continue;
             }
             if (st != ST_STABLE) continue;
-            ev_txn_keys(c, g, ST_STABLE, ST_STABLE, exec_of(c.v, g), lane);
+            ev_txn_keys(c, S, g, ST_STABLE, ST_STABLE, exec_of(c.v, g));
         }
     } else {
         for (uint32_t j = 0; j < c.ntkeys; ++j) {        // notifyAndUpdatePending(safeStore, prevCfk)
             const uint32_t kk = c.tkeys[j];
             uint32_t mu;
             Cand nx, nwr;
-            ev_nexts(c, kk, lane, mu, nx, nwr);
-            if (mu == NONE || nx.g != NONE) ev_unmanaged(c, kk, false, mu, nx, lane);
+            ev_nexts(c, S, kk, mu, nx, nwr);
+            if (mu == NONE || nx.g != NONE) ev_unmanaged(c, kk, false, mu, nx);
             __threadfence();
+            __syncthreads();
         }
     }
 }
@@ -1410,7 +1473,7 @@ int32_t ready_register_events(accord_store *s, uint32_t n, const uint32_t *pos, 
     c.st = s->rg_status.as<uint8_t>();
     c.xmsb = s->rg_emsb.as<uint64_t>(); c.xlsb = s->rg_elsb.as<uint64_t>(); c.xnode = s->rg_enode.as<int32_t>();
     c.chg = s->rg_chg.as<uint32_t>(); c.cchg = s->rg_cchg.as<uint32_t>(); c.epoch = epoch;
-    hipLaunchKernelGGL(rd_event_kernel<0>, dim3(1), dim3(64), 0, s->stream, c);
+    hipLaunchKernelGGL(rd_event_kernel<0>, dim3(1), dim3(EV_T), 0, s->stream, c);
     HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;
 }
@@ -1424,7 +1487,7 @@ int32_t ready_init_events(accord_store *s)
     EV_RC(ev_prepare(s, c, r, &gi));
     if (gi == ~0u) return ACCORD_OK;
     c.init_gi = gi;
-    hipLaunchKernelGGL(rd_event_kernel<1>, dim3(1), dim3(64), 0, s->stream, c);
+    hipLaunchKernelGGL(rd_event_kernel<1>, dim3(1), dim3(EV_T), 0, s->stream, c);
     HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;
 }
@@ -1465,7 +1528,7 @@ int32_t ready_truncate_events(accord_store *s, const std::vector<uint32_t> &keys
     HIPCHECK(s, hipMemcpyAsync(s->ev_tk.p, keys.data(), keys.size() * 4, hipMemcpyHostToDevice, s->stream));
     HIPCHECK(s, hipStreamSynchronize(s->stream));
     c.tkeys = s->ev_tk.as<uint32_t>(); c.ntkeys = (uint32_t)keys.size();
-    hipLaunchKernelGGL(rd_event_kernel<2>, dim3(1), dim3(64), 0, s->stream, c);
+    hipLaunchKernelGGL(rd_event_kernel<2>, dim3(1), dim3(EV_T), 0, s->stream, c);
     HIPCHECK(s, hipGetLastError());
     return ACCORD_OK;
 }
@@ -1539,7 +1602,8 @@ extern "C" int32_t accord_ready_update(accord_store *s, accord_ready *out)
     // everything is re-evaluated after a new carry (batch, truncation) or RedundantBefore bound
     // (and after a call that failed part-way: its bookkeeping below may be ahead of the device)
     const bool force = s->rdy_force_full;
-    const bool full = force || s->rdy_kb_dirty || s->rdy_sum_version != s->carry_version || s->rdy_event_mode;
+    // (event-exact mode too: a key bit its events cleared stamps the waiter changed, ev_clear)
+    const bool full = force || s->rdy_kb_dirty || s->rdy_sum_version != s->carry_version;
     const uint32_t seen = s->rdy_seen, call = ++s->rdy_call;
     s->rdy_force_full = true;                  // cleared once this call has synchronised
     s->rdy_seen = s->rg_epoch;
