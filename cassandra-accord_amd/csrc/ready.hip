@@ -812,7 +812,7 @@ __device__ __forceinline__ Cand cand_xor(const Cand &c, uint32_t d)
 constexpr uint32_t EV_T = 1024, EV_W = EV_T / 64;
 struct EvSh {
     uint32_t mu[EV_W];
-    Cand nx[EV_W], nw[EV_W];
+    Cand nx[EV_W], nw[EV_W], cm[3][EV_W], cmf[3];
     EalRec eal[EV_W];
     uint32_t ncand;
     uint32_t cgi[EV_T], ct[EV_T], cq[EV_T];
@@ -861,23 +861,69 @@ __device__ void ev_nexts(const EvCtx &c, EvSh &S, uint32_t kk, uint32_t &mu, Can
     }
 }
 
-// notify's count test for waiter (gi, t) on key slot q of key kk (expectMissingCount == |missing|):
-// no unapplied committed txn of a witnessed kind executes before it on the key, and none of its
-// deps on the key is uncommitted (uniform result)
-__device__ bool ev_managed_ok(const EvCtx &c, const ReadyParams &p, uint32_t t, uint32_t q, uint32_t kk)
+// the unapplied committed txn with the earliest executeAt per kind class (Read, Write, SyncPoints)
+// on key kk, into S.cmf: notify's count tests read these minima (statuses do not change inside an
+// event), so the key is scanned once per notify that has candidates, not once per candidate (the
+// minima stay in LDS: held in registers across the candidate loop they spilled)
+__device__ void ev_class_minima(const EvCtx &c, EvSh &S, uint32_t kk)
 {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t g = p.g[t], kind = (uint32_t)(p.lsb[t] >> 1) & 7u, wmask = witness_mask(kind);
-    const Ts ex = exec_of(c.v, g);
-    bool blocked = false;
-#pragma unroll 4
+    const uint32_t tid = threadIdx.x, w = tid >> 6;
+    Cand cm[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cm[k] = Cand{NONE, {0, 0, 0}};
     for (uint32_t x = c.kseg0[kk] + tid; x < c.kseg1[kk]; x += EV_T) {
         const uint32_t e = c.cent[x], u = e & ENT_TXN_MASK, uk = e >> ENT_KIND_SHIFT;
         if (uk == 2u) continue;
         const uint32_t st = status_of(c.v, u);
         if (st < ST_COMMITTED || st >= ST_APPLIED) continue;
-        const uint32_t cls = kind_class(uk), gate = cls == 0u ? 0u : cls == 1u ? 1u : 3u;
-        if (((wmask >> gate) & 1u) && tcmp(exec_of(c.v, u), ex) < 0) blocked = true;
+        const Cand me{u, exec_of(c.v, u)};
+        const uint32_t kc = kind_class(uk);
+#pragma unroll
+        for (uint32_t k = 0; k < 3; ++k)                // static indices: the array stays in registers
+            if (k == kc) cand_min(cm[k], me);
+    }
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cand_min(cm[k], cand_xor(cm[k], d));
+    if ((tid & 63u) == 0)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) S.cm[k][w] = cm[k];
+    __syncthreads();
+    if (tid < 3) {
+        Cand m{NONE, {0, 0, 0}};
+        for (uint32_t j = 0; j < EV_W; ++j) cand_min(m, S.cm[tid][j]);
+        S.cmf[tid] = m;
+    }
+    __syncthreads();
+}
+
+// notify's count test for waiter (gi, t) on key slot q of key kk (expectMissingCount == |missing|):
+// no unapplied committed txn of a witnessed kind executes before it on the key -- the key's class
+// minima cm[] (ev_class_minima; the waiter itself, at its own executeAt, never blocks) -- and none of
+// its deps on the key is uncommitted (a registered-status waiter can hold thousands on a hot key:
+// the whole workgroup scans them; uniform result)
+__device__ bool ev_managed_ok(const EvCtx &c, const EvSh &S, const ReadyParams &p, uint32_t t, uint32_t q, uint32_t kk,
+                              bool use_cm)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint32_t g = p.g[t], kind = (uint32_t)(p.lsb[t] >> 1) & 7u, wmask = witness_mask(kind);
+    const Ts ex = exec_of(c.v, g);
+#pragma unroll
+    for (uint32_t cls = 0; cls < 3; ++cls) {
+        const uint32_t gate = cls == 0u ? 0u : cls == 1u ? 1u : 3u;
+        if (use_cm && ((wmask >> gate) & 1u) && S.cmf[cls].g != NONE && tcmp(S.cmf[cls].ex, ex) < 0) return false;
+    }
+    bool blocked = false;
+    if (!use_cm) {                                       // a lone candidate: its own scan of the key
+        for (uint32_t x = c.kseg0[kk] + tid; x < c.kseg1[kk]; x += EV_T) {
+            const uint32_t e = c.cent[x], u = e & ENT_TXN_MASK, uk = e >> ENT_KIND_SHIFT;
+            if (uk == 2u) continue;
+            const uint32_t st = status_of(c.v, u);
+            if (st < ST_COMMITTED || st >= ST_APPLIED) continue;
+            const uint32_t cls = kind_class(uk), gate = cls == 0u ? 0u : cls == 1u ? 1u : 3u;
+            if (((wmask >> gate) & 1u) && tcmp(exec_of(c.v, u), ex) < 0) blocked = true;
+        }
     }
     const uint32_t kbound = c.kb ? c.kb[kk] : 0u;
     const uint32_t K = p.key_off[t + 1] - p.key_off[t], hb = p.k2v_off[t];
@@ -896,6 +942,7 @@ __device__ void ev_notify(const EvCtx &c, EvSh &S, uint32_t kk, bool has_from, c
                           const Ts &to)
 {
     const uint32_t tid = threadIdx.x, key = c.key_lo + kk;
+    bool have_cm = false;
     for (uint32_t x0 = c.kseg0[kk]; x0 < c.kseg1[kk]; x0 += EV_T) {
         const uint32_t x = x0 + tid;
         bool cand = false;
@@ -923,10 +970,15 @@ __device__ void ev_notify(const EvCtx &c, EvSh &S, uint32_t kk, bool has_from, c
         }
         __syncthreads();
         const uint32_t nc = S.ncand;
+        if (nc > 1 && !have_cm) {                        // uniform: nc was read after the barrier
+            __syncthreads();                             // every thread has read S.ncand
+            ev_class_minima(c, S, kk);
+            have_cm = true;
+        }
         for (uint32_t j = 0; j < nc; ++j) {
             const uint32_t lgi = S.cgi[j], lt = S.ct[j], lq = S.cq[j];
             const ReadyParams &p = c.gens[lgi];
-            if (ev_managed_ok(c, p, lt, lq, kk) && tid == 0) {
+            if (ev_managed_ok(c, S, p, lt, lq, kk, have_cm) && tid == 0) {
                 const uint32_t R = p.rd_off[lt + 1] - p.rd_off[lt];
                 ev_clear(c, p, lt, R + lq);
             }
@@ -1025,19 +1077,24 @@ __device__ void ev_key_event(const EvCtx &c, EvSh &S, uint32_t kk, uint32_t X, u
     uint32_t mu;
     Cand nx, nwr;
     ev_nexts(c, S, kk, mu, nx, nwr);
+    // the notify range of the event (one call site: the notify is inlined once)
+    bool doit = false, hf = false, ht = false;
+    Ts from{0, 0, 0}, to{0, 0, 0};
     if (nw == ST_STABLE || nw == ST_COMMITTED) {
         const int cmp = nwr.g == NONE ? -1 : tcmp(exec, nwr.ex);
         if (cmp <= 0) {
-            if (nw == ST_STABLE) ev_notify(c, S, kk, nx.g != NONE, nx.ex, true, exec);   // we may execute
+            if (nw == ST_STABLE) { doit = true; hf = nx.g != NONE; from = nx.ex; ht = true; to = exec; }   // we may execute
         } else {
             const Ts tx = ev_tid(c, X);
             // waiters on us may be ready, if we execute after them, were known and not committed
-            if (!(prev == ST_COMMITTED || tcmp(nwr.ex, tx) < 0 || tcmp(exec, tx) == 0))
-                ev_notify(c, S, kk, true, nx.ex, true, nwr.ex);
+            if (!(prev == ST_COMMITTED || tcmp(nwr.ex, tx) < 0 || tcmp(exec, tx) == 0)) {
+                doit = true; hf = true; from = nx.ex; ht = true; to = nwr.ex;
+            }
         }
     } else if ((nw == ST_APPLIED || nw == ST_INVALID) && nx.g != NONE) {
-        ev_notify(c, S, kk, true, nx.ex, nwr.g != NONE, nwr.ex);
+        doit = true; hf = true; from = nx.ex; ht = nwr.g != NONE; to = nwr.ex;
     }
+    if (doit) ev_notify(c, S, kk, hf, from, ht, to);
     if (nw >= ST_COMMITTED && prev < ST_COMMITTED) {
         ev_unmanaged(c, kk, true, mu, nx);
         __threadfence();
