@@ -1227,9 +1227,12 @@ void launch_rangekeys_union(const RangeDepsParams &p, hipStream_t s)
     uint32_t cb = (p.n_range_txns + 255) / 256;
     hipLaunchKernelGGL(rk_classes_kernel, dim3(cb > 2048 ? 2048 : cb), dim3(256), 0, s, p);
     const dim3 g(rk_blocks(p.n_range_txns)), b(RK_WAVES * 64);
-    hipLaunchKernelGGL((rangekeys_union_kernel<4, 1>), g, b, 0, s, p, 0u);
-    hipLaunchKernelGGL((rangekeys_union_kernel<16, 1>), g, b, 0, s, p, 1u);
-    hipLaunchKernelGGL((rangekeys_union_kernel<32, 1>), g, b, 0, s, p, 2u);
+    // occupancy targets per class (waves per SIMD; no spills at any of them): 1024-element sorts at 5
+    // (105 -> 96 VGPRs) and 2048-element ones at 4 (163 -> 128 VGPRs, LDS-balanced at 4 blocks per CU)
+    // took config 3 from 7.13 to 6.93 ms/step (profiles/r06_c3/union_occupancy.txt)
+    hipLaunchKernelGGL((rangekeys_union_kernel<4, 8>), g, b, 0, s, p, 0u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<16, 5>), g, b, 0, s, p, 1u);
+    hipLaunchKernelGGL((rangekeys_union_kernel<32, 4>), g, b, 0, s, p, 2u);
     hipLaunchKernelGGL((rangekeys_union_kernel<64, 2>), g, b, 0, s, p, 3u);
     hipLaunchKernelGGL((rangekeys_union_kernel<RK_EMAX, 1>), g, b, 0, s, p, 4u);
 }
