@@ -593,7 +593,9 @@ constexpr uint32_t RK_BITMAP_SPAN = 4096;      // 128 LDS words of one wave's un
 // in ascending order, clipped to the store) and the KeyDeps sizes; the fill pass writes keys, the
 // keysToTxnIds header and the body holding the dep txn indices (key order).
 template <bool FILL, int U>                          // U keys per lane per step
-__global__ __launch_bounds__(RK_WAVES * 64) void rangekeys_kernel(RangeDepsParams p)
+// (8 waves per SIMD: 67 -> 64 VGPRs with 12 B of scratch; rangekeys count 1.62 -> 1.39 ms, config 3
+// 6.80 -> 6.58 ms/step on one box, profiles/r06_c3/union_occupancy.txt)
+__global__ __launch_bounds__(RK_WAVES * 64) __attribute__((amdgpu_waves_per_eu(8))) void rangekeys_kernel(RangeDepsParams p)
 {
     __shared__ uint32_t rex_all[RK_WAVES][64 * U], rlo_all[RK_WAVES][64 * U];
     __shared__ uint32_t cmap_all[FILL ? RK_WAVES : 1][FILL ? RK_CM : 1];
