@@ -1214,7 +1214,9 @@ void launch_rangekeys_nkeys(const RangeDepsParams &p, uint32_t *cnt, hipStream_t
 void launch_rangekeys_count(const RangeDepsParams &p, hipStream_t s)
 {
     if (p.n_range_txns == 0) return;
-    hipLaunchKernelGGL((rangekeys_kernel<false, 8>), dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
+    // 4 keys per lane: at 8 waves per SIMD, 1.38 -> 1.355 ms against 8 (12: 2.39, spilling;
+    // profiles/r06_c3/union_occupancy.txt)
+    hipLaunchKernelGGL((rangekeys_kernel<false, 4>), dim3(rk_blocks(p.n_range_txns)), dim3(RK_WAVES * 64), 0, s, p);
 }
 
 void launch_rangekeys_fill(const RangeDepsParams &p, hipStream_t s)
