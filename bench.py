@@ -106,8 +106,8 @@ def launch(gpus, argv, dry_run=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)     # ~60 ms timed at config 2: one hiccup no longer moves the line
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 5),
                     help="BASELINE.json configs[1] (2), configs[2] (3: 20%% range txns), configs[4] "
                          "(5: 4M txns, deep chains, + WaitingOn levelling)")
